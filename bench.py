@@ -1,0 +1,283 @@
+#!/usr/bin/env python3
+"""Benchmark of the Chunky Bits hot path on MI355X (BASELINE.json metric).
+
+A "step" is one pass of the hot path over one batch: for every part, RS(10,4) encode_sep of
+the parity chunks plus SHA-256 of all d+p chunks (FilePart::write_with_encoder's compute,
+reference src/file/file_part.rs:150-185), over BASELINE.json configs[1]'s shape: 4096 parts x
+10 data chunks x 1 MiB on each GPU, inputs already resident in HBM.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4]
+
+For N > 1 the driver launches one rank per GPU with torch.distributed.run; each rank owns its
+own 4096 parts (parts are independent: weak scaling, no collective on the data path); the
+process group is used only for the barrier and the max-over-ranks step time.
+
+Rank 0 prints ONE JSON line.  `roofline` describes the dominant kernel, timed with HIP events
+on the stream its launches go to; `cpu_baseline` times the CPU restatement of the reference
+crates (oracle/, the same scalar galois_8 table path + SHA-256 with SHA-NI like sha2 0.9.9's
+cpufeatures dispatch) on this host's cores over a bounded sample of the same workload.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "chunky-bits_amd"))
+
+import torch  # noqa: E402  (import before chunky_ec: one HIP runtime)
+import torch.distributed as dist  # noqa: E402
+
+import chunky_ec as ce  # noqa: E402
+
+METRIC = "RS(10,4) encode+sha256 GB/s per node at 1/2/4/8 GPUs; % of HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md); 6.3 TB/s measured copy
+MiB = 1 << 20
+
+CONFIGS = {
+    # BASELINE.json configs[1]: the metric's workload.
+    "c2": dict(d=10, p=4, chunk=1 * MiB, parts=4096, op="encode_hash",
+               workload="C2: batched RS(10,4) encode_sep + SHA-256 of all 14 chunks per part, "
+                        "4096 parts x 1 MiB chunks per GPU"),
+    # configs[2]: reconstruct, 1-4 random erasures per part (data + parity rebuilt).
+    "c3": dict(d=10, p=4, chunk=1 * MiB, parts=4096, op="reconstruct",
+               workload="C3: RS(10,4) reconstruct, 1-4 random erasures per part, "
+                        "4096 parts x 1 MiB chunks per GPU"),
+    # configs[3]: wide stripe with fused per-chunk hashing.
+    "c4": dict(d=20, p=8, chunk=256 * 1024, parts=4096, op="encode_hash",
+               workload="C4: RS(20,8) encode_sep + SHA-256 of all 28 chunks per part, "
+                        "4096 parts x 256 KiB chunks per GPU"),
+    # encode only (HBM roofline of the GF kernel alone).
+    "c2enc": dict(d=10, p=4, chunk=1 * MiB, parts=4096, op="encode",
+                  workload="RS(10,4) encode_sep only, 4096 parts x 1 MiB chunks per GPU"),
+}
+
+
+def dist_env():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return world, rank, local
+
+
+def max_over_ranks(x: float, world: int, device) -> float:
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def barrier(world: int):
+    if world > 1:
+        dist.barrier()
+
+
+def cpu_baseline(cfg, threads: int):
+    """Oracle restatement of the crate path timed on this host (rank 0, N=1 only)."""
+    import oracle
+    d, p, L = cfg["d"], cfg["p"], cfg["chunk"]
+    hashed = cfg["op"] != "encode"
+    # calibrate on a few parts, then size the sample for ~1.5 s wall on `threads` cores
+    # (~10-25 s of CPU work)
+    probe = max(threads, 4)
+    sec = oracle.baseline_encode_sha(d, p, L, probe, 1, threads, True, hashed)
+    per_part = sec / probe
+    total = max(threads, int(1.5 / max(per_part, 1e-6)))
+    total = min(total, 4096)
+    sec = oracle.baseline_encode_sha(d, p, L, total, 2, threads, True, hashed)
+    gbs = total * d * L / sec / 1e9
+    return {
+        "value": round(gbs, 3),
+        "unit": "GB/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{total} parts of RS({d},{p}) x {L // 1024} KiB "
+                  f"({'encode_sep + sha256 of all chunks' if hashed else 'encode_sep'}), "
+                  f"{threads} threads, one part per task; {sec:.2f} s wall; "
+                  f"SHA-NI={'yes' if oracle.has_shani() else 'no'}",
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--parts", type=int, default=None, help="override parts per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--check", action="store_true", help="verify a sampled part vs the oracle")
+    args = ap.parse_args()
+
+    cfg = dict(CONFIGS[args.config])
+    if args.parts:
+        cfg["parts"] = args.parts
+    world, rank, local = dist_env()
+    if world != args.gpus and rank == 0:
+        print(f"note: WORLD_SIZE={world} but --gpus={args.gpus}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    d, p, L, n_parts = cfg["d"], cfg["p"], cfg["chunk"], cfg["parts"]
+    t = d + p
+    codec = ce.ReedSolomon(d, p)
+    buf = torch.empty((n_parts, t, L), dtype=torch.uint8, device=device)
+    digests = torch.empty((n_parts, t, 32), dtype=torch.uint8, device=device)
+    batch = ce.PartBatch.from_tensor(buf, L)
+    stream = torch.cuda.current_stream(device)
+    seed = 0x5EED0000 + rank
+    ce.fill_synthetic(batch, t, seed, stream)  # data chunks + (overwritten) parity slots
+
+    present = None
+    if cfg["op"] == "reconstruct":
+        ce.encode_batch(codec, batch, stream)
+        # 1..4 random erasures per part (seeded); rebuilt in place every step
+        g = torch.Generator().manual_seed(1234 + rank)
+        pres = torch.ones((n_parts, t), dtype=torch.uint8)
+        k = torch.randint(1, p + 1, (n_parts,), generator=g)
+        for i in range(n_parts):
+            idx = torch.randperm(t, generator=g)[: int(k[i])]
+            pres[i, idx] = 0
+        present = bytes(pres.flatten().tolist())
+        missing_bytes = int((t - pres.sum(1)).sum().item()) * L
+
+    # One step = the hot path over the batch.  Each library call is one kernel launch on
+    # `stream`; events bracket each launch so per-kernel averages come from the timed steps.
+    def step(evs=None):
+        if cfg["op"] == "encode_hash":
+            if evs is not None:
+                evs[0].record(stream)
+            ce.encode_batch(codec, batch, stream)
+            if evs is not None:
+                evs[1].record(stream)
+            ce.sha256_batch(batch, 0, t, digests.data_ptr(), stream)
+            if evs is not None:
+                evs[2].record(stream)
+        elif cfg["op"] == "encode":
+            if evs is not None:
+                evs[0].record(stream)
+            ce.encode_batch(codec, batch, stream)
+            if evs is not None:
+                evs[1].record(stream)
+        else:
+            if evs is not None:
+                evs[0].record(stream)
+            ce.reconstruct_batch(codec, batch, present, False, stream)
+            if evs is not None:
+                evs[1].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(device)
+    barrier(world)
+
+    n_ev = 3 if cfg["op"] == "encode_hash" else 2
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(n_ev)]
+              for _ in range(args.steps)]
+    barrier(world)
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(events[k])
+    torch.cuda.synchronize(device)
+    barrier(world)
+    t1 = time.perf_counter()
+    local_s = (t1 - t0) / args.steps
+    step_s = max_over_ranks(local_s, world, device)
+
+    # per-kernel averages over the timed steps
+    def avg_ms(i, j):
+        return sum(events[k][i].elapsed_time(events[k][j]) for k in range(args.steps)) / args.steps
+
+    data_bytes = n_parts * d * L
+    kernels = {}
+    if cfg["op"] == "encode_hash":
+        enc_ms, sha_ms = avg_ms(0, 1), avg_ms(1, 2)
+        kernels["rs_apply_kernel"] = {"ms": round(enc_ms, 4),
+                                      "algorithmic_bytes": n_parts * t * L,
+                                      "GBs": round(n_parts * t * L / enc_ms / 1e6, 1)}
+        kernels["sha256_kernel"] = {"ms": round(sha_ms, 4),
+                                    "algorithmic_bytes": n_parts * t * (L + 32),
+                                    "GBs": round(n_parts * t * (L + 32) / sha_ms / 1e6, 1)}
+    elif cfg["op"] == "encode":
+        enc_ms = avg_ms(0, 1)
+        kernels["rs_apply_kernel"] = {"ms": round(enc_ms, 4),
+                                      "algorithmic_bytes": n_parts * t * L,
+                                      "GBs": round(n_parts * t * L / enc_ms / 1e6, 1)}
+    else:
+        rec_ms = avg_ms(0, 1)
+        # each part with k missing reads d chunks and writes k: (d*parts_touched + missing)
+        touched = sum(1 for i in range(n_parts) if any(present[i * t + j] == 0 for j in range(t)))
+        algo = touched * d * L + missing_bytes
+        kernels["rs_apply_kernel(reconstruct)"] = {"ms": round(rec_ms, 4),
+                                                   "algorithmic_bytes": algo,
+                                                   "GBs": round(algo / rec_ms / 1e6, 1)}
+    dom_name = max(kernels, key=lambda k: kernels[k]["ms"])
+    dom = kernels[dom_name]
+    achieved = dom["algorithmic_bytes"] / (dom["ms"] / 1e3) / 1e9
+
+    ok = None
+    if args.check and rank == 0 and cfg["op"] != "reconstruct":
+        import hashlib
+        import numpy as np
+        import oracle
+        k = n_parts // 2
+        host = buf[k].cpu().numpy()
+        st, par = oracle.encode_sep(d, p, [host[j] for j in range(d)])
+        ok = st == 0 and all(np.array_equal(par[i], host[d + i]) for i in range(p))
+        if cfg["op"] == "encode_hash":
+            dg = digests[k].cpu().numpy()
+            ok = ok and all(hashlib.sha256(host[j].tobytes()).digest() == dg[j].tobytes()
+                            for j in range(t))
+
+    if rank == 0:
+        total_data = data_bytes * world
+        value = total_data / step_s / 1e9
+        line = {
+            "metric": METRIC if args.config == "c2" else f"{METRIC} [{args.config}]",
+            "value": round(value, 2),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(step_s * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (counter-based generator on device; inputs resident in HBM)",
+            "config": {
+                "workload": cfg["workload"],
+                "d": d, "p": p, "chunk_bytes": L, "parts_per_gpu": n_parts,
+                "data_bytes_per_step": total_data,
+                "parallelism": f"part-sharded x{world}, no collective",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": dom_name,
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": None,
+            },
+            "kernels": kernels,
+        }
+        if ok is not None:
+            line["check_vs_oracle"] = bool(ok)
+        if world == 1 and not args.no_cpu_baseline:
+            threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+            line["cpu_baseline"] = cpu_baseline(cfg, threads)
+        print(json.dumps(line), flush=True)
+
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,701 @@
+// capi.cpp — implementation of include/chunky_ec.h.
+//
+// Host responsibilities only: argument checks in the crate's order, coding/decode matrices
+// (tiny), erasure-pattern grouping, staging, and kernel launches.  Every shard byte is
+// processed by the gfx950 kernels in kernels.hip; there is no CPU compute path.
+#include "chunky_ec.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <array>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "gf256.hpp"
+#include "kernels.hpp"
+
+using namespace cec;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int hip_fail(hipError_t e, const char* what) {
+    g_last_error = std::string(what) + ": " + hipGetErrorString(e);
+    return e == hipErrorOutOfMemory ? CEC_ERR_OUT_OF_MEMORY : CEC_ERR_HIP;
+}
+
+#define HIP_TRY(expr)                                        \
+    do {                                                     \
+        hipError_t _e = (expr);                              \
+        if (_e != hipSuccess) return hip_fail(_e, #expr);    \
+    } while (0)
+
+#define CEC_TRY(expr)              \
+    do {                           \
+        int _s = (expr);           \
+        if (_s != CEC_OK) return _s; \
+    } while (0)
+
+int current_device(int* dev) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        g_last_error = "no HIP device";
+        return CEC_ERR_NO_DEVICE;
+    }
+    HIP_TRY(hipGetDevice(dev));
+    return CEC_OK;
+}
+
+constexpr size_t kChunkAlign = 256;
+size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+bool aligned16(const void* p, size_t a, size_t b) {
+    return (reinterpret_cast<uintptr_t>(p) % 16 == 0) && (a % 16 == 0) && (b % 16 == 0);
+}
+
+// ------------------------------------------------------------------------------------------
+// Host buffers that must outlive an asynchronous upload: released once their event fires.
+// ------------------------------------------------------------------------------------------
+struct PendingUpload {
+    hipEvent_t ev;
+    std::vector<uint32_t> words;
+};
+std::mutex g_pending_mu;
+std::deque<PendingUpload> g_pending;
+
+void reap_pending() {
+    std::lock_guard<std::mutex> lk(g_pending_mu);
+    for (auto it = g_pending.begin(); it != g_pending.end();) {
+        if (hipEventQuery(it->ev) == hipSuccess) {
+            (void)hipEventDestroy(it->ev);
+            it = g_pending.erase(it);
+        } else {
+            ++it;
+        }
+    }
+}
+
+// Upload `words` to a stream-ordered device allocation; the allocation is released (stream
+// ordered) by free_upload after the consumer launches.
+int upload_words(std::vector<uint32_t>&& words, hipStream_t s, uint32_t** dptr) {
+    reap_pending();
+    const size_t bytes = std::max<size_t>(words.size() * sizeof(uint32_t), 4);
+    HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(dptr), bytes, s));
+    HIP_TRY(hipMemcpyAsync(*dptr, words.data(), words.size() * sizeof(uint32_t),
+                           hipMemcpyHostToDevice, s));
+    PendingUpload pu;
+    HIP_TRY(hipEventCreateWithFlags(&pu.ev, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(pu.ev, s));
+    pu.words = std::move(words);
+    std::lock_guard<std::mutex> lk(g_pending_mu);
+    g_pending.push_back(std::move(pu));
+    return CEC_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// Per-thread staging for the host-buffer API.
+// ------------------------------------------------------------------------------------------
+struct ThreadCtx {
+    hipStream_t stream = nullptr;
+    uint8_t* dbuf = nullptr;
+    size_t dcap = 0;
+};
+thread_local std::unordered_map<int, ThreadCtx> t_ctx;
+
+int thread_ctx(ThreadCtx** out, size_t device_bytes) {
+    int dev = 0;
+    CEC_TRY(current_device(&dev));
+    ThreadCtx& c = t_ctx[dev];
+    if (!c.stream) HIP_TRY(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+    if (c.dcap < device_bytes) {
+        if (c.dbuf) HIP_TRY(hipFree(c.dbuf));
+        c.dbuf = nullptr;
+        c.dcap = 0;
+        const size_t cap = round_up(std::max<size_t>(device_bytes, 1 << 20), 1 << 20);
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c.dbuf), cap));
+        c.dcap = cap;
+    }
+    *out = &c;
+    return CEC_OK;
+}
+
+// Erasure-pattern key: present bitset (<= 256 shards) + data_only.
+struct PatternKey {
+    std::array<uint64_t, 4> bits{};
+    bool data_only = false;
+    bool operator<(const PatternKey& o) const {
+        if (bits != o.bits) return bits < o.bits;
+        return data_only < o.data_only;
+    }
+};
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+// Codec
+// ------------------------------------------------------------------------------------------
+struct cec_codec {
+    size_t d = 0, p = 0;
+    ByteMatrix m;                  // (d+p) x d
+    std::vector<uint32_t> enc;     // pattern record: parity rows over the d data chunks
+    std::mutex mu;
+    std::unordered_map<int, uint32_t*> dev_enc;  // encode record per device
+    std::map<PatternKey, std::shared_ptr<const std::vector<uint32_t>>> dec_cache;
+
+    ~cec_codec() {
+        int cur = 0;
+        if (hipGetDevice(&cur) != hipSuccess) return;
+        for (auto& kv : dev_enc) {
+            if (hipSetDevice(kv.first) == hipSuccess) (void)hipFree(kv.second);
+        }
+        (void)hipSetDevice(cur);
+    }
+
+    // Device copy of the encode record on the current device.
+    int encode_record(uint32_t** out) {
+        int dev = 0;
+        CEC_TRY(current_device(&dev));
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = dev_enc.find(dev);
+        if (it != dev_enc.end()) {
+            *out = it->second;
+            return CEC_OK;
+        }
+        uint32_t* ptr = nullptr;
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&ptr), enc.size() * sizeof(uint32_t)));
+        HIP_TRY(hipMemcpy(ptr, enc.data(), enc.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        dev_enc[dev] = ptr;
+        *out = ptr;
+        return CEC_OK;
+    }
+
+    // Decode record for a present set: inputs = first d present chunks (the crate's choice,
+    // reconstruct_internal), outputs = missing data (+ missing parity unless data_only).
+    // Missing data rows = rows of inv(M[valid]); missing parity rows = M[r] * inv(M[valid]),
+    // i.e. the crate's "recompute parity from the rebuilt data" folded into one pass
+    // (identical bytes: GF(2^8) arithmetic is exact).
+    std::shared_ptr<const std::vector<uint32_t>> decode_record(const PatternKey& key) {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = dec_cache.find(key);
+        if (it != dec_cache.end()) return it->second;
+        const size_t t = d + p;
+        std::vector<uint32_t> in_idx, out_idx;
+        std::vector<size_t> miss_par;
+        for (size_t i = 0; i < t; ++i) {
+            const bool present = (key.bits[i / 64] >> (i % 64)) & 1;
+            if (present) {
+                if (in_idx.size() < d) in_idx.push_back(uint32_t(i));
+            } else if (i < d) {
+                out_idx.push_back(uint32_t(i));
+            } else if (!key.data_only) {
+                miss_par.push_back(i);
+            }
+        }
+        for (size_t i : miss_par) out_idx.push_back(uint32_t(i));
+        ByteMatrix sub(d, d), dec;
+        for (size_t r = 0; r < d; ++r)
+            for (size_t c = 0; c < d; ++c) sub.at(r, c) = m.at(in_idx[r], c);
+        invert(sub, dec);  // any d rows of M are independent (distinct Vandermonde points)
+        ByteMatrix rows(out_idx.size(), d);
+        for (size_t k = 0; k < out_idx.size(); ++k) {
+            const size_t o = out_idx[k];
+            if (o < d) {
+                for (size_t c = 0; c < d; ++c) rows.at(k, c) = dec.at(o, c);
+            } else {
+                const Gf256& g = Gf256::get();
+                for (size_t c = 0; c < d; ++c) {
+                    uint8_t acc = 0;
+                    for (size_t q = 0; q < d; ++q) acc ^= g.mul(m.at(o, q), dec.at(q, c));
+                    rows.at(k, c) = acc;
+                }
+            }
+        }
+        auto rec = std::make_shared<std::vector<uint32_t>>(pattern_words(d, out_idx.size()));
+        write_pattern(rec->data(), d, in_idx, out_idx, rows);
+        dec_cache.emplace(key, rec);
+        return rec;
+    }
+};
+
+namespace {
+
+// Crate checks shared by the per-part reconstruct entry points.  Returns CEC_OK with *len set
+// and *work = true if something must be rebuilt.
+int check_reconstruct(const cec_codec* c, const size_t* lens, const uint8_t* present,
+                      size_t n_shards, size_t* len, bool* work) {
+    const size_t t = c->d + c->p;
+    if (n_shards < t) return CEC_TOO_FEW_SHARDS;
+    if (n_shards > t) return CEC_TOO_MANY_SHARDS;
+    size_t n_present = 0;
+    bool have = false;
+    for (size_t i = 0; i < t; ++i) {
+        if (!present[i]) continue;
+        if (lens[i] == 0) return CEC_EMPTY_SHARD;
+        ++n_present;
+        if (have && lens[i] != *len) return CEC_INCORRECT_SHARD_SIZE;
+        *len = lens[i];
+        have = true;
+    }
+    *work = n_present != t;
+    if (!*work) return CEC_OK;
+    if (n_present < c->d) return CEC_TOO_FEW_SHARDS_PRESENT;
+    return CEC_OK;
+}
+
+PatternKey make_key(const uint8_t* present, size_t t, bool data_only) {
+    PatternKey k;
+    for (size_t i = 0; i < t; ++i)
+        if (present[i]) k.bits[i / 64] |= uint64_t(1) << (i % 64);
+    k.data_only = data_only;
+    return k;
+}
+
+int reconstruct_host(const cec_codec* cc, uint8_t* const* shards, const size_t* lens,
+                     uint8_t* present, size_t n_shards, bool data_only) {
+    if (!cc || !shards || !lens || !present) return CEC_ERR_INVALID_ARGUMENT;
+    cec_codec* c = const_cast<cec_codec*>(cc);
+    size_t len = 0;
+    bool work = false;
+    CEC_TRY(check_reconstruct(c, lens, present, n_shards, &len, &work));
+    if (!work) return CEC_OK;
+    const size_t t = c->d + c->p;
+    auto rec = c->decode_record(make_key(present, t, data_only));
+    const size_t n_out = (*rec)[0];
+    const uint32_t* out_idx = rec->data() + 1 + c->d;
+    for (size_t k = 0; k < n_out; ++k) {
+        const size_t o = out_idx[k];
+        if (!shards[o] || lens[o] < len) {
+            g_last_error = "missing shard buffer too small";
+            return CEC_ERR_INVALID_ARGUMENT;
+        }
+    }
+    if (n_out == 0) return CEC_OK;  // data_only with only parity missing
+    const size_t cs = round_up(len, kChunkAlign);
+    const size_t rec_bytes = round_up(rec->size() * sizeof(uint32_t), kChunkAlign);
+    ThreadCtx* ctx = nullptr;
+    CEC_TRY(thread_ctx(&ctx, rec_bytes + t * cs));
+    uint32_t* drec = reinterpret_cast<uint32_t*>(ctx->dbuf);
+    uint8_t* dbase = ctx->dbuf + rec_bytes;
+    HIP_TRY(hipMemcpyAsync(drec, rec->data(), rec->size() * sizeof(uint32_t),
+                           hipMemcpyHostToDevice, ctx->stream));
+    const uint32_t* in_idx = rec->data() + 1;
+    for (size_t j = 0; j < c->d; ++j)
+        HIP_TRY(hipMemcpyAsync(dbase + in_idx[j] * cs, shards[in_idx[j]], len,
+                               hipMemcpyHostToDevice, ctx->stream));
+    ApplyParams a{};
+    a.base = dbase;
+    a.part_stride = t * cs;
+    a.chunk_stride = cs;
+    a.len = len;
+    a.pat = drec;
+    a.n_parts = 1;
+    a.d = uint32_t(c->d);
+    a.n_rows = uint32_t(n_out);
+    HIP_TRY(launch_rs_apply(a, true, ctx->stream));
+    for (size_t k = 0; k < n_out; ++k)
+        HIP_TRY(hipMemcpyAsync(shards[out_idx[k]], dbase + out_idx[k] * cs, len,
+                               hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    for (size_t k = 0; k < n_out; ++k) present[out_idx[k]] = 1;
+    return CEC_OK;
+}
+
+int batch_ok(const cec_part_batch* b) {
+    if (!b || !b->base) return CEC_ERR_INVALID_ARGUMENT;
+    return CEC_OK;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+// Library
+// ------------------------------------------------------------------------------------------
+extern "C" {
+
+int cec_abi_version(void) { return CEC_ABI_VERSION; }
+
+const char* cec_status_name(int s) {
+    switch (s) {
+        case CEC_OK: return "Ok";
+        case CEC_TOO_FEW_SHARDS: return "TooFewShards";
+        case CEC_TOO_MANY_SHARDS: return "TooManyShards";
+        case CEC_TOO_FEW_DATA_SHARDS: return "TooFewDataShards";
+        case CEC_TOO_MANY_DATA_SHARDS: return "TooManyDataShards";
+        case CEC_TOO_FEW_PARITY_SHARDS: return "TooFewParityShards";
+        case CEC_TOO_MANY_PARITY_SHARDS: return "TooManyParityShards";
+        case CEC_TOO_FEW_BUFFER_SHARDS: return "TooFewBufferShards";
+        case CEC_TOO_MANY_BUFFER_SHARDS: return "TooManyBufferShards";
+        case CEC_INCORRECT_SHARD_SIZE: return "IncorrectShardSize";
+        case CEC_TOO_FEW_SHARDS_PRESENT: return "TooFewShardsPresent";
+        case CEC_EMPTY_SHARD: return "EmptyShard";
+        case CEC_INVALID_SHARD_FLAGS: return "InvalidShardFlags";
+        case CEC_INVALID_INDEX: return "InvalidIndex";
+        case CEC_ERR_INVALID_ARGUMENT: return "InvalidArgument";
+        case CEC_ERR_HIP: return "HipError";
+        case CEC_ERR_NO_DEVICE: return "NoDevice";
+        case CEC_ERR_OUT_OF_MEMORY: return "OutOfMemory";
+        default: return "Unknown";
+    }
+}
+
+const char* cec_last_error(void) { return g_last_error.c_str(); }
+
+int cec_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+// ------------------------------------------------------------------------------------------
+// Codec
+// ------------------------------------------------------------------------------------------
+
+int cec_codec_new(size_t d, size_t p, cec_codec** out) {
+    if (!out) return CEC_ERR_INVALID_ARGUMENT;
+    *out = nullptr;
+    // ReedSolomon::new order of checks.
+    if (d == 0) return CEC_TOO_FEW_DATA_SHARDS;
+    if (p == 0) return CEC_TOO_FEW_PARITY_SHARDS;
+    if (d + p > 256) return CEC_TOO_MANY_SHARDS;
+    auto c = std::make_unique<cec_codec>();
+    c->d = d;
+    c->p = p;
+    c->m = build_coding_matrix(d, p);
+    ByteMatrix rows(p, d);
+    std::vector<uint32_t> in_idx(d), out_idx(p);
+    for (size_t j = 0; j < d; ++j) in_idx[j] = uint32_t(j);
+    for (size_t i = 0; i < p; ++i) {
+        out_idx[i] = uint32_t(d + i);
+        for (size_t j = 0; j < d; ++j) rows.at(i, j) = c->m.at(d + i, j);
+    }
+    c->enc.resize(pattern_words(d, p));
+    write_pattern(c->enc.data(), d, in_idx, out_idx, rows);
+    *out = c.release();
+    return CEC_OK;
+}
+
+void cec_codec_free(cec_codec* c) { delete c; }
+size_t cec_codec_data_shards(const cec_codec* c) { return c ? c->d : 0; }
+size_t cec_codec_parity_shards(const cec_codec* c) { return c ? c->p : 0; }
+size_t cec_codec_total_shards(const cec_codec* c) { return c ? c->d + c->p : 0; }
+
+int cec_codec_matrix(const cec_codec* c, uint8_t* out, size_t out_len) {
+    if (!c || !out || out_len < c->m.v.size()) return CEC_ERR_INVALID_ARGUMENT;
+    std::memcpy(out, c->m.v.data(), c->m.v.size());
+    return CEC_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// Host-buffer API
+// ------------------------------------------------------------------------------------------
+
+int cec_encode_sep(const cec_codec* cc, const uint8_t* const* data, const size_t* data_lens,
+                   size_t n_data, uint8_t* const* parity, const size_t* parity_lens,
+                   size_t n_parity) {
+    if (!cc) return CEC_ERR_INVALID_ARGUMENT;
+    cec_codec* c = const_cast<cec_codec*>(cc);
+    // check_piece_count!(data), check_piece_count!(parity)
+    if (n_data < c->d) return CEC_TOO_FEW_DATA_SHARDS;
+    if (n_data > c->d) return CEC_TOO_MANY_DATA_SHARDS;
+    if (n_parity < c->p) return CEC_TOO_FEW_PARITY_SHARDS;
+    if (n_parity > c->p) return CEC_TOO_MANY_PARITY_SHARDS;
+    if (!data || !data_lens || !parity || !parity_lens) return CEC_ERR_INVALID_ARGUMENT;
+    // check_slices!(multi => data, multi => parity)
+    const size_t len = data_lens[0];
+    if (len == 0) return CEC_EMPTY_SHARD;
+    for (size_t j = 0; j < n_data; ++j)
+        if (data_lens[j] != len) return CEC_INCORRECT_SHARD_SIZE;
+    if (parity_lens[0] == 0) return CEC_EMPTY_SHARD;
+    for (size_t i = 0; i < n_parity; ++i)
+        if (parity_lens[i] != parity_lens[0]) return CEC_INCORRECT_SHARD_SIZE;
+    if (parity_lens[0] != len) return CEC_INCORRECT_SHARD_SIZE;
+
+    const size_t t = c->d + c->p, cs = round_up(len, kChunkAlign);
+    uint32_t* drec = nullptr;
+    CEC_TRY(c->encode_record(&drec));
+    ThreadCtx* ctx = nullptr;
+    CEC_TRY(thread_ctx(&ctx, t * cs));
+    for (size_t j = 0; j < c->d; ++j)
+        HIP_TRY(hipMemcpyAsync(ctx->dbuf + j * cs, data[j], len, hipMemcpyHostToDevice,
+                               ctx->stream));
+    ApplyParams a{};
+    a.base = ctx->dbuf;
+    a.part_stride = t * cs;
+    a.chunk_stride = cs;
+    a.len = len;
+    a.pat = drec;
+    a.n_parts = 1;
+    a.d = uint32_t(c->d);
+    a.n_rows = uint32_t(c->p);
+    HIP_TRY(launch_rs_apply(a, true, ctx->stream));
+    for (size_t i = 0; i < c->p; ++i)
+        HIP_TRY(hipMemcpyAsync(parity[i], ctx->dbuf + (c->d + i) * cs, len,
+                               hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return CEC_OK;
+}
+
+int cec_reconstruct(const cec_codec* c, uint8_t* const* shards, const size_t* lens,
+                    uint8_t* present, size_t n) {
+    return reconstruct_host(c, shards, lens, present, n, false);
+}
+
+int cec_reconstruct_data(const cec_codec* c, uint8_t* const* shards, const size_t* lens,
+                         uint8_t* present, size_t n) {
+    return reconstruct_host(c, shards, lens, present, n, true);
+}
+
+int cec_sha256_many(const uint8_t* const* bufs, const size_t* lens, size_t n, uint8_t* out) {
+    if (n == 0) return CEC_OK;
+    if (!bufs || !lens || !out) return CEC_ERR_INVALID_ARGUMENT;
+    std::vector<size_t> off(n);
+    size_t total = 0;
+    for (size_t i = 0; i < n; ++i) {
+        if (lens[i] && !bufs[i]) return CEC_ERR_INVALID_ARGUMENT;
+        off[i] = total;
+        total += round_up(std::max<size_t>(lens[i], 1), kChunkAlign);
+    }
+    const size_t meta = round_up(2 * n * sizeof(uint64_t), kChunkAlign);
+    const size_t dig = round_up(n * 32, kChunkAlign);
+    ThreadCtx* ctx = nullptr;
+    CEC_TRY(thread_ctx(&ctx, meta + dig + total));
+    uint64_t* dptrs = reinterpret_cast<uint64_t*>(ctx->dbuf);
+    uint64_t* dlens = dptrs + n;
+    uint8_t* ddig = ctx->dbuf + meta;
+    uint8_t* ddata = ddig + dig;
+    std::vector<uint64_t> hmeta(2 * n);
+    for (size_t i = 0; i < n; ++i) {
+        hmeta[i] = reinterpret_cast<uint64_t>(ddata + off[i]);
+        hmeta[n + i] = lens[i];
+        if (lens[i])
+            HIP_TRY(hipMemcpyAsync(ddata + off[i], bufs[i], lens[i], hipMemcpyHostToDevice,
+                                   ctx->stream));
+    }
+    HIP_TRY(hipMemcpyAsync(dptrs, hmeta.data(), hmeta.size() * sizeof(uint64_t),
+                           hipMemcpyHostToDevice, ctx->stream));
+    ShaParams a{};
+    a.ptrs = dptrs;
+    a.lens = dlens;
+    a.n_parts = uint32_t(n);
+    a.n_chunks = 1;
+    a.digests = ddig;
+    HIP_TRY(launch_sha256(a, true, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(out, ddig, n * 32, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return CEC_OK;
+}
+
+int cec_sha256(const uint8_t* buf, size_t len, uint8_t* out32) {
+    return cec_sha256_many(&buf, &len, 1, out32);
+}
+
+int cec_part_encode(const cec_codec* cc, const uint8_t* data_buf, size_t length,
+                    uint8_t* parity_out, uint8_t* digests_out, size_t* chunksize) {
+    if (!cc || !parity_out || !digests_out || !chunksize) return CEC_ERR_INVALID_ARGUMENT;
+    cec_codec* c = const_cast<cec_codec*>(cc);
+    if (length == 0) return CEC_EMPTY_SHARD;
+    if (!data_buf) return CEC_ERR_INVALID_ARGUMENT;
+    const size_t d = c->d, p = c->p, t = d + p;
+    const size_t L = (length + d - 1) / d;
+    const size_t cs = round_up(L, kChunkAlign);
+    const size_t dig = round_up(t * 32, kChunkAlign);
+    uint32_t* drec = nullptr;
+    CEC_TRY(c->encode_record(&drec));
+    ThreadCtx* ctx = nullptr;
+    CEC_TRY(thread_ctx(&ctx, dig + t * cs));
+    uint8_t* ddig = ctx->dbuf;
+    uint8_t* dbase = ctx->dbuf + dig;
+    for (size_t j = 0; j < d; ++j)
+        HIP_TRY(hipMemcpyAsync(dbase + j * cs, data_buf + j * L, L, hipMemcpyHostToDevice,
+                               ctx->stream));
+    ApplyParams a{};
+    a.base = dbase;
+    a.part_stride = t * cs;
+    a.chunk_stride = cs;
+    a.len = L;
+    a.pat = drec;
+    a.n_parts = 1;
+    a.d = uint32_t(d);
+    a.n_rows = uint32_t(p);
+    HIP_TRY(launch_rs_apply(a, true, ctx->stream));
+    ShaParams h{};
+    h.base = dbase;
+    h.part_stride = t * cs;
+    h.chunk_stride = cs;
+    h.len = L;
+    h.n_parts = 1;
+    h.first_chunk = 0;
+    h.n_chunks = uint32_t(t);
+    h.digests = ddig;
+    HIP_TRY(launch_sha256(h, true, ctx->stream));
+    for (size_t i = 0; i < p; ++i)
+        HIP_TRY(hipMemcpyAsync(parity_out + i * L, dbase + (d + i) * cs, L,
+                               hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(digests_out, ddig, t * 32, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    *chunksize = L;
+    return CEC_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// Device-resident batch API
+// ------------------------------------------------------------------------------------------
+
+int cec_encode_batch(const cec_codec* cc, const cec_part_batch* b, void* stream) {
+    if (!cc) return CEC_ERR_INVALID_ARGUMENT;
+    CEC_TRY(batch_ok(b));
+    if (b->n_parts == 0) return CEC_OK;
+    if (b->chunk_len == 0) return CEC_EMPTY_SHARD;
+    if (b->n_parts > 0xFFFFFFFFull) return CEC_ERR_INVALID_ARGUMENT;
+    cec_codec* c = const_cast<cec_codec*>(cc);
+    uint32_t* drec = nullptr;
+    CEC_TRY(c->encode_record(&drec));
+    ApplyParams a{};
+    a.base = b->base;
+    a.part_stride = b->part_stride;
+    a.chunk_stride = b->chunk_stride;
+    a.len = b->chunk_len;
+    a.pat = drec;
+    a.n_parts = uint32_t(b->n_parts);
+    a.d = uint32_t(c->d);
+    a.n_rows = uint32_t(c->p);
+    HIP_TRY(launch_rs_apply(a, aligned16(b->base, b->part_stride, b->chunk_stride),
+                            static_cast<hipStream_t>(stream)));
+    return CEC_OK;
+}
+
+int cec_sha256_batch(const cec_part_batch* b, size_t first_chunk, size_t n_chunks,
+                     uint8_t* digests, void* stream) {
+    CEC_TRY(batch_ok(b));
+    if (!digests) return CEC_ERR_INVALID_ARGUMENT;
+    if (b->n_parts == 0 || n_chunks == 0) return CEC_OK;
+    if (b->n_parts * n_chunks > 0xFFFFFFFFull) return CEC_ERR_INVALID_ARGUMENT;
+    ShaParams h{};
+    h.base = b->base;
+    h.part_stride = b->part_stride;
+    h.chunk_stride = b->chunk_stride;
+    h.len = b->chunk_len;
+    h.n_parts = uint32_t(b->n_parts);
+    h.first_chunk = uint32_t(first_chunk);
+    h.n_chunks = uint32_t(n_chunks);
+    h.digests = digests;
+    HIP_TRY(launch_sha256(h, aligned16(b->base, b->part_stride, b->chunk_stride),
+                          static_cast<hipStream_t>(stream)));
+    return CEC_OK;
+}
+
+int cec_encode_hash_batch(const cec_codec* c, const cec_part_batch* b, uint8_t* digests,
+                          void* stream) {
+    CEC_TRY(cec_encode_batch(c, b, stream));
+    if (!c || !digests) return CEC_ERR_INVALID_ARGUMENT;
+    return cec_sha256_batch(b, 0, c->d + c->p, digests, stream);
+}
+
+int cec_reconstruct_batch(const cec_codec* cc, const cec_part_batch* b, const uint8_t* present,
+                          int data_only, void* stream) {
+    if (!cc || !present) return CEC_ERR_INVALID_ARGUMENT;
+    CEC_TRY(batch_ok(b));
+    if (b->n_parts == 0) return CEC_OK;
+    if (b->chunk_len == 0) return CEC_EMPTY_SHARD;
+    if (b->n_parts > 0xFFFFFFFFull) return CEC_ERR_INVALID_ARGUMENT;
+    cec_codec* c = const_cast<cec_codec*>(cc);
+    const size_t d = c->d, t = c->d + c->p;
+    // Validate every part before launching anything.
+    for (size_t k = 0; k < b->n_parts; ++k) {
+        size_t n_present = 0;
+        for (size_t i = 0; i < t; ++i) n_present += present[k * t + i] ? 1 : 0;
+        if (n_present != t && n_present < d) return CEC_TOO_FEW_SHARDS_PRESENT;
+    }
+    // Group parts by pattern; bucket patterns by output-row count.
+    std::map<PatternKey, std::pair<uint32_t, std::vector<uint32_t>>> groups;  // key -> (n_out, parts)
+    for (size_t k = 0; k < b->n_parts; ++k) {
+        const uint8_t* pr = present + k * t;
+        size_t n_present = 0;
+        for (size_t i = 0; i < t; ++i) n_present += pr[i] ? 1 : 0;
+        if (n_present == t) continue;
+        PatternKey key = make_key(pr, t, data_only != 0);
+        auto& g = groups[key];
+        g.second.push_back(uint32_t(k));
+    }
+    if (groups.empty()) return CEC_OK;
+    // words = [records...][per bucket: part_ids..., part_pat...]
+    std::vector<uint32_t> words;
+    std::map<uint32_t, std::pair<std::vector<uint32_t>, std::vector<uint32_t>>> buckets;
+    for (auto& kv : groups) {
+        auto rec = c->decode_record(kv.first);
+        const uint32_t n_out = (*rec)[0];
+        if (n_out == 0) continue;  // data_only: only parity missing, nothing to do
+        const uint32_t off = uint32_t(words.size());
+        words.insert(words.end(), rec->begin(), rec->end());
+        auto& bk = buckets[n_out];
+        for (uint32_t part : kv.second.second) {
+            bk.first.push_back(part);
+            bk.second.push_back(off);
+        }
+    }
+    if (buckets.empty()) return CEC_OK;
+    std::vector<std::pair<uint32_t, size_t>> launches;  // (n_out, word offset of part_ids)
+    for (auto& kv : buckets) {
+        launches.push_back({kv.first, words.size()});
+        words.insert(words.end(), kv.second.first.begin(), kv.second.first.end());
+        words.insert(words.end(), kv.second.second.begin(), kv.second.second.end());
+    }
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    uint32_t* dwords = nullptr;
+    std::vector<size_t> counts;
+    for (auto& kv : buckets) counts.push_back(kv.second.first.size());
+    CEC_TRY(upload_words(std::move(words), s, &dwords));
+    const bool vec = aligned16(b->base, b->part_stride, b->chunk_stride);
+    int status = CEC_OK;
+    for (size_t i = 0; i < launches.size() && status == CEC_OK; ++i) {
+        ApplyParams a{};
+        a.base = b->base;
+        a.part_stride = b->part_stride;
+        a.chunk_stride = b->chunk_stride;
+        a.len = b->chunk_len;
+        a.pat = dwords;
+        a.part_ids = dwords + launches[i].second;
+        a.part_pat = dwords + launches[i].second + counts[i];
+        a.n_parts = uint32_t(counts[i]);
+        a.d = uint32_t(d);
+        a.n_rows = launches[i].first;
+        hipError_t e = launch_rs_apply(a, vec, s);
+        if (e != hipSuccess) status = hip_fail(e, "launch_rs_apply");
+    }
+    hipError_t e = hipFreeAsync(dwords, s);
+    if (status == CEC_OK && e != hipSuccess) status = hip_fail(e, "hipFreeAsync");
+    return status;
+}
+
+// ------------------------------------------------------------------------------------------
+// Utilities
+// ------------------------------------------------------------------------------------------
+
+int cec_fill_synthetic(const cec_part_batch* b, size_t n_chunks, uint64_t seed, void* stream) {
+    CEC_TRY(batch_ok(b));
+    if (b->n_parts > 0xFFFFFFFFull || n_chunks > 0xFFFFFFFFull) return CEC_ERR_INVALID_ARGUMENT;
+    FillParams f{};
+    f.base = b->base;
+    f.part_stride = b->part_stride;
+    f.chunk_stride = b->chunk_stride;
+    f.len = b->chunk_len;
+    f.seed = seed;
+    f.n_parts = uint32_t(b->n_parts);
+    f.n_chunks = uint32_t(n_chunks);
+    HIP_TRY(launch_fill(f, static_cast<hipStream_t>(stream)));
+    return CEC_OK;
+}
+
+uint8_t cec_synth_byte(uint64_t seed, uint64_t part, uint64_t chunk, uint64_t offset) {
+    return synth_byte(seed, part, chunk, offset);
+}
+
+}  // extern "C"

@@ -1,0 +1,60 @@
+// kernels.hpp — launch interface of the gfx950 kernels (kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace cec {
+
+// One launch of the GF(2^8) matrix-apply kernel over a set of parts that share the output-row
+// count.  Part `lp` of the launch is batch part part_ids[lp] (or lp), uses the pattern record at
+// pat + part_pat[lp] (or pat + 0); see gf256.hpp for the record layout.  For each part:
+//   chunk[out_idx[r]] = XOR_j coef[r][j] (x) chunk[in_idx[j]]     (bytes [0, len))
+struct ApplyParams {
+    uint8_t* base;
+    uint64_t part_stride;
+    uint64_t chunk_stride;
+    uint64_t len;
+    const uint32_t* pat;
+    const uint32_t* part_ids;
+    const uint32_t* part_pat;
+    uint32_t n_parts;
+    uint32_t d;
+    uint32_t n_rows;  // n_out shared by every pattern of this launch
+};
+
+// SHA-256 of n_parts * n_chunks chunks.  Strided mode: chunk (k, first_chunk + c) at
+// base + k*part_stride + (first_chunk + c)*chunk_stride, len bytes, digest at (k*n_chunks+c)*32.
+// List mode (ptrs != nullptr): item i hashes lens[i] bytes at ptrs[i] (n_parts = items,
+// n_chunks = 1).
+struct ShaParams {
+    const uint8_t* base;
+    uint64_t part_stride;
+    uint64_t chunk_stride;
+    uint64_t len;
+    const uint64_t* ptrs;
+    const uint64_t* lens;
+    uint32_t n_parts;
+    uint32_t first_chunk;
+    uint32_t n_chunks;
+    uint8_t* digests;
+};
+
+struct FillParams {
+    uint8_t* base;
+    uint64_t part_stride;
+    uint64_t chunk_stride;
+    uint64_t len;
+    uint64_t seed;
+    uint32_t n_parts;
+    uint32_t n_chunks;
+};
+
+hipError_t launch_rs_apply(const ApplyParams& a, bool vec16, hipStream_t s);
+hipError_t launch_sha256(const ShaParams& a, bool vec16, hipStream_t s);
+hipError_t launch_fill(const FillParams& a, hipStream_t s);
+
+// Host mirror of the device generator (cec_synth_byte).
+uint8_t synth_byte(uint64_t seed, uint64_t part, uint64_t chunk, uint64_t offset);
+
+}  // namespace cec

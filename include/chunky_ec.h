@@ -1,0 +1,191 @@
+/*
+ * chunky_ec.h — C-ABI of the MI355X (gfx950) erasure-coding + chunk-hashing engine for Chunky Bits.
+ *
+ * This is the drop-in boundary.  It replaces the two third-party crates the
+ * reference's part layer calls (neither is vendored in /root/reference):
+ *
+ *   reed_solomon_erasure 4.0.2 (Cargo.lock:1031-1037), galois_8 field:
+ *     ReedSolomon::new            src/file/file_part.rs:77,302   src/file/writer.rs:131
+ *                                 src/bin/chunky-bits/main.rs:557          -> cec_codec_new
+ *     ReedSolomon::encode_sep     src/file/file_part.rs:161-165  main.rs:289 -> cec_encode_sep
+ *     ReedSolomon::reconstruct_data  src/file/file_part.rs:128  main.rs:263 -> cec_reconstruct_data
+ *     ReedSolomon::reconstruct    src/file/file_part.rs:304                 -> cec_reconstruct
+ *     reed_solomon_erasure::Error (wrapped by FileWriteError::Erasure / FileReadError::Erasure,
+ *                                 src/error.rs:44,55)                       -> cec_status 1..13
+ *   sha2 0.9.9 (Cargo.lock:1221-1231):
+ *     Sha256Hash::from_buf        src/file/hash/sha256.rs:20-26 (DataHasher, any.rs:17-25)
+ *                                                                           -> cec_sha256
+ *     DataVerifier::verify        src/file/hash/any.rs:27-52                -> cec_sha256 + compare
+ *
+ * and adds the batched, device-resident forms the GPU needs (many parts per launch):
+ *     FilePart::write_with_encoder compute (file_part.rs:150-185: ceil(len/d) slicing, encode_sep,
+ *       sha256 of the d+p chunks in order)                 -> cec_part_encode, cec_encode_hash_batch
+ *     FilePart::read_with_context compute (file_part.rs:86-133: verify, reconstruct_data)
+ *                                                          -> cec_reconstruct_batch, cec_sha256_batch
+ *     FilePart::resilver compute (file_part.rs:266-308)    -> cec_reconstruct_batch (data_only = 0)
+ *     FilePart::verify (file_part.rs:228-251)              -> cec_sha256_batch
+ *
+ * Conventions
+ *   - Plain pointers and sizes only; every buffer is owned by the caller.
+ *   - Functions return int status codes (cec_status).  1..13 map 1:1 onto the variants of
+ *     reed_solomon_erasure::Error in declaration order, so a Rust shim can rebuild the crate
+ *     error.  Codes >= 100 are engine errors with no crate equivalent.
+ *   - Thread-safety: a cec_codec is immutable after cec_codec_new and may be shared by any
+ *     number of threads (like the Arc<ReedSolomon> at writer.rs:131,200).  Host-buffer calls use a
+ *     per-thread HIP stream and staging area on the calling thread's current HIP device.
+ *   - Device-batch calls take a hipStream_t as `void* stream` (NULL = the null stream) and are
+ *     asynchronous with respect to the host; device pointers must live on the current device.
+ *   - All computation runs on the GPU.  There is no CPU fallback: without a usable HIP device
+ *     the compute entry points return CEC_ERR_NO_DEVICE.
+ */
+#ifndef CHUNKY_EC_H
+#define CHUNKY_EC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CEC_ABI_VERSION 1
+
+typedef enum cec_status {
+    CEC_OK = 0,
+    /* reed_solomon_erasure::Error (4.0.2), declaration order */
+    CEC_TOO_FEW_SHARDS = 1,
+    CEC_TOO_MANY_SHARDS = 2,
+    CEC_TOO_FEW_DATA_SHARDS = 3,
+    CEC_TOO_MANY_DATA_SHARDS = 4,
+    CEC_TOO_FEW_PARITY_SHARDS = 5,
+    CEC_TOO_MANY_PARITY_SHARDS = 6,
+    CEC_TOO_FEW_BUFFER_SHARDS = 7,   /* no entry point of this ABI can raise it */
+    CEC_TOO_MANY_BUFFER_SHARDS = 8,  /* no entry point of this ABI can raise it */
+    CEC_INCORRECT_SHARD_SIZE = 9,
+    CEC_TOO_FEW_SHARDS_PRESENT = 10,
+    CEC_EMPTY_SHARD = 11,
+    CEC_INVALID_SHARD_FLAGS = 12,    /* no entry point of this ABI can raise it */
+    CEC_INVALID_INDEX = 13,          /* no entry point of this ABI can raise it */
+    /* engine errors */
+    CEC_ERR_INVALID_ARGUMENT = 101,
+    CEC_ERR_HIP = 102,
+    CEC_ERR_NO_DEVICE = 103,
+    CEC_ERR_OUT_OF_MEMORY = 104
+} cec_status;
+
+/* ---------------------------------------------------------------------------------------- */
+/* Library                                                                                   */
+/* ---------------------------------------------------------------------------------------- */
+
+int cec_abi_version(void);
+/* Static description of a status code ("TooFewShardsPresent", ...). */
+const char* cec_status_name(int status);
+/* Message of the last CEC_ERR_HIP on the calling thread (empty string if none). */
+const char* cec_last_error(void);
+/* Number of visible HIP devices (0 when none; never fails). */
+int cec_device_count(void);
+
+/* ---------------------------------------------------------------------------------------- */
+/* Codec: ReedSolomon<galois_8::Field>                                                       */
+/* ---------------------------------------------------------------------------------------- */
+
+typedef struct cec_codec cec_codec;
+
+/* ReedSolomon::new(data_shards, parity_shards).  Errors: TooFewDataShards (d == 0),
+ * TooFewParityShards (p == 0), TooManyShards (d + p > 256).  Host-only; needs no GPU. */
+int cec_codec_new(size_t data_shards, size_t parity_shards, cec_codec** out);
+void cec_codec_free(cec_codec* codec);
+size_t cec_codec_data_shards(const cec_codec* codec);
+size_t cec_codec_parity_shards(const cec_codec* codec);
+size_t cec_codec_total_shards(const cec_codec* codec);
+/* Copies the (d+p) x d coding matrix (row major; top d x d = identity) into out[out_len]. */
+int cec_codec_matrix(const cec_codec* codec, uint8_t* out, size_t out_len);
+
+/* ---------------------------------------------------------------------------------------- */
+/* Host-buffer API: one call per part, staged through the GPU (drop-in for the crate calls) */
+/* ---------------------------------------------------------------------------------------- */
+
+/* ReedSolomon::encode_sep(&data, &mut parity): data[n_data] slices of data_lens[i] bytes,
+ * parity[n_parity] caller-allocated slices of parity_lens[i] bytes, overwritten. */
+int cec_encode_sep(const cec_codec* codec,
+                   const uint8_t* const* data, const size_t* data_lens, size_t n_data,
+                   uint8_t* const* parity, const size_t* parity_lens, size_t n_parity);
+
+/* ReedSolomon::reconstruct / reconstruct_data on &mut [Option<Vec<u8>>].
+ * present[i] != 0 <=> Some(shard) of shard_lens[i] bytes at shards[i].  For every missing slot
+ * the crate would fill (all missing slots for reconstruct; missing DATA slots only for
+ * reconstruct_data) shards[i] must point to caller memory of shard_lens[i] >= the present shard
+ * length (else CEC_ERR_INVALID_ARGUMENT).  On success those slots are written and present[i] is
+ * set to 1; slots the crate would leave None keep present[i] == 0. */
+int cec_reconstruct(const cec_codec* codec, uint8_t* const* shards, const size_t* shard_lens,
+                    uint8_t* present, size_t n_shards);
+int cec_reconstruct_data(const cec_codec* codec, uint8_t* const* shards,
+                         const size_t* shard_lens, uint8_t* present, size_t n_shards);
+
+/* Sha256Hash::from_buf: out[32] = SHA-256(buf[0..len]). */
+int cec_sha256(const uint8_t* buf, size_t len, uint8_t* out32);
+/* n independent digests in one launch: out[i*32..] = SHA-256(bufs[i][0..lens[i]]). */
+int cec_sha256_many(const uint8_t* const* bufs, const size_t* lens, size_t n, uint8_t* out);
+
+/* FilePart::write_with_encoder compute (file_part.rs:150-185) for one part:
+ * L = ceil(length / d); data chunk j = data_buf[j*L .. (j+1)*L] (data_buf holds d*L bytes,
+ * zero padded past `length` like writer.rs:172); parity_out receives p*L bytes (chunk i at
+ * parity_out + i*L); digests_out receives (d+p)*32 bytes, chunks in order (d data then p
+ * parity); *chunksize = L.  length == 0 -> CEC_EMPTY_SHARD (as encode_sep on empty slices). */
+int cec_part_encode(const cec_codec* codec, const uint8_t* data_buf, size_t length,
+                    uint8_t* parity_out, uint8_t* digests_out, size_t* chunksize);
+
+/* ---------------------------------------------------------------------------------------- */
+/* Device-resident batch API (inputs already in HBM; asynchronous on `stream`)              */
+/* ---------------------------------------------------------------------------------------- */
+
+/* Part k's chunk i (0 <= i < d+p, d data then p parity, in order) lives at
+ *   base + k*part_stride + i*chunk_stride
+ * and is chunk_len (= FilePart::chunksize) bytes long.  Fast path: base, part_stride and
+ * chunk_stride multiples of 16; any other layout is supported at lower speed. */
+typedef struct cec_part_batch {
+    uint8_t* base;
+    size_t part_stride;
+    size_t chunk_stride;
+    size_t n_parts;
+    size_t chunk_len;
+} cec_part_batch;
+
+/* encode_sep for every part: writes the p parity chunks of each part from its d data chunks. */
+int cec_encode_batch(const cec_codec* codec, const cec_part_batch* batch, void* stream);
+
+/* encode_sep + SHA-256 of all d+p chunks of every part (write_with_encoder's compute).
+ * digests: device buffer of n_parts*(d+p)*32 bytes, part-major, chunks in order. */
+int cec_encode_hash_batch(const cec_codec* codec, const cec_part_batch* batch, uint8_t* digests,
+                          void* stream);
+
+/* SHA-256 of chunks [first_chunk, first_chunk + n_chunks) of every part.
+ * digests: device buffer, digest of (part k, chunk first_chunk + c) at (k*n_chunks + c)*32. */
+int cec_sha256_batch(const cec_part_batch* batch, size_t first_chunk, size_t n_chunks,
+                     uint8_t* digests, void* stream);
+
+/* reconstruct (data_only = 0) / reconstruct_data (data_only = 1) for every part.
+ * present: HOST array of n_parts*(d+p) flags (part-major).  Every part must have >= d present
+ * chunks (else CEC_TOO_FEW_SHARDS_PRESENT, nothing launched).  Missing chunks are rebuilt in
+ * place from the first d present chunks of their part (the crate's choice); parts with nothing
+ * missing are skipped.  Parts are grouped by erasure pattern on the host; decode matrices are
+ * inverted once per pattern and cached in the codec. */
+int cec_reconstruct_batch(const cec_codec* codec, const cec_part_batch* batch,
+                          const uint8_t* present, int data_only, void* stream);
+
+/* ---------------------------------------------------------------------------------------- */
+/* Utilities for benchmarks and tests                                                        */
+/* ---------------------------------------------------------------------------------------- */
+
+/* Deterministic synthetic bytes: for every part k, bytes [0, n_chunks*chunk_len) of chunks
+ * 0..n_chunks-1 are filled from a counter-based generator keyed by (seed, k, chunk, offset).
+ * Byte value = cec_synth_byte(seed, k, chunk, offset) (see below). */
+int cec_fill_synthetic(const cec_part_batch* batch, size_t n_chunks, uint64_t seed, void* stream);
+/* Host reference of the generator (same bytes), for checking sampled parts. */
+uint8_t cec_synth_byte(uint64_t seed, uint64_t part, uint64_t chunk, uint64_t offset);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CHUNKY_EC_H */

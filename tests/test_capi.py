@@ -1,0 +1,107 @@
+"""C-ABI library checks that need no GPU: it loads, exports every function include/chunky_ec.h
+declares, and its host-only entry points (codec construction, coding matrix, status names,
+the synthetic-data mirror) behave like the crate / oracle."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "chunky_ec.h")
+LIB = os.path.join(ROOT, "chunky-bits_amd", "chunky_ec", "libchunky_ec.so")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"\b([a-z_0-9]+)\s*\(", src)
+    return sorted({n for n in names if n.startswith("cec_")})
+
+
+def test_header_declares_expected_surface():
+    fns = declared_functions()
+    for must in ["cec_codec_new", "cec_encode_sep", "cec_reconstruct", "cec_reconstruct_data",
+                 "cec_sha256", "cec_part_encode", "cec_encode_batch", "cec_encode_hash_batch",
+                 "cec_reconstruct_batch", "cec_sha256_batch"]:
+        assert must in fns
+
+
+def test_library_exports_every_declared_symbol():
+    assert os.path.exists(LIB), "build first: make -C chunky-bits_amd/csrc"
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True,
+                         check=True).stdout
+    exported = set(re.findall(r" T (cec_\w+)", out))
+    missing = [f for f in declared_functions() if f not in exported]
+    assert not missing, missing
+    lib = ctypes.CDLL(LIB)
+    for f in declared_functions():
+        getattr(lib, f)
+
+
+def test_library_has_gfx950_code_object():
+    data = open(LIB, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data  # offload bundle entry id of the .hip_fatbin
+
+
+def test_status_codes_match_crate_order():
+    import chunky_ec as ce
+    names = ["Ok", "TooFewShards", "TooManyShards", "TooFewDataShards", "TooManyDataShards",
+             "TooFewParityShards", "TooManyParityShards", "TooFewBufferShards",
+             "TooManyBufferShards", "IncorrectShardSize", "TooFewShardsPresent", "EmptyShard",
+             "InvalidShardFlags", "InvalidIndex"]
+    for code, name in enumerate(names):
+        assert ce.status_name(code) == name
+    assert ce.abi_version() == 1
+
+
+@pytest.mark.parametrize("d,p", [(1, 1), (3, 2), (10, 4), (20, 8), (5, 5), (17, 3), (128, 128),
+                                 (1, 255)])
+def test_codec_matrix_matches_oracle(d, p):
+    import chunky_ec as ce
+    rs = ce.ReedSolomon(d, p)
+    assert (rs.data_shard_count(), rs.parity_shard_count(), rs.total_shard_count()) == (d, p, d + p)
+    assert np.array_equal(np.array(rs.matrix(), dtype=np.uint8), oracle.coding_matrix(d, p))
+
+
+def test_codec_new_errors():
+    import chunky_ec as ce
+    for (d, p), code in [((0, 1), ce.TOO_FEW_DATA_SHARDS), ((1, 0), ce.TOO_FEW_PARITY_SHARDS),
+                         ((0, 0), ce.TOO_FEW_DATA_SHARDS), ((200, 57), ce.TOO_MANY_SHARDS)]:
+        with pytest.raises(ce.Error) as e:
+            ce.ReedSolomon(d, p)
+        assert e.value.code == code
+    ce.ReedSolomon(128, 128)
+
+
+def test_argument_errors_precede_device_use():
+    """Crate argument errors are reported before any HIP call (so they hold with or without a
+    GPU); compute entry points without a device report NoDevice rather than computing on CPU."""
+    import chunky_ec as ce
+    rs = ce.ReedSolomon(3, 2)
+    with pytest.raises(ce.Error) as e:
+        rs.encode_sep([b"ab", b"ab"], [bytearray(2), bytearray(2)])
+    assert e.value.code == ce.TOO_FEW_DATA_SHARDS
+    with pytest.raises(ce.Error) as e:
+        rs.encode_sep([b"ab", b"ab", b"a"], [bytearray(2), bytearray(2)])
+    assert e.value.code == ce.INCORRECT_SHARD_SIZE
+    with pytest.raises(ce.Error) as e:
+        rs.reconstruct([b"ab", None, None, None, b"ab"])
+    assert e.value.code == ce.TOO_FEW_SHARDS_PRESENT
+    shards = [b"ab"] * 5
+    rs.reconstruct(shards)  # nothing missing: Ok without touching the device
+    if ce.device_count() == 0:
+        with pytest.raises(ce.Error) as e:
+            rs.encode_sep([b"ab"] * 3, [bytearray(2), bytearray(2)])
+        assert e.value.code == ce.ERR_NO_DEVICE
+
+
+def test_synth_byte_host_mirror_is_deterministic():
+    import chunky_ec as ce
+    a = [ce.synth_byte(7, k, c, o) for k in range(3) for c in range(3) for o in (0, 1, 7, 8, 1000)]
+    b = [ce.synth_byte(7, k, c, o) for k in range(3) for c in range(3) for o in (0, 1, 7, 8, 1000)]
+    assert a == b and len(set(a)) > 10

@@ -1,0 +1,393 @@
+"""GPU parity tests: the HIP path (through the C-ABI) against the oracle, hashlib and the
+committed golden vectors.  Bit-exact everywhere (integer / byte work).
+
+Cases follow the reference's tests and SURVEY.md §8d: KATs (tests/hash.rs), part slicing and
+counts (tests/file.rs:26-56, zeros 2^23+7 bytes), the tests/cluster.rs generator (chunk 2^10,
+d=3, p=2, 683-byte last chunks), delete-and-rebuild (tests/cluster.rs:145-231), every erasure
+pattern of small codes, odd lengths, unaligned layouts, and the full BASELINE shapes via
+size-independent properties (encode -> erase -> reconstruct -> same digests).
+"""
+import hashlib
+import itertools
+
+import numpy as np
+import pytest
+
+import oracle
+from _gen import cluster_reader_bytes, gen_bytes
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+import chunky_ec as ce  # noqa: E402  (after torch: one HIP runtime)
+
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("no GPU", allow_module_level=True)
+
+DEV = torch.device("cuda", 0)
+
+
+def sha(b) -> str:
+    return hashlib.sha256(bytes(b)).hexdigest()
+
+
+# ----------------------------------------------------------------------------------------------
+# SHA-256 (Sha256Hash::from_buf)
+# ----------------------------------------------------------------------------------------------
+
+def test_sha256_reference_and_fips_kats(kats):
+    for v in kats["sha256_reference"] + kats["sha256_fips"]:
+        b = v["input_utf8"].encode() if "input_utf8" in v else \
+            v["input_repeat"][0].encode() * v["input_repeat"][1]
+        h = ce.Sha256Hash.from_buf(b)
+        assert str(h) == v["digest"]
+        assert h.verify(b)
+        assert str(ce.AnyHash(h)) == "sha256-" + v["digest"]
+
+
+def test_sha256_many_lengths_vs_hashlib():
+    lens = [0, 1, 2, 3, 15, 16, 17, 55, 56, 57, 63, 64, 65, 111, 112, 119, 120, 127, 128, 129,
+            191, 192, 683, 1000, 1023, 1024, 4097, 65539, 699051, 1 << 20]
+    bufs = [gen_bytes(900 + n, n).tobytes() for n in lens]
+    hs = ce.Sha256Hash.from_bufs(bufs)
+    for b, h in zip(bufs, hs):
+        assert h.digest == hashlib.sha256(b).digest(), len(b)
+
+
+def test_sha256_verify_detects_single_bit_flip():
+    b = bytearray(gen_bytes(3, 4096).tobytes())
+    h = ce.Sha256Hash.from_buf(bytes(b))
+    b[1234] ^= 0x10
+    assert not h.verify(bytes(b))
+
+
+# ----------------------------------------------------------------------------------------------
+# encode_sep (host-buffer API)
+# ----------------------------------------------------------------------------------------------
+
+def test_encode_one_encode_kat(kats):
+    k = kats["rs_one_encode"]
+    rs = ce.ReedSolomon(k["data_shards"], k["parity_shards"])
+    par = [bytearray(2) for _ in range(k["parity_shards"])]
+    rs.encode_sep([bytes(x) for x in k["data"]], par)
+    assert [list(x) for x in par] == k["parity"]
+
+
+def test_encode_golden(golden):
+    for c in golden["encode"]:
+        d, p, L = c["d"], c["p"], c["len"]
+        data = gen_bytes(c["seed"], d * L).reshape(d, L)
+        rs = ce.ReedSolomon(d, p)
+        par = [bytearray(L) for _ in range(p)]
+        rs.encode_sep([x.tobytes() for x in data], par)
+        assert [sha(x) for x in par] == c["parity_sha256"], (d, p, L)
+        if "parity_hex" in c:
+            assert [bytes(x).hex() for x in par] == c["parity_hex"]
+
+
+@pytest.mark.parametrize("d,p", [(1, 1), (2, 1), (3, 2), (4, 4), (6, 3), (10, 4), (12, 9),
+                                 (20, 8), (16, 16), (30, 2), (64, 8), (200, 56)])
+@pytest.mark.parametrize("L", [1, 7, 16, 33, 4095, 4097, 16385, 20000])
+def test_encode_vs_oracle(d, p, L):
+    data = gen_bytes(d * 1000 + p * 10 + L, d * L).reshape(d, L)
+    st, ref = oracle.encode_sep(d, p, list(data))
+    assert st == 0
+    rs = ce.ReedSolomon(d, p)
+    par = [bytearray(L) for _ in range(p)]
+    rs.encode_sep([x.tobytes() for x in data], par)
+    for i in range(p):
+        assert bytes(par[i]) == ref[i].tobytes(), (d, p, L, i)
+
+
+def test_encode_errors_match_crate():
+    rs = ce.ReedSolomon(3, 2)
+    four = [b"abcd"] * 3
+    cases = [
+        (four[:2], [bytearray(4)] * 2, ce.TOO_FEW_DATA_SHARDS),
+        (four + [b"abcd"], [bytearray(4)] * 2, ce.TOO_MANY_DATA_SHARDS),
+        (four, [bytearray(4)], ce.TOO_FEW_PARITY_SHARDS),
+        (four, [bytearray(4)] * 3, ce.TOO_MANY_PARITY_SHARDS),
+        ([b"abcd", b"abc", b"abcd"], [bytearray(4)] * 2, ce.INCORRECT_SHARD_SIZE),
+        (four, [bytearray(4), bytearray(5)], ce.INCORRECT_SHARD_SIZE),
+        (four, [bytearray(5), bytearray(5)], ce.INCORRECT_SHARD_SIZE),
+        ([b"", b"", b""], [bytearray(0)] * 2, ce.EMPTY_SHARD),
+    ]
+    for data, par, code in cases:
+        with pytest.raises(ce.Error) as e:
+            rs.encode_sep(data, [bytearray(x) for x in par])
+        assert e.value.code == code
+        ost, _ = oracle.encode_sep(3, 2, data, [len(x) for x in par])
+        assert ost == code
+
+
+# ----------------------------------------------------------------------------------------------
+# reconstruct / reconstruct_data (host-buffer API)
+# ----------------------------------------------------------------------------------------------
+
+def _encoded(d, p, L, seed):
+    data = gen_bytes(seed, d * L).reshape(d, L)
+    st, par = oracle.encode_sep(d, p, list(data))
+    return [x.tobytes() for x in data] + [x.tobytes() for x in par]
+
+
+def test_reconstruct_golden(golden):
+    cache = {}
+    for c in golden["reconstruct"]:
+        key = (c["d"], c["p"], c["len"], c["seed"])
+        if key not in cache:
+            cache[key] = _encoded(*key)
+        full = cache[key]
+        rs = ce.ReedSolomon(c["d"], c["p"])
+        shards = [None if i in c["missing"] else bytearray(full[i]) for i in range(len(full))]
+        fn = rs.reconstruct_data if c["data_only"] else rs.reconstruct
+        if c["status"] != 0:
+            with pytest.raises(ce.Error) as e:
+                fn(shards)
+            assert e.value.code == c["status"]
+            continue
+        fn(shards)
+        got = [None if s is None else sha(s) for s in shards]
+        assert got == c["out_sha256"], (c["missing"], c["data_only"])
+
+
+@pytest.mark.parametrize("d,p,L", [(3, 2, 683), (4, 3, 129), (5, 5, 1), (2, 6, 4096)])
+def test_reconstruct_every_pattern(d, p, L):
+    full = _encoded(d, p, L, d * 97 + L)
+    rs = ce.ReedSolomon(d, p)
+    t = d + p
+    for k in range(1, p + 1):
+        for miss in itertools.combinations(range(t), k):
+            shards = [None if i in miss else bytearray(full[i]) for i in range(t)]
+            rs.reconstruct(shards)
+            assert [bytes(s) for s in shards] == full, miss
+            shards = [None if i in miss else bytearray(full[i]) for i in range(t)]
+            rs.reconstruct_data(shards)
+            for i in range(t):
+                if i < d:
+                    assert bytes(shards[i]) == full[i]
+                elif i in miss:
+                    assert shards[i] is None
+
+
+def test_reconstruct_first_d_present_rule():
+    """A corrupt shard beyond the first d present ones is never read (crate behaviour)."""
+    d, p, L = 3, 3, 40
+    full = _encoded(d, p, L, 12)
+    rs = ce.ReedSolomon(d, p)
+    shards = [None, bytearray(full[1]), bytearray(full[2]), bytearray(full[3]),
+              bytearray(b"\xff" * L), bytearray(full[5])]
+    rs.reconstruct_data(shards)
+    assert bytes(shards[0]) == full[0]
+    st, ref = oracle.reconstruct(d, p, [None, full[1], full[2], full[3], b"\xff" * L, full[5]])
+    shards = [None, bytearray(full[1]), bytearray(full[2]), bytearray(full[3]),
+              bytearray(b"\xff" * L), bytearray(full[5])]
+    rs.reconstruct(shards)
+    assert [bytes(s) for s in shards] == [bytes(r) for r in ref]
+
+
+def test_reconstruct_errors_match_crate():
+    rs = ce.ReedSolomon(3, 2)
+    ok = b"abcd"
+    cases = [
+        ([ok] * 4, ce.TOO_FEW_SHARDS),
+        ([ok] * 6, ce.TOO_MANY_SHARDS),
+        ([ok, ok, b"abc", None, None], ce.INCORRECT_SHARD_SIZE),
+        ([ok, b"", ok, None, None], ce.EMPTY_SHARD),
+        ([ok, None, None, None, ok], ce.TOO_FEW_SHARDS_PRESENT),
+    ]
+    for shards, code in cases:
+        with pytest.raises(ce.Error) as e:
+            rs.reconstruct([None if s is None else bytearray(s) for s in shards])
+        assert e.value.code == code
+        assert oracle.reconstruct(3, 2, shards)[0] == code
+
+
+# ----------------------------------------------------------------------------------------------
+# Part layer (FilePart::write_with_encoder compute)
+# ----------------------------------------------------------------------------------------------
+
+def test_part_encode_cluster_fixture(golden):
+    """tests/cluster.rs generator through d=3,p=2 parts of 2^10-byte chunks (7 parts)."""
+    c = golden["cluster"]
+    data = cluster_reader_bytes()
+    rs = ce.ReedSolomon(c["d"], c["p"])
+    step = c["d"] * c["chunk_size"]
+    assert len(c["parts"]) == (len(data) + step - 1) // step
+    for i, part in enumerate(c["parts"]):
+        piece = data[i * step:(i + 1) * step]
+        enc = ce.part_encode(rs, piece, len(piece))
+        assert enc.chunksize == part["chunksize"]
+        assert [str(h) for h in enc.hashes] == part["sha256"]
+
+
+def test_part_encode_zeros_fixture(golden):
+    """tests/file.rs:26-56: zeros of 2^23+7 bytes, 1 MiB chunks, (d, p) in 1..=3."""
+    for z in golden["zeros"]:
+        if (z["d"], z["p"]) not in [(1, 1), (3, 2), (2, 3)]:
+            continue
+        rs = ce.ReedSolomon(z["d"], z["p"])
+        chunk = 1 << 20
+        length = z["length"]
+        step = z["d"] * chunk
+        n_parts = 0
+        for k, off in enumerate(range(0, length, step)):
+            n = min(step, length - off)
+            enc = ce.part_encode(rs, bytes(n), n)
+            assert enc.chunksize == z["parts"][k]["chunksize"]
+            assert [str(h) for h in enc.hashes] == z["parts"][k]["sha256"]
+            n_parts += 1
+        assert n_parts == z["n_parts"]
+
+
+@pytest.mark.parametrize("d,p,length", [(3, 2, 1), (3, 2, 50 * (1 << 20) % (3 << 20) or 7),
+                                        (10, 4, 10 * 65536 + 13), (20, 8, 20 * 4096)])
+def test_part_encode_vs_oracle(d, p, length):
+    buf = gen_bytes(length, length).tobytes()
+    rs = ce.ReedSolomon(d, p)
+    enc = ce.part_encode(rs, buf, length)
+    cs, par, dig = oracle.part_encode(d, p, np.frombuffer(buf, np.uint8), length)
+    assert enc.chunksize == cs
+    assert [bytes(x) for x in enc.parity] == [x.tobytes() for x in par]
+    assert [h.digest for h in enc.hashes] == [x.tobytes() for x in dig]
+
+
+# ----------------------------------------------------------------------------------------------
+# Device-resident batches
+# ----------------------------------------------------------------------------------------------
+
+def _device_parts(n_parts, t, L, cstride=None, seed=1):
+    cstride = cstride or L
+    buf = torch.zeros((n_parts, t, cstride), dtype=torch.uint8, device=DEV)
+    batch = ce.PartBatch.from_tensor(buf, L)
+    ce.fill_synthetic(batch, t, seed)
+    return buf, batch
+
+
+@pytest.mark.parametrize("d,p,L,cstride", [
+    (10, 4, 65536, None),          # aligned fast path
+    (10, 4, 65536 + 13, 65536 + 16),  # aligned strides, ragged tail
+    (3, 2, 683, 683),              # odd stride: unaligned path (reference's packed slices)
+    (20, 8, 4096, None),
+    (6, 10, 1000, 1008),           # > 8 output rows: two row groups
+])
+def test_encode_hash_batch_vs_oracle(d, p, L, cstride):
+    n_parts, t = 24, d + p
+    buf, batch = _device_parts(n_parts, t, L, cstride, seed=d * 31 + L)
+    # synthetic generator mirror: spot-check a few bytes against the host mirror
+    host_before = buf.cpu().numpy()
+    for (k, c, o) in [(0, 0, 0), (3, 1, L - 1), (n_parts - 1, d - 1, L // 2)]:
+        assert host_before[k, c, o] == ce.synth_byte(d * 31 + L, k, c, o)
+    dig = torch.zeros((n_parts, t, 32), dtype=torch.uint8, device=DEV)
+    rs = ce.ReedSolomon(d, p)
+    ce.encode_hash_batch(rs, batch, dig.data_ptr())
+    torch.cuda.synchronize()
+    host = buf.cpu().numpy()
+    hdig = dig.cpu().numpy()
+    for k in range(n_parts):
+        st, par = oracle.encode_sep(d, p, [host[k, j, :L] for j in range(d)])
+        for i in range(p):
+            assert np.array_equal(host[k, d + i, :L], par[i]), (k, i)
+        for j in range(t):
+            assert hdig[k, j].tobytes() == hashlib.sha256(host[k, j, :L].tobytes()).digest()
+    # bytes past chunk_len in the stride padding are untouched
+    if cstride and cstride > L:
+        assert not host[:, d:, L:].any()
+
+
+def test_sha256_batch_subrange():
+    d, p, L = 4, 2, 5000
+    buf, batch = _device_parts(8, d + p, L, 5008, seed=5)
+    dig = torch.zeros((8, 3, 32), dtype=torch.uint8, device=DEV)
+    ce.sha256_batch(batch, 2, 3, dig.data_ptr())
+    torch.cuda.synchronize()
+    host, hd = buf.cpu().numpy(), dig.cpu().numpy()
+    for k in range(8):
+        for c in range(3):
+            assert hd[k, c].tobytes() == hashlib.sha256(host[k, 2 + c, :L].tobytes()).digest()
+
+
+@pytest.mark.parametrize("data_only", [False, True])
+@pytest.mark.parametrize("d,p,L", [(10, 4, 16384), (3, 2, 683), (20, 8, 4096 + 5)])
+def test_reconstruct_batch_random_patterns(d, p, L, data_only):
+    n_parts, t = 96, d + p
+    buf, batch = _device_parts(n_parts, t, L, None, seed=L + d)
+    rs = ce.ReedSolomon(d, p)
+    ce.encode_batch(rs, batch)
+    ref = buf.clone()
+    rng = np.random.default_rng(d * 7 + L)
+    present = np.ones((n_parts, t), dtype=np.uint8)
+    for k in range(n_parts):
+        n_miss = k % (p + 1)  # includes parts with nothing missing
+        present[k, rng.choice(t, n_miss, replace=False)] = 0
+    # erase (zero) the missing chunks
+    mask = torch.from_numpy(present).to(DEV).bool()
+    buf[~mask] = 0
+    ce.reconstruct_batch(rs, batch, present.tobytes(), data_only)
+    torch.cuda.synchronize()
+    got, want = buf.cpu().numpy(), ref.cpu().numpy()
+    for k in range(n_parts):
+        for i in range(t):
+            if present[k, i] or i < d or not data_only:
+                assert np.array_equal(got[k, i], want[k, i]), (k, i)
+            else:  # data_only leaves missing parity untouched (None in the crate)
+                assert not got[k, i].any()
+    # cross-check a few parts against the oracle's reconstruct on the erased inputs
+    for k in range(0, n_parts, 17):
+        shards = [want[k, i].tobytes() if present[k, i] else None for i in range(t)]
+        st, out = oracle.reconstruct(d, p, shards, data_only=data_only)
+        assert st == 0
+        for i in range(t):
+            if out[i] is not None:
+                assert out[i].tobytes() == got[k, i].tobytes()
+
+
+def test_reconstruct_batch_too_few_present_launches_nothing():
+    d, p, L = 3, 2, 256
+    buf, batch = _device_parts(4, d + p, L, None, seed=9)
+    rs = ce.ReedSolomon(d, p)
+    before = buf.clone()
+    present = np.ones((4, d + p), dtype=np.uint8)
+    present[2, :3] = 0  # 2 present < d
+    with pytest.raises(ce.Error) as e:
+        ce.reconstruct_batch(rs, batch, present.tobytes(), False)
+    assert e.value.code == ce.TOO_FEW_SHARDS_PRESENT
+    torch.cuda.synchronize()
+    assert torch.equal(buf, before)
+
+
+# ----------------------------------------------------------------------------------------------
+# Full BASELINE shapes: size-independent properties
+# ----------------------------------------------------------------------------------------------
+
+@pytest.mark.slow
+@pytest.mark.parametrize("d,p,L,n_parts", [(10, 4, 1 << 20, 4096), (20, 8, 256 << 10, 2048)])
+def test_full_size_encode_erase_reconstruct_roundtrip(d, p, L, n_parts):
+    """C2 / C4 at full size: encode+hash, sampled parts vs oracle, then erase 1..p chunks per
+    part, reconstruct, and re-hash: every digest must match the encode-time digest."""
+    t = d + p
+    buf = torch.empty((n_parts, t, L), dtype=torch.uint8, device=DEV)
+    batch = ce.PartBatch.from_tensor(buf, L)
+    ce.fill_synthetic(batch, t, 424242)
+    rs = ce.ReedSolomon(d, p)
+    dig = torch.empty((n_parts, t, 32), dtype=torch.uint8, device=DEV)
+    ce.encode_hash_batch(rs, batch, dig.data_ptr())
+    torch.cuda.synchronize()
+    for k in (0, n_parts // 2 + 1, n_parts - 1):
+        host = buf[k].cpu().numpy()
+        st, par = oracle.encode_sep(d, p, [host[j] for j in range(d)])
+        for i in range(p):
+            assert np.array_equal(host[d + i], par[i])
+        hd = dig[k].cpu().numpy()
+        for j in range(t):
+            assert hd[j].tobytes() == hashlib.sha256(host[j].tobytes()).digest()
+    rng = np.random.default_rng(7)
+    present = np.ones((n_parts, t), dtype=np.uint8)
+    for k in range(n_parts):
+        present[k, rng.choice(t, int(rng.integers(1, p + 1)), replace=False)] = 0
+    mask = torch.from_numpy(present).to(DEV).bool()
+    buf[~mask] = 0
+    ce.reconstruct_batch(rs, batch, present.tobytes(), False)
+    dig2 = torch.empty_like(dig)
+    ce.sha256_batch(batch, 0, t, dig2.data_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(dig, dig2)

@@ -1,0 +1,197 @@
+"""Pin the oracle (oracle/cec_oracle.c) before trusting it (CPU only).
+
+- the reference's own SHA-256 KAT (reference tests/hash.rs:7-8) and FIPS 180-2 vectors;
+- hashlib (OpenSSL) on every length class, scalar and SHA-NI paths;
+- the crate's / JavaReedSolomon's published GF and RS(5,5) known answers;
+- structural properties of the coding matrix and reconstruct (first-d-present rule);
+- the committed golden vectors (tests/golden/golden_vectors.json) reproduce exactly.
+"""
+import hashlib
+import itertools
+
+import numpy as np
+import pytest
+
+import oracle
+from _gen import gen_bytes
+
+
+def _kat_input(v):
+    if "input_utf8" in v:
+        return v["input_utf8"].encode()
+    ch, n = v["input_repeat"]
+    return ch.encode() * n
+
+
+def test_sha256_reference_kat(kats):
+    for v in kats["sha256_reference"]:
+        assert oracle.sha256(_kat_input(v)).hex() == v["digest"]
+
+
+def test_sha256_fips_vectors(kats):
+    for v in kats["sha256_fips"]:
+        assert oracle.sha256(_kat_input(v)).hex() == v["digest"]
+        if oracle.has_shani():
+            assert oracle.sha256_shani(_kat_input(v)).hex() == v["digest"]
+
+
+@pytest.mark.parametrize("n", [0, 1, 3, 55, 56, 57, 63, 64, 65, 119, 120, 127, 128, 129, 683,
+                               1000, 4096, 65539, 699051])
+def test_sha256_vs_hashlib(n):
+    b = gen_bytes(n + 5, n).tobytes()
+    ref = hashlib.sha256(b).digest()
+    assert oracle.sha256(b) == ref
+    if oracle.has_shani():
+        assert oracle.sha256_shani(b) == ref
+
+
+def test_gf_kats(kats):
+    for a, b, r in kats["gf_mul"]:
+        assert oracle.gf_mul(a, b) == r
+    for a, n, r in kats["gf_exp"]:
+        assert oracle.gf_exp(a, n) == r
+
+
+def test_gf_field_axioms():
+    # every nonzero element has an inverse; mul is commutative; distributive over xor
+    for a in range(1, 256):
+        assert oracle.gf_mul(a, oracle.gf_div(1, a)) == 1
+    rng = np.frombuffer(gen_bytes(5, 3000), np.uint8).reshape(-1, 3)
+    for a, b, c in rng:
+        a, b, c = int(a), int(b), int(c)
+        assert oracle.gf_mul(a, b) == oracle.gf_mul(b, a)
+        assert oracle.gf_mul(a, b ^ c) == oracle.gf_mul(a, b) ^ oracle.gf_mul(a, c)
+
+
+def test_rs_one_encode_kat(kats):
+    k = kats["rs_one_encode"]
+    st, par = oracle.encode_sep(k["data_shards"], k["parity_shards"], k["data"])
+    assert st == 0
+    assert [list(map(int, x)) for x in par] == k["parity"]
+
+
+@pytest.mark.parametrize("d,p", [(1, 1), (3, 2), (10, 4), (20, 8), (5, 5), (128, 128), (255, 1)])
+def test_matrix_systematic_and_mds(d, p):
+    m = oracle.coding_matrix(d, p)
+    assert m.shape == (d + p, d)
+    assert np.array_equal(m[:d], np.eye(d, dtype=np.uint8))
+    # MDS: a sample of d-row subsets is invertible
+    t = d + p
+    sel = np.frombuffer(gen_bytes(d * 131 + p, 8 * t), np.uint8)
+    for trial in range(4):
+        rows = sorted(set(int(x) % t for x in sel[trial * t:(trial + 1) * t]))
+        rows = (rows + [r for r in range(t) if r not in rows])[:d]
+        oracle.gf_invert(m[sorted(rows)])
+
+
+def test_matrix_errors():
+    with pytest.raises(ValueError) as e:
+        oracle.coding_matrix(0, 2)
+    assert e.value.args[0] == oracle.TOO_FEW_DATA_SHARDS
+    with pytest.raises(ValueError) as e:
+        oracle.coding_matrix(2, 0)
+    assert e.value.args[0] == oracle.TOO_FEW_PARITY_SHARDS
+    with pytest.raises(ValueError) as e:
+        oracle.coding_matrix(200, 57)
+    assert e.value.args[0] == oracle.TOO_MANY_SHARDS
+    oracle.coding_matrix(200, 56)
+
+
+def test_encode_sep_errors():
+    d4 = [b"abcd"] * 3
+    assert oracle.encode_sep(3, 2, d4[:2])[0] == oracle.TOO_FEW_DATA_SHARDS
+    assert oracle.encode_sep(3, 2, d4 + [b"abcd"])[0] == oracle.TOO_MANY_DATA_SHARDS
+    assert oracle.encode_sep(3, 2, d4, [4])[0] == oracle.TOO_FEW_PARITY_SHARDS
+    assert oracle.encode_sep(3, 2, d4, [4, 4, 4])[0] == oracle.TOO_MANY_PARITY_SHARDS
+    assert oracle.encode_sep(3, 2, [b"abcd", b"abc", b"abcd"])[0] == oracle.INCORRECT_SHARD_SIZE
+    assert oracle.encode_sep(3, 2, d4, [4, 5])[0] == oracle.INCORRECT_SHARD_SIZE
+    assert oracle.encode_sep(3, 2, d4, [5, 5])[0] == oracle.INCORRECT_SHARD_SIZE
+    assert oracle.encode_sep(3, 2, [b"", b"", b""], [0, 0])[0] == oracle.EMPTY_SHARD
+
+
+def test_reconstruct_roundtrip_all_patterns():
+    d, p, L = 4, 3, 129
+    data = gen_bytes(11, d * L).reshape(d, L)
+    st, par = oracle.encode_sep(d, p, list(data))
+    full = [bytes(x) for x in data] + [bytes(x) for x in par]
+    t = d + p
+    for k in range(0, t + 1):
+        for miss in itertools.combinations(range(t), k):
+            shards = [None if i in miss else full[i] for i in range(t)]
+            st, out = oracle.reconstruct(d, p, shards)
+            if k > p:
+                assert st == oracle.TOO_FEW_SHARDS_PRESENT
+                continue
+            assert st == 0
+            assert [bytes(o) for o in out] == full
+            st, out = oracle.reconstruct(d, p, shards, data_only=True)
+            assert st == 0
+            for i in range(t):
+                if i < d:
+                    assert bytes(out[i]) == full[i]
+                elif i in miss:
+                    assert out[i] is None
+
+
+def test_reconstruct_uses_first_d_present():
+    """reconstruct_internal inverts the rows of the FIRST d present shards: corrupting a later
+    present shard must not change the result (the crate never reads it)."""
+    d, p, L = 3, 3, 40
+    data = gen_bytes(12, d * L).reshape(d, L)
+    st, par = oracle.encode_sep(d, p, list(data))
+    full = [bytes(x) for x in data] + [bytes(x) for x in par]
+    shards = [None, full[1], full[2], full[3], b"\xff" * L, full[5]]
+    st, out = oracle.reconstruct(d, p, shards, data_only=True)
+    assert st == 0 and bytes(out[0]) == full[0]
+
+
+def test_reconstruct_errors():
+    d, p = 3, 2
+    ok = b"abcd"
+    assert oracle.reconstruct(d, p, [ok] * 4)[0] == oracle.TOO_FEW_SHARDS
+    assert oracle.reconstruct(d, p, [ok] * 6)[0] == oracle.TOO_MANY_SHARDS
+    assert oracle.reconstruct(d, p, [ok, ok, b"abc", None, None])[0] == oracle.INCORRECT_SHARD_SIZE
+    assert oracle.reconstruct(d, p, [ok, b"", ok, None, None])[0] == oracle.EMPTY_SHARD
+    assert oracle.reconstruct(d, p, [ok, None, None, None, ok])[0] == oracle.TOO_FEW_SHARDS_PRESENT
+    assert oracle.reconstruct(d, p, [ok] * 5)[0] == 0
+
+
+def test_golden_encode(golden):
+    for c in golden["encode"]:
+        data = gen_bytes(c["seed"], c["d"] * c["len"]).reshape(c["d"], c["len"])
+        st, par = oracle.encode_sep(c["d"], c["p"], list(data))
+        assert st == 0
+        assert [hashlib.sha256(bytes(x)).hexdigest() for x in par] == c["parity_sha256"]
+        if "parity_hex" in c:
+            assert [bytes(x).hex() for x in par] == c["parity_hex"]
+
+
+def test_golden_reconstruct(golden):
+    cache = {}
+    for c in golden["reconstruct"]:
+        key = (c["d"], c["p"], c["len"], c["seed"])
+        if key not in cache:
+            data = gen_bytes(c["seed"], c["d"] * c["len"]).reshape(c["d"], c["len"])
+            st, par = oracle.encode_sep(c["d"], c["p"], list(data))
+            cache[key] = [bytes(x) for x in data] + [bytes(x) for x in par]
+        full = cache[key]
+        shards = [None if i in c["missing"] else full[i] for i in range(len(full))]
+        st, out = oracle.reconstruct(c["d"], c["p"], shards, data_only=c["data_only"])
+        assert st == c["status"]
+        if st == 0:
+            got = [None if o is None else hashlib.sha256(bytes(o)).hexdigest() for o in out]
+            assert got == c["out_sha256"]
+
+
+def test_golden_cluster_parts(golden):
+    from _gen import cluster_reader_bytes
+    c = golden["cluster"]
+    data = cluster_reader_bytes()
+    assert hashlib.sha256(data).hexdigest() == c["data_sha256"]
+    step = c["d"] * c["chunk_size"]
+    for i, part in enumerate(c["parts"]):
+        piece = data[i * step:(i + 1) * step]
+        cs, par, dig = oracle.part_encode(c["d"], c["p"], np.frombuffer(piece, np.uint8),
+                                          len(piece))
+        assert cs == part["chunksize"]
+        assert [bytes(x).hex() for x in dig] == part["sha256"]
