@@ -1,13 +1,10 @@
-// kernels.hip — gfx950 (MI355X, CDNA4) kernels of the erasure-coding + chunk-hashing engine.
+// rs_kernels.hip — gfx950 (MI355X, CDNA4) GF(2^8) Reed-Solomon kernels + synthetic fill.
 //
 //  rs_apply_kernel   GF(2^8) matrix x chunk-set multiply.  One kernel serves
 //                    ReedSolomon::encode_sep (rows = parity rows of M, inputs = the d data chunks)
 //                    and reconstruct / reconstruct_data (rows = decode rows, inputs = the first d
 //                    present chunks), for thousands of parts per launch.  HBM-bound:
 //                    algorithmic bytes per part = (d + n_out) * len.
-//  sha256_kernel     FIPS 180-4 SHA-256, one lane per chunk (Sha256Hash::from_buf,
-//                    src/file/hash/sha256.rs:20-26).  VALU-bound: a chunk is a serial chain of
-//                    64-byte compressions, so parallelism = number of chunks.
 //  fill_kernel       counter-based synthetic bytes for benchmarks/tests.
 //
 // GF multiply: no GF instruction exists, so a product c*x of four packed bytes is three
@@ -15,8 +12,9 @@
 // with one v_bitop3_b32 (xor3).  The selectors of a data word are shared by every output row.
 // Coefficient tables are wave-uniform and come in through scalar loads (s_load), so a row costs
 // 3 v_perm + ~1.5 xor per data dword, with no LDS traffic and no bank conflicts.
-#include "kernels.hpp"
+#include "device_common.hpp"
 #include "gf256.hpp"
+#include "kernels.hpp"
 
 namespace cec {
 namespace {
@@ -24,15 +22,6 @@ namespace {
 constexpr int kApplyThreads = 256;
 constexpr int kApplyIters = 4;  // 16-byte columns per thread per block
 constexpr uint64_t kApplyTile = uint64_t(kApplyThreads) * 16u * kApplyIters;  // 16 KiB
-
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
-}
-
-// v_perm_b32: byte lane i of the result = byte sel[i] (0..7) of the 8-byte value {hi:lo}.
-__device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
-    return __builtin_amdgcn_perm(hi, lo, sel);
-}
 
 struct Sel {
     uint32_t s0, s1, s2;
@@ -46,28 +35,6 @@ __device__ __forceinline__ Sel selectors(uint32_t x) {
 __device__ __forceinline__ uint32_t gmul(const Sel& s, uint32_t t0, uint32_t t1, uint32_t t2,
                                          uint32_t t3, uint32_t t4) {
     return xor3(perm(t1, t0, s.s0), perm(t3, t2, s.s1), perm(0u, t4, s.s2));
-}
-
-__device__ __forceinline__ uint4 load_partial(const uint8_t* p, uint64_t n) {
-    uint32_t w[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int k = 0; k < 16; ++k)
-        if (uint64_t(k) < n) w[k >> 2] |= uint32_t(p[k]) << (8 * (k & 3));
-    return make_uint4(w[0], w[1], w[2], w[3]);
-}
-
-__device__ __forceinline__ void store_partial(uint8_t* p, const uint32_t w[4], uint64_t n) {
-#pragma unroll
-    for (int k = 0; k < 16; ++k)
-        if (uint64_t(k) < n) p[k] = uint8_t(w[k >> 2] >> (8 * (k & 3)));
-}
-
-// Wave-uniform metadata (pattern records, part maps) is read through the constant address space
-// so it lands in SGPRs via s_load instead of per-lane vector loads.
-typedef __attribute__((address_space(4))) const uint32_t cu32;
-
-__device__ __forceinline__ cu32* as_const(const uint32_t* p) {
-    return (cu32*)(p);
 }
 
 // One 16-byte column (x .. x+16) of a part: acc[r] = XOR_j coef[r][j] (x) in_j[x..x+16).
@@ -157,169 +124,6 @@ __global__ __launch_bounds__(kApplyThreads) void rs_apply_kernel(ApplyParams a,
 }
 
 // ------------------------------------------------------------------------------------------
-// SHA-256
-// ------------------------------------------------------------------------------------------
-
-constexpr uint32_t kK[64] = {
-    0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u,
-    0xab1c5ed5u, 0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu,
-    0x9bdc06a7u, 0xc19bf174u, 0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu,
-    0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau, 0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u,
-    0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u, 0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu,
-    0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u, 0xa2bfe8a1u, 0xa81a664bu,
-    0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u, 0x19a4c116u,
-    0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
-    0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u,
-    0xc67178f2u};
-
-__device__ __forceinline__ uint32_t rotr(uint32_t x, int n) {
-    return __builtin_amdgcn_alignbit(x, x, n);
-}
-
-__device__ __forceinline__ uint32_t bswap32(uint32_t x) {
-    return __builtin_amdgcn_perm(x, x, 0x00010203u);
-}
-
-// One 64-byte compression; w[] holds the 16 big-endian message words (clobbered).
-__device__ __forceinline__ void sha256_compress(uint32_t st[8], uint32_t w[16]) {
-    uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
-    uint32_t e = st[4], f = st[5], g = st[6], h = st[7];
-#pragma unroll
-    for (int i = 0; i < 64; ++i) {
-        uint32_t wi;
-        if (i < 16) {
-            wi = w[i];
-        } else {
-            const uint32_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
-            const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
-            const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
-            wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
-            w[i & 15] = wi;
-        }
-        const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
-        const uint32_t ch = (e & f) ^ (~e & g);
-        const uint32_t t1 = h + S1 + ch + kK[i] + wi;
-        const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
-        const uint32_t mj = (a & b) | (c & (a | b));
-        const uint32_t t2 = S0 + mj;
-        h = g;
-        g = f;
-        f = e;
-        e = d + t1;
-        d = c;
-        c = b;
-        b = a;
-        a = t1 + t2;
-    }
-    st[0] += a;
-    st[1] += b;
-    st[2] += c;
-    st[3] += d;
-    st[4] += e;
-    st[5] += f;
-    st[6] += g;
-    st[7] += h;
-}
-
-template <bool VEC>
-__device__ __forceinline__ void load_block(const uint8_t* p, uint4 q[4]) {
-    if (VEC) {
-        const uint4* v = reinterpret_cast<const uint4*>(p);
-        q[0] = v[0];
-        q[1] = v[1];
-        q[2] = v[2];
-        q[3] = v[3];
-    } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) q[i] = load_partial(p + 16 * i, 16);
-    }
-}
-
-__device__ __forceinline__ void block_words(const uint4 q[4], uint32_t w[16]) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        w[4 * i + 0] = bswap32(q[i].x);
-        w[4 * i + 1] = bswap32(q[i].y);
-        w[4 * i + 2] = bswap32(q[i].z);
-        w[4 * i + 3] = bswap32(q[i].w);
-    }
-}
-
-__device__ __forceinline__ void sha256_chunk(const uint8_t* p, uint64_t len, uint32_t st[8],
-                                             bool vec) {
-    st[0] = 0x6a09e667u;
-    st[1] = 0xbb67ae85u;
-    st[2] = 0x3c6ef372u;
-    st[3] = 0xa54ff53au;
-    st[4] = 0x510e527fu;
-    st[5] = 0x9b05688cu;
-    st[6] = 0x1f83d9abu;
-    st[7] = 0x5be0cd19u;
-    const uint64_t nfull = len >> 6;
-    uint32_t w[16];
-    if (nfull) {
-        uint4 q[4];
-        if (vec) load_block<true>(p, q);
-        else load_block<false>(p, q);
-#pragma unroll 1
-        for (uint64_t b = 0; b < nfull; ++b) {
-            block_words(q, w);
-            if (b + 1 < nfull) {
-                if (vec) load_block<true>(p + 64 * (b + 1), q);
-                else load_block<false>(p + 64 * (b + 1), q);
-            }
-            sha256_compress(st, w);
-        }
-    }
-    const uint8_t* tp = p + 64 * nfull;
-    const uint32_t rem = uint32_t(len - 64 * nfull);
-    const uint32_t tb = (rem + 9 <= 64) ? 1u : 2u;
-    const uint64_t bits = len * 8;
-#pragma unroll 1
-    for (uint32_t blk = 0; blk < tb; ++blk) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            uint32_t word = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t pos = blk * 64 + uint32_t(i * 4 + k);
-                const uint32_t byte = pos < rem ? uint32_t(tp[pos]) : (pos == rem ? 0x80u : 0u);
-                word = (word << 8) | byte;
-            }
-            w[i] = word;
-        }
-        if (blk == tb - 1) {
-            w[14] = uint32_t(bits >> 32);
-            w[15] = uint32_t(bits);
-        }
-        sha256_compress(st, w);
-    }
-}
-
-template <bool VEC>
-__global__ __launch_bounds__(64) void sha256_kernel(ShaParams a) {
-    const uint32_t item = blockIdx.x * 64u + threadIdx.x;
-    const uint32_t total = a.n_parts * a.n_chunks;
-    if (item >= total) return;
-    const uint8_t* p;
-    uint64_t len;
-    if (a.ptrs) {
-        p = reinterpret_cast<const uint8_t*>(a.ptrs[item]);
-        len = a.lens[item];
-    } else {
-        const uint32_t k = item / a.n_chunks;
-        const uint32_t c = item - k * a.n_chunks;
-        p = a.base + uint64_t(k) * a.part_stride + uint64_t(a.first_chunk + c) * a.chunk_stride;
-        len = a.len;
-    }
-    uint32_t st[8];
-    sha256_chunk(p, len, st, VEC);
-    uint4* out = reinterpret_cast<uint4*>(a.digests + uint64_t(item) * 32u);
-    out[0] = make_uint4(bswap32(st[0]), bswap32(st[1]), bswap32(st[2]), bswap32(st[3]));
-    out[1] = make_uint4(bswap32(st[4]), bswap32(st[5]), bswap32(st[6]), bswap32(st[7]));
-}
-
-// ------------------------------------------------------------------------------------------
 // Synthetic data
 // ------------------------------------------------------------------------------------------
 
@@ -405,15 +209,6 @@ hipError_t launch_rs_apply(const ApplyParams& a, bool vec16, hipStream_t s) {
     }
     if (rem) return launch_rows(a, rem, full * kMaxRows, 1, vec16, s);
     return hipSuccess;
-}
-
-hipError_t launch_sha256(const ShaParams& a, bool vec16, hipStream_t s) {
-    const uint64_t total = uint64_t(a.n_parts) * a.n_chunks;
-    if (total == 0) return hipSuccess;
-    dim3 grid(uint32_t((total + 63) / 64));
-    if (vec16) hipLaunchKernelGGL((sha256_kernel<true>), grid, dim3(64), 0, s, a);
-    else hipLaunchKernelGGL((sha256_kernel<false>), grid, dim3(64), 0, s, a);
-    return hipGetLastError();
 }
 
 hipError_t launch_fill(const FillParams& a, hipStream_t s) {
