@@ -8,7 +8,7 @@
 // rotate (v_alignbit_b32) and 3-input add (v_add3_u32) that SHA-256 lives on are half-rate ops:
 // one wave per SIMD is issue-bound.  Two kernels:
 //
-//  sha256_lane_kernel   (v1, default) one lane = one chunk; 64-thread workgroups.  Message
+//  sha256_lane_kernel   (v1, default) one lane = one chunk, one wave per SIMD.  Message
 //                       load, byte swap, message schedule and the 64 rounds all in one wave;
 //                       T1 = (h + K[t]+W[t] + Ch) + Sigma1 adds the long-latency Sigma1 last, and
 //                       Ch/Maj are single full-rate v_bitop3 (1482 VALU per block, ~4.2 cycles
@@ -186,10 +186,18 @@ __device__ __forceinline__ void compress(uint32_t st[8], uint32_t w[16]) {
     st[7] += h;
 }
 
-template <bool VEC, int SPW>
-__global__ __launch_bounds__(64) void sha256_lane_kernel(ShaParams a) {
-    const uint32_t item = blockIdx.x * uint32_t(SPW) + threadIdx.x;
-    if (threadIdx.x >= uint32_t(SPW) || item >= a.n_parts * a.n_chunks) return;
+// 256-thread workgroups: the four waves of a workgroup land on the four SIMDs of a CU, and
+// launch_sha256 reserves enough (otherwise unused) LDS that at most one such workgroup fits on
+// a CU.  The waves of this kernel live for the whole launch, so this pins exactly one wave per
+// SIMD whatever ran before: without it, launched behind the encode kernel the dispatcher stacked
+// two waves on some SIMDs and the launch took 80 ms instead of 42 ms (C2, MI355X).
+constexpr int kLaneThreads = 256;
+
+template <bool VEC>
+__global__ __launch_bounds__(kLaneThreads) void sha256_lane_kernel(ShaParams a) {
+    extern __shared__ uint32_t cu_reservation[];  // never touched: occupancy control only
+    const uint32_t item = blockIdx.x * uint32_t(kLaneThreads) + threadIdx.x;
+    if (item >= a.n_parts * a.n_chunks) return;
     const uint8_t* p;
     uint64_t len;
     item_source(a, item, p, len);
@@ -314,29 +322,47 @@ int sha_variant() {
     return e ? std::atoi(e) : 1;
 }
 
-template <int SPW>
-void launch_variant(int variant, const ShaParams& a, bool vec16, hipStream_t s) {
+// Dynamic LDS requested per lane-kernel workgroup: more than half of the 160 KiB of a CU, so
+// two workgroups never share a CU.
+constexpr size_t kCuReservation = 96 * 1024;
+
+hipError_t launch_lane(const ShaParams& a, bool vec16, hipStream_t s) {
+    static const bool attr_ok = [] {
+        return hipFuncSetAttribute(reinterpret_cast<const void*>(&sha256_lane_kernel<true>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   int(kCuReservation)) == hipSuccess &&
+               hipFuncSetAttribute(reinterpret_cast<const void*>(&sha256_lane_kernel<false>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   int(kCuReservation)) == hipSuccess;
+    }();
+    if (!attr_ok) return hipErrorInvalidValue;
     const uint64_t total = uint64_t(a.n_parts) * a.n_chunks;
-    dim3 grid(uint32_t((total + SPW - 1) / SPW));
-    if (variant == 1) {
-        if (vec16) hipLaunchKernelGGL((sha256_lane_kernel<true, SPW>), grid, dim3(64), 0, s, a);
-        else hipLaunchKernelGGL((sha256_lane_kernel<false, SPW>), grid, dim3(64), 0, s, a);
-    } else {
-        if (vec16) hipLaunchKernelGGL((sha256_split_kernel<true, SPW>), grid, dim3(128), 0, s, a);
-        else hipLaunchKernelGGL((sha256_split_kernel<false, SPW>), grid, dim3(128), 0, s, a);
-    }
+    dim3 grid(uint32_t((total + kLaneThreads - 1) / kLaneThreads));
+    if (vec16)
+        hipLaunchKernelGGL((sha256_lane_kernel<true>), grid, dim3(kLaneThreads), kCuReservation,
+                           s, a);
+    else
+        hipLaunchKernelGGL((sha256_lane_kernel<false>), grid, dim3(kLaneThreads),
+                           kCuReservation, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_split(const ShaParams& a, bool vec16, hipStream_t s) {
+    const uint64_t total = uint64_t(a.n_parts) * a.n_chunks;
+    dim3 grid(uint32_t((total + 63) / 64));
+    if (vec16) hipLaunchKernelGGL((sha256_split_kernel<true, 64>), grid, dim3(128), 0, s, a);
+    else hipLaunchKernelGGL((sha256_split_kernel<false, 64>), grid, dim3(128), 0, s, a);
+    return hipGetLastError();
 }
 
 }  // namespace
 
-// CEC_SHA_VARIANT (tuning knob, read per launch): 1 = one lane per chunk (default; fastest
-// measured on MI355X: 43.3 ms for C2 vs 50.6 ms for the split kernel), 2 = split
+// CEC_SHA_VARIANT (tuning knob, read per launch): 1 = one lane per chunk (default), 2 = split
 // producer/rounds waves.
 hipError_t launch_sha256(const ShaParams& a, bool vec16, hipStream_t s) {
     const uint64_t total = uint64_t(a.n_parts) * a.n_chunks;
     if (total == 0) return hipSuccess;
-    launch_variant<64>(sha_variant() == 2 ? 2 : 1, a, vec16, s);
-    return hipGetLastError();
+    return sha_variant() == 2 ? launch_split(a, vec16, s) : launch_lane(a, vec16, s);
 }
 
 }  // namespace cec

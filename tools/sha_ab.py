@@ -21,13 +21,16 @@ def main():
     ap.add_argument("--chunks", type=int, default=14)
     ap.add_argument("--chunk", type=int, default=1 << 20)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--variants", default="1,2,3,4")
+    ap.add_argument("--variants", default="1,2")
+    ap.add_argument("--encode-first", action="store_true",
+                    help="launch an RS(10,4) encode on the same stream right before each SHA")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     buf = torch.empty((args.parts, args.chunks, args.chunk), dtype=torch.uint8, device=dev)
     batch = ce.PartBatch.from_tensor(buf)
     ce.fill_synthetic(batch, args.chunks, 99)
     variants = [int(v) for v in args.variants.split(",")]
+    codec = ce.ReedSolomon(10, 4) if args.chunks == 14 else None
     digs = {v: torch.empty((args.parts, args.chunks, 32), dtype=torch.uint8, device=dev)
             for v in variants}
     times = {v: [] for v in variants}
@@ -36,6 +39,10 @@ def main():
         for v in variants:
             os.environ["CEC_SHA_VARIANT"] = str(v)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            if args.encode_first:
+                ce.encode_batch(codec, ce.PartBatch(batch.base, batch.part_stride,
+                                                    batch.chunk_stride, batch.n_parts,
+                                                    batch.chunk_len), s)
             e0.record(s)
             ce.sha256_batch(batch, 0, args.chunks, digs[v].data_ptr(), s)
             e1.record(s)
