@@ -75,6 +75,22 @@ def barrier(world: int):
         dist.barrier()
 
 
+KERNEL_SYMBOL = {"sha256_kernel": "sha256_lane_kernel", "rs_apply_kernel": "rs_apply_kernel",
+                 "rs_apply_kernel(reconstruct)": "rs_apply_kernel",
+                 "encode_hash_kernel": "encode_hash_kernel"}
+
+
+def measured_traffic(config: str, kernel: str, full_size: bool):
+    """HBM bytes per launch of `kernel` from the committed PMC runs (profiles/traffic.json,
+    written by profiles/summarize.py from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes
+    with the gfx950 x2 FETCH_SIZE correction), or None when this workload was not profiled."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    if not full_size or not os.path.exists(path):
+        return None
+    entry = json.load(open(path)).get(config, {}).get(KERNEL_SYMBOL.get(kernel, kernel))
+    return entry["bytes_per_launch"] if entry else None
+
+
 def cpu_baseline(cfg, threads: int):
     """Oracle restatement of the crate path timed on this host (rank 0, N=1 only)."""
     import oracle
@@ -220,6 +236,7 @@ def main():
     dom_name = max(kernels, key=lambda k: kernels[k]["ms"])
     dom = kernels[dom_name]
     achieved = dom["algorithmic_bytes"] / (dom["ms"] / 1e3) / 1e9
+    traffic = measured_traffic(args.config, dom_name, n_parts == CONFIGS[args.config]["parts"])
 
     ok = None
     if args.check and rank == 0 and cfg["op"] != "reconstruct":
@@ -264,7 +281,7 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": None,
+                "traffic": traffic,
             },
             "kernels": kernels,
         }

@@ -1,0 +1,310 @@
+//! Rust side of the drop-in boundary (include/chunky_ec.h).
+//!
+//! `sys` mirrors the C-ABI one-to-one; [`ReedSolomon`] and [`sha256`] reproduce the surface of
+//! `reed_solomon_erasure::ReedSolomon<galois_8::Field>` and `sha2::Sha256::digest` that
+//! Chunky Bits calls (src/file/file_part.rs:77,128,161-165,185,302-304), returning the crate's
+//! own `reed_solomon_erasure::Error` so `FileWriteError::Erasure` / `FileReadError::Erasure`
+//! keep working unchanged.  Written against the header; compile-checked only where `cargo` is
+//! available (not in the build container — see DESIGN.md).
+use std::os::raw::{c_int, c_void};
+
+pub mod sys {
+    use super::*;
+
+    #[repr(C)]
+    pub struct cec_codec {
+        _private: [u8; 0],
+    }
+
+    #[repr(C)]
+    #[derive(Clone, Copy, Debug)]
+    pub struct cec_part_batch {
+        pub base: *mut u8,
+        pub part_stride: usize,
+        pub chunk_stride: usize,
+        pub n_parts: usize,
+        pub chunk_len: usize,
+    }
+
+    extern "C" {
+        pub fn cec_abi_version() -> c_int;
+        pub fn cec_status_name(status: c_int) -> *const std::os::raw::c_char;
+        pub fn cec_last_error() -> *const std::os::raw::c_char;
+        pub fn cec_device_count() -> c_int;
+        pub fn cec_codec_new(d: usize, p: usize, out: *mut *mut cec_codec) -> c_int;
+        pub fn cec_codec_free(codec: *mut cec_codec);
+        pub fn cec_codec_data_shards(codec: *const cec_codec) -> usize;
+        pub fn cec_codec_parity_shards(codec: *const cec_codec) -> usize;
+        pub fn cec_codec_total_shards(codec: *const cec_codec) -> usize;
+        pub fn cec_codec_matrix(codec: *const cec_codec, out: *mut u8, out_len: usize) -> c_int;
+        pub fn cec_encode_sep(
+            codec: *const cec_codec,
+            data: *const *const u8,
+            data_lens: *const usize,
+            n_data: usize,
+            parity: *const *mut u8,
+            parity_lens: *const usize,
+            n_parity: usize,
+        ) -> c_int;
+        pub fn cec_reconstruct(
+            codec: *const cec_codec,
+            shards: *const *mut u8,
+            shard_lens: *const usize,
+            present: *mut u8,
+            n_shards: usize,
+        ) -> c_int;
+        pub fn cec_reconstruct_data(
+            codec: *const cec_codec,
+            shards: *const *mut u8,
+            shard_lens: *const usize,
+            present: *mut u8,
+            n_shards: usize,
+        ) -> c_int;
+        pub fn cec_sha256(buf: *const u8, len: usize, out32: *mut u8) -> c_int;
+        pub fn cec_sha256_many(
+            bufs: *const *const u8,
+            lens: *const usize,
+            n: usize,
+            out: *mut u8,
+        ) -> c_int;
+        pub fn cec_part_encode(
+            codec: *const cec_codec,
+            data_buf: *const u8,
+            length: usize,
+            parity_out: *mut u8,
+            digests_out: *mut u8,
+            chunksize: *mut usize,
+        ) -> c_int;
+        pub fn cec_encode_batch(
+            codec: *const cec_codec,
+            batch: *const cec_part_batch,
+            stream: *mut c_void,
+        ) -> c_int;
+        pub fn cec_encode_hash_batch(
+            codec: *const cec_codec,
+            batch: *const cec_part_batch,
+            digests: *mut u8,
+            stream: *mut c_void,
+        ) -> c_int;
+        pub fn cec_sha256_batch(
+            batch: *const cec_part_batch,
+            first_chunk: usize,
+            n_chunks: usize,
+            digests: *mut u8,
+            stream: *mut c_void,
+        ) -> c_int;
+        pub fn cec_reconstruct_batch(
+            codec: *const cec_codec,
+            batch: *const cec_part_batch,
+            present: *const u8,
+            data_only: c_int,
+            stream: *mut c_void,
+        ) -> c_int;
+    }
+}
+
+pub use reed_solomon_erasure::Error;
+
+/// Engine failures with no crate equivalent (no GPU, HIP error, allocation failure).
+#[derive(Debug)]
+pub struct EngineError {
+    pub code: c_int,
+    pub message: String,
+}
+
+/// Error of a call through the boundary: a crate error (codes 1..13) or an engine error.
+#[derive(Debug)]
+pub enum CecError {
+    Erasure(Error),
+    Engine(EngineError),
+}
+
+impl From<CecError> for Error {
+    /// For call sites typed `Result<_, reed_solomon_erasure::Error>`; engine errors have no
+    /// crate variant and abort loudly instead of being disguised as one.
+    fn from(e: CecError) -> Error {
+        match e {
+            CecError::Erasure(e) => e,
+            CecError::Engine(e) => panic!("chunky_ec engine error {}: {}", e.code, e.message),
+        }
+    }
+}
+
+fn check(code: c_int) -> Result<(), CecError> {
+    Err(CecError::Erasure(match code {
+        0 => return Ok(()),
+        1 => Error::TooFewShards,
+        2 => Error::TooManyShards,
+        3 => Error::TooFewDataShards,
+        4 => Error::TooManyDataShards,
+        5 => Error::TooFewParityShards,
+        6 => Error::TooManyParityShards,
+        7 => Error::TooFewBufferShards,
+        8 => Error::TooManyBufferShards,
+        9 => Error::IncorrectShardSize,
+        10 => Error::TooFewShardsPresent,
+        11 => Error::EmptyShard,
+        12 => Error::InvalidShardFlags,
+        13 => Error::InvalidIndex,
+        other => {
+            let message = unsafe { std::ffi::CStr::from_ptr(sys::cec_last_error()) }
+                .to_string_lossy()
+                .into_owned();
+            return Err(CecError::Engine(EngineError { code: other, message }));
+        },
+    }))
+}
+
+/// `ReedSolomon<galois_8::Field>` backed by the gfx950 kernels.  Immutable after `new`, so it
+/// is `Send + Sync` and can be shared through `Arc` exactly like the crate's (writer.rs:131).
+pub struct ReedSolomon {
+    raw: *mut sys::cec_codec,
+}
+
+unsafe impl Send for ReedSolomon {}
+unsafe impl Sync for ReedSolomon {}
+
+impl Drop for ReedSolomon {
+    fn drop(&mut self) {
+        unsafe { sys::cec_codec_free(self.raw) }
+    }
+}
+
+impl ReedSolomon {
+    pub fn new(data_shards: usize, parity_shards: usize) -> Result<ReedSolomon, Error> {
+        let mut raw = std::ptr::null_mut();
+        check(unsafe { sys::cec_codec_new(data_shards, parity_shards, &mut raw) })?;
+        Ok(ReedSolomon { raw })
+    }
+
+    pub fn data_shard_count(&self) -> usize {
+        unsafe { sys::cec_codec_data_shards(self.raw) }
+    }
+
+    pub fn parity_shard_count(&self) -> usize {
+        unsafe { sys::cec_codec_parity_shards(self.raw) }
+    }
+
+    pub fn total_shard_count(&self) -> usize {
+        unsafe { sys::cec_codec_total_shards(self.raw) }
+    }
+
+    /// `encode_sep::<T, U>(&data, &mut parity)`.
+    pub fn encode_sep<T: AsRef<[u8]>, U: AsRef<[u8]> + AsMut<[u8]>>(
+        &self,
+        data: &[T],
+        parity: &mut [U],
+    ) -> Result<(), Error> {
+        let dptr: Vec<*const u8> = data.iter().map(|d| d.as_ref().as_ptr()).collect();
+        let dlen: Vec<usize> = data.iter().map(|d| d.as_ref().len()).collect();
+        let plen: Vec<usize> = parity.iter().map(|p| p.as_ref().len()).collect();
+        let pptr: Vec<*mut u8> = parity.iter_mut().map(|p| p.as_mut().as_mut_ptr()).collect();
+        check(unsafe {
+            sys::cec_encode_sep(
+                self.raw,
+                dptr.as_ptr(),
+                dlen.as_ptr(),
+                dptr.len(),
+                pptr.as_ptr(),
+                plen.as_ptr(),
+                pptr.len(),
+            )
+        })?;
+        Ok(())
+    }
+
+    fn reconstruct_inner(&self, shards: &mut [Option<Vec<u8>>], data_only: bool) -> Result<(), Error> {
+        // The crate allocates missing slots zeroed at the present length; do the same so the
+        // engine writes straight into the caller's Vec.
+        let len = shards.iter().flatten().map(|s| s.len()).find(|&l| l > 0).unwrap_or(0);
+        let mut present: Vec<u8> = shards.iter().map(|s| s.is_some() as u8).collect();
+        let d = self.data_shard_count();
+        let mut scratch: Vec<Option<Vec<u8>>> = shards
+            .iter()
+            .enumerate()
+            .map(|(i, s)| match s {
+                None if !(data_only && i >= d) => Some(vec![0u8; len]),
+                _ => None,
+            })
+            .collect();
+        let ptrs: Vec<*mut u8> = shards
+            .iter_mut()
+            .zip(scratch.iter_mut())
+            .map(|(s, t)| match (s, t) {
+                (Some(v), _) => v.as_mut_ptr(),
+                (None, Some(v)) => v.as_mut_ptr(),
+                (None, None) => std::ptr::null_mut(),
+            })
+            .collect();
+        let lens: Vec<usize> = shards
+            .iter()
+            .zip(scratch.iter())
+            .map(|(s, t)| s.as_ref().or(t.as_ref()).map(|v| v.len()).unwrap_or(0))
+            .collect();
+        let f = if data_only { sys::cec_reconstruct_data } else { sys::cec_reconstruct };
+        check(unsafe { f(self.raw, ptrs.as_ptr(), lens.as_ptr(), present.as_mut_ptr(), ptrs.len()) })?;
+        for (i, slot) in shards.iter_mut().enumerate() {
+            if slot.is_none() && present[i] != 0 {
+                *slot = scratch[i].take();
+            }
+        }
+        Ok(())
+    }
+
+    /// `reconstruct(&mut shards)`: rebuilds missing data and parity.
+    pub fn reconstruct(&self, shards: &mut [Option<Vec<u8>>]) -> Result<(), Error> {
+        self.reconstruct_inner(shards, false)
+    }
+
+    /// `reconstruct_data(&mut shards)`: rebuilds missing data only.
+    pub fn reconstruct_data(&self, shards: &mut [Option<Vec<u8>>]) -> Result<(), Error> {
+        self.reconstruct_inner(shards, true)
+    }
+
+    pub fn as_raw(&self) -> *const sys::cec_codec {
+        self.raw
+    }
+}
+
+/// `Sha256::digest(buf)` (sha256.rs:20-26) computed on the GPU.
+pub fn sha256(buf: &[u8]) -> [u8; 32] {
+    let mut out = [0u8; 32];
+    check(unsafe { sys::cec_sha256(buf.as_ptr(), buf.len(), out.as_mut_ptr()) })
+        .map_err(Error::from)
+        .expect("cec_sha256");
+    out
+}
+
+/// `FilePart::write_with_encoder`'s compute for one part: (chunksize, parity chunks, d+p digests).
+pub fn part_encode(
+    codec: &ReedSolomon,
+    data_buf: &[u8],
+    length: usize,
+) -> Result<(usize, Vec<Vec<u8>>, Vec<[u8; 32]>), Error> {
+    let d = codec.data_shard_count();
+    let p = codec.parity_shard_count();
+    let l = (length + d - 1) / d;
+    let mut parity = vec![0u8; p * l];
+    let mut digests = vec![0u8; 32 * (d + p)];
+    let mut chunksize = 0usize;
+    check(unsafe {
+        sys::cec_part_encode(
+            codec.raw,
+            data_buf.as_ptr(),
+            length,
+            parity.as_mut_ptr(),
+            digests.as_mut_ptr(),
+            &mut chunksize,
+        )
+    })?;
+    let parity = parity.chunks(l.max(1)).map(|c| c.to_vec()).take(p).collect();
+    let digests = digests
+        .chunks(32)
+        .map(|c| {
+            let mut a = [0u8; 32];
+            a.copy_from_slice(c);
+            a
+        })
+        .collect();
+    Ok((chunksize, parity, digests))
+}

@@ -1,0 +1,108 @@
+"""Summarize a profiles/collect.sh run (gpurun_out/prof_<tag>/) into profiles/<tag>_summary.md
+and merge per-kernel HBM traffic into profiles/traffic.json (read by bench.py).
+
+    python profiles/summarize.py <tag> [--config c2]
+
+HBM traffic per launch follows MI355X_MICROARCH.md §HBM / cdna_hip_programming.md §7:
+FETCH_SIZE and WRITE_SIZE come from separate --pmc passes, are in KiB, and on gfx950
+FETCH_SIZE reports half the bytes of a wide (16 B/lane) streaming read, so
+    traffic_bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024.
+The x2 is calibrated for coalesced 16 B/lane streams (rs_apply_kernel); for the SHA kernel's
+per-lane 16 B loads (one 1 MiB-apart stream per lane) it is uncalibrated and flagged as such.
+"""
+import collections
+import csv
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def short(name: str) -> str:
+    for k in ("rs_apply_kernel", "sha256_lane_kernel", "sha256_split_kernel", "fill_kernel",
+              "encode_hash_kernel", "copyBuffer"):
+        if k in name:
+            return k
+    return name[:40]
+
+
+def pmc(path):
+    out = collections.defaultdict(lambda: collections.defaultdict(list))
+    dur = collections.defaultdict(list)
+    if not os.path.exists(path):
+        return out, dur
+    for r in csv.DictReader(open(path)):
+        k = short(r["Kernel_Name"])
+        out[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        dur[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+    return out, dur
+
+
+def mean(v):
+    return sum(v) / len(v) if v else float("nan")
+
+
+def main():
+    tag = sys.argv[1]
+    config = sys.argv[sys.argv.index("--config") + 1] if "--config" in sys.argv else "c2"
+    src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+    stats = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
+    sq, _ = pmc(os.path.join(src, "pmc_sq", "run_counter_collection.csv"))
+    fetch, _ = pmc(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"))
+    write, _ = pmc(os.path.join(src, "pmc_write", "run_counter_collection.csv"))
+    lines = [f"# rocprofv3 summary `{tag}` ({config})", "",
+             "Source: `profiles/collect.sh` on one MI355X (gfx950); raw CSVs under "
+             f"`profiles/{tag}/`.", "",
+             "## Kernel trace (`--kernel-trace --stats`)", "",
+             "| kernel | calls | avg ms | min ms | max ms |", "|---|---|---|---|---|"]
+    for r in stats:
+        lines.append(f"| {short(r['Name'])} | {r['Calls']} | {float(r['AverageNs'])/1e6:.3f} | "
+                     f"{float(r['MinNs'])/1e6:.3f} | {float(r['MaxNs'])/1e6:.3f} |")
+    lines += ["", "## Counters (separate `--pmc` passes; per-launch means)", "",
+              "| kernel | clock GHz (GRBM_GUI_ACTIVE/8/dur) | SQ_WAVES | VALU insts/wave | "
+              "FETCH_SIZE KiB | WRITE_SIZE KiB | HBM traffic GB (2xFETCH+WRITE) |",
+              "|---|---|---|---|---|---|---|"]
+    traffic = {}
+    tpath = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(tpath):
+        traffic = json.load(open(tpath))
+    for k in sq:
+        if k in ("copyBuffer",):
+            continue
+        c = sq[k]
+        _, durs = pmc(os.path.join(src, "pmc_sq", "run_counter_collection.csv"))
+        d_ms = mean(durs[k])
+        ghz = mean(c["GRBM_GUI_ACTIVE"]) / 8 / (d_ms / 1e3) / 1e9 if d_ms else float("nan")
+        waves = mean(c["SQ_WAVES"])
+        vpw = mean(c["SQ_INSTS_VALU"]) / waves if waves else float("nan")
+        f = mean(fetch[k].get("FETCH_SIZE", []))
+        w = mean(write[k].get("WRITE_SIZE", []))
+        tb = (2 * f + w) * 1024 if f == f and w == w else None
+        lines.append(f"| {k} | {ghz:.2f} | {waves:.0f} | {vpw:.0f} | {f:.0f} | {w:.0f} | "
+                     f"{tb/1e9 if tb else float('nan'):.2f} |")
+        if tb and k in ("rs_apply_kernel", "sha256_lane_kernel", "encode_hash_kernel"):
+            traffic.setdefault(config, {})[k] = {
+                "bytes_per_launch": int(tb),
+                "fetch_kib": f, "write_kib": w,
+                "calibrated": k == "rs_apply_kernel",
+                "source": f"profiles/{tag}_summary.md",
+            }
+    with open(os.path.join(ROOT, "profiles", f"{tag}_summary.md"), "w") as fh:
+        fh.write("\n".join(lines) + "\n")
+    with open(tpath, "w") as fh:
+        json.dump(traffic, fh, indent=1)
+    # keep the raw CSVs that the summary is built from
+    dst = os.path.join(ROOT, "profiles", tag)
+    os.makedirs(dst, exist_ok=True)
+    for sub in ("trace", "pmc_sq", "pmc_fetch", "pmc_write"):
+        for fn in ("run_kernel_stats.csv", "run_counter_collection.csv"):
+            p = os.path.join(src, sub, fn)
+            if os.path.exists(p):
+                with open(p) as fi, open(os.path.join(dst, f"{sub}_{fn}"), "w") as fo:
+                    fo.write(fi.read())
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main()
