@@ -31,6 +31,7 @@ import torch  # noqa: E402  (import before chunky_ec: one HIP runtime)
 import torch.distributed as dist  # noqa: E402
 
 import chunky_ec as ce  # noqa: E402
+from chunky_ec.sharding import barrier, dist_env, max_over_ranks, rank_seed  # noqa: E402
 
 METRIC = "RS(10,4) encode+sha256 GB/s per node at 1/2/4/8 GPUs; % of HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md); 6.3 TB/s measured copy
@@ -53,26 +54,6 @@ CONFIGS = {
     "c2enc": dict(d=10, p=4, chunk=1 * MiB, parts=4096, op="encode",
                   workload="RS(10,4) encode_sep only, 4096 parts x 1 MiB chunks per GPU"),
 }
-
-
-def dist_env():
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    return world, rank, local
-
-
-def max_over_ranks(x: float, world: int, device) -> float:
-    if world == 1:
-        return x
-    t = torch.tensor([x], dtype=torch.float64, device=device)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
-
-
-def barrier(world: int):
-    if world > 1:
-        dist.barrier()
 
 
 KERNEL_SYMBOL = {"sha256_kernel": "sha256_lane_kernel", "rs_apply_kernel": "rs_apply_kernel",
@@ -146,7 +127,7 @@ def main():
     digests = torch.empty((n_parts, t, 32), dtype=torch.uint8, device=device)
     batch = ce.PartBatch.from_tensor(buf, L)
     stream = torch.cuda.current_stream(device)
-    seed = 0x5EED0000 + rank
+    seed = rank_seed(0x5EED0000, rank)
     ce.fill_synthetic(batch, t, seed, stream)  # data chunks + (overwritten) parity slots
 
     present = None

@@ -1,0 +1,39 @@
+"""Part-wise sharding across GPUs: one process per GPU, contiguous part
+ranges, no data exchange.  Only the timing/barrier helpers touch torch.distributed."""
+from __future__ import annotations
+
+import os
+from typing import Tuple
+
+
+def dist_env() -> Tuple[int, int, int]:
+    """(world_size, rank, local_rank) from the torch.distributed.run environment."""
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def part_range(n_parts: int, rank: int, world: int) -> Tuple[int, int]:
+    """[start, stop) of the contiguous part range owned by `rank` ([g·N/G, (g+1)·N/G))."""
+    return n_parts * rank // world, n_parts * (rank + 1) // world
+
+
+def max_over_ranks(x: float, world: int, device=None) -> float:
+    """Max of a per-rank float over all ranks (the step time the bench reports)."""
+    if world == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def barrier(world: int) -> None:
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def rank_seed(base: int, rank: int) -> int:
+    """Synthetic-data seed of a rank's parts (weak scaling: every rank owns distinct parts)."""
+    return base + rank

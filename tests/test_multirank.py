@@ -1,0 +1,83 @@
+"""N > 1 path on CPU: two gloo ranks shard parts with chunky_ec.sharding exactly as bench.py
+does, compute their parts independently (oracle, since there is no GPU here), and the union of
+the per-rank results equals the single-process result; the max-over-ranks step time and the
+barrier behave as the bench needs."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from chunky_ec.sharding import part_range
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _part_digests(part, d, p, L):
+    import hashlib
+    import oracle
+    from _gen import gen_bytes
+    data = gen_bytes(10_000 + part, d * L).reshape(d, L)
+    st, par = oracle.encode_sep(d, p, list(data))
+    assert st == 0
+    chunks = [x.tobytes() for x in data] + [x.tobytes() for x in par]
+    return [hashlib.sha256(c).hexdigest() for c in chunks]
+
+
+def _worker(rank, world, port, n_parts, out_q):
+    import torch
+    import torch.distributed as dist
+    from chunky_ec.sharding import barrier, max_over_ranks
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lo, hi = part_range(n_parts, rank, world)
+        res = {k: _part_digests(k, 3, 2, 257) for k in range(lo, hi)}
+        barrier(world)
+        t = max_over_ranks(float(rank + 1) * 0.5, world, torch.device("cpu"))
+        gathered = [None] * world
+        dist.all_gather_object(gathered, res)
+        out_q.put((rank, t, gathered))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_part_range_partitions_exactly():
+    for n in (0, 1, 7, 4096, 4097):
+        for world in (1, 2, 3, 8):
+            seen = []
+            for r in range(world):
+                lo, hi = part_range(n, r, world)
+                assert lo <= hi
+                seen.extend(range(lo, hi))
+            assert seen == list(range(n))
+
+
+def test_two_rank_gloo_sharding_matches_single_process():
+    world, n_parts = 2, 9
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_parts, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    results = [q.get(timeout=120) for _ in range(world)]
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    single = {k: _part_digests(k, 3, 2, 257) for k in range(n_parts)}
+    for rank, t, gathered in results:
+        assert t == pytest.approx(1.0)  # max over ranks of (rank+1)*0.5
+        merged = {}
+        for part_map in gathered:
+            assert not (set(merged) & set(part_map))  # disjoint ownership
+            merged.update(part_map)
+        assert merged == single
