@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <array>
 #include <cstring>
 #include <deque>
@@ -592,11 +593,35 @@ int cec_sha256_batch(const cec_part_batch* b, size_t first_chunk, size_t n_chunk
     return CEC_OK;
 }
 
-int cec_encode_hash_batch(const cec_codec* c, const cec_part_batch* b, uint8_t* digests,
+int cec_encode_hash_batch(const cec_codec* cc, const cec_part_batch* b, uint8_t* digests,
                           void* stream) {
-    CEC_TRY(cec_encode_batch(c, b, stream));
-    if (!c || !digests) return CEC_ERR_INVALID_ARGUMENT;
-    return cec_sha256_batch(b, 0, c->d + c->p, digests, stream);
+    if (!cc || !digests) return CEC_ERR_INVALID_ARGUMENT;
+    CEC_TRY(batch_ok(b));
+    if (b->n_parts == 0) return CEC_OK;
+    if (b->chunk_len == 0) return CEC_EMPTY_SHARD;
+    if (b->n_parts * (cc->d + cc->p) > 0xFFFFFFFFull) return CEC_ERR_INVALID_ARGUMENT;
+    cec_codec* c = const_cast<cec_codec*>(cc);
+    const char* env = std::getenv("CEC_FUSED");  // tuning knob: 0 = separate kernels
+    const bool fused = fused_supported(uint32_t(c->d), uint32_t(c->p)) && !(env && env[0] == '0');
+    if (!fused) {
+        CEC_TRY(cec_encode_batch(c, b, stream));
+        return cec_sha256_batch(b, 0, c->d + c->p, digests, stream);
+    }
+    uint32_t* drec = nullptr;
+    CEC_TRY(c->encode_record(&drec));
+    FusedParams f{};
+    f.base = b->base;
+    f.part_stride = b->part_stride;
+    f.chunk_stride = b->chunk_stride;
+    f.len = b->chunk_len;
+    f.pat = drec;
+    f.digests = digests;
+    f.n_parts = uint32_t(b->n_parts);
+    f.d = uint32_t(c->d);
+    f.p = uint32_t(c->p);
+    HIP_TRY(launch_encode_hash(f, aligned16(b->base, b->part_stride, b->chunk_stride),
+                               static_cast<hipStream_t>(stream)));
+    return CEC_OK;
 }
 
 int cec_reconstruct_batch(const cec_codec* cc, const cec_part_batch* b, const uint8_t* present,

@@ -50,7 +50,24 @@ struct FillParams {
     uint32_t n_chunks;
 };
 
+// Fused encode_sep + SHA-256 of all d+p chunks (fused_kernels.hip).  Encode tables come from
+// the codec's encode pattern record `pat`; digests as in ShaParams ((k*(d+p) + i) * 32).
+struct FusedParams {
+    uint8_t* base;
+    uint64_t part_stride;
+    uint64_t chunk_stride;
+    uint64_t len;
+    const uint32_t* pat;
+    uint8_t* digests;
+    uint32_t n_parts;
+    uint32_t d;
+    uint32_t p;
+    uint32_t parts_per_wg;  // set by launch_encode_hash
+};
+
 hipError_t launch_rs_apply(const ApplyParams& a, bool vec16, hipStream_t s);
+bool fused_supported(uint32_t d, uint32_t p);
+hipError_t launch_encode_hash(const FusedParams& a, bool vec16, hipStream_t s);
 hipError_t launch_sha256(const ShaParams& a, bool vec16, hipStream_t s);
 hipError_t launch_fill(const FillParams& a, hipStream_t s);
 

@@ -14,28 +14,17 @@
 // 3 v_perm + ~1.5 xor per data dword, with no LDS traffic and no bank conflicts.
 #include "device_common.hpp"
 #include "gf256.hpp"
+#include "gf_device.hpp"
 #include "kernels.hpp"
 
 namespace cec {
 namespace {
 
+using namespace gf;
+
 constexpr int kApplyThreads = 256;
 constexpr int kApplyIters = 4;  // 16-byte columns per thread per block
 constexpr uint64_t kApplyTile = uint64_t(kApplyThreads) * 16u * kApplyIters;  // 16 KiB
-
-struct Sel {
-    uint32_t s0, s1, s2;
-};
-
-__device__ __forceinline__ Sel selectors(uint32_t x) {
-    return {x & 0x07070707u, (x >> 3) & 0x07070707u, (x >> 6) & 0x03030303u};
-}
-
-// c (x) x for 4 packed bytes, c given by its 5 packed table words.
-__device__ __forceinline__ uint32_t gmul(const Sel& s, uint32_t t0, uint32_t t1, uint32_t t2,
-                                         uint32_t t3, uint32_t t4) {
-    return xor3(perm(t1, t0, s.s0), perm(t3, t2, s.s1), perm(0u, t4, s.s2));
-}
 
 // One 16-byte column (x .. x+16) of a part: acc[r] = XOR_j coef[r][j] (x) in_j[x..x+16).
 // FULL: every lane of the block has 16 valid bytes and the layout is 16-byte aligned.

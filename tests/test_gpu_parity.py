@@ -391,3 +391,42 @@ def test_full_size_encode_erase_reconstruct_roundtrip(d, p, L, n_parts):
     ce.sha256_batch(batch, 0, t, dig2.data_ptr())
     torch.cuda.synchronize()
     assert torch.equal(dig, dig2)
+
+
+# ----------------------------------------------------------------------------------------------
+# Fused encode+hash kernel vs the separate kernels and the oracle
+# ----------------------------------------------------------------------------------------------
+
+@pytest.mark.parametrize("d,p,L,cstride,n_parts", [
+    (10, 4, 4096 + 13, 4112, 40),     # ragged tail, 18 parts per workgroup, 3 workgroups
+    (10, 4, 64, None, 19),            # exactly one SHA block, last workgroup with 1 part
+    (10, 4, 63, 64, 5),               # shorter than a block (tail only)
+    (3, 2, 100, 112, 13100),          # > 256 workgroups: 128-byte steps, 2 per CU
+    (20, 8, 200, 208, 2400),          # > 256 workgroups for t = 28
+    (3, 2, 683, 683, 30),             # odd stride: unaligned path
+    (1, 1, 1000, 1008, 17),
+    (200, 8, 300, 304, 3),            # one part per workgroup (t = 208)
+    (6, 10, 500, 512, 4),             # p > 8: falls back to the separate kernels
+])
+def test_fused_encode_hash_matches_separate_and_oracle(d, p, L, cstride, n_parts, monkeypatch):
+    t = d + p
+    buf, batch = _device_parts(n_parts, t, L, cstride, seed=L * 3 + d)
+    ref = buf.clone()
+    rs = ce.ReedSolomon(d, p)
+    dig = torch.zeros((n_parts, t, 32), dtype=torch.uint8, device=DEV)
+    ce.encode_hash_batch(rs, batch, dig.data_ptr())  # fused (p <= 8)
+    fused_buf = buf.clone()
+    buf.copy_(ref)
+    dig2 = torch.zeros_like(dig)
+    monkeypatch.setenv("CEC_FUSED", "0")
+    ce.encode_hash_batch(rs, batch, dig2.data_ptr())  # encode kernel + sha256 kernel
+    torch.cuda.synchronize()
+    assert torch.equal(fused_buf, buf)
+    assert torch.equal(dig, dig2)
+    host, hd = buf.cpu().numpy(), dig.cpu().numpy()
+    for k in sorted({0, n_parts // 2, n_parts - 1}):
+        st, par = oracle.encode_sep(d, p, [host[k, j, :L] for j in range(d)])
+        for i in range(p):
+            assert np.array_equal(host[k, d + i, :L], par[i])
+        for j in range(t):
+            assert hd[k, j].tobytes() == hashlib.sha256(host[k, j, :L].tobytes()).digest()
