@@ -85,6 +85,16 @@ _sig("cec_sha256_batch", [ctypes.POINTER(PartBatchStruct), ctypes.c_size_t, ctyp
 _sig("cec_reconstruct_batch", [_vp, ctypes.POINTER(PartBatchStruct), _u8p, ctypes.c_int, _vp])
 _sig("cec_fill_synthetic", [ctypes.POINTER(PartBatchStruct), ctypes.c_size_t, ctypes.c_uint64,
                             _vp])
+_sig("cec_pipeline_new", [_vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t,
+                          ctypes.POINTER(_vp)])
+_sig("cec_pipeline_free", [_vp], None)
+_sig("cec_pipeline_depth", [_vp], ctypes.c_size_t)
+_sig("cec_pipeline_acquire", [_vp, _szp, ctypes.POINTER(_u8p)])
+_sig("cec_pipeline_submit", [_vp, ctypes.c_size_t, ctypes.c_size_t])
+_sig("cec_pipeline_wait", [_vp, ctypes.c_size_t, ctypes.POINTER(_u8p), ctypes.POINTER(_u8p),
+                           _szp])
+_sig("cec_pipeline_drain", [_vp])
+_sig("cec_pipeline_last_error", [], ctypes.c_char_p)
 _sig("cec_synth_byte", [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64],
      ctypes.c_uint8)
 
@@ -401,3 +411,64 @@ def fill_synthetic(batch: PartBatch, n_chunks: int, seed: int, stream=None) -> N
 
 def synth_byte(seed: int, part: int, chunk: int, offset: int) -> int:
     return _lib.cec_synth_byte(seed, part, chunk, offset)
+
+
+# ---------------------------------------------------------------------------------------------
+# Host-staged write pipeline (FileWriteBuilder::write's part loop, batched)
+# ---------------------------------------------------------------------------------------------
+
+
+class Pipeline:
+    """cec_pipeline: pinned host slots -> H2D -> fused encode+hash -> D2H, `depth` in flight.
+
+    Usage per batch: ``slot, data = pl.acquire()`` (a writable numpy view of the pinned
+    [parts][d][L] buffer), fill it, ``pl.submit(slot, n_parts)``, later
+    ``parity, digests = pl.wait(slot)`` (numpy views valid until the slot is re-acquired).
+    """
+
+    def __init__(self, codec: ReedSolomon, chunk_len: int, parts_per_batch: int, depth: int = 4):
+        import numpy as np  # noqa: F401
+        h = _vp()
+        code = _lib.cec_pipeline_new(codec.handle, chunk_len, parts_per_batch, depth,
+                                     ctypes.byref(h))
+        if code != OK:
+            raise Error(code)
+        self._h = h
+        self.codec = codec  # keep the codec alive
+        self.d, self.p = codec.data_shard_count(), codec.parity_shard_count()
+        self.L = chunk_len
+        self.parts = parts_per_batch
+
+    def __del__(self, _free=_lib.cec_pipeline_free):
+        h = getattr(self, "_h", None)
+        if h:
+            _free(h)
+            self._h = None
+
+    def acquire(self):
+        import numpy as np
+        slot = ctypes.c_size_t(0)
+        ptr = _u8p()
+        _check(_lib.cec_pipeline_acquire(self._h, ctypes.byref(slot), ctypes.byref(ptr)))
+        n = self.parts * self.d * self.L
+        arr = np.ctypeslib.as_array(ptr, shape=(n,)).reshape(self.parts, self.d, self.L)
+        return slot.value, arr
+
+    def submit(self, slot: int, n_parts: int) -> None:
+        _check(_lib.cec_pipeline_submit(self._h, slot, n_parts))
+
+    def wait(self, slot: int):
+        import numpy as np
+        par, dig = _u8p(), _u8p()
+        n = ctypes.c_size_t(0)
+        _check(_lib.cec_pipeline_wait(self._h, slot, ctypes.byref(par), ctypes.byref(dig),
+                                      ctypes.byref(n)))
+        k = n.value
+        parity = np.ctypeslib.as_array(par, shape=(max(k * self.p * self.L, 1),))[
+            : k * self.p * self.L].reshape(k, self.p, self.L)
+        digests = np.ctypeslib.as_array(dig, shape=(max(k * (self.d + self.p) * 32, 1),))[
+            : k * (self.d + self.p) * 32].reshape(k, self.d + self.p, 32)
+        return parity, digests
+
+    def drain(self) -> None:
+        _check(_lib.cec_pipeline_drain(self._h))

@@ -1,0 +1,203 @@
+// pipeline.cpp — host-staged write pipeline (cec_pipeline_*): the batched form of
+// FileWriteBuilder::write's part loop (reference src/file/writer.rs:166-231: read d*chunk_size
+// bytes per part, encode + hash each part, hand back parity and digests in order).
+//
+// A pipeline owns `depth` slots on one GPU.  Each slot has pinned host buffers (the caller
+// writes part data straight into them: no extra host copy), a device batch, and its own HIP
+// stream: H2D (one 2-D copy scattering [part][d][L] into the device's [part][d+p][L]), the fused
+// encode_hash kernel, and D2H of parity + digests are queued on the slot's stream, so the copies
+// of one slot overlap the kernels of the others.  A batch's kernel time is the per-chunk serial
+// SHA-256 time whatever its part count (sha256_kernels.hip), so several modest batches in
+// flight on separate streams (their workgroups run on disjoint CUs) keep the PCIe link busy.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "chunky_ec.h"
+
+namespace {
+
+thread_local std::string g_pipe_error;
+
+int pipe_fail(hipError_t e, const char* what) {
+    g_pipe_error = std::string(what) + ": " + hipGetErrorString(e);
+    return e == hipErrorOutOfMemory ? CEC_ERR_OUT_OF_MEMORY : CEC_ERR_HIP;
+}
+
+#define PIPE_TRY(expr)                                      \
+    do {                                                    \
+        hipError_t _e = (expr);                             \
+        if (_e != hipSuccess) return pipe_fail(_e, #expr);  \
+    } while (0)
+
+struct Slot {
+    uint8_t* h_data = nullptr;    // pinned [parts][d][L]
+    uint8_t* h_parity = nullptr;  // pinned [parts][p][L]
+    uint8_t* h_dig = nullptr;     // pinned [parts][d+p][32]
+    uint8_t* d_buf = nullptr;     // device [parts][d+p][cs]
+    uint8_t* d_dig = nullptr;     // device [parts][d+p][32]
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    bool in_flight = false;
+    size_t n_parts = 0;
+};
+
+}  // namespace
+
+struct cec_pipeline {
+    const cec_codec* codec = nullptr;
+    int device = 0;
+    size_t d = 0, p = 0, t = 0, L = 0, cs = 0, parts = 0;
+    std::vector<Slot> slots;
+    size_t next = 0;
+
+    ~cec_pipeline() {
+        int cur = 0;
+        if (hipGetDevice(&cur) != hipSuccess) return;
+        (void)hipSetDevice(device);
+        for (Slot& s : slots) {
+            if (s.stream) (void)hipStreamSynchronize(s.stream);
+            if (s.done) (void)hipEventDestroy(s.done);
+            if (s.stream) (void)hipStreamDestroy(s.stream);
+            if (s.d_buf) (void)hipFree(s.d_buf);
+            if (s.d_dig) (void)hipFree(s.d_dig);
+            if (s.h_data) (void)hipHostFree(s.h_data);
+            if (s.h_parity) (void)hipHostFree(s.h_parity);
+            if (s.h_dig) (void)hipHostFree(s.h_dig);
+        }
+        (void)hipSetDevice(cur);
+    }
+};
+
+extern "C" {
+
+const char* cec_pipeline_last_error(void) { return g_pipe_error.c_str(); }
+
+int cec_pipeline_new(const cec_codec* codec, size_t chunk_len, size_t parts_per_batch,
+                     size_t depth, cec_pipeline** out) {
+    if (!codec || !out || chunk_len == 0 || parts_per_batch == 0 || depth == 0 || depth > 16)
+        return CEC_ERR_INVALID_ARGUMENT;
+    *out = nullptr;
+    if (cec_device_count() <= 0) return CEC_ERR_NO_DEVICE;
+    auto* pl = new cec_pipeline();
+    pl->codec = codec;
+    PIPE_TRY(hipGetDevice(&pl->device));
+    pl->d = cec_codec_data_shards(codec);
+    pl->p = cec_codec_parity_shards(codec);
+    pl->t = pl->d + pl->p;
+    pl->L = chunk_len;
+    pl->cs = (chunk_len + 255) / 256 * 256;
+    pl->parts = parts_per_batch;
+    pl->slots.resize(depth);
+    for (Slot& s : pl->slots) {
+        hipError_t e = hipSuccess;
+        if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&s.h_data), pl->parts * pl->d * pl->L, hipHostMallocDefault);
+        if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&s.h_parity), pl->parts * pl->p * pl->L, hipHostMallocDefault);
+        if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&s.h_dig), pl->parts * pl->t * 32, hipHostMallocDefault);
+        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_buf), pl->parts * pl->t * pl->cs);
+        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_dig), pl->parts * pl->t * 32);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
+        if (e != hipSuccess) {
+            delete pl;
+            return pipe_fail(e, "cec_pipeline_new allocation");
+        }
+    }
+    *out = pl;
+    return CEC_OK;
+}
+
+void cec_pipeline_free(cec_pipeline* pl) { delete pl; }
+
+size_t cec_pipeline_depth(const cec_pipeline* pl) { return pl ? pl->slots.size() : 0; }
+
+// Next slot in round-robin order; waits for that slot's previous batch to finish, after which
+// its previous results are no longer valid.  *data receives the pinned [parts][d][L] buffer.
+int cec_pipeline_acquire(cec_pipeline* pl, size_t* slot, uint8_t** data) {
+    if (!pl || !slot || !data) return CEC_ERR_INVALID_ARGUMENT;
+    const size_t i = pl->next;
+    pl->next = (pl->next + 1) % pl->slots.size();
+    Slot& s = pl->slots[i];
+    if (s.in_flight) {
+        PIPE_TRY(hipEventSynchronize(s.done));
+        s.in_flight = false;
+    }
+    *slot = i;
+    *data = s.h_data;
+    return CEC_OK;
+}
+
+// Queue one batch of n_parts (<= parts_per_batch) parts whose data the caller wrote into the
+// slot's pinned buffer: H2D, fused encode + SHA-256 of all d+p chunks, D2H parity + digests.
+int cec_pipeline_submit(cec_pipeline* pl, size_t slot, size_t n_parts) {
+    if (!pl || slot >= pl->slots.size() || n_parts == 0 || n_parts > pl->parts)
+        return CEC_ERR_INVALID_ARGUMENT;
+    Slot& s = pl->slots[slot];
+    int cur = 0;
+    PIPE_TRY(hipGetDevice(&cur));
+    if (cur != pl->device) PIPE_TRY(hipSetDevice(pl->device));
+    const size_t dw = pl->d * pl->L, pitch = pl->t * pl->cs;
+    if (pl->cs == pl->L) {
+        PIPE_TRY(hipMemcpy2DAsync(s.d_buf, pitch, s.h_data, dw, dw, n_parts,
+                                  hipMemcpyHostToDevice, s.stream));
+    } else {  // chunk stride padded past L: one 2-D copy per data chunk column
+        for (size_t j = 0; j < pl->d; ++j)
+            PIPE_TRY(hipMemcpy2DAsync(s.d_buf + j * pl->cs, pitch, s.h_data + j * pl->L, dw, pl->L,
+                                      n_parts, hipMemcpyHostToDevice, s.stream));
+    }
+    cec_part_batch b{s.d_buf, pitch, pl->cs, n_parts, pl->L};
+    int st = cec_encode_hash_batch(pl->codec, &b, s.d_dig, s.stream);
+    if (st != CEC_OK) {
+        g_pipe_error = cec_last_error();
+        return st;
+    }
+    const size_t pw = pl->p * pl->L;
+    if (pl->cs == pl->L) {
+        PIPE_TRY(hipMemcpy2DAsync(s.h_parity, pw, s.d_buf + dw, pitch, pw, n_parts,
+                                  hipMemcpyDeviceToHost, s.stream));
+    } else {
+        for (size_t i = 0; i < pl->p; ++i)
+            PIPE_TRY(hipMemcpy2DAsync(s.h_parity + i * pl->L, pw,
+                                      s.d_buf + (pl->d + i) * pl->cs, pitch, pl->L, n_parts,
+                                      hipMemcpyDeviceToHost, s.stream));
+    }
+    PIPE_TRY(hipMemcpyAsync(s.h_dig, s.d_dig, n_parts * pl->t * 32, hipMemcpyDeviceToHost,
+                            s.stream));
+    PIPE_TRY(hipEventRecord(s.done, s.stream));
+    s.in_flight = true;
+    s.n_parts = n_parts;
+    if (cur != pl->device) PIPE_TRY(hipSetDevice(cur));
+    return CEC_OK;
+}
+
+// Wait for a submitted slot; *parity = pinned [parts][p][L], *digests = pinned [parts][d+p][32]
+// (chunks in order).  Valid until the slot is acquired again.
+int cec_pipeline_wait(cec_pipeline* pl, size_t slot, const uint8_t** parity,
+                      const uint8_t** digests, size_t* n_parts) {
+    if (!pl || slot >= pl->slots.size()) return CEC_ERR_INVALID_ARGUMENT;
+    Slot& s = pl->slots[slot];
+    if (s.in_flight) {
+        PIPE_TRY(hipEventSynchronize(s.done));
+        s.in_flight = false;
+    }
+    if (parity) *parity = s.h_parity;
+    if (digests) *digests = s.h_dig;
+    if (n_parts) *n_parts = s.n_parts;
+    return CEC_OK;
+}
+
+// Wait for every slot.
+int cec_pipeline_drain(cec_pipeline* pl) {
+    if (!pl) return CEC_ERR_INVALID_ARGUMENT;
+    for (Slot& s : pl->slots) {
+        if (s.in_flight) {
+            PIPE_TRY(hipEventSynchronize(s.done));
+            s.in_flight = false;
+        }
+    }
+    return CEC_OK;
+}
+
+}  // extern "C"

@@ -174,6 +174,28 @@ int cec_reconstruct_batch(const cec_codec* codec, const cec_part_batch* batch,
                           const uint8_t* present, int data_only, void* stream);
 
 /* ---------------------------------------------------------------------------------------- */
+/* Host-staged write pipeline (FileWriteBuilder::write's part loop, writer.rs:166-231)      */
+/* ---------------------------------------------------------------------------------------- */
+
+/* `depth` slots on the current device, each with pinned host buffers for parts_per_batch parts
+ * of d chunks of chunk_len bytes, a device batch and its own HIP stream.  One thread drives a
+ * pipeline.  Per slot: acquire (waits for the slot's previous batch; *data = pinned
+ * [parts][d][chunk_len] buffer the caller fills, i.e. each part's zero-padded d*L data_buf),
+ * submit (H2D, encode + SHA-256 of all d+p chunks, D2H parity + digests, asynchronously),
+ * wait (*parity = pinned [parts][p][L], *digests = pinned [parts][d+p][32]). */
+typedef struct cec_pipeline cec_pipeline;
+int cec_pipeline_new(const cec_codec* codec, size_t chunk_len, size_t parts_per_batch,
+                     size_t depth, cec_pipeline** out);
+void cec_pipeline_free(cec_pipeline* pipeline);
+size_t cec_pipeline_depth(const cec_pipeline* pipeline);
+int cec_pipeline_acquire(cec_pipeline* pipeline, size_t* slot, uint8_t** data);
+int cec_pipeline_submit(cec_pipeline* pipeline, size_t slot, size_t n_parts);
+int cec_pipeline_wait(cec_pipeline* pipeline, size_t slot, const uint8_t** parity,
+                      const uint8_t** digests, size_t* n_parts);
+int cec_pipeline_drain(cec_pipeline* pipeline);
+const char* cec_pipeline_last_error(void);
+
+/* ---------------------------------------------------------------------------------------- */
 /* Utilities for benchmarks and tests                                                        */
 /* ---------------------------------------------------------------------------------------- */
 

@@ -430,3 +430,40 @@ def test_fused_encode_hash_matches_separate_and_oracle(d, p, L, cstride, n_parts
             assert np.array_equal(host[k, d + i, :L], par[i])
         for j in range(t):
             assert hd[k, j].tobytes() == hashlib.sha256(host[k, j, :L].tobytes()).digest()
+
+
+# ----------------------------------------------------------------------------------------------
+# Host-staged write pipeline
+# ----------------------------------------------------------------------------------------------
+
+@pytest.mark.parametrize("d,p,L,parts,depth,batches", [
+    (10, 4, 4096, 16, 3, 7),      # more batches than slots: slot reuse
+    (3, 2, 683, 5, 2, 3),         # odd chunk length (padded device stride)
+    (20, 8, 1000, 4, 4, 4),
+])
+def test_pipeline_matches_oracle(d, p, L, parts, depth, batches):
+    rs = ce.ReedSolomon(d, p)
+    pl = ce.Pipeline(rs, L, parts, depth)
+    sent, done, pending = {}, {}, {}
+    for b in range(batches):
+        slot, data = pl.acquire()  # waits for this slot's previous batch: collect it first
+        if slot in pending:
+            done[pending[slot]] = tuple(x.copy() for x in pl.wait(slot))
+        n = parts if b % 2 == 0 else max(1, parts - 1)
+        data[:n] = gen_bytes(700 + b, n * d * L).reshape(n, d, L)
+        sent[b] = (slot, data[:n].copy())
+        pl.submit(slot, n)  # up to `depth` batches in flight
+        pending[slot] = b
+    for slot, b in pending.items():
+        if b not in done:
+            done[b] = tuple(x.copy() for x in pl.wait(slot))
+    pl.drain()
+    for b, (slot, data) in sent.items():
+        parity, digests = done[b]
+        for k in range(data.shape[0]):
+            st, par = oracle.encode_sep(d, p, [data[k, j] for j in range(d)])
+            for i in range(p):
+                assert np.array_equal(parity[k, i], par[i]), (b, k, i)
+            chunks = [data[k, j] for j in range(d)] + par
+            for j in range(d + p):
+                assert digests[k, j].tobytes() == hashlib.sha256(chunks[j].tobytes()).digest()
