@@ -85,6 +85,12 @@ _sig("cec_sha256_batch", [ctypes.POINTER(PartBatchStruct), ctypes.c_size_t, ctyp
 _sig("cec_reconstruct_batch", [_vp, ctypes.POINTER(PartBatchStruct), _u8p, ctypes.c_int, _vp])
 _sig("cec_fill_synthetic", [ctypes.POINTER(PartBatchStruct), ctypes.c_size_t, ctypes.c_uint64,
                             _vp])
+_sig("cec_verify_batch", [ctypes.POINTER(PartBatchStruct), ctypes.c_size_t, ctypes.c_size_t,
+                          _vp, _vp, _vp, _vp])
+_sig("cec_read_batch", [_vp, ctypes.POINTER(PartBatchStruct), _u8p, _vp, _u8p,
+                        ctypes.POINTER(ctypes.c_int), _vp])
+_sig("cec_resilver_batch", [_vp, ctypes.POINTER(PartBatchStruct), _u8p, _vp, _u8p,
+                            ctypes.POINTER(ctypes.c_int), _vp])
 _sig("cec_pipeline_new", [_vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t,
                           ctypes.POINTER(_vp)])
 _sig("cec_pipeline_free", [_vp], None)
@@ -402,6 +408,39 @@ def reconstruct_batch(codec: ReedSolomon, batch: PartBatch, present, data_only: 
     _check(_lib.cec_reconstruct_batch(codec.handle, ctypes.byref(s),
                                       ctypes.cast(ctypes.c_char_p(pres), _u8p),
                                       1 if data_only else 0, _stream_ptr(stream)))
+
+
+def verify_batch(batch: PartBatch, first_chunk: int, n_chunks: int, expected_ptr: int,
+                 ok_ptr: int, present_ptr: int = 0, stream=None) -> None:
+    """DataVerifier::verify over a batch (device pointers; present_ptr 0 = all present)."""
+    s = batch.struct()
+    _check(_lib.cec_verify_batch(ctypes.byref(s), first_chunk, n_chunks, present_ptr or None,
+                                 expected_ptr, ok_ptr, _stream_ptr(stream)))
+
+
+def _verify_rebuild(fn, codec, batch, present, expected_ptr, stream):
+    t = codec.total_shard_count()
+    n = batch.n_parts * t
+    pres = bytes(present)
+    assert len(pres) == n
+    verified = (ctypes.c_uint8 * max(n, 1))()
+    status = (ctypes.c_int * max(batch.n_parts, 1))()
+    s = batch.struct()
+    _check(fn(codec.handle, ctypes.byref(s), ctypes.cast(ctypes.c_char_p(pres), _u8p),
+              expected_ptr, verified, status, _stream_ptr(stream)))
+    return bytes(verified)[:n], list(status)[:batch.n_parts]
+
+
+def read_batch(codec: ReedSolomon, batch: PartBatch, present, expected_ptr: int, stream=None):
+    """FilePart::read_with_context compute: verify loaded chunks, reconstruct_data.
+    Returns (verified flags, per-part status)."""
+    return _verify_rebuild(_lib.cec_read_batch, codec, batch, present, expected_ptr, stream)
+
+
+def resilver_batch(codec: ReedSolomon, batch: PartBatch, present, expected_ptr: int,
+                   stream=None):
+    """FilePart::resilver compute: verify all chunks, rebuild missing data and parity."""
+    return _verify_rebuild(_lib.cec_resilver_batch, codec, batch, present, expected_ptr, stream)
 
 
 def fill_synthetic(batch: PartBatch, n_chunks: int, seed: int, stream=None) -> None:

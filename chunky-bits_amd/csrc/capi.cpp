@@ -700,6 +700,81 @@ int cec_reconstruct_batch(const cec_codec* cc, const cec_part_batch* b, const ui
     return status;
 }
 
+int cec_verify_batch(const cec_part_batch* b, size_t first_chunk, size_t n_chunks,
+                     const uint8_t* present, const uint8_t* expected, uint8_t* ok, void* stream) {
+    CEC_TRY(batch_ok(b));
+    if (!expected || !ok) return CEC_ERR_INVALID_ARGUMENT;
+    if (b->n_parts == 0 || n_chunks == 0) return CEC_OK;
+    if (b->n_parts * n_chunks > 0xFFFFFFFFull) return CEC_ERR_INVALID_ARGUMENT;
+    ShaParams h{};
+    h.base = b->base;
+    h.part_stride = b->part_stride;
+    h.chunk_stride = b->chunk_stride;
+    h.len = b->chunk_len;
+    h.n_parts = uint32_t(b->n_parts);
+    h.first_chunk = uint32_t(first_chunk);
+    h.n_chunks = uint32_t(n_chunks);
+    h.present = present;
+    h.expected = expected;
+    h.ok = ok;
+    HIP_TRY(launch_sha256(h, aligned16(b->base, b->part_stride, b->chunk_stride),
+                          static_cast<hipStream_t>(stream)));
+    return CEC_OK;
+}
+
+namespace {
+
+// Shared body of cec_read_batch / cec_resilver_batch: verify the loaded chunks, then rebuild
+// from the first d verified chunks of each part.
+int verify_then_reconstruct(const cec_codec* c, const cec_part_batch* b,
+                            const uint8_t* present_host, const uint8_t* expected,
+                            uint8_t* verified_host, int* part_status, bool data_only,
+                            hipStream_t s) {
+    if (!c || !present_host || !expected || !verified_host || !part_status)
+        return CEC_ERR_INVALID_ARGUMENT;
+    CEC_TRY(batch_ok(b));
+    if (b->n_parts == 0) return CEC_OK;
+    if (b->chunk_len == 0) return CEC_EMPTY_SHARD;
+    const size_t t = c->d + c->p, n = b->n_parts * t;
+    if (n > 0xFFFFFFFFull) return CEC_ERR_INVALID_ARGUMENT;
+    uint8_t* flags = nullptr;  // [present | ok]
+    HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&flags), 2 * n, s));
+    HIP_TRY(hipMemcpyAsync(flags, present_host, n, hipMemcpyHostToDevice, s));
+    int st = cec_verify_batch(b, 0, t, flags, expected, flags + n, s);
+    if (st == CEC_OK) {
+        hipError_t e = hipMemcpyAsync(verified_host, flags + n, n, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) st = hip_fail(e, "verify readback");
+    }
+    (void)hipFreeAsync(flags, s);
+    if (st != CEC_OK) return st;
+    // Parts with fewer than d verified chunks cannot be decoded (the reference's read returns
+    // the part short / resilver reports it); rebuild the others.
+    std::vector<uint8_t> pres(verified_host, verified_host + n);
+    for (size_t k = 0; k < b->n_parts; ++k) {
+        size_t good = 0;
+        for (size_t i = 0; i < t; ++i) good += pres[k * t + i] ? 1 : 0;
+        part_status[k] = good >= c->d ? CEC_OK : CEC_TOO_FEW_SHARDS_PRESENT;
+        if (good < c->d) std::fill(pres.begin() + k * t, pres.begin() + (k + 1) * t, uint8_t(1));
+    }
+    return cec_reconstruct_batch(c, b, pres.data(), data_only ? 1 : 0, s);
+}
+
+}  // namespace
+
+int cec_read_batch(const cec_codec* c, const cec_part_batch* b, const uint8_t* present,
+                   const uint8_t* expected, uint8_t* verified, int* part_status, void* stream) {
+    return verify_then_reconstruct(c, b, present, expected, verified, part_status, true,
+                                   static_cast<hipStream_t>(stream));
+}
+
+int cec_resilver_batch(const cec_codec* c, const cec_part_batch* b, const uint8_t* present,
+                       const uint8_t* expected, uint8_t* verified, int* part_status,
+                       void* stream) {
+    return verify_then_reconstruct(c, b, present, expected, verified, part_status, false,
+                                   static_cast<hipStream_t>(stream));
+}
+
 // ------------------------------------------------------------------------------------------
 // Utilities
 // ------------------------------------------------------------------------------------------

@@ -37,7 +37,12 @@ struct ShaParams {
     uint32_t n_parts;
     uint32_t first_chunk;
     uint32_t n_chunks;
-    uint8_t* digests;
+    uint8_t* digests;     // may be null when only verifying
+    // Verify mode (DataVerifier::verify): items with present[item] == 0 are skipped (ok = 0);
+    // ok[item] = digest == expected[item*32 .. +32].  All three optional (device pointers).
+    const uint8_t* present;
+    const uint8_t* expected;
+    uint8_t* ok;
 };
 
 struct FillParams {

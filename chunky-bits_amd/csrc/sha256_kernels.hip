@@ -46,6 +46,21 @@ __device__ __forceinline__ void item_source(const ShaParams& a, uint32_t item, c
     }
 }
 
+// Digest out and/or compare with the expected digest (verify mode).
+__device__ __forceinline__ void finish_item(const ShaParams& a, uint32_t item,
+                                            const uint32_t st[8]) {
+    if (a.digests) store_digest(a.digests + uint64_t(item) * 32u, st);
+    if (a.expected && a.ok) {
+        const uint4* e = reinterpret_cast<const uint4*>(a.expected + uint64_t(item) * 32u);
+        const uint4 e0 = e[0], e1 = e[1];
+        const bool eq = e0.x == bswap32(st[0]) && e0.y == bswap32(st[1]) &&
+                        e0.z == bswap32(st[2]) && e0.w == bswap32(st[3]) &&
+                        e1.x == bswap32(st[4]) && e1.y == bswap32(st[5]) &&
+                        e1.z == bswap32(st[6]) && e1.w == bswap32(st[7]);
+        a.ok[item] = eq ? 1 : 0;
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // v1: one lane per chunk, everything in one wave
 // ------------------------------------------------------------------------------------------
@@ -62,6 +77,10 @@ __global__ __launch_bounds__(kLaneThreads) void sha256_lane_kernel(ShaParams a) 
     extern __shared__ uint32_t cu_reservation[];  // never touched: occupancy control only
     const uint32_t item = blockIdx.x * uint32_t(kLaneThreads) + threadIdx.x;
     if (item >= a.n_parts * a.n_chunks) return;
+    if (a.present && !a.present[item]) {
+        if (a.ok) a.ok[item] = 0;
+        return;
+    }
     const uint8_t* p;
     uint64_t len;
     item_source(a, item, p, len);
@@ -87,7 +106,7 @@ __global__ __launch_bounds__(kLaneThreads) void sha256_lane_kernel(ShaParams a) 
         tail_words(p + 64 * nfull, rem, blk, tb, len * 8, w);
         compress(st, w);
     }
-    store_digest(a.digests + uint64_t(item) * 32u, st);
+    finish_item(a, item, st);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -177,7 +196,7 @@ __global__ __launch_bounds__(128) void sha256_split_kernel(ShaParams a) {
             }
             __syncthreads();
         }
-        if (valid) store_digest(a.digests + uint64_t(item) * 32u, st);
+        if (valid) finish_item(a, item, st);
     }
 }
 
@@ -226,7 +245,9 @@ hipError_t launch_split(const ShaParams& a, bool vec16, hipStream_t s) {
 hipError_t launch_sha256(const ShaParams& a, bool vec16, hipStream_t s) {
     const uint64_t total = uint64_t(a.n_parts) * a.n_chunks;
     if (total == 0) return hipSuccess;
-    return sha_variant() == 2 ? launch_split(a, vec16, s) : launch_lane(a, vec16, s);
+    // verify mode with absent chunks is lane-kernel only (the split kernel has no skip path)
+    return (sha_variant() == 2 && !a.present) ? launch_split(a, vec16, s)
+                                              : launch_lane(a, vec16, s);
 }
 
 }  // namespace cec

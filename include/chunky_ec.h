@@ -173,6 +173,28 @@ int cec_sha256_batch(const cec_part_batch* batch, size_t first_chunk, size_t n_c
 int cec_reconstruct_batch(const cec_codec* codec, const cec_part_batch* batch,
                           const uint8_t* present, int data_only, void* stream);
 
+/* DataVerifier::verify (src/file/hash/any.rs:27-52, called per chunk at file_part.rs:102,239)
+ * for chunks [first_chunk, first_chunk + n_chunks) of every part:
+ * ok[k*n_chunks + c] = 1 iff SHA-256(chunk) == expected[(k*n_chunks + c)*32 .. +32]; chunks
+ * whose present flag is 0 are not read and get ok = 0.  present (nullable: all present),
+ * expected and ok are DEVICE buffers. */
+int cec_verify_batch(const cec_part_batch* batch, size_t first_chunk, size_t n_chunks,
+                     const uint8_t* present, const uint8_t* expected, uint8_t* ok, void* stream);
+
+/* FilePart::read_with_context compute (file_part.rs:86-129) for every part: verify the loaded
+ * chunks (present: HOST flags, n_parts*(d+p)) against expected (DEVICE digests, part-major,
+ * chunks in order), then reconstruct_data from the first d verified chunks.  Outputs (HOST):
+ * verified[k*(d+p)+i] = verification result; part_status[k] = CEC_OK, or
+ * CEC_TOO_FEW_SHARDS_PRESENT when fewer than d chunks verified (that part is left untouched).
+ * Waits on `stream` once, for the verification flags that decide the decode. */
+int cec_read_batch(const cec_codec* codec, const cec_part_batch* batch, const uint8_t* present,
+                   const uint8_t* expected, uint8_t* verified, int* part_status, void* stream);
+/* FilePart::resilver compute (file_part.rs:266-308): as cec_read_batch over all d+p chunks,
+ * then reconstruct (missing data AND parity) in place. */
+int cec_resilver_batch(const cec_codec* codec, const cec_part_batch* batch,
+                       const uint8_t* present, const uint8_t* expected, uint8_t* verified,
+                       int* part_status, void* stream);
+
 /* ---------------------------------------------------------------------------------------- */
 /* Host-staged write pipeline (FileWriteBuilder::write's part loop, writer.rs:166-231)      */
 /* ---------------------------------------------------------------------------------------- */

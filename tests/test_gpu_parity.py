@@ -467,3 +467,79 @@ def test_pipeline_matches_oracle(d, p, L, parts, depth, batches):
             chunks = [data[k, j] for j in range(d)] + par
             for j in range(d + p):
                 assert digests[k, j].tobytes() == hashlib.sha256(chunks[j].tobytes()).digest()
+
+
+# ----------------------------------------------------------------------------------------------
+# Verify / read / resilver (FilePart::verify, read_with_context, resilver compute)
+# ----------------------------------------------------------------------------------------------
+
+def _encoded_batch(d, p, L, n_parts, seed):
+    t = d + p
+    buf, batch = _device_parts(n_parts, t, L, None, seed=seed)
+    rs = ce.ReedSolomon(d, p)
+    dig = torch.zeros((n_parts, t, 32), dtype=torch.uint8, device=DEV)
+    ce.encode_hash_batch(rs, batch, dig.data_ptr())
+    torch.cuda.synchronize()
+    return rs, buf, batch, dig
+
+
+def test_verify_batch_flags():
+    d, p, L, n = 4, 2, 3000, 10
+    rs, buf, batch, dig = _encoded_batch(d, p, L, n, 31)
+    t = d + p
+    buf[3, 1, 17] ^= 0x01            # corrupt one chunk
+    present = torch.ones((n, t), dtype=torch.uint8, device=DEV)
+    present[5, 4] = 0                # absent chunk: not read, ok = 0
+    ok = torch.full((n, t), 7, dtype=torch.uint8, device=DEV)
+    ce.verify_batch(batch, 0, t, dig.data_ptr(), ok.data_ptr(), present.data_ptr())
+    torch.cuda.synchronize()
+    want = torch.ones((n, t), dtype=torch.uint8)
+    want[3, 1] = 0
+    want[5, 4] = 0
+    assert torch.equal(ok.cpu(), want)
+
+
+def test_read_batch_restores_data_and_reports_undecodable_parts():
+    d, p, L, n = 10, 4, 4096 + 5, 12
+    rs, buf, batch, dig = _encoded_batch(d, p, L, n, 41)
+    t = d + p
+    ref = buf.clone()
+    present = np.ones((n, t), dtype=np.uint8)
+    present[0, [0, 3]] = 0           # two data chunks not fetched
+    buf[1, 2, 100] ^= 0xFF           # a fetched chunk that fails its hash
+    present[2, [0, 1, 2, 3, 4]] = 0  # 9 chunks left < d: undecodable
+    buf[4, 13, 0] ^= 1               # corrupt parity: data intact, nothing to rebuild
+    for k, i in [(0, 0), (0, 3), (2, 0)]:
+        buf[k, i] = 0
+    verified, status = ce.read_batch(rs, batch, present.tobytes(), dig.data_ptr())
+    torch.cuda.synchronize()
+    v = np.frombuffer(verified, np.uint8).reshape(n, t)
+    assert v[1, 2] == 0 and v[0, 0] == 0 and v[4, 13] == 0 and v[3].all()
+    assert status[2] == ce.TOO_FEW_SHARDS_PRESENT
+    assert all(status[k] == ce.OK for k in range(n) if k != 2)
+    got, want = buf.cpu(), ref.cpu()
+    for k in range(n):
+        if k == 2:
+            continue
+        assert torch.equal(got[k, :d], want[k, :d]), k   # data chunks are the read's output
+
+
+def test_resilver_batch_cluster_style():
+    """tests/cluster.rs:145-231: delete data[0] and parity[0] of every part, resilver, verify
+    is ideal again (every chunk matches its digest)."""
+    d, p, L, n = 3, 2, 683, 7
+    rs, buf, batch, dig = _encoded_batch(d, p, L, n, 51)
+    t = d + p
+    ref = buf.clone()
+    buf[:, 0] = 0
+    buf[:, d] = 0
+    present = np.ones((n, t), dtype=np.uint8)
+    present[:, 0] = 0
+    present[:, d] = 0
+    verified, status = ce.resilver_batch(rs, batch, present.tobytes(), dig.data_ptr())
+    assert status == [ce.OK] * n
+    ok = torch.zeros((n, t), dtype=torch.uint8, device=DEV)
+    ce.verify_batch(batch, 0, t, dig.data_ptr(), ok.data_ptr())
+    torch.cuda.synchronize()
+    assert bool(ok.all())
+    assert torch.equal(buf, ref)
