@@ -4,8 +4,8 @@
 // written once and hashed from LDS (never re-read).
 //
 // Workgroup = 512 threads, one per CU:
-//   waves 0-3  SHA lanes: lane = one chunk of one of the workgroup's G = floor(256/(d+p)) parts
-//              (RS(10,4): 18 parts = 252 lanes), so each SIMD carries exactly one SHA wave —
+//   waves 0-3  SHA lanes: lane = one chunk of one of the workgroup's G parts (G*(d+p) <= 256;
+//              RS(10,4): 16 parts = 224 lanes), so each SIMD carries exactly one SHA wave —
 //              the long-lived, issue-bound wave that sets the pace (sha256_kernels.hip).
 //   waves 4-7  encoders: per pipeline step of STEP bytes, load the G*d data columns (16 B per
 //              lane) from HBM into an LDS slot, compute the G*p parity columns with the v_perm
@@ -15,6 +15,8 @@
 // (≈139 KB for STEP=256) also keeps a second workgroup off the CU.  The encoder waves share
 // each SIMD with a SHA wave and use the issue slots the SHA wave leaves (it runs ~4.2 cycles per
 // VALU op, below the SIMD's rate).
+#include <algorithm>
+
 #include "device_common.hpp"
 #include "gf256.hpp"
 #include "gf_device.hpp"
@@ -176,20 +178,30 @@ hipError_t launch_step(const FusedParams& a, uint32_t p, hipStream_t s) {
 
 bool fused_supported(uint32_t d, uint32_t p) { return p >= 1 && p <= 8 && d + p <= kShaLanes; }
 
-// STEP: 256-byte steps (one workgroup per CU) when the grid fits the 256 CUs of one MI355X in
-// one pass; 128-byte steps (ring under 80 KB: two workgroups per CU, two SHA waves per SIMD)
-// when it would otherwise take two passes.
+// Parts per workgroup for a STEP: every SHA lane holds one chunk (G*(d+p) <= 256) and every
+// encoder thread gets at most one 16-byte column per step (G*STEP/16 <= 256): one extra task
+// round on one encoder wave would stall the whole workgroup at each step's barrier while its
+// SIMD also carries a SHA wave.  RS(10,4), STEP 256: G = 16 (not 18), 4096 parts = 256 groups.
+uint32_t parts_per_group(uint32_t t, uint32_t step) {
+    return std::min(kShaLanes / t, kEncThreads / (step / 16));
+}
+
+// STEP: 256-byte steps (ring ≈ 139 KB: one workgroup per CU) when the grid fits the CUs in one
+// pass; 128-byte steps (ring < 80 KB: two workgroups per CU, two SHA waves per SIMD) when it
+// would otherwise take two passes.
 hipError_t launch_encode_hash(const FusedParams& in, bool vec16, hipStream_t s) {
     if (in.n_parts == 0 || in.len == 0) return hipSuccess;
     if (!fused_supported(in.d, in.p)) return hipErrorInvalidValue;
     FusedParams a = in;
-    a.parts_per_wg = kShaLanes / (a.d + a.p);
-    const uint32_t grid = (a.n_parts + a.parts_per_wg - 1) / a.parts_per_wg;
+    const uint32_t t = a.d + a.p;
     int cus = 256;
     int dev = 0;
     if (hipGetDevice(&dev) == hipSuccess)
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    a.parts_per_wg = parts_per_group(t, 256);
+    const uint32_t grid = (a.n_parts + a.parts_per_wg - 1) / a.parts_per_wg;
     const bool two_per_cu = grid > uint32_t(cus);
+    if (two_per_cu) a.parts_per_wg = parts_per_group(t, 128);
     if (vec16)
         return two_per_cu ? launch_step<true, 128>(a, a.p, s) : launch_step<true, 256>(a, a.p, s);
     return two_per_cu ? launch_step<false, 128>(a, a.p, s) : launch_step<false, 256>(a, a.p, s);
