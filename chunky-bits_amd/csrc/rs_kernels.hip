@@ -12,6 +12,9 @@
 // with one v_bitop3_b32 (xor3).  The selectors of a data word are shared by every output row.
 // Coefficient tables are wave-uniform and come in through scalar loads (s_load), so a row costs
 // 3 v_perm + ~1.5 xor per data dword, with no LDS traffic and no bank conflicts.
+#include <cstdlib>
+#include <cstring>
+
 #include "device_common.hpp"
 #include "gf256.hpp"
 #include "gf_device.hpp"
@@ -28,8 +31,31 @@ constexpr uint64_t kApplyTile = uint64_t(kApplyThreads) * 16u * kApplyIters;  //
 
 // One 16-byte column (x .. x+16) of a part: acc[r] = XOR_j coef[r][j] (x) in_j[x..x+16).
 // FULL: every lane of the block has 16 valid bytes and the layout is 16-byte aligned.
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+
+template <bool NT>
+__device__ __forceinline__ uint4 ld16(const uint8_t* p) {
+    if (NT) {
+        const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+        return make_uint4(v.x, v.y, v.z, v.w);
+    }
+    return *reinterpret_cast<const uint4*>(p);
+}
+
+template <bool NT>
+__device__ __forceinline__ void st16(uint8_t* p, uint4 v) {
+    if (NT) {
+        v4u w = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(w, reinterpret_cast<v4u*>(p));
+    } else {
+        *reinterpret_cast<uint4*>(p) = v;
+    }
+}
+
 // tab points at row0's table of input 0; input j's RG tables start at tab + j*tab_stride.
-template <int RG, bool FULL>
+// GROUP inputs are loaded before any is multiplied (loads in flight per lane); NT selects
+// non-temporal loads/stores (streamed once, never re-read).
+template <int RG, bool FULL, int GROUP, bool NT>
 __device__ __forceinline__ void apply_column(uint8_t* pbase, uint64_t cs, uint64_t x,
                                              uint64_t rem, uint32_t d, uint32_t tab_stride,
                                              cu32* in_idx, cu32* out_idx, cu32* tab) {
@@ -39,19 +65,19 @@ __device__ __forceinline__ void apply_column(uint8_t* pbase, uint64_t cs, uint64
     const uint64_t n = rem < 16 ? rem : 16;
 
 #pragma unroll 1
-    for (uint32_t j0 = 0; j0 < d; j0 += 4) {
-        uint4 v[4];
+    for (uint32_t j0 = 0; j0 < d; j0 += GROUP) {
+        uint4 v[GROUP];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < GROUP; ++u) {
             v[u] = make_uint4(0u, 0u, 0u, 0u);
             if (j0 + u < d) {
                 const uint8_t* src = pbase + uint64_t(in_idx[j0 + u]) * cs + x;
-                if (FULL) v[u] = *reinterpret_cast<const uint4*>(src);
+                if (FULL) v[u] = ld16<NT>(src);
                 else v[u] = load_partial(src, n);
             }
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < GROUP; ++u) {
             if (j0 + u < d) {
                 const Sel s0 = selectors(v[u].x), s1 = selectors(v[u].y),
                           s2 = selectors(v[u].z), s3 = selectors(v[u].w);
@@ -71,15 +97,14 @@ cu32* tj = tab + size_t(j0 + u) * tab_stride;
 #pragma unroll
     for (int r = 0; r < RG; ++r) {
         uint8_t* dst = pbase + uint64_t(out_idx[r]) * cs + x;
-        if (FULL)
-            *reinterpret_cast<uint4*>(dst) = make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
+        if (FULL) st16<NT>(dst, make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]));
         else store_partial(dst, acc[r], n);
     }
 }
 
 // grid.x = n_parts * tiles_per_part (one 16 KiB column tile of one part per block),
 // grid.y = row groups of exactly RG output rows starting at row_base.
-template <int RG, bool VEC>
+template <int RG, bool VEC, int GROUP, bool NT>
 __global__ __launch_bounds__(kApplyThreads) void rs_apply_kernel(ApplyParams a,
                                                                  uint32_t tiles_per_part,
                                                                  uint32_t row_base) {
@@ -105,9 +130,11 @@ __global__ __launch_bounds__(kApplyThreads) void rs_apply_kernel(ApplyParams a,
         if (xb >= len) break;
         const uint64_t x = xb + uint64_t(threadIdx.x) * 16u;
         if (VEC && xb + kStep <= len) {
-            apply_column<RG, true>(pbase, cs, x, len - x, d, tab_stride, in_idx, out_idx, tab);
+            apply_column<RG, true, GROUP, NT>(pbase, cs, x, len - x, d, tab_stride, in_idx,
+                                              out_idx, tab);
         } else if (x < len) {
-            apply_column<RG, false>(pbase, cs, x, len - x, d, tab_stride, in_idx, out_idx, tab);
+            apply_column<RG, false, 4, false>(pbase, cs, x, len - x, d, tab_stride, in_idx,
+                                              out_idx, tab);
         }
     }
 }
@@ -156,17 +183,35 @@ __global__ __launch_bounds__(256) void fill_kernel(FillParams a, bool aligned8) 
     }
 }
 
+// CEC_APPLY_TUNE (tuning knob, read per launch): "nt" = non-temporal loads/stores,
+// "g8" = 8 inputs in flight per lane instead of 4.  Default: plain loads, groups of 4.
+int apply_tune() {
+    const char* e = std::getenv("CEC_APPLY_TUNE");
+    if (!e) return 0;
+    return (std::strstr(e, "nt") ? 1 : 0) | (std::strstr(e, "g8") ? 2 : 0);
+}
+
 template <int RG>
 hipError_t launch_rg(const ApplyParams& a, uint32_t row_base, uint32_t groups, bool vec16,
                      hipStream_t s) {
     const uint32_t tiles = uint32_t((a.len + kApplyTile - 1) / kApplyTile);
     dim3 grid(a.n_parts * tiles, groups);
-    if (vec16)
-        hipLaunchKernelGGL((rs_apply_kernel<RG, true>), grid, dim3(kApplyThreads), 0, s, a, tiles,
+    dim3 block(kApplyThreads);
+    if (!vec16) {
+        hipLaunchKernelGGL((rs_apply_kernel<RG, false, 4, false>), grid, block, 0, s, a, tiles,
                            row_base);
-    else
-        hipLaunchKernelGGL((rs_apply_kernel<RG, false>), grid, dim3(kApplyThreads), 0, s, a,
-                           tiles, row_base);
+        return hipGetLastError();
+    }
+    switch (apply_tune()) {
+        case 1: hipLaunchKernelGGL((rs_apply_kernel<RG, true, 4, true>), grid, block, 0, s, a,
+                                   tiles, row_base); break;
+        case 2: hipLaunchKernelGGL((rs_apply_kernel<RG, true, 8, false>), grid, block, 0, s, a,
+                                   tiles, row_base); break;
+        case 3: hipLaunchKernelGGL((rs_apply_kernel<RG, true, 8, true>), grid, block, 0, s, a,
+                                   tiles, row_base); break;
+        default: hipLaunchKernelGGL((rs_apply_kernel<RG, true, 4, false>), grid, block, 0, s, a,
+                                    tiles, row_base); break;
+    }
     return hipGetLastError();
 }
 
