@@ -11,10 +11,12 @@
 //              lane) from HBM into an LDS slot, compute the G*p parity columns with the v_perm
 //              GF(2^8) multiply (gf_device.hpp), write them to the slot and to HBM.
 // Double-buffered LDS ring [2][G*(d+p)][STEP+16]: while the SHA waves hash slot s%2 the
-// encoders fill slot (s+1)%2; one __syncthreads per step hands the slots over.  The ring
-// (≈139 KB for STEP=256) also keeps a second workgroup off the CU.  The encoder waves share
-// each SIMD with a SHA wave and use the issue slots the SHA wave leaves (it runs ~4.2 cycles per
-// VALU op, below the SIMD's rate).
+// encoders fill slot (s+1)%2; one barrier per step hands the slots over.  The encoders hold the
+// next step's d inputs in registers (loads issued right after the current step's compute) and
+// hand over with lgkmcnt(0) + s_barrier, so HBM latency never sits on the step.  The ring
+// (≈122 KB for RS(10,4)) also keeps a second workgroup off the CU.  The encoder waves share each
+// SIMD with a SHA wave and use the issue slots it leaves (it runs ~4.2 cycles per VALU op,
+// below the SIMD's rate).
 #include <algorithm>
 
 #include "device_common.hpp"
@@ -32,13 +34,25 @@ using namespace sha;
 constexpr int kFusedThreads = 512;
 constexpr uint32_t kShaLanes = 256;
 constexpr uint32_t kEncThreads = 256;
+constexpr int kMaxFusedData = 16;  // d > 16: separate encode + SHA kernels
 
-template <int P, bool VEC, int STEP>
+// LDS hand-over barrier that does not drain vector memory: the encoders keep next step's
+// global loads in flight across it (a __syncthreads() would wait for them: vmcnt(0)).
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// PMAX: parity rows (exact when a.p == PMAX; rows r >= a.p skipped by uniform guards).
+// Up to kMaxFusedData data inputs are held in registers per encoder thread (next step's
+// prefetch).  Aligned (16-byte) layouts only; others use the separate kernels.
+template <int PMAX, int STEP>
 __global__ __launch_bounds__(kFusedThreads) void encode_hash_kernel(FusedParams a) {
+    constexpr bool VEC = true;
+    constexpr int DMAX = kMaxFusedData;
     extern __shared__ __attribute__((aligned(16))) uint8_t ring[];
     constexpr uint32_t kRow = STEP + 16;  // 16-byte pad: conflict-free 16 B per lane accesses
     constexpr uint32_t kCols = STEP / 16;
-    const uint32_t d = a.d, t = a.d + P;
+    const uint32_t d = a.d, P = a.p, t = a.d + a.p;
     const uint32_t G = a.parts_per_wg;
     const uint32_t rows = G * t;
     const uint32_t part0 = blockIdx.x * G;
@@ -49,35 +63,48 @@ __global__ __launch_bounds__(kFusedThreads) void encode_hash_kernel(FusedParams 
 
     if (threadIdx.x >= kShaLanes) {
         // ------------------------------ encoders ------------------------------
+        // Each encoder thread owns one 16-byte column (g, col) of every step (launch_encode_hash
+        // guarantees G*kCols <= kEncThreads).  Per step: multiply the d inputs already in
+        // registers, write data + parity into the LDS slot, store parity to HBM, then issue the
+        // next step's d loads (all in flight at once) before the barrier.
         cu32* pat = as_const(a.pat);
         cu32* tab = pat + 1 + d + P;  // input j, row r at (j*P + r) * 5
         const uint32_t et = threadIdx.x - kShaLanes;
-        const uint32_t tasks = g_here * kCols;
-        auto fill = [&](uint32_t s, uint32_t slot) {
-            uint8_t* sl = ring + size_t(slot) * rows * kRow;
-#pragma unroll 1
-            for (uint32_t task = et; task < tasks; task += kEncThreads) {
-                const uint32_t g = task / kCols, col = task - g * kCols;
-                const uint64_t x = uint64_t(s) * STEP + col * 16u;
-                if (x >= L) continue;
-                const uint64_t n = (L - x) < 16 ? (L - x) : 16;
-                const bool full = VEC && n == 16;
-                uint8_t* pb = a.base + uint64_t(part0 + g) * a.part_stride;
-                uint8_t* lrow = sl + size_t(g) * t * kRow + col * 16u;
-                uint32_t acc[P][4];
+        const bool has_task = et < g_here * kCols;
+        const uint32_t g = et / kCols, col = et - g * kCols;
+        uint8_t* pb = a.base + uint64_t(part0 + g) * a.part_stride;
+        uint4 v[DMAX];
+        auto load_step = [&](uint32_t s) {
+            const uint64_t x = uint64_t(s) * STEP + col * 16u;
+            if (!has_task || x >= L) return;
+            const uint64_t n = (L - x) < 16 ? (L - x) : 16;
 #pragma unroll
-                for (int r = 0; r < P; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0u;
-#pragma unroll 2
-                for (uint32_t j = 0; j < d; ++j) {
+            for (int j = 0; j < DMAX; ++j) {
+                if (uint32_t(j) < d) {
                     const uint8_t* src = pb + uint64_t(j) * cs + x;
-                    const uint4 v = full ? *reinterpret_cast<const uint4*>(src)
-                                         : load_partial(src, n);
-                    *reinterpret_cast<uint4*>(lrow + size_t(j) * kRow) = v;
-                    const Sel s0 = selectors(v.x), s1 = selectors(v.y), s2 = selectors(v.z),
-                              s3 = selectors(v.w);
+                    v[j] = (VEC && n == 16) ? *reinterpret_cast<const uint4*>(src)
+                                            : load_partial(src, n);
+                }
+            }
+        };
+        auto emit_step = [&](uint32_t s, uint32_t slot) {
+            const uint64_t x = uint64_t(s) * STEP + col * 16u;
+            if (!has_task || x >= L) return;
+            const uint64_t n = (L - x) < 16 ? (L - x) : 16;
+            uint8_t* lrow = ring + (size_t(slot) * rows + size_t(g) * t) * kRow + col * 16u;
+            uint32_t acc[PMAX][4];
+#pragma unroll
+            for (int r = 0; r < PMAX; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0u;
+#pragma unroll
+            for (int j = 0; j < DMAX; ++j) {
+                if (uint32_t(j) < d) {
+                    *reinterpret_cast<uint4*>(lrow + size_t(j) * kRow) = v[j];
+                    const Sel s0 = selectors(v[j].x), s1 = selectors(v[j].y),
+                              s2 = selectors(v[j].z), s3 = selectors(v[j].w);
                     cu32* tj = tab + size_t(j) * P * kTabWords;
 #pragma unroll
-                    for (int r = 0; r < P; ++r) {
+                    for (int r = 0; r < PMAX; ++r) {
+                        if (uint32_t(r) >= P) break;
                         cu32* c = tj + r * kTabWords;
                         const uint32_t t0 = c[0], t1 = c[1], t2 = c[2], t3 = c[3], t4 = c[4];
                         acc[r][0] ^= gmul(s0, t0, t1, t2, t3, t4);
@@ -86,22 +113,28 @@ __global__ __launch_bounds__(kFusedThreads) void encode_hash_kernel(FusedParams 
                         acc[r][3] ^= gmul(s3, t0, t1, t2, t3, t4);
                     }
                 }
+            }
 #pragma unroll
-                for (int r = 0; r < P; ++r) {
-                    const uint4 o = make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
-                    *reinterpret_cast<uint4*>(lrow + size_t(d + r) * kRow) = o;
-                    uint8_t* dst = pb + uint64_t(d + r) * cs + x;
-                    if (full) *reinterpret_cast<uint4*>(dst) = o;
-                    else store_partial(dst, acc[r], n);
-                }
+            for (int r = 0; r < PMAX; ++r) {
+                if (uint32_t(r) >= P) break;
+                const uint4 o = make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
+                *reinterpret_cast<uint4*>(lrow + size_t(d + r) * kRow) = o;
+                uint8_t* dst = pb + uint64_t(d + r) * cs + x;
+                if (VEC && n == 16) *reinterpret_cast<uint4*>(dst) = o;
+                else store_partial(dst, acc[r], n);
             }
         };
-        fill(0, 0);
-        __syncthreads();
+        load_step(0);
+        emit_step(0, 0);
+        if (n_steps > 1) load_step(1);
+        lds_barrier();
 #pragma unroll 1
         for (uint32_t s = 0; s < n_steps; ++s) {
-            if (s + 1 < n_steps) fill(s + 1, (s + 1) & 1u);
-            __syncthreads();
+            if (s + 1 < n_steps) {
+                emit_step(s + 1, (s + 1) & 1u);
+                if (s + 2 < n_steps) load_step(s + 2);
+            }
+            lds_barrier();
         }
     } else {
         // ------------------------------ SHA lanes ------------------------------
@@ -146,37 +179,29 @@ __global__ __launch_bounds__(kFusedThreads) void encode_hash_kernel(FusedParams 
     }
 }
 
-template <int P, bool VEC, int STEP>
+template <int PMAX, int STEP>
 hipError_t launch_p(const FusedParams& a, hipStream_t s) {
-    const size_t lds = size_t(2) * a.parts_per_wg * (a.d + P) * (STEP + 16);
+    const size_t lds = size_t(2) * a.parts_per_wg * (a.d + a.p) * (STEP + 16);
     static const bool attr = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&encode_hash_kernel<P, VEC, STEP>),
+        reinterpret_cast<const void*>(&encode_hash_kernel<PMAX, STEP>),
         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
     if (!attr) return hipErrorInvalidValue;
     const uint32_t grid = (a.n_parts + a.parts_per_wg - 1) / a.parts_per_wg;
-    hipLaunchKernelGGL((encode_hash_kernel<P, VEC, STEP>), dim3(grid), dim3(kFusedThreads), lds,
-                       s, a);
+    hipLaunchKernelGGL((encode_hash_kernel<PMAX, STEP>), dim3(grid), dim3(kFusedThreads), lds, s,
+                       a);
     return hipGetLastError();
 }
 
-template <bool VEC, int STEP>
-hipError_t launch_step(const FusedParams& a, uint32_t p, hipStream_t s) {
-    switch (p) {
-        case 1: return launch_p<1, VEC, STEP>(a, s);
-        case 2: return launch_p<2, VEC, STEP>(a, s);
-        case 3: return launch_p<3, VEC, STEP>(a, s);
-        case 4: return launch_p<4, VEC, STEP>(a, s);
-        case 5: return launch_p<5, VEC, STEP>(a, s);
-        case 6: return launch_p<6, VEC, STEP>(a, s);
-        case 7: return launch_p<7, VEC, STEP>(a, s);
-        case 8: return launch_p<8, VEC, STEP>(a, s);
-        default: return hipErrorInvalidValue;
-    }
+template <int STEP>
+hipError_t launch_step(const FusedParams& a, hipStream_t s) {
+    return a.p == 4 ? launch_p<4, STEP>(a, s) : launch_p<8, STEP>(a, s);
 }
 
 }  // namespace
 
-bool fused_supported(uint32_t d, uint32_t p) { return p >= 1 && p <= 8 && d + p <= kShaLanes; }
+bool fused_supported(uint32_t d, uint32_t p) {
+    return p >= 1 && p <= 8 && d >= 1 && d <= uint32_t(kMaxFusedData) && d + p <= kShaLanes;
+}
 
 // Parts per workgroup for a STEP: every SHA lane holds one chunk (G*(d+p) <= 256) and every
 // encoder thread gets at most one 16-byte column per step (G*STEP/16 <= 256): one extra task
@@ -186,25 +211,16 @@ uint32_t parts_per_group(uint32_t t, uint32_t step) {
     return std::min(kShaLanes / t, kEncThreads / (step / 16));
 }
 
-// STEP: 256-byte steps (ring ≈ 139 KB: one workgroup per CU) when the grid fits the CUs in one
-// pass; 128-byte steps (ring < 80 KB: two workgroups per CU, two SHA waves per SIMD) when it
-// would otherwise take two passes.
+// 256-byte steps: the ring (≈122 KB for RS(10,4)) admits one workgroup per CU.  Grids larger
+// than the CU count run in passes, as the separate SHA kernel does; a second workgroup per CU
+// would need <= 128 VGPRs per wave and could gain at most ~16% (one SHA wave already keeps its
+// SIMD ~86% busy).
 hipError_t launch_encode_hash(const FusedParams& in, bool vec16, hipStream_t s) {
     if (in.n_parts == 0 || in.len == 0) return hipSuccess;
-    if (!fused_supported(in.d, in.p)) return hipErrorInvalidValue;
+    if (!fused_supported(in.d, in.p) || !vec16) return hipErrorInvalidValue;
     FusedParams a = in;
-    const uint32_t t = a.d + a.p;
-    int cus = 256;
-    int dev = 0;
-    if (hipGetDevice(&dev) == hipSuccess)
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    a.parts_per_wg = parts_per_group(t, 256);
-    const uint32_t grid = (a.n_parts + a.parts_per_wg - 1) / a.parts_per_wg;
-    const bool two_per_cu = grid > uint32_t(cus);
-    if (two_per_cu) a.parts_per_wg = parts_per_group(t, 128);
-    if (vec16)
-        return two_per_cu ? launch_step<true, 128>(a, a.p, s) : launch_step<true, 256>(a, a.p, s);
-    return two_per_cu ? launch_step<false, 128>(a, a.p, s) : launch_step<false, 256>(a, a.p, s);
+    a.parts_per_wg = parts_per_group(a.d + a.p, 256);
+    return launch_step<256>(a, s);
 }
 
 }  // namespace cec

@@ -398,15 +398,17 @@ def test_full_size_encode_erase_reconstruct_roundtrip(d, p, L, n_parts):
 # ----------------------------------------------------------------------------------------------
 
 @pytest.mark.parametrize("d,p,L,cstride,n_parts", [
-    (10, 4, 4096 + 13, 4112, 40),     # ragged tail, 18 parts per workgroup, 3 workgroups
-    (10, 4, 64, None, 19),            # exactly one SHA block, last workgroup with 1 part
+    (10, 4, 4096 + 13, 4112, 40),     # ragged tail, 16 parts per workgroup, 3 workgroups
+    (10, 4, 64, None, 17),            # exactly one SHA block, last workgroup with 1 part
     (10, 4, 63, 64, 5),               # shorter than a block (tail only)
-    (3, 2, 100, 112, 13100),          # > 256 workgroups: 128-byte steps, 2 per CU
-    (20, 8, 200, 208, 2400),          # > 256 workgroups for t = 28
-    (3, 2, 683, 683, 30),             # odd stride: unaligned path
+    (10, 4, 4096, None, 4100),        # > 256 workgroups: two passes
+    (16, 8, 1000, 1008, 21),          # largest fused d; generic (p != 4) parity-row path
+    (12, 3, 777, 784, 9),
     (1, 1, 1000, 1008, 17),
-    (200, 8, 300, 304, 3),            # one part per workgroup (t = 208)
-    (6, 10, 500, 512, 4),             # p > 8: falls back to the separate kernels
+    (3, 2, 100, 112, 300),
+    (3, 2, 683, 683, 30),             # odd stride: unaligned -> separate kernels
+    (20, 8, 200, 208, 40),            # d > 16 -> separate kernels
+    (6, 10, 500, 512, 4),             # p > 8 -> separate kernels
 ])
 def test_fused_encode_hash_matches_separate_and_oracle(d, p, L, cstride, n_parts, monkeypatch):
     t = d + p
