@@ -36,6 +36,27 @@ constexpr uint32_t kShaLanes = 256;
 constexpr uint32_t kEncThreads = 256;
 constexpr int kMaxFusedData = 16;  // d > 16: separate encode + SHA kernels
 
+// 4x4 byte transpose: r_k byte i = a_i byte k.  acc words hold, per data byte position, the
+// products of all parity rows (row r in byte r); the transpose turns 4 byte positions into one
+// output word per row.  8 v_perm per 4 words.
+__device__ __forceinline__ void transpose4(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3,
+                                           uint32_t r[4]) {
+    const uint32_t t01 = perm(a1, a0, 0x05010400u), t23 = perm(a3, a2, 0x05010400u);
+    const uint32_t u01 = perm(a1, a0, 0x07030602u), u23 = perm(a3, a2, 0x07030602u);
+    r[0] = perm(t23, t01, 0x05040100u);
+    r[1] = perm(t23, t01, 0x07060302u);
+    r[2] = perm(u23, u01, 0x05040100u);
+    r[3] = perm(u23, u01, 0x07060302u);
+}
+
+// Byte k of w, scaled to a table entry offset of 1 << SHIFT bytes (k constant after unroll).
+template <int SHIFT>
+__device__ __forceinline__ uint32_t entry_off(uint32_t w, int k) {
+    constexpr uint32_t mask = 0xFFu << SHIFT;
+    const int sh = 8 * k - SHIFT;
+    return sh >= 0 ? ((w >> sh) & mask) : ((w << -sh) & mask);
+}
+
 // LDS hand-over barrier that does not drain vector memory: the encoders keep next step's
 // global loads in flight across it (a __syncthreads() would wait for them: vmcnt(0)).
 __device__ __forceinline__ void lds_barrier() {
@@ -78,52 +99,109 @@ __global__ __launch_bounds__(kFusedThreads) void encode_hash_kernel(FusedParams 
             const uint64_t x = uint64_t(s) * STEP + col * 16u;
             if (!has_task || x >= L) return;
             const uint64_t n = (L - x) < 16 ? (L - x) : 16;
+            const uint8_t* src = pb + x;  // per-lane pointer walked by chunk_stride: no
+                                          // per-input 64-bit base held in SGPRs
 #pragma unroll
             for (int j = 0; j < DMAX; ++j) {
                 if (uint32_t(j) < d) {
-                    const uint8_t* src = pb + uint64_t(j) * cs + x;
                     v[j] = (VEC && n == 16) ? *reinterpret_cast<const uint4*>(src)
                                             : load_partial(src, n);
+                    src += cs;
                 }
             }
         };
+        // Product tables in LDS behind the ring: for input j and byte value x, one entry packs
+        // c[r][j] * x for every parity row r (row r in byte r; 4 B per entry for p <= 4, 8 B for
+        // p <= 8).  A data byte then costs one ds_read + one xor for all rows, instead of three
+        // half-rate v_perm per row: the GF multiply moves off the VALU the SHA waves saturate.
+        constexpr int kEntry = PMAX <= 4 ? 4 : 8;
+        uint8_t* tabs = ring + size_t(2) * rows * kRow;
+        {
+            const uint32_t x = et;  // 256 encoder threads = 256 byte values
+            const Sel sx = selectors(x);
+#pragma unroll 1
+            for (uint32_t j = 0; j < d; ++j) {
+                uint32_t lo = 0u, hi = 0u;
+                cu32* tj = tab + size_t(j) * P * kTabWords;
+#pragma unroll
+                for (int r = 0; r < PMAX; ++r) {
+                    if (uint32_t(r) >= P) break;
+                    cu32* c = tj + r * kTabWords;
+                    const uint32_t prod = gmul(sx, c[0], c[1], c[2], c[3], c[4]) & 0xFFu;
+                    if (r < 4) lo |= prod << (8 * r);
+                    else hi |= prod << (8 * (r - 4));
+                }
+                uint32_t* e = reinterpret_cast<uint32_t*>(tabs + (size_t(j) * 256 + x) * kEntry);
+                e[0] = lo;
+                if (kEntry == 8) e[1] = hi;
+            }
+        }
         auto emit_step = [&](uint32_t s, uint32_t slot) {
             const uint64_t x = uint64_t(s) * STEP + col * 16u;
             if (!has_task || x >= L) return;
             const uint64_t n = (L - x) < 16 ? (L - x) : 16;
             uint8_t* lrow = ring + (size_t(slot) * rows + size_t(g) * t) * kRow + col * 16u;
-            uint32_t acc[PMAX][4];
+            uint32_t acc_lo[16], acc_hi[16];
 #pragma unroll
-            for (int r = 0; r < PMAX; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0u;
+            for (int b = 0; b < 16; ++b) acc_lo[b] = acc_hi[b] = 0u;
 #pragma unroll
             for (int j = 0; j < DMAX; ++j) {
                 if (uint32_t(j) < d) {
                     *reinterpret_cast<uint4*>(lrow + size_t(j) * kRow) = v[j];
-                    const Sel s0 = selectors(v[j].x), s1 = selectors(v[j].y),
-                              s2 = selectors(v[j].z), s3 = selectors(v[j].w);
-                    cu32* tj = tab + size_t(j) * P * kTabWords;
+                    const uint8_t* tj = tabs + size_t(j) * 256 * kEntry;
+                    const uint32_t wq[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
 #pragma unroll
-                    for (int r = 0; r < PMAX; ++r) {
-                        if (uint32_t(r) >= P) break;
-                        cu32* c = tj + r * kTabWords;
-                        const uint32_t t0 = c[0], t1 = c[1], t2 = c[2], t3 = c[3], t4 = c[4];
-                        acc[r][0] ^= gmul(s0, t0, t1, t2, t3, t4);
-                        acc[r][1] ^= gmul(s1, t0, t1, t2, t3, t4);
-                        acc[r][2] ^= gmul(s2, t0, t1, t2, t3, t4);
-                        acc[r][3] ^= gmul(s3, t0, t1, t2, t3, t4);
+                    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            if (kEntry == 4) {
+                                acc_lo[4 * q + k] ^= *reinterpret_cast<const uint32_t*>(
+                                    tj + entry_off<2>(wq[q], k));
+                            } else {
+                                const uint2 e = *reinterpret_cast<const uint2*>(
+                                    tj + entry_off<3>(wq[q], k));
+                                acc_lo[4 * q + k] ^= e.x;
+                                acc_hi[4 * q + k] ^= e.y;
+                            }
+                        }
                     }
+                }
+            }
+            // rows 0..3 from acc_lo, rows 4..7 from acc_hi: out[r][q] = word q of parity row r
+            uint32_t out[8][4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                uint32_t r4[4];
+                transpose4(acc_lo[4 * q], acc_lo[4 * q + 1], acc_lo[4 * q + 2], acc_lo[4 * q + 3],
+                           r4);
+                out[0][q] = r4[0];
+                out[1][q] = r4[1];
+                out[2][q] = r4[2];
+                out[3][q] = r4[3];
+                if (PMAX > 4) {
+                    transpose4(acc_hi[4 * q], acc_hi[4 * q + 1], acc_hi[4 * q + 2],
+                               acc_hi[4 * q + 3], r4);
+                    out[4][q] = r4[0];
+                    out[5][q] = r4[1];
+                    out[6][q] = r4[2];
+                    out[7][q] = r4[3];
                 }
             }
 #pragma unroll
             for (int r = 0; r < PMAX; ++r) {
                 if (uint32_t(r) >= P) break;
-                const uint4 o = make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
+                const uint4 o = make_uint4(out[r][0], out[r][1], out[r][2], out[r][3]);
                 *reinterpret_cast<uint4*>(lrow + size_t(d + r) * kRow) = o;
                 uint8_t* dst = pb + uint64_t(d + r) * cs + x;
-                if (VEC && n == 16) *reinterpret_cast<uint4*>(dst) = o;
-                else store_partial(dst, acc[r], n);
+                if (VEC && n == 16) {
+                    *reinterpret_cast<uint4*>(dst) = o;
+                } else {
+                    const uint32_t o4[4] = {o.x, o.y, o.z, o.w};
+                    store_partial(dst, o4, n);
+                }
             }
         };
+        __syncthreads();  // tables built (the SHA waves join this barrier too)
         load_step(0);
         emit_step(0, 0);
         if (n_steps > 1) load_step(1);
@@ -145,6 +223,7 @@ __global__ __launch_bounds__(kFusedThreads) void encode_hash_kernel(FusedParams 
         for (int i = 0; i < 8; ++i) st[i] = kH0[i];
         const uint64_t nfull = L >> 6;
         uint32_t w[16];
+        __syncthreads();  // encoders' product tables built
         __syncthreads();  // slot 0 filled
 #pragma unroll 1
         for (uint32_t s = 0; s < n_steps; ++s) {
@@ -181,7 +260,8 @@ __global__ __launch_bounds__(kFusedThreads) void encode_hash_kernel(FusedParams 
 
 template <int PMAX, int STEP>
 hipError_t launch_p(const FusedParams& a, hipStream_t s) {
-    const size_t lds = size_t(2) * a.parts_per_wg * (a.d + a.p) * (STEP + 16);
+    const size_t lds = size_t(2) * a.parts_per_wg * (a.d + a.p) * (STEP + 16) +
+                       size_t(a.d) * 256 * (PMAX <= 4 ? 4 : 8);
     static const bool attr = hipFuncSetAttribute(
         reinterpret_cast<const void*>(&encode_hash_kernel<PMAX, STEP>),
         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
