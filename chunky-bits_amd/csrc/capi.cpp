@@ -602,7 +602,7 @@ int cec_encode_hash_batch(const cec_codec* cc, const cec_part_batch* b, uint8_t*
     if (b->n_parts * (cc->d + cc->p) > 0xFFFFFFFFull) return CEC_ERR_INVALID_ARGUMENT;
     cec_codec* c = const_cast<cec_codec*>(cc);
     const char* env = std::getenv("CEC_FUSED");  // tuning knob: 0 = separate kernels
-    const bool fused = fused_supported(uint32_t(c->d), uint32_t(c->p)) &&
+    const bool fused = fused_covers(uint32_t(c->d), uint32_t(c->p), b->chunk_len) &&
                        aligned16(b->base, b->part_stride, b->chunk_stride) &&
                        !(env && env[0] == '0');
     if (!fused) {

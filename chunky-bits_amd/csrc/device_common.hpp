@@ -41,4 +41,19 @@ typedef __attribute__((address_space(4))) const uint32_t cu32;
 
 __device__ __forceinline__ cu32* as_const(const uint32_t* p) { return (cu32*)(p); }
 
+// 16-byte load through the global address space: global_load_dwordx4 counts in vmcnt only (a
+// flat load also counts in lgkmcnt, so an LDS-only wait would drain it too).
+typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const v4u32 gv4u32;
+__device__ __forceinline__ uint4 gload16(const uint8_t* p) {
+    const v4u32 t = *(gv4u32*)(reinterpret_cast<uintptr_t>(p));
+    return make_uint4(t.x, t.y, t.z, t.w);
+}
+
+// Workgroup barrier that orders LDS only: waits for this wave's LDS ops (lgkmcnt) but leaves
+// global loads in flight across it (__syncthreads() would also wait for vmcnt(0)).
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 }  // namespace cec

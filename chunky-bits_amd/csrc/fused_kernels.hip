@@ -18,6 +18,7 @@
 // SIMD with a SHA wave and use the issue slots it leaves (it runs ~4.2 cycles per VALU op,
 // below the SIMD's rate).
 #include <algorithm>
+#include <cstdlib>
 
 #include "device_common.hpp"
 #include "gf256.hpp"
@@ -34,7 +35,7 @@ using namespace sha;
 constexpr int kFusedThreads = 512;
 constexpr uint32_t kShaLanes = 256;
 constexpr uint32_t kEncThreads = 256;
-constexpr int kMaxFusedData = 16;  // d > 16: separate encode + SHA kernels
+constexpr int kMaxFusedData = 16;  // generic build: d <= 16 (RS(20,p) has its own build)
 
 // 4x4 byte transpose: r_k byte i = a_i byte k.  acc words hold, per data byte position, the
 // products of all parity rows (row r in byte r); the transpose turns 4 byte positions into one
@@ -49,31 +50,96 @@ __device__ __forceinline__ void transpose4(uint32_t a0, uint32_t a1, uint32_t a2
     r[3] = perm(u23, u01, 0x07060302u);
 }
 
-// Byte k of w, scaled to a table entry offset of 1 << SHIFT bytes (k constant after unroll).
-template <int SHIFT>
-__device__ __forceinline__ uint32_t entry_off(uint32_t w, int k) {
-    constexpr uint32_t mask = 0xFFu << SHIFT;
-    const int sh = 8 * k - SHIFT;
-    return sh >= 0 ? ((w >> sh) & mask) : ((w << -sh) & mask);
+// Byte k of w times E (E = 4 or 8): one SDWA shift (src1_sel picks the byte, zero-extended).
+// The compiler's own form is v_bfe + v_lshl_add (two ops, one of them half-rate).
+template <int E>
+__device__ __forceinline__ uint32_t byte_scaled(uint32_t w, int k) {
+    static_assert(E == 4 || E == 8, "entry size");
+    uint32_t r;
+    if (E == 4) {
+        switch (k) {
+            case 0: asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(r) : "v"(w)); break;
+            case 1: asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(w)); break;
+            case 2: asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(w)); break;
+            default: asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(w)); break;
+        }
+    } else {
+        switch (k) {
+            case 0: asm("v_lshlrev_b32_sdwa %0, 3, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(r) : "v"(w)); break;
+            case 1: asm("v_lshlrev_b32_sdwa %0, 3, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(w)); break;
+            case 2: asm("v_lshlrev_b32_sdwa %0, 3, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(w)); break;
+            default: asm("v_lshlrev_b32_sdwa %0, 3, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(w)); break;
+        }
+    }
+    return r;
 }
 
-// LDS hand-over barrier that does not drain vector memory: the encoders keep next step's
-// global loads in flight across it (a __syncthreads() would wait for them: vmcnt(0)).
-__device__ __forceinline__ void lds_barrier() {
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+constexpr int col_width(int dmax) { return dmax > kMaxFusedData ? 8 : 16; }
+
+// NW words (NW*4 bytes) of one column: a full 16- or 8-byte load, or the n < NW*4 bytes of a
+// ragged chunk's last column (zero-filled).
+template <int NW, bool RAGGED>
+__device__ __forceinline__ void load_words(const uint8_t* src, uint64_t n, uint32_t w[NW]) {
+    if (!RAGGED || n == NW * 4) {
+        if (NW == 4) {
+            const uint4 q = *reinterpret_cast<const uint4*>(src);
+            w[0] = q.x; w[1] = q.y; w[2 % NW] = q.z; w[3 % NW] = q.w;
+        } else {
+            const uint2 q = *reinterpret_cast<const uint2*>(src);
+            w[0] = q.x; w[1] = q.y;
+        }
+    } else {
+        const uint4 q = load_partial(src, n);
+        w[0] = q.x; w[1] = q.y;
+        if (NW == 4) { w[2 % NW] = q.z; w[3 % NW] = q.w; }
+    }
+}
+
+template <int NW, bool RAGGED>
+__device__ __forceinline__ void store_words(uint8_t* dst, uint64_t n, const uint32_t w[NW]) {
+    if (!RAGGED || n == NW * 4) {
+        if (NW == 4) *reinterpret_cast<uint4*>(dst) = make_uint4(w[0], w[1], w[2 % NW], w[3 % NW]);
+        else *reinterpret_cast<uint2*>(dst) = make_uint2(w[0], w[1]);
+    } else {
+        const uint32_t o4[4] = {w[0], w[1], NW == 4 ? w[2 % NW] : 0u, NW == 4 ? w[3 % NW] : 0u};
+        store_partial(dst, o4, n);
+    }
+}
+
+template <int NW>
+__device__ __forceinline__ void lds_store_words(uint8_t* dst, const uint32_t w[NW]) {
+    if (NW == 4) *reinterpret_cast<uint4*>(dst) = make_uint4(w[0], w[1], w[2 % NW], w[3 % NW]);
+    else *reinterpret_cast<uint2*>(dst) = make_uint2(w[0], w[1]);
 }
 
 // PMAX: parity rows (exact when a.p == PMAX; rows r >= a.p skipped by uniform guards).
 // Up to kMaxFusedData data inputs are held in registers per encoder thread (next step's
 // prefetch).  Aligned (16-byte) layouts only; others use the separate kernels.
-template <int PMAX, int STEP>
+// MODE (timing attribution only, CEC_FUSED_MODE): 0 = the product; 1 = encoders skip the GF
+// multiply (parity = data chunk 0); 2 = encoders only join the barriers (SHA hashes whatever the
+// ring holds).  Modes 1 and 2 produce wrong parity/digests by design.
+// DT: data chunk count fixed at compile time (0 = a.d at run time, <= kMaxFusedData).
+template <int PMAX, int STEP, int MODE, int DT>
 __global__ __launch_bounds__(kFusedThreads) void encode_hash_kernel(FusedParams a) {
-    constexpr bool VEC = true;
-    constexpr int DMAX = kMaxFusedData;
+    constexpr int DMAX = DT ? DT : kMaxFusedData;
+    constexpr int kEntry = PMAX <= 4 ? 4 : 8;
+    // Column width per encoder task: 16 bytes, or 8 for builds with more than 16 inputs so the
+    // prefetched inputs plus accumulators stay in registers.
+    constexpr int CW = col_width(DMAX);
+    constexpr int NW = CW / 4;  // words per column
+    // Shape builds (DT != 0) run only when len is a multiple of CW (launch_step): no ragged
+    // last column, whose byte-wise path would cost the wide builds their registers.
+    constexpr bool RAGGED = DT == 0;
+    // LDS: product tables in static LDS (fixed addresses: input j's table base folds into the
+    // ds_read instruction offset), the ring in dynamic LDS behind them.
+    __shared__ __attribute__((aligned(16))) uint8_t tabs[DMAX * 256 * kEntry];
     extern __shared__ __attribute__((aligned(16))) uint8_t ring[];
     constexpr uint32_t kRow = STEP + 16;  // 16-byte pad: conflict-free 16 B per lane accesses
-    constexpr uint32_t kCols = STEP / 16;
-    const uint32_t d = a.d, P = a.p, t = a.d + a.p;
+    constexpr uint32_t kCols = STEP / CW;
+    // d is a compile-time constant only in the 4-byte-entry shape builds: with 8-byte entries
+    // the per-input uniform branches of a run-time d are what keep the scheduler from hoisting
+    // every input's lookups at once (fully unrolled, the RS(20,8) build spills).
+    const uint32_t d = (DT && kEntry == 4) ? uint32_t(DT) : a.d, P = a.p, t = d + a.p;
     const uint32_t G = a.parts_per_wg;
     const uint32_t rows = G * t;
     const uint32_t part0 = blockIdx.x * G;
@@ -84,38 +150,39 @@ __global__ __launch_bounds__(kFusedThreads) void encode_hash_kernel(FusedParams 
 
     if (threadIdx.x >= kShaLanes) {
         // ------------------------------ encoders ------------------------------
-        // Each encoder thread owns one 16-byte column (g, col) of every step (launch_encode_hash
-        // guarantees G*kCols <= kEncThreads).  Per step: multiply the d inputs already in
-        // registers, write data + parity into the LDS slot, store parity to HBM, then issue the
-        // next step's d loads (all in flight at once) before the barrier.
+        // Each encoder thread owns one CW-byte column (g, col) of every step
+        // (launch_encode_hash guarantees G*kCols <= kEncThreads).  Per step: multiply the d
+        // inputs already in registers, write data + parity into the LDS slot, store parity to
+        // HBM, then issue the next step's d loads (all in flight at once) before the barrier.
         cu32* pat = as_const(a.pat);
         cu32* tab = pat + 1 + d + P;  // input j, row r at (j*P + r) * 5
         const uint32_t et = threadIdx.x - kShaLanes;
-        const bool has_task = et < g_here * kCols;
-        const uint32_t g = et / kCols, col = et - g * kCols;
+        // Fewer column tasks than encoder threads (wide stripes, 128-byte steps): deal them
+        // round-robin over the 4 encoder waves so every SIMD's SHA wave shares its issue slots
+        // with the same amount of encoder work (the step barrier waits for the slowest SIMD).
+        const uint32_t task = G * kCols < kEncThreads ? (et & 63u) * 4u + (et >> 6) : et;
+        const bool has_task = task < g_here * kCols;
+        const uint32_t g = task / kCols, col = task - g * kCols;
         uint8_t* pb = a.base + uint64_t(part0 + g) * a.part_stride;
-        uint4 v[DMAX];
+        uint32_t v[DMAX][NW];
         auto load_step = [&](uint32_t s) {
-            const uint64_t x = uint64_t(s) * STEP + col * 16u;
-            if (!has_task || x >= L) return;
-            const uint64_t n = (L - x) < 16 ? (L - x) : 16;
+            const uint64_t x = uint64_t(s) * STEP + col * CW;
+            if (!has_task || x >= L || MODE == 2) return;
+            const uint64_t n = (L - x) < CW ? (L - x) : CW;
             const uint8_t* src = pb + x;  // per-lane pointer walked by chunk_stride: no
                                           // per-input 64-bit base held in SGPRs
 #pragma unroll
             for (int j = 0; j < DMAX; ++j) {
                 if (uint32_t(j) < d) {
-                    v[j] = (VEC && n == 16) ? *reinterpret_cast<const uint4*>(src)
-                                            : load_partial(src, n);
+                    load_words<NW, RAGGED>(src, n, v[j]);
                     src += cs;
                 }
             }
         };
-        // Product tables in LDS behind the ring: for input j and byte value x, one entry packs
-        // c[r][j] * x for every parity row r (row r in byte r; 4 B per entry for p <= 4, 8 B for
-        // p <= 8).  A data byte then costs one ds_read + one xor for all rows, instead of three
+        // Product tables in static LDS: for input j and byte value x, one entry packs c[r][j]*x
+        // for every parity row r (row r in byte r; 4 B per entry for p <= 4, 8 B for p <= 8).
+        // A data byte then costs one ds_read + half an xor3 for all rows, instead of three
         // half-rate v_perm per row: the GF multiply moves off the VALU the SHA waves saturate.
-        constexpr int kEntry = PMAX <= 4 ? 4 : 8;
-        uint8_t* tabs = ring + size_t(2) * rows * kRow;
         {
             const uint32_t x = et;  // 256 encoder threads = 256 byte values
             const Sel sx = selectors(x);
@@ -137,40 +204,72 @@ __global__ __launch_bounds__(kFusedThreads) void encode_hash_kernel(FusedParams 
             }
         }
         auto emit_step = [&](uint32_t s, uint32_t slot) {
-            const uint64_t x = uint64_t(s) * STEP + col * 16u;
-            if (!has_task || x >= L) return;
-            const uint64_t n = (L - x) < 16 ? (L - x) : 16;
-            uint8_t* lrow = ring + (size_t(slot) * rows + size_t(g) * t) * kRow + col * 16u;
-            uint32_t acc_lo[16], acc_hi[16];
+            const uint64_t x = uint64_t(s) * STEP + col * CW;
+            if (!has_task || x >= L || MODE == 2) return;
+            const uint64_t n = (L - x) < CW ? (L - x) : CW;
+            uint8_t* lrow = ring + (size_t(slot) * rows + size_t(g) * t) * kRow + col * CW;
+            uint32_t acc_lo[4 * NW], acc_hi[4 * NW];
 #pragma unroll
-            for (int b = 0; b < 16; ++b) acc_lo[b] = acc_hi[b] = 0u;
+            for (int b = 0; b < 4 * NW; ++b) acc_lo[b] = acc_hi[b] = 0u;
 #pragma unroll
-            for (int j = 0; j < DMAX; ++j) {
-                if (uint32_t(j) < d) {
-                    *reinterpret_cast<uint4*>(lrow + size_t(j) * kRow) = v[j];
-                    const uint8_t* tj = tabs + size_t(j) * 256 * kEntry;
-                    const uint32_t wq[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+            for (int j = 0; j < DMAX; ++j)
+                if (uint32_t(j) < d) lds_store_words<NW>(lrow + size_t(j) * kRow, v[j]);
+            if (MODE == 1) {
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
+                for (int q = 0; q < NW; ++q) acc_lo[4 * q] = v[0][q];
+            } else {
+                // Inputs in pairs: two lookups folded into the accumulator by one full-rate
+                // xor3.  Table j sits at LDS offset j*256*kEntry (an instruction offset); the
+                // entry index is one byte of the data word (byte select + scale: one SDWA op).
 #pragma unroll
-                        for (int k = 0; k < 4; ++k) {
-                            if (kEntry == 4) {
-                                acc_lo[4 * q + k] ^= *reinterpret_cast<const uint32_t*>(
-                                    tj + entry_off<2>(wq[q], k));
-                            } else {
-                                const uint2 e = *reinterpret_cast<const uint2*>(
-                                    tj + entry_off<3>(wq[q], k));
-                                acc_lo[4 * q + k] ^= e.x;
-                                acc_hi[4 * q + k] ^= e.y;
+                for (int j = 0; j < DMAX; j += 2) {
+                    if (j + 1 < DMAX && uint32_t(j + 1) < d) {
+                        const int j1 = j + 1 < DMAX ? j + 1 : j;
+                        const uint8_t* t0 = tabs + size_t(j) * 256 * kEntry;
+                        const uint8_t* t1 = tabs + size_t(j1) * 256 * kEntry;
+#pragma unroll
+                        for (int q = 0; q < NW; ++q) {
+#pragma unroll
+                            for (int k = 0; k < 4; ++k) {
+                                const uint32_t i0 = byte_scaled<kEntry>(v[j][q], k);
+                                const uint32_t i1 = byte_scaled<kEntry>(v[j1][q], k);
+                                if (kEntry == 4) {
+                                    acc_lo[4 * q + k] = xor3(
+                                        acc_lo[4 * q + k],
+                                        *reinterpret_cast<const uint32_t*>(t0 + i0),
+                                        *reinterpret_cast<const uint32_t*>(t1 + i1));
+                                } else {
+                                    const uint2 e0 = *reinterpret_cast<const uint2*>(t0 + i0);
+                                    const uint2 e1 = *reinterpret_cast<const uint2*>(t1 + i1);
+                                    acc_lo[4 * q + k] = xor3(acc_lo[4 * q + k], e0.x, e1.x);
+                                    acc_hi[4 * q + k] = xor3(acc_hi[4 * q + k], e0.y, e1.y);
+                                }
+                            }
+                        }
+                    } else if (uint32_t(j) < d) {
+                        const uint8_t* t0 = tabs + size_t(j) * 256 * kEntry;
+#pragma unroll
+                        for (int q = 0; q < NW; ++q) {
+#pragma unroll
+                            for (int k = 0; k < 4; ++k) {
+                                const uint32_t i0 = byte_scaled<kEntry>(v[j][q], k);
+                                if (kEntry == 4) {
+                                    acc_lo[4 * q + k] ^=
+                                        *reinterpret_cast<const uint32_t*>(t0 + i0);
+                                } else {
+                                    const uint2 e0 = *reinterpret_cast<const uint2*>(t0 + i0);
+                                    acc_lo[4 * q + k] ^= e0.x;
+                                    acc_hi[4 * q + k] ^= e0.y;
+                                }
                             }
                         }
                     }
                 }
             }
             // rows 0..3 from acc_lo, rows 4..7 from acc_hi: out[r][q] = word q of parity row r
-            uint32_t out[8][4];
+            uint32_t out[8][NW];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
+            for (int q = 0; q < NW; ++q) {
                 uint32_t r4[4];
                 transpose4(acc_lo[4 * q], acc_lo[4 * q + 1], acc_lo[4 * q + 2], acc_lo[4 * q + 3],
                            r4);
@@ -190,15 +289,8 @@ __global__ __launch_bounds__(kFusedThreads) void encode_hash_kernel(FusedParams 
 #pragma unroll
             for (int r = 0; r < PMAX; ++r) {
                 if (uint32_t(r) >= P) break;
-                const uint4 o = make_uint4(out[r][0], out[r][1], out[r][2], out[r][3]);
-                *reinterpret_cast<uint4*>(lrow + size_t(d + r) * kRow) = o;
-                uint8_t* dst = pb + uint64_t(d + r) * cs + x;
-                if (VEC && n == 16) {
-                    *reinterpret_cast<uint4*>(dst) = o;
-                } else {
-                    const uint32_t o4[4] = {o.x, o.y, o.z, o.w};
-                    store_partial(dst, o4, n);
-                }
+                lds_store_words<NW>(lrow + size_t(d + r) * kRow, out[r]);
+                store_words<NW, RAGGED>(pb + uint64_t(d + r) * cs + x, n, out[r]);
             }
         };
         __syncthreads();  // tables built (the SHA waves join this barrier too)
@@ -258,37 +350,66 @@ __global__ __launch_bounds__(kFusedThreads) void encode_hash_kernel(FusedParams 
     }
 }
 
-template <int PMAX, int STEP>
+template <int PMAX, int STEP, int MODE, int DT>
 hipError_t launch_p(const FusedParams& a, hipStream_t s) {
-    const size_t lds = size_t(2) * a.parts_per_wg * (a.d + a.p) * (STEP + 16) +
-                       size_t(a.d) * 256 * (PMAX <= 4 ? 4 : 8);
+    const size_t lds = size_t(2) * a.parts_per_wg * (a.d + a.p) * (STEP + 16);  // ring
+    const size_t tabs = size_t(DT ? DT : kMaxFusedData) * 256 * (PMAX <= 4 ? 4 : 8);
+    if (lds + tabs > 160 * 1024) return hipErrorInvalidValue;
     static const bool attr = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&encode_hash_kernel<PMAX, STEP>),
-        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+        reinterpret_cast<const void*>(&encode_hash_kernel<PMAX, STEP, MODE, DT>),
+        hipFuncAttributeMaxDynamicSharedMemorySize,
+        int(160 * 1024 - size_t(DT ? DT : kMaxFusedData) * 256 * (PMAX <= 4 ? 4 : 8))) ==
+        hipSuccess;
     if (!attr) return hipErrorInvalidValue;
     const uint32_t grid = (a.n_parts + a.parts_per_wg - 1) / a.parts_per_wg;
-    hipLaunchKernelGGL((encode_hash_kernel<PMAX, STEP>), dim3(grid), dim3(kFusedThreads), lds, s,
+    hipLaunchKernelGGL((encode_hash_kernel<PMAX, STEP, MODE, DT>), dim3(grid), dim3(kFusedThreads), lds, s,
                        a);
     return hipGetLastError();
 }
 
+int fused_mode() {
+    const char* e = std::getenv("CEC_FUSED_MODE");
+    return e ? std::atoi(e) : 0;
+}
+
 template <int STEP>
 hipError_t launch_step(const FusedParams& a, hipStream_t s) {
-    return a.p == 4 ? launch_p<4, STEP>(a, s) : launch_p<8, STEP>(a, s);
+    const int mode = fused_mode();
+    if constexpr (STEP == 256) {
+        if (mode == 1)
+            return a.p == 4 ? launch_p<4, STEP, 1, 0>(a, s) : launch_p<8, STEP, 1, 0>(a, s);
+        if (mode == 2)
+            return a.p == 4 ? launch_p<4, STEP, 2, 0>(a, s) : launch_p<8, STEP, 2, 0>(a, s);
+        // mode 3: the generic-d build on every shape it covers (A/B and tests against the
+        // shape builds)
+        if (mode != 3 && a.d == 10 && a.p == 4 && a.len % col_width(10) == 0)
+            return launch_p<4, STEP, 0, 10>(a, s);
+    }
+    if constexpr (STEP == 128) {
+        if (a.d == 20) {  // RS(20, p <= 8); launch_encode_hash checked len % col_width(20)
+            return launch_p<8, STEP, 0, 20>(a, s);
+        }
+    }
+    return a.p <= 4 ? launch_p<4, STEP, 0, 0>(a, s) : launch_p<8, STEP, 0, 0>(a, s);
 }
 
 }  // namespace
 
 bool fused_supported(uint32_t d, uint32_t p) {
-    return p >= 1 && p <= 8 && d >= 1 && d <= uint32_t(kMaxFusedData) && d + p <= kShaLanes;
+    return p >= 1 && p <= 8 && ((d >= 1 && d <= uint32_t(kMaxFusedData)) || d == 20);
+}
+
+// The fused kernel covers this (d, p, len): the RS(20,p) build has no ragged-column path.
+bool fused_covers(uint32_t d, uint32_t p, uint64_t len) {
+    return fused_supported(d, p) && (d != 20 || len % uint64_t(col_width(20)) == 0);
 }
 
 // Parts per workgroup for a STEP: every SHA lane holds one chunk (G*(d+p) <= 256) and every
 // encoder thread gets at most one 16-byte column per step (G*STEP/16 <= 256): one extra task
 // round on one encoder wave would stall the whole workgroup at each step's barrier while its
 // SIMD also carries a SHA wave.  RS(10,4), STEP 256: G = 16 (not 18), 4096 parts = 256 groups.
-uint32_t parts_per_group(uint32_t t, uint32_t step) {
-    return std::min(kShaLanes / t, kEncThreads / (step / 16));
+uint32_t parts_per_group(uint32_t t, uint32_t step, uint32_t cw = 16) {
+    return std::min(kShaLanes / t, kEncThreads / (step / cw));
 }
 
 // 256-byte steps: the ring (≈122 KB for RS(10,4)) admits one workgroup per CU.  Grids larger
@@ -297,10 +418,19 @@ uint32_t parts_per_group(uint32_t t, uint32_t step) {
 // SIMD ~86% busy).
 hipError_t launch_encode_hash(const FusedParams& in, bool vec16, hipStream_t s) {
     if (in.n_parts == 0 || in.len == 0) return hipSuccess;
-    if (!fused_supported(in.d, in.p) || !vec16) return hipErrorInvalidValue;
+    if (!fused_covers(in.d, in.p, in.len) || !vec16) return hipErrorInvalidValue;
     FusedParams a = in;
-    a.parts_per_wg = parts_per_group(a.d + a.p, 256);
-    return launch_step<256>(a, s);
+    const uint32_t t = a.d + a.p;
+    // 256-byte steps when the ring and the (generic-size) product tables fit the CU's LDS,
+    // else 128-byte steps (wide p = 8 stripes).
+    const size_t tabs = size_t(a.d > uint32_t(kMaxFusedData) ? a.d : kMaxFusedData) * 256 *
+                        (a.p <= 4 ? 4 : 8);
+    a.parts_per_wg = parts_per_group(t, 256);
+    if (a.d <= uint32_t(kMaxFusedData) &&
+        size_t(2) * a.parts_per_wg * t * (256 + 16) + tabs <= 160 * 1024)
+        return launch_step<256>(a, s);
+    a.parts_per_wg = parts_per_group(t, 128, uint32_t(col_width(int(a.d))));
+    return launch_step<128>(a, s);
 }
 
 }  // namespace cec

@@ -72,6 +72,7 @@ struct FusedParams {
 
 hipError_t launch_rs_apply(const ApplyParams& a, bool vec16, hipStream_t s);
 bool fused_supported(uint32_t d, uint32_t p);
+bool fused_covers(uint32_t d, uint32_t p, uint64_t len);
 hipError_t launch_encode_hash(const FusedParams& a, bool vec16, hipStream_t s);
 hipError_t launch_sha256(const ShaParams& a, bool vec16, hipStream_t s);
 hipError_t launch_fill(const FillParams& a, hipStream_t s);

@@ -200,6 +200,150 @@ __global__ __launch_bounds__(128) void sha256_split_kernel(ShaParams a) {
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// v3: split with balanced placement.  512-thread workgroup, one per CU (LDS ring > 80 KiB):
+// waves 0-3 producers, waves 4-7 rounds, so every SIMD carries exactly one rounds wave and one
+// producer wave (waves of a workgroup are dealt to the 4 SIMDs round-robin).  224 streams per
+// workgroup (56 per wave pair): C2's 57 344 chunks fill the 256 CUs in one pass.
+// Strided mode with one chunk length (every lane has the same block count).
+// ------------------------------------------------------------------------------------------
+constexpr uint32_t kS4Spw = 56;
+constexpr uint32_t kS4Streams = 4 * kS4Spw;
+constexpr size_t kS4Lds = size_t(2) * 256 * kKwRow * 4;  // 2 slots x 256 rows
+
+__device__ __forceinline__ void round_split(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d,
+                                            uint32_t& e, uint32_t& f, uint32_t& g, uint32_t& h,
+                                            uint32_t kw) {
+    const uint32_t x = h + kw + ch(e, f, g);
+    const uint32_t y = x + big_s1(e);
+    const uint32_t na = y + big_s0(a) + maj(a, b, c);
+    h = g;
+    g = f;
+    f = e;
+    e = d + y;
+    d = c;
+    c = b;
+    b = a;
+    a = na;
+}
+
+template <bool PRIO>
+__global__ __launch_bounds__(512) void sha256_split4_kernel(ShaParams a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t kw4[];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const bool producer = wave < 4u;
+    // Ring row = wave pair * 64 + lane.  Lanes without a stream of their own (lanes 56-63, past
+    // the last chunk) hash a copy of the workgroup's first chunk and store nothing: no lane
+    // branches, so the waitcnt that guards each prefetch is exact.
+    const uint32_t slot_lane = (wave & 3u) * 64u + lane;
+    const uint32_t item = blockIdx.x * kS4Streams + (wave & 3u) * kS4Spw + lane;
+    const bool valid = lane < kS4Spw && item < a.n_parts * a.n_chunks;
+    const uint32_t src_item = valid ? item : blockIdx.x * kS4Streams;
+    const uint64_t len = a.len;
+    const uint64_t nfull = len >> 6;
+    const uint32_t rem = uint32_t(len - 64 * nfull);
+    const uint32_t tb = tail_blocks(rem);
+    const uint32_t nb = uint32_t(nfull) + tb;
+    const uint8_t* p = nullptr;
+    uint64_t dummy;
+    item_source(a, src_item, p, dummy);
+    if (producer) {
+        // K[t]+W[t] of one block into ring slot `slot`
+        auto produce = [&](uint32_t w[16], uint32_t slot) {
+            uint32_t* row = &kw4[(slot * 256u + slot_lane) * kKwRow];
+#pragma unroll
+            for (int i = 0; i < 64; i += 4) {
+                uint32_t v[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    v[k] = (i + k < 16 ? w[i + k] : schedule_next(w, i + k)) + kK[i + k];
+                *reinterpret_cast<uint4*>(row + i) = make_uint4(v[0], v[1], v[2], v[3]);
+            }
+        };
+        auto load = [&](uint4 q[4], uint64_t blk) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) q[i] = gload16(p + 64 * blk + 16 * i);
+        };
+        // Full blocks, unrolled by two with two register sets so the next block's load stays
+        // in flight across the barrier (no copy back into a loop-carried set).
+        uint4 qa[4], qb[4];
+        const uint32_t nf = uint32_t(nfull);
+        // loads past the last full block re-read it (no branch around the prefetch)
+        if (nf) load(qa, 0);
+#pragma unroll 1
+        for (uint32_t b = 0; b < nf; b += 2) {
+            load(qb, min(b + 1, nf - 1));
+            {
+                uint32_t w[16];
+                block_words(qa, w);
+                produce(w, b & 1u);
+            }
+            lds_barrier();
+            if (b + 1 < nf) {
+                load(qa, min(b + 2, nf - 1));
+                uint32_t w[16];
+                block_words(qb, w);
+                produce(w, (b + 1) & 1u);
+                lds_barrier();
+            }
+        }
+#pragma unroll 1
+        for (uint32_t t = 0; t < tb; ++t) {
+            uint32_t w[16];
+            tail_words(p + 64 * nfull, rem, t, tb, len * 8, w);
+            produce(w, (nf + t) & 1u);
+            lds_barrier();
+        }
+        lds_barrier();  // matches the rounds waves' last hand-over
+    } else {
+        // The rounds waves carry the serial chain: let them win VALU arbitration (they are
+        // the younger half and would otherwise get the producers' leftover issue slots).
+        if (PRIO && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+        uint32_t st[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) st[i] = kH0[i];
+        lds_barrier();
+#pragma unroll 1
+        for (uint32_t b = 0; b < nb; ++b) {
+            {
+                const uint32_t* row = &kw4[((b & 1u) * 256u + slot_lane) * kKwRow];
+                uint32_t x0 = st[0], x1 = st[1], x2 = st[2], x3 = st[3];
+                uint32_t x4 = st[4], x5 = st[5], x6 = st[6], x7 = st[7];
+#pragma unroll
+                for (int i = 0; i < 64; i += 4) {
+                    const uint4 v = *reinterpret_cast<const uint4*>(row + i);
+                    round_split(x0, x1, x2, x3, x4, x5, x6, x7, v.x);
+                    round_split(x0, x1, x2, x3, x4, x5, x6, x7, v.y);
+                    round_split(x0, x1, x2, x3, x4, x5, x6, x7, v.z);
+                    round_split(x0, x1, x2, x3, x4, x5, x6, x7, v.w);
+                }
+                st[0] += x0;
+                st[1] += x1;
+                st[2] += x2;
+                st[3] += x3;
+                st[4] += x4;
+                st[5] += x5;
+                st[6] += x6;
+                st[7] += x7;
+            }
+            lds_barrier();
+        }
+        if (valid) finish_item(a, item, st);
+    }
+}
+
+template <bool PRIO>
+hipError_t launch_split4(const ShaParams& a, hipStream_t s) {
+    static const bool attr_ok =
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&sha256_split4_kernel<PRIO>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, int(kS4Lds)) == hipSuccess;
+    if (!attr_ok) return hipErrorInvalidValue;
+    const uint64_t total = uint64_t(a.n_parts) * a.n_chunks;
+    dim3 grid(uint32_t((total + kS4Streams - 1) / kS4Streams));
+    hipLaunchKernelGGL(sha256_split4_kernel<PRIO>, grid, dim3(512), kS4Lds, s, a);
+    return hipGetLastError();
+}
+
 int sha_variant() {
     const char* e = std::getenv("CEC_SHA_VARIANT");
     return e ? std::atoi(e) : 1;
@@ -208,8 +352,25 @@ int sha_variant() {
 // Dynamic LDS requested per lane-kernel workgroup: more than half of the 160 KiB of a CU, so
 // two workgroups never share a CU.
 constexpr size_t kCuReservation = 96 * 1024;
+// ... and at most two (grids larger than one workgroup per CU).
+constexpr size_t kCuReservation2 = 64 * 1024;
 
-hipError_t launch_lane(const ShaParams& a, bool vec16, hipStream_t s) {
+// CUs of the current device (cached per device ordinal).
+int device_cus() {
+    static int cache[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (!cache[dev]) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            n <= 0)
+            n = 256;
+        cache[dev] = n;
+    }
+    return cache[dev];
+}
+
+hipError_t launch_lane(const ShaParams& a, bool vec16, hipStream_t s, bool one_per_cu = false) {
     static const bool attr_ok = [] {
         return hipFuncSetAttribute(reinterpret_cast<const void*>(&sha256_lane_kernel<true>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -221,12 +382,16 @@ hipError_t launch_lane(const ShaParams& a, bool vec16, hipStream_t s) {
     if (!attr_ok) return hipErrorInvalidValue;
     const uint64_t total = uint64_t(a.n_parts) * a.n_chunks;
     dim3 grid(uint32_t((total + kLaneThreads - 1) / kLaneThreads));
+    // One workgroup (one wave per SIMD) per CU while the grid fits the chip in one pass.  When
+    // it does not, a second co-resident wave per SIMD turns the lone wave's issue-bound ~6000
+    // cycles per block into a shared SIMD-bound ~5100 per wave: every wave starts at once
+    // instead of a second, partly empty pass.
+    const size_t lds =
+        (!one_per_cu && grid.x > uint32_t(device_cus())) ? kCuReservation2 : kCuReservation;
     if (vec16)
-        hipLaunchKernelGGL((sha256_lane_kernel<true>), grid, dim3(kLaneThreads), kCuReservation,
-                           s, a);
+        hipLaunchKernelGGL((sha256_lane_kernel<true>), grid, dim3(kLaneThreads), lds, s, a);
     else
-        hipLaunchKernelGGL((sha256_lane_kernel<false>), grid, dim3(kLaneThreads),
-                           kCuReservation, s, a);
+        hipLaunchKernelGGL((sha256_lane_kernel<false>), grid, dim3(kLaneThreads), lds, s, a);
     return hipGetLastError();
 }
 
@@ -246,8 +411,12 @@ hipError_t launch_sha256(const ShaParams& a, bool vec16, hipStream_t s) {
     const uint64_t total = uint64_t(a.n_parts) * a.n_chunks;
     if (total == 0) return hipSuccess;
     // verify mode with absent chunks is lane-kernel only (the split kernel has no skip path)
-    return (sha_variant() == 2 && !a.present) ? launch_split(a, vec16, s)
-                                              : launch_lane(a, vec16, s);
+    const int v = sha_variant();
+    if (v == 2 && !a.present) return launch_split(a, vec16, s);
+    if (v == 3 && !a.present && !a.ptrs && vec16) return launch_split4<false>(a, s);
+    if (v == 4 && !a.present && !a.ptrs && vec16) return launch_split4<true>(a, s);
+    if (v == 5) return launch_lane(a, vec16, s, true);
+    return launch_lane(a, vec16, s);
 }
 
 }  // namespace cec

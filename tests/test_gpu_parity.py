@@ -397,7 +397,7 @@ def test_full_size_encode_erase_reconstruct_roundtrip(d, p, L, n_parts):
 # Fused encode+hash kernel vs the separate kernels and the oracle
 # ----------------------------------------------------------------------------------------------
 
-@pytest.mark.parametrize("d,p,L,cstride,n_parts", [
+@pytest.mark.parametrize("d,p,L,cstride,n_parts,mode", [(*c, "0")[:6] for c in [
     (10, 4, 4096 + 13, 4112, 40),     # ragged tail, 16 parts per workgroup, 3 workgroups
     (10, 4, 64, None, 17),            # exactly one SHA block, last workgroup with 1 part
     (10, 4, 63, 64, 5),               # shorter than a block (tail only)
@@ -407,10 +407,18 @@ def test_full_size_encode_erase_reconstruct_roundtrip(d, p, L, n_parts):
     (1, 1, 1000, 1008, 17),
     (3, 2, 100, 112, 300),
     (3, 2, 683, 683, 30),             # odd stride: unaligned -> separate kernels
-    (20, 8, 200, 208, 40),            # d > 16 -> separate kernels
+    (20, 8, 200, 208, 40),            # RS(20,8) build, 128-byte steps
+    (20, 8, 256 * 1024, None, 20),    # C4 chunk shape
+    (20, 4, 1000, 1008, 11),          # RS(20,p<8) on the p <= 8 build
+    (24, 4, 300, 304, 5),             # d > 16, d != 20 -> separate kernels
     (6, 10, 500, 512, 4),             # p > 8 -> separate kernels
-])
-def test_fused_encode_hash_matches_separate_and_oracle(d, p, L, cstride, n_parts, monkeypatch):
+    (16, 8, 4096, None, 30),          # p = 8, d = 16: 128-byte steps (LDS budget)
+    (10, 4, 4096 + 13, 4112, 40, "3"),  # generic-d build on the RS(10,4) shape
+    (10, 4, 64, None, 17, "3"),
+]])
+def test_fused_encode_hash_matches_separate_and_oracle(d, p, L, cstride, n_parts, mode,
+                                                       monkeypatch):
+    monkeypatch.setenv("CEC_FUSED_MODE", mode)
     t = d + p
     buf, batch = _device_parts(n_parts, t, L, cstride, seed=L * 3 + d)
     ref = buf.clone()
