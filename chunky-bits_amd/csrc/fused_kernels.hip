@@ -32,9 +32,8 @@ namespace {
 using namespace gf;
 using namespace sha;
 
-constexpr int kFusedThreads = 512;
-constexpr uint32_t kShaLanes = 256;
-constexpr uint32_t kEncThreads = 256;
+constexpr uint32_t kShaLanes = 256;   // SHA lanes of the one-wave-per-SIMD build (SW = 4)
+constexpr uint32_t kEncThreads = 256;  // 4 encoder waves in every build
 constexpr int kMaxFusedData = 16;  // generic build: d <= 16 (RS(20,p) has its own build)
 
 // 4x4 byte transpose: r_k byte i = a_i byte k.  acc words hold, per data byte position, the
@@ -119,8 +118,12 @@ __device__ __forceinline__ void lds_store_words(uint8_t* dst, const uint32_t w[N
 // multiply (parity = data chunk 0); 2 = encoders only join the barriers (SHA hashes whatever the
 // ring holds).  Modes 1 and 2 produce wrong parity/digests by design.
 // DT: data chunk count fixed at compile time (0 = a.d at run time, <= kMaxFusedData).
-template <int PMAX, int STEP, int MODE, int DT>
-__global__ __launch_bounds__(kFusedThreads) void encode_hash_kernel(FusedParams a) {
+// SW: SHA waves per workgroup, 4 (one per SIMD) or 8 (two per SIMD: batches with more chunks
+// than one wave per SIMD can hold, where two co-resident SHA waves turn the lone wave's
+// issue-bound ~6000 cycles per block into a SIMD-bound ~5100 each).
+template <int PMAX, int STEP, int MODE, int DT, int SW = 4>
+__global__ __launch_bounds__(64 * (SW + 4)) void encode_hash_kernel(FusedParams a) {
+    constexpr uint32_t kSha = 64u * SW;
     constexpr int DMAX = DT ? DT : kMaxFusedData;
     constexpr int kEntry = PMAX <= 4 ? 4 : 8;
     // Column width per encoder task: 16 bytes, or 8 for builds with more than 16 inputs so the
@@ -148,15 +151,18 @@ __global__ __launch_bounds__(kFusedThreads) void encode_hash_kernel(FusedParams 
     const uint64_t cs = a.chunk_stride;
     const uint32_t n_steps = uint32_t((L + STEP - 1) / STEP);
 
-    if (threadIdx.x >= kShaLanes) {
+    if (threadIdx.x >= kSha) {
         // ------------------------------ encoders ------------------------------
         // Each encoder thread owns one CW-byte column (g, col) of every step
         // (launch_encode_hash guarantees G*kCols <= kEncThreads).  Per step: multiply the d
         // inputs already in registers, write data + parity into the LDS slot, store parity to
         // HBM, then issue the next step's d loads (all in flight at once) before the barrier.
+        // Two SHA waves saturate their SIMD: without priority the encoders would get no issue
+        // slots until the SHA waves park at the step barrier, which then waits for them.
+        if (a.enc_prio) __builtin_amdgcn_s_setprio(1);
         cu32* pat = as_const(a.pat);
         cu32* tab = pat + 1 + d + P;  // input j, row r at (j*P + r) * 5
-        const uint32_t et = threadIdx.x - kShaLanes;
+        const uint32_t et = threadIdx.x - kSha;
         // Fewer column tasks than encoder threads (wide stripes, 128-byte steps): deal them
         // round-robin over the 4 encoder waves so every SIMD's SHA wave shares its issue slots
         // with the same amount of encoder work (the step barrier waits for the slowest SIMD).
@@ -350,21 +356,27 @@ __global__ __launch_bounds__(kFusedThreads) void encode_hash_kernel(FusedParams 
     }
 }
 
-template <int PMAX, int STEP, int MODE, int DT>
+template <int PMAX, int STEP, int MODE, int DT, int SW = 4>
 hipError_t launch_p(const FusedParams& a, hipStream_t s) {
     const size_t lds = size_t(2) * a.parts_per_wg * (a.d + a.p) * (STEP + 16);  // ring
     const size_t tabs = size_t(DT ? DT : kMaxFusedData) * 256 * (PMAX <= 4 ? 4 : 8);
     if (lds + tabs > 160 * 1024) return hipErrorInvalidValue;
     static const bool attr = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&encode_hash_kernel<PMAX, STEP, MODE, DT>),
+        reinterpret_cast<const void*>(&encode_hash_kernel<PMAX, STEP, MODE, DT, SW>),
         hipFuncAttributeMaxDynamicSharedMemorySize,
         int(160 * 1024 - size_t(DT ? DT : kMaxFusedData) * 256 * (PMAX <= 4 ? 4 : 8))) ==
         hipSuccess;
     if (!attr) return hipErrorInvalidValue;
     const uint32_t grid = (a.n_parts + a.parts_per_wg - 1) / a.parts_per_wg;
-    hipLaunchKernelGGL((encode_hash_kernel<PMAX, STEP, MODE, DT>), dim3(grid), dim3(kFusedThreads), lds, s,
-                       a);
+    hipLaunchKernelGGL((encode_hash_kernel<PMAX, STEP, MODE, DT, SW>), dim3(grid),
+                       dim3(64 * (SW + 4)), lds, s, a);
     return hipGetLastError();
+}
+
+// Encoder waves at s_setprio 1: the build's default, or CEC_FUSED_PRIO=0/1 (dev knob, A/B).
+uint32_t fused_prio(uint32_t dflt) {
+    const char* e = std::getenv("CEC_FUSED_PRIO");
+    return e && (e[0] == '0' || e[0] == '1') ? uint32_t(e[0] - '0') : dflt;
 }
 
 int fused_mode() {
@@ -421,10 +433,25 @@ hipError_t launch_encode_hash(const FusedParams& in, bool vec16, hipStream_t s) 
     if (!fused_covers(in.d, in.p, in.len) || !vec16) return hipErrorInvalidValue;
     FusedParams a = in;
     const uint32_t t = a.d + a.p;
+    // RS(20,p) batches with more chunks than one SHA wave per SIMD holds: two SHA waves per
+    // SIMD (8 + 4 waves per workgroup), one workgroup per CU, 64-byte steps (the ring for 16
+    // parts x 28 chunks then fits beside the 40 KB of tables), parts spread over every CU.
+    if (a.d == 20 && fused_mode() != 3) {
+        const uint32_t cus = uint32_t(device_cus());
+        if (uint64_t(a.n_parts) * t > uint64_t(cus) * kShaLanes) {
+            const uint32_t cap = std::min(2 * kShaLanes / t, kEncThreads / (64u / 8u));
+            const uint32_t want = uint32_t((uint64_t(a.n_parts) + cus - 1) / cus);
+            a.parts_per_wg = std::min(cap, want);
+            a.enc_prio = fused_prio(1u);
+            if (size_t(2) * a.parts_per_wg * t * (64 + 16) + size_t(20) * 256 * 8 <= 160 * 1024)
+                return launch_p<8, 64, 0, 20, 8>(a, s);
+        }
+    }
     // 256-byte steps when the ring and the (generic-size) product tables fit the CU's LDS,
     // else 128-byte steps (wide p = 8 stripes).
     const size_t tabs = size_t(a.d > uint32_t(kMaxFusedData) ? a.d : kMaxFusedData) * 256 *
                         (a.p <= 4 ? 4 : 8);
+    a.enc_prio = fused_prio(0u);
     a.parts_per_wg = parts_per_group(t, 256);
     if (a.d <= uint32_t(kMaxFusedData) &&
         size_t(2) * a.parts_per_wg * t * (256 + 16) + tabs <= 160 * 1024)

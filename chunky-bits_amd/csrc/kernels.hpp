@@ -68,6 +68,7 @@ struct FusedParams {
     uint32_t d;
     uint32_t p;
     uint32_t parts_per_wg;  // set by launch_encode_hash
+    uint32_t enc_prio;      // set by launch_encode_hash: encoder waves at s_setprio 1
 };
 
 hipError_t launch_rs_apply(const ApplyParams& a, bool vec16, hipStream_t s);
@@ -75,6 +76,7 @@ bool fused_supported(uint32_t d, uint32_t p);
 bool fused_covers(uint32_t d, uint32_t p, uint64_t len);
 hipError_t launch_encode_hash(const FusedParams& a, bool vec16, hipStream_t s);
 hipError_t launch_sha256(const ShaParams& a, bool vec16, hipStream_t s);
+int device_cus();  // CUs of the current device
 hipError_t launch_fill(const FillParams& a, hipStream_t s);
 
 // Host mirror of the device generator (cec_synth_byte).

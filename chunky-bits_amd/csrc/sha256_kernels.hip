@@ -355,20 +355,6 @@ constexpr size_t kCuReservation = 96 * 1024;
 // ... and at most two (grids larger than one workgroup per CU).
 constexpr size_t kCuReservation2 = 64 * 1024;
 
-// CUs of the current device (cached per device ordinal).
-int device_cus() {
-    static int cache[64] = {0};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-    if (!cache[dev]) {
-        int n = 0;
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            n <= 0)
-            n = 256;
-        cache[dev] = n;
-    }
-    return cache[dev];
-}
 
 hipError_t launch_lane(const ShaParams& a, bool vec16, hipStream_t s, bool one_per_cu = false) {
     static const bool attr_ok = [] {
@@ -404,6 +390,21 @@ hipError_t launch_split(const ShaParams& a, bool vec16, hipStream_t s) {
 }
 
 }  // namespace
+
+// CUs of the current device (cached per device ordinal).
+int device_cus() {
+    static int cache[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (!cache[dev]) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            n <= 0)
+            n = 256;
+        cache[dev] = n;
+    }
+    return cache[dev];
+}
 
 // CEC_SHA_VARIANT (tuning knob, read per launch): 1 = one lane per chunk (default), 2 = split
 // producer/rounds waves.

@@ -410,6 +410,8 @@ def test_full_size_encode_erase_reconstruct_roundtrip(d, p, L, n_parts):
     (20, 8, 200, 208, 40),            # RS(20,8) build, 128-byte steps
     (20, 8, 256 * 1024, None, 20),    # C4 chunk shape
     (20, 4, 1000, 1008, 11),          # RS(20,p<8) on the p <= 8 build
+    (20, 8, 1024, None, 2400),        # > 65 536 chunks: two SHA waves per SIMD, 64-byte steps
+    (20, 4, 512 + 8, None, 2800),
     (24, 4, 300, 304, 5),             # d > 16, d != 20 -> separate kernels
     (6, 10, 500, 512, 4),             # p > 8 -> separate kernels
     (16, 8, 4096, None, 30),          # p = 8, d = 16: 128-byte steps (LDS budget)
