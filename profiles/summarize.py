@@ -46,6 +46,11 @@ def mean(v):
 def main():
     tag = sys.argv[1]
     config = sys.argv[sys.argv.index("--config") + 1] if "--config" in sys.argv else "c2"
+    # FETCH_SIZE multiplier: 2 for 16 B/lane streaming reads (the guide's gfx950 calibration);
+    # 1 for 8 B/lane reads (the RS(20,p) fused build), whose 64-B requests FETCH_SIZE counts in
+    # full: r1f_c4 reports 20 895 570 KiB = 0.996 x the 21.47 GB of data the kernel reads once.
+    fmult = float(sys.argv[sys.argv.index("--fetch-mult") + 1]) if "--fetch-mult" in sys.argv \
+        else 2.0
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
     stats = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
     sq, _ = pmc(os.path.join(src, "pmc_sq", "run_counter_collection.csv"))
@@ -61,7 +66,7 @@ def main():
                      f"{float(r['MinNs'])/1e6:.3f} | {float(r['MaxNs'])/1e6:.3f} |")
     lines += ["", "## Counters (separate `--pmc` passes; per-launch means)", "",
               "| kernel | clock GHz (GRBM_GUI_ACTIVE/8/dur) | SQ_WAVES | VALU insts/wave | "
-              "FETCH_SIZE KiB | WRITE_SIZE KiB | HBM traffic GB (2xFETCH+WRITE) |",
+              f"FETCH_SIZE KiB | WRITE_SIZE KiB | HBM traffic GB ({fmult:g}xFETCH+WRITE) |",
               "|---|---|---|---|---|---|---|"]
     traffic = {}
     tpath = os.path.join(ROOT, "profiles", "traffic.json")
@@ -78,14 +83,15 @@ def main():
         vpw = mean(c["SQ_INSTS_VALU"]) / waves if waves else float("nan")
         f = mean(fetch[k].get("FETCH_SIZE", []))
         w = mean(write[k].get("WRITE_SIZE", []))
-        tb = (2 * f + w) * 1024 if f == f and w == w else None
+        tb = (fmult * f + w) * 1024 if f == f and w == w else None
         lines.append(f"| {k} | {ghz:.2f} | {waves:.0f} | {vpw:.0f} | {f:.0f} | {w:.0f} | "
                      f"{tb/1e9 if tb else float('nan'):.2f} |")
         if tb and k in ("rs_apply_kernel", "sha256_lane_kernel", "encode_hash_kernel"):
             traffic.setdefault(config, {})[k] = {
                 "bytes_per_launch": int(tb),
                 "fetch_kib": f, "write_kib": w,
-                "calibrated": k == "rs_apply_kernel",
+                "calibrated": k == "rs_apply_kernel" or fmult != 2.0,
+                "fetch_mult": fmult,
                 "source": f"profiles/{tag}_summary.md",
             }
     with open(os.path.join(ROOT, "profiles", f"{tag}_summary.md"), "w") as fh:
