@@ -34,8 +34,19 @@ import chunky_ec as ce  # noqa: E402
 from chunky_ec.sharding import barrier, dist_env, max_over_ranks, rank_seed  # noqa: E402
 
 METRIC = "RS(10,4) encode+sha256 GB/s per node at 1/2/4/8 GPUs; % of HBM roofline"
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md); 6.3 TB/s measured copy
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md); 5.79 TB/s measured
+# streaming ceiling of the 10-read/4-write RS(10,4) pattern (tools/ubench_stream.hip)
 MiB = 1 << 20
+
+# VALU roofline of SHA-256 (the bound of every hashed config).  Per 64-byte block one lane issues
+# 1406 VALU instructions (gfx950 ISA of the SHA loop: 576 v_alignbit, 241 v_add3, 16 v_perm
+# half-rate; 352 v_bitop3, 121 v_add, 96 v_lshrrev full-rate).  Measured SIMD cost per wave64
+# instruction with the SIMD saturated (tools/ubench_valu.hip): half-rate 4.45
+# cycles, full-rate 2.34.  Peak = 1024 SIMDs x 2.4 GHz / (mix-weighted cycles per instruction).
+SHA_VALU_PER_BLOCK = 1406
+SHA_HALF, SHA_FULL = 833, 573
+SHA_SIMD_CYCLES = (SHA_HALF * 4.45 + SHA_FULL * 2.34) / SHA_VALU_PER_BLOCK
+MI355X_SIMDS, MI355X_CLOCK_GHZ = 1024, 2.4
 
 CONFIGS = {
     # BASELINE.json configs[1]: the metric's workload.
@@ -62,7 +73,7 @@ CONFIGS = {
 
 
 KERNEL_SYMBOL = {"sha256_kernel": "sha256_lane_kernel", "rs_apply_kernel": "rs_apply_kernel",
-                 "rs_apply_kernel(reconstruct)": "rs_apply_kernel",
+                 "rs_apply_kernel(reconstruct)": "rs_apply_var_kernel",
                  "encode_hash_kernel": "encode_hash_kernel"}
 
 
@@ -310,6 +321,21 @@ def main():
     achieved = dom["algorithmic_bytes"] / (dom["ms"] / 1e3) / 1e9
     traffic = measured_traffic(args.config, dom_name, n_parts == CONFIGS[args.config]["parts"])
 
+    valu = None
+    if cfg["op"] == "encode_hash":
+        # useful SHA work: one lane-block per 64-byte block of every chunk (incl. FIPS padding)
+        blocks = L // 64 + (1 if L % 64 + 9 <= 64 else 2)
+        sha_ms = kernels["encode_hash_kernel" if fused else "sha256_kernel"]["ms"]
+        wave_inst = n_parts * t * blocks * SHA_VALU_PER_BLOCK / 64
+        achieved_g = wave_inst / (sha_ms / 1e3) / 1e9
+        peak_g = MI355X_SIMDS * MI355X_CLOCK_GHZ / SHA_SIMD_CYCLES
+        valu = {"bound": "valu", "kernel": "encode_hash_kernel" if fused else "sha256_kernel",
+                "achieved": round(achieved_g, 1), "peak": round(peak_g, 1),
+                "unit": "G wave64-inst/s", "frac": round(achieved_g / peak_g, 4),
+                "basis": f"SHA-256: {SHA_VALU_PER_BLOCK} VALU/64-B block/lane, "
+                         f"{SHA_SIMD_CYCLES:.2f} SIMD cycles/inst saturated, "
+                         f"{MI355X_SIMDS} SIMDs x {MI355X_CLOCK_GHZ} GHz"}
+
     ok = None
     if args.check and rank == 0 and cfg["op"] != "reconstruct":
         import hashlib
@@ -357,6 +383,8 @@ def main():
             },
             "kernels": kernels,
         }
+        if valu is not None:
+            line["valu_roofline"] = valu
         if ok is not None:
             line["check_vs_oracle"] = bool(ok)
         if world == 1 and not args.no_cpu_baseline:

@@ -653,7 +653,9 @@ int cec_reconstruct_batch(const cec_codec* cc, const cec_part_batch* b, const ui
         g.second.push_back(uint32_t(k));
     }
     if (groups.empty()) return CEC_OK;
-    // words = [records...][per bucket: part_ids..., part_pat...]
+    // words = [records...][launch lists: part_ids..., part_pat...].  Patterns of up to
+    // max_var_rows() rows (every RS(10,4) erasure set) share ONE launch that dispatches on each
+    // part's row count; wider patterns get a row-group launch per row count.
     std::vector<uint32_t> words;
     std::map<uint32_t, std::pair<std::vector<uint32_t>, std::vector<uint32_t>>> buckets;
     for (auto& kv : groups) {
@@ -662,23 +664,26 @@ int cec_reconstruct_batch(const cec_codec* cc, const cec_part_batch* b, const ui
         if (n_out == 0) continue;  // data_only: only parity missing, nothing to do
         const uint32_t off = uint32_t(words.size());
         words.insert(words.end(), rec->begin(), rec->end());
-        auto& bk = buckets[n_out];
+        auto& bk = buckets[n_out <= max_var_rows() ? 0u : n_out];  // 0 = the shared launch
         for (uint32_t part : kv.second.second) {
             bk.first.push_back(part);
             bk.second.push_back(off);
         }
     }
     if (buckets.empty()) return CEC_OK;
-    std::vector<std::pair<uint32_t, size_t>> launches;  // (n_out, word offset of part_ids)
+    struct Launch {
+        uint32_t n_out;  // 0: per-part row counts (launch_rs_apply_var)
+        size_t ids;      // word offset of part_ids
+        size_t count;
+    };
+    std::vector<Launch> launches;
     for (auto& kv : buckets) {
-        launches.push_back({kv.first, words.size()});
+        launches.push_back({kv.first, words.size(), kv.second.first.size()});
         words.insert(words.end(), kv.second.first.begin(), kv.second.first.end());
         words.insert(words.end(), kv.second.second.begin(), kv.second.second.end());
     }
     hipStream_t s = static_cast<hipStream_t>(stream);
     uint32_t* dwords = nullptr;
-    std::vector<size_t> counts;
-    for (auto& kv : buckets) counts.push_back(kv.second.first.size());
     CEC_TRY(upload_words(std::move(words), s, &dwords));
     const bool vec = aligned16(b->base, b->part_stride, b->chunk_stride);
     int status = CEC_OK;
@@ -689,12 +694,13 @@ int cec_reconstruct_batch(const cec_codec* cc, const cec_part_batch* b, const ui
         a.chunk_stride = b->chunk_stride;
         a.len = b->chunk_len;
         a.pat = dwords;
-        a.part_ids = dwords + launches[i].second;
-        a.part_pat = dwords + launches[i].second + counts[i];
-        a.n_parts = uint32_t(counts[i]);
+        a.part_ids = dwords + launches[i].ids;
+        a.part_pat = dwords + launches[i].ids + launches[i].count;
+        a.n_parts = uint32_t(launches[i].count);
         a.d = uint32_t(d);
-        a.n_rows = launches[i].first;
-        hipError_t e = launch_rs_apply(a, vec, s);
+        a.n_rows = launches[i].n_out;
+        hipError_t e = launches[i].n_out ? launch_rs_apply(a, vec, s)
+                                         : launch_rs_apply_var(a, vec, s);
         if (e != hipSuccess) status = hip_fail(e, "launch_rs_apply");
     }
     hipError_t e = hipFreeAsync(dwords, s);

@@ -72,6 +72,10 @@ struct FusedParams {
 };
 
 hipError_t launch_rs_apply(const ApplyParams& a, bool vec16, hipStream_t s);
+// Listed parts whose patterns carry their own row count (1..max_var_rows()), one launch;
+// a.n_rows is ignored.
+hipError_t launch_rs_apply_var(const ApplyParams& a, bool vec16, hipStream_t s);
+uint32_t max_var_rows();
 bool fused_supported(uint32_t d, uint32_t p);
 bool fused_covers(uint32_t d, uint32_t p, uint64_t len);
 hipError_t launch_encode_hash(const FusedParams& a, bool vec16, hipStream_t s);

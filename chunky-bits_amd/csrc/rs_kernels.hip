@@ -1,19 +1,28 @@
 // rs_kernels.hip — gfx950 (MI355X, CDNA4) GF(2^8) Reed-Solomon kernels + synthetic fill.
 //
-//  rs_apply_kernel   GF(2^8) matrix x chunk-set multiply.  One kernel serves
-//                    ReedSolomon::encode_sep (rows = parity rows of M, inputs = the d data chunks)
-//                    and reconstruct / reconstruct_data (rows = decode rows, inputs = the first d
-//                    present chunks), for thousands of parts per launch.  HBM-bound:
-//                    algorithmic bytes per part = (d + n_out) * len.
-//  fill_kernel       counter-based synthetic bytes for benchmarks/tests.
+//  rs_apply_kernel      GF(2^8) matrix x chunk-set multiply.  One kernel serves
+//                       ReedSolomon::encode_sep (rows = parity rows of M, inputs = the d data
+//                       chunks) and reconstruct / reconstruct_data (rows = decode rows, inputs =
+//                       the first d present chunks), for thousands of parts per launch.
+//                       HBM-bound: algorithmic bytes per part = (d + n_out) * len.
+//  rs_apply_var_kernel  the same for a reconstruct batch whose parts miss different numbers of
+//                       chunks: one launch, each block dispatched on its pattern's row count.
+//  fill_kernel          counter-based synthetic bytes for benchmarks/tests.
 //
 // GF multiply: no GF instruction exists, so a product c*x of four packed bytes is three
 // v_perm_b32 byte-table lookups (x split into bits [2:0], [5:3], [7:6]; see gf256.hpp) combined
 // with one v_bitop3_b32 (xor3).  The selectors of a data word are shared by every output row.
 // Coefficient tables are wave-uniform and come in through scalar loads (s_load), so a row costs
 // 3 v_perm + ~1.5 xor per data dword, with no LDS traffic and no bank conflicts.
+//
+// Memory shape: a block owns a 16 KiB column range of one part; each lane moves V 16-byte
+// columns per input per step (V = 2: two 1 KiB-per-wave loads per input in flight) with
+// non-temporal loads and stores (every byte is touched once).  That is the best of the
+// streaming-ceiling sweep of this 10-read/4-write pattern with no GF work at all
+// (tools/ubench_stream.hip: 5.79 TB/s) and the best rs_apply variant (5.57 TB/s, C2 encode).
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 #include "device_common.hpp"
 #include "gf256.hpp"
@@ -26,11 +35,10 @@ namespace {
 using namespace gf;
 
 constexpr int kApplyThreads = 256;
-constexpr int kApplyIters = 4;  // 16-byte columns per thread per block
-constexpr uint64_t kApplyTile = uint64_t(kApplyThreads) * 16u * kApplyIters;  // 16 KiB
+constexpr uint64_t kApplyTile = 16384;  // bytes of one part's column range per block
+constexpr uint64_t kSpan = uint64_t(kApplyThreads) * 16u;  // bytes per block per column step
+constexpr uint32_t kMaxApplyRows = 8;
 
-// One 16-byte column (x .. x+16) of a part: acc[r] = XOR_j coef[r][j] (x) in_j[x..x+16).
-// FULL: every lane of the block has 16 valid bytes and the layout is 16-byte aligned.
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 
 template <bool NT>
@@ -52,44 +60,57 @@ __device__ __forceinline__ void st16(uint8_t* p, uint4 v) {
     }
 }
 
+// V 16-byte columns (x + c*kSpan, c < V) of a part: acc[r] = XOR_j coef[r][j] (x) in_j[...].
+// FULL: every lane of the block has V*16 valid bytes and the layout is 16-byte aligned
+// (otherwise V == 1 with a byte-granular load/store of a rem < 16 tail).
 // tab points at row0's table of input 0; input j's RG tables start at tab + j*tab_stride.
-// GROUP inputs are loaded before any is multiplied (loads in flight per lane); NT selects
-// non-temporal loads/stores (streamed once, never re-read).
-template <int RG, bool FULL, int GROUP, bool NT>
+// GROUP inputs (x V columns) are loaded before any is multiplied; NT selects non-temporal
+// loads/stores (streamed once, never re-read).
+template <int RG, bool FULL, int GROUP, int V, bool NT>
 __device__ __forceinline__ void apply_column(uint8_t* pbase, uint64_t cs, uint64_t x,
                                              uint64_t rem, uint32_t d, uint32_t tab_stride,
                                              cu32* in_idx, cu32* out_idx, cu32* tab) {
-    uint32_t acc[RG][4];
+    static_assert(FULL || V == 1, "ragged columns are single");
+    uint32_t acc[RG][V][4];
 #pragma unroll
-    for (int r = 0; r < RG; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0u;
+    for (int r = 0; r < RG; ++r)
+#pragma unroll
+        for (int c = 0; c < V; ++c) acc[r][c][0] = acc[r][c][1] = acc[r][c][2] = acc[r][c][3] = 0u;
     const uint64_t n = rem < 16 ? rem : 16;
 
 #pragma unroll 1
     for (uint32_t j0 = 0; j0 < d; j0 += GROUP) {
-        uint4 v[GROUP];
+        uint4 v[GROUP][V];
 #pragma unroll
         for (int u = 0; u < GROUP; ++u) {
-            v[u] = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+            for (int c = 0; c < V; ++c) v[u][c] = make_uint4(0u, 0u, 0u, 0u);
             if (j0 + u < d) {
                 const uint8_t* src = pbase + uint64_t(in_idx[j0 + u]) * cs + x;
-                if (FULL) v[u] = ld16<NT>(src);
-                else v[u] = load_partial(src, n);
+#pragma unroll
+                for (int c = 0; c < V; ++c) {
+                    if (FULL) v[u][c] = ld16<NT>(src + c * kSpan);
+                    else v[u][c] = load_partial(src, n);
+                }
             }
         }
 #pragma unroll
         for (int u = 0; u < GROUP; ++u) {
             if (j0 + u < d) {
-                const Sel s0 = selectors(v[u].x), s1 = selectors(v[u].y),
-                          s2 = selectors(v[u].z), s3 = selectors(v[u].w);
-cu32* tj = tab + size_t(j0 + u) * tab_stride;
+                cu32* tj = tab + size_t(j0 + u) * tab_stride;
 #pragma unroll
-                for (int r = 0; r < RG; ++r) {
-                    cu32* t = tj + r * kTabWords;
-                    const uint32_t t0 = t[0], t1 = t[1], t2 = t[2], t3 = t[3], t4 = t[4];
-                    acc[r][0] ^= gmul(s0, t0, t1, t2, t3, t4);
-                    acc[r][1] ^= gmul(s1, t0, t1, t2, t3, t4);
-                    acc[r][2] ^= gmul(s2, t0, t1, t2, t3, t4);
-                    acc[r][3] ^= gmul(s3, t0, t1, t2, t3, t4);
+                for (int c = 0; c < V; ++c) {
+                    const Sel s0 = selectors(v[u][c].x), s1 = selectors(v[u][c].y),
+                              s2 = selectors(v[u][c].z), s3 = selectors(v[u][c].w);
+#pragma unroll
+                    for (int r = 0; r < RG; ++r) {
+                        cu32* t = tj + r * kTabWords;
+                        const uint32_t t0 = t[0], t1 = t[1], t2 = t[2], t3 = t[3], t4 = t[4];
+                        acc[r][c][0] ^= gmul(s0, t0, t1, t2, t3, t4);
+                        acc[r][c][1] ^= gmul(s1, t0, t1, t2, t3, t4);
+                        acc[r][c][2] ^= gmul(s2, t0, t1, t2, t3, t4);
+                        acc[r][c][3] ^= gmul(s3, t0, t1, t2, t3, t4);
+                    }
                 }
             }
         }
@@ -97,24 +118,24 @@ cu32* tj = tab + size_t(j0 + u) * tab_stride;
 #pragma unroll
     for (int r = 0; r < RG; ++r) {
         uint8_t* dst = pbase + uint64_t(out_idx[r]) * cs + x;
-        if (FULL) st16<NT>(dst, make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]));
-        else store_partial(dst, acc[r], n);
+#pragma unroll
+        for (int c = 0; c < V; ++c) {
+            if (FULL)
+                st16<NT>(dst + c * kSpan,
+                         make_uint4(acc[r][c][0], acc[r][c][1], acc[r][c][2], acc[r][c][3]));
+            else
+                store_partial(dst, acc[r][c], n);
+        }
     }
 }
 
-// grid.x = n_parts * tiles_per_part (one 16 KiB column tile of one part per block),
-// grid.y = row groups of exactly RG output rows starting at row_base.
-template <int RG, bool VEC, int GROUP, bool NT>
-__global__ __launch_bounds__(kApplyThreads) void rs_apply_kernel(ApplyParams a,
-                                                                 uint32_t tiles_per_part,
-                                                                 uint32_t row_base) {
-    const uint32_t lp = blockIdx.x / tiles_per_part;
-    const uint32_t tile = blockIdx.x - lp * tiles_per_part;
-    const uint32_t part = a.part_ids ? as_const(a.part_ids)[lp] : lp;
-    cu32* pat = as_const(a.pat) + (a.part_pat ? as_const(a.part_pat)[lp] : 0u);
+// One 16 KiB column tile of one part, rows [row0, row0 + RG) of its pattern record (n_out rows
+// in all).  Full column steps (kSpan*V bytes, aligned layout) take the V-wide path; the rest
+// (ragged end, unaligned layouts) the byte-granular single-column path.
+template <int RG, bool VEC, int GROUP, int V, bool NT>
+__device__ __forceinline__ void apply_tile(const ApplyParams& a, cu32* pat, uint32_t part,
+                                           uint32_t tile, uint32_t n_out, uint32_t row0) {
     const uint32_t d = a.d;
-    const uint32_t n_out = a.n_rows;
-    const uint32_t row0 = row_base + blockIdx.y * RG;
     cu32* in_idx = pat + 1;
     cu32* out_idx = pat + 1 + d + row0;
     cu32* tab = pat + 1 + d + n_out + size_t(row0) * kTabWords;
@@ -122,20 +143,56 @@ __global__ __launch_bounds__(kApplyThreads) void rs_apply_kernel(ApplyParams a,
     uint8_t* pbase = a.base + uint64_t(part) * a.part_stride;
     const uint64_t len = a.len;
     const uint64_t cs = a.chunk_stride;
-    constexpr uint64_t kStep = uint64_t(kApplyThreads) * 16u;
-
+    const uint64_t t0 = uint64_t(tile) * kApplyTile;
+    const uint64_t t1 = t0 + kApplyTile < len ? t0 + kApplyTile : len;
 #pragma unroll 1
-    for (int it = 0; it < kApplyIters; ++it) {
-        const uint64_t xb = (uint64_t(tile) * kApplyIters + it) * kStep;  // block-uniform
-        if (xb >= len) break;
+    for (uint64_t xb = t0; xb < t1; xb += kSpan * V) {  // block-uniform
         const uint64_t x = xb + uint64_t(threadIdx.x) * 16u;
-        if (VEC && xb + kStep <= len) {
-            apply_column<RG, true, GROUP, NT>(pbase, cs, x, len - x, d, tab_stride, in_idx,
-                                              out_idx, tab);
-        } else if (x < len) {
-            apply_column<RG, false, 4, false>(pbase, cs, x, len - x, d, tab_stride, in_idx,
-                                              out_idx, tab);
+        if (VEC && xb + kSpan * V <= len) {
+            apply_column<RG, true, GROUP, V, NT>(pbase, cs, x, len - x, d, tab_stride, in_idx,
+                                                 out_idx, tab);
+        } else {
+#pragma unroll 1
+            for (uint64_t xc = x; xc < t1 && xc < xb + kSpan * V; xc += kSpan)
+                apply_column<RG, false, 4, 1, false>(pbase, cs, xc, len - xc, d, tab_stride,
+                                                     in_idx, out_idx, tab);
         }
+    }
+}
+
+// grid.x = n_parts * tiles_per_part (one 16 KiB column tile of one part per block),
+// grid.y = row groups of exactly RG output rows starting at row_base.
+template <int RG, bool VEC, int GROUP, int V, bool NT>
+__global__ __launch_bounds__(kApplyThreads) void rs_apply_kernel(ApplyParams a,
+                                                                 uint32_t tiles_per_part,
+                                                                 uint32_t row_base) {
+    const uint32_t lp = blockIdx.x / tiles_per_part;
+    const uint32_t tile = blockIdx.x - lp * tiles_per_part;
+    const uint32_t part = a.part_ids ? as_const(a.part_ids)[lp] : lp;
+    cu32* pat = as_const(a.pat) + (a.part_pat ? as_const(a.part_pat)[lp] : 0u);
+    apply_tile<RG, VEC, GROUP, V, NT>(a, pat, part, tile, a.n_rows, row_base + blockIdx.y * RG);
+}
+
+// Reconstruct with mixed erasure counts in ONE launch: every listed part's pattern carries its
+// own row count n_out (1..8, the record's first word); each block branches (block-uniformly)
+// to the exact-RG body, so no row is predicated inside the inner loop.
+template <bool VEC, int GROUP, int V, bool NT>
+__global__ __launch_bounds__(kApplyThreads) void rs_apply_var_kernel(ApplyParams a,
+                                                                     uint32_t tiles_per_part) {
+    const uint32_t lp = blockIdx.x / tiles_per_part;
+    const uint32_t tile = blockIdx.x - lp * tiles_per_part;
+    const uint32_t part = as_const(a.part_ids)[lp];
+    cu32* pat = as_const(a.pat) + as_const(a.part_pat)[lp];
+    switch (pat[0]) {
+        case 1: apply_tile<1, VEC, GROUP, V, NT>(a, pat, part, tile, 1, 0); break;
+        case 2: apply_tile<2, VEC, GROUP, V, NT>(a, pat, part, tile, 2, 0); break;
+        case 3: apply_tile<3, VEC, GROUP, V, NT>(a, pat, part, tile, 3, 0); break;
+        case 4: apply_tile<4, VEC, GROUP, V, NT>(a, pat, part, tile, 4, 0); break;
+        case 5: apply_tile<5, VEC, GROUP, V, NT>(a, pat, part, tile, 5, 0); break;
+        case 6: apply_tile<6, VEC, GROUP, V, NT>(a, pat, part, tile, 6, 0); break;
+        case 7: apply_tile<7, VEC, GROUP, V, NT>(a, pat, part, tile, 7, 0); break;
+        case 8: apply_tile<8, VEC, GROUP, V, NT>(a, pat, part, tile, 8, 0); break;
+        default: break;  // the host routes n_out > 8 to row-group launches
     }
 }
 
@@ -183,36 +240,52 @@ __global__ __launch_bounds__(256) void fill_kernel(FillParams a, bool aligned8) 
     }
 }
 
-// CEC_APPLY_TUNE (tuning knob, read per launch): "nt" = non-temporal loads/stores,
-// "g8" = 8 inputs in flight per lane instead of 4.  Default: plain loads, groups of 4.
+// CEC_APPLY_TUNE (tuning knob, read per launch; unset = "nt"): "nt" = non-temporal loads and
+// stores, "v1" = one 16-byte column per lane per step instead of two, "g8" = 8 inputs in
+// flight per lane instead of 4; any other string = plain loads, two columns, groups of 4.
+// Measured on C2 encode (tools/apply_ab.py, MI355X): nt 10.79 ms, plain 11.20, v1 11.25,
+// v1+nt 11.15, g8 11.26, nt+g8 10.85.
 int apply_tune() {
     const char* e = std::getenv("CEC_APPLY_TUNE");
-    if (!e) return 0;
-    return (std::strstr(e, "nt") ? 1 : 0) | (std::strstr(e, "g8") ? 2 : 0);
+    if (!e) return 1;
+    return (std::strstr(e, "nt") ? 1 : 0) | (std::strstr(e, "g8") ? 2 : 0) |
+           (std::strstr(e, "v1") ? 4 : 0);
 }
+
+// Launch KERNEL<PRE... VEC, GROUP, V, NT> as picked by the tuning knob; layouts that are not
+// 16-byte aligned take the byte-granular instantiation.
+template <typename Launch>
+hipError_t dispatch_apply(bool vec16, Launch&& go) {
+    if (!vec16) return go(std::integral_constant<int, -1>{});
+    switch (apply_tune()) {
+        case 1: return go(std::integral_constant<int, 1>{});
+        case 2: return go(std::integral_constant<int, 2>{});
+        case 3: return go(std::integral_constant<int, 3>{});
+        case 4: return go(std::integral_constant<int, 4>{});
+        case 5: return go(std::integral_constant<int, 5>{});
+        default: return go(std::integral_constant<int, 0>{});
+    }
+}
+
+// tune code -> template arguments
+template <int K> struct Tune {
+    static constexpr bool kVec = K >= 0;
+    static constexpr int kGroup = K >= 0 && (K & 2) ? 8 : 4;
+    static constexpr int kV = K < 0 || (K & 4) ? 1 : 2;
+    static constexpr bool kNt = K >= 0 && (K & 1);
+};
 
 template <int RG>
 hipError_t launch_rg(const ApplyParams& a, uint32_t row_base, uint32_t groups, bool vec16,
                      hipStream_t s) {
     const uint32_t tiles = uint32_t((a.len + kApplyTile - 1) / kApplyTile);
-    dim3 grid(a.n_parts * tiles, groups);
-    dim3 block(kApplyThreads);
-    if (!vec16) {
-        hipLaunchKernelGGL((rs_apply_kernel<RG, false, 4, false>), grid, block, 0, s, a, tiles,
-                           row_base);
+    const dim3 grid(a.n_parts * tiles, groups);
+    return dispatch_apply(vec16, [&](auto k) {
+        using T = Tune<decltype(k)::value>;
+        hipLaunchKernelGGL((rs_apply_kernel<RG, T::kVec, T::kGroup, T::kV, T::kNt>), grid,
+                           dim3(kApplyThreads), 0, s, a, tiles, row_base);
         return hipGetLastError();
-    }
-    switch (apply_tune()) {
-        case 1: hipLaunchKernelGGL((rs_apply_kernel<RG, true, 4, true>), grid, block, 0, s, a,
-                                   tiles, row_base); break;
-        case 2: hipLaunchKernelGGL((rs_apply_kernel<RG, true, 8, false>), grid, block, 0, s, a,
-                                   tiles, row_base); break;
-        case 3: hipLaunchKernelGGL((rs_apply_kernel<RG, true, 8, true>), grid, block, 0, s, a,
-                                   tiles, row_base); break;
-        default: hipLaunchKernelGGL((rs_apply_kernel<RG, true, 4, false>), grid, block, 0, s, a,
-                                    tiles, row_base); break;
-    }
-    return hipGetLastError();
+    });
 }
 
 hipError_t launch_rows(const ApplyParams& a, uint32_t rg, uint32_t row_base, uint32_t groups,
@@ -231,19 +304,34 @@ hipError_t launch_rows(const ApplyParams& a, uint32_t rg, uint32_t row_base, uin
 
 }  // namespace
 
-// Rows are processed in groups of kMaxRows (8) plus one remainder group, so every kernel
+// Rows are processed in groups of kMaxApplyRows (8) plus one remainder group, so every kernel
 // instance handles exactly RG rows (no per-row predicate in the inner loop).
 hipError_t launch_rs_apply(const ApplyParams& a, bool vec16, hipStream_t s) {
     if (a.n_parts == 0 || a.n_rows == 0 || a.len == 0) return hipSuccess;
-    constexpr uint32_t kMaxRows = 8;
-    const uint32_t full = a.n_rows / kMaxRows, rem = a.n_rows % kMaxRows;
+    const uint32_t full = a.n_rows / kMaxApplyRows, rem = a.n_rows % kMaxApplyRows;
     if (full) {
-        hipError_t e = launch_rows(a, kMaxRows, 0, full, vec16, s);
+        hipError_t e = launch_rows(a, kMaxApplyRows, 0, full, vec16, s);
         if (e != hipSuccess) return e;
     }
-    if (rem) return launch_rows(a, rem, full * kMaxRows, 1, vec16, s);
+    if (rem) return launch_rows(a, rem, full * kMaxApplyRows, 1, vec16, s);
     return hipSuccess;
 }
+
+// Listed parts (part_ids / part_pat) whose patterns have 1..kMaxApplyRows rows each: one launch.
+hipError_t launch_rs_apply_var(const ApplyParams& a, bool vec16, hipStream_t s) {
+    if (a.n_parts == 0 || a.len == 0) return hipSuccess;
+    if (!a.part_ids || !a.part_pat) return hipErrorInvalidValue;
+    const uint32_t tiles = uint32_t((a.len + kApplyTile - 1) / kApplyTile);
+    const dim3 grid(a.n_parts * tiles);
+    return dispatch_apply(vec16, [&](auto k) {
+        using T = Tune<decltype(k)::value>;
+        hipLaunchKernelGGL((rs_apply_var_kernel<T::kVec, T::kGroup, T::kV, T::kNt>), grid,
+                           dim3(kApplyThreads), 0, s, a, tiles);
+        return hipGetLastError();
+    });
+}
+
+uint32_t max_var_rows() { return kMaxApplyRows; }
 
 hipError_t launch_fill(const FillParams& a, hipStream_t s) {
     const uint64_t n_inst = uint64_t(a.n_parts) * a.n_chunks;

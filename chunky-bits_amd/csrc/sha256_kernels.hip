@@ -227,7 +227,9 @@ __device__ __forceinline__ void round_split(uint32_t& a, uint32_t& b, uint32_t& 
     a = na;
 }
 
-template <bool PRIO>
+// MODE (timing experiments only): 0 = normal, 1 = producers only hand over (no schedule work),
+// 2 = rounds waves only hand over (no rounds work).
+template <bool PRIO, int MODE = 0>
 __global__ __launch_bounds__(512) void sha256_split4_kernel(ShaParams a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t kw4[];
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
@@ -250,6 +252,7 @@ __global__ __launch_bounds__(512) void sha256_split4_kernel(ShaParams a) {
     if (producer) {
         // K[t]+W[t] of one block into ring slot `slot`
         auto produce = [&](uint32_t w[16], uint32_t slot) {
+            if (MODE == 1) return;
             uint32_t* row = &kw4[(slot * 256u + slot_lane) * kKwRow];
 #pragma unroll
             for (int i = 0; i < 64; i += 4) {
@@ -305,7 +308,7 @@ __global__ __launch_bounds__(512) void sha256_split4_kernel(ShaParams a) {
         lds_barrier();
 #pragma unroll 1
         for (uint32_t b = 0; b < nb; ++b) {
-            {
+            if (MODE != 2) {
                 const uint32_t* row = &kw4[((b & 1u) * 256u + slot_lane) * kKwRow];
                 uint32_t x0 = st[0], x1 = st[1], x2 = st[2], x3 = st[3];
                 uint32_t x4 = st[4], x5 = st[5], x6 = st[6], x7 = st[7];
@@ -332,15 +335,15 @@ __global__ __launch_bounds__(512) void sha256_split4_kernel(ShaParams a) {
     }
 }
 
-template <bool PRIO>
+template <bool PRIO, int MODE = 0>
 hipError_t launch_split4(const ShaParams& a, hipStream_t s) {
     static const bool attr_ok =
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&sha256_split4_kernel<PRIO>),
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&sha256_split4_kernel<PRIO, MODE>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, int(kS4Lds)) == hipSuccess;
     if (!attr_ok) return hipErrorInvalidValue;
     const uint64_t total = uint64_t(a.n_parts) * a.n_chunks;
     dim3 grid(uint32_t((total + kS4Streams - 1) / kS4Streams));
-    hipLaunchKernelGGL(sha256_split4_kernel<PRIO>, grid, dim3(512), kS4Lds, s, a);
+    hipLaunchKernelGGL((sha256_split4_kernel<PRIO, MODE>), grid, dim3(512), kS4Lds, s, a);
     return hipGetLastError();
 }
 
@@ -416,6 +419,8 @@ hipError_t launch_sha256(const ShaParams& a, bool vec16, hipStream_t s) {
     if (v == 2 && !a.present) return launch_split(a, vec16, s);
     if (v == 3 && !a.present && !a.ptrs && vec16) return launch_split4<false>(a, s);
     if (v == 4 && !a.present && !a.ptrs && vec16) return launch_split4<true>(a, s);
+    if (v == 7 && !a.present && !a.ptrs && vec16) return launch_split4<true, 1>(a, s);
+    if (v == 8 && !a.present && !a.ptrs && vec16) return launch_split4<true, 2>(a, s);
     if (v == 5) return launch_lane(a, vec16, s, true);
     return launch_lane(a, vec16, s);
 }

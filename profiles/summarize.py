@@ -20,7 +20,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def short(name: str) -> str:
-    for k in ("rs_apply_kernel", "sha256_lane_kernel", "sha256_split_kernel", "fill_kernel",
+    for k in ("rs_apply_var_kernel", "rs_apply_kernel", "sha256_lane_kernel", "sha256_split_kernel", "fill_kernel",
               "encode_hash_kernel", "copyBuffer"):
         if k in name:
             return k

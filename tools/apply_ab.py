@@ -1,6 +1,6 @@
 """A/B the rs_apply_kernel tuning variants (CEC_APPLY_TUNE) in ONE process on the C2 encode.
 
-python tools/apply_ab.py [--rounds 5] [--variants ",nt,g8,nt+g8"]
+python tools/apply_ab.py [--rounds 5] [--variants "plain,nt,v1,v1+nt,g8,nt+g8"]
 """
 import argparse
 import os
@@ -20,7 +20,7 @@ def main():
     ap.add_argument("--p", type=int, default=4)
     ap.add_argument("--chunk", type=int, default=1 << 20)
     ap.add_argument("--rounds", type=int, default=5)
-    ap.add_argument("--variants", default=",nt,g8,nt+g8")
+    ap.add_argument("--variants", default="plain,nt,v1,v1+nt,g8,nt+g8")
     args = ap.parse_args()
     t = args.d + args.p
     dev = torch.device("cuda", 0)
