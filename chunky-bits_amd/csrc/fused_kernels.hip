@@ -120,9 +120,16 @@ __device__ __forceinline__ void lds_store_words(uint8_t* dst, const uint32_t w[N
 // DT: data chunk count fixed at compile time (0 = a.d at run time, <= kMaxFusedData).
 // SW: SHA waves per workgroup, 4 (one per SIMD) or 8 (two per SIMD: batches with more chunks
 // than one wave per SIMD can hold, where two co-resident SHA waves turn the lone wave's
-// issue-bound ~6000 cycles per block into a SIMD-bound ~5100 each).
-template <int PMAX, int STEP, int MODE, int DT, int SW = 4>
+// issue-bound ~6000 cycles per block into a SIMD-bound ~5800 each).
+// ENC3 (SW == 8 only): the column tasks run on SIMD 3 only.  Waves are dealt to the 4 SIMDs
+// round-robin (wave w on SIMD w % 4), so with at most 7 SHA waves (G*(d+p) <= 448) SIMD 3
+// carries ONE SHA wave where SIMDs 0-2 carry two: its spare issue slots absorb all the encoder
+// work, as waves 7 (an otherwise empty SHA slot) and 11 (tasks 0-63 and 64-127; needs
+// G*STEP/CW <= 128), while encoder waves 8-10 only build the product tables and join the
+// barriers.  The SIMDs with two SHA waves then carry no encoder work at all.
+template <int PMAX, int STEP, int MODE, int DT, int SW = 4, bool ENC3 = false>
 __global__ __launch_bounds__(64 * (SW + 4)) void encode_hash_kernel(FusedParams a) {
+    static_assert(!ENC3 || SW == 8, "ENC3 needs the two-SHA-wave build");
     constexpr uint32_t kSha = 64u * SW;
     constexpr int DMAX = DT ? DT : kMaxFusedData;
     constexpr int kEntry = PMAX <= 4 ? 4 : 8;
@@ -151,7 +158,8 @@ __global__ __launch_bounds__(64 * (SW + 4)) void encode_hash_kernel(FusedParams 
     const uint64_t cs = a.chunk_stride;
     const uint32_t n_steps = uint32_t((L + STEP - 1) / STEP);
 
-    if (threadIdx.x >= kSha) {
+    const uint32_t wave = threadIdx.x >> 6;
+    if (threadIdx.x >= kSha || (ENC3 && wave == 7u)) {
         // ------------------------------ encoders ------------------------------
         // Each encoder thread owns one CW-byte column (g, col) of every step
         // (launch_encode_hash guarantees G*kCols <= kEncThreads).  Per step: multiply the d
@@ -162,11 +170,14 @@ __global__ __launch_bounds__(64 * (SW + 4)) void encode_hash_kernel(FusedParams 
         if (a.enc_prio) __builtin_amdgcn_s_setprio(1);
         cu32* pat = as_const(a.pat);
         cu32* tab = pat + 1 + d + P;  // input j, row r at (j*P + r) * 5
-        const uint32_t et = threadIdx.x - kSha;
+        const uint32_t et = threadIdx.x - kSha;  // table builders: et < kEncThreads
         // Fewer column tasks than encoder threads (wide stripes, 128-byte steps): deal them
         // round-robin over the 4 encoder waves so every SIMD's SHA wave shares its issue slots
         // with the same amount of encoder work (the step barrier waits for the slowest SIMD).
-        const uint32_t task = G * kCols < kEncThreads ? (et & 63u) * 4u + (et >> 6) : et;
+        // ENC3: waves 7 and 11 (SIMD 3) take every task.
+        const uint32_t lane = threadIdx.x & 63u;
+        const uint32_t task = ENC3 ? (wave == 7u ? lane : (wave == 11u ? 64u + lane : ~0u))
+                              : G * kCols < kEncThreads ? (et & 63u) * 4u + (et >> 6) : et;
         const bool has_task = task < g_here * kCols;
         const uint32_t g = task / kCols, col = task - g * kCols;
         uint8_t* pb = a.base + uint64_t(part0 + g) * a.part_stride;
@@ -189,7 +200,7 @@ __global__ __launch_bounds__(64 * (SW + 4)) void encode_hash_kernel(FusedParams 
         // for every parity row r (row r in byte r; 4 B per entry for p <= 4, 8 B for p <= 8).
         // A data byte then costs one ds_read + half an xor3 for all rows, instead of three
         // half-rate v_perm per row: the GF multiply moves off the VALU the SHA waves saturate.
-        {
+        if (threadIdx.x >= kSha) {
             const uint32_t x = et;  // 256 encoder threads = 256 byte values
             const Sel sx = selectors(x);
 #pragma unroll 1
@@ -356,19 +367,19 @@ __global__ __launch_bounds__(64 * (SW + 4)) void encode_hash_kernel(FusedParams 
     }
 }
 
-template <int PMAX, int STEP, int MODE, int DT, int SW = 4>
+template <int PMAX, int STEP, int MODE, int DT, int SW = 4, bool ENC3 = false>
 hipError_t launch_p(const FusedParams& a, hipStream_t s) {
     const size_t lds = size_t(2) * a.parts_per_wg * (a.d + a.p) * (STEP + 16);  // ring
     const size_t tabs = size_t(DT ? DT : kMaxFusedData) * 256 * (PMAX <= 4 ? 4 : 8);
     if (lds + tabs > 160 * 1024) return hipErrorInvalidValue;
     static const bool attr = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&encode_hash_kernel<PMAX, STEP, MODE, DT, SW>),
+        reinterpret_cast<const void*>(&encode_hash_kernel<PMAX, STEP, MODE, DT, SW, ENC3>),
         hipFuncAttributeMaxDynamicSharedMemorySize,
         int(160 * 1024 - size_t(DT ? DT : kMaxFusedData) * 256 * (PMAX <= 4 ? 4 : 8))) ==
         hipSuccess;
     if (!attr) return hipErrorInvalidValue;
     const uint32_t grid = (a.n_parts + a.parts_per_wg - 1) / a.parts_per_wg;
-    hipLaunchKernelGGL((encode_hash_kernel<PMAX, STEP, MODE, DT, SW>), dim3(grid),
+    hipLaunchKernelGGL((encode_hash_kernel<PMAX, STEP, MODE, DT, SW, ENC3>), dim3(grid),
                        dim3(64 * (SW + 4)), lds, s, a);
     return hipGetLastError();
 }
@@ -377,6 +388,12 @@ hipError_t launch_p(const FusedParams& a, hipStream_t s) {
 uint32_t fused_prio(uint32_t dflt) {
     const char* e = std::getenv("CEC_FUSED_PRIO");
     return e && (e[0] == '0' || e[0] == '1') ? uint32_t(e[0] - '0') : dflt;
+}
+
+// CEC_FUSED_ENC3=0 turns the SIMD-3 encoder placement of the two-SHA-wave build off (A/B).
+bool fused_enc3() {
+    const char* e = std::getenv("CEC_FUSED_ENC3");
+    return !(e && e[0] == '0');
 }
 
 int fused_mode() {
@@ -443,8 +460,12 @@ hipError_t launch_encode_hash(const FusedParams& in, bool vec16, hipStream_t s) 
             const uint32_t want = uint32_t((uint64_t(a.n_parts) + cus - 1) / cus);
             a.parts_per_wg = std::min(cap, want);
             a.enc_prio = fused_prio(1u);
-            if (size_t(2) * a.parts_per_wg * t * (64 + 16) + size_t(20) * 256 * 8 <= 160 * 1024)
+            if (size_t(2) * a.parts_per_wg * t * (64 + 16) + size_t(20) * 256 * 8 <= 160 * 1024) {
+                if (fused_enc3() && a.parts_per_wg * t <= 7 * 64 &&
+                    a.parts_per_wg * (64u / 8u) <= 128)
+                    return launch_p<8, 64, 0, 20, 8, true>(a, s);
                 return launch_p<8, 64, 0, 20, 8>(a, s);
+            }
         }
     }
     // 256-byte steps when the ring and the (generic-size) product tables fit the CU's LDS,

@@ -417,9 +417,14 @@ def test_full_size_encode_erase_reconstruct_roundtrip(d, p, L, n_parts):
     (16, 8, 4096, None, 30),          # p = 8, d = 16: 128-byte steps (LDS budget)
     (10, 4, 4096 + 13, 4112, 40, "3"),  # generic-d build on the RS(10,4) shape
     (10, 4, 64, None, 17, "3"),
+    (20, 8, 1024, None, 2400, "enc3off"),  # two SHA waves per SIMD, encoders on every SIMD
+    (20, 8, 64 * 3 + 8, None, 4096),       # C4 part count: 16 parts/CU, encoders on SIMD 3
 ]])
 def test_fused_encode_hash_matches_separate_and_oracle(d, p, L, cstride, n_parts, mode,
                                                        monkeypatch):
+    if mode == "enc3off":
+        monkeypatch.setenv("CEC_FUSED_ENC3", "0")
+        mode = "0"
     monkeypatch.setenv("CEC_FUSED_MODE", mode)
     t = d + p
     buf, batch = _device_parts(n_parts, t, L, cstride, seed=L * 3 + d)
