@@ -251,6 +251,41 @@ def test_part_encode_vs_oracle(d, p, length):
     assert [h.digest for h in enc.hashes] == [x.tobytes() for x in dig]
 
 
+def test_host_api_concurrent_part_tasks_share_one_codec():
+    """FileWriteBuilder runs up to `concurrency` (10) part tasks that share one
+    Arc<ReedSolomon> (src/file/writer.rs:130-131,200-210) and call it from blocking threads, and
+    reads rebuild concurrently too (reader.rs:63 buffered(5)).  The C-ABI must be thread-safe and
+    reentrant: 10 threads hammer one codec with part_encode / reconstruct / sha256 (ctypes drops
+    the GIL during each call) and every result must equal the oracle's."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    d, p = 10, 4
+    rs = ce.ReedSolomon(d, p)
+
+    def task(i):
+        length = 10 * 4096 + 97 * i + 1
+        buf = gen_bytes(1000 + i, length).tobytes()
+        for _ in range(3):
+            enc = ce.part_encode(rs, buf, length)
+            cs, par, dig = oracle.part_encode(d, p, np.frombuffer(buf, np.uint8), length)
+            assert enc.chunksize == cs
+            assert [bytes(x) for x in enc.parity] == [x.tobytes() for x in par]
+            assert [h.digest for h in enc.hashes] == [x.tobytes() for x in dig]
+            data = np.frombuffer(buf + bytes(d * cs - length), np.uint8).reshape(d, cs)
+            shards = [bytearray(data[j].tobytes()) for j in range(d)] + \
+                     [bytearray(bytes(x)) for x in enc.parity]
+            full = [bytes(x) for x in shards]
+            lost = [(i + k * 3) % (d + p) for k in range(1 + i % p)]
+            for k in lost:
+                shards[k] = None
+            rs.reconstruct(shards)
+            assert [bytes(x) for x in shards] == full
+        return i
+
+    with ThreadPoolExecutor(max_workers=10) as ex:
+        assert sorted(ex.map(task, range(20))) == list(range(20))
+
+
 # ----------------------------------------------------------------------------------------------
 # Device-resident batches
 # ----------------------------------------------------------------------------------------------
