@@ -17,6 +17,11 @@ pub mod sys {
     }
 
     #[repr(C)]
+    pub struct cec_pipeline {
+        _private: [u8; 0],
+    }
+
+    #[repr(C)]
     #[derive(Clone, Copy, Debug)]
     pub struct cec_part_batch {
         pub base: *mut u8,
@@ -100,6 +105,57 @@ pub mod sys {
             data_only: c_int,
             stream: *mut c_void,
         ) -> c_int;
+        pub fn cec_verify_batch(
+            batch: *const cec_part_batch,
+            first_chunk: usize,
+            n_chunks: usize,
+            present: *const u8,
+            expected: *const u8,
+            ok: *mut u8,
+            stream: *mut c_void,
+        ) -> c_int;
+        pub fn cec_read_batch(
+            codec: *const cec_codec,
+            batch: *const cec_part_batch,
+            present: *const u8,
+            expected: *const u8,
+            verified: *mut u8,
+            part_status: *mut c_int,
+            stream: *mut c_void,
+        ) -> c_int;
+        pub fn cec_resilver_batch(
+            codec: *const cec_codec,
+            batch: *const cec_part_batch,
+            present: *const u8,
+            expected: *const u8,
+            verified: *mut u8,
+            part_status: *mut c_int,
+            stream: *mut c_void,
+        ) -> c_int;
+        pub fn cec_pipeline_new(
+            codec: *const cec_codec,
+            chunk_len: usize,
+            parts_per_batch: usize,
+            depth: usize,
+            out: *mut *mut cec_pipeline,
+        ) -> c_int;
+        pub fn cec_pipeline_free(pipeline: *mut cec_pipeline);
+        pub fn cec_pipeline_depth(pipeline: *const cec_pipeline) -> usize;
+        pub fn cec_pipeline_acquire(
+            pipeline: *mut cec_pipeline,
+            slot: *mut usize,
+            data: *mut *mut u8,
+        ) -> c_int;
+        pub fn cec_pipeline_submit(pipeline: *mut cec_pipeline, slot: usize, n_parts: usize) -> c_int;
+        pub fn cec_pipeline_wait(
+            pipeline: *mut cec_pipeline,
+            slot: usize,
+            parity: *mut *const u8,
+            digests: *mut *const u8,
+            n_parts: *mut usize,
+        ) -> c_int;
+        pub fn cec_pipeline_drain(pipeline: *mut cec_pipeline) -> c_int;
+        pub fn cec_pipeline_last_error() -> *const std::os::raw::c_char;
     }
 }
 
@@ -153,6 +209,19 @@ fn check(code: c_int) -> Result<(), CecError> {
             return Err(CecError::Engine(EngineError { code: other, message }));
         },
     }))
+}
+
+/// As [`check`], with the pipeline's own message for engine errors.
+fn check_pipe(code: c_int) -> Result<(), CecError> {
+    match check(code) {
+        Err(CecError::Engine(mut e)) => {
+            e.message = unsafe { std::ffi::CStr::from_ptr(sys::cec_pipeline_last_error()) }
+                .to_string_lossy()
+                .into_owned();
+            Err(CecError::Engine(e))
+        },
+        other => other,
+    }
 }
 
 /// `ReedSolomon<galois_8::Field>` backed by the gfx950 kernels.  Immutable after `new`, so it
@@ -307,4 +376,89 @@ pub fn part_encode(
         })
         .collect();
     Ok((chunksize, parity, digests))
+}
+
+/// Batched `FileWriteBuilder::write` compute (writer.rs:166-231): `depth` slots of
+/// `parts_per_batch` parts each, pinned host buffers, one HIP stream per slot.  One thread
+/// drives a pipeline (it is `Send`, not `Sync`).  Per slot: [`acquire`](Self::acquire) hands
+/// out the pinned `[parts][d][chunk_len]` input area (each part's zero-padded `data_buf`,
+/// writer.rs:172-197), [`submit`](Self::submit) queues H2D + fused encode/SHA-256 + D2H, and
+/// [`wait`](Self::wait) returns the parity chunks and the d+p digests of every part, in order.
+pub struct WritePipeline {
+    raw: *mut sys::cec_pipeline,
+    d: usize,
+    p: usize,
+    chunk_len: usize,
+}
+
+unsafe impl Send for WritePipeline {}
+
+impl Drop for WritePipeline {
+    fn drop(&mut self) {
+        unsafe { sys::cec_pipeline_free(self.raw) }
+    }
+}
+
+/// One completed batch: parity `[parts][p][chunk_len]` and digests `[parts][d+p][32]`
+/// (pinned host memory owned by the pipeline slot until it is acquired again).
+pub struct BatchResult<'a> {
+    pub parity: &'a [u8],
+    pub digests: &'a [u8],
+    pub n_parts: usize,
+}
+
+impl WritePipeline {
+    pub fn new(
+        codec: &ReedSolomon,
+        chunk_len: usize,
+        parts_per_batch: usize,
+        depth: usize,
+    ) -> Result<WritePipeline, CecError> {
+        let mut raw = std::ptr::null_mut();
+        check_pipe(unsafe { sys::cec_pipeline_new(codec.raw, chunk_len, parts_per_batch, depth, &mut raw) })?;
+        Ok(WritePipeline {
+            raw,
+            d: codec.data_shard_count(),
+            p: codec.parity_shard_count(),
+            chunk_len,
+        })
+    }
+
+    pub fn depth(&self) -> usize {
+        unsafe { sys::cec_pipeline_depth(self.raw) }
+    }
+
+    /// Next free slot (waits for its previous batch) and its pinned input area.
+    pub fn acquire(&mut self, parts_per_batch: usize) -> Result<(usize, &mut [u8]), CecError> {
+        let mut slot = 0usize;
+        let mut data = std::ptr::null_mut();
+        check_pipe(unsafe { sys::cec_pipeline_acquire(self.raw, &mut slot, &mut data) })?;
+        let len = parts_per_batch * self.d * self.chunk_len;
+        Ok((slot, unsafe { std::slice::from_raw_parts_mut(data, len) }))
+    }
+
+    /// Queue the first `n_parts` parts of `slot` (asynchronous).
+    pub fn submit(&mut self, slot: usize, n_parts: usize) -> Result<(), CecError> {
+        check_pipe(unsafe { sys::cec_pipeline_submit(self.raw, slot, n_parts) })
+    }
+
+    /// Wait for `slot`'s batch and borrow its parity and digests.
+    pub fn wait(&mut self, slot: usize) -> Result<BatchResult<'_>, CecError> {
+        let mut parity = std::ptr::null();
+        let mut digests = std::ptr::null();
+        let mut n_parts = 0usize;
+        check_pipe(unsafe { sys::cec_pipeline_wait(self.raw, slot, &mut parity, &mut digests, &mut n_parts) })?;
+        let plen = n_parts * self.p * self.chunk_len;
+        let dlen = n_parts * (self.d + self.p) * 32;
+        Ok(BatchResult {
+            parity: unsafe { std::slice::from_raw_parts(parity, plen) },
+            digests: unsafe { std::slice::from_raw_parts(digests, dlen) },
+            n_parts,
+        })
+    }
+
+    /// Wait for every submitted batch.
+    pub fn drain(&mut self) -> Result<(), CecError> {
+        check_pipe(unsafe { sys::cec_pipeline_drain(self.raw) })
+    }
 }
