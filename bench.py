@@ -114,7 +114,7 @@ def cpu_baseline(cfg, threads: int):
     }
 
 
-def run_stream(args, cfg, codec, world, rank, device):
+def run_stream(args, cfg, codec, world, rank, device, reduce_dev):
     """C5: host data -> pinned slot -> H2D -> fused encode+hash -> D2H parity + digests.
 
     The stream's bytes come from the slots' pinned buffers, filled once with synthetic data; each
@@ -154,7 +154,7 @@ def run_stream(args, cfg, codec, world, rank, device):
     pl.drain()
     barrier(world)
     t1 = time.perf_counter()
-    el = max_over_ranks(t1 - t0, world, device)
+    el = max_over_ranks(t1 - t0, world, reduce_dev)
     if rank == 0:
         total = total_parts * part_bytes
         line = {
@@ -202,16 +202,25 @@ def main():
     world, rank, local = dist_env()
     if world != args.gpus and rank == 0:
         print(f"note: WORLD_SIZE={world} but --gpus={args.gpus}", file=sys.stderr)
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+    # one rank per GPU; more ranks than GPUs (gloo rehearsal) share them round-robin
+    ordinal = local % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(ordinal)
+    device = torch.device("cuda", ordinal)
+    # RCCL ("nccl") carries only the barrier and the max-over-ranks all-reduce.
+    # CEC_BENCH_BACKEND=gloo rehearses N > 1 with several ranks on one GPU.
+    backend = os.environ.get("CEC_BENCH_BACKEND", "nccl")
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(backend)
+    reduce_dev = device if backend == "nccl" else None
 
     d, p, L, n_parts = cfg["d"], cfg["p"], cfg["chunk"], cfg["parts"]
     t = d + p
     codec = ce.ReedSolomon(d, p)
     if cfg["op"] == "stream":
-        return run_stream(args, cfg, codec, world, rank, device)
+        return run_stream(args, cfg, codec, world, rank, device, reduce_dev)
     buf = torch.empty((n_parts, t, L), dtype=torch.uint8, device=device)
     digests = torch.empty((n_parts, t, 32), dtype=torch.uint8, device=device)
     batch = ce.PartBatch.from_tensor(buf, L)
@@ -282,7 +291,7 @@ def main():
     barrier(world)
     t1 = time.perf_counter()
     local_s = (t1 - t0) / args.steps
-    step_s = max_over_ranks(local_s, world, device)
+    step_s = max_over_ranks(local_s, world, reduce_dev)
 
     # per-kernel averages over the timed steps
     def avg_ms(i, j):
