@@ -1,0 +1,480 @@
+// chunky_ec.hpp — C++17 host layer over the C-ABI (chunky_ec.h) that mirrors the interface of
+// the reference's part layer for this path, so host code and tests read like the reference's
+// own (Rust) code.  Header-only; every computation goes through libchunky_ec.so on the GPU.
+//
+//   reference (Rust)                                   here
+//   reed_solomon_erasure::ReedSolomon<galois_8::Field> chunky_ec::ReedSolomon
+//     ::new / encode_sep / reconstruct / reconstruct_data   (same names, same argument meaning)
+//   reed_solomon_erasure::Error (13 variants)          chunky_ec::Error + ErasureError exception
+//   file::hash::Sha256Hash (sha256.rs:14-47)           chunky_ec::Sha256Hash
+//     from_buf / verify / Display (lower-case hex)        from_buf / verify / to_string
+//   file::Chunk (chunk.rs:10-17)                       chunky_ec::Chunk (hash; locations are
+//                                                        keys of a ChunkStore, below)
+//   file::FilePart (file_part.rs:57-390)               chunky_ec::FilePart
+//     write_with_encoder (137-225)                        write_with_encoder
+//     read_with_context (73-135)                          read_with_context
+//     verify (228-251) / resilver (253-390)               verify / resilver
+//   file::FileWriteBuilder (writer.rs:88-255)          chunky_ec::FileWriteBuilder
+//   file::FileReference (file_reference.rs)            chunky_ec::FileReference
+//
+// Storage, placement and networking are out of scope: a ChunkStore stands in
+// for the content-addressed locations (`sha256-<hex>` files, location.rs:612).  Rust's
+// `Result<_, Error>` + `?` becomes a thrown ErasureError carrying the same variant; engine
+// failures (no GPU, HIP errors) throw EngineError and are never disguised as crate errors.
+#ifndef CHUNKY_EC_HPP
+#define CHUNKY_EC_HPP
+
+#include <algorithm>
+#include <array>
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <optional>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "chunky_ec.h"
+
+namespace chunky_ec {
+
+using Bytes = std::vector<uint8_t>;
+// &mut [Option<Vec<u8>>] of reconstruct / reconstruct_data
+using Shards = std::vector<std::optional<Bytes>>;
+
+// reed_solomon_erasure::Error, declaration order (cec_status 1..13).
+enum class Error {
+    TooFewShards = CEC_TOO_FEW_SHARDS,
+    TooManyShards = CEC_TOO_MANY_SHARDS,
+    TooFewDataShards = CEC_TOO_FEW_DATA_SHARDS,
+    TooManyDataShards = CEC_TOO_MANY_DATA_SHARDS,
+    TooFewParityShards = CEC_TOO_FEW_PARITY_SHARDS,
+    TooManyParityShards = CEC_TOO_MANY_PARITY_SHARDS,
+    TooFewBufferShards = CEC_TOO_FEW_BUFFER_SHARDS,
+    TooManyBufferShards = CEC_TOO_MANY_BUFFER_SHARDS,
+    IncorrectShardSize = CEC_INCORRECT_SHARD_SIZE,
+    TooFewShardsPresent = CEC_TOO_FEW_SHARDS_PRESENT,
+    EmptyShard = CEC_EMPTY_SHARD,
+    InvalidShardFlags = CEC_INVALID_SHARD_FLAGS,
+    InvalidIndex = CEC_INVALID_INDEX,
+};
+
+// A crate error (FileWriteError::Erasure / FileReadError::Erasure in the reference).
+class ErasureError : public std::runtime_error {
+   public:
+    explicit ErasureError(Error e) : std::runtime_error(cec_status_name(int(e))), error_(e) {}
+    Error error() const { return error_; }
+
+   private:
+    Error error_;
+};
+
+// Engine failure with no crate equivalent.
+class EngineError : public std::runtime_error {
+   public:
+    EngineError(int code, const std::string& what) : std::runtime_error(what), code_(code) {}
+    int code() const { return code_; }
+
+   private:
+    int code_;
+};
+
+namespace detail {
+inline void check(int status) {
+    if (status == CEC_OK) return;
+    if (status >= CEC_TOO_FEW_SHARDS && status <= CEC_INVALID_INDEX)
+        throw ErasureError(static_cast<Error>(status));
+    throw EngineError(status, std::string(cec_status_name(status)) + ": " + cec_last_error());
+}
+
+inline char hex_digit(unsigned v) { return char(v < 10 ? '0' + v : 'a' + (v - 10)); }
+
+inline int hex_value(char c) {
+    if (c >= '0' && c <= '9') return c - '0';
+    if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+    if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+    return -1;
+}
+}  // namespace detail
+
+// ReedSolomon<galois_8::Field>.  Immutable after construction; share it like the reference's
+// Arc<ReedSolomon> (writer.rs:131,200): every method is const and thread-safe.
+class ReedSolomon {
+   public:
+    ReedSolomon(size_t data_shards, size_t parity_shards) {
+        cec_codec* raw = nullptr;
+        detail::check(cec_codec_new(data_shards, parity_shards, &raw));
+        raw_ = std::shared_ptr<cec_codec>(raw, Free{});
+    }
+
+    size_t data_shard_count() const { return cec_codec_data_shards(raw_.get()); }
+    size_t parity_shard_count() const { return cec_codec_parity_shards(raw_.get()); }
+    size_t total_shard_count() const { return cec_codec_total_shards(raw_.get()); }
+
+    // The (d+p) x d coding matrix, row major (top d x d = identity).
+    std::vector<Bytes> matrix() const {
+        const size_t d = data_shard_count(), t = total_shard_count();
+        Bytes flat(t * d);
+        detail::check(cec_codec_matrix(raw_.get(), flat.data(), flat.size()));
+        std::vector<Bytes> rows(t);
+        for (size_t r = 0; r < t; ++r) rows[r].assign(flat.begin() + r * d, flat.begin() + (r + 1) * d);
+        return rows;
+    }
+
+    // encode_sep(&data, &mut parity): parity slices are overwritten.
+    void encode_sep(const std::vector<std::pair<const uint8_t*, size_t>>& data,
+                    std::vector<Bytes>& parity) const {
+        std::vector<const uint8_t*> dp;
+        std::vector<size_t> dl;
+        for (const auto& s : data) {
+            dp.push_back(s.first);
+            dl.push_back(s.second);
+        }
+        std::vector<uint8_t*> pp;
+        std::vector<size_t> pl;
+        for (auto& v : parity) {
+            pp.push_back(v.data());
+            pl.push_back(v.size());
+        }
+        detail::check(cec_encode_sep(raw_.get(), dp.data(), dl.data(), dp.size(), pp.data(),
+                                     pl.data(), pp.size()));
+    }
+
+    void encode_sep(const std::vector<Bytes>& data, std::vector<Bytes>& parity) const {
+        std::vector<std::pair<const uint8_t*, size_t>> views;
+        for (const auto& v : data) views.emplace_back(v.data(), v.size());
+        encode_sep(views, parity);
+    }
+
+    // reconstruct(&mut shards): rebuilds every missing shard (data and parity).
+    void reconstruct(Shards& shards) const { reconstruct_inner(shards, false); }
+    // reconstruct_data(&mut shards): rebuilds missing data shards only.
+    void reconstruct_data(Shards& shards) const { reconstruct_inner(shards, true); }
+
+    const cec_codec* raw() const { return raw_.get(); }
+
+   private:
+    struct Free {
+        void operator()(cec_codec* c) const { cec_codec_free(c); }
+    };
+    std::shared_ptr<cec_codec> raw_{nullptr, Free{}};
+
+    void reconstruct_inner(Shards& shards, bool data_only) const {
+        // The crate allocates missing slots zeroed at the present length: do the same so the
+        // engine writes straight into the caller's vectors.
+        size_t len = 0;
+        for (const auto& s : shards)
+            if (s && !s->empty()) {
+                len = s->size();
+                break;
+            }
+        const size_t d = data_shard_count();
+        std::vector<uint8_t> present(shards.size());
+        Shards scratch(shards.size());
+        std::vector<uint8_t*> ptrs(shards.size(), nullptr);
+        std::vector<size_t> lens(shards.size(), 0);
+        for (size_t i = 0; i < shards.size(); ++i) {
+            present[i] = shards[i].has_value();
+            if (shards[i]) {
+                ptrs[i] = shards[i]->data();
+                lens[i] = shards[i]->size();
+            } else if (!(data_only && i >= d)) {
+                scratch[i].emplace(len, 0);
+                ptrs[i] = scratch[i]->data();
+                lens[i] = len;
+            }
+        }
+        auto f = data_only ? cec_reconstruct_data : cec_reconstruct;
+        detail::check(f(raw_.get(), ptrs.data(), lens.data(), present.data(), shards.size()));
+        for (size_t i = 0; i < shards.size(); ++i)
+            if (!shards[i] && present[i]) shards[i] = std::move(scratch[i]);
+    }
+};
+
+// file::hash::Sha256Hash.
+class Sha256Hash {
+   public:
+    Sha256Hash() = default;
+    explicit Sha256Hash(const std::array<uint8_t, 32>& digest) : digest_(digest) {}
+
+    static Sha256Hash from_buf(const uint8_t* buf, size_t len) {
+        std::array<uint8_t, 32> d{};
+        detail::check(cec_sha256(buf, len, d.data()));
+        return Sha256Hash(d);
+    }
+    static Sha256Hash from_buf(const Bytes& buf) { return from_buf(buf.data(), buf.size()); }
+    static Sha256Hash from_buf(const std::string& s) {
+        return from_buf(reinterpret_cast<const uint8_t*>(s.data()), s.size());
+    }
+
+    // Many digests in one launch (DataHasher over a part's chunks).
+    static std::vector<Sha256Hash> from_bufs(const std::vector<const Bytes*>& bufs) {
+        std::vector<const uint8_t*> p;
+        std::vector<size_t> l;
+        for (const Bytes* b : bufs) {
+            p.push_back(b->data());
+            l.push_back(b->size());
+        }
+        std::vector<uint8_t> out(32 * bufs.size());
+        if (!bufs.empty()) detail::check(cec_sha256_many(p.data(), l.data(), p.size(), out.data()));
+        std::vector<Sha256Hash> r(bufs.size());
+        for (size_t i = 0; i < bufs.size(); ++i) std::memcpy(r[i].digest_.data(), &out[32 * i], 32);
+        return r;
+    }
+
+    // Display: lower-case hex (the metadata's `sha256: <hex>` and `sha256-<hex>` file names).
+    std::string to_string() const {
+        std::string s(64, '0');
+        for (size_t i = 0; i < 32; ++i) {
+            s[2 * i] = detail::hex_digit(digest_[i] >> 4);
+            s[2 * i + 1] = detail::hex_digit(digest_[i] & 15);
+        }
+        return s;
+    }
+
+    static Sha256Hash from_str(const std::string& hex) {
+        if (hex.size() != 64) throw std::invalid_argument("sha256 hex must be 64 digits");
+        std::array<uint8_t, 32> d{};
+        for (size_t i = 0; i < 32; ++i) {
+            const int hi = detail::hex_value(hex[2 * i]), lo = detail::hex_value(hex[2 * i + 1]);
+            if (hi < 0 || lo < 0) throw std::invalid_argument("bad sha256 hex digit");
+            d[i] = uint8_t(hi * 16 + lo);
+        }
+        return Sha256Hash(d);
+    }
+
+    // DataVerifier::verify: digest of buf equals this hash.
+    bool verify(const uint8_t* buf, size_t len) const { return from_buf(buf, len) == *this; }
+    bool verify(const Bytes& buf) const { return verify(buf.data(), buf.size()); }
+    bool verify(const std::string& s) const {
+        return verify(reinterpret_cast<const uint8_t*>(s.data()), s.size());
+    }
+
+    const std::array<uint8_t, 32>& digest() const { return digest_; }
+    bool operator==(const Sha256Hash& o) const { return digest_ == o.digest_; }
+    bool operator!=(const Sha256Hash& o) const { return !(*this == o); }
+    bool operator<(const Sha256Hash& o) const { return digest_ < o.digest_; }
+
+   private:
+    std::array<uint8_t, 32> digest_{};
+};
+
+// Content-addressed chunk storage standing in for the reference's locations (a shard is
+// written under its hash, location.rs:612).  Not thread-safe.
+class ChunkStore {
+   public:
+    void write_shard(const Sha256Hash& hash, Bytes bytes) { store_[hash] = std::move(bytes); }
+    std::optional<Bytes> read(const Sha256Hash& hash) const {
+        auto it = store_.find(hash);
+        if (it == store_.end()) return std::nullopt;
+        return it->second;
+    }
+    bool erase(const Sha256Hash& hash) { return store_.erase(hash) > 0; }
+    // Replace a stored shard's bytes (bit rot / tampering in tests).
+    bool corrupt(const Sha256Hash& hash, size_t offset) {
+        auto it = store_.find(hash);
+        if (it == store_.end() || offset >= it->second.size()) return false;
+        it->second[offset] ^= 0x01;
+        return true;
+    }
+    size_t size() const { return store_.size(); }
+
+   private:
+    std::map<Sha256Hash, Bytes> store_;
+};
+
+// file::Chunk: the hash of one chunk (its locations are the ChunkStore key).
+struct Chunk {
+    Sha256Hash hash;
+};
+
+enum class LocationIntegrity { Valid, Invalid, Unavailable, Resilvered };
+
+// VerifyPartReport / ResilverPartReport (file_part.rs:392-520), reduced to per-chunk status.
+struct PartReport {
+    std::vector<LocationIntegrity> chunks;  // d data then p parity
+    bool is_ideal() const {
+        for (auto c : chunks)
+            if (c != LocationIntegrity::Valid && c != LocationIntegrity::Resilvered) return false;
+        return true;
+    }
+    size_t count(LocationIntegrity what) const {
+        size_t n = 0;
+        for (auto c : chunks) n += c == what;
+        return n;
+    }
+};
+
+// file::FilePart.
+struct FilePart {
+    size_t chunksize = 0;
+    std::vector<Chunk> data;
+    std::vector<Chunk> parity;
+
+    size_t len_bytes() const { return chunksize * data.size(); }
+
+    // write_with_encoder (file_part.rs:137-225): L = ceil(length/d); data chunk j =
+    // data_buf[L*j .. L*(j+1)] (data_buf zero padded to d*L, writer.rs:172); parity from
+    // encode_sep; every chunk hashed, in order, and written to `dest` under its hash.
+    static FilePart write_with_encoder(const ReedSolomon& encoder, ChunkStore& dest,
+                                       const Bytes& data_buf, size_t length) {
+        const size_t d = encoder.data_shard_count(), p = encoder.parity_shard_count();
+        if (length > data_buf.size()) throw std::invalid_argument("length > data_buf.len()");
+        const size_t L = (length + d - 1) / d;
+        if (data_buf.size() < d * L) throw std::invalid_argument("data_buf shorter than d*L");
+        Bytes parity(p * L);
+        std::vector<uint8_t> digests(32 * (d + p));
+        size_t chunksize = 0;
+        detail::check(cec_part_encode(encoder.raw(), data_buf.data(), length, parity.data(),
+                                      digests.data(), &chunksize));
+        FilePart part;
+        part.chunksize = chunksize;
+        for (size_t i = 0; i < d + p; ++i) {
+            std::array<uint8_t, 32> h{};
+            std::memcpy(h.data(), &digests[32 * i], 32);
+            const Chunk c{Sha256Hash(h)};
+            const uint8_t* src = i < d ? &data_buf[i * L] : &parity[(i - d) * L];
+            dest.write_shard(c.hash, Bytes(src, src + L));
+            (i < d ? part.data : part.parity).push_back(c);
+        }
+        return part;
+    }
+
+    // read_with_context (file_part.rs:73-135): read the chunks, keep those whose hash
+    // verifies, rebuild missing data with reconstruct_data (TooFewShardsPresent when fewer than
+    // d verify) and return the d data chunks concatenated (len_bytes() bytes).  The reference
+    // samples d random chunks; any d verified chunks decode to the same bytes.
+    Bytes read_with_context(const ChunkStore& src) const {
+        const ReedSolomon r(data.size(), parity.size());
+        Shards all = load_verified(src, nullptr);
+        bool complete = true;
+        for (size_t i = 0; i < data.size(); ++i) complete = complete && all[i].has_value();
+        if (!complete) r.reconstruct_data(all);
+        Bytes out;
+        out.reserve(len_bytes());
+        for (size_t i = 0; i < data.size(); ++i) out.insert(out.end(), all[i]->begin(), all[i]->end());
+        return out;
+    }
+
+    // verify (file_part.rs:228-251): every chunk read and checked against its hash.
+    PartReport verify(const ChunkStore& src) const {
+        PartReport rep;
+        load_verified(src, &rep);
+        return rep;
+    }
+
+    // resilver (file_part.rs:253-390): verify, reconstruct every missing/invalid chunk (data
+    // and parity) and write it back under its hash.  Rebuilt chunks report Resilvered.
+    PartReport resilver(ChunkStore& dest) const {
+        PartReport rep;
+        Shards all = load_verified(dest, &rep);
+        bool any_missing = false;
+        for (const auto& s : all) any_missing = any_missing || !s;
+        if (!any_missing) return rep;
+        const ReedSolomon r(data.size(), parity.size());
+        r.reconstruct(all);
+        for (size_t i = 0; i < all.size(); ++i) {
+            if (rep.chunks[i] == LocationIntegrity::Valid) continue;
+            dest.write_shard(chunk(i).hash, *all[i]);
+            rep.chunks[i] = LocationIntegrity::Resilvered;
+        }
+        return rep;
+    }
+
+    const Chunk& chunk(size_t i) const { return i < data.size() ? data[i] : parity[i - data.size()]; }
+
+   private:
+    Shards load_verified(const ChunkStore& src, PartReport* rep) const {
+        const size_t t = data.size() + parity.size();
+        Shards all(t);
+        std::vector<const Bytes*> loaded;
+        std::vector<size_t> idx;
+        for (size_t i = 0; i < t; ++i) {
+            all[i] = src.read(chunk(i).hash);
+            if (all[i]) {
+                loaded.push_back(&*all[i]);
+                idx.push_back(i);
+            }
+        }
+        if (rep) rep->chunks.assign(t, LocationIntegrity::Unavailable);
+        const std::vector<Sha256Hash> got = Sha256Hash::from_bufs(loaded);  // one launch
+        for (size_t k = 0; k < idx.size(); ++k) {
+            const bool ok = got[k] == chunk(idx[k]).hash;
+            if (rep) rep->chunks[idx[k]] = ok ? LocationIntegrity::Valid : LocationIntegrity::Invalid;
+            if (!ok) all[idx[k]].reset();
+        }
+        return all;
+    }
+};
+
+// file::FileReference: total length + parts (the metadata document).
+struct FileReference {
+    std::optional<uint64_t> length;
+    std::vector<FilePart> parts;
+
+    // FileReference::read: every part's data, truncated to `length` (file_reference.rs:49-56).
+    Bytes read(const ChunkStore& src) const {
+        Bytes out;
+        for (const auto& part : parts) {
+            Bytes b = part.read_with_context(src);
+            out.insert(out.end(), b.begin(), b.end());
+        }
+        if (length && out.size() > *length) out.resize(size_t(*length));
+        return out;
+    }
+    std::vector<PartReport> verify(const ChunkStore& src) const {
+        std::vector<PartReport> r;
+        for (const auto& part : parts) r.push_back(part.verify(src));
+        return r;
+    }
+    std::vector<PartReport> resilver(ChunkStore& dest) const {
+        std::vector<PartReport> r;
+        for (const auto& part : parts) r.push_back(part.resilver(dest));
+        return r;
+    }
+};
+
+// file::FileWriteBuilder (writer.rs:88-255): the part loop of write().  Parts are
+// d*chunk_size bytes of the input (the last one shorter), each zero padded and handed to
+// FilePart::write_with_encoder with one shared codec.
+class FileWriteBuilder {
+   public:
+    FileWriteBuilder& chunk_size(size_t n) {
+        chunk_size_ = n;
+        return *this;
+    }
+    FileWriteBuilder& data_chunks(size_t n) {
+        data_ = n;
+        return *this;
+    }
+    FileWriteBuilder& parity_chunks(size_t n) {
+        parity_ = n;
+        return *this;
+    }
+
+    FileReference write(const uint8_t* bytes, size_t n, ChunkStore& dest) const {
+        const ReedSolomon encoder(data_, parity_);  // writer.rs:131
+        FileReference file;
+        const size_t part_cap = data_ * chunk_size_;
+        for (size_t off = 0; off < n; off += part_cap) {
+            const size_t bytes_read = std::min(part_cap, n - off);
+            Bytes data_buf(part_cap, 0);  // vec![0; data * chunk_size] (writer.rs:172)
+            std::memcpy(data_buf.data(), bytes + off, bytes_read);
+            file.parts.push_back(FilePart::write_with_encoder(encoder, dest, data_buf, bytes_read));
+        }
+        file.length = n;
+        return file;
+    }
+    FileReference write(const Bytes& b, ChunkStore& dest) const { return write(b.data(), b.size(), dest); }
+
+   private:
+    size_t chunk_size_ = size_t(1) << 20;
+    size_t data_ = 3;
+    size_t parity_ = 2;
+};
+
+}  // namespace chunky_ec
+
+#endif  // CHUNKY_EC_HPP

@@ -1,0 +1,288 @@
+// reference_mirror_test.cpp — the reference's own tests for this path, restated against the C++
+// host layer (include/chunky_ec.hpp) so they read like the Rust originals:
+//
+//   sha256                      tests/hash.rs:10-16        Hello World KAT, Display, verify
+//   test_file_write             tests/file.rs:26-56        zeros (2^23 + 7 B), d,p in 1..3:
+//                                                          part count and length
+//   test_resilver               tests/cluster.rs:145-190   tests/cluster.rs generator (d=3, p=2,
+//                                                          2^10-byte chunks): delete 1 data + 1
+//                                                          parity chunk per part, verify, resilver,
+//                                                          verify ideal, read back bit-exact
+//   test_cluster_digests        golden fixture of the same write (tests/golden, pinned oracle)
+//   test_one_encode             JavaReedSolomon testOneEncode RS(5,5) (crate KAT)
+//   test_matrix_rows            SURVEY.md Appendix A RS(3,2) / RS(10,4) parity rows
+//   test_errors                 reed_solomon_erasure::Error variants of ReedSolomon::new,
+//                               encode_sep and reconstruct argument checks
+//   test_reconstruct_every_pattern  every 1..p erasure set of RS(4,3), data+parity
+//
+// Runs on a GPU (every computation goes through libchunky_ec.so).  `--list` prints the test
+// names without touching the GPU.  Exit status 0 iff every test passed.
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "chunky_ec.hpp"
+
+namespace {
+
+using namespace chunky_ec;
+
+#include "golden_cluster.inc"
+
+int g_failures = 0;
+
+#define CHECK(cond)                                                                   \
+    do {                                                                              \
+        if (!(cond)) {                                                                \
+            std::fprintf(stderr, "  CHECK failed %s:%d: %s\n", __FILE__, __LINE__, #cond); \
+            ++g_failures;                                                             \
+            return;                                                                   \
+        }                                                                             \
+    } while (0)
+
+template <typename F>
+bool throws_erasure(F&& f, Error want) {
+    try {
+        f();
+    } catch (const ErasureError& e) {
+        return e.error() == want;
+    }
+    return false;
+}
+
+// tests/cluster.rs:95-102: 80 blocks of 256 bytes, byte x of block i = (x % 128) + i.
+Bytes cluster_reader_bytes() {
+    Bytes b;
+    for (int i = 0; i < 80; ++i)
+        for (int x = 0; x < 256; ++x) b.push_back(uint8_t((x % 128) + i));
+    return b;
+}
+
+// tests/hash.rs
+void sha256() {
+    const std::string payload = "Hello World";
+    const Sha256Hash hash = Sha256Hash::from_buf(payload);
+    CHECK(hash.to_string() == "a591a6d40bf420404a011733cfb7b190d62c65bf0bcda32b57b277d9ad9f146e");
+    CHECK(hash.verify(payload));
+    CHECK(!hash.verify(std::string("Hello World!")));
+    CHECK(Sha256Hash::from_str(hash.to_string()) == hash);
+}
+
+// tests/file.rs:26-56
+void test_file_write() {
+    const size_t length = (size_t(1) << 23) + 7;  // not divisible by d+p
+    const size_t chunk_size = size_t(1) << 20;
+    const Bytes zeros(length, 0);
+    const std::string zero_mib = "30e14955ebf1352266dc2ff8067e68104607e750abb9d3b36582b8af909fcb58";
+    for (size_t data = 1; data <= 3; ++data) {
+        for (size_t parity = 1; parity <= 3; ++parity) {
+            ChunkStore store;
+            const FileReference file_ref =
+                FileWriteBuilder().chunk_size(chunk_size).data_chunks(data).parity_chunks(parity).write(
+                    zeros, store);
+            CHECK(file_ref.length && *file_ref.length == length);
+            const size_t part_size = chunk_size * data;
+            CHECK(file_ref.parts.size() == (length + part_size - 1) / part_size);
+            // full parts: every chunk (data and parity of zeros) is 1 MiB of zeros
+            CHECK(file_ref.parts.front().data[0].hash.to_string() == zero_mib);
+            CHECK(file_ref.parts.front().parity.back().hash.to_string() == zero_mib);
+            CHECK(file_ref.read(store) == zeros);
+        }
+    }
+}
+
+// tests/cluster.rs:145-190 (test_resilver)
+void test_resilver() {
+    ChunkStore store;
+    const Bytes input = cluster_reader_bytes();
+    const FileReference file_ref =
+        FileWriteBuilder().chunk_size(size_t(1) << 10).data_chunks(3).parity_chunks(2).write(input, store);
+    // File should be 100% valid
+    for (const auto& r : file_ref.verify(store)) CHECK(r.is_ideal());
+    size_t deleted_chunks = 0;
+    for (const auto& part : file_ref.parts) {
+        CHECK(store.erase(part.data.front().hash));    // delete 1 / 3 data chunks
+        CHECK(!store.read(part.data.front().hash));
+        CHECK(store.erase(part.parity.front().hash));  // delete 1 / 2 parity chunks
+        CHECK(!store.read(part.parity.front().hash));
+        deleted_chunks += 2;
+    }
+    // File should not be 100% valid, but still available
+    size_t unavailable = 0;
+    for (const auto& r : file_ref.verify(store)) {
+        CHECK(!r.is_ideal());
+        unavailable += r.count(LocationIntegrity::Unavailable);
+    }
+    CHECK(unavailable == deleted_chunks);
+    CHECK(file_ref.read(store) == input);  // reads decode around the holes
+    size_t resilvered = 0;
+    for (const auto& r : file_ref.resilver(store)) {
+        CHECK(r.is_ideal());
+        resilvered += r.count(LocationIntegrity::Resilvered);
+    }
+    CHECK(resilvered == deleted_chunks);
+    for (const auto& r : file_ref.verify(store)) CHECK(r.is_ideal());
+    CHECK(file_ref.read(store) == input);
+    // a corrupted chunk is not trusted: it verifies Invalid and is rebuilt by resilver
+    const Sha256Hash& victim = file_ref.parts[2].data[1].hash;
+    CHECK(store.corrupt(victim, 17));
+    CHECK(file_ref.parts[2].verify(store).count(LocationIntegrity::Invalid) == 1);
+    CHECK(file_ref.read(store) == input);
+    CHECK(file_ref.parts[2].resilver(store).count(LocationIntegrity::Resilvered) == 1);
+    CHECK(file_ref.parts[2].verify(store).is_ideal());
+}
+
+// Golden digests of the tests/cluster.rs write (tests/golden/golden_vectors.json "cluster").
+void test_cluster_digests() {
+    ChunkStore store;
+    const Bytes input = cluster_reader_bytes();
+    CHECK(input.size() == kClusterTotal);
+    CHECK(Sha256Hash::from_buf(input).to_string() == kClusterDataSha256);
+    const FileReference file_ref = FileWriteBuilder()
+                                       .chunk_size(kClusterChunk)
+                                       .data_chunks(kClusterD)
+                                       .parity_chunks(kClusterP)
+                                       .write(input, store);
+    const size_t n = sizeof(kClusterParts) / sizeof(kClusterParts[0]);
+    CHECK(file_ref.parts.size() == n);
+    for (size_t k = 0; k < n; ++k) {
+        const FilePart& part = file_ref.parts[k];
+        CHECK(part.chunksize == kClusterParts[k].chunksize);
+        for (size_t i = 0; i < kClusterD + kClusterP; ++i)
+            CHECK(part.chunk(i).hash.to_string() == kClusterParts[k].sha256[i]);
+    }
+}
+
+// JavaReedSolomon testOneEncode / reed-solomon-erasure test_encoding (RS(5,5)).
+void test_one_encode() {
+    const ReedSolomon rs(5, 5);
+    const std::vector<Bytes> data = {{0, 1}, {4, 5}, {2, 3}, {6, 7}, {8, 9}};
+    std::vector<Bytes> parity(5, Bytes(2, 0xEE));
+    rs.encode_sep(data, parity);
+    const std::vector<Bytes> want = {{12, 13}, {10, 11}, {14, 15}, {90, 91}, {94, 95}};
+    CHECK(parity == want);
+}
+
+// M = V * inv(V[0..d]) over GF(2^8)/0x11D, parity rows.
+void test_matrix_rows() {
+    const auto m32 = ReedSolomon(3, 2).matrix();
+    CHECK((m32[3] == Bytes{1, 1, 1}));
+    CHECK((m32[4] == Bytes{15, 8, 6}));
+    const auto m = ReedSolomon(10, 4).matrix();
+    CHECK((m[10] == Bytes{129, 150, 175, 184, 210, 196, 254, 232, 3, 2}));
+    CHECK((m[11] == Bytes{150, 129, 184, 175, 196, 210, 232, 254, 2, 3}));
+    CHECK((m[12] == Bytes{191, 214, 98, 10, 6, 111, 223, 183, 5, 4}));
+    CHECK((m[13] == Bytes{214, 191, 10, 98, 111, 6, 183, 223, 4, 5}));
+    for (size_t r = 0; r < 10; ++r)
+        for (size_t c = 0; c < 10; ++c) CHECK(m[r][c] == (r == c ? 1 : 0));
+}
+
+void test_errors() {
+    CHECK(throws_erasure([] { ReedSolomon(0, 1); }, Error::TooFewDataShards));
+    CHECK(throws_erasure([] { ReedSolomon(1, 0); }, Error::TooFewParityShards));
+    CHECK(throws_erasure([] { ReedSolomon(200, 57); }, Error::TooManyShards));
+    const ReedSolomon rs(3, 2);
+    CHECK(throws_erasure(
+        [&] {
+            std::vector<Bytes> parity(2, Bytes(4));
+            rs.encode_sep(std::vector<Bytes>(2, Bytes(4)), parity);
+        },
+        Error::TooFewDataShards));
+    CHECK(throws_erasure(
+        [&] {
+            std::vector<Bytes> parity(2, Bytes(4));
+            rs.encode_sep(std::vector<Bytes>{Bytes(4), Bytes(4), Bytes(5)}, parity);
+        },
+        Error::IncorrectShardSize));
+    CHECK(throws_erasure(
+        [&] {
+            std::vector<Bytes> parity(2, Bytes(0));
+            rs.encode_sep(std::vector<Bytes>(3, Bytes(0)), parity);
+        },
+        Error::EmptyShard));
+    CHECK(throws_erasure(
+        [&] {
+            Shards s = {Bytes(8, 1), std::nullopt, std::nullopt, std::nullopt, Bytes(8, 2)};
+            rs.reconstruct(s);
+        },
+        Error::TooFewShardsPresent));
+    // FilePart::read_with_context with fewer than d verifiable chunks
+    ChunkStore store;
+    const FileReference f = FileWriteBuilder().chunk_size(1024).data_chunks(3).parity_chunks(2).write(
+        Bytes(3000, 7), store);
+    for (size_t i = 0; i < 3; ++i) store.erase(f.parts[0].chunk(i).hash);
+    CHECK(throws_erasure([&] { f.read(store); }, Error::TooFewShardsPresent));
+}
+
+void test_reconstruct_every_pattern() {
+    const size_t d = 4, p = 3, t = d + p, L = 1000 + 3;
+    const ReedSolomon rs(d, p);
+    std::vector<Bytes> data(d, Bytes(L));
+    for (size_t j = 0; j < d; ++j)
+        for (size_t x = 0; x < L; ++x) data[j][x] = uint8_t(x * 31 + j * 7 + (x >> 5));
+    std::vector<Bytes> parity(p, Bytes(L));
+    rs.encode_sep(data, parity);
+    std::vector<Bytes> full = data;
+    full.insert(full.end(), parity.begin(), parity.end());
+    for (uint32_t mask = 1; mask < (1u << t); ++mask) {
+        if (size_t(__builtin_popcount(mask)) > p) continue;
+        for (int data_only = 0; data_only < 2; ++data_only) {
+            Shards s(t);
+            for (size_t i = 0; i < t; ++i)
+                if (!(mask >> i & 1)) s[i] = full[i];
+            if (data_only) rs.reconstruct_data(s);
+            else rs.reconstruct(s);
+            for (size_t i = 0; i < t; ++i) {
+                if (data_only && i >= d && (mask >> i & 1)) {
+                    CHECK(!s[i]);  // reconstruct_data leaves missing parity None
+                } else {
+                    CHECK(s[i] && *s[i] == full[i]);
+                }
+            }
+        }
+    }
+}
+
+struct Test {
+    const char* name;
+    void (*fn)();
+};
+
+const Test kTests[] = {
+    {"sha256", sha256},
+    {"test_file_write", test_file_write},
+    {"test_resilver", test_resilver},
+    {"test_cluster_digests", test_cluster_digests},
+    {"test_one_encode", test_one_encode},
+    {"test_matrix_rows", test_matrix_rows},
+    {"test_errors", test_errors},
+    {"test_reconstruct_every_pattern", test_reconstruct_every_pattern},
+};
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    if (argc > 1 && std::strcmp(argv[1], "--list") == 0) {
+        for (const Test& t : kTests) std::printf("%s\n", t.name);
+        return 0;
+    }
+    int failed_tests = 0;
+    for (const Test& t : kTests) {
+        if (argc > 1 && std::strcmp(argv[1], t.name) != 0) continue;
+        const int before = g_failures;
+        try {
+            t.fn();
+        } catch (const std::exception& e) {
+            std::fprintf(stderr, "  exception: %s\n", e.what());
+            ++g_failures;
+        }
+        const bool ok = g_failures == before;
+        failed_tests += ok ? 0 : 1;
+        std::printf("%s ... %s\n", t.name, ok ? "ok" : "FAILED");
+        std::fflush(stdout);
+    }
+    std::printf("%s\n", failed_tests ? "FAILED" : "all passed");
+    return failed_tests ? 1 : 0;
+}
