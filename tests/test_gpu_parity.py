@@ -304,6 +304,7 @@ def _device_parts(n_parts, t, L, cstride=None, seed=1):
     (3, 2, 683, 683),              # odd stride: unaligned path (reference's packed slices)
     (20, 8, 4096, None),
     (6, 10, 1000, 1008),           # > 8 output rows: two row groups
+    (10, 4, 20512, None),          # aligned, last step partial: 2-column + single-column tails
 ])
 def test_encode_hash_batch_vs_oracle(d, p, L, cstride):
     n_parts, t = 24, d + p
@@ -342,7 +343,9 @@ def test_sha256_batch_subrange():
 
 
 @pytest.mark.parametrize("data_only", [False, True])
-@pytest.mark.parametrize("d,p,L", [(10, 4, 16384), (3, 2, 683), (20, 8, 4096 + 5)])
+@pytest.mark.parametrize("d,p,L", [(10, 4, 16384), (3, 2, 683), (20, 8, 4096 + 5),
+                                   (10, 4, 12368),   # partial last 8 KiB step (2-column path)
+                                   (6, 10, 1024)])   # up to 10 rows: shared + row-group launches
 def test_reconstruct_batch_random_patterns(d, p, L, data_only):
     n_parts, t = 96, d + p
     buf, batch = _device_parts(n_parts, t, L, None, seed=L + d)
