@@ -9,6 +9,8 @@
 //                                                          parity chunk per part, verify, resilver,
 //                                                          verify ideal, read back bit-exact
 //   test_cluster_digests        golden fixture of the same write (tests/golden, pinned oracle)
+//   test_cp_50mib               BASELINE configs[0]: `cp` of a 50 MiB file, d=3 p=2, 1 MiB
+//                               chunks: 17 parts, last chunksize 699 051, read back bit-exact
 //   test_one_encode             JavaReedSolomon testOneEncode RS(5,5) (crate KAT)
 //   test_matrix_rows            SURVEY.md Appendix A RS(3,2) / RS(10,4) parity rows
 //   test_errors                 reed_solomon_erasure::Error variants of ReedSolomon::new,
@@ -155,6 +157,37 @@ void test_cluster_digests() {
     }
 }
 
+// BASELINE.json configs[0] (`chunky-bits cp` of 50 MiB into a d=3, p=2, 1 MiB-chunk cluster),
+// compute part: 16 full parts + one of 2 MiB (L = ceil(2 MiB / 3) = 699 051), every chunk
+// stored under its digest, the file read back bit-exact after losing 2 chunks per part.
+void test_cp_50mib() {
+    const size_t length = size_t(50) << 20;
+    Bytes input(length);
+    uint64_t z = 0x9E3779B97F4A7C15ull;
+    for (size_t i = 0; i < length; i += 8) {  // splitmix64 stream
+        z += 0x9E3779B97F4A7C15ull;
+        uint64_t v = z;
+        v = (v ^ (v >> 30)) * 0xBF58476D1CE4E5B9ull;
+        v = (v ^ (v >> 27)) * 0x94D049BB133111EBull;
+        v ^= v >> 31;
+        std::memcpy(&input[i], &v, std::min<size_t>(8, length - i));
+    }
+    ChunkStore store;
+    const FileReference f =
+        FileWriteBuilder().chunk_size(size_t(1) << 20).data_chunks(3).parity_chunks(2).write(input, store);
+    CHECK(f.parts.size() == 17);
+    CHECK(f.parts[0].chunksize == (size_t(1) << 20));
+    CHECK(f.parts[16].chunksize == 699051);
+    CHECK(store.size() == 17 * 5);
+    CHECK(Sha256Hash::from_buf(&input[0], size_t(1) << 20) == f.parts[0].data[0].hash);
+    CHECK(Sha256Hash::from_buf(&input[size_t(48) << 20], 699051) == f.parts[16].data[0].hash);
+    for (const auto& part : f.parts) {
+        store.erase(part.data[2].hash);
+        store.erase(part.parity[1].hash);
+    }
+    CHECK(f.read(store) == input);
+}
+
 // JavaReedSolomon testOneEncode / reed-solomon-erasure test_encoding (RS(5,5)).
 void test_one_encode() {
     const ReedSolomon rs(5, 5);
@@ -255,6 +288,7 @@ const Test kTests[] = {
     {"test_file_write", test_file_write},
     {"test_resilver", test_resilver},
     {"test_cluster_digests", test_cluster_digests},
+    {"test_cp_50mib", test_cp_50mib},
     {"test_one_encode", test_one_encode},
     {"test_matrix_rows", test_matrix_rows},
     {"test_errors", test_errors},
