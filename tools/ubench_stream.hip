@@ -63,6 +63,84 @@ __global__ void stream_kernel(uint8_t* base, uint32_t tiles_per_part) {
     }
 }
 
+// Read-only (14 streams) / write-only (14 streams) ceilings of the same layout.
+template <bool NT>
+__global__ void read_kernel(const uint8_t* base, uint32_t tiles_per_part, uint32_t* sink) {
+    const uint32_t part = blockIdx.x / tiles_per_part;
+    const uint32_t tile = blockIdx.x - part * tiles_per_part;
+    const uint8_t* pb = base + size_t(part) * T * L;
+    const size_t x = size_t(tile) * blockDim.x * 32 + size_t(threadIdx.x) * 16;
+    v4u acc = {0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < T; ++j) {
+        acc ^= ld<NT>(pb + j * L + x);
+        acc ^= ld<NT>(pb + j * L + x + blockDim.x * 16);
+    }
+    if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) sink[0] = 1;
+}
+
+template <bool NT>
+__global__ void write_kernel(uint8_t* base, uint32_t tiles_per_part) {
+    const uint32_t part = blockIdx.x / tiles_per_part;
+    const uint32_t tile = blockIdx.x - part * tiles_per_part;
+    uint8_t* pb = base + size_t(part) * T * L;
+    const size_t x = size_t(tile) * blockDim.x * 32 + size_t(threadIdx.x) * 16;
+    const v4u v = {part, tile, threadIdx.x, 7u};
+#pragma unroll
+    for (int j = 0; j < T; ++j) {
+        st<NT>(pb + j * L + x, v);
+        st<NT>(pb + j * L + x + blockDim.x * 16, v);
+    }
+}
+
+// Persistent: one workgroup per CU slot walks whole parts (grid-stride over 8 KiB steps).
+template <bool NT>
+__global__ void persistent_kernel(uint8_t* base, uint32_t parts) {
+    const size_t steps_per_part = L / (size_t(blockDim.x) * 32);
+    const size_t total = size_t(parts) * steps_per_part;
+    for (size_t s = blockIdx.x; s < total; s += gridDim.x) {
+        const size_t part = s / steps_per_part, step = s - part * steps_per_part;
+        uint8_t* pb = base + part * T * L;
+        const size_t x = step * blockDim.x * 32 + size_t(threadIdx.x) * 16;
+        v4u acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
+        v4u in0[D], in1[D];
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            in0[j] = ld<NT>(pb + j * L + x);
+            in1[j] = ld<NT>(pb + j * L + x + blockDim.x * 16);
+        }
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            acc0 ^= in0[j];
+            acc1 ^= in1[j];
+        }
+#pragma unroll
+        for (int r = 0; r < P; ++r) {
+            st<NT>(pb + (D + r) * L + x, acc0);
+            st<NT>(pb + (D + r) * L + x + blockDim.x * 16, acc1);
+        }
+    }
+}
+
+template <typename K>
+void run_simple(const char* name, K launch, double bytes) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    float best = 1e30f;
+    for (int r = 0; r < 6; ++r) {
+        CK(hipEventRecord(a));
+        launch();
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        float ms;
+        CK(hipEventElapsedTime(&ms, a, b));
+        if (r && ms < best) best = ms;
+    }
+    printf("%-40s : %8.3f ms  %7.0f GB/s\n", name, best, bytes / best / 1e6);
+    fflush(stdout);
+}
+
 template <int V, int ITERS, bool NT>
 void run(uint8_t* base, uint32_t parts, int threads, const char* name) {
     const size_t per_block = size_t(threads) * 16 * V * ITERS;
@@ -104,6 +182,27 @@ int main(int argc, char** argv) {
     run<2, 2, false>(base, parts, 512, "v2 it2 t512");
     run<1, 4, false>(base, parts, 1024, "v1 it4 t1024");
     run<2, 2, true>(base, parts, 256, "v2 it2 nt");
+    run<2, 1, true>(base, parts, 256, "v2 it1 nt");
+    run<4, 1, true>(base, parts, 256, "v4 it1 nt");
+    run<2, 2, true>(base, parts, 512, "v2 it2 nt t512");
+    const double all = double(parts) * T * L;
+    const uint32_t tiles = uint32_t(L / (256 * 32));
+    uint32_t* sink;
+    CK(hipMalloc(&sink, 64));
+    run_simple("read-only 14 streams", [&] {
+        hipLaunchKernelGGL((read_kernel<false>), dim3(parts * tiles), dim3(256), 0, 0, base, tiles, sink); }, all);
+    run_simple("read-only 14 streams nt", [&] {
+        hipLaunchKernelGGL((read_kernel<true>), dim3(parts * tiles), dim3(256), 0, 0, base, tiles, sink); }, all);
+    run_simple("write-only 14 streams", [&] {
+        hipLaunchKernelGGL((write_kernel<false>), dim3(parts * tiles), dim3(256), 0, 0, base, tiles); }, all);
+    run_simple("write-only 14 streams nt", [&] {
+        hipLaunchKernelGGL((write_kernel<true>), dim3(parts * tiles), dim3(256), 0, 0, base, tiles); }, all);
+    for (int wg : {1024, 2048, 4096, 8192}) {
+        char name[64];
+        snprintf(name, sizeof name, "persistent nt grid %d", wg);
+        run_simple(name, [&] {
+            hipLaunchKernelGGL((persistent_kernel<true>), dim3(wg), dim3(256), 0, 0, base, parts); }, all);
+    }
     CK(hipFree(base));
     return 0;
 }
