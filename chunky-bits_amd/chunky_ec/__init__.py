@@ -78,6 +78,8 @@ _sig("cec_reconstruct_data", [_vp, ctypes.POINTER(_u8p), _szp, _u8p, ctypes.c_si
 _sig("cec_sha256", [_u8p, ctypes.c_size_t, _u8p])
 _sig("cec_sha256_many", [ctypes.POINTER(_u8p), _szp, ctypes.c_size_t, _u8p])
 _sig("cec_part_encode", [_vp, _u8p, ctypes.c_size_t, _u8p, _u8p, _szp])
+_sig("cec_coalesce_stats", [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)],
+     None)
 _sig("cec_encode_batch", [_vp, ctypes.POINTER(PartBatchStruct), _vp])
 _sig("cec_encode_hash_batch", [_vp, ctypes.POINTER(PartBatchStruct), _vp, _vp])
 _sig("cec_sha256_batch", [ctypes.POINTER(PartBatchStruct), ctypes.c_size_t, ctypes.c_size_t,
@@ -446,6 +448,13 @@ def resilver_batch(codec: ReedSolomon, batch: PartBatch, present, expected_ptr: 
 def fill_synthetic(batch: PartBatch, n_chunks: int, seed: int, stream=None) -> None:
     s = batch.struct()
     _check(_lib.cec_fill_synthetic(ctypes.byref(s), n_chunks, seed, _stream_ptr(stream)))
+
+
+def coalesce_stats():
+    """(calls, launches) made through the per-call coalescing path (cec_coalesce_stats)."""
+    calls, launches = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    _lib.cec_coalesce_stats(ctypes.byref(calls), ctypes.byref(launches))
+    return calls.value, launches.value
 
 
 def synth_byte(seed: int, part: int, chunk: int, offset: int) -> int:

@@ -10,6 +10,9 @@
 #include <algorithm>
 #include <cstdlib>
 #include <array>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstring>
 #include <deque>
 #include <map>
@@ -111,10 +114,8 @@ struct ThreadCtx {
 };
 thread_local std::unordered_map<int, ThreadCtx> t_ctx;
 
-int thread_ctx(ThreadCtx** out, size_t device_bytes) {
-    int dev = 0;
-    CEC_TRY(current_device(&dev));
-    ThreadCtx& c = t_ctx[dev];
+// Stream + device staging of at least device_bytes (grown, never shrunk).
+int ctx_reserve(ThreadCtx& c, size_t device_bytes) {
     if (!c.stream) HIP_TRY(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
     if (c.dcap < device_bytes) {
         if (c.dbuf) HIP_TRY(hipFree(c.dbuf));
@@ -124,6 +125,14 @@ int thread_ctx(ThreadCtx** out, size_t device_bytes) {
         HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c.dbuf), cap));
         c.dcap = cap;
     }
+    return CEC_OK;
+}
+
+int thread_ctx(ThreadCtx** out, size_t device_bytes) {
+    int dev = 0;
+    CEC_TRY(current_device(&dev));
+    ThreadCtx& c = t_ctx[dev];
+    CEC_TRY(ctx_reserve(c, device_bytes));
     *out = &c;
     return CEC_OK;
 }
@@ -309,6 +318,286 @@ int reconstruct_host(const cec_codec* cc, uint8_t* const* shards, const size_t* 
     return CEC_OK;
 }
 
+// ------------------------------------------------------------------------------------------
+// Per-call coalescing ("a batch queue behind the per-part call").
+//
+// A GPU SHA-256 lane hashes one chunk as a serial chain (~42 ms per MiB), so one part per
+// launch leaves the chip idle and the reference's own concurrency (≤10 part tasks,
+// writer.rs:130; `concurrency` is a builder knob) only helps if concurrent calls share a
+// launch.  cec_part_encode / cec_sha256(_many) therefore go through a leader/follower queue:
+// the first caller to find no batch in progress becomes the leader, waits up to
+// CEC_COALESCE_US microseconds (default 200; 0 = off) for more requests, and runs every queued
+// request with its key (codec, chunk length, device) as ONE batch on a queue-owned stream and
+// staging buffer; the others sleep until their results are in their own buffers.  Results are
+// bit-identical to the one-at-a-time path (same kernels, same inputs).
+// ------------------------------------------------------------------------------------------
+std::atomic<uint64_t> g_calls{0}, g_launches{0};
+
+uint32_t coalesce_window_us() {
+    static const uint32_t us = [] {
+        const char* e = std::getenv("CEC_COALESCE_US");
+        return e ? uint32_t(std::strtoul(e, nullptr, 10)) : 200u;
+    }();
+    return us;
+}
+constexpr size_t kMaxCoalesced = 4096;  // requests per batch
+
+template <typename Req>
+class Coalescer {
+   public:
+    // Runs `run(batch)` for a batch holding r (r may be run by another thread).  run() must set
+    // each request's status / err.
+    template <typename Run>
+    int submit(Req* r, Run&& run) {
+        g_calls.fetch_add(1, std::memory_order_relaxed);
+        std::unique_lock<std::mutex> lk(mu_);
+        queue_.push_back(r);
+        cv_.notify_all();
+        while (!r->done) {
+            if (leader_) {
+                cv_.wait(lk);
+                continue;
+            }
+            leader_ = true;
+            const auto until =
+                std::chrono::steady_clock::now() + std::chrono::microseconds(coalesce_window_us());
+            cv_.wait_until(lk, until, [&] { return queue_.size() >= kMaxCoalesced; });
+            std::vector<Req*> batch;
+            const auto key = queue_.front()->key();
+            for (auto it = queue_.begin(); it != queue_.end() && batch.size() < kMaxCoalesced;) {
+                if ((*it)->key() == key) {
+                    batch.push_back(*it);
+                    it = queue_.erase(it);
+                } else {
+                    ++it;
+                }
+            }
+            lk.unlock();
+            g_launches.fetch_add(1, std::memory_order_relaxed);
+            run(batch, staging_[key.device]);
+            lk.lock();
+            for (Req* b : batch) b->done = true;
+            leader_ = false;
+            cv_.notify_all();
+        }
+        if (r->status != CEC_OK) g_last_error = r->err;
+        return r->status;
+    }
+
+   private:
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<Req*> queue_;
+    bool leader_ = false;
+    std::map<int, ThreadCtx> staging_;  // per device; used by the current leader only
+};
+
+struct CoalesceKey {
+    const void* codec;
+    size_t len;
+    int device;
+    bool operator==(const CoalesceKey& o) const {
+        return codec == o.codec && len == o.len && device == o.device;
+    }
+};
+
+struct ShaReq {
+    const uint8_t* const* bufs;
+    const size_t* lens;
+    size_t n;
+    uint8_t* out;
+    int device;
+    int status = CEC_OK;
+    std::string err;
+    bool done = false;
+    CoalesceKey key() const { return {nullptr, 0, device}; }
+};
+
+struct PartReq {
+    cec_codec* codec;
+    const uint8_t* data_buf;  // d*L bytes
+    size_t L;
+    uint8_t* parity_out;      // p*L bytes
+    uint8_t* digests_out;     // (d+p)*32 bytes
+    int device;
+    int status = CEC_OK;
+    std::string err;
+    bool done = false;
+    CoalesceKey key() const { return {codec, L, device}; }
+};
+
+Coalescer<ShaReq> g_sha_queue;
+Coalescer<PartReq> g_part_queue;
+
+// SHA-256 of n host buffers in one launch (list mode) on ctx's stream.
+int sha256_many_on(ThreadCtx& ctx, const uint8_t* const* bufs, const size_t* lens, size_t n,
+                   uint8_t* out) {
+    std::vector<size_t> off(n);
+    size_t total = 0;
+    for (size_t i = 0; i < n; ++i) {
+        off[i] = total;
+        total += round_up(std::max<size_t>(lens[i], 1), kChunkAlign);
+    }
+    const size_t meta = round_up(2 * n * sizeof(uint64_t), kChunkAlign);
+    const size_t dig = round_up(n * 32, kChunkAlign);
+    CEC_TRY(ctx_reserve(ctx, meta + dig + total));
+    uint64_t* dptrs = reinterpret_cast<uint64_t*>(ctx.dbuf);
+    uint64_t* dlens = dptrs + n;
+    uint8_t* ddig = ctx.dbuf + meta;
+    uint8_t* ddata = ddig + dig;
+    std::vector<uint64_t> hmeta(2 * n);
+    for (size_t i = 0; i < n; ++i) {
+        hmeta[i] = reinterpret_cast<uint64_t>(ddata + off[i]);
+        hmeta[n + i] = lens[i];
+        if (lens[i])
+            HIP_TRY(hipMemcpyAsync(ddata + off[i], bufs[i], lens[i], hipMemcpyHostToDevice,
+                                   ctx.stream));
+    }
+    HIP_TRY(hipMemcpyAsync(dptrs, hmeta.data(), hmeta.size() * sizeof(uint64_t),
+                           hipMemcpyHostToDevice, ctx.stream));
+    ShaParams a{};
+    a.ptrs = dptrs;
+    a.lens = dlens;
+    a.n_parts = uint32_t(n);
+    a.n_chunks = 1;
+    a.digests = ddig;
+    HIP_TRY(launch_sha256(a, true, ctx.stream));
+    HIP_TRY(hipMemcpyAsync(out, ddig, n * 32, hipMemcpyDeviceToHost, ctx.stream));
+    HIP_TRY(hipStreamSynchronize(ctx.stream));
+    return CEC_OK;
+}
+
+// FilePart::write_with_encoder's compute for B parts of chunk length L in one launch: each
+// part's d*L data_buf is scattered into a [B][d+p][cs] device batch (2-D copy), encoded and
+// hashed (fused kernel when it covers the shape), and parity + digests copied back.
+int part_encode_many_on(ThreadCtx& ctx, cec_codec* c, const std::vector<PartReq*>& reqs) {
+    const size_t d = c->d, p = c->p, t = d + p, B = reqs.size();
+    const size_t L = reqs[0]->L;
+    const size_t cs = round_up(L, kChunkAlign);
+    const size_t dig = round_up(B * t * 32, kChunkAlign);
+    uint32_t* drec = nullptr;
+    CEC_TRY(c->encode_record(&drec));
+    CEC_TRY(ctx_reserve(ctx, dig + B * t * cs));
+    uint8_t* ddig = ctx.dbuf;
+    uint8_t* dbase = ctx.dbuf + dig;
+    for (size_t k = 0; k < B; ++k)
+        HIP_TRY(hipMemcpy2DAsync(dbase + k * t * cs, cs, reqs[k]->data_buf, L, L, d,
+                                 hipMemcpyHostToDevice, ctx.stream));
+    if (fused_covers(uint32_t(d), uint32_t(p), L)) {
+        FusedParams f{};
+        f.base = dbase;
+        f.part_stride = t * cs;
+        f.chunk_stride = cs;
+        f.len = L;
+        f.pat = drec;
+        f.digests = ddig;
+        f.n_parts = uint32_t(B);
+        f.d = uint32_t(d);
+        f.p = uint32_t(p);
+        HIP_TRY(launch_encode_hash(f, true, ctx.stream));
+    } else {
+        ApplyParams a{};
+        a.base = dbase;
+        a.part_stride = t * cs;
+        a.chunk_stride = cs;
+        a.len = L;
+        a.pat = drec;
+        a.n_parts = uint32_t(B);
+        a.d = uint32_t(d);
+        a.n_rows = uint32_t(p);
+        HIP_TRY(launch_rs_apply(a, true, ctx.stream));
+        ShaParams h{};
+        h.base = dbase;
+        h.part_stride = t * cs;
+        h.chunk_stride = cs;
+        h.len = L;
+        h.n_parts = uint32_t(B);
+        h.first_chunk = 0;
+        h.n_chunks = uint32_t(t);
+        h.digests = ddig;
+        HIP_TRY(launch_sha256(h, true, ctx.stream));
+    }
+    for (size_t k = 0; k < B; ++k) {
+        HIP_TRY(hipMemcpy2DAsync(reqs[k]->parity_out, L, dbase + k * t * cs + d * cs, cs, L, p,
+                                 hipMemcpyDeviceToHost, ctx.stream));
+        HIP_TRY(hipMemcpyAsync(reqs[k]->digests_out, ddig + k * t * 32, t * 32,
+                               hipMemcpyDeviceToHost, ctx.stream));
+    }
+    HIP_TRY(hipStreamSynchronize(ctx.stream));
+    return CEC_OK;
+}
+
+template <typename Req>
+void finish_batch(std::vector<Req*>& batch, int st) {
+    for (Req* r : batch) {
+        r->status = st;
+        if (st != CEC_OK) r->err = g_last_error;
+    }
+}
+
+int sha256_coalesced(const uint8_t* const* bufs, const size_t* lens, size_t n, uint8_t* out) {
+    int dev = 0;
+    CEC_TRY(current_device(&dev));
+    if (coalesce_window_us() == 0) {
+        ThreadCtx* ctx = nullptr;
+        CEC_TRY(thread_ctx(&ctx, 0));
+        g_calls.fetch_add(1, std::memory_order_relaxed);
+        g_launches.fetch_add(1, std::memory_order_relaxed);
+        return sha256_many_on(*ctx, bufs, lens, n, out);
+    }
+    ShaReq r;
+    r.bufs = bufs;
+    r.lens = lens;
+    r.n = n;
+    r.out = out;
+    r.device = dev;
+    return g_sha_queue.submit(&r, [](std::vector<ShaReq*>& batch, ThreadCtx& ctx) {
+        std::vector<const uint8_t*> b;
+        std::vector<size_t> l;
+        for (ShaReq* q : batch)
+            for (size_t i = 0; i < q->n; ++i) {
+                b.push_back(q->bufs[i]);
+                l.push_back(q->lens[i]);
+            }
+        std::vector<uint8_t> digests(32 * b.size());
+        const int st = sha256_many_on(ctx, b.data(), l.data(), b.size(), digests.data());
+        size_t at = 0;
+        for (ShaReq* q : batch) {
+            if (st == CEC_OK) std::memcpy(q->out, &digests[32 * at], 32 * q->n);
+            at += q->n;
+        }
+        finish_batch(batch, st);
+    });
+}
+
+int part_encode_coalesced(cec_codec* c, const uint8_t* data_buf, size_t L, uint8_t* parity_out,
+                          uint8_t* digests_out) {
+    int dev = 0;
+    CEC_TRY(current_device(&dev));
+    PartReq r;
+    r.codec = c;
+    r.data_buf = data_buf;
+    r.L = L;
+    r.parity_out = parity_out;
+    r.digests_out = digests_out;
+    r.device = dev;
+    if (coalesce_window_us() == 0) {
+        ThreadCtx* ctx = nullptr;
+        CEC_TRY(thread_ctx(&ctx, 0));
+        g_calls.fetch_add(1, std::memory_order_relaxed);
+        g_launches.fetch_add(1, std::memory_order_relaxed);
+        return part_encode_many_on(*ctx, c, std::vector<PartReq*>{&r});
+    }
+    return g_part_queue.submit(&r, [](std::vector<PartReq*>& batch, ThreadCtx& ctx) {
+        finish_batch(batch, part_encode_many_on(ctx, batch[0]->codec, batch));
+    });
+}
+
+void coalesce_stats(uint64_t* calls, uint64_t* launches) {
+    if (calls) *calls = g_calls.load();
+    if (launches) *launches = g_launches.load();
+}
+
 int batch_ok(const cec_part_batch* b) {
     if (!b || !b->base) return CEC_ERR_INVALID_ARGUMENT;
     return CEC_OK;
@@ -457,41 +746,9 @@ int cec_reconstruct_data(const cec_codec* c, uint8_t* const* shards, const size_
 int cec_sha256_many(const uint8_t* const* bufs, const size_t* lens, size_t n, uint8_t* out) {
     if (n == 0) return CEC_OK;
     if (!bufs || !lens || !out) return CEC_ERR_INVALID_ARGUMENT;
-    std::vector<size_t> off(n);
-    size_t total = 0;
-    for (size_t i = 0; i < n; ++i) {
+    for (size_t i = 0; i < n; ++i)
         if (lens[i] && !bufs[i]) return CEC_ERR_INVALID_ARGUMENT;
-        off[i] = total;
-        total += round_up(std::max<size_t>(lens[i], 1), kChunkAlign);
-    }
-    const size_t meta = round_up(2 * n * sizeof(uint64_t), kChunkAlign);
-    const size_t dig = round_up(n * 32, kChunkAlign);
-    ThreadCtx* ctx = nullptr;
-    CEC_TRY(thread_ctx(&ctx, meta + dig + total));
-    uint64_t* dptrs = reinterpret_cast<uint64_t*>(ctx->dbuf);
-    uint64_t* dlens = dptrs + n;
-    uint8_t* ddig = ctx->dbuf + meta;
-    uint8_t* ddata = ddig + dig;
-    std::vector<uint64_t> hmeta(2 * n);
-    for (size_t i = 0; i < n; ++i) {
-        hmeta[i] = reinterpret_cast<uint64_t>(ddata + off[i]);
-        hmeta[n + i] = lens[i];
-        if (lens[i])
-            HIP_TRY(hipMemcpyAsync(ddata + off[i], bufs[i], lens[i], hipMemcpyHostToDevice,
-                                   ctx->stream));
-    }
-    HIP_TRY(hipMemcpyAsync(dptrs, hmeta.data(), hmeta.size() * sizeof(uint64_t),
-                           hipMemcpyHostToDevice, ctx->stream));
-    ShaParams a{};
-    a.ptrs = dptrs;
-    a.lens = dlens;
-    a.n_parts = uint32_t(n);
-    a.n_chunks = 1;
-    a.digests = ddig;
-    HIP_TRY(launch_sha256(a, true, ctx->stream));
-    HIP_TRY(hipMemcpyAsync(out, ddig, n * 32, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
-    return CEC_OK;
+    return sha256_coalesced(bufs, lens, n, out);
 }
 
 int cec_sha256(const uint8_t* buf, size_t len, uint8_t* out32) {
@@ -501,54 +758,18 @@ int cec_sha256(const uint8_t* buf, size_t len, uint8_t* out32) {
 int cec_part_encode(const cec_codec* cc, const uint8_t* data_buf, size_t length,
                     uint8_t* parity_out, uint8_t* digests_out, size_t* chunksize) {
     if (!cc || !parity_out || !digests_out || !chunksize) return CEC_ERR_INVALID_ARGUMENT;
-    cec_codec* c = const_cast<cec_codec*>(cc);
     if (length == 0) return CEC_EMPTY_SHARD;
     if (!data_buf) return CEC_ERR_INVALID_ARGUMENT;
-    const size_t d = c->d, p = c->p, t = d + p;
-    const size_t L = (length + d - 1) / d;
-    const size_t cs = round_up(L, kChunkAlign);
-    const size_t dig = round_up(t * 32, kChunkAlign);
-    uint32_t* drec = nullptr;
-    CEC_TRY(c->encode_record(&drec));
-    ThreadCtx* ctx = nullptr;
-    CEC_TRY(thread_ctx(&ctx, dig + t * cs));
-    uint8_t* ddig = ctx->dbuf;
-    uint8_t* dbase = ctx->dbuf + dig;
-    for (size_t j = 0; j < d; ++j)
-        HIP_TRY(hipMemcpyAsync(dbase + j * cs, data_buf + j * L, L, hipMemcpyHostToDevice,
-                               ctx->stream));
-    ApplyParams a{};
-    a.base = dbase;
-    a.part_stride = t * cs;
-    a.chunk_stride = cs;
-    a.len = L;
-    a.pat = drec;
-    a.n_parts = 1;
-    a.d = uint32_t(d);
-    a.n_rows = uint32_t(p);
-    HIP_TRY(launch_rs_apply(a, true, ctx->stream));
-    ShaParams h{};
-    h.base = dbase;
-    h.part_stride = t * cs;
-    h.chunk_stride = cs;
-    h.len = L;
-    h.n_parts = 1;
-    h.first_chunk = 0;
-    h.n_chunks = uint32_t(t);
-    h.digests = ddig;
-    HIP_TRY(launch_sha256(h, true, ctx->stream));
-    for (size_t i = 0; i < p; ++i)
-        HIP_TRY(hipMemcpyAsync(parity_out + i * L, dbase + (d + i) * cs, L,
-                               hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(hipMemcpyAsync(digests_out, ddig, t * 32, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    const size_t L = (length + cc->d - 1) / cc->d;
+    CEC_TRY(part_encode_coalesced(const_cast<cec_codec*>(cc), data_buf, L, parity_out,
+                                  digests_out));
     *chunksize = L;
     return CEC_OK;
 }
 
-// ------------------------------------------------------------------------------------------
-// Device-resident batch API
-// ------------------------------------------------------------------------------------------
+void cec_coalesce_stats(uint64_t* calls, uint64_t* launches) {
+    coalesce_stats(calls, launches);
+}
 
 int cec_encode_batch(const cec_codec* cc, const cec_part_batch* b, void* stream) {
     if (!cc) return CEC_ERR_INVALID_ARGUMENT;

@@ -135,6 +135,15 @@ int cec_sha256_many(const uint8_t* const* bufs, const size_t* lens, size_t n, ui
 int cec_part_encode(const cec_codec* codec, const uint8_t* data_buf, size_t length,
                     uint8_t* parity_out, uint8_t* digests_out, size_t* chunksize);
 
+/* Per-call coalescing.  Concurrent cec_part_encode calls with the same codec and chunk length
+ * (and concurrent cec_sha256 / cec_sha256_many calls) on the same device are gathered into one
+ * launch: the first caller waits up to CEC_COALESCE_US microseconds (environment, default 200,
+ * 0 = off) for others, runs the whole batch and wakes them with their results.  A lone GPU
+ * SHA-256 lane hashes ~25 MB/s (a serial chain), so the reference's per-part calls only pay off
+ * when their concurrency becomes batch width.  Results are identical either way.
+ * cec_coalesce_stats: calls made and launches issued through this path since load. */
+void cec_coalesce_stats(uint64_t* calls, uint64_t* launches);
+
 /* ---------------------------------------------------------------------------------------- */
 /* Device-resident batch API (inputs already in HBM; asynchronous on `stream`)              */
 /* ---------------------------------------------------------------------------------------- */

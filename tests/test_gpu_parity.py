@@ -286,6 +286,35 @@ def test_host_api_concurrent_part_tasks_share_one_codec():
         assert sorted(ex.map(task, range(20))) == list(range(20))
 
 
+def test_per_call_coalescing_batches_concurrent_parts_bit_exact():
+    """Concurrent cec_part_encode / cec_sha256 calls (the reference's part tasks) share launches
+    through the coalescing queue; every caller still gets exactly its own part's parity and
+    digests (vs the oracle), including callers with a different chunk length in the mix."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    d, p = 10, 4
+    rs = ce.ReedSolomon(d, p)
+    c0, l0 = ce.coalesce_stats()
+
+    def task(i):
+        length = 10 * 65536 if i % 5 else 10 * 4096 + 3  # two chunk lengths in flight
+        buf = gen_bytes(5000 + i, length).tobytes()
+        enc = ce.part_encode(rs, buf, length)
+        cs, par, dig = oracle.part_encode(d, p, np.frombuffer(buf, np.uint8), length)
+        assert enc.chunksize == cs
+        assert [bytes(x) for x in enc.parity] == [x.tobytes() for x in par]
+        assert [h.digest for h in enc.hashes] == [x.tobytes() for x in dig]
+        msg = gen_bytes(9000 + i, 1000 + 37 * i).tobytes()
+        assert ce.Sha256Hash.from_buf(msg).digest == hashlib.sha256(msg).digest()
+        return i
+
+    with ThreadPoolExecutor(max_workers=48) as ex:
+        assert sorted(ex.map(task, range(96))) == list(range(96))
+    c1, l1 = ce.coalesce_stats()
+    assert c1 - c0 == 2 * 96
+    assert l1 - l0 < c1 - c0  # some calls shared a launch
+
+
 # ----------------------------------------------------------------------------------------------
 # Device-resident batches
 # ----------------------------------------------------------------------------------------------
