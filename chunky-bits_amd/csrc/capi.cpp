@@ -13,6 +13,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdio>
 #include <cstring>
 #include <deque>
 #include <map>
@@ -326,10 +327,16 @@ int reconstruct_host(const cec_codec* cc, uint8_t* const* shards, const size_t* 
 // writer.rs:130; `concurrency` is a builder knob) only helps if concurrent calls share a
 // launch.  cec_part_encode / cec_sha256(_many) therefore go through a leader/follower queue:
 // the first caller to find no batch in progress becomes the leader, waits up to
-// CEC_COALESCE_US microseconds (default 200; 0 = off) for more requests, and runs every queued
-// request with its key (codec, chunk length, device) as ONE batch on a queue-owned stream and
-// staging buffer; the others sleep until their results are in their own buffers.  Results are
-// bit-identical to the one-at-a-time path (same kernels, same inputs).
+// CEC_COALESCE_US microseconds (default 200) for more requests with its key (codec, chunk
+// length, device), and runs them as ONE batch:
+//   1. copy-in   every caller copies its own (pageable) input into the queue's pinned staging,
+//                in parallel on its own thread;
+//   2. launch    the leader moves the whole batch with one H2D copy, runs the fused
+//                encode+hash (or the SHA) kernel over every part, and brings parity and
+//                digests back with one D2H copy into pinned staging;
+//   3. copy-out  every caller copies its results out into its own buffers, in parallel.
+// Batches are capped at CEC_COALESCE_MAX_MIB of input (default 4096).  Results are
+// bit-identical to one call per launch (same kernels, same inputs).
 // ------------------------------------------------------------------------------------------
 std::atomic<uint64_t> g_calls{0}, g_launches{0};
 
@@ -340,56 +347,44 @@ uint32_t coalesce_window_us() {
     }();
     return us;
 }
-constexpr size_t kMaxCoalesced = 4096;  // requests per batch
 
-template <typename Req>
-class Coalescer {
-   public:
-    // Runs `run(batch)` for a batch holding r (r may be run by another thread).  run() must set
-    // each request's status / err.
-    template <typename Run>
-    int submit(Req* r, Run&& run) {
-        g_calls.fetch_add(1, std::memory_order_relaxed);
-        std::unique_lock<std::mutex> lk(mu_);
-        queue_.push_back(r);
-        cv_.notify_all();
-        while (!r->done) {
-            if (leader_) {
-                cv_.wait(lk);
-                continue;
-            }
-            leader_ = true;
-            const auto until =
-                std::chrono::steady_clock::now() + std::chrono::microseconds(coalesce_window_us());
-            cv_.wait_until(lk, until, [&] { return queue_.size() >= kMaxCoalesced; });
-            std::vector<Req*> batch;
-            const auto key = queue_.front()->key();
-            for (auto it = queue_.begin(); it != queue_.end() && batch.size() < kMaxCoalesced;) {
-                if ((*it)->key() == key) {
-                    batch.push_back(*it);
-                    it = queue_.erase(it);
-                } else {
-                    ++it;
-                }
-            }
-            lk.unlock();
-            g_launches.fetch_add(1, std::memory_order_relaxed);
-            run(batch, staging_[key.device]);
-            lk.lock();
-            for (Req* b : batch) b->done = true;
-            leader_ = false;
-            cv_.notify_all();
-        }
-        if (r->status != CEC_OK) g_last_error = r->err;
-        return r->status;
+size_t coalesce_max_bytes() {
+    static const size_t b = [] {
+        const char* e = std::getenv("CEC_COALESCE_MAX_MIB");
+        const size_t mib = e ? size_t(std::strtoull(e, nullptr, 10)) : 4096;
+        return std::max<size_t>(mib, 1) << 20;
+    }();
+    return b;
+}
+
+bool coalesce_trace() {
+    static const bool on = std::getenv("CEC_COALESCE_TRACE") != nullptr;
+    return on;
+}
+
+// Pinned host staging, never shrunk.  Pinning costs ~0.35 s per GiB, so the first growth
+// past 64 MiB goes straight to the batch cap (one pinning per process, not one per size step).
+struct PinnedBuf {
+    uint8_t* ptr = nullptr;
+    size_t cap = 0;
+    int reserve(size_t bytes, size_t cap_hint) {
+        if (cap >= bytes) return CEC_OK;
+        if (ptr) HIP_TRY(hipHostFree(ptr));
+        ptr = nullptr;
+        cap = 0;
+        const size_t want =
+            round_up(bytes <= (size_t(64) << 20) ? std::max(bytes, size_t(64) << 20)
+                                                 : std::max(bytes, cap_hint),
+                     1 << 20);
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ptr), want, hipHostMallocDefault));
+        cap = want;
+        return CEC_OK;
     }
+};
 
-   private:
-    std::mutex mu_;
-    std::condition_variable cv_;
-    std::deque<Req*> queue_;
-    bool leader_ = false;
-    std::map<int, ThreadCtx> staging_;  // per device; used by the current leader only
+struct Arena {
+    ThreadCtx dev;  // stream + device staging
+    PinnedBuf in, out;
 };
 
 struct CoalesceKey {
@@ -401,196 +396,340 @@ struct CoalesceKey {
     }
 };
 
-struct ShaReq {
-    const uint8_t* const* bufs;
-    const size_t* lens;
-    size_t n;
-    uint8_t* out;
-    int device;
+enum class Phase { Queued, CopyIn, Staged, CopyOut, Finished };
+
+struct ReqBase {
+    int device = 0;
     int status = CEC_OK;
     std::string err;
-    bool done = false;
+    Phase phase = Phase::Queued;
+    size_t slot = 0;        // index in the batch
+    size_t in_off = 0;      // byte offset in the pinned input staging
+    size_t item0 = 0;       // sha: first item index; parts: parts in the batch
+    Arena* arena = nullptr;
+    std::condition_variable cv;  // this caller's wake-ups
+};
+
+// Impl: bytes(r) = input bytes; prepare(batch, arena) lays out + reserves; copy_in(r);
+// run(batch, arena) launches and waits; copy_out(r).
+// Wake-ups are targeted (one condition variable per request plus one for the leader) so a
+// batch of hundreds of callers costs O(batch) wake-ups, not O(batch^2).
+template <typename Req, typename Impl>
+class Coalescer {
+   public:
+    int submit(Req* r) {
+        g_calls.fetch_add(1, std::memory_order_relaxed);
+        std::unique_lock<std::mutex> lk(mu_);
+        queue_.push_back(r);
+        if (leader_) leader_cv_.notify_one();  // a gathering leader re-checks its batch size
+        for (;;) {
+            if (r->phase == Phase::CopyIn) {
+                lk.unlock();
+                Impl::copy_in(*r);
+                lk.lock();
+                r->phase = Phase::Staged;
+                if (++staged_ == batch_size_) leader_cv_.notify_one();
+            } else if (r->phase == Phase::CopyOut) {
+                lk.unlock();
+                if (r->status == CEC_OK) Impl::copy_out(*r);
+                lk.lock();
+                r->phase = Phase::Finished;
+                if (++finished_ == batch_size_) leader_cv_.notify_one();
+                break;
+            } else if (r->phase == Phase::Queued && !leader_) {
+                lead(r, lk);
+                break;
+            } else {
+                r->cv.wait(lk);
+            }
+        }
+        if (r->status != CEC_OK) g_last_error = r->err;
+        return r->status;
+    }
+
+   private:
+    // Called with lk held; returns with r finished and the next queued request (if any) woken
+    // to lead the next batch.
+    void lead(Req* r, std::unique_lock<std::mutex>& lk) {
+        leader_ = true;
+        const auto key = r->key();
+        auto matching_bytes = [&] {
+            size_t b = 0;
+            for (Req* q : queue_)
+                if (q->key() == key) b += Impl::bytes(*q);
+            return b;
+        };
+        const auto until =
+            std::chrono::steady_clock::now() + std::chrono::microseconds(coalesce_window_us());
+        leader_cv_.wait_until(lk, until, [&] { return matching_bytes() >= coalesce_max_bytes(); });
+        std::vector<Req*> batch{r};
+        size_t bytes = Impl::bytes(*r);
+        for (auto it = queue_.begin(); it != queue_.end();) {
+            if (*it == r) {
+                it = queue_.erase(it);
+            } else if ((*it)->key() == key && bytes + Impl::bytes(**it) <= coalesce_max_bytes()) {
+                bytes += Impl::bytes(**it);
+                batch.push_back(*it);
+                it = queue_.erase(it);
+            } else {
+                ++it;
+            }
+        }
+        batch_size_ = batch.size();
+        Arena& arena = arenas_[key.device];
+        lk.unlock();
+        const auto t0 = std::chrono::steady_clock::now();
+        auto t1 = t0, t2 = t0, t3 = t0;
+        int st = Impl::prepare(batch, arena);
+        if (st == CEC_OK) {
+            lk.lock();
+            staged_ = 1;  // the leader's own copy, done below
+            for (Req* q : batch)
+                if (q != r) {
+                    q->phase = Phase::CopyIn;
+                    q->cv.notify_one();
+                }
+            t1 = std::chrono::steady_clock::now();
+            lk.unlock();
+            Impl::copy_in(*r);
+            lk.lock();
+            leader_cv_.wait(lk, [&] { return staged_ == batch_size_; });
+            lk.unlock();
+            t2 = std::chrono::steady_clock::now();
+            g_launches.fetch_add(1, std::memory_order_relaxed);
+            st = Impl::run(batch, arena);
+            t3 = std::chrono::steady_clock::now();
+        }
+        const std::string err = st == CEC_OK ? std::string() : g_last_error;
+        lk.lock();
+        finished_ = 1;
+        for (Req* q : batch) {
+            q->status = st;
+            q->err = err;
+            if (q != r) {
+                q->phase = Phase::CopyOut;
+                q->cv.notify_one();
+            }
+        }
+        lk.unlock();
+        if (st == CEC_OK) Impl::copy_out(*r);
+        lk.lock();
+        // the staging is reused by the next batch: wait for every copy-out
+        leader_cv_.wait(lk, [&] { return finished_ == batch_size_; });
+        if (coalesce_trace()) {
+            auto ms = [](auto a, auto b) {
+                return std::chrono::duration<double, std::milli>(b - a).count();
+            };
+            std::fprintf(stderr,
+                         "[cec coalesce] batch %zu (%zu B): prepare %.2f ms, copy-in %.2f ms, "
+                         "run %.2f ms, copy-out %.2f ms\n",
+                         batch.size(), bytes, ms(t0, t1), ms(t1, t2), ms(t2, t3),
+                         ms(t3, std::chrono::steady_clock::now()));
+        }
+        r->phase = Phase::Finished;
+        leader_ = false;
+        if (!queue_.empty()) queue_.front()->cv.notify_one();  // next leader
+    }
+
+    std::mutex mu_;
+    std::condition_variable leader_cv_;
+    std::deque<Req*> queue_;
+    bool leader_ = false;
+    size_t staged_ = 0, finished_ = 0, batch_size_ = 0;
+    std::map<int, Arena> arenas_;  // per device; used by the current leader's batch only
+};
+
+// ---- cec_sha256(_many): one request = n buffers ----
+struct ShaReq : ReqBase {
+    const uint8_t* const* bufs = nullptr;
+    const size_t* lens = nullptr;
+    size_t n = 0;
+    uint8_t* out = nullptr;
     CoalesceKey key() const { return {nullptr, 0, device}; }
 };
 
-struct PartReq {
-    cec_codec* codec;
-    const uint8_t* data_buf;  // d*L bytes
-    size_t L;
-    uint8_t* parity_out;      // p*L bytes
-    uint8_t* digests_out;     // (d+p)*32 bytes
-    int device;
-    int status = CEC_OK;
-    std::string err;
-    bool done = false;
+struct ShaImpl {
+    static size_t item_bytes(size_t len) { return round_up(std::max<size_t>(len, 1), kChunkAlign); }
+    static size_t bytes(const ShaReq& r) {
+        size_t b = 0;
+        for (size_t i = 0; i < r.n; ++i) b += item_bytes(r.lens[i]);
+        return b;
+    }
+    static int prepare(std::vector<ShaReq*>& batch, Arena& a) {
+        size_t off = 0, items = 0;
+        for (ShaReq* r : batch) {
+            r->arena = &a;
+            r->in_off = off;
+            r->item0 = items;
+            off += bytes(*r);
+            items += r->n;
+        }
+        CEC_TRY(a.in.reserve(off, coalesce_max_bytes()));
+        CEC_TRY(a.out.reserve(items * 32, coalesce_max_bytes() / 8));
+        const size_t meta = round_up(2 * items * sizeof(uint64_t), kChunkAlign);
+        return ctx_reserve(a.dev, meta + round_up(items * 32, kChunkAlign) + off);
+    }
+    static void copy_in(ShaReq& r) {
+        size_t off = r.in_off;
+        for (size_t i = 0; i < r.n; ++i) {
+            if (r.lens[i]) std::memcpy(r.arena->in.ptr + off, r.bufs[i], r.lens[i]);
+            off += item_bytes(r.lens[i]);
+        }
+    }
+    static int run(std::vector<ShaReq*>& batch, Arena& a) {
+        size_t items = 0, total = 0;
+        for (ShaReq* r : batch) {
+            items += r->n;
+            total += bytes(*r);
+        }
+        const size_t meta = round_up(2 * items * sizeof(uint64_t), kChunkAlign);
+        const size_t dig = round_up(items * 32, kChunkAlign);
+        uint64_t* dptrs = reinterpret_cast<uint64_t*>(a.dev.dbuf);
+        uint8_t* ddig = a.dev.dbuf + meta;
+        uint8_t* ddata = ddig + dig;
+        std::vector<uint64_t> hmeta(2 * items);
+        size_t k = 0, off = 0;
+        for (ShaReq* r : batch)
+            for (size_t i = 0; i < r->n; ++i, ++k) {
+                hmeta[k] = reinterpret_cast<uint64_t>(ddata + off);
+                hmeta[items + k] = r->lens[i];
+                off += item_bytes(r->lens[i]);
+            }
+        hipStream_t s = a.dev.stream;
+        HIP_TRY(hipMemcpyAsync(ddata, a.in.ptr, total, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(dptrs, hmeta.data(), hmeta.size() * sizeof(uint64_t),
+                               hipMemcpyHostToDevice, s));
+        ShaParams h{};
+        h.ptrs = dptrs;
+        h.lens = dptrs + items;
+        h.n_parts = uint32_t(items);
+        h.n_chunks = 1;
+        h.digests = ddig;
+        HIP_TRY(launch_sha256(h, true, s));
+        HIP_TRY(hipMemcpyAsync(a.out.ptr, ddig, items * 32, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        return CEC_OK;
+    }
+    static void copy_out(ShaReq& r) {
+        std::memcpy(r.out, r.arena->out.ptr + r.item0 * 32, r.n * 32);
+    }
+};
+
+// ---- cec_part_encode: one request = one part (d*L bytes of data_buf) ----
+struct PartReq : ReqBase {
+    cec_codec* codec = nullptr;
+    const uint8_t* data_buf = nullptr;  // d*L bytes
+    size_t L = 0;
+    uint8_t* parity_out = nullptr;      // p*L bytes
+    uint8_t* digests_out = nullptr;     // (d+p)*32 bytes
     CoalesceKey key() const { return {codec, L, device}; }
 };
 
-Coalescer<ShaReq> g_sha_queue;
-Coalescer<PartReq> g_part_queue;
+// Pinned layout: input [part][d][cs], output [part][p][cs] then digests [part][d+p][32];
+// device batch [part][d+p][cs] (cs = L rounded up to 256 B).
+struct PartImpl {
+    static size_t cs_of(const PartReq& r) { return round_up(r.L, kChunkAlign); }
+    static size_t bytes(const PartReq& r) { return r.codec->d * cs_of(r); }
+    static int prepare(std::vector<PartReq*>& batch, Arena& a) {
+        const cec_codec* c = batch[0]->codec;
+        const size_t d = c->d, p = c->p, t = d + p, B = batch.size(), cs = cs_of(*batch[0]);
+        for (size_t k = 0; k < B; ++k) {
+            batch[k]->arena = &a;
+            batch[k]->slot = k;
+            batch[k]->item0 = B;  // parts in the batch: locates the digest block
+        }
+        CEC_TRY(a.in.reserve(B * d * cs, coalesce_max_bytes()));
+        CEC_TRY(a.out.reserve(B * p * cs + B * t * 32,
+                              coalesce_max_bytes() / d * p + coalesce_max_bytes() / cs * t * 32));
+        return ctx_reserve(a.dev, round_up(B * t * 32, kChunkAlign) + B * t * cs);
+    }
+    static void copy_in(PartReq& r) {
+        const size_t d = r.codec->d, cs = cs_of(r);
+        uint8_t* dst = r.arena->in.ptr + r.slot * d * cs;
+        for (size_t j = 0; j < d; ++j) std::memcpy(dst + j * cs, r.data_buf + j * r.L, r.L);
+    }
+    static int run(std::vector<PartReq*>& batch, Arena& a) {
+        cec_codec* c = batch[0]->codec;
+        const size_t d = c->d, p = c->p, t = d + p, B = batch.size();
+        const size_t L = batch[0]->L, cs = cs_of(*batch[0]);
+        uint32_t* drec = nullptr;
+        CEC_TRY(c->encode_record(&drec));
+        uint8_t* ddig = a.dev.dbuf;
+        uint8_t* dbase = a.dev.dbuf + round_up(B * t * 32, kChunkAlign);
+        hipStream_t s = a.dev.stream;
+        HIP_TRY(hipMemcpy2DAsync(dbase, t * cs, a.in.ptr, d * cs, d * cs, B,
+                                 hipMemcpyHostToDevice, s));
+        if (fused_covers(uint32_t(d), uint32_t(p), L)) {
+            FusedParams f{};
+            f.base = dbase;
+            f.part_stride = t * cs;
+            f.chunk_stride = cs;
+            f.len = L;
+            f.pat = drec;
+            f.digests = ddig;
+            f.n_parts = uint32_t(B);
+            f.d = uint32_t(d);
+            f.p = uint32_t(p);
+            HIP_TRY(launch_encode_hash(f, true, s));
+        } else {
+            ApplyParams ap{};
+            ap.base = dbase;
+            ap.part_stride = t * cs;
+            ap.chunk_stride = cs;
+            ap.len = L;
+            ap.pat = drec;
+            ap.n_parts = uint32_t(B);
+            ap.d = uint32_t(d);
+            ap.n_rows = uint32_t(p);
+            HIP_TRY(launch_rs_apply(ap, true, s));
+            ShaParams h{};
+            h.base = dbase;
+            h.part_stride = t * cs;
+            h.chunk_stride = cs;
+            h.len = L;
+            h.n_parts = uint32_t(B);
+            h.first_chunk = 0;
+            h.n_chunks = uint32_t(t);
+            h.digests = ddig;
+            HIP_TRY(launch_sha256(h, true, s));
+        }
+        HIP_TRY(hipMemcpy2DAsync(a.out.ptr, p * cs, dbase + d * cs, t * cs, p * cs, B,
+                                 hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(a.out.ptr + B * p * cs, ddig, B * t * 32, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        return CEC_OK;
+    }
+    static void copy_out(PartReq& r) {
+        const size_t d = r.codec->d, p = r.codec->p, t = d + p, cs = cs_of(r);
+        const uint8_t* par = r.arena->out.ptr + r.slot * p * cs;
+        for (size_t i = 0; i < p; ++i) std::memcpy(r.parity_out + i * r.L, par + i * cs, r.L);
+        std::memcpy(r.digests_out, r.arena->out.ptr + r.item0 * p * cs + r.slot * t * 32, t * 32);
+    }
+};
 
-// SHA-256 of n host buffers in one launch (list mode) on ctx's stream.
-int sha256_many_on(ThreadCtx& ctx, const uint8_t* const* bufs, const size_t* lens, size_t n,
-                   uint8_t* out) {
-    std::vector<size_t> off(n);
-    size_t total = 0;
-    for (size_t i = 0; i < n; ++i) {
-        off[i] = total;
-        total += round_up(std::max<size_t>(lens[i], 1), kChunkAlign);
-    }
-    const size_t meta = round_up(2 * n * sizeof(uint64_t), kChunkAlign);
-    const size_t dig = round_up(n * 32, kChunkAlign);
-    CEC_TRY(ctx_reserve(ctx, meta + dig + total));
-    uint64_t* dptrs = reinterpret_cast<uint64_t*>(ctx.dbuf);
-    uint64_t* dlens = dptrs + n;
-    uint8_t* ddig = ctx.dbuf + meta;
-    uint8_t* ddata = ddig + dig;
-    std::vector<uint64_t> hmeta(2 * n);
-    for (size_t i = 0; i < n; ++i) {
-        hmeta[i] = reinterpret_cast<uint64_t>(ddata + off[i]);
-        hmeta[n + i] = lens[i];
-        if (lens[i])
-            HIP_TRY(hipMemcpyAsync(ddata + off[i], bufs[i], lens[i], hipMemcpyHostToDevice,
-                                   ctx.stream));
-    }
-    HIP_TRY(hipMemcpyAsync(dptrs, hmeta.data(), hmeta.size() * sizeof(uint64_t),
-                           hipMemcpyHostToDevice, ctx.stream));
-    ShaParams a{};
-    a.ptrs = dptrs;
-    a.lens = dlens;
-    a.n_parts = uint32_t(n);
-    a.n_chunks = 1;
-    a.digests = ddig;
-    HIP_TRY(launch_sha256(a, true, ctx.stream));
-    HIP_TRY(hipMemcpyAsync(out, ddig, n * 32, hipMemcpyDeviceToHost, ctx.stream));
-    HIP_TRY(hipStreamSynchronize(ctx.stream));
-    return CEC_OK;
-}
-
-// FilePart::write_with_encoder's compute for B parts of chunk length L in one launch: each
-// part's d*L data_buf is scattered into a [B][d+p][cs] device batch (2-D copy), encoded and
-// hashed (fused kernel when it covers the shape), and parity + digests copied back.
-int part_encode_many_on(ThreadCtx& ctx, cec_codec* c, const std::vector<PartReq*>& reqs) {
-    const size_t d = c->d, p = c->p, t = d + p, B = reqs.size();
-    const size_t L = reqs[0]->L;
-    const size_t cs = round_up(L, kChunkAlign);
-    const size_t dig = round_up(B * t * 32, kChunkAlign);
-    uint32_t* drec = nullptr;
-    CEC_TRY(c->encode_record(&drec));
-    CEC_TRY(ctx_reserve(ctx, dig + B * t * cs));
-    uint8_t* ddig = ctx.dbuf;
-    uint8_t* dbase = ctx.dbuf + dig;
-    for (size_t k = 0; k < B; ++k)
-        HIP_TRY(hipMemcpy2DAsync(dbase + k * t * cs, cs, reqs[k]->data_buf, L, L, d,
-                                 hipMemcpyHostToDevice, ctx.stream));
-    if (fused_covers(uint32_t(d), uint32_t(p), L)) {
-        FusedParams f{};
-        f.base = dbase;
-        f.part_stride = t * cs;
-        f.chunk_stride = cs;
-        f.len = L;
-        f.pat = drec;
-        f.digests = ddig;
-        f.n_parts = uint32_t(B);
-        f.d = uint32_t(d);
-        f.p = uint32_t(p);
-        HIP_TRY(launch_encode_hash(f, true, ctx.stream));
-    } else {
-        ApplyParams a{};
-        a.base = dbase;
-        a.part_stride = t * cs;
-        a.chunk_stride = cs;
-        a.len = L;
-        a.pat = drec;
-        a.n_parts = uint32_t(B);
-        a.d = uint32_t(d);
-        a.n_rows = uint32_t(p);
-        HIP_TRY(launch_rs_apply(a, true, ctx.stream));
-        ShaParams h{};
-        h.base = dbase;
-        h.part_stride = t * cs;
-        h.chunk_stride = cs;
-        h.len = L;
-        h.n_parts = uint32_t(B);
-        h.first_chunk = 0;
-        h.n_chunks = uint32_t(t);
-        h.digests = ddig;
-        HIP_TRY(launch_sha256(h, true, ctx.stream));
-    }
-    for (size_t k = 0; k < B; ++k) {
-        HIP_TRY(hipMemcpy2DAsync(reqs[k]->parity_out, L, dbase + k * t * cs + d * cs, cs, L, p,
-                                 hipMemcpyDeviceToHost, ctx.stream));
-        HIP_TRY(hipMemcpyAsync(reqs[k]->digests_out, ddig + k * t * 32, t * 32,
-                               hipMemcpyDeviceToHost, ctx.stream));
-    }
-    HIP_TRY(hipStreamSynchronize(ctx.stream));
-    return CEC_OK;
-}
-
-template <typename Req>
-void finish_batch(std::vector<Req*>& batch, int st) {
-    for (Req* r : batch) {
-        r->status = st;
-        if (st != CEC_OK) r->err = g_last_error;
-    }
-}
+Coalescer<ShaReq, ShaImpl> g_sha_queue;
+Coalescer<PartReq, PartImpl> g_part_queue;
 
 int sha256_coalesced(const uint8_t* const* bufs, const size_t* lens, size_t n, uint8_t* out) {
-    int dev = 0;
-    CEC_TRY(current_device(&dev));
-    if (coalesce_window_us() == 0) {
-        ThreadCtx* ctx = nullptr;
-        CEC_TRY(thread_ctx(&ctx, 0));
-        g_calls.fetch_add(1, std::memory_order_relaxed);
-        g_launches.fetch_add(1, std::memory_order_relaxed);
-        return sha256_many_on(*ctx, bufs, lens, n, out);
-    }
     ShaReq r;
+    CEC_TRY(current_device(&r.device));
     r.bufs = bufs;
     r.lens = lens;
     r.n = n;
     r.out = out;
-    r.device = dev;
-    return g_sha_queue.submit(&r, [](std::vector<ShaReq*>& batch, ThreadCtx& ctx) {
-        std::vector<const uint8_t*> b;
-        std::vector<size_t> l;
-        for (ShaReq* q : batch)
-            for (size_t i = 0; i < q->n; ++i) {
-                b.push_back(q->bufs[i]);
-                l.push_back(q->lens[i]);
-            }
-        std::vector<uint8_t> digests(32 * b.size());
-        const int st = sha256_many_on(ctx, b.data(), l.data(), b.size(), digests.data());
-        size_t at = 0;
-        for (ShaReq* q : batch) {
-            if (st == CEC_OK) std::memcpy(q->out, &digests[32 * at], 32 * q->n);
-            at += q->n;
-        }
-        finish_batch(batch, st);
-    });
+    return g_sha_queue.submit(&r);
 }
 
 int part_encode_coalesced(cec_codec* c, const uint8_t* data_buf, size_t L, uint8_t* parity_out,
                           uint8_t* digests_out) {
-    int dev = 0;
-    CEC_TRY(current_device(&dev));
     PartReq r;
+    CEC_TRY(current_device(&r.device));
     r.codec = c;
     r.data_buf = data_buf;
     r.L = L;
     r.parity_out = parity_out;
     r.digests_out = digests_out;
-    r.device = dev;
-    if (coalesce_window_us() == 0) {
-        ThreadCtx* ctx = nullptr;
-        CEC_TRY(thread_ctx(&ctx, 0));
-        g_calls.fetch_add(1, std::memory_order_relaxed);
-        g_launches.fetch_add(1, std::memory_order_relaxed);
-        return part_encode_many_on(*ctx, c, std::vector<PartReq*>{&r});
-    }
-    return g_part_queue.submit(&r, [](std::vector<PartReq*>& batch, ThreadCtx& ctx) {
-        finish_batch(batch, part_encode_many_on(ctx, batch[0]->codec, batch));
-    });
+    return g_part_queue.submit(&r);
 }
 
 void coalesce_stats(uint64_t* calls, uint64_t* launches) {

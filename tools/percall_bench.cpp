@@ -52,9 +52,10 @@ int main() {
         std::fflush(stdout);
     }
     for (int threads : {1, 10, 100, 400}) {
+        run(threads, 1, true, rs);  // warm: pinned staging grown to this batch size
         uint64_t c0, l0, c1, l1;
         cec_coalesce_stats(&c0, &l0);
-        const double gbs = run(threads, 2, true, rs);
+        const double gbs = run(threads, 3, true, rs);
         cec_coalesce_stats(&c1, &l1);
         std::printf("part_encode RS(10,4) 1 MiB, %3d thread(s): %6.2f GB/s of data "
                     "(%llu calls in %llu launches)\n",
