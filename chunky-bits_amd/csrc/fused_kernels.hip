@@ -167,7 +167,7 @@ __global__ __launch_bounds__(64 * (SW + 4)) void encode_hash_kernel(FusedParams 
         // HBM, then issue the next step's d loads (all in flight at once) before the barrier.
         // Two SHA waves saturate their SIMD: without priority the encoders would get no issue
         // slots until the SHA waves park at the step barrier, which then waits for them.
-        if (a.enc_prio) __builtin_amdgcn_s_setprio(1);
+        if (a.enc_prio == 1u) __builtin_amdgcn_s_setprio(1);
         cu32* pat = as_const(a.pat);
         cu32* tab = pat + 1 + d + P;  // input j, row r at (j*P + r) * 5
         const uint32_t et = threadIdx.x - kSha;  // table builders: et < kEncThreads
@@ -325,6 +325,7 @@ __global__ __launch_bounds__(64 * (SW + 4)) void encode_hash_kernel(FusedParams 
         }
     } else {
         // ------------------------------ SHA lanes ------------------------------
+        if (a.enc_prio == 2u) __builtin_amdgcn_s_setprio(1);  // A/B: SHA waves first
         const uint32_t lane = threadIdx.x;
         const bool valid = lane < g_here * t;
         uint32_t st[8];
@@ -384,10 +385,11 @@ hipError_t launch_p(const FusedParams& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-// Encoder waves at s_setprio 1: the build's default, or CEC_FUSED_PRIO=0/1 (dev knob, A/B).
+// Wave priorities: 0 = none, 1 = encoder waves at s_setprio 1, 2 = SHA waves at s_setprio 1.
+// The build's default, or CEC_FUSED_PRIO=0/1/2 (dev knob, A/B).
 uint32_t fused_prio(uint32_t dflt) {
     const char* e = std::getenv("CEC_FUSED_PRIO");
-    return e && (e[0] == '0' || e[0] == '1') ? uint32_t(e[0] - '0') : dflt;
+    return e && (e[0] >= '0' && e[0] <= '2') ? uint32_t(e[0] - '0') : dflt;
 }
 
 // CEC_FUSED_ENC3=0 turns the SIMD-3 encoder placement of the two-SHA-wave build off (A/B).

@@ -68,7 +68,7 @@ struct FusedParams {
     uint32_t d;
     uint32_t p;
     uint32_t parts_per_wg;  // set by launch_encode_hash
-    uint32_t enc_prio;      // set by launch_encode_hash: encoder waves at s_setprio 1
+    uint32_t enc_prio;      // set by launch_encode_hash: 1 = encoder waves, 2 = SHA waves at s_setprio 1
 };
 
 hipError_t launch_rs_apply(const ApplyParams& a, bool vec16, hipStream_t s);

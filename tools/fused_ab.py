@@ -36,7 +36,7 @@ def main():
     for r in range(args.rounds + 1):
         for m in modes:
             os.environ["CEC_FUSED"] = "0" if m == "sep" else "1"
-            os.environ["CEC_FUSED_PRIO"] = {"noprio": "0", "prio": "1"}.get(m, "")
+            os.environ["CEC_FUSED_PRIO"] = {"noprio": "0", "prio": "1", "shaprio": "2"}.get(m, "")
             os.environ["CEC_FUSED_MODE"] = m if m in ("1", "2", "3") else "0"
             os.environ["CEC_FUSED_ENC3"] = "0" if m == "enc3off" else "1"
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
