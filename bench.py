@@ -66,6 +66,12 @@ CONFIGS = {
     "c5": dict(d=10, p=4, chunk=1 * MiB, parts=256, op="stream",
                workload="C5: 1 TiB synthetic object stream, RS(10,4) encode + SHA-256, 1 MiB "
                         "chunks, pinned-host staged batches of 256 parts, 4 slots in flight"),
+    # configs[4], read side: the same stream read back through verify + repair (FileReadBuilder /
+    # read_with_context batched): d random chunks loaded per part, verified, data rebuilt.
+    "c5r": dict(d=10, p=4, chunk=1 * MiB, parts=256, op="read_stream",
+                workload="C5 read side: 1 TiB synthetic object stream read back, RS(10,4), d random "
+                         "chunks loaded per part, SHA-256 verify + reconstruct_data, pinned-host "
+                         "staged batches of 256 parts, 4 slots in flight"),
     # encode only (HBM roofline of the GF kernel alone).
     "c2enc": dict(d=10, p=4, chunk=1 * MiB, parts=4096, op="encode",
                   workload="RS(10,4) encode_sep only, 4096 parts x 1 MiB chunks per GPU"),
@@ -180,6 +186,105 @@ def run_stream(args, cfg, codec, world, rank, device, reduce_dev):
         dist.destroy_process_group()
 
 
+def run_read_stream(args, cfg, codec, world, rank, device, reduce_dev):
+    """C5 read side: pinned slots -> H2D of the loaded chunks -> SHA-256 verify + speculative
+    reconstruct_data -> D2H of the part data (cec_read_pipeline).  Every part loads d random
+    chunks of its d+p (file_part.rs:97 samples d); the chunks and their metadata digests are
+    filled into the slots once (a GPU-encoded block of parts), the loaded set changes per batch.
+    Time = first submit to last result, max over ranks; value = part data bytes delivered / s."""
+    import numpy as np
+    d, p, L, P = cfg["d"], cfg["p"], cfg["chunk"], cfg["parts"]
+    t = d + p
+    depth = 4
+    part_bytes = d * L
+    total_parts = int(args.stream_gib * (1 << 30)) // part_bytes
+    lo = total_parts * rank // world
+    hi = total_parts * (rank + 1) // world
+    mine = hi - lo
+    # one encoded block of P parts (data + parity + digests) from the GPU
+    blk = torch.empty((P, t, L), dtype=torch.uint8, device=device)
+    batch = ce.PartBatch.from_tensor(blk, L)
+    ce.fill_synthetic(batch, d, rank_seed(0xC5, rank))
+    dig = torch.empty((P, t, 32), dtype=torch.uint8, device=device)
+    ce.encode_hash_batch(codec, batch, dig.data_ptr())
+    torch.cuda.synchronize(device)
+    host_blk, host_dig = blk.cpu().numpy(), dig.cpu().numpy()
+    del blk, dig
+    rp = ce.ReadPipeline(codec, L, P, depth)
+    rng = np.random.default_rng(rank)
+    masks = []
+    mask_mode = os.environ.get("CEC_C5R_MASK", "random")  # dev A/B: "data" = chunks 0..d-1
+    for _ in range(8):  # d random loaded chunks per part, a few distinct batch patterns
+        m = np.zeros((P, t), np.uint8)
+        for k in range(P):
+            m[k, np.arange(d) if mask_mode == "data" else rng.choice(t, d, replace=False)] = 1
+        masks.append(m)
+    for i in range(depth):
+        slot, chunks, present, expected = rp.acquire()
+        chunks[:] = host_blk
+        expected[:] = host_dig
+    n_batches = (mine + P - 1) // P
+    for i in range(min(depth, n_batches)):  # warmup
+        slot, chunks, present, expected = rp.acquire()
+        present[:] = masks[i % len(masks)]
+        rp.submit(slot, P)
+    rp.drain()
+    barrier(world)
+    t0 = time.perf_counter()
+    part = lo
+    bad = 0
+    for i in range(n_batches):
+        slot, chunks, present, expected = rp.acquire()
+        if i >= depth:
+            _, _, status = rp.wait(slot)
+            bad += int((status != 0).sum())
+        n = min(P, hi - part)
+        present[:n] = masks[i % len(masks)][:n]
+        rp.submit(slot, n)
+        part += n
+    for i in range(depth):
+        _, _, status = rp.wait(i)
+        bad += int((status != 0).sum())
+    rp.drain()
+    barrier(world)
+    t1 = time.perf_counter()
+    el = max_over_ranks(t1 - t0, world, reduce_dev)
+    ok = None
+    if args.check and rank == 0:
+        # the last batch's data must equal the encoded block's data chunks
+        slot = (n_batches - 1) % depth
+        data, ver, status = rp.wait(slot)
+        k = int(data.shape[0]) - 1
+        ok = bool(bad == 0 and np.array_equal(data[k], host_blk[k, :d]))
+    if rank == 0:
+        total = total_parts * part_bytes
+        line = {
+            "metric": f"{METRIC} [c5r]",
+            "value": round(total / el / 1e9, 2),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": n_batches,
+            "warmup": min(depth, n_batches),
+            "ms_per_step": round(el / max(n_batches, 1) * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic host stream (GPU-encoded block of parts, d random chunks loaded "
+                    "per part, loaded sets vary per batch)",
+            "config": {"workload": cfg["workload"], "d": d, "p": p, "chunk_bytes": L,
+                       "parts_per_batch": P, "slots": depth, "stream_bytes": total,
+                       "parallelism": f"part-range-sharded x{world}, no collective"},
+            "seconds": round(el, 3),
+            "undecodable_parts": bad,
+        }
+        if ok is not None:
+            line["check_vs_written"] = ok
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -221,6 +326,8 @@ def main():
     codec = ce.ReedSolomon(d, p)
     if cfg["op"] == "stream":
         return run_stream(args, cfg, codec, world, rank, device, reduce_dev)
+    if cfg["op"] == "read_stream":
+        return run_read_stream(args, cfg, codec, world, rank, device, reduce_dev)
     buf = torch.empty((n_parts, t, L), dtype=torch.uint8, device=device)
     digests = torch.empty((n_parts, t, 32), dtype=torch.uint8, device=device)
     batch = ce.PartBatch.from_tensor(buf, L)

@@ -103,6 +103,16 @@ _sig("cec_pipeline_wait", [_vp, ctypes.c_size_t, ctypes.POINTER(_u8p), ctypes.PO
                            _szp])
 _sig("cec_pipeline_drain", [_vp])
 _sig("cec_pipeline_last_error", [], ctypes.c_char_p)
+_sig("cec_read_pipeline_new", [_vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t,
+                               ctypes.POINTER(_vp)])
+_sig("cec_read_pipeline_free", [_vp], None)
+_sig("cec_read_pipeline_depth", [_vp], ctypes.c_size_t)
+_sig("cec_read_pipeline_acquire", [_vp, _szp, ctypes.POINTER(_u8p), ctypes.POINTER(_u8p),
+                                   ctypes.POINTER(_u8p)])
+_sig("cec_read_pipeline_submit", [_vp, ctypes.c_size_t, ctypes.c_size_t])
+_sig("cec_read_pipeline_wait", [_vp, ctypes.c_size_t, ctypes.POINTER(_u8p), ctypes.POINTER(_u8p),
+                                ctypes.POINTER(ctypes.POINTER(ctypes.c_int)), _szp])
+_sig("cec_read_pipeline_drain", [_vp])
 _sig("cec_synth_byte", [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64],
      ctypes.c_uint8)
 
@@ -520,3 +530,65 @@ class Pipeline:
 
     def drain(self) -> None:
         _check(_lib.cec_pipeline_drain(self._h))
+
+
+class ReadPipeline:
+    """cec_read_pipeline: FileReadBuilder's part loop batched over pinned slots.
+
+    ``slot, chunks, present, expected = rp.acquire()`` gives writable numpy views of the pinned
+    [parts][d+p][L] chunk buffer, [parts][d+p] loaded flags and [parts][d+p][32] metadata
+    digests; fill them, ``rp.submit(slot, n_parts)``; later
+    ``data, verified, status = rp.wait(slot)`` -> [parts][d][L] part bytes (read_with_context's
+    output), [parts][d+p] verification flags, [parts] status codes (views valid until the slot
+    is re-acquired).
+    """
+
+    def __init__(self, codec: ReedSolomon, chunk_len: int, parts_per_batch: int, depth: int = 4):
+        h = _vp()
+        code = _lib.cec_read_pipeline_new(codec.handle, chunk_len, parts_per_batch, depth,
+                                          ctypes.byref(h))
+        if code != OK:
+            raise Error(code)
+        self._h = h
+        self.codec = codec
+        self.d, self.p = codec.data_shard_count(), codec.parity_shard_count()
+        self.t = self.d + self.p
+        self.L = chunk_len
+        self.parts = parts_per_batch
+
+    def __del__(self, _free=_lib.cec_read_pipeline_free):
+        h = getattr(self, "_h", None)
+        if h:
+            _free(h)
+            self._h = None
+
+    def acquire(self):
+        import numpy as np
+        slot = ctypes.c_size_t(0)
+        ch, pr, ex = _u8p(), _u8p(), _u8p()
+        _check(_lib.cec_read_pipeline_acquire(self._h, ctypes.byref(slot), ctypes.byref(ch),
+                                              ctypes.byref(pr), ctypes.byref(ex)))
+        P, t, L = self.parts, self.t, self.L
+        chunks = np.ctypeslib.as_array(ch, shape=(P * t * L,)).reshape(P, t, L)
+        present = np.ctypeslib.as_array(pr, shape=(P * t,)).reshape(P, t)
+        expected = np.ctypeslib.as_array(ex, shape=(P * t * 32,)).reshape(P, t, 32)
+        return slot.value, chunks, present, expected
+
+    def submit(self, slot: int, n_parts: int) -> None:
+        _check(_lib.cec_read_pipeline_submit(self._h, slot, n_parts))
+
+    def wait(self, slot: int):
+        import numpy as np
+        data, ok = _u8p(), _u8p()
+        status = ctypes.POINTER(ctypes.c_int)()
+        n = ctypes.c_size_t(0)
+        _check(_lib.cec_read_pipeline_wait(self._h, slot, ctypes.byref(data), ctypes.byref(ok),
+                                           ctypes.byref(status), ctypes.byref(n)))
+        k, t, d, L = n.value, self.t, self.d, self.L
+        out = np.ctypeslib.as_array(data, shape=(max(k * d * L, 1),))[: k * d * L].reshape(k, d, L)
+        ver = np.ctypeslib.as_array(ok, shape=(max(k * t, 1),))[: k * t].reshape(k, t)
+        st = np.ctypeslib.as_array(status, shape=(max(k, 1),))[:k]
+        return out, ver, st
+
+    def drain(self) -> None:
+        _check(_lib.cec_read_pipeline_drain(self._h))

@@ -11,6 +11,7 @@
 // flight on separate streams (their workgroups run on disjoint CUs) keep the PCIe link busy.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -197,6 +198,280 @@ int cec_pipeline_drain(cec_pipeline* pl) {
             s.in_flight = false;
         }
     }
+    return CEC_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// Read pipeline (cec_read_pipeline_*): the batched form of FileReadBuilder's part loop
+// (reference src/file/reader.rs:40-75, buffered(5) reads of FilePart::read_with_context,
+// file_part.rs:73-135): per part, the chunks the caller could load, verified against their
+// metadata digests, and the d data chunks rebuilt from the verified ones.
+//
+// Per slot, asynchronously on the slot's stream: the loaded chunks go up (one copy per run of
+// consecutive loaded chunks), the SHA-256 kernel verifies every loaded chunk against its
+// expected digest, and the missing data chunks are rebuilt SPECULATIVELY from the first d
+// loaded chunks (the pattern is known at submit time, so no host round trip sits between
+// verification and decode); the d data chunks and the verification flags come back.  wait()
+// checks the flags: a part whose loaded chunks all verified is done (the common case); a part
+// with a chunk that failed is decoded again from its verified chunks only (or reported
+// TooFewShardsPresent when fewer than d verify) before wait() returns.
+// ------------------------------------------------------------------------------------------
+}  // extern "C"
+
+namespace {
+
+struct ReadSlot {
+    uint8_t* h_chunks = nullptr;    // pinned [parts][t][L]   (caller: loaded chunk bytes)
+    uint8_t* h_present = nullptr;   // pinned [parts][t]      (caller: 1 = loaded)
+    uint8_t* h_expected = nullptr;  // pinned [parts][t][32]  (caller: metadata digests)
+    uint8_t* h_data = nullptr;      // pinned [parts][d][L]   (result: data chunks)
+    uint8_t* h_ok = nullptr;        // pinned [parts][t]      (result: verified flags)
+    int* h_status = nullptr;        // host [parts]
+    uint8_t* d_buf = nullptr;       // device [parts][t][cs]
+    uint8_t* d_expected = nullptr;  // device [parts][t][32]
+    uint8_t* d_flags = nullptr;     // device [parts][t] present, then [parts][t] ok
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    bool in_flight = false;
+    bool checked = false;
+    size_t n_parts = 0;
+    std::vector<uint8_t> decode_mask;  // present mask the speculative decode used
+};
+
+}  // namespace
+
+struct cec_read_pipeline {
+    const cec_codec* codec = nullptr;
+    int device = 0;
+    size_t d = 0, p = 0, t = 0, L = 0, cs = 0, parts = 0;
+    std::vector<ReadSlot> slots;
+    size_t next = 0;
+
+    ~cec_read_pipeline() {
+        int cur = 0;
+        if (hipGetDevice(&cur) != hipSuccess) return;
+        (void)hipSetDevice(device);
+        for (ReadSlot& s : slots) {
+            if (s.stream) (void)hipStreamSynchronize(s.stream);
+            if (s.done) (void)hipEventDestroy(s.done);
+            if (s.stream) (void)hipStreamDestroy(s.stream);
+            for (uint8_t* dptr : {s.d_buf, s.d_expected, s.d_flags})
+                if (dptr) (void)hipFree(dptr);
+            for (uint8_t* hptr : {s.h_chunks, s.h_present, s.h_expected, s.h_data, s.h_ok})
+                if (hptr) (void)hipHostFree(hptr);
+            delete[] s.h_status;
+        }
+        (void)hipSetDevice(cur);
+    }
+
+    cec_part_batch batch(ReadSlot& s, size_t n) const {
+        return cec_part_batch{s.d_buf, t * cs, cs, n, L};
+    }
+
+    // D2H of the d data chunks of parts [k0, k0 + n) into h_data.
+    int copy_data_back(ReadSlot& s, size_t k0, size_t n) const {
+        const size_t pitch = t * cs, dw = d * L;
+        if (cs == L) {
+            PIPE_TRY(hipMemcpy2DAsync(s.h_data + k0 * dw, dw, s.d_buf + k0 * pitch, pitch, dw, n,
+                                      hipMemcpyDeviceToHost, s.stream));
+        } else {
+            for (size_t j = 0; j < d; ++j)
+                PIPE_TRY(hipMemcpy2DAsync(s.h_data + k0 * dw + j * L, dw,
+                                          s.d_buf + k0 * pitch + j * cs, pitch, L, n,
+                                          hipMemcpyDeviceToHost, s.stream));
+        }
+        return CEC_OK;
+    }
+};
+
+extern "C" {
+
+int cec_read_pipeline_new(const cec_codec* codec, size_t chunk_len, size_t parts_per_batch,
+                          size_t depth, cec_read_pipeline** out) {
+    if (!codec || !out || chunk_len == 0 || parts_per_batch == 0 || depth == 0 || depth > 16)
+        return CEC_ERR_INVALID_ARGUMENT;
+    *out = nullptr;
+    if (cec_device_count() <= 0) return CEC_ERR_NO_DEVICE;
+    auto* pl = new cec_read_pipeline();
+    pl->codec = codec;
+    PIPE_TRY(hipGetDevice(&pl->device));
+    pl->d = cec_codec_data_shards(codec);
+    pl->p = cec_codec_parity_shards(codec);
+    pl->t = pl->d + pl->p;
+    pl->L = chunk_len;
+    pl->cs = (chunk_len + 255) / 256 * 256;
+    pl->parts = parts_per_batch;
+    pl->slots.resize(depth);
+    const size_t P = pl->parts, t = pl->t;
+    for (ReadSlot& s : pl->slots) {
+        hipError_t e = hipSuccess;
+        auto host = [&](uint8_t** ptr, size_t bytes) {
+            if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(ptr), bytes, hipHostMallocDefault);
+        };
+        auto dev = [&](uint8_t** ptr, size_t bytes) {
+            if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(ptr), bytes);
+        };
+        host(&s.h_chunks, P * t * pl->L);
+        host(&s.h_present, P * t);
+        host(&s.h_expected, P * t * 32);
+        host(&s.h_data, P * pl->d * pl->L);
+        host(&s.h_ok, P * t);
+        dev(&s.d_buf, P * t * pl->cs);
+        dev(&s.d_expected, P * t * 32);
+        dev(&s.d_flags, 2 * P * t);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
+        s.h_status = new int[P];
+        if (e != hipSuccess) {
+            delete pl;
+            return pipe_fail(e, "cec_read_pipeline_new allocation");
+        }
+        std::memset(s.h_present, 0, P * t);
+    }
+    *out = pl;
+    return CEC_OK;
+}
+
+void cec_read_pipeline_free(cec_read_pipeline* pl) { delete pl; }
+
+size_t cec_read_pipeline_depth(const cec_read_pipeline* pl) { return pl ? pl->slots.size() : 0; }
+
+int cec_read_pipeline_acquire(cec_read_pipeline* pl, size_t* slot, uint8_t** chunks,
+                              uint8_t** present, uint8_t** expected) {
+    if (!pl || !slot || !chunks || !present || !expected) return CEC_ERR_INVALID_ARGUMENT;
+    const size_t i = pl->next;
+    pl->next = (pl->next + 1) % pl->slots.size();
+    ReadSlot& s = pl->slots[i];
+    if (s.in_flight) {
+        PIPE_TRY(hipEventSynchronize(s.done));
+        s.in_flight = false;
+    }
+    *slot = i;
+    *chunks = s.h_chunks;
+    *present = s.h_present;
+    *expected = s.h_expected;
+    return CEC_OK;
+}
+
+int cec_read_pipeline_submit(cec_read_pipeline* pl, size_t slot, size_t n_parts) {
+    if (!pl || slot >= pl->slots.size() || n_parts == 0 || n_parts > pl->parts)
+        return CEC_ERR_INVALID_ARGUMENT;
+    ReadSlot& s = pl->slots[slot];
+    int cur = 0;
+    PIPE_TRY(hipGetDevice(&cur));
+    if (cur != pl->device) PIPE_TRY(hipSetDevice(pl->device));
+    const size_t d = pl->d, t = pl->t, L = pl->L, cs = pl->cs, n = n_parts * t;
+    // loaded chunks up: one copy per run of consecutive loaded chunks of a part
+    for (size_t k = 0; k < n_parts; ++k) {
+        const uint8_t* pr = s.h_present + k * t;
+        for (size_t i = 0; i < t;) {
+            if (!pr[i]) {
+                ++i;
+                continue;
+            }
+            size_t j = i;
+            while (j < t && pr[j]) ++j;
+            const uint8_t* src = s.h_chunks + (k * t + i) * L;
+            uint8_t* dst = s.d_buf + (k * t + i) * cs;
+            if (cs == L)
+                PIPE_TRY(hipMemcpyAsync(dst, src, (j - i) * L, hipMemcpyHostToDevice, s.stream));
+            else
+                PIPE_TRY(hipMemcpy2DAsync(dst, cs, src, L, L, j - i, hipMemcpyHostToDevice,
+                                          s.stream));
+            i = j;
+        }
+    }
+    PIPE_TRY(hipMemcpyAsync(s.d_expected, s.h_expected, n * 32, hipMemcpyHostToDevice, s.stream));
+    PIPE_TRY(hipMemcpyAsync(s.d_flags, s.h_present, n, hipMemcpyHostToDevice, s.stream));
+    cec_part_batch b = pl->batch(s, n_parts);
+    int st = cec_verify_batch(&b, 0, t, s.d_flags, s.d_expected, s.d_flags + n, s.stream);
+    // speculative decode from the loaded chunks; parts with fewer than d loaded are skipped
+    // (reported at wait)
+    s.decode_mask.assign(s.h_present, s.h_present + n);
+    for (size_t k = 0; k < n_parts; ++k) {
+        const size_t loaded = size_t(std::count(s.decode_mask.begin() + k * t,
+                                                s.decode_mask.begin() + (k + 1) * t, uint8_t(1)));
+        s.h_status[k] = loaded >= d ? CEC_OK : CEC_TOO_FEW_SHARDS_PRESENT;
+        if (loaded < d) std::fill(s.decode_mask.begin() + k * t, s.decode_mask.begin() + (k + 1) * t, uint8_t(1));
+    }
+    if (st == CEC_OK) st = cec_reconstruct_batch(pl->codec, &b, s.decode_mask.data(), 1, s.stream);
+    if (st != CEC_OK) {
+        g_pipe_error = cec_last_error();
+        return st;
+    }
+    st = pl->copy_data_back(s, 0, n_parts);
+    if (st != CEC_OK) return st;
+    PIPE_TRY(hipMemcpyAsync(s.h_ok, s.d_flags + n, n, hipMemcpyDeviceToHost, s.stream));
+    PIPE_TRY(hipEventRecord(s.done, s.stream));
+    s.in_flight = true;
+    s.checked = false;
+    s.n_parts = n_parts;
+    if (cur != pl->device) PIPE_TRY(hipSetDevice(cur));
+    return CEC_OK;
+}
+
+int cec_read_pipeline_wait(cec_read_pipeline* pl, size_t slot, const uint8_t** data,
+                           const uint8_t** verified, const int** part_status, size_t* n_parts) {
+    if (!pl || slot >= pl->slots.size()) return CEC_ERR_INVALID_ARGUMENT;
+    ReadSlot& s = pl->slots[slot];
+    if (s.in_flight) {
+        PIPE_TRY(hipEventSynchronize(s.done));
+        s.in_flight = false;
+    }
+    if (!s.checked && s.n_parts) {
+        // parts whose loaded chunks did not all verify: decode again from the verified ones
+        const size_t t = pl->t, d = pl->d, n = s.n_parts;
+        std::vector<uint8_t> mask(n * t, 1);
+        std::vector<size_t> redo;
+        for (size_t k = 0; k < n; ++k) {
+            if (s.h_status[k] != CEC_OK) continue;
+            bool bad = false;
+            size_t good = 0;
+            for (size_t i = 0; i < t; ++i) {
+                bad |= s.h_present[k * t + i] && !s.h_ok[k * t + i];
+                good += s.h_ok[k * t + i] ? 1 : 0;
+            }
+            if (!bad) continue;
+            if (good < d) {
+                s.h_status[k] = CEC_TOO_FEW_SHARDS_PRESENT;
+                continue;
+            }
+            std::copy(s.h_ok + k * t, s.h_ok + (k + 1) * t, mask.begin() + k * t);
+            redo.push_back(k);
+        }
+        if (!redo.empty()) {
+            int cur = 0;
+            PIPE_TRY(hipGetDevice(&cur));
+            if (cur != pl->device) PIPE_TRY(hipSetDevice(pl->device));
+            cec_part_batch b = pl->batch(s, n);
+            int st = cec_reconstruct_batch(pl->codec, &b, mask.data(), 1, s.stream);
+            if (st != CEC_OK) {
+                g_pipe_error = cec_last_error();
+                return st;
+            }
+            for (size_t k : redo) {
+                st = pl->copy_data_back(s, k, 1);
+                if (st != CEC_OK) return st;
+            }
+            PIPE_TRY(hipStreamSynchronize(s.stream));
+            if (cur != pl->device) PIPE_TRY(hipSetDevice(cur));
+        }
+        s.checked = true;
+    }
+    if (data) *data = s.h_data;
+    if (verified) *verified = s.h_ok;
+    if (part_status) *part_status = s.h_status;
+    if (n_parts) *n_parts = s.n_parts;
+    return CEC_OK;
+}
+
+int cec_read_pipeline_drain(cec_read_pipeline* pl) {
+    if (!pl) return CEC_ERR_INVALID_ARGUMENT;
+    for (size_t i = 0; i < pl->slots.size(); ++i)
+        if (pl->slots[i].in_flight) {
+            const int st = cec_read_pipeline_wait(pl, i, nullptr, nullptr, nullptr, nullptr);
+            if (st != CEC_OK) return st;
+        }
     return CEC_OK;
 }
 

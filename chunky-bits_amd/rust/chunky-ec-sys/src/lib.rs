@@ -22,6 +22,11 @@ pub mod sys {
     }
 
     #[repr(C)]
+    pub struct cec_read_pipeline {
+        _private: [u8; 0],
+    }
+
+    #[repr(C)]
     #[derive(Clone, Copy, Debug)]
     pub struct cec_part_batch {
         pub base: *mut u8,
@@ -156,6 +161,37 @@ pub mod sys {
         ) -> c_int;
         pub fn cec_pipeline_drain(pipeline: *mut cec_pipeline) -> c_int;
         pub fn cec_pipeline_last_error() -> *const std::os::raw::c_char;
+        pub fn cec_read_pipeline_new(
+            codec: *const cec_codec,
+            chunk_len: usize,
+            parts_per_batch: usize,
+            depth: usize,
+            out: *mut *mut cec_read_pipeline,
+        ) -> c_int;
+        pub fn cec_read_pipeline_free(pipeline: *mut cec_read_pipeline);
+        pub fn cec_read_pipeline_depth(pipeline: *const cec_read_pipeline) -> usize;
+        pub fn cec_read_pipeline_acquire(
+            pipeline: *mut cec_read_pipeline,
+            slot: *mut usize,
+            chunks: *mut *mut u8,
+            present: *mut *mut u8,
+            expected: *mut *mut u8,
+        ) -> c_int;
+        pub fn cec_read_pipeline_submit(
+            pipeline: *mut cec_read_pipeline,
+            slot: usize,
+            n_parts: usize,
+        ) -> c_int;
+        pub fn cec_read_pipeline_wait(
+            pipeline: *mut cec_read_pipeline,
+            slot: usize,
+            data: *mut *const u8,
+            verified: *mut *const u8,
+            part_status: *mut *const c_int,
+            n_parts: *mut usize,
+        ) -> c_int;
+        pub fn cec_read_pipeline_drain(pipeline: *mut cec_read_pipeline) -> c_int;
+        pub fn cec_coalesce_stats(calls: *mut u64, launches: *mut u64);
     }
 }
 
@@ -460,5 +496,106 @@ impl WritePipeline {
     /// Wait for every submitted batch.
     pub fn drain(&mut self) -> Result<(), CecError> {
         check_pipe(unsafe { sys::cec_pipeline_drain(self.raw) })
+    }
+}
+
+/// Batched `FileReadBuilder` / `FilePart::read_with_context` compute (reader.rs:40-75,
+/// file_part.rs:73-135) over pinned slots: the caller writes the chunks it loaded, their
+/// loaded flags and the metadata digests; the engine verifies every loaded chunk, rebuilds the
+/// d data chunks from verified ones, and returns the part bytes, the flags and a per-part
+/// status (`Error::TooFewShardsPresent` when fewer than d verify).
+pub struct ReadPipeline {
+    raw: *mut sys::cec_read_pipeline,
+    d: usize,
+    t: usize,
+    chunk_len: usize,
+    parts: usize,
+}
+
+unsafe impl Send for ReadPipeline {}
+
+impl Drop for ReadPipeline {
+    fn drop(&mut self) {
+        unsafe { sys::cec_read_pipeline_free(self.raw) }
+    }
+}
+
+/// A slot's input areas: chunks `[parts][d+p][chunk_len]`, present `[parts][d+p]`,
+/// expected digests `[parts][d+p][32]`.
+pub struct ReadSlotInput<'a> {
+    pub slot: usize,
+    pub chunks: &'a mut [u8],
+    pub present: &'a mut [u8],
+    pub expected: &'a mut [u8],
+}
+
+/// A completed read batch: data `[parts][d][chunk_len]`, verified `[parts][d+p]`, statuses.
+pub struct ReadBatchResult<'a> {
+    pub data: &'a [u8],
+    pub verified: &'a [u8],
+    pub part_status: Vec<Result<(), Error>>,
+}
+
+impl ReadPipeline {
+    pub fn new(
+        codec: &ReedSolomon,
+        chunk_len: usize,
+        parts_per_batch: usize,
+        depth: usize,
+    ) -> Result<ReadPipeline, CecError> {
+        let mut raw = std::ptr::null_mut();
+        check_pipe(unsafe {
+            sys::cec_read_pipeline_new(codec.raw, chunk_len, parts_per_batch, depth, &mut raw)
+        })?;
+        Ok(ReadPipeline {
+            raw,
+            d: codec.data_shard_count(),
+            t: codec.total_shard_count(),
+            chunk_len,
+            parts: parts_per_batch,
+        })
+    }
+
+    pub fn depth(&self) -> usize {
+        unsafe { sys::cec_read_pipeline_depth(self.raw) }
+    }
+
+    pub fn acquire(&mut self) -> Result<ReadSlotInput<'_>, CecError> {
+        let (mut slot, mut c, mut p, mut e) =
+            (0usize, std::ptr::null_mut(), std::ptr::null_mut(), std::ptr::null_mut());
+        check_pipe(unsafe { sys::cec_read_pipeline_acquire(self.raw, &mut slot, &mut c, &mut p, &mut e) })?;
+        let n = self.parts * self.t;
+        Ok(ReadSlotInput {
+            slot,
+            chunks: unsafe { std::slice::from_raw_parts_mut(c, n * self.chunk_len) },
+            present: unsafe { std::slice::from_raw_parts_mut(p, n) },
+            expected: unsafe { std::slice::from_raw_parts_mut(e, n * 32) },
+        })
+    }
+
+    pub fn submit(&mut self, slot: usize, n_parts: usize) -> Result<(), CecError> {
+        check_pipe(unsafe { sys::cec_read_pipeline_submit(self.raw, slot, n_parts) })
+    }
+
+    pub fn wait(&mut self, slot: usize) -> Result<ReadBatchResult<'_>, CecError> {
+        let (mut data, mut ver) = (std::ptr::null(), std::ptr::null());
+        let mut status: *const c_int = std::ptr::null();
+        let mut n = 0usize;
+        check_pipe(unsafe {
+            sys::cec_read_pipeline_wait(self.raw, slot, &mut data, &mut ver, &mut status, &mut n)
+        })?;
+        let codes = unsafe { std::slice::from_raw_parts(status, n) };
+        Ok(ReadBatchResult {
+            data: unsafe { std::slice::from_raw_parts(data, n * self.d * self.chunk_len) },
+            verified: unsafe { std::slice::from_raw_parts(ver, n * self.t) },
+            part_status: codes
+                .iter()
+                .map(|&c| check(c).map_err(Error::from))
+                .collect(),
+        })
+    }
+
+    pub fn drain(&mut self) -> Result<(), CecError> {
+        check_pipe(unsafe { sys::cec_read_pipeline_drain(self.raw) })
     }
 }

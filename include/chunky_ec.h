@@ -226,6 +226,29 @@ int cec_pipeline_wait(cec_pipeline* pipeline, size_t slot, const uint8_t** parit
 int cec_pipeline_drain(cec_pipeline* pipeline);
 const char* cec_pipeline_last_error(void);
 
+/* Host-staged READ pipeline (FileReadBuilder's part loop, reader.rs:40-75, over
+ * FilePart::read_with_context, file_part.rs:73-135).  `depth` slots; per slot the caller fills
+ * (acquire): chunks = pinned [parts][d+p][chunk_len] (the chunk bytes it could load), present =
+ * pinned [parts][d+p] (1 = loaded; every slot starts all-0 and keeps what the caller wrote),
+ * expected = pinned [parts][d+p][32] (the metadata digests).  submit: loaded chunks H2D,
+ * SHA-256 verification of every loaded chunk, speculative reconstruct_data from the first d
+ * loaded chunks, D2H of the d data chunks - all asynchronous.  wait: *data = pinned
+ * [parts][d][chunk_len] (the part's bytes, as read_with_context returns them), *verified =
+ * [parts][d+p] flags, *part_status = [parts] (CEC_OK or CEC_TOO_FEW_SHARDS_PRESENT); parts
+ * whose loaded chunks did not all verify are decoded again from their verified chunks before
+ * wait returns.  Errors: cec_pipeline_last_error(). */
+typedef struct cec_read_pipeline cec_read_pipeline;
+int cec_read_pipeline_new(const cec_codec* codec, size_t chunk_len, size_t parts_per_batch,
+                          size_t depth, cec_read_pipeline** out);
+void cec_read_pipeline_free(cec_read_pipeline* pipeline);
+size_t cec_read_pipeline_depth(const cec_read_pipeline* pipeline);
+int cec_read_pipeline_acquire(cec_read_pipeline* pipeline, size_t* slot, uint8_t** chunks,
+                              uint8_t** present, uint8_t** expected);
+int cec_read_pipeline_submit(cec_read_pipeline* pipeline, size_t slot, size_t n_parts);
+int cec_read_pipeline_wait(cec_read_pipeline* pipeline, size_t slot, const uint8_t** data,
+                           const uint8_t** verified, const int** part_status, size_t* n_parts);
+int cec_read_pipeline_drain(cec_read_pipeline* pipeline);
+
 /* ---------------------------------------------------------------------------------------- */
 /* Utilities for benchmarks and tests                                                        */
 /* ---------------------------------------------------------------------------------------- */

@@ -553,6 +553,72 @@ def test_pipeline_matches_oracle(d, p, L, parts, depth, batches):
                 assert digests[k, j].tobytes() == hashlib.sha256(chunks[j].tobytes()).digest()
 
 
+@pytest.mark.parametrize("d,p,L,parts,depth,batches", [
+    (10, 4, 4096, 12, 3, 5),      # more batches than slots: slot reuse
+    (3, 2, 683, 9, 2, 3),         # odd chunk length (padded device stride)
+    (20, 8, 1000, 6, 2, 2),
+])
+def test_read_pipeline_matches_read_with_context(d, p, L, parts, depth, batches):
+    """FileReadBuilder's loop batched: per part the loaded chunks (all; d random ones like
+    file_part.rs:97; fewer than d; a corrupted loaded chunk with enough others; a corrupted one
+    without), verification against the metadata digests, and the part's data rebuilt from the
+    verified chunks.  Data must equal the written bytes; flags and statuses as the reference's
+    read would see them (TooFewShardsPresent when fewer than d verify)."""
+    t = d + p
+    rs = ce.ReedSolomon(d, p)
+    rp = ce.ReadPipeline(rs, L, parts, depth)
+    rng = np.random.default_rng(d * 100 + L)
+    pending, want = {}, {}
+
+    def check(b, out):
+        data, ver, status = out
+        exp_data, exp_ok, exp_status = want[b]
+        assert list(status) == exp_status, b
+        assert np.array_equal(ver, exp_ok), b
+        for k, st in enumerate(exp_status):
+            if st == 0:
+                assert np.array_equal(data[k], exp_data[k]), (b, k)
+
+    for b in range(batches):
+        slot, chunks, present, expected = rp.acquire()
+        if slot in pending:
+            check(pending[slot], tuple(x.copy() for x in rp.wait(slot)))
+        n = parts if b % 2 == 0 else parts - 1
+        exp_data, exp_ok, exp_status = [], np.zeros((n, t), np.uint8), []
+        for k in range(n):
+            dat = gen_bytes(3000 + 97 * b + k, d * L).reshape(d, L)
+            st, par = oracle.encode_sep(d, p, list(dat))
+            full = [dat[j] for j in range(d)] + par
+            for i in range(t):
+                chunks[k, i] = full[i]
+                expected[k, i] = np.frombuffer(hashlib.sha256(full[i].tobytes()).digest(), np.uint8)
+            kind = (k + b) % 5
+            if kind == 0:
+                loaded = list(range(t))
+            elif kind == 1:
+                loaded = sorted(rng.choice(t, d, replace=False))
+            elif kind == 2:
+                loaded = sorted(rng.choice(t, d - 1, replace=False))
+            else:
+                loaded = sorted(rng.choice(t, d + 1 if kind == 3 else d, replace=False))
+            present[k] = 0
+            present[k, loaded] = 1
+            ok = present[k].copy()
+            if kind >= 3:  # corrupt one loaded chunk (a data chunk if one is loaded)
+                victim = next((i for i in loaded if i < d), loaded[0])
+                chunks[k, victim, L // 2] ^= 0x5A
+                ok[victim] = 0
+            exp_ok[k] = ok
+            exp_status.append(0 if ok.sum() >= d else 10)
+            exp_data.append(dat)
+        rp.submit(slot, n)
+        pending[slot] = b
+        want[b] = (exp_data, exp_ok, exp_status)
+    for slot, b in pending.items():
+        check(b, tuple(x.copy() for x in rp.wait(slot)))
+    rp.drain()
+
+
 # ----------------------------------------------------------------------------------------------
 # Verify / read / resilver (FilePart::verify, read_with_context, resilver compute)
 # ----------------------------------------------------------------------------------------------
