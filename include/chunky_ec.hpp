@@ -89,6 +89,14 @@ inline void check(int status) {
     throw EngineError(status, std::string(cec_status_name(status)) + ": " + cec_last_error());
 }
 
+// Pipeline calls keep their messages in cec_pipeline_last_error().
+inline void check_pipe(int status) {
+    if (status == CEC_OK) return;
+    if (status >= CEC_TOO_FEW_SHARDS && status <= CEC_INVALID_INDEX)
+        throw ErasureError(static_cast<Error>(status));
+    throw EngineError(status, std::string(cec_status_name(status)) + ": " + cec_pipeline_last_error());
+}
+
 inline char hex_digit(unsigned v) { return char(v < 10 ? '0' + v : 'a' + (v - 10)); }
 
 inline int hex_value(char c) {
@@ -193,6 +201,31 @@ class ReedSolomon {
     }
 };
 
+namespace detail {
+// Host-staged pipelines pin GiBs of host memory (~0.35 s per GiB to pin), so they are made
+// once per thread and shape and reused by every later write/read of that shape.
+template <typename Pipe>
+struct CachedPipe {
+    std::shared_ptr<ReedSolomon> codec;
+    std::shared_ptr<Pipe> pipe;
+};
+
+template <typename Pipe, typename New, typename Free>
+CachedPipe<Pipe>& cached_pipe(size_t d, size_t p, size_t L, size_t parts, size_t depth, New make,
+                              Free free_fn) {
+    using Key = std::array<size_t, 5>;
+    thread_local std::map<Key, CachedPipe<Pipe>> cache;
+    CachedPipe<Pipe>& e = cache[Key{d, p, L, parts, depth}];
+    if (!e.pipe) {
+        e.codec = std::make_shared<ReedSolomon>(d, p);
+        Pipe* raw = nullptr;
+        make(e.codec->raw(), L, parts, depth, &raw);
+        e.pipe = std::shared_ptr<Pipe>(raw, free_fn);
+    }
+    return e;
+}
+}  // namespace detail
+
 // file::hash::Sha256Hash.
 class Sha256Hash {
    public:
@@ -265,11 +298,29 @@ class Sha256Hash {
 // written under its hash, location.rs:612).  Not thread-safe.
 class ChunkStore {
    public:
-    void write_shard(const Sha256Hash& hash, Bytes bytes) { store_[hash] = std::move(bytes); }
+    ChunkStore() = default;
+    // A sink that records nothing (shards to /dev/null): for measuring the write path alone.
+    static ChunkStore discard() {
+        ChunkStore s;
+        s.discard_ = true;
+        return s;
+    }
+    bool discards() const { return discard_; }
+    void write_shard(const Sha256Hash& hash, Bytes bytes) {
+        if (!discard_) store_[hash] = std::move(bytes);
+    }
+    void write_shard(const Sha256Hash& hash, const uint8_t* bytes, size_t n) {
+        if (!discard_) store_[hash] = Bytes(bytes, bytes + n);
+    }
     std::optional<Bytes> read(const Sha256Hash& hash) const {
         auto it = store_.find(hash);
         if (it == store_.end()) return std::nullopt;
         return it->second;
+    }
+    // The stored bytes without a copy (nullptr if absent); valid until the shard is erased.
+    const Bytes* find(const Sha256Hash& hash) const {
+        auto it = store_.find(hash);
+        return it == store_.end() ? nullptr : &it->second;
     }
     bool erase(const Sha256Hash& hash) { return store_.erase(hash) > 0; }
     // Replace a stored shard's bytes (bit rot / tampering in tests).
@@ -283,6 +334,7 @@ class ChunkStore {
 
    private:
     std::map<Sha256Hash, Bytes> store_;
+    bool discard_ = false;
 };
 
 // file::Chunk: the hash of one chunk (its locations are the ChunkStore key).
@@ -336,7 +388,7 @@ struct FilePart {
             std::memcpy(h.data(), &digests[32 * i], 32);
             const Chunk c{Sha256Hash(h)};
             const uint8_t* src = i < d ? &data_buf[i * L] : &parity[(i - d) * L];
-            dest.write_shard(c.hash, Bytes(src, src + L));
+            dest.write_shard(c.hash, src, L);
             (i < d ? part.data : part.parity).push_back(c);
         }
         return part;
@@ -415,11 +467,27 @@ struct FileReference {
     std::vector<FilePart> parts;
 
     // FileReference::read: every part's data, truncated to `length` (file_reference.rs:49-56).
-    Bytes read(const ChunkStore& src) const {
+    // parts_per_batch > 0: runs of parts with one chunksize go through the host-staged read
+    // pipeline (cec_read_pipeline_*: verify + rebuild for a whole batch per launch); the same
+    // bytes and the same TooFewShardsPresent failure as the per-part path.
+    Bytes read(const ChunkStore& src, size_t parts_per_batch = 0, size_t depth = 4) const {
         Bytes out;
-        for (const auto& part : parts) {
-            Bytes b = part.read_with_context(src);
-            out.insert(out.end(), b.begin(), b.end());
+        size_t total = 0;
+        for (const auto& part : parts) total += part.len_bytes();
+        out.reserve(total);
+        size_t k = 0;
+        while (k < parts.size()) {
+            size_t run = 1;
+            while (parts_per_batch && k + run < parts.size() &&
+                   parts[k + run].chunksize == parts[k].chunksize)
+                ++run;
+            if (run < 2) {
+                Bytes b = parts[k].read_with_context(src);
+                out.insert(out.end(), b.begin(), b.end());
+            } else {
+                read_run(src, k, run, parts_per_batch, depth, out);
+            }
+            k += run;
         }
         if (length && out.size() > *length) out.resize(size_t(*length));
         return out;
@@ -433,6 +501,57 @@ struct FileReference {
         std::vector<PartReport> r;
         for (const auto& part : parts) r.push_back(part.resilver(dest));
         return r;
+    }
+
+   private:
+    void read_run(const ChunkStore& src, size_t k0, size_t n, size_t ppb, size_t depth,
+                  Bytes& out) const {
+        const FilePart& first = parts[k0];
+        const size_t d = first.data.size(), t = d + first.parity.size(), L = first.chunksize;
+        auto& cached = detail::cached_pipe<cec_read_pipeline>(
+            d, t - d, L, ppb, depth,
+            [](const cec_codec* c, size_t l, size_t parts, size_t dep, cec_read_pipeline** out) {
+                detail::check_pipe(cec_read_pipeline_new(c, l, parts, dep, out));
+            },
+            cec_read_pipeline_free);
+        cec_read_pipeline* rp = cached.pipe.get();
+        const size_t nd = cec_read_pipeline_depth(rp);
+        std::vector<std::pair<size_t, size_t>> pending(nd, {0, 0});  // slot -> (first, count)
+        auto collect = [&](size_t slot) {
+            const uint8_t *data = nullptr, *ver = nullptr;
+            const int* status = nullptr;
+            size_t got = 0;
+            detail::check(cec_read_pipeline_wait(rp, slot, &data, &ver, &status, &got));
+            for (size_t i = 0; i < got; ++i) detail::check(status[i]);
+            out.insert(out.end(), data, data + got * d * L);
+        };
+        size_t done = 0, submitted = 0;
+        const size_t per = ppb;
+        while (done < n) {
+            size_t slot = 0;
+            uint8_t *chunks = nullptr, *present = nullptr, *expected = nullptr;
+            detail::check(cec_read_pipeline_acquire(rp, &slot, &chunks, &present, &expected));
+            if (pending[slot].second) {  // this slot's previous batch: in order, oldest first
+                collect(slot);
+                done += pending[slot].second;
+                pending[slot] = {0, 0};
+            }
+            if (submitted == n) continue;
+            const size_t b = std::min(per, n - submitted);
+            for (size_t q = 0; q < b; ++q) {
+                const FilePart& part = parts[k0 + submitted + q];
+                for (size_t i = 0; i < t; ++i) {
+                    const Bytes* bytes = src.find(part.chunk(i).hash);
+                    const bool ok = bytes && bytes->size() == L;
+                    present[q * t + i] = ok ? 1 : 0;
+                    if (ok) std::memcpy(chunks + (q * t + i) * L, bytes->data(), L);
+                    std::memcpy(expected + (q * t + i) * 32, part.chunk(i).hash.digest().data(), 32);
+                }
+            }
+            detail::check(cec_read_pipeline_submit(rp, slot, b));
+            pending[slot] = {submitted, b};
+            submitted += b;
+        }
     }
 };
 
@@ -454,11 +573,25 @@ class FileWriteBuilder {
         return *this;
     }
 
+    // Parts per host-staged batch (cec_pipeline_*) and batches in flight; 0 = one
+    // write_with_encoder call per part (the reference's shape).
+    FileWriteBuilder& batch(size_t parts_per_batch, size_t depth = 4) {
+        batch_ = parts_per_batch;
+        depth_ = depth;
+        return *this;
+    }
+
     FileReference write(const uint8_t* bytes, size_t n, ChunkStore& dest) const {
         const ReedSolomon encoder(data_, parity_);  // writer.rs:131
         FileReference file;
         const size_t part_cap = data_ * chunk_size_;
-        for (size_t off = 0; off < n; off += part_cap) {
+        const size_t full = n / part_cap;
+        size_t off = 0;
+        if (batch_ && full >= 2) {  // full parts: L = chunk_size for every one of them
+            write_full_parts(encoder, bytes, full, dest, file);
+            off = full * part_cap;
+        }
+        for (; off < n; off += part_cap) {
             const size_t bytes_read = std::min(part_cap, n - off);
             Bytes data_buf(part_cap, 0);  // vec![0; data * chunk_size] (writer.rs:172)
             std::memcpy(data_buf.data(), bytes + off, bytes_read);
@@ -473,6 +606,61 @@ class FileWriteBuilder {
     size_t chunk_size_ = size_t(1) << 20;
     size_t data_ = 3;
     size_t parity_ = 2;
+    size_t batch_ = 0;
+    size_t depth_ = 4;
+
+    // The write pipeline over `full` parts of d*chunk_size bytes: same FileParts and stored
+    // chunks as write_with_encoder part by part.
+    void write_full_parts(const ReedSolomon& encoder, const uint8_t* bytes, size_t full,
+                          ChunkStore& dest, FileReference& file) const {
+        (void)encoder;
+        const size_t d = data_, p = parity_, t = d + p, L = chunk_size_, per = batch_;
+        auto& cached = detail::cached_pipe<cec_pipeline>(
+            d, p, L, batch_, depth_,
+            [](const cec_codec* c, size_t l, size_t parts, size_t dep, cec_pipeline** out) {
+                detail::check_pipe(cec_pipeline_new(c, l, parts, dep, out));
+            },
+            cec_pipeline_free);
+        cec_pipeline* pl = cached.pipe.get();
+        std::vector<std::pair<size_t, size_t>> pending(cec_pipeline_depth(pl), {0, 0});
+        auto collect = [&](size_t slot) {
+            const uint8_t *parity = nullptr, *digests = nullptr;
+            size_t got = 0;
+            detail::check_pipe(cec_pipeline_wait(pl, slot, &parity, &digests, &got));
+            const size_t first = pending[slot].first;
+            for (size_t k = 0; k < got; ++k) {
+                FilePart part;
+                part.chunksize = L;
+                for (size_t i = 0; i < t; ++i) {
+                    std::array<uint8_t, 32> h{};
+                    std::memcpy(h.data(), digests + (k * t + i) * 32, 32);
+                    const Chunk c{Sha256Hash(h)};
+                    const uint8_t* src = i < d ? bytes + ((first + k) * d + i) * L
+                                               : parity + (k * p + (i - d)) * L;
+                    dest.write_shard(c.hash, src, L);
+                    (i < d ? part.data : part.parity).push_back(c);
+                }
+                file.parts.push_back(std::move(part));
+            }
+        };
+        size_t submitted = 0, done = 0;
+        while (done < full) {
+            size_t slot = 0;
+            uint8_t* data = nullptr;
+            detail::check_pipe(cec_pipeline_acquire(pl, &slot, &data));
+            if (pending[slot].second) {  // oldest batch first: parts stay in file order
+                collect(slot);
+                done += pending[slot].second;
+                pending[slot] = {0, 0};
+            }
+            if (submitted == full) continue;
+            const size_t b = std::min(per, full - submitted);
+            std::memcpy(data, bytes + submitted * d * L, b * d * L);
+            detail::check_pipe(cec_pipeline_submit(pl, slot, b));
+            pending[slot] = {submitted, b};
+            submitted += b;
+        }
+    }
 };
 
 }  // namespace chunky_ec

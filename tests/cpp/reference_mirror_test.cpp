@@ -11,6 +11,8 @@
 //   test_cluster_digests        golden fixture of the same write (tests/golden, pinned oracle)
 //   test_cp_50mib               BASELINE configs[0]: `cp` of a 50 MiB file, d=3 p=2, 1 MiB
 //                               chunks: 17 parts, last chunksize 699 051, read back bit-exact
+//   test_batched_paths          FileWriteBuilder::batch / FileReference::read batched through
+//                               the host-staged pipelines == the per-part path, bit-exact
 //   test_one_encode             JavaReedSolomon testOneEncode RS(5,5) (crate KAT)
 //   test_matrix_rows            SURVEY.md Appendix A RS(3,2) / RS(10,4) parity rows
 //   test_errors                 reed_solomon_erasure::Error variants of ReedSolomon::new,
@@ -19,6 +21,7 @@
 //
 // Runs on a GPU (every computation goes through libchunky_ec.so).  `--list` prints the test
 // names without touching the GPU.  Exit status 0 iff every test passed.
+#include <array>
 #include <cstdio>
 #include <cstring>
 #include <functional>
@@ -157,21 +160,27 @@ void test_cluster_digests() {
     }
 }
 
-// BASELINE.json configs[0] (`chunky-bits cp` of 50 MiB into a d=3, p=2, 1 MiB-chunk cluster),
-// compute part: 16 full parts + one of 2 MiB (L = ceil(2 MiB / 3) = 699 051), every chunk
-// stored under its digest, the file read back bit-exact after losing 2 chunks per part.
-void test_cp_50mib() {
-    const size_t length = size_t(50) << 20;
-    Bytes input(length);
-    uint64_t z = 0x9E3779B97F4A7C15ull;
-    for (size_t i = 0; i < length; i += 8) {  // splitmix64 stream
+// n bytes of a splitmix64 stream (no repeated chunks: the store is content-addressed).
+Bytes random_bytes(size_t n, uint64_t seed) {
+    Bytes out(n);
+    uint64_t z = seed * 0x2545F4914F6CDD1Dull + 0x9E3779B97F4A7C15ull;
+    for (size_t i = 0; i < n; i += 8) {
         z += 0x9E3779B97F4A7C15ull;
         uint64_t v = z;
         v = (v ^ (v >> 30)) * 0xBF58476D1CE4E5B9ull;
         v = (v ^ (v >> 27)) * 0x94D049BB133111EBull;
         v ^= v >> 31;
-        std::memcpy(&input[i], &v, std::min<size_t>(8, length - i));
+        std::memcpy(&out[i], &v, std::min<size_t>(8, n - i));
     }
+    return out;
+}
+
+// BASELINE.json configs[0] (`chunky-bits cp` of 50 MiB into a d=3, p=2, 1 MiB-chunk cluster),
+// compute part: 16 full parts + one of 2 MiB (L = ceil(2 MiB / 3) = 699 051), every chunk
+// stored under its digest, the file read back bit-exact after losing 2 chunks per part.
+void test_cp_50mib() {
+    const size_t length = size_t(50) << 20;
+    const Bytes input = random_bytes(length, 50);
     ChunkStore store;
     const FileReference f =
         FileWriteBuilder().chunk_size(size_t(1) << 20).data_chunks(3).parity_chunks(2).write(input, store);
@@ -186,6 +195,43 @@ void test_cp_50mib() {
         store.erase(part.parity[1].hash);
     }
     CHECK(f.read(store) == input);
+}
+
+// The host-staged pipelines behind FileWriteBuilder::batch and FileReference::read(src, n):
+// identical FileParts, identical stored chunks, identical bytes read back (with holes).
+void test_batched_paths() {
+    for (const auto& shape : std::vector<std::array<size_t, 4>>{
+             {10, 4, size_t(1) << 16, 37}, {3, 2, 1024, 20}, {20, 8, 4096, 9}}) {
+        const size_t d = shape[0], p = shape[1], chunk = shape[2], n_parts = shape[3];
+        const size_t length = d * chunk * (n_parts - 1) + 12345 % (d * chunk - 1) + 1;  // short last
+        const Bytes input = random_bytes(length, d * 1000 + chunk);
+        ChunkStore per_part, batched;
+        const auto b = FileWriteBuilder().chunk_size(chunk).data_chunks(d).parity_chunks(p);
+        const FileReference a = b.write(input, per_part);
+        const FileReference c = FileWriteBuilder(b).batch(8, 3).write(input, batched);
+        CHECK(a.parts.size() == n_parts && c.parts.size() == n_parts);
+        CHECK(per_part.size() == batched.size());
+        for (size_t k = 0; k < n_parts; ++k) {
+            CHECK(a.parts[k].chunksize == c.parts[k].chunksize);
+            for (size_t i = 0; i < d + p; ++i) {
+                CHECK(a.parts[k].chunk(i).hash == c.parts[k].chunk(i).hash);
+                CHECK(batched.read(c.parts[k].chunk(i).hash) == per_part.read(a.parts[k].chunk(i).hash));
+            }
+        }
+        // holes: one data + one parity chunk per part, then (where p leaves room) a corrupted
+        // chunk in part 3 that the read must not trust
+        for (const auto& part : c.parts) {
+            batched.erase(part.data[1 % d].hash);
+            batched.erase(part.parity[0].hash);
+        }
+        if (p >= 3) CHECK(batched.corrupt(c.parts[3].data[0].hash, 5));
+        CHECK(c.read(batched, 8, 3) == input);
+        CHECK(c.read(batched) == input);
+        // a part with fewer than d usable chunks fails like the per-part read
+        for (size_t i = 2; i < d + p; ++i) batched.erase(c.parts[5].chunk(i).hash);
+        CHECK(batched.corrupt(c.parts[5].chunk(0).hash, 1));
+        CHECK(throws_erasure([&] { c.read(batched, 8, 3); }, Error::TooFewShardsPresent));
+    }
 }
 
 // JavaReedSolomon testOneEncode / reed-solomon-erasure test_encoding (RS(5,5)).
@@ -289,6 +335,7 @@ const Test kTests[] = {
     {"test_resilver", test_resilver},
     {"test_cluster_digests", test_cluster_digests},
     {"test_cp_50mib", test_cp_50mib},
+    {"test_batched_paths", test_batched_paths},
     {"test_one_encode", test_one_encode},
     {"test_matrix_rows", test_matrix_rows},
     {"test_errors", test_errors},

@@ -1,0 +1,68 @@
+// End-to-end `cp` through the C++ host layer (dev tool): FileWriteBuilder::write of an in-memory
+// file into a ChunkStore (RAM stand-in for the locations), then FileReference::read back after
+// losing one data + one parity chunk per part — per-part calls (the reference's shape) vs the
+// host-staged pipelines (FileWriteBuilder::batch / read(src, parts_per_batch)).
+//   make -C chunky-bits_amd/csrc cp_bench ; tools/cp_bench [GiB]
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+
+#include "chunky_ec.hpp"
+
+using namespace chunky_ec;
+
+int main(int argc, char** argv) {
+    const double gib = argc > 1 ? std::atof(argv[1]) : 4.0;
+    const size_t d = 10, p = 4, chunk = size_t(1) << 20;
+    const size_t length = size_t(gib * double(size_t(1) << 30)) / (d * chunk) * (d * chunk) + 4321;
+    Bytes input(length);
+    uint64_t z = 7;
+    for (size_t i = 0; i + 8 <= length; i += 8) {
+        z += 0x9E3779B97F4A7C15ull;
+        uint64_t v = z;
+        v = (v ^ (v >> 30)) * 0xBF58476D1CE4E5B9ull;
+        v = (v ^ (v >> 27)) * 0x94D049BB133111EBull;
+        v ^= v >> 31;
+        std::memcpy(&input[i], &v, 8);
+    }
+    auto secs = [](auto t0) {
+        return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    };
+    const auto builder = FileWriteBuilder().chunk_size(chunk).data_chunks(d).parity_chunks(p);
+    for (int batched = 1; batched >= 0; --batched) {
+        const size_t n = batched ? length : std::min(length, size_t(64) * d * chunk);
+        auto write = [&](ChunkStore& store) {
+            return batched ? FileWriteBuilder(builder).batch(256, 4).write(input.data(), n, store)
+                           : builder.write(input.data(), n, store);
+        };
+        // write path alone (shards discarded, as if written to /dev/null); the first write
+        // of a shape pins the pipeline's host buffers (made once per thread and shape)
+        ChunkStore sink = ChunkStore::discard();
+        write(sink);
+        auto t0 = std::chrono::steady_clock::now();
+        write(sink);
+        const double w = secs(t0);
+        // write into RAM, lose one data + one parity chunk per part, read back
+        ChunkStore store;
+        t0 = std::chrono::steady_clock::now();
+        const FileReference f = write(store);
+        const double w_ram = secs(t0);
+        for (const auto& part : f.parts) {
+            store.erase(part.data[3].hash);
+            store.erase(part.parity[1].hash);
+        }
+        if (batched) (void)f.read(store, 256, 4);  // pins the read pipeline
+        t0 = std::chrono::steady_clock::now();
+        const Bytes back = batched ? f.read(store, 256, 4) : f.read(store);
+        const double r = secs(t0);
+        const bool ok = back.size() == n && std::memcmp(back.data(), input.data(), n) == 0;
+        std::printf("%-9s %6.2f GiB, %zu parts: write %6.2f GB/s (%6.2f GB/s into the RAM store), "
+                    "read with 2 holes/part %6.2f GB/s, bit-exact %s\n",
+                    batched ? "batched" : "per-part", double(n) / double(size_t(1) << 30),
+                    f.parts.size(), double(n) / w / 1e9, double(n) / w_ram / 1e9,
+                    double(n) / r / 1e9, ok ? "yes" : "NO");
+        std::fflush(stdout);
+        if (!ok) return 1;
+    }
+    return 0;
+}
