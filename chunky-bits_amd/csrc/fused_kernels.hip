@@ -105,10 +105,51 @@ __device__ __forceinline__ void store_words(uint8_t* dst, uint64_t n, const uint
     }
 }
 
-template <int NW>
+// BE builds keep every chunk in the LDS ring as big-endian 32-bit words (SHA-256's message word
+// order): the encoder waves byte-swap while storing, so the SHA waves read message words
+// directly (16 fewer half-rate v_perm per 64-byte block).  GF(2^8) arithmetic is byte-wise, so
+// the encoders compute parity on their native words.  See fused_be() for where it pays.
+template <int NW, bool BE = true>
 __device__ __forceinline__ void lds_store_words(uint8_t* dst, const uint32_t w[NW]) {
-    if (NW == 4) *reinterpret_cast<uint4*>(dst) = make_uint4(w[0], w[1], w[2 % NW], w[3 % NW]);
-    else *reinterpret_cast<uint2*>(dst) = make_uint2(w[0], w[1]);
+    if (!BE) {
+        if (NW == 4) *reinterpret_cast<uint4*>(dst) = make_uint4(w[0], w[1], w[2 % NW], w[3 % NW]);
+        else *reinterpret_cast<uint2*>(dst) = make_uint2(w[0], w[1]);
+    } else if (NW == 4)
+        *reinterpret_cast<uint4*>(dst) = make_uint4(bswap32(w[0]), bswap32(w[1]),
+                                                    bswap32(w[2 % NW]), bswap32(w[3 % NW]));
+    else
+        *reinterpret_cast<uint2*>(dst) = make_uint2(bswap32(w[0]), bswap32(w[1]));
+}
+
+// block_words for a ring row that already holds big-endian words.
+__device__ __forceinline__ void ring_block_words(const uint4 q[4], uint32_t w[16]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        w[4 * i + 0] = q[i].x;
+        w[4 * i + 1] = q[i].y;
+        w[4 * i + 2] = q[i].z;
+        w[4 * i + 3] = q[i].w;
+    }
+}
+
+// tail_words over a ring row of big-endian words: message byte pos sits at row byte pos ^ 3.
+__device__ __forceinline__ void ring_tail_words(const uint8_t* tp, uint32_t rem, uint32_t blk,
+                                                uint32_t tb, uint64_t bits, uint32_t w[16]) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        uint32_t word = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t pos = blk * 64 + uint32_t(i * 4 + k);
+            const uint32_t byte = pos < rem ? uint32_t(tp[pos ^ 3u]) : (pos == rem ? 0x80u : 0u);
+            word = (word << 8) | byte;
+        }
+        w[i] = word;
+    }
+    if (blk == tb - 1) {
+        w[14] = uint32_t(bits >> 32);
+        w[15] = uint32_t(bits);
+    }
 }
 
 // PMAX: parity rows (exact when a.p == PMAX; rows r >= a.p skipped by uniform guards).
@@ -127,7 +168,7 @@ __device__ __forceinline__ void lds_store_words(uint8_t* dst, const uint32_t w[N
 // work, as waves 7 (an otherwise empty SHA slot) and 11 (tasks 0-63 and 64-127; needs
 // G*STEP/CW <= 128), while encoder waves 8-10 only build the product tables and join the
 // barriers.  The SIMDs with two SHA waves then carry no encoder work at all.
-template <int PMAX, int STEP, int MODE, int DT, int SW = 4, bool ENC3 = false>
+template <int PMAX, int STEP, int MODE, int DT, int SW = 4, bool ENC3 = false, bool BE = false>
 __global__ __launch_bounds__(64 * (SW + 4)) void encode_hash_kernel(FusedParams a) {
     static_assert(!ENC3 || SW == 8, "ENC3 needs the two-SHA-wave build");
     constexpr uint32_t kSha = 64u * SW;
@@ -230,7 +271,7 @@ __global__ __launch_bounds__(64 * (SW + 4)) void encode_hash_kernel(FusedParams 
             for (int b = 0; b < 4 * NW; ++b) acc_lo[b] = acc_hi[b] = 0u;
 #pragma unroll
             for (int j = 0; j < DMAX; ++j)
-                if (uint32_t(j) < d) lds_store_words<NW>(lrow + size_t(j) * kRow, v[j]);
+                if (uint32_t(j) < d) lds_store_words<NW, BE>(lrow + size_t(j) * kRow, v[j]);
             if (MODE == 1) {
 #pragma unroll
                 for (int q = 0; q < NW; ++q) acc_lo[4 * q] = v[0][q];
@@ -306,7 +347,7 @@ __global__ __launch_bounds__(64 * (SW + 4)) void encode_hash_kernel(FusedParams 
 #pragma unroll
             for (int r = 0; r < PMAX; ++r) {
                 if (uint32_t(r) >= P) break;
-                lds_store_words<NW>(lrow + size_t(d + r) * kRow, out[r]);
+                lds_store_words<NW, BE>(lrow + size_t(d + r) * kRow, out[r]);
                 store_words<NW, RAGGED>(pb + uint64_t(d + r) * cs + x, n, out[r]);
             }
         };
@@ -345,7 +386,8 @@ __global__ __launch_bounds__(64 * (SW + 4)) void encode_hash_kernel(FusedParams 
                 for (uint64_t b = b0; b < b1; ++b) {
                     const uint4* q = reinterpret_cast<const uint4*>(row + (b - b0) * 64);
                     const uint4 qq[4] = {q[0], q[1], q[2], q[3]};
-                    block_words(qq, w);
+                    if (BE) ring_block_words(qq, w);
+                    else block_words(qq, w);
                     compress(st, w);
                 }
                 if (s + 1 == n_steps) {
@@ -354,7 +396,8 @@ __global__ __launch_bounds__(64 * (SW + 4)) void encode_hash_kernel(FusedParams 
                     const uint8_t* tp = row + (64 * nfull - uint64_t(s) * STEP);
 #pragma unroll 1
                     for (uint32_t blk = 0; blk < tb; ++blk) {
-                        tail_words(tp, rem, blk, tb, L * 8, w);
+                        if (BE) ring_tail_words(tp, rem, blk, tb, L * 8, w);
+                        else tail_words(tp, rem, blk, tb, L * 8, w);
                         compress(st, w);
                     }
                 }
@@ -368,19 +411,19 @@ __global__ __launch_bounds__(64 * (SW + 4)) void encode_hash_kernel(FusedParams 
     }
 }
 
-template <int PMAX, int STEP, int MODE, int DT, int SW = 4, bool ENC3 = false>
+template <int PMAX, int STEP, int MODE, int DT, int SW = 4, bool ENC3 = false, bool BE = false>
 hipError_t launch_p(const FusedParams& a, hipStream_t s) {
     const size_t lds = size_t(2) * a.parts_per_wg * (a.d + a.p) * (STEP + 16);  // ring
     const size_t tabs = size_t(DT ? DT : kMaxFusedData) * 256 * (PMAX <= 4 ? 4 : 8);
     if (lds + tabs > 160 * 1024) return hipErrorInvalidValue;
     static const bool attr = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&encode_hash_kernel<PMAX, STEP, MODE, DT, SW, ENC3>),
+        reinterpret_cast<const void*>(&encode_hash_kernel<PMAX, STEP, MODE, DT, SW, ENC3, BE>),
         hipFuncAttributeMaxDynamicSharedMemorySize,
         int(160 * 1024 - size_t(DT ? DT : kMaxFusedData) * 256 * (PMAX <= 4 ? 4 : 8))) ==
         hipSuccess;
     if (!attr) return hipErrorInvalidValue;
     const uint32_t grid = (a.n_parts + a.parts_per_wg - 1) / a.parts_per_wg;
-    hipLaunchKernelGGL((encode_hash_kernel<PMAX, STEP, MODE, DT, SW, ENC3>), dim3(grid),
+    hipLaunchKernelGGL((encode_hash_kernel<PMAX, STEP, MODE, DT, SW, ENC3, BE>), dim3(grid),
                        dim3(64 * (SW + 4)), lds, s, a);
     return hipGetLastError();
 }
@@ -390,6 +433,16 @@ hipError_t launch_p(const FusedParams& a, hipStream_t s) {
 uint32_t fused_prio(uint32_t dflt) {
     const char* e = std::getenv("CEC_FUSED_PRIO");
     return e && (e[0] >= '0' && e[0] <= '2') ? uint32_t(e[0] - '0') : dflt;
+}
+
+// Byte order of the LDS ring (BE = encoders store big-endian words, the SHA waves skip their
+// 16 byte-swaps per block).  It pays where the encoders run on a SIMD with spare issue slots
+// (the ENC3 build: C4 21.06 -> 20.47 ms) and costs where they share a saturated SIMD with a SHA
+// wave (RS(10,4) build: C2 42.63 -> 42.97 ms), so it is on for ENC3 only.  CEC_FUSED_BE=0/1
+// overrides (A/B).
+bool fused_be(bool dflt) {
+    const char* e = std::getenv("CEC_FUSED_BE");
+    return e && (e[0] == '0' || e[0] == '1') ? e[0] == '1' : dflt;
 }
 
 // CEC_FUSED_ENC3=0 turns the SIMD-3 encoder placement of the two-SHA-wave build off (A/B).
@@ -414,7 +467,8 @@ hipError_t launch_step(const FusedParams& a, hipStream_t s) {
         // mode 3: the generic-d build on every shape it covers (A/B and tests against the
         // shape builds)
         if (mode != 3 && a.d == 10 && a.p == 4 && a.len % col_width(10) == 0)
-            return launch_p<4, STEP, 0, 10>(a, s);
+            return fused_be(false) ? launch_p<4, STEP, 0, 10, 4, false, true>(a, s)
+                                   : launch_p<4, STEP, 0, 10, 4, false, false>(a, s);
     }
     if constexpr (STEP == 128) {
         if (a.d == 20) {  // RS(20, p <= 8); launch_encode_hash checked len % col_width(20)
@@ -465,7 +519,8 @@ hipError_t launch_encode_hash(const FusedParams& in, bool vec16, hipStream_t s) 
             if (size_t(2) * a.parts_per_wg * t * (64 + 16) + size_t(20) * 256 * 8 <= 160 * 1024) {
                 if (fused_enc3() && a.parts_per_wg * t <= 7 * 64 &&
                     a.parts_per_wg * (64u / 8u) <= 128)
-                    return launch_p<8, 64, 0, 20, 8, true>(a, s);
+                    return fused_be(true) ? launch_p<8, 64, 0, 20, 8, true, true>(a, s)
+                                          : launch_p<8, 64, 0, 20, 8, true, false>(a, s);
                 return launch_p<8, 64, 0, 20, 8>(a, s);
             }
         }

@@ -467,6 +467,8 @@ def test_full_size_encode_erase_reconstruct_roundtrip(d, p, L, n_parts):
 @pytest.mark.parametrize("d,p,L,cstride,n_parts,mode", [(*c, "0")[:6] for c in [
     (10, 4, 4096 + 13, 4112, 40),     # ragged tail, 16 parts per workgroup, 3 workgroups
     (10, 4, 64, None, 17),            # exactly one SHA block, last workgroup with 1 part
+    (10, 4, 4096 + 48, None, 19),     # RS(10,4) shape build with a 48-byte message tail
+    (10, 4, 256 + 16, None, 7),       # shape build, tail 16 bytes in the second step
     (10, 4, 63, 64, 5),               # shorter than a block (tail only)
     (10, 4, 4096, None, 4100),        # > 256 workgroups: two passes
     (16, 8, 1000, 1008, 21),          # largest fused d; generic (p != 4) parity-row path
@@ -485,12 +487,17 @@ def test_full_size_encode_erase_reconstruct_roundtrip(d, p, L, n_parts):
     (10, 4, 4096 + 13, 4112, 40, "3"),  # generic-d build on the RS(10,4) shape
     (10, 4, 64, None, 17, "3"),
     (20, 8, 1024, None, 2400, "enc3off"),  # two SHA waves per SIMD, encoders on every SIMD
+    (20, 8, 200, None, 4096, "le"),        # ENC3 build with a little-endian ring (A/B path)
+    (10, 4, 4096 + 48, None, 19, "be"),    # RS(10,4) build with a big-endian ring (A/B path)
     (20, 8, 64 * 3 + 8, None, 4096),       # C4 part count: 16 parts/CU, encoders on SIMD 3
 ]])
 def test_fused_encode_hash_matches_separate_and_oracle(d, p, L, cstride, n_parts, mode,
                                                        monkeypatch):
     if mode == "enc3off":
         monkeypatch.setenv("CEC_FUSED_ENC3", "0")
+        mode = "0"
+    elif mode in ("le", "be"):
+        monkeypatch.setenv("CEC_FUSED_BE", "1" if mode == "be" else "0")
         mode = "0"
     monkeypatch.setenv("CEC_FUSED_MODE", mode)
     t = d + p
