@@ -327,7 +327,8 @@ int reconstruct_host(const cec_codec* cc, uint8_t* const* shards, const size_t* 
 // writer.rs:130; `concurrency` is a builder knob) only helps if concurrent calls share a
 // launch.  cec_part_encode / cec_sha256(_many) therefore go through a leader/follower queue:
 // the first caller to find no batch in progress becomes the leader, waits up to
-// CEC_COALESCE_US microseconds (default 200) for more requests with its key (codec, chunk
+// CEC_COALESCE_US microseconds (default 200; only when calls are concurrent) for more requests
+// with its key (codec, chunk
 // length, device), and runs them as ONE batch:
 //   1. copy-in   every caller copies its own (pageable) input into the queue's pinned staging,
 //                in parallel on its own thread;
@@ -459,9 +460,14 @@ class Coalescer {
                 if (q->key() == key) b += Impl::bytes(*q);
             return b;
         };
-        const auto until =
-            std::chrono::steady_clock::now() + std::chrono::microseconds(coalesce_window_us());
-        leader_cv_.wait_until(lk, until, [&] { return matching_bytes() >= coalesce_max_bytes(); });
+        // Wait for company only when calls are actually concurrent (the last batch had several
+        // callers, or others are queued now): a lone caller's calls never pay the window.
+        if (last_batch_ > 1 || queue_.size() > 1) {
+            const auto until = std::chrono::steady_clock::now() +
+                               std::chrono::microseconds(coalesce_window_us());
+            leader_cv_.wait_until(lk, until,
+                                  [&] { return matching_bytes() >= coalesce_max_bytes(); });
+        }
         std::vector<Req*> batch{r};
         size_t bytes = Impl::bytes(*r);
         for (auto it = queue_.begin(); it != queue_.end();) {
@@ -476,6 +482,7 @@ class Coalescer {
             }
         }
         batch_size_ = batch.size();
+        last_batch_ = batch.size();
         Arena& arena = arenas_[key.device];
         lk.unlock();
         const auto t0 = std::chrono::steady_clock::now();
@@ -535,7 +542,7 @@ class Coalescer {
     std::condition_variable leader_cv_;
     std::deque<Req*> queue_;
     bool leader_ = false;
-    size_t staged_ = 0, finished_ = 0, batch_size_ = 0;
+    size_t staged_ = 0, finished_ = 0, batch_size_ = 0, last_batch_ = 0;
     std::map<int, Arena> arenas_;  // per device; used by the current leader's batch only
 };
 
