@@ -328,8 +328,7 @@ int reconstruct_host(const cec_codec* cc, uint8_t* const* shards, const size_t* 
 // launch.  cec_part_encode / cec_sha256(_many) therefore go through a leader/follower queue:
 // the first caller to find no batch in progress becomes the leader, waits up to
 // CEC_COALESCE_US microseconds (default 200; only when calls are concurrent) for more requests
-// with its key (codec, chunk
-// length, device), and runs them as ONE batch:
+// with its key (codec, chunk length, device), and runs them as ONE batch:
 //   1. copy-in   every caller copies its own (pageable) input into the queue's pinned staging,
 //                in parallel on its own thread;
 //   2. launch    the leader moves the whole batch with one H2D copy, runs the fused
