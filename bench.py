@@ -108,6 +108,9 @@ def cpu_baseline(cfg, threads: int):
     total = min(total, 4096)
     sec = oracle.baseline_encode_sha(d, p, L, total, 2, threads, True, hashed)
     gbs = total * d * L / sec / 1e9
+    # one core (SURVEY.md §8d asks for it beside the all-cores figure): ~1.5 s of work
+    n1 = max(2, int(1.5 / max(per_part * threads, 1e-6)))
+    sec1 = oracle.baseline_encode_sha(d, p, L, n1, 2, 1, True, hashed)
     return {
         "value": round(gbs, 3),
         "unit": "GB/s",
@@ -117,6 +120,8 @@ def cpu_baseline(cfg, threads: int):
                   f"({'encode_sep + sha256 of all chunks' if hashed else 'encode_sep'}), "
                   f"{threads} threads, one part per task; {sec:.2f} s wall; "
                   f"SHA-NI={'yes' if oracle.has_shani() else 'no'}",
+        "single_core": {"value": round(n1 * d * L / sec1 / 1e9, 3), "unit": "GB/s",
+                        "sample": f"{n1} parts on 1 thread; {sec1:.2f} s"},
     }
 
 
