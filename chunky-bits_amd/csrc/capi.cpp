@@ -351,7 +351,7 @@ uint32_t coalesce_window_us() {
 size_t coalesce_max_bytes() {
     static const size_t b = [] {
         const char* e = std::getenv("CEC_COALESCE_MAX_MIB");
-        const size_t mib = e ? size_t(std::strtoull(e, nullptr, 10)) : 4096;
+        const size_t mib = e ? size_t(std::strtoull(e, nullptr, 10)) : 1024;
         return std::max<size_t>(mib, 1) << 20;
     }();
     return b;
@@ -407,13 +407,29 @@ struct ReqBase {
     size_t in_off = 0;      // byte offset in the pinned input staging
     size_t item0 = 0;       // sha: first item index; parts: parts in the batch
     Arena* arena = nullptr;
-    std::condition_variable cv;  // this caller's wake-ups
+    struct Batch* batch = nullptr;  // the batch this request runs in
+    std::condition_variable cv;     // this caller's wake-ups
 };
 
 // Impl: bytes(r) = input bytes; prepare(batch, arena) lays out + reserves; copy_in(r);
 // run(batch, arena) launches and waits; copy_out(r).
 // Wake-ups are targeted (one condition variable per request plus one for the leader) so a
 // batch of hundreds of callers costs O(batch) wake-ups, not O(batch^2).
+// One batch in flight: its size and copy counters, and the leader's wake-ups.
+struct Batch {
+    size_t size = 0, staged = 0, finished = 0;
+    std::condition_variable cv;
+};
+
+uint32_t coalesce_inflight() {
+    static const uint32_t n = [] {
+        const char* e = std::getenv("CEC_COALESCE_INFLIGHT");
+        const unsigned long v = e ? std::strtoul(e, nullptr, 10) : 4ul;
+        return uint32_t(std::min<unsigned long>(std::max<unsigned long>(v, 1ul), 16ul));
+    }();
+    return n;
+}
+
 template <typename Req, typename Impl>
 class Coalescer {
    public:
@@ -421,22 +437,22 @@ class Coalescer {
         g_calls.fetch_add(1, std::memory_order_relaxed);
         std::unique_lock<std::mutex> lk(mu_);
         queue_.push_back(r);
-        if (leader_) leader_cv_.notify_one();  // a gathering leader re-checks its batch size
+        if (gathering_) gather_cv_.notify_one();  // the gathering leader re-checks its batch
         for (;;) {
             if (r->phase == Phase::CopyIn) {
                 lk.unlock();
                 Impl::copy_in(*r);
                 lk.lock();
                 r->phase = Phase::Staged;
-                if (++staged_ == batch_size_) leader_cv_.notify_one();
+                if (++r->batch->staged == r->batch->size) r->batch->cv.notify_one();
             } else if (r->phase == Phase::CopyOut) {
                 lk.unlock();
                 if (r->status == CEC_OK) Impl::copy_out(*r);
                 lk.lock();
                 r->phase = Phase::Finished;
-                if (++finished_ == batch_size_) leader_cv_.notify_one();
+                if (++r->batch->finished == r->batch->size) r->batch->cv.notify_one();
                 break;
-            } else if (r->phase == Phase::Queued && !leader_) {
+            } else if (r->phase == Phase::Queued && !gathering_ && active_ < coalesce_inflight()) {
                 lead(r, lk);
                 break;
             } else {
@@ -448,10 +464,17 @@ class Coalescer {
     }
 
    private:
-    // Called with lk held; returns with r finished and the next queued request (if any) woken
-    // to lead the next batch.
+    // Wake the oldest queued request so it can lead the next batch (if a slot is free).
+    void wake_next() {
+        if (!queue_.empty()) queue_.front()->cv.notify_one();
+    }
+
+    // Called with lk held; returns with r finished.  Up to coalesce_inflight() leaders run their
+    // batches at once (one arena = pinned staging + device buffer + stream each), so the next
+    // batch gathers, copies and launches while earlier ones are still on the GPU.
     void lead(Req* r, std::unique_lock<std::mutex>& lk) {
-        leader_ = true;
+        ++active_;
+        gathering_ = true;
         const auto key = r->key();
         auto matching_bytes = [&] {
             size_t b = 0;
@@ -464,9 +487,10 @@ class Coalescer {
         if (last_batch_ > 1 || queue_.size() > 1) {
             const auto until = std::chrono::steady_clock::now() +
                                std::chrono::microseconds(coalesce_window_us());
-            leader_cv_.wait_until(lk, until,
+            gather_cv_.wait_until(lk, until,
                                   [&] { return matching_bytes() >= coalesce_max_bytes(); });
         }
+        Batch batch_state;
         std::vector<Req*> batch{r};
         size_t bytes = Impl::bytes(*r);
         for (auto it = queue_.begin(); it != queue_.end();) {
@@ -480,16 +504,19 @@ class Coalescer {
                 ++it;
             }
         }
-        batch_size_ = batch.size();
+        for (Req* q : batch) q->batch = &batch_state;
+        batch_state.size = batch.size();
         last_batch_ = batch.size();
-        Arena& arena = arenas_[key.device];
+        Arena* arena = take_arena(key.device);
+        gathering_ = false;
+        wake_next();  // the next batch can gather while this one runs
         lk.unlock();
         const auto t0 = std::chrono::steady_clock::now();
         auto t1 = t0, t2 = t0, t3 = t0;
-        int st = Impl::prepare(batch, arena);
+        int st = Impl::prepare(batch, *arena);
         if (st == CEC_OK) {
             lk.lock();
-            staged_ = 1;  // the leader's own copy, done below
+            batch_state.staged = 1;  // the leader's own copy, done below
             for (Req* q : batch)
                 if (q != r) {
                     q->phase = Phase::CopyIn;
@@ -499,16 +526,16 @@ class Coalescer {
             lk.unlock();
             Impl::copy_in(*r);
             lk.lock();
-            leader_cv_.wait(lk, [&] { return staged_ == batch_size_; });
+            batch_state.cv.wait(lk, [&] { return batch_state.staged == batch_state.size; });
             lk.unlock();
             t2 = std::chrono::steady_clock::now();
             g_launches.fetch_add(1, std::memory_order_relaxed);
-            st = Impl::run(batch, arena);
+            st = Impl::run(batch, *arena);
             t3 = std::chrono::steady_clock::now();
         }
         const std::string err = st == CEC_OK ? std::string() : g_last_error;
         lk.lock();
-        finished_ = 1;
+        batch_state.finished = 1;
         for (Req* q : batch) {
             q->status = st;
             q->err = err;
@@ -520,8 +547,8 @@ class Coalescer {
         lk.unlock();
         if (st == CEC_OK) Impl::copy_out(*r);
         lk.lock();
-        // the staging is reused by the next batch: wait for every copy-out
-        leader_cv_.wait(lk, [&] { return finished_ == batch_size_; });
+        // the arena is reused by a later batch: wait for every copy-out
+        batch_state.cv.wait(lk, [&] { return batch_state.finished == batch_state.size; });
         if (coalesce_trace()) {
             auto ms = [](auto a, auto b) {
                 return std::chrono::duration<double, std::milli>(b - a).count();
@@ -533,16 +560,31 @@ class Coalescer {
                          ms(t3, std::chrono::steady_clock::now()));
         }
         r->phase = Phase::Finished;
-        leader_ = false;
-        if (!queue_.empty()) queue_.front()->cv.notify_one();  // next leader
+        free_[key.device].push_back(arena);
+        --active_;
+        wake_next();
+    }
+
+    // A free arena of `device` (called with mu_ held; at most coalesce_inflight() are in use).
+    Arena* take_arena(int device) {
+        auto& free_list = free_[device];
+        if (free_list.empty()) {
+            arenas_.push_back(std::make_unique<Arena>());
+            return arenas_.back().get();
+        }
+        Arena* a = free_list.back();
+        free_list.pop_back();
+        return a;
     }
 
     std::mutex mu_;
-    std::condition_variable leader_cv_;
+    std::condition_variable gather_cv_;
     std::deque<Req*> queue_;
-    bool leader_ = false;
-    size_t staged_ = 0, finished_ = 0, batch_size_ = 0, last_batch_ = 0;
-    std::map<int, Arena> arenas_;  // per device; used by the current leader's batch only
+    bool gathering_ = false;
+    uint32_t active_ = 0;
+    size_t last_batch_ = 0;
+    std::vector<std::unique_ptr<Arena>> arenas_;  // owned; free lists per device below
+    std::map<int, std::vector<Arena*>> free_;
 };
 
 // ---- cec_sha256(_many): one request = n buffers ----
