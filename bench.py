@@ -72,6 +72,13 @@ CONFIGS = {
                 workload="C5 read side: 1 TiB synthetic object stream read back, RS(10,4), d random "
                          "chunks loaded per part, SHA-256 verify + reconstruct_data, pinned-host "
                          "staged batches of 256 parts, 4 slots in flight"),
+    # configs[2], device-resident read: FilePart::read_with_context batched -- d random chunks
+    # loaded per part (file_part.rs:86-122), SHA-256 verify + reconstruct_data of the missing data
+    # chunks (the decode runs speculatively beside the verification).
+    "c3r": dict(d=10, p=4, chunk=1 * MiB, parts=4096, op="read",
+                workload="C3 read: RS(10,4) read_with_context batched, d random chunks loaded per "
+                         "part, SHA-256 verify + reconstruct_data, 4096 parts x 1 MiB chunks per "
+                         "GPU"),
     # encode only (HBM roofline of the GF kernel alone).
     "c2enc": dict(d=10, p=4, chunk=1 * MiB, parts=4096, op="encode",
                   workload="RS(10,4) encode_sep only, 4096 parts x 1 MiB chunks per GPU"),
@@ -352,10 +359,24 @@ def main():
             pres[i, idx] = 0
         present = bytes(pres.flatten().tolist())
         missing_bytes = int((t - pres.sum(1)).sum().item()) * L
+    elif cfg["op"] == "read":
+        ce.encode_hash_batch(codec, batch, digests.data_ptr(), stream)
+        # d random chunks loaded per part (the reference's read); the others are rebuilt (data)
+        # or left alone (parity) in place every step
+        g = torch.Generator().manual_seed(4321 + rank)
+        pres = torch.zeros((n_parts, t), dtype=torch.uint8)
+        for i in range(n_parts):
+            pres[i, torch.randperm(t, generator=g)[:d]] = 1
+        present = bytes(pres.flatten().tolist())
+        # the chunks that were not loaded start zeroed, so the first step really rebuilds them
+        buf.mul_(pres.to(device).view(n_parts, t, 1))
+        missing_data = int((d - pres[:, :d].sum(1)).sum().item())
+        touched = int(((d - pres[:, :d].sum(1)) > 0).sum().item())
 
     # One step = the hot path over the batch.  Each library call is one kernel launch on
     # `stream`; events bracket each launch so per-kernel averages come from the timed steps.
     fused = cfg["op"] == "encode_hash" and not args.separate
+    read_status = []
 
     def step(evs=None):
         if cfg["op"] == "encode_hash" and fused:
@@ -379,6 +400,13 @@ def main():
             ce.encode_batch(codec, batch, stream)
             if evs is not None:
                 evs[1].record(stream)
+        elif cfg["op"] == "read":
+            if evs is not None:
+                evs[0].record(stream)
+            _, st = ce.read_batch(codec, batch, present, digests.data_ptr(), stream)
+            if evs is not None:
+                evs[1].record(stream)
+            read_status.append(sum(1 for x in st if x != ce.OK))
         else:
             if evs is not None:
                 evs[0].record(stream)
@@ -429,6 +457,13 @@ def main():
         kernels["rs_apply_kernel"] = {"ms": round(enc_ms, 4),
                                       "algorithmic_bytes": n_parts * t * L,
                                       "GBs": round(n_parts * t * L / enc_ms / 1e6, 1)}
+    elif cfg["op"] == "read":
+        # one read_batch call: verify (sha256_lane_kernel, d chunks per part) on the caller's
+        # stream, the speculative decode (rs_apply_var_kernel) beside it on a side stream
+        ms = avg_ms(0, 1)
+        algo = n_parts * d * (L + 32) + touched * d * L + missing_data * L
+        kernels["read_batch(verify+decode)"] = {"ms": round(ms, 4), "algorithmic_bytes": algo,
+                                                "GBs": round(algo / ms / 1e6, 1)}
     else:
         rec_ms = avg_ms(0, 1)
         # each part with k missing reads d chunks and writes k: (d*parts_touched + missing)
@@ -443,14 +478,17 @@ def main():
     traffic = measured_traffic(args.config, dom_name, n_parts == CONFIGS[args.config]["parts"])
 
     valu = None
-    if cfg["op"] == "encode_hash":
+    if cfg["op"] in ("encode_hash", "read"):
         # useful SHA work: one lane-block per 64-byte block of every chunk (incl. FIPS padding)
         blocks = L // 64 + (1 if L % 64 + 9 <= 64 else 2)
-        sha_ms = kernels["encode_hash_kernel" if fused else "sha256_kernel"]["ms"]
-        wave_inst = n_parts * t * blocks * SHA_VALU_PER_BLOCK / 64
+        sha_kernel = ("read_batch(verify+decode)" if cfg["op"] == "read" else
+                      "encode_hash_kernel" if fused else "sha256_kernel")
+        sha_ms = kernels[sha_kernel]["ms"]
+        hashed = d if cfg["op"] == "read" else t
+        wave_inst = n_parts * hashed * blocks * SHA_VALU_PER_BLOCK / 64
         achieved_g = wave_inst / (sha_ms / 1e3) / 1e9
         peak_g = MI355X_SIMDS * MI355X_CLOCK_GHZ / SHA_SIMD_CYCLES
-        valu = {"bound": "valu", "kernel": "encode_hash_kernel" if fused else "sha256_kernel",
+        valu = {"bound": "valu", "kernel": sha_kernel,
                 "achieved": round(achieved_g, 1), "peak": round(peak_g, 1),
                 "unit": "G wave64-inst/s", "frac": round(achieved_g / peak_g, 4),
                 "basis": f"SHA-256: {SHA_VALU_PER_BLOCK} VALU/64-B block/lane, "
@@ -458,7 +496,17 @@ def main():
                          f"{MI355X_SIMDS} SIMDs x {MI355X_CLOCK_GHZ} GHz"}
 
     ok = None
-    if args.check and rank == 0 and cfg["op"] != "reconstruct":
+    if args.check and rank == 0 and cfg["op"] == "read":
+        import numpy as np
+        import oracle
+        k = n_parts // 2
+        host = buf[k].cpu().numpy()
+        pr = present[k * t:(k + 1) * t]
+        st, out = oracle.reconstruct(d, p, [host[i] if pr[i] else None for i in range(t)],
+                                     data_only=True)
+        ok = (st == 0 and not any(read_status) and
+              all(np.array_equal(out[i], host[i]) for i in range(d)))
+    elif args.check and rank == 0 and cfg["op"] != "reconstruct":
         import hashlib
         import numpy as np
         import oracle
@@ -508,7 +556,7 @@ def main():
             line["valu_roofline"] = valu
         if ok is not None:
             line["check_vs_oracle"] = bool(ok)
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and cfg["op"] in ("encode_hash", "encode"):
             threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
             line["cpu_baseline"] = cpu_baseline(cfg, threads)
         print(json.dumps(line), flush=True)

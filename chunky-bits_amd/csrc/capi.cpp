@@ -1034,8 +1034,10 @@ int cec_encode_hash_batch(const cec_codec* cc, const cec_part_batch* b, uint8_t*
     return CEC_OK;
 }
 
-int cec_reconstruct_batch(const cec_codec* cc, const cec_part_batch* b, const uint8_t* present,
-                          int data_only, void* stream) {
+// cec_reconstruct_batch with each decode block reserving lds_reserve bytes of LDS (see
+// ApplyParams::lds_reserve).
+static int reconstruct_batch(const cec_codec* cc, const cec_part_batch* b, const uint8_t* present,
+                             int data_only, void* stream, uint32_t lds_reserve) {
     if (!cc || !present) return CEC_ERR_INVALID_ARGUMENT;
     CEC_TRY(batch_ok(b));
     if (b->n_parts == 0) return CEC_OK;
@@ -1107,6 +1109,7 @@ int cec_reconstruct_batch(const cec_codec* cc, const cec_part_batch* b, const ui
         a.n_parts = uint32_t(launches[i].count);
         a.d = uint32_t(d);
         a.n_rows = launches[i].n_out;
+        a.lds_reserve = lds_reserve;
         hipError_t e = launches[i].n_out ? launch_rs_apply(a, vec, s)
                                          : launch_rs_apply_var(a, vec, s);
         if (e != hipSuccess) status = hip_fail(e, "launch_rs_apply");
@@ -1114,6 +1117,11 @@ int cec_reconstruct_batch(const cec_codec* cc, const cec_part_batch* b, const ui
     hipError_t e = hipFreeAsync(dwords, s);
     if (status == CEC_OK && e != hipSuccess) status = hip_fail(e, "hipFreeAsync");
     return status;
+}
+
+int cec_reconstruct_batch(const cec_codec* c, const cec_part_batch* b, const uint8_t* present,
+                          int data_only, void* stream) {
+    return reconstruct_batch(c, b, present, data_only, stream, 0);
 }
 
 int cec_verify_batch(const cec_part_batch* b, size_t first_chunk, size_t n_chunks,
@@ -1140,8 +1148,95 @@ int cec_verify_batch(const cec_part_batch* b, size_t first_chunk, size_t n_chunk
 
 namespace {
 
-// Shared body of cec_read_batch / cec_resilver_batch: verify the loaded chunks, then rebuild
-// from the first d verified chunks of each part.
+// Side stream of the speculative decode in cec_read_batch / cec_resilver_batch (per thread and
+// device), with the fork/join events that order it against the caller's stream.
+struct SideCtx {
+    hipStream_t stream = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+thread_local std::unordered_map<int, SideCtx> t_side;
+
+int side_ctx(SideCtx** out) {
+    int dev = 0;
+    CEC_TRY(current_device(&dev));
+    SideCtx& c = t_side[dev];
+    if (!c.stream) HIP_TRY(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+    if (!c.fork) HIP_TRY(hipEventCreateWithFlags(&c.fork, hipEventDisableTiming));
+    if (!c.join) HIP_TRY(hipEventCreateWithFlags(&c.join, hipEventDisableTiming));
+    *out = &c;
+    return CEC_OK;
+}
+
+// LDS each speculative-decode block reserves (A/B knob CEC_SPEC_LDS_KIB).  100 KiB keeps decode
+// blocks off the CUs holding SHA workgroups (>= 64 KiB each) and runs one per free CU: a
+// low-intensity decode spread under the SHA chains.  Measured on the c3r read (4 096 parts,
+// RS(10,4), d loaded, tools/c3r_ab.sh): 43.2 ms vs 45.3 (65 KiB: two per free CU) vs 46.5 (none:
+// decode everywhere, done in 17 ms, but the SHA chains slow from 42.6 to 46.4 ms beside it) vs
+// 53.0 ms without speculation.
+uint32_t decode_lds() {
+    const char* e = std::getenv("CEC_SPEC_LDS_KIB");
+    return e ? uint32_t(std::atoi(e)) * 1024u : 100u * 1024u;
+}
+
+// CEC_READ_SPECULATE=0 (A/B knob): verify, wait, then decode from the verified chunks only.
+bool read_speculate() {
+    const char* e = std::getenv("CEC_READ_SPECULATE");
+    return !(e && e[0] == '0');
+}
+
+// DataVerifier::verify of the loaded chunks (present_host[k*t + i] != 0) of a batch: ok[item] =
+// digest matches (ok of the others is left as is).  The loaded chunks are packed into a
+// compacted item list, so a read with d of d+p chunks loaded runs d/(d+p) of the waves of a
+// strided launch with skipped lanes (a SHA wave costs the same with idle lanes), which leaves
+// SIMDs free for the decode running beside it.
+int verify_loaded(const cec_part_batch* b, size_t t, const uint8_t* present_host,
+                  const uint8_t* expected, uint8_t* ok, hipStream_t s) {
+    const size_t n = b->n_parts * t;
+    const char* knob = std::getenv("CEC_VERIFY_COMPACT");
+    if (knob && knob[0] == '0') {  // A/B: strided launch with the skipped lanes
+        uint8_t* dpresent = nullptr;
+        HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&dpresent), n, s));
+        HIP_TRY(hipMemcpyAsync(dpresent, present_host, n, hipMemcpyHostToDevice, s));
+        CEC_TRY(cec_verify_batch(b, 0, t, dpresent, expected, ok, s));
+        HIP_TRY(hipFreeAsync(dpresent, s));
+        return CEC_OK;
+    }
+    std::vector<uint32_t> items;
+    items.reserve(n);
+    for (size_t i = 0; i < n; ++i)
+        if (present_host[i]) items.push_back(uint32_t(i));
+    if (items.empty()) return CEC_OK;
+    const uint32_t n_items = uint32_t(items.size());
+    uint32_t* ditems = nullptr;
+    CEC_TRY(upload_words(std::move(items), s, &ditems));
+    ShaParams h{};
+    h.base = b->base;
+    h.part_stride = b->part_stride;
+    h.chunk_stride = b->chunk_stride;
+    h.len = b->chunk_len;
+    h.n_parts = uint32_t(b->n_parts);
+    h.first_chunk = 0;
+    h.n_chunks = uint32_t(t);
+    h.expected = expected;
+    h.ok = ok;
+    h.items = ditems;
+    h.n_items = n_items;
+    hipError_t e = launch_sha256(h, aligned16(b->base, b->part_stride, b->chunk_stride), s);
+    const hipError_t f = hipFreeAsync(ditems, s);
+    if (e != hipSuccess) return hip_fail(e, "launch_sha256 (verify)");
+    if (f != hipSuccess) return hip_fail(f, "hipFreeAsync");
+    return CEC_OK;
+}
+
+// Shared body of cec_read_batch / cec_resilver_batch.  The result is the reference's: rebuild
+// from the first d VERIFIED chunks of each part (file_part.rs:98-128 keeps only chunks whose hash
+// matched).  The decode does not wait for the verdict: the pattern is known from the loaded
+// flags, so it runs speculatively from the first d LOADED chunks on a side stream, concurrently
+// with the SHA-256 verification (which leaves 384 of 1 024 SIMDs idle on a 4 096-part RS(10,4)
+// read: 40 960 chains = 640 waves).  Both only read the loaded chunks and the decode writes only
+// chunks that were not loaded, so they do not race.  When every loaded chunk verifies (the
+// common case) the speculative result is the final one; a part with a loaded chunk that failed
+// is decoded again from its verified chunks, which rewrites every chunk the first pass wrote.
 int verify_then_reconstruct(const cec_codec* c, const cec_part_batch* b,
                             const uint8_t* present_host, const uint8_t* expected,
                             uint8_t* verified_host, int* part_status, bool data_only,
@@ -1151,29 +1246,67 @@ int verify_then_reconstruct(const cec_codec* c, const cec_part_batch* b,
     CEC_TRY(batch_ok(b));
     if (b->n_parts == 0) return CEC_OK;
     if (b->chunk_len == 0) return CEC_EMPTY_SHARD;
-    const size_t t = c->d + c->p, n = b->n_parts * t;
+    const size_t d = c->d, t = c->d + c->p, n = b->n_parts * t;
     if (n > 0xFFFFFFFFull) return CEC_ERR_INVALID_ARGUMENT;
-    uint8_t* flags = nullptr;  // [present | ok]
-    HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&flags), 2 * n, s));
-    HIP_TRY(hipMemcpyAsync(flags, present_host, n, hipMemcpyHostToDevice, s));
-    int st = cec_verify_batch(b, 0, t, flags, expected, flags + n, s);
+    const bool speculate = read_speculate();
+    uint8_t* ok = nullptr;  // device verification flags
+    HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&ok), n, s));
+    HIP_TRY(hipMemsetAsync(ok, 0, n, s));
+    // Fork point: the caller's work on s so far (the chunks).
+    SideCtx* side = nullptr;
+    if (speculate) {
+        CEC_TRY(side_ctx(&side));
+        HIP_TRY(hipEventRecord(side->fork, s));
+    }
+    // Verification goes first so its long-lived workgroups claim their CUs (one or two per CU)
+    // before the decode's blocks take the CUs left free.
+    int st = verify_loaded(b, t, present_host, expected, ok, s);
+    if (st == CEC_OK && speculate) {
+        // Parts with fewer than d loaded chunks cannot be decoded: left out (mask all ones).
+        std::vector<uint8_t> spec(present_host, present_host + n);
+        for (size_t k = 0; k < b->n_parts; ++k) {
+            const size_t loaded =
+                size_t(std::count_if(spec.begin() + k * t, spec.begin() + (k + 1) * t,
+                                     [](uint8_t f) { return f != 0; }));
+            if (loaded < d) std::fill(spec.begin() + k * t, spec.begin() + (k + 1) * t, uint8_t(1));
+        }
+        hipError_t e = hipStreamWaitEvent(side->stream, side->fork, 0);
+        if (e != hipSuccess) st = hip_fail(e, "speculative decode fork");
+        if (st == CEC_OK)
+            st = reconstruct_batch(c, b, spec.data(), data_only ? 1 : 0, side->stream,
+                                   decode_lds());
+        if (st == CEC_OK) {
+            e = hipEventRecord(side->join, side->stream);
+            if (e == hipSuccess) e = hipStreamWaitEvent(s, side->join, 0);
+            if (e != hipSuccess) st = hip_fail(e, "speculative decode join");
+        }
+    }
     if (st == CEC_OK) {
-        hipError_t e = hipMemcpyAsync(verified_host, flags + n, n, hipMemcpyDeviceToHost, s);
+        hipError_t e = hipMemcpyAsync(verified_host, ok, n, hipMemcpyDeviceToHost, s);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) st = hip_fail(e, "verify readback");
     }
-    (void)hipFreeAsync(flags, s);
+    (void)hipFreeAsync(ok, s);
     if (st != CEC_OK) return st;
     // Parts with fewer than d verified chunks cannot be decoded (the reference's read returns
-    // the part short / resilver reports it); rebuild the others.
-    std::vector<uint8_t> pres(verified_host, verified_host + n);
+    // the part short / resilver reports it).  Decode (again) the parts whose loaded chunks did
+    // not all verify — or every part, without speculation.
+    std::vector<uint8_t> pres(n, uint8_t(1));
+    bool any = false;
     for (size_t k = 0; k < b->n_parts; ++k) {
         size_t good = 0;
-        for (size_t i = 0; i < t; ++i) good += pres[k * t + i] ? 1 : 0;
-        part_status[k] = good >= c->d ? CEC_OK : CEC_TOO_FEW_SHARDS_PRESENT;
-        if (good < c->d) std::fill(pres.begin() + k * t, pres.begin() + (k + 1) * t, uint8_t(1));
+        bool bad = false;
+        for (size_t i = 0; i < t; ++i) {
+            good += verified_host[k * t + i] ? 1 : 0;
+            bad |= present_host[k * t + i] && !verified_host[k * t + i];
+        }
+        part_status[k] = good >= d ? CEC_OK : CEC_TOO_FEW_SHARDS_PRESENT;
+        if (good >= d && (bad || !speculate)) {
+            std::copy(verified_host + k * t, verified_host + (k + 1) * t, pres.begin() + k * t);
+            any = true;
+        }
     }
-    return cec_reconstruct_batch(c, b, pres.data(), data_only ? 1 : 0, s);
+    return any ? cec_reconstruct_batch(c, b, pres.data(), data_only ? 1 : 0, s) : CEC_OK;
 }
 
 }  // namespace

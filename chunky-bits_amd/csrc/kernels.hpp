@@ -21,6 +21,10 @@ struct ApplyParams {
     uint32_t n_parts;
     uint32_t d;
     uint32_t n_rows;  // n_out shared by every pattern of this launch
+    // Dynamic LDS each workgroup reserves (never touched; 0 = none).  Above 64 KiB a block
+    // cannot share a CU with a SHA-256 lane-kernel workgroup (>= 64 KiB reserved each), which
+    // keeps a decode running beside a verification off the SHA waves' SIMDs.
+    uint32_t lds_reserve;
 };
 
 // SHA-256 of n_parts * n_chunks chunks.  Strided mode: chunk (k, first_chunk + c) at
@@ -43,6 +47,11 @@ struct ShaParams {
     const uint8_t* present;
     const uint8_t* expected;
     uint8_t* ok;
+    // Compacted item list (nullable, lane kernel only): lane g hashes item items[g] of the
+    // strided batch, g < n_items; present is ignored and unlisted items are not touched.  Packs
+    // the loaded chunks of a read into full waves (RS(10,4), d of 14 loaded: 640 waves, not 896).
+    const uint32_t* items;
+    uint32_t n_items;
 };
 
 struct FillParams {

@@ -275,6 +275,15 @@ template <int K> struct Tune {
     static constexpr bool kNt = K >= 0 && (K & 1);
 };
 
+// Lets `kernel` reserve `bytes` of dynamic LDS (a host-side attribute; set on every such launch,
+// since the instantiations share one function-pointer type).
+template <typename K>
+bool allow_lds(K kernel, uint32_t bytes) {
+    return bytes <= 64 * 1024 ||
+           hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, int(bytes)) == hipSuccess;
+}
+
 template <int RG>
 hipError_t launch_rg(const ApplyParams& a, uint32_t row_base, uint32_t groups, bool vec16,
                      hipStream_t s) {
@@ -282,8 +291,9 @@ hipError_t launch_rg(const ApplyParams& a, uint32_t row_base, uint32_t groups, b
     const dim3 grid(a.n_parts * tiles, groups);
     return dispatch_apply(vec16, [&](auto k) {
         using T = Tune<decltype(k)::value>;
-        hipLaunchKernelGGL((rs_apply_kernel<RG, T::kVec, T::kGroup, T::kV, T::kNt>), grid,
-                           dim3(kApplyThreads), 0, s, a, tiles, row_base);
+        auto* kern = &rs_apply_kernel<RG, T::kVec, T::kGroup, T::kV, T::kNt>;
+        if (!allow_lds(kern, a.lds_reserve)) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(kern, grid, dim3(kApplyThreads), a.lds_reserve, s, a, tiles, row_base);
         return hipGetLastError();
     });
 }
@@ -325,8 +335,9 @@ hipError_t launch_rs_apply_var(const ApplyParams& a, bool vec16, hipStream_t s) 
     const dim3 grid(a.n_parts * tiles);
     return dispatch_apply(vec16, [&](auto k) {
         using T = Tune<decltype(k)::value>;
-        hipLaunchKernelGGL((rs_apply_var_kernel<T::kVec, T::kGroup, T::kV, T::kNt>), grid,
-                           dim3(kApplyThreads), 0, s, a, tiles);
+        auto* kern = &rs_apply_var_kernel<T::kVec, T::kGroup, T::kV, T::kNt>;
+        if (!allow_lds(kern, a.lds_reserve)) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(kern, grid, dim3(kApplyThreads), a.lds_reserve, s, a, tiles);
         return hipGetLastError();
     });
 }

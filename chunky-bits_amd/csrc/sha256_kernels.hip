@@ -75,11 +75,16 @@ constexpr int kLaneThreads = 256;
 template <bool VEC>
 __global__ __launch_bounds__(kLaneThreads) void sha256_lane_kernel(ShaParams a) {
     extern __shared__ uint32_t cu_reservation[];  // never touched: occupancy control only
-    const uint32_t item = blockIdx.x * uint32_t(kLaneThreads) + threadIdx.x;
-    if (item >= a.n_parts * a.n_chunks) return;
-    if (a.present && !a.present[item]) {
-        if (a.ok) a.ok[item] = 0;
-        return;
+    uint32_t item = blockIdx.x * uint32_t(kLaneThreads) + threadIdx.x;
+    if (a.items) {
+        if (item >= a.n_items) return;
+        item = a.items[item];
+    } else {
+        if (item >= a.n_parts * a.n_chunks) return;
+        if (a.present && !a.present[item]) {
+            if (a.ok) a.ok[item] = 0;
+            return;
+        }
     }
     const uint8_t* p;
     uint64_t len;
@@ -369,7 +374,7 @@ hipError_t launch_lane(const ShaParams& a, bool vec16, hipStream_t s, bool one_p
                                    int(kCuReservation)) == hipSuccess;
     }();
     if (!attr_ok) return hipErrorInvalidValue;
-    const uint64_t total = uint64_t(a.n_parts) * a.n_chunks;
+    const uint64_t total = a.items ? a.n_items : uint64_t(a.n_parts) * a.n_chunks;
     dim3 grid(uint32_t((total + kLaneThreads - 1) / kLaneThreads));
     // One workgroup (one wave per SIMD) per CU while the grid fits the chip in one pass.  When
     // it does not, a second co-resident wave per SIMD turns the lone wave's issue-bound ~6000
@@ -412,8 +417,9 @@ int device_cus() {
 // CEC_SHA_VARIANT (tuning knob, read per launch): 1 = one lane per chunk (default), 2 = split
 // producer/rounds waves.
 hipError_t launch_sha256(const ShaParams& a, bool vec16, hipStream_t s) {
-    const uint64_t total = uint64_t(a.n_parts) * a.n_chunks;
+    const uint64_t total = a.items ? a.n_items : uint64_t(a.n_parts) * a.n_chunks;
     if (total == 0) return hipSuccess;
+    if (a.items) return launch_lane(a, vec16, s);
     // verify mode with absent chunks is lane-kernel only (the split kernel has no skip path)
     const int v = sha_variant();
     if (v == 2 && !a.present) return launch_split(a, vec16, s);

@@ -194,8 +194,11 @@ int cec_verify_batch(const cec_part_batch* batch, size_t first_chunk, size_t n_c
  * chunks (present: HOST flags, n_parts*(d+p)) against expected (DEVICE digests, part-major,
  * chunks in order), then reconstruct_data from the first d verified chunks.  Outputs (HOST):
  * verified[k*(d+p)+i] = verification result; part_status[k] = CEC_OK, or
- * CEC_TOO_FEW_SHARDS_PRESENT when fewer than d chunks verified (that part is left untouched).
- * Waits on `stream` once, for the verification flags that decide the decode. */
+ * CEC_TOO_FEW_SHARDS_PRESENT when fewer than d chunks verified (its loaded chunks are left
+ * untouched; its other chunks are unspecified).  The decode runs speculatively from the first d
+ * LOADED chunks, concurrently with the verification, and parts with a loaded chunk that failed
+ * are decoded again from their verified chunks, so the result is always the verified decode.
+ * Waits on `stream` once, for the verification flags; the re-decode (if any) is queued on it. */
 int cec_read_batch(const cec_codec* codec, const cec_part_batch* batch, const uint8_t* present,
                    const uint8_t* expected, uint8_t* verified, int* part_status, void* stream);
 /* FilePart::resilver compute (file_part.rs:266-308): as cec_read_batch over all d+p chunks,

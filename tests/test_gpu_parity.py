@@ -656,7 +656,12 @@ def test_verify_batch_flags():
     assert torch.equal(ok.cpu(), want)
 
 
-def test_read_batch_restores_data_and_reports_undecodable_parts():
+@pytest.mark.parametrize("speculate", ["1", "0"])
+def test_read_batch_restores_data_and_reports_undecodable_parts(speculate, monkeypatch):
+    """file_part.rs:86-129 batched.  speculate=1: the decode runs from the loaded chunks
+    alongside verification and is redone for parts with a failed chunk; 0: verify, then decode
+    (CEC_READ_SPECULATE A/B knob).  Both must give the verified decode."""
+    monkeypatch.setenv("CEC_READ_SPECULATE", speculate)
     d, p, L, n = 10, 4, 4096 + 5, 12
     rs, buf, batch, dig = _encoded_batch(d, p, L, n, 41)
     t = d + p
@@ -666,19 +671,71 @@ def test_read_batch_restores_data_and_reports_undecodable_parts():
     buf[1, 2, 100] ^= 0xFF           # a fetched chunk that fails its hash
     present[2, [0, 1, 2, 3, 4]] = 0  # 9 chunks left < d: undecodable
     buf[4, 13, 0] ^= 1               # corrupt parity: data intact, nothing to rebuild
-    for k, i in [(0, 0), (0, 3), (2, 0)]:
+    present[5, 1] = 0                # missing data chunk AND a corrupt chunk among the first d
+    buf[5, 4, 7] ^= 0x10             # loaded: the speculative decode used it, must be redone
+    present[6, [0, 1, 2, 3]] = 0     # exactly d loaded, one fails: < d verified, undecodable
+    buf[6, 5, 0] ^= 0x80
+    present[7, [10, 11, 12, 13]] = 0  # only the d data chunks loaded: nothing to rebuild
+    present[8, [1, 6, 10, 12]] = 0   # d random chunks (the reference's read), one of them
+    buf[8, 13, 9] ^= 2               # (parity 13) corrupt: 9 verified, undecodable
+    for k, i in [(0, 0), (0, 3), (2, 0), (5, 1), (8, 1), (8, 6)]:
         buf[k, i] = 0
+    before = buf.cpu()
     verified, status = ce.read_batch(rs, batch, present.tobytes(), dig.data_ptr())
     torch.cuda.synchronize()
     v = np.frombuffer(verified, np.uint8).reshape(n, t)
     assert v[1, 2] == 0 and v[0, 0] == 0 and v[4, 13] == 0 and v[3].all()
-    assert status[2] == ce.TOO_FEW_SHARDS_PRESENT
-    assert all(status[k] == ce.OK for k in range(n) if k != 2)
+    assert v[5, 4] == 0 and v[5, 1] == 0 and v[6, 5] == 0 and v[8, 13] == 0
+    bad = {2, 6, 8}                   # part 8: 9 verified after losing parity 13
+    assert [status[k] for k in sorted(bad)] == [ce.TOO_FEW_SHARDS_PRESENT] * 3
+    assert all(status[k] == ce.OK for k in range(n) if k not in bad)
     got, want = buf.cpu(), ref.cpu()
     for k in range(n):
-        if k == 2:
+        if k in bad:
+            # loaded chunks of an undecodable part are never written
+            for i in range(t):
+                if present[k, i]:
+                    assert torch.equal(got[k, i], before[k, i]), (k, i)
             continue
         assert torch.equal(got[k, :d], want[k, :d]), k   # data chunks are the read's output
+
+
+@pytest.mark.parametrize("speculate", ["1", "0"])
+def test_read_batch_random_patterns_vs_oracle(speculate, monkeypatch):
+    """d random chunks loaded per part (reader.rs / file_part.rs:86-122), a few corrupted;
+    the rebuilt data chunks equal the oracle's reconstruct_data from the verified chunks."""
+    monkeypatch.setenv("CEC_READ_SPECULATE", speculate)
+    d, p, L, n = 10, 4, 1 << 12, 64
+    rs, buf, batch, dig = _encoded_batch(d, p, L, n, 43)
+    t = d + p
+    ref = buf.cpu().numpy().copy()
+    rng = np.random.default_rng(7)
+    present = np.zeros((n, t), dtype=np.uint8)
+    for k in range(n):
+        present[k, rng.choice(t, size=d + int(rng.integers(0, p + 1)), replace=False)] = 1
+    host = buf.cpu().numpy()
+    host[present == 0] = 0
+    corrupt = rng.choice(n, size=8, replace=False)
+    for k in corrupt:
+        i = int(rng.choice(np.flatnonzero(present[k])))
+        host[k, i, int(rng.integers(0, L))] ^= 1 << int(rng.integers(0, 8))
+    buf.copy_(torch.from_numpy(host))
+    verified, status = ce.read_batch(rs, batch, present.tobytes(), dig.data_ptr())
+    torch.cuda.synchronize()
+    v = np.frombuffer(verified, np.uint8).reshape(n, t)
+    got = buf.cpu().numpy()
+    for k in range(n):
+        good = v[k].astype(bool)
+        assert np.array_equal(good, present[k].astype(bool) & (host[k] == ref[k]).all(1)), k
+        if good.sum() < d:
+            assert status[k] == ce.TOO_FEW_SHARDS_PRESENT
+            continue
+        assert status[k] == ce.OK
+        shards = [ref[k, i] if good[i] else None for i in range(t)]
+        st, out = oracle.reconstruct(d, p, shards, data_only=True)
+        assert st == 0
+        for i in range(d):
+            assert np.array_equal(got[k, i], out[i]), (k, i)
 
 
 def test_resilver_batch_cluster_style():

@@ -5,6 +5,7 @@ timeout -k 10 240 python -u bench.py --check > gpurun_out/bench_c2.log 2>&1 && \
 timeout -k 10 200 python -u bench.py --config c2 --separate --no-cpu-baseline --check > gpurun_out/bench_c2sep.log 2>&1 && \
 timeout -k 10 200 python -u bench.py --config c2enc --no-cpu-baseline --check > gpurun_out/bench_c2enc.log 2>&1 && \
 timeout -k 10 200 python -u bench.py --config c3 --no-cpu-baseline > gpurun_out/bench_c3.log 2>&1 && \
+timeout -k 10 200 python -u bench.py --config c3r --check > gpurun_out/bench_c3r.log 2>&1 && \
 timeout -k 10 200 python -u bench.py --config c4 --check > gpurun_out/bench_c4.log 2>&1 && \
 timeout -k 10 300 python -u bench.py --config c5 --stream-gib 128 > gpurun_out/bench_c5.log 2>&1 && \
 timeout -k 10 300 python -u bench.py --config c5r --stream-gib 128 --check > gpurun_out/bench_c5r.log 2>&1 && \
