@@ -319,6 +319,18 @@ int reconstruct_host(const cec_codec* cc, uint8_t* const* shards, const size_t* 
     return CEC_OK;
 }
 
+// Fused encode+hash kernel or encode kernel + SHA kernel for a batch of `chunks` chunks (d+p per
+// part).  The fused kernel reads every byte once and wins when the SHA lanes fill the chip; a
+// small batch leaves most SIMDs idle, and the split SHA kernel's lower per-chain latency (31 vs
+// 42 ms per MiB) wins while the encode's extra pass is negligible.  CEC_FUSED (A/B knob): 0 =
+// always separate, 1 = always fused where supported.
+bool prefer_fused(size_t chunks) {
+    const char* e = std::getenv("CEC_FUSED");
+    if (e && e[0] == '0') return false;
+    if (e && e[0] == '1') return true;
+    return !use_split(chunks);
+}
+
 // ------------------------------------------------------------------------------------------
 // Per-call coalescing ("a batch queue behind the per-part call").
 //
@@ -421,10 +433,16 @@ struct Batch {
     std::condition_variable cv;
 };
 
+// Batches on the GPU at once (CEC_COALESCE_INFLIGHT, 1..16; default 1).  More than one lets the
+// next batch gather and copy while earlier ones run, but a leader then starts as soon as an arena
+// is free, and since a launch costs one chunk's SHA chain whatever its size, the callers split
+// into ever smaller batches that each pay it: measured on one box, interleaved
+// (profiles/r1y_percall_ab.log), 100 threads 7.1-8.2 GB/s with 1 vs 3.6-3.8 with 4, 400 threads
+// 6.9-7.9 vs 6.0-7.1.
 uint32_t coalesce_inflight() {
     static const uint32_t n = [] {
         const char* e = std::getenv("CEC_COALESCE_INFLIGHT");
-        const unsigned long v = e ? std::strtoul(e, nullptr, 10) : 4ul;
+        const unsigned long v = e ? std::strtoul(e, nullptr, 10) : 1ul;
         return uint32_t(std::min<unsigned long>(std::max<unsigned long>(v, 1ul), 16ul));
     }();
     return n;
@@ -482,9 +500,9 @@ class Coalescer {
                 if (q->key() == key) b += Impl::bytes(*q);
             return b;
         };
-        // Wait for company only when calls are actually concurrent (the last batch had several
-        // callers, or others are queued now): a lone caller's calls never pay the window.
         if (last_batch_ > 1 || queue_.size() > 1) {
+            // Wait for company only when calls are actually concurrent (the last batch had several
+            // callers, or others are queued now): a lone caller's calls never pay the window.
             const auto until = std::chrono::steady_clock::now() +
                                std::chrono::microseconds(coalesce_window_us());
             gather_cv_.wait_until(lk, until,
@@ -707,7 +725,7 @@ struct PartImpl {
         hipStream_t s = a.dev.stream;
         HIP_TRY(hipMemcpy2DAsync(dbase, t * cs, a.in.ptr, d * cs, d * cs, B,
                                  hipMemcpyHostToDevice, s));
-        if (fused_covers(uint32_t(d), uint32_t(p), L)) {
+        if (fused_covers(uint32_t(d), uint32_t(p), L) && prefer_fused(B * t)) {
             FusedParams f{};
             f.base = dbase;
             f.part_stride = t * cs;
@@ -1009,10 +1027,9 @@ int cec_encode_hash_batch(const cec_codec* cc, const cec_part_batch* b, uint8_t*
     if (b->chunk_len == 0) return CEC_EMPTY_SHARD;
     if (b->n_parts * (cc->d + cc->p) > 0xFFFFFFFFull) return CEC_ERR_INVALID_ARGUMENT;
     cec_codec* c = const_cast<cec_codec*>(cc);
-    const char* env = std::getenv("CEC_FUSED");  // tuning knob: 0 = separate kernels
     const bool fused = fused_covers(uint32_t(c->d), uint32_t(c->p), b->chunk_len) &&
                        aligned16(b->base, b->part_stride, b->chunk_stride) &&
-                       !(env && env[0] == '0');
+                       prefer_fused(b->n_parts * (c->d + c->p));
     if (!fused) {
         CEC_TRY(cec_encode_batch(c, b, stream));
         return cec_sha256_batch(b, 0, c->d + c->p, digests, stream);

@@ -89,6 +89,10 @@ bool fused_supported(uint32_t d, uint32_t p);
 bool fused_covers(uint32_t d, uint32_t p, uint64_t len);
 hipError_t launch_encode_hash(const FusedParams& a, bool vec16, hipStream_t s);
 hipError_t launch_sha256(const ShaParams& a, bool vec16, hipStream_t s);
+// Whether launch_sha256 takes the split producer/rounds kernel for `chunks` chunks (small
+// launches: lower latency per chain); callers pick separate encode + SHA over the fused kernel
+// when it does.
+bool use_split(uint64_t chunks);
 int device_cus();  // CUs of the current device
 hipError_t launch_fill(const FillParams& a, hipStream_t s);
 

@@ -134,8 +134,15 @@ __global__ __launch_bounds__(128) void sha256_split_kernel(ShaParams a) {
     __shared__ __attribute__((aligned(16))) uint32_t kw[2][SPW * kKwRow];
     const uint32_t lane = threadIdx.x & 63u;
     const bool producer = threadIdx.x < 64u;  // wave-uniform
-    const uint32_t item = blockIdx.x * uint32_t(SPW) + lane;
-    const bool valid = lane < uint32_t(SPW) && item < a.n_parts * a.n_chunks;
+    const uint32_t idx = blockIdx.x * uint32_t(SPW) + lane;
+    bool valid = lane < uint32_t(SPW) &&
+                 idx < (a.items ? a.n_items : a.n_parts * a.n_chunks);
+    const uint32_t item = valid && a.items ? a.items[idx] : idx;
+    bool skipped = false;  // verify mode, chunk not loaded: no blocks, ok = 0
+    if (valid && !a.items && a.present && !a.present[item]) {
+        skipped = true;
+        valid = false;
+    }
     const uint8_t* p = nullptr;
     uint64_t len = 0;
     if (valid) item_source(a, item, p, len);
@@ -202,6 +209,7 @@ __global__ __launch_bounds__(128) void sha256_split_kernel(ShaParams a) {
             __syncthreads();
         }
         if (valid) finish_item(a, item, st);
+        else if (skipped && a.ok) a.ok[item] = 0;
     }
 }
 
@@ -354,7 +362,7 @@ hipError_t launch_split4(const ShaParams& a, hipStream_t s) {
 
 int sha_variant() {
     const char* e = std::getenv("CEC_SHA_VARIANT");
-    return e ? std::atoi(e) : 1;
+    return e ? std::atoi(e) : 0;
 }
 
 // Dynamic LDS requested per lane-kernel workgroup: more than half of the 160 KiB of a CU, so
@@ -390,7 +398,7 @@ hipError_t launch_lane(const ShaParams& a, bool vec16, hipStream_t s, bool one_p
 }
 
 hipError_t launch_split(const ShaParams& a, bool vec16, hipStream_t s) {
-    const uint64_t total = uint64_t(a.n_parts) * a.n_chunks;
+    const uint64_t total = a.items ? a.n_items : uint64_t(a.n_parts) * a.n_chunks;
     dim3 grid(uint32_t((total + 63) / 64));
     if (vec16) hipLaunchKernelGGL((sha256_split_kernel<true, 64>), grid, dim3(128), 0, s, a);
     else hipLaunchKernelGGL((sha256_split_kernel<false, 64>), grid, dim3(128), 0, s, a);
@@ -414,15 +422,28 @@ int device_cus() {
     return cache[dev];
 }
 
-// CEC_SHA_VARIANT (tuning knob, read per launch): 1 = one lane per chunk (default), 2 = split
-// producer/rounds waves.
+// Chunks up to which a launch takes the split kernel: its 2 waves per 64 chunks then fill at
+// most a quarter of the SIMDs (4 x CUs), leaving room for the other launches in flight (write /
+// read pipeline slots, coalesced per-call batches: 4 each).  Past it the chip fills and the lane
+// kernel's one wave per 64 chunks wins (C2: split 50.6 ms vs lane 42.1 ms).
+uint64_t split_max_chunks() { return uint64_t(device_cus()) * 32; }
+
+bool use_split(uint64_t chunks) {
+    const int v = sha_variant();
+    if (v) return v == 2;
+    return chunks <= split_max_chunks();
+}
+
+// CEC_SHA_VARIANT (tuning knob, read per launch): unset = by size (use_split), 1 = one lane per
+// chunk, 2 = split producer/rounds waves, 3/4/5/7/8 = experiments.  A lone 1 MiB chain: lane
+// kernel ~42 ms, split kernel ~31 ms (rounds wave alone on its SIMD; tools/sha_ab.py,
+// profiles/r1z_sha_ab_small.log).
 hipError_t launch_sha256(const ShaParams& a, bool vec16, hipStream_t s) {
     const uint64_t total = a.items ? a.n_items : uint64_t(a.n_parts) * a.n_chunks;
     if (total == 0) return hipSuccess;
-    if (a.items) return launch_lane(a, vec16, s);
-    // verify mode with absent chunks is lane-kernel only (the split kernel has no skip path)
     const int v = sha_variant();
-    if (v == 2 && !a.present) return launch_split(a, vec16, s);
+    if (use_split(total)) return launch_split(a, vec16, s);
+    if (a.items) return launch_lane(a, vec16, s);
     if (v == 3 && !a.present && !a.ptrs && vec16) return launch_split4<false>(a, s);
     if (v == 4 && !a.present && !a.ptrs && vec16) return launch_split4<true>(a, s);
     if (v == 7 && !a.present && !a.ptrs && vec16) return launch_split4<true, 1>(a, s);

@@ -45,7 +45,9 @@ def test_sha256_reference_and_fips_kats(kats):
         assert str(ce.AnyHash(h)) == "sha256-" + v["digest"]
 
 
-def test_sha256_many_lengths_vs_hashlib():
+@pytest.mark.parametrize("variant", ["", "1", "2"])  # by size (split here), lane, split
+def test_sha256_many_lengths_vs_hashlib(variant, monkeypatch):
+    monkeypatch.setenv("CEC_SHA_VARIANT", variant)
     lens = [0, 1, 2, 3, 15, 16, 17, 55, 56, 57, 63, 64, 65, 111, 112, 119, 120, 127, 128, 129,
             191, 192, 683, 1000, 1023, 1024, 4097, 65539, 699051, 1 << 20]
     bufs = [gen_bytes(900 + n, n).tobytes() for n in lens]
@@ -359,7 +361,9 @@ def test_encode_hash_batch_vs_oracle(d, p, L, cstride):
         assert not host[:, d:, L:].any()
 
 
-def test_sha256_batch_subrange():
+@pytest.mark.parametrize("variant", ["1", "2"])
+def test_sha256_batch_subrange(variant, monkeypatch):
+    monkeypatch.setenv("CEC_SHA_VARIANT", variant)
     d, p, L = 4, 2, 5000
     buf, batch = _device_parts(8, d + p, L, 5008, seed=5)
     dig = torch.zeros((8, 3, 32), dtype=torch.uint8, device=DEV)
@@ -500,6 +504,7 @@ def test_fused_encode_hash_matches_separate_and_oracle(d, p, L, cstride, n_parts
         monkeypatch.setenv("CEC_FUSED_BE", "1" if mode == "be" else "0")
         mode = "0"
     monkeypatch.setenv("CEC_FUSED_MODE", mode)
+    monkeypatch.setenv("CEC_FUSED", "1")  # the fused kernel whatever the batch size
     t = d + p
     buf, batch = _device_parts(n_parts, t, L, cstride, seed=L * 3 + d)
     ref = buf.clone()
@@ -640,7 +645,9 @@ def _encoded_batch(d, p, L, n_parts, seed):
     return rs, buf, batch, dig
 
 
-def test_verify_batch_flags():
+@pytest.mark.parametrize("variant", ["1", "2"])  # skip path of both kernels
+def test_verify_batch_flags(variant, monkeypatch):
+    monkeypatch.setenv("CEC_SHA_VARIANT", variant)
     d, p, L, n = 4, 2, 3000, 10
     rs, buf, batch, dig = _encoded_batch(d, p, L, n, 31)
     t = d + p
@@ -700,8 +707,10 @@ def test_read_batch_restores_data_and_reports_undecodable_parts(speculate, monke
         assert torch.equal(got[k, :d], want[k, :d]), k   # data chunks are the read's output
 
 
+@pytest.mark.parametrize("variant", ["1", "2"])  # compacted item list in both SHA kernels
 @pytest.mark.parametrize("speculate", ["1", "0"])
-def test_read_batch_random_patterns_vs_oracle(speculate, monkeypatch):
+def test_read_batch_random_patterns_vs_oracle(speculate, variant, monkeypatch):
+    monkeypatch.setenv("CEC_SHA_VARIANT", variant)
     """d random chunks loaded per part (reader.rs / file_part.rs:86-122), a few corrupted;
     the rebuilt data chunks equal the oracle's reconstruct_data from the verified chunks."""
     monkeypatch.setenv("CEC_READ_SPECULATE", speculate)
