@@ -85,9 +85,11 @@ CONFIGS = {
 }
 
 
+# bench kernel name -> rocprofv3 symbol(s); a step of concurrent kernels sums their traffic
 KERNEL_SYMBOL = {"sha256_kernel": "sha256_lane_kernel", "rs_apply_kernel": "rs_apply_kernel",
                  "rs_apply_kernel(reconstruct)": "rs_apply_var_kernel",
-                 "encode_hash_kernel": "encode_hash_kernel"}
+                 "encode_hash_kernel": "encode_hash_kernel",
+                 "read_batch(verify+decode)": ("sha256_lane_kernel", "rs_apply_var_kernel")}
 
 
 def measured_traffic(config: str, kernel: str, full_size: bool):
@@ -97,8 +99,10 @@ def measured_traffic(config: str, kernel: str, full_size: bool):
     path = os.path.join(ROOT, "profiles", "traffic.json")
     if not full_size or not os.path.exists(path):
         return None
-    entry = json.load(open(path)).get(config, {}).get(KERNEL_SYMBOL.get(kernel, kernel))
-    return entry["bytes_per_launch"] if entry else None
+    table = json.load(open(path)).get(config, {})
+    syms = KERNEL_SYMBOL.get(kernel, kernel)
+    entries = [table.get(k) for k in ((syms,) if isinstance(syms, str) else syms)]
+    return sum(e["bytes_per_launch"] for e in entries) if all(entries) else None
 
 
 def cpu_baseline(cfg, threads: int):
@@ -475,7 +479,9 @@ def main():
     dom_name = max(kernels, key=lambda k: kernels[k]["ms"])
     dom = kernels[dom_name]
     achieved = dom["algorithmic_bytes"] / (dom["ms"] / 1e3) / 1e9
-    traffic = measured_traffic(args.config, dom_name, n_parts == CONFIGS[args.config]["parts"])
+    traffic = measured_traffic(args.config + ("sep" if cfg["op"] == "encode_hash" and not fused
+                                              else ""),
+                               dom_name, n_parts == CONFIGS[args.config]["parts"])
 
     valu = None
     if cfg["op"] in ("encode_hash", "read"):

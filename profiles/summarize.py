@@ -7,8 +7,9 @@ HBM traffic per launch follows MI355X_MICROARCH.md §HBM / cdna_hip_programming.
 FETCH_SIZE and WRITE_SIZE come from separate --pmc passes, are in KiB, and on gfx950
 FETCH_SIZE reports half the bytes of a wide (16 B/lane) streaming read, so
     traffic_bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024.
-The x2 is calibrated for coalesced 16 B/lane streams (rs_apply_kernel); for the SHA kernel's
-per-lane 16 B loads (one 1 MiB-apart stream per lane) it is uncalibrated and flagged as such.
+The x2 is calibrated for coalesced 16 B/lane streams (rs_apply_kernel) and for the SHA kernel's
+per-lane loads (one 1 MiB-apart stream per lane): tools/ubench_fetch.hip reads a known byte count
+in each pattern and FETCH_SIZE reports exactly half (profiles/r1y_fetch_calibration.log).
 """
 import collections
 import csv
@@ -86,11 +87,15 @@ def main():
         tb = (fmult * f + w) * 1024 if f == f and w == w else None
         lines.append(f"| {k} | {ghz:.2f} | {waves:.0f} | {vpw:.0f} | {f:.0f} | {w:.0f} | "
                      f"{tb/1e9 if tb else float('nan'):.2f} |")
-        if tb and k in ("rs_apply_kernel", "sha256_lane_kernel", "encode_hash_kernel"):
+        if tb and k in ("rs_apply_kernel", "rs_apply_var_kernel", "sha256_lane_kernel",
+                        "encode_hash_kernel"):
             traffic.setdefault(config, {})[k] = {
                 "bytes_per_launch": int(tb),
                 "fetch_kib": f, "write_kib": w,
-                "calibrated": k == "rs_apply_kernel" or fmult != 2.0,
+                # x2 measured for both read patterns (tools/ubench_fetch.hip,
+                # profiles/r1y_fetch_calibration.log): coalesced 16 B/lane and per-lane streams
+                "calibrated": k in ("rs_apply_kernel", "rs_apply_var_kernel", "encode_hash_kernel",
+                                    "sha256_lane_kernel") or fmult != 2.0,
                 "fetch_mult": fmult,
                 "source": f"profiles/{tag}_summary.md",
             }
