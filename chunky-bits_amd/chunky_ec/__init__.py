@@ -113,6 +113,9 @@ _sig("cec_read_pipeline_submit", [_vp, ctypes.c_size_t, ctypes.c_size_t])
 _sig("cec_read_pipeline_wait", [_vp, ctypes.c_size_t, ctypes.POINTER(_u8p), ctypes.POINTER(_u8p),
                                 ctypes.POINTER(ctypes.POINTER(ctypes.c_int)), _szp])
 _sig("cec_read_pipeline_drain", [_vp])
+_sig("cec_read_pipeline_new_ex", [_vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t,
+                                  ctypes.c_uint, ctypes.POINTER(_vp)])
+_sig("cec_read_pipeline_data_chunks", [_vp, ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)])
 _sig("cec_synth_byte", [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64],
      ctypes.c_uint8)
 
@@ -543,10 +546,13 @@ class ReadPipeline:
     is re-acquired).
     """
 
-    def __init__(self, codec: ReedSolomon, chunk_len: int, parts_per_batch: int, depth: int = 4):
+    REBUILT_ONLY = 1  # CEC_READ_REBUILT_ONLY
+
+    def __init__(self, codec: ReedSolomon, chunk_len: int, parts_per_batch: int, depth: int = 4,
+                 flags: int = 0):
         h = _vp()
-        code = _lib.cec_read_pipeline_new(codec.handle, chunk_len, parts_per_batch, depth,
-                                          ctypes.byref(h))
+        code = _lib.cec_read_pipeline_new_ex(codec.handle, chunk_len, parts_per_batch, depth,
+                                             flags, ctypes.byref(h))
         if code != OK:
             raise Error(code)
         self._h = h
@@ -589,6 +595,18 @@ class ReadPipeline:
         ver = np.ctypeslib.as_array(ok, shape=(max(k * t, 1),))[: k * t].reshape(k, t)
         st = np.ctypeslib.as_array(status, shape=(max(k, 1),))[:k]
         return out, ver, st
+
+    def data_chunks(self, slot: int, n_parts: int):
+        """[n_parts][d] addresses of the data chunks (cec_read_pipeline_data_chunks)."""
+        import numpy as np
+        ptrs = (ctypes.c_void_p * max(n_parts * self.d, 1))()
+        _check(_lib.cec_read_pipeline_data_chunks(self._h, slot, ptrs))
+        return np.array([p or 0 for p in ptrs[: n_parts * self.d]],
+                        dtype=np.uint64).reshape(n_parts, self.d)
+
+    def part_bytes(self, slot: int, n_parts: int, k: int) -> bytes:
+        """Part k's d data chunks concatenated (read_with_context's output), via data_chunks."""
+        return b"".join(ctypes.string_at(int(a), self.L) for a in self.data_chunks(slot, n_parts)[k])
 
     def drain(self) -> None:
         _check(_lib.cec_read_pipeline_drain(self._h))

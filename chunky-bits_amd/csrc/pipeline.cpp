@@ -236,6 +236,7 @@ struct ReadSlot {
     bool checked = false;
     size_t n_parts = 0;
     std::vector<uint8_t> decode_mask;  // present mask the speculative decode used
+    std::vector<const uint8_t*> data_ptrs;  // [parts][d]: where each data chunk is (after wait)
 };
 
 }  // namespace
@@ -244,6 +245,7 @@ struct cec_read_pipeline {
     const cec_codec* codec = nullptr;
     int device = 0;
     size_t d = 0, p = 0, t = 0, L = 0, cs = 0, parts = 0;
+    bool rebuilt_only = false;  // CEC_READ_REBUILT_ONLY: D2H only the data chunks rebuilt
     std::vector<ReadSlot> slots;
     size_t next = 0;
 
@@ -268,6 +270,29 @@ struct cec_read_pipeline {
         return cec_part_batch{s.d_buf, t * cs, cs, n, L};
     }
 
+    // D2H of the data chunks of part k that were not loaded (the speculative decode rebuilt
+    // them) into their h_data slots: one copy per run of consecutive missing data chunks.
+    int copy_rebuilt_back(ReadSlot& s, size_t k) const {
+        const uint8_t* pr = s.h_present + k * t;
+        for (size_t j = 0; j < d;) {
+            if (pr[j]) {
+                ++j;
+                continue;
+            }
+            size_t e = j;
+            while (e < d && !pr[e]) ++e;
+            uint8_t* dst = s.h_data + (k * d + j) * L;
+            const uint8_t* src = s.d_buf + (k * t + j) * cs;
+            if (cs == L)
+                PIPE_TRY(hipMemcpyAsync(dst, src, (e - j) * L, hipMemcpyDeviceToHost, s.stream));
+            else
+                PIPE_TRY(hipMemcpy2DAsync(dst, L, src, cs, L, e - j, hipMemcpyDeviceToHost,
+                                          s.stream));
+            j = e;
+        }
+        return CEC_OK;
+    }
+
     // D2H of the d data chunks of parts [k0, k0 + n) into h_data.
     int copy_data_back(ReadSlot& s, size_t k0, size_t n) const {
         const size_t pitch = t * cs, dw = d * L;
@@ -288,7 +313,13 @@ extern "C" {
 
 int cec_read_pipeline_new(const cec_codec* codec, size_t chunk_len, size_t parts_per_batch,
                           size_t depth, cec_read_pipeline** out) {
-    if (!codec || !out || chunk_len == 0 || parts_per_batch == 0 || depth == 0 || depth > 16)
+    return cec_read_pipeline_new_ex(codec, chunk_len, parts_per_batch, depth, 0u, out);
+}
+
+int cec_read_pipeline_new_ex(const cec_codec* codec, size_t chunk_len, size_t parts_per_batch,
+                             size_t depth, unsigned flags, cec_read_pipeline** out) {
+    if (!codec || !out || chunk_len == 0 || parts_per_batch == 0 || depth == 0 || depth > 16 ||
+        (flags & ~unsigned(CEC_READ_REBUILT_ONLY)))
         return CEC_ERR_INVALID_ARGUMENT;
     *out = nullptr;
     if (cec_device_count() <= 0) return CEC_ERR_NO_DEVICE;
@@ -301,6 +332,7 @@ int cec_read_pipeline_new(const cec_codec* codec, size_t chunk_len, size_t parts
     pl->L = chunk_len;
     pl->cs = (chunk_len + 255) / 256 * 256;
     pl->parts = parts_per_batch;
+    pl->rebuilt_only = (flags & CEC_READ_REBUILT_ONLY) != 0;
     pl->slots.resize(depth);
     const size_t P = pl->parts, t = pl->t;
     for (ReadSlot& s : pl->slots) {
@@ -399,7 +431,12 @@ int cec_read_pipeline_submit(cec_read_pipeline* pl, size_t slot, size_t n_parts)
         g_pipe_error = cec_last_error();
         return st;
     }
-    st = pl->copy_data_back(s, 0, n_parts);
+    if (pl->rebuilt_only) {
+        for (size_t k = 0; k < n_parts && st == CEC_OK; ++k)
+            if (s.h_status[k] == CEC_OK) st = pl->copy_rebuilt_back(s, k);
+    } else {
+        st = pl->copy_data_back(s, 0, n_parts);
+    }
     if (st != CEC_OK) return st;
     PIPE_TRY(hipMemcpyAsync(s.h_ok, s.d_flags + n, n, hipMemcpyDeviceToHost, s.stream));
     PIPE_TRY(hipEventRecord(s.done, s.stream));
@@ -456,12 +493,35 @@ int cec_read_pipeline_wait(cec_read_pipeline* pl, size_t slot, const uint8_t** d
             PIPE_TRY(hipStreamSynchronize(s.stream));
             if (cur != pl->device) PIPE_TRY(hipSetDevice(cur));
         }
+        // Where each data chunk is: re-decoded parts and (without REBUILT_ONLY) every part in
+        // h_data; otherwise a loaded chunk stays in the caller's h_chunks slot (it verified:
+        // parts with a failed chunk were re-decoded) and a rebuilt one came back into h_data.
+        std::vector<uint8_t> redone(n, 0);
+        for (size_t k : redo) redone[k] = 1;
+        s.data_ptrs.resize(n * d);
+        for (size_t k = 0; k < n; ++k)
+            for (size_t j = 0; j < d; ++j) {
+                const bool in_place = pl->rebuilt_only && !redone[k] && s.h_present[k * t + j];
+                s.data_ptrs[k * d + j] =
+                    in_place ? s.h_chunks + (k * t + j) * pl->L : s.h_data + (k * d + j) * pl->L;
+            }
         s.checked = true;
     }
     if (data) *data = s.h_data;
     if (verified) *verified = s.h_ok;
     if (part_status) *part_status = s.h_status;
     if (n_parts) *n_parts = s.n_parts;
+    return CEC_OK;
+}
+
+int cec_read_pipeline_data_chunks(cec_read_pipeline* pl, size_t slot, const uint8_t** ptrs) {
+    if (!pl || slot >= pl->slots.size() || !ptrs) return CEC_ERR_INVALID_ARGUMENT;
+    ReadSlot& s = pl->slots[slot];
+    if (s.in_flight || !s.checked) {
+        const int st = cec_read_pipeline_wait(pl, slot, nullptr, nullptr, nullptr, nullptr);
+        if (st != CEC_OK) return st;
+    }
+    std::copy(s.data_ptrs.begin(), s.data_ptrs.end(), ptrs);
     return CEC_OK;
 }
 

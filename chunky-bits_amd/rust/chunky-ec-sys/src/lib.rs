@@ -26,6 +26,9 @@ pub mod sys {
         _private: [u8; 0],
     }
 
+    /// cec_read_pipeline_new_ex flag: only rebuilt data chunks come back over PCIe.
+    pub const CEC_READ_REBUILT_ONLY: std::os::raw::c_uint = 1;
+
     #[repr(C)]
     #[derive(Clone, Copy, Debug)]
     pub struct cec_part_batch {
@@ -191,6 +194,19 @@ pub mod sys {
             n_parts: *mut usize,
         ) -> c_int;
         pub fn cec_read_pipeline_drain(pipeline: *mut cec_read_pipeline) -> c_int;
+        pub fn cec_read_pipeline_new_ex(
+            codec: *const cec_codec,
+            chunk_len: usize,
+            parts_per_batch: usize,
+            depth: usize,
+            flags: std::os::raw::c_uint,
+            out: *mut *mut cec_read_pipeline,
+        ) -> c_int;
+        pub fn cec_read_pipeline_data_chunks(
+            pipeline: *mut cec_read_pipeline,
+            slot: usize,
+            ptrs: *mut *const u8,
+        ) -> c_int;
         pub fn cec_coalesce_stats(calls: *mut u64, launches: *mut u64);
     }
 }

@@ -251,6 +251,19 @@ int cec_read_pipeline_submit(cec_read_pipeline* pipeline, size_t slot, size_t n_
 int cec_read_pipeline_wait(cec_read_pipeline* pipeline, size_t slot, const uint8_t** data,
                            const uint8_t** verified, const int** part_status, size_t* n_parts);
 int cec_read_pipeline_drain(cec_read_pipeline* pipeline);
+/* As cec_read_pipeline_new with flags.  CEC_READ_REBUILT_ONLY: submit copies back only the data
+ * chunks it rebuilt (RS(10,4) with d random chunks loaded: 2.9 of 10 per part), since the
+ * loaded ones are already in the caller's pinned chunk buffer; wait's *data then holds only
+ * those, and cec_read_pipeline_data_chunks says where each data chunk is. */
+#define CEC_READ_REBUILT_ONLY 1u
+int cec_read_pipeline_new_ex(const cec_codec* codec, size_t chunk_len, size_t parts_per_batch,
+                             size_t depth, unsigned flags, cec_read_pipeline** out);
+/* After (or instead of) wait: ptrs[k*d + j] = the chunk_len bytes of data chunk j of part k —
+ * in the slot's chunk buffer (loaded and verified, REBUILT_ONLY) or in its data buffer
+ * (rebuilt, re-decoded, or without REBUILT_ONLY).  Valid until the slot is acquired again;
+ * undefined for parts whose status is not CEC_OK. */
+int cec_read_pipeline_data_chunks(cec_read_pipeline* pipeline, size_t slot,
+                                  const uint8_t** ptrs);
 
 /* ---------------------------------------------------------------------------------------- */
 /* Utilities for benchmarks and tests                                                        */

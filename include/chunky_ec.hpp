@@ -511,19 +511,25 @@ struct FileReference {
         auto& cached = detail::cached_pipe<cec_read_pipeline>(
             d, t - d, L, ppb, depth,
             [](const cec_codec* c, size_t l, size_t parts, size_t dep, cec_read_pipeline** out) {
-                detail::check_pipe(cec_read_pipeline_new(c, l, parts, dep, out));
+                detail::check_pipe(
+                    cec_read_pipeline_new_ex(c, l, parts, dep, CEC_READ_REBUILT_ONLY, out));
             },
             cec_read_pipeline_free);
         cec_read_pipeline* rp = cached.pipe.get();
         const size_t nd = cec_read_pipeline_depth(rp);
         std::vector<std::pair<size_t, size_t>> pending(nd, {0, 0});  // slot -> (first, count)
+        std::vector<const uint8_t*> where;
+        // Called right after acquire(slot), before its chunk buffer is refilled: the loaded data
+        // chunks are read from there (only the rebuilt ones came back from the GPU).
         auto collect = [&](size_t slot) {
             const uint8_t *data = nullptr, *ver = nullptr;
             const int* status = nullptr;
             size_t got = 0;
             detail::check(cec_read_pipeline_wait(rp, slot, &data, &ver, &status, &got));
             for (size_t i = 0; i < got; ++i) detail::check(status[i]);
-            out.insert(out.end(), data, data + got * d * L);
+            where.resize(got * d);
+            detail::check(cec_read_pipeline_data_chunks(rp, slot, where.data()));
+            for (const uint8_t* c : where) out.insert(out.end(), c, c + L);
         };
         size_t done = 0, submitted = 0;
         const size_t per = ppb;

@@ -570,7 +570,8 @@ def test_pipeline_matches_oracle(d, p, L, parts, depth, batches):
     (3, 2, 683, 9, 2, 3),         # odd chunk length (padded device stride)
     (20, 8, 1000, 6, 2, 2),
 ])
-def test_read_pipeline_matches_read_with_context(d, p, L, parts, depth, batches):
+@pytest.mark.parametrize("flags", [0, ce.ReadPipeline.REBUILT_ONLY])
+def test_read_pipeline_matches_read_with_context(d, p, L, parts, depth, batches, flags):
     """FileReadBuilder's loop batched: per part the loaded chunks (all; d random ones like
     file_part.rs:97; fewer than d; a corrupted loaded chunk with enough others; a corrupted one
     without), verification against the metadata digests, and the part's data rebuilt from the
@@ -578,23 +579,27 @@ def test_read_pipeline_matches_read_with_context(d, p, L, parts, depth, batches)
     read would see them (TooFewShardsPresent when fewer than d verify)."""
     t = d + p
     rs = ce.ReedSolomon(d, p)
-    rp = ce.ReadPipeline(rs, L, parts, depth)
+    rp = ce.ReadPipeline(rs, L, parts, depth, flags)
     rng = np.random.default_rng(d * 100 + L)
     pending, want = {}, {}
 
-    def check(b, out):
-        data, ver, status = out
+    def check(b, slot):
+        # before the slot's chunk buffer is refilled: REBUILT_ONLY data points into it
+        data, ver, status = rp.wait(slot)
         exp_data, exp_ok, exp_status = want[b]
         assert list(status) == exp_status, b
         assert np.array_equal(ver, exp_ok), b
         for k, st in enumerate(exp_status):
             if st == 0:
-                assert np.array_equal(data[k], exp_data[k]), (b, k)
+                got = rp.part_bytes(slot, len(exp_status), k)
+                assert got == exp_data[k].tobytes(), (b, k)
+                if not flags:
+                    assert np.array_equal(data[k], exp_data[k]), (b, k)
 
     for b in range(batches):
         slot, chunks, present, expected = rp.acquire()
         if slot in pending:
-            check(pending[slot], tuple(x.copy() for x in rp.wait(slot)))
+            check(pending[slot], slot)
         n = parts if b % 2 == 0 else parts - 1
         exp_data, exp_ok, exp_status = [], np.zeros((n, t), np.uint8), []
         for k in range(n):
@@ -627,7 +632,7 @@ def test_read_pipeline_matches_read_with_context(d, p, L, parts, depth, batches)
         pending[slot] = b
         want[b] = (exp_data, exp_ok, exp_status)
     for slot, b in pending.items():
-        check(b, tuple(x.copy() for x in rp.wait(slot)))
+        check(b, slot)
     rp.drain()
 
 
