@@ -614,4 +614,48 @@ impl ReadPipeline {
     pub fn drain(&mut self) -> Result<(), CecError> {
         check_pipe(unsafe { sys::cec_read_pipeline_drain(self.raw) })
     }
+
+    /// As [`ReadPipeline::new`] with `CEC_READ_REBUILT_ONLY`: only the rebuilt data chunks come
+    /// back over PCIe; read a part's bytes through [`ReadPipeline::data_chunks`].
+    pub fn new_rebuilt_only(
+        codec: &ReedSolomon,
+        chunk_len: usize,
+        parts_per_batch: usize,
+        depth: usize,
+    ) -> Result<ReadPipeline, CecError> {
+        let mut raw = std::ptr::null_mut();
+        check_pipe(unsafe {
+            sys::cec_read_pipeline_new_ex(
+                codec.raw,
+                chunk_len,
+                parts_per_batch,
+                depth,
+                sys::CEC_READ_REBUILT_ONLY,
+                &mut raw,
+            )
+        })?;
+        Ok(ReadPipeline {
+            raw,
+            d: codec.data_shard_count(),
+            t: codec.total_shard_count(),
+            chunk_len,
+            parts: parts_per_batch,
+        })
+    }
+
+    /// The d data chunks of each of the slot's `n_parts` parts (`[part][chunk]`), wherever they
+    /// are (the slot's chunk buffer or the rebuilt buffer); valid until the slot is re-acquired.
+    /// `read_with_context`'s output is their concatenation (file_part.rs:130-133).
+    pub fn data_chunks(&mut self, slot: usize, n_parts: usize) -> Result<Vec<Vec<&[u8]>>, CecError> {
+        let mut ptrs = vec![std::ptr::null::<u8>(); n_parts * self.d];
+        check_pipe(unsafe { sys::cec_read_pipeline_data_chunks(self.raw, slot, ptrs.as_mut_ptr()) })?;
+        Ok(ptrs
+            .chunks(self.d)
+            .map(|part| {
+                part.iter()
+                    .map(|&p| unsafe { std::slice::from_raw_parts(p, self.chunk_len) })
+                    .collect()
+            })
+            .collect())
+    }
 }
