@@ -1297,6 +1297,9 @@ int verify_then_reconstruct(const cec_codec* c, const cec_part_batch* b,
             if (e == hipSuccess) e = hipStreamWaitEvent(s, side->join, 0);
             if (e != hipSuccess) st = hip_fail(e, "speculative decode join");
         }
+        // On failure nothing joins the side stream: let what it launched finish before the
+        // caller gets its buffers back.
+        if (st != CEC_OK) (void)hipStreamSynchronize(side->stream);
     }
     if (st == CEC_OK) {
         hipError_t e = hipMemcpyAsync(verified_host, ok, n, hipMemcpyDeviceToHost, s);
