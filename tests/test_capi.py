@@ -100,6 +100,22 @@ def test_argument_errors_precede_device_use():
         assert e.value.code == ce.ERR_NO_DEVICE
 
 
+def test_read_pipeline_argument_checks_precede_device_use():
+    """cec_read_pipeline_new_ex rejects unknown flags and bad shapes before any HIP call; without
+    a device a valid request reports NoDevice (no host-side fallback pipeline)."""
+    import chunky_ec as ce
+    rs = ce.ReedSolomon(10, 4)
+    for args in [(1 << 20, 4, 2, 2), (0, 4, 2, 0), (1 << 20, 0, 2, 0), (1 << 20, 4, 0, 0),
+                 (1 << 20, 4, 17, 0)]:
+        with pytest.raises(ce.Error) as e:
+            ce.ReadPipeline(rs, *args)
+        assert e.value.code == ce.ERR_INVALID_ARGUMENT, args
+    if ce.device_count() == 0:
+        with pytest.raises(ce.Error) as e:
+            ce.ReadPipeline(rs, 1 << 20, 4, 2, ce.ReadPipeline.REBUILT_ONLY)
+        assert e.value.code == ce.ERR_NO_DEVICE
+
+
 def test_synth_byte_host_mirror_is_deterministic():
     import chunky_ec as ce
     a = [ce.synth_byte(7, k, c, o) for k in range(3) for c in range(3) for o in (0, 1, 7, 8, 1000)]
