@@ -439,6 +439,15 @@ struct Batch {
 // into ever smaller batches that each pay it: measured on one box, interleaved
 // (profiles/r1y_percall_ab.log), 100 threads 7.1-8.2 GB/s with 1 vs 3.6-3.8 with 4, 400 threads
 // 6.9-7.9 vs 6.0-7.1.
+// CEC_COALESCE_ADAPT=0 (A/B knob): fixed CEC_COALESCE_US window, no early exit.
+bool coalesce_adaptive() {
+    static const bool on = [] {
+        const char* e = std::getenv("CEC_COALESCE_ADAPT");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 uint32_t coalesce_inflight() {
     static const uint32_t n = [] {
         const char* e = std::getenv("CEC_COALESCE_INFLIGHT");
@@ -454,6 +463,7 @@ class Coalescer {
     int submit(Req* r) {
         g_calls.fetch_add(1, std::memory_order_relaxed);
         std::unique_lock<std::mutex> lk(mu_);
+        peak_ = std::max(peak_, ++callers_);
         queue_.push_back(r);
         if (gathering_) gather_cv_.notify_one();  // the gathering leader re-checks its batch
         for (;;) {
@@ -477,6 +487,8 @@ class Coalescer {
                 r->cv.wait(lk);
             }
         }
+        --callers_;
+        lk.unlock();
         if (r->status != CEC_OK) g_last_error = r->err;
         return r->status;
     }
@@ -500,13 +512,27 @@ class Coalescer {
                 if (q->key() == key) b += Impl::bytes(*q);
             return b;
         };
+        auto matching_count = [&] {
+            size_t n = 0;
+            for (Req* q : queue_) n += q->key() == key ? 1 : 0;
+            return n;
+        };
         if (last_batch_ > 1 || queue_.size() > 1) {
             // Wait for company only when calls are actually concurrent (the last batch had several
             // callers, or others are queued now): a lone caller's calls never pay the window.
-            const auto until = std::chrono::steady_clock::now() +
-                               std::chrono::microseconds(coalesce_window_us());
-            gather_cv_.wait_until(lk, until,
-                                  [&] { return matching_bytes() >= coalesce_max_bytes(); });
+            // The window scales with the last launch (1/8 of its run time, at least
+            // CEC_COALESCE_US): callers of the batch that just finished are still copying their
+            // results out and come back a few ms later; a short window splits the callers into
+            // two alternating groups, each paying a full launch (10 threads: 5 parts per launch).
+            // It ends early once as many callers are queued as were ever inside at once lately.
+            uint64_t window = coalesce_window_us();
+            if (coalesce_adaptive()) window = std::max<uint64_t>(window, last_run_us_ / 8);
+            const auto until =
+                std::chrono::steady_clock::now() + std::chrono::microseconds(window);
+            gather_cv_.wait_until(lk, until, [&] {
+                return matching_bytes() >= coalesce_max_bytes() ||
+                       (coalesce_adaptive() && matching_count() >= peak_);
+            });
         }
         Batch batch_state;
         std::vector<Req*> batch{r};
@@ -525,6 +551,10 @@ class Coalescer {
         for (Req* q : batch) q->batch = &batch_state;
         batch_state.size = batch.size();
         last_batch_ = batch.size();
+        if (++batches_since_peak_ >= 32) {  // forget an old burst of callers
+            peak_ = callers_;
+            batches_since_peak_ = 0;
+        }
         Arena* arena = take_arena(key.device);
         gathering_ = false;
         wake_next();  // the next batch can gather while this one runs
@@ -553,6 +583,7 @@ class Coalescer {
         }
         const std::string err = st == CEC_OK ? std::string() : g_last_error;
         lk.lock();
+        last_run_us_ = uint64_t(std::chrono::duration_cast<std::chrono::microseconds>(t3 - t2).count());
         batch_state.finished = 1;
         for (Req* q : batch) {
             q->status = st;
@@ -601,6 +632,10 @@ class Coalescer {
     bool gathering_ = false;
     uint32_t active_ = 0;
     size_t last_batch_ = 0;
+    size_t callers_ = 0;             // submit() calls in progress
+    size_t peak_ = 0;                // most callers in progress at once, lately
+    uint32_t batches_since_peak_ = 0;
+    uint64_t last_run_us_ = 0;       // launch-to-results time of the last batch
     std::vector<std::unique_ptr<Arena>> arenas_;  // owned; free lists per device below
     std::map<int, std::vector<Arena*>> free_;
 };
