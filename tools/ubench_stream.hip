@@ -35,11 +35,12 @@ __device__ __forceinline__ void st(uint8_t* p, v4u v) {
 }
 
 // V = 16-byte vectors per lane per input (1, 2, 4); ITERS column steps per thread (grid-tile).
+// cs = chunk stride (L, or L + a pad that staggers the 14 streams of a part across channels).
 template <int V, int ITERS, bool NT>
-__global__ void stream_kernel(uint8_t* base, uint32_t tiles_per_part) {
+__global__ void stream_kernel(uint8_t* base, uint32_t tiles_per_part, size_t cs) {
     const uint32_t part = blockIdx.x / tiles_per_part;
     const uint32_t tile = blockIdx.x - part * tiles_per_part;
-    uint8_t* pb = base + size_t(part) * T * L;
+    uint8_t* pb = base + size_t(part) * T * cs;
     const size_t step = size_t(blockDim.x) * 16 * V;
 #pragma unroll 1
     for (int it = 0; it < ITERS; ++it) {
@@ -50,7 +51,7 @@ __global__ void stream_kernel(uint8_t* base, uint32_t tiles_per_part) {
 #pragma unroll
         for (int j = 0; j < D; ++j)
 #pragma unroll
-            for (int u = 0; u < V; ++u) in[j][u] = ld<NT>(pb + j * L + x + size_t(u) * blockDim.x * 16);
+            for (int u = 0; u < V; ++u) in[j][u] = ld<NT>(pb + j * cs + x + size_t(u) * blockDim.x * 16);
 #pragma unroll
         for (int j = 0; j < D; ++j)
 #pragma unroll
@@ -59,7 +60,7 @@ __global__ void stream_kernel(uint8_t* base, uint32_t tiles_per_part) {
         for (int r = 0; r < P; ++r)
 #pragma unroll
             for (int u = 0; u < V; ++u)
-                st<NT>(pb + (D + r) * L + x + size_t(u) * blockDim.x * 16, acc[u] + v4u{unsigned(r), unsigned(r), unsigned(r), unsigned(r)});
+                st<NT>(pb + (D + r) * cs + x + size_t(u) * blockDim.x * 16, acc[u] + v4u{unsigned(r), unsigned(r), unsigned(r), unsigned(r)});
     }
 }
 
@@ -142,7 +143,7 @@ void run_simple(const char* name, K launch, double bytes) {
 }
 
 template <int V, int ITERS, bool NT>
-void run(uint8_t* base, uint32_t parts, int threads, const char* name) {
+void run(uint8_t* base, uint32_t parts, int threads, const char* name, size_t pad = 0) {
     const size_t per_block = size_t(threads) * 16 * V * ITERS;
     const uint32_t tiles = uint32_t(L / per_block);
     hipEvent_t a, b;
@@ -152,7 +153,7 @@ void run(uint8_t* base, uint32_t parts, int threads, const char* name) {
     for (int r = 0; r < 6; ++r) {
         CK(hipEventRecord(a));
         hipLaunchKernelGGL((stream_kernel<V, ITERS, NT>), dim3(parts * tiles), dim3(threads), 0, 0,
-                           base, tiles);
+                           base, tiles, L + pad);
         CK(hipEventRecord(b));
         CK(hipEventSynchronize(b));
         float ms;
@@ -160,16 +161,25 @@ void run(uint8_t* base, uint32_t parts, int threads, const char* name) {
         if (r && ms < best) best = ms;
     }
     const double bytes = double(parts) * T * L;
-    printf("%-28s threads %4d  V %d ITERS %d NT %d : %8.3f ms  %7.0f GB/s\n", name, threads, V,
-           ITERS, int(NT), best, bytes / best / 1e6);
+    printf("%-28s threads %4d  V %d ITERS %d NT %d pad %6zu : %8.3f ms  %7.0f GB/s\n", name,
+           threads, V, ITERS, int(NT), pad, best, bytes / best / 1e6);
     fflush(stdout);
 }
 
 int main(int argc, char** argv) {
     const uint32_t parts = argc > 1 ? uint32_t(atoi(argv[1])) : 4096;
+    const size_t max_pad = 64 * 1024 + 256;
     uint8_t* base;
-    CK(hipMalloc(&base, size_t(parts) * T * L));
-    CK(hipMemset(base, 1, size_t(parts) * T * L));
+    CK(hipMalloc(&base, size_t(parts) * T * (L + max_pad)));
+    CK(hipMemset(base, 1, size_t(parts) * T * (L + max_pad)));
+    if (argc > 2 && argv[2][0] == 'p') {  // chunk-stride pad sweep of the best shapes
+        for (size_t pad : {size_t(0), size_t(256), size_t(1024), size_t(4096), size_t(8192 + 256),
+                           size_t(65536), max_pad}) {
+            run<2, 1, true>(base, parts, 256, "v2 it1 nt", pad);
+            run<4, 1, true>(base, parts, 256, "v4 it1 nt", pad);
+        }
+        return 0;
+    }
     run<1, 4, false>(base, parts, 256, "v1 it4 (rs_apply shape)");
     run<1, 4, true>(base, parts, 256, "v1 it4 nt");
     run<1, 1, false>(base, parts, 256, "v1 it1");
