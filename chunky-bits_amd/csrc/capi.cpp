@@ -347,7 +347,7 @@ bool prefer_fused(size_t chunks) {
 //                encode+hash (or the SHA) kernel over every part, and brings parity and
 //                digests back with one D2H copy into pinned staging;
 //   3. copy-out  every caller copies its results out into its own buffers, in parallel.
-// Batches are capped at CEC_COALESCE_MAX_MIB of input (default 4096).  Results are
+// Batches are capped at CEC_COALESCE_MAX_MIB of input (default 1024).  Results are
 // bit-identical to one call per launch (same kernels, same inputs).
 // ------------------------------------------------------------------------------------------
 std::atomic<uint64_t> g_calls{0}, g_launches{0};
