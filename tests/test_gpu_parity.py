@@ -771,3 +771,38 @@ def test_resilver_batch_cluster_style():
     torch.cuda.synchronize()
     assert bool(ok.all())
     assert torch.equal(buf, ref)
+
+
+@pytest.mark.parametrize("speculate", ["1", "0"])
+def test_resilver_batch_random_patterns_with_corruption(speculate, monkeypatch):
+    """FilePart::resilver compute (file_part.rs:253-308) batched: random loaded sets (d..d+p),
+    some loaded chunks corrupted (including ones the speculative decode uses); every decodable
+    part ends with all d+p chunks equal to the written ones, flags mark the bad chunks."""
+    monkeypatch.setenv("CEC_READ_SPECULATE", speculate)
+    d, p, L, n = 6, 3, 2048 + 7, 40
+    rs, buf, batch, dig = _encoded_batch(d, p, L, n, 61)
+    t = d + p
+    ref = buf.cpu().numpy().copy()
+    rng = np.random.default_rng(11)
+    present = np.zeros((n, t), dtype=np.uint8)
+    for k in range(n):
+        present[k, rng.choice(t, size=d + int(rng.integers(0, p + 1)), replace=False)] = 1
+    host = ref.copy()
+    host[present == 0] = 0
+    bad = np.zeros((n, t), dtype=bool)
+    for k in rng.choice(n, size=10, replace=False):
+        i = int(np.flatnonzero(present[k])[0])  # the first loaded chunk: always decode input
+        host[k, i, int(rng.integers(0, L))] ^= 0x21
+        bad[k, i] = True
+    buf.copy_(torch.from_numpy(host))
+    verified, status = ce.resilver_batch(rs, batch, present.tobytes(), dig.data_ptr())
+    torch.cuda.synchronize()
+    v = np.frombuffer(verified, np.uint8).reshape(n, t).astype(bool)
+    assert np.array_equal(v, present.astype(bool) & ~bad)
+    got = buf.cpu().numpy()
+    for k in range(n):
+        if v[k].sum() < d:
+            assert status[k] == ce.TOO_FEW_SHARDS_PRESENT
+            continue
+        assert status[k] == ce.OK
+        assert np.array_equal(got[k], ref[k]), k
