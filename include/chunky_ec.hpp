@@ -27,12 +27,14 @@
 #include <algorithm>
 #include <array>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
 #include <optional>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -95,6 +97,45 @@ inline void check_pipe(int status) {
     if (status >= CEC_TOO_FEW_SHARDS && status <= CEC_INVALID_INDEX)
         throw ErasureError(static_cast<Error>(status));
     throw EngineError(status, std::string(cec_status_name(status)) + ": " + cec_pipeline_last_error());
+}
+
+// Host threads for the batched paths' copies into / out of pinned staging (CEC_HOST_COPY_THREADS,
+// default 8).  One thread's memcpy (~10-20 GB/s) is below the PCIe rate the pipelines reach.
+inline size_t copy_threads() {
+    static const size_t n = [] {
+        const char* e = std::getenv("CEC_HOST_COPY_THREADS");
+        const long v = e ? std::atol(e) : 8;
+        return size_t(std::min<long>(std::max<long>(v, 1), 64));
+    }();
+    return n;
+}
+
+// fn(i) for i in [0, n) over copy_threads() threads (contiguous ranges; inline when small).
+template <typename Fn>
+inline void parallel_for(size_t n, Fn fn) {
+    const size_t w = std::min(copy_threads(), n);
+    if (w <= 1) {
+        for (size_t i = 0; i < n; ++i) fn(i);
+        return;
+    }
+    std::vector<std::thread> pool;
+    pool.reserve(w - 1);
+    for (size_t k = 1; k < w; ++k)
+        pool.emplace_back([&, k] {
+            for (size_t i = n * k / w; i < n * (k + 1) / w; ++i) fn(i);
+        });
+    for (size_t i = 0; i < n / w; ++i) fn(i);
+    for (auto& th : pool) th.join();
+}
+
+// memcpy of n bytes split over copy_threads() threads (1 MiB grain).
+inline void parallel_copy(uint8_t* dst, const uint8_t* src, size_t n) {
+    constexpr size_t kGrain = size_t(1) << 20;
+    const size_t pieces = (n + kGrain - 1) / kGrain;
+    parallel_for(pieces, [&](size_t i) {
+        const size_t off = i * kGrain;
+        std::memcpy(dst + off, src + off, std::min(kGrain, n - off));
+    });
 }
 
 inline char hex_digit(unsigned v) { return char(v < 10 ? '0' + v : 'a' + (v - 10)); }
@@ -544,7 +585,8 @@ struct FileReference {
             }
             if (submitted == n) continue;
             const size_t b = std::min(per, n - submitted);
-            for (size_t q = 0; q < b; ++q) {
+            // the loads (store lookups + copies into the pinned slot) run on copy_threads()
+            detail::parallel_for(b, [&](size_t q) {
                 const FilePart& part = parts[k0 + submitted + q];
                 for (size_t i = 0; i < t; ++i) {
                     const Bytes* bytes = src.find(part.chunk(i).hash);
@@ -553,7 +595,7 @@ struct FileReference {
                     if (ok) std::memcpy(chunks + (q * t + i) * L, bytes->data(), L);
                     std::memcpy(expected + (q * t + i) * 32, part.chunk(i).hash.digest().data(), 32);
                 }
-            }
+            });
             detail::check(cec_read_pipeline_submit(rp, slot, b));
             pending[slot] = {submitted, b};
             submitted += b;
@@ -661,7 +703,7 @@ class FileWriteBuilder {
             }
             if (submitted == full) continue;
             const size_t b = std::min(per, full - submitted);
-            std::memcpy(data, bytes + submitted * d * L, b * d * L);
+            detail::parallel_copy(data, bytes + submitted * d * L, b * d * L);
             detail::check_pipe(cec_pipeline_submit(pl, slot, b));
             pending[slot] = {submitted, b};
             submitted += b;
