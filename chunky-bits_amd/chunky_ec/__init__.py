@@ -30,7 +30,10 @@ except Exception:  # pragma: no cover - torch is optional for the host-buffer AP
     torch = None
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libchunky_ec.so")
+# CEC_LIBRARY points the A/B timing tools (tools/*_ab.py) at the attribution build
+# (tools/ab/libchunky_ec.so, `make -C chunky-bits_amd/csrc ab`); everything else loads the product
+# library next to this file.
+LIB_PATH = os.environ.get("CEC_LIBRARY") or os.path.join(_HERE, "libchunky_ec.so")
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(
@@ -65,6 +68,8 @@ _sig("cec_abi_version", [])
 _sig("cec_status_name", [ctypes.c_int], ctypes.c_char_p)
 _sig("cec_last_error", [], ctypes.c_char_p)
 _sig("cec_device_count", [])
+_sig("cec_build_info", [], ctypes.c_char_p)
+_sig("cec_codec_cached_patterns", [_vp], ctypes.c_size_t)
 _sig("cec_codec_new", [ctypes.c_size_t, ctypes.c_size_t, ctypes.POINTER(_vp)])
 _sig("cec_codec_free", [_vp], None)
 _sig("cec_codec_data_shards", [_vp], ctypes.c_size_t)
@@ -118,6 +123,30 @@ _sig("cec_read_pipeline_new_ex", [_vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.
 _sig("cec_read_pipeline_data_chunks", [_vp, ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)])
 _sig("cec_synth_byte", [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64],
      ctypes.c_uint8)
+_sig("cec_current_device", [ctypes.POINTER(ctypes.c_int)])
+_sig("cec_set_device", [ctypes.c_int])
+_sig("cec_device_numa_node", [ctypes.c_int])
+_sig("cec_host_alloc", [ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(_vp)])
+_sig("cec_host_free", [_vp], None)
+_sig("cec_host_is_pinned", [_vp, ctypes.c_size_t])
+_sig("cec_host_numa_node", [_vp])
+_sig("cec_pipeline_new_ex", [_vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_uint,
+                             ctypes.POINTER(_vp)])
+_sig("cec_pipeline_submit_from", [_vp, ctypes.c_size_t, _vp, ctypes.c_size_t, _vp, _vp])
+_sig("cec_read_pipeline_submit_from", [_vp, ctypes.c_size_t, _vp, _vp, _vp, ctypes.c_size_t, _vp])
+_sig("cec_multi_new", [_vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t,
+                       ctypes.POINTER(ctypes.c_int), ctypes.c_size_t, ctypes.POINTER(_vp)])
+_sig("cec_multi_free", [_vp], None)
+_sig("cec_multi_shards", [_vp], ctypes.c_size_t)
+_sig("cec_multi_shard_info", [_vp, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int),
+                              ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_uint64)])
+_sig("cec_multi_encode_hash", [_vp, _vp, ctypes.c_size_t, _vp, _vp,
+                               ctypes.POINTER(ctypes.c_uint64)])
+_sig("cec_multi_read", [_vp, _vp, _vp, _vp, ctypes.c_size_t, _vp, _vp,
+                        ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint,
+                        ctypes.POINTER(ctypes.c_uint64)])
+_sig("cec_multi_wait", [_vp, ctypes.c_uint64])
+_sig("cec_multi_last_error", [], ctypes.c_char_p)
 
 # Status codes (include/chunky_ec.h).
 OK = 0
@@ -161,6 +190,10 @@ def abi_version() -> int:
 
 def device_count() -> int:
     return _lib.cec_device_count()
+
+
+def build_info() -> str:
+    return _lib.cec_build_info().decode()
 
 
 def status_name(code: int) -> str:
@@ -211,6 +244,10 @@ class ReedSolomon:
 
     def total_shard_count(self) -> int:
         return _lib.cec_codec_total_shards(self._h)
+
+    def cached_patterns(self) -> int:
+        """Decode matrices cached in the codec (bounded LRU)."""
+        return _lib.cec_codec_cached_patterns(self._h)
 
     def matrix(self) -> List[List[int]]:
         d, t = self.data_shard_count(), self.total_shard_count()
@@ -339,6 +376,8 @@ class EncodedPart:
 def part_encode(codec: ReedSolomon, data_buf, length: int) -> EncodedPart:
     """FilePart::write_with_encoder's compute (file_part.rs:150-185) for one part."""
     d, p = codec.data_shard_count(), codec.parity_shard_count()
+    if length > _nbytes(data_buf):  # file_part.rs:150 asserts length <= data_buf.len()
+        raise ValueError(f"length {length} > data_buf length {_nbytes(data_buf)}")
     L = (length + d - 1) // d if length else 0
     buf = bytearray(d * L)
     src = memoryview(data_buf)[:length]
@@ -487,11 +526,11 @@ class Pipeline:
     ``parity, digests = pl.wait(slot)`` (numpy views valid until the slot is re-acquired).
     """
 
-    def __init__(self, codec: ReedSolomon, chunk_len: int, parts_per_batch: int, depth: int = 4):
-        import numpy as np  # noqa: F401
+    def __init__(self, codec: ReedSolomon, chunk_len: int, parts_per_batch: int, depth: int = 4,
+                 flags: int = 0):
         h = _vp()
-        code = _lib.cec_pipeline_new(codec.handle, chunk_len, parts_per_batch, depth,
-                                     ctypes.byref(h))
+        code = _lib.cec_pipeline_new_ex(codec.handle, chunk_len, parts_per_batch, depth, flags,
+                                        ctypes.byref(h))
         if code != OK:
             raise Error(code)
         self._h = h
@@ -517,6 +556,12 @@ class Pipeline:
 
     def submit(self, slot: int, n_parts: int) -> None:
         _check(_lib.cec_pipeline_submit(self._h, slot, n_parts))
+
+    def submit_from(self, slot: int, data, n_parts: int, parity=None, digests=None) -> None:
+        """Batch from the caller's buffers (page-locked ones are DMA'd directly)."""
+        _check(_lib.cec_pipeline_submit_from(self._h, slot, _addr(data), n_parts,
+                                             _addr(parity) if parity is not None else None,
+                                             _addr(digests) if digests is not None else None))
 
     def wait(self, slot: int):
         import numpy as np
@@ -583,6 +628,12 @@ class ReadPipeline:
     def submit(self, slot: int, n_parts: int) -> None:
         _check(_lib.cec_read_pipeline_submit(self._h, slot, n_parts))
 
+    def submit_from(self, slot: int, chunks, present, expected, n_parts: int, data=None) -> None:
+        """Batch from the caller's buffers (page-locked ones are DMA'd directly)."""
+        _check(_lib.cec_read_pipeline_submit_from(
+            self._h, slot, _addr(chunks), _addr(present), _addr(expected), n_parts,
+            _addr(data) if data is not None else None))
+
     def wait(self, slot: int):
         import numpy as np
         data, ok = _u8p(), _u8p()
@@ -610,3 +661,159 @@ class ReadPipeline:
 
     def drain(self) -> None:
         _check(_lib.cec_read_pipeline_drain(self._h))
+
+
+# ---------------------------------------------------------------------------------------------
+# Page-locked host memory (cec_host_alloc): buffers the engine DMAs directly
+# ---------------------------------------------------------------------------------------------
+
+
+def _addr(buf) -> int:
+    """Address of a host buffer: a HostBuffer, a numpy array, or any writable bytes-like."""
+    if isinstance(buf, HostBuffer):
+        return buf.ptr
+    if hasattr(buf, "__array_interface__"):
+        return buf.__array_interface__["data"][0]
+    mv = memoryview(buf)
+    return ctypes.addressof((ctypes.c_char * mv.nbytes).from_buffer(mv.cast("B")))
+
+
+class HostBuffer:
+    """Page-locked, portable host memory from cec_host_alloc (pages on `device`'s NUMA node).
+    ``.array`` is a writable numpy uint8 view; the memory is freed with the object."""
+
+    def __init__(self, nbytes: int, device: int = -1):
+        import numpy as np
+        h = _vp()
+        _check(_lib.cec_host_alloc(nbytes, device, ctypes.byref(h)))
+        self.ptr = h.value
+        self.nbytes = nbytes
+        self.array = np.ctypeslib.as_array(ctypes.cast(h, _u8p), shape=(nbytes,))
+
+    def view(self, *shape):
+        return self.array.reshape(*shape)
+
+    def __del__(self, _free=_lib.cec_host_free):
+        p = getattr(self, "ptr", None)
+        if p:
+            self.array = None
+            _free(p)
+            self.ptr = None
+
+
+def host_is_pinned(buf, nbytes: Optional[int] = None) -> bool:
+    n = nbytes if nbytes is not None else (buf.nbytes if hasattr(buf, "nbytes") else _nbytes(buf))
+    return bool(_lib.cec_host_is_pinned(_addr(buf), n))
+
+
+def host_numa_node(buf) -> int:
+    return _lib.cec_host_numa_node(_addr(buf))
+
+
+def device_numa_node(device: int) -> int:
+    return _lib.cec_device_numa_node(device)
+
+
+def current_device() -> int:
+    d = ctypes.c_int(0)
+    _check(_lib.cec_current_device(ctypes.byref(d)))
+    return d.value
+
+
+def set_device(device: int) -> None:
+    _check(_lib.cec_set_device(device))
+
+
+# ---------------------------------------------------------------------------------------------
+# Multi-GPU part scheduler (cec_multi_*): one process, contiguous part ranges per shard
+# ---------------------------------------------------------------------------------------------
+
+PIPE_EXTERNAL = 2  # CEC_PIPE_EXTERNAL
+
+
+class MultiError(Error):
+    def __init__(self, code: int):
+        Exception.__init__(self, f"{_lib.cec_status_name(code).decode()}: "
+                                 f"{_lib.cec_multi_last_error().decode()}")
+        self.code = code
+        self.name = _lib.cec_status_name(code).decode()
+
+
+class Multi:
+    """cec_multi: FileWriteBuilder::write / FileReadBuilder over several GPUs in one process.
+
+    ``devices`` lists one device ordinal per shard (repeats allowed).  ``encode_hash`` /
+    ``read`` take host buffers (numpy arrays or HostBuffer views; page-locked ones are DMA'd
+    directly) and return a job id for ``wait``; the blocking forms ``encode_hash_sync`` /
+    ``read_sync`` do both.  Shard g owns parts [g*n/G, (g+1)*n/G) of every job."""
+
+    def __init__(self, codec: ReedSolomon, chunk_len: int, parts_per_batch: int, depth: int,
+                 devices: Sequence[int]):
+        h = _vp()
+        devs = (ctypes.c_int * max(len(devices), 1))(*devices)
+        code = _lib.cec_multi_new(codec.handle, chunk_len, parts_per_batch, depth, devs,
+                                  len(devices), ctypes.byref(h))
+        if code != OK:
+            raise Error(code)
+        self._h = h
+        self.codec = codec
+        self.d, self.p = codec.data_shard_count(), codec.parity_shard_count()
+        self.t = self.d + self.p
+        self.L = chunk_len
+        self._keep = {}
+
+    def __del__(self, _free=_lib.cec_multi_free):
+        h = getattr(self, "_h", None)
+        if h:
+            _free(h)
+            self._h = None
+
+    def shards(self) -> int:
+        return _lib.cec_multi_shards(self._h)
+
+    def shard_info(self, g: int):
+        dev, numa, parts = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_uint64(0)
+        _check(_lib.cec_multi_shard_info(self._h, g, ctypes.byref(dev), ctypes.byref(numa),
+                                         ctypes.byref(parts)))
+        return dev.value, numa.value, parts.value
+
+    def encode_hash(self, data, n_parts: int, parity, digests) -> int:
+        job = ctypes.c_uint64(0)
+        code = _lib.cec_multi_encode_hash(self._h, _addr(data), n_parts, _addr(parity),
+                                          _addr(digests), ctypes.byref(job))
+        if code != OK:
+            raise MultiError(code)
+        self._keep[job.value] = (data, parity, digests)
+        return job.value
+
+    def read(self, chunks, present, expected, n_parts: int, data, verified, status,
+             rebuilt_only: bool = False):
+        """Returns (job, data_ptrs) where data_ptrs ([n*d] c_void_p) is filled at wait()."""
+        job = ctypes.c_uint64(0)
+        ptrs = (ctypes.c_void_p * max(n_parts * self.d, 1))()
+        code = _lib.cec_multi_read(self._h, _addr(chunks), _addr(present), _addr(expected),
+                                   n_parts, _addr(data), _addr(verified),
+                                   ctypes.cast(_addr(status), ctypes.POINTER(ctypes.c_int)),
+                                   ptrs, 1 if rebuilt_only else 0, ctypes.byref(job))
+        if code != OK:
+            raise MultiError(code)
+        self._keep[job.value] = (chunks, present, expected, data, verified, status, ptrs)
+        return job.value, ptrs
+
+    def wait(self, job: int) -> None:
+        code = _lib.cec_multi_wait(self._h, job)
+        self._keep.pop(job, None)
+        if code != OK:
+            raise MultiError(code)
+
+    def encode_hash_sync(self, data, n_parts: int, parity, digests) -> None:
+        self.wait(self.encode_hash(data, n_parts, parity, digests))
+
+    def read_sync(self, chunks, present, expected, n_parts: int, data, verified, status,
+                  rebuilt_only: bool = False):
+        job, ptrs = self.read(chunks, present, expected, n_parts, data, verified, status,
+                              rebuilt_only)
+        keep = self._keep[job]
+        self.wait(job)
+        del keep
+        return [p or 0 for p in ptrs[: n_parts * self.d]]

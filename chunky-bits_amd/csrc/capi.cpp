@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstring>
 #include <deque>
+#include <list>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -24,6 +25,7 @@
 #include <vector>
 
 #include "gf256.hpp"
+#include "hostmem.hpp"
 #include "kernels.hpp"
 
 using namespace cec;
@@ -106,22 +108,37 @@ int upload_words(std::vector<uint32_t>&& words, hipStream_t s, uint32_t** dptr) 
 }
 
 // ------------------------------------------------------------------------------------------
-// Per-thread staging for the host-buffer API.
+// Staging contexts for the host-buffer API: a stream + a device buffer, leased per call from a
+// bounded per-device pool (not thread_local: the reference calls the crate from tokio's
+// blocking pool, whose threads come and go, file_part.rs:128,161 / any.rs:19-24, so per-thread
+// resources would leak with every retired thread).  At most kMaxIdleCtx contexts per device
+// stay alive between calls; idle buffers above kMaxIdleBytes are freed when returned.
 // ------------------------------------------------------------------------------------------
-struct ThreadCtx {
+struct StageCtx {
+    int device = 0;
     hipStream_t stream = nullptr;
     uint8_t* dbuf = nullptr;
     size_t dcap = 0;
+    void release_buffer() {
+        if (dbuf) (void)hipFree(dbuf);
+        dbuf = nullptr;
+        dcap = 0;
+    }
+    void destroy() {  // on `device` (callers set it)
+        if (stream) {
+            (void)hipStreamSynchronize(stream);
+            (void)hipStreamDestroy(stream);
+        }
+        stream = nullptr;
+        release_buffer();
+    }
 };
-thread_local std::unordered_map<int, ThreadCtx> t_ctx;
 
-// Stream + device staging of at least device_bytes (grown, never shrunk).
-int ctx_reserve(ThreadCtx& c, size_t device_bytes) {
+// Stream + device staging of at least device_bytes (grown, never shrunk while leased).
+int ctx_reserve(StageCtx& c, size_t device_bytes) {
     if (!c.stream) HIP_TRY(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
     if (c.dcap < device_bytes) {
-        if (c.dbuf) HIP_TRY(hipFree(c.dbuf));
-        c.dbuf = nullptr;
-        c.dcap = 0;
+        c.release_buffer();
         const size_t cap = round_up(std::max<size_t>(device_bytes, 1 << 20), 1 << 20);
         HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c.dbuf), cap));
         c.dcap = cap;
@@ -129,14 +146,69 @@ int ctx_reserve(ThreadCtx& c, size_t device_bytes) {
     return CEC_OK;
 }
 
-int thread_ctx(ThreadCtx** out, size_t device_bytes) {
-    int dev = 0;
-    CEC_TRY(current_device(&dev));
-    ThreadCtx& c = t_ctx[dev];
-    CEC_TRY(ctx_reserve(c, device_bytes));
-    *out = &c;
-    return CEC_OK;
+constexpr size_t kMaxIdleCtx = 8;
+constexpr size_t kMaxIdleBytes = size_t(64) << 20;
+
+class CtxPool {
+   public:
+    std::unique_ptr<StageCtx> take(int device) {
+        std::lock_guard<std::mutex> lk(mu_);
+        auto& v = idle_[device];
+        if (v.empty()) {
+            auto c = std::make_unique<StageCtx>();
+            c->device = device;
+            return c;
+        }
+        auto c = std::move(v.back());
+        v.pop_back();
+        return c;
+    }
+    // The caller's current device is the context's (leases never cross devices).
+    void give(std::unique_ptr<StageCtx> c) {
+        if (!c) return;
+        if (c->stream) (void)hipStreamSynchronize(c->stream);
+        if (c->dcap > kMaxIdleBytes) c->release_buffer();
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            auto& v = idle_[c->device];
+            if (v.size() < kMaxIdleCtx) {
+                v.push_back(std::move(c));
+                return;
+            }
+        }
+        c->destroy();
+    }
+
+   private:
+    std::mutex mu_;
+    std::map<int, std::vector<std::unique_ptr<StageCtx>>> idle_;
+};
+
+// Leaked on purpose: destroying HIP objects from a static destructor races the runtime's own
+// teardown at process exit.
+CtxPool& ctx_pool() {
+    static CtxPool* pool = new CtxPool();
+    return *pool;
 }
+
+// RAII lease of a staging context on the current device.
+class CtxLease {
+   public:
+    CtxLease() = default;
+    CtxLease(const CtxLease&) = delete;
+    CtxLease& operator=(const CtxLease&) = delete;
+    ~CtxLease() { ctx_pool().give(std::move(c_)); }
+    int acquire(size_t device_bytes) {
+        int dev = 0;
+        CEC_TRY(current_device(&dev));
+        c_ = ctx_pool().take(dev);
+        return ctx_reserve(*c_, device_bytes);
+    }
+    StageCtx* operator->() { return c_.get(); }
+
+   private:
+    std::unique_ptr<StageCtx> c_;
+};
 
 // Erasure-pattern key: present bitset (<= 256 shards) + data_only.
 struct PatternKey {
@@ -159,7 +231,12 @@ struct cec_codec {
     std::vector<uint32_t> enc;     // pattern record: parity rows over the d data chunks
     std::mutex mu;
     std::unordered_map<int, uint32_t*> dev_enc;  // encode record per device
-    std::map<PatternKey, std::shared_ptr<const std::vector<uint32_t>>> dec_cache;
+    // Decode records, least recently used first out once kDecCacheCap patterns are cached (every
+    // 1..4-erasure pattern of RS(10,4), both modes, is 2 940).
+    static constexpr size_t kDecCacheCap = 4096;
+    using Record = std::shared_ptr<const std::vector<uint32_t>>;
+    std::list<PatternKey> dec_lru;  // front = most recent
+    std::map<PatternKey, std::pair<Record, std::list<PatternKey>::iterator>> dec_cache;
 
     ~cec_codec() {
         int cur = 0;
@@ -196,7 +273,10 @@ struct cec_codec {
     std::shared_ptr<const std::vector<uint32_t>> decode_record(const PatternKey& key) {
         std::lock_guard<std::mutex> lk(mu);
         auto it = dec_cache.find(key);
-        if (it != dec_cache.end()) return it->second;
+        if (it != dec_cache.end()) {
+            dec_lru.splice(dec_lru.begin(), dec_lru, it->second.second);
+            return it->second.first;
+        }
         const size_t t = d + p;
         std::vector<uint32_t> in_idx, out_idx;
         std::vector<size_t> miss_par;
@@ -231,8 +311,18 @@ struct cec_codec {
         }
         auto rec = std::make_shared<std::vector<uint32_t>>(pattern_words(d, out_idx.size()));
         write_pattern(rec->data(), d, in_idx, out_idx, rows);
-        dec_cache.emplace(key, rec);
+        if (dec_cache.size() >= kDecCacheCap) {
+            dec_cache.erase(dec_lru.back());
+            dec_lru.pop_back();
+        }
+        dec_lru.push_front(key);
+        dec_cache.emplace(key, std::make_pair(Record(rec), dec_lru.begin()));
         return rec;
+    }
+
+    size_t cached_patterns() {
+        std::lock_guard<std::mutex> lk(mu);
+        return dec_cache.size();
     }
 };
 
@@ -291,8 +381,8 @@ int reconstruct_host(const cec_codec* cc, uint8_t* const* shards, const size_t* 
     if (n_out == 0) return CEC_OK;  // data_only with only parity missing
     const size_t cs = round_up(len, kChunkAlign);
     const size_t rec_bytes = round_up(rec->size() * sizeof(uint32_t), kChunkAlign);
-    ThreadCtx* ctx = nullptr;
-    CEC_TRY(thread_ctx(&ctx, rec_bytes + t * cs));
+    CtxLease ctx;
+    CEC_TRY(ctx.acquire(rec_bytes + t * cs));
     uint32_t* drec = reinterpret_cast<uint32_t*>(ctx->dbuf);
     uint8_t* dbase = ctx->dbuf + rec_bytes;
     HIP_TRY(hipMemcpyAsync(drec, rec->data(), rec->size() * sizeof(uint32_t),
@@ -395,7 +485,7 @@ struct PinnedBuf {
 };
 
 struct Arena {
-    ThreadCtx dev;  // stream + device staging
+    StageCtx dev;  // stream + device staging
     PinnedBuf in, out;
 };
 
@@ -509,7 +599,7 @@ class Coalescer {
         auto matching_bytes = [&] {
             size_t b = 0;
             for (Req* q : queue_)
-                if (q->key() == key) b += Impl::bytes(*q);
+                if (q->key() == key) b += Impl::cap_bytes(*q);
             return b;
         };
         auto matching_count = [&] {
@@ -536,12 +626,13 @@ class Coalescer {
         }
         Batch batch_state;
         std::vector<Req*> batch{r};
-        size_t bytes = Impl::bytes(*r);
+        size_t bytes = Impl::cap_bytes(*r);
         for (auto it = queue_.begin(); it != queue_.end();) {
             if (*it == r) {
                 it = queue_.erase(it);
-            } else if ((*it)->key() == key && bytes + Impl::bytes(**it) <= coalesce_max_bytes()) {
-                bytes += Impl::bytes(**it);
+            } else if ((*it)->key() == key &&
+                       bytes + Impl::cap_bytes(**it) <= coalesce_max_bytes()) {
+                bytes += Impl::cap_bytes(**it);
                 batch.push_back(*it);
                 it = queue_.erase(it);
             } else {
@@ -656,6 +747,7 @@ struct ShaImpl {
         for (size_t i = 0; i < r.n; ++i) b += item_bytes(r.lens[i]);
         return b;
     }
+    static size_t cap_bytes(const ShaReq& r) { return bytes(r); }
     static int prepare(std::vector<ShaReq*>& batch, Arena& a) {
         size_t off = 0, items = 0;
         for (ShaReq* r : batch) {
@@ -723,43 +815,85 @@ struct PartReq : ReqBase {
     size_t L = 0;
     uint8_t* parity_out = nullptr;      // p*L bytes
     uint8_t* digests_out = nullptr;     // (d+p)*32 bytes
+    // Page-locked caller buffers (cec_host_alloc): DMA'd directly, no copy-in / copy-out.
+    bool in_pinned = false, out_pinned = false;
+    size_t out_off = 0;                 // parity offset in the pinned output staging
     CoalesceKey key() const { return {codec, L, device}; }
 };
 
-// Pinned layout: input [part][d][cs], output [part][p][cs] then digests [part][d+p][32];
-// device batch [part][d+p][cs] (cs = L rounded up to 256 B).
+// Pinned layout: input [part][d][cs] (staged parts only, at in_off), output [part][p][cs]
+// (staged parts only, at out_off) then digests [part][d+p][32]; device batch [part][d+p][cs]
+// (cs = L rounded up to 256 B).  A batch with no page-locked caller buffer moves with one
+// 2-D copy each way; otherwise every part is copied on its own (pinned ones straight from /
+// into the caller's memory).
 struct PartImpl {
     static size_t cs_of(const PartReq& r) { return round_up(r.L, kChunkAlign); }
     static size_t bytes(const PartReq& r) { return r.codec->d * cs_of(r); }
+    // Weight against CEC_COALESCE_MAX_MIB: the cap bounds the pinned staging a batch needs; a
+    // page-locked caller needs none, so its part counts a quarter (its batch is bounded by the
+    // device buffer, 4x the staging cap).
+    static size_t cap_bytes(const PartReq& r) { return r.in_pinned ? bytes(r) / 4 : bytes(r); }
+    static bool any_pinned(const std::vector<PartReq*>& batch) {
+        for (const PartReq* r : batch)
+            if (r->in_pinned || r->out_pinned) return true;
+        return false;
+    }
+    static size_t digest_base(const std::vector<PartReq*>& batch) {
+        size_t off = 0;
+        for (const PartReq* r : batch)
+            if (!r->out_pinned) off += r->codec->p * cs_of(*r);
+        return off;
+    }
     static int prepare(std::vector<PartReq*>& batch, Arena& a) {
         const cec_codec* c = batch[0]->codec;
         const size_t d = c->d, p = c->p, t = d + p, B = batch.size(), cs = cs_of(*batch[0]);
+        size_t in_bytes = 0, out_bytes = 0;
         for (size_t k = 0; k < B; ++k) {
-            batch[k]->arena = &a;
-            batch[k]->slot = k;
-            batch[k]->item0 = B;  // parts in the batch: locates the digest block
+            PartReq* r = batch[k];
+            r->arena = &a;
+            r->slot = k;
+            r->in_off = in_bytes;
+            r->out_off = out_bytes;
+            if (!r->in_pinned) in_bytes += d * cs;
+            if (!r->out_pinned) out_bytes += p * cs;
         }
-        CEC_TRY(a.in.reserve(B * d * cs, coalesce_max_bytes()));
-        CEC_TRY(a.out.reserve(B * p * cs + B * t * 32,
+        const size_t dig0 = out_bytes;
+        for (PartReq* r : batch) r->item0 = dig0;  // locates the digest block
+        CEC_TRY(a.in.reserve(std::max<size_t>(in_bytes, 1), coalesce_max_bytes()));
+        CEC_TRY(a.out.reserve(out_bytes + B * t * 32,
                               coalesce_max_bytes() / d * p + coalesce_max_bytes() / cs * t * 32));
         return ctx_reserve(a.dev, round_up(B * t * 32, kChunkAlign) + B * t * cs);
     }
     static void copy_in(PartReq& r) {
+        if (r.in_pinned) return;
         const size_t d = r.codec->d, cs = cs_of(r);
-        uint8_t* dst = r.arena->in.ptr + r.slot * d * cs;
+        uint8_t* dst = r.arena->in.ptr + r.in_off;
         for (size_t j = 0; j < d; ++j) std::memcpy(dst + j * cs, r.data_buf + j * r.L, r.L);
     }
     static int run(std::vector<PartReq*>& batch, Arena& a) {
         cec_codec* c = batch[0]->codec;
         const size_t d = c->d, p = c->p, t = d + p, B = batch.size();
         const size_t L = batch[0]->L, cs = cs_of(*batch[0]);
+        const bool per_part = any_pinned(batch);
         uint32_t* drec = nullptr;
         CEC_TRY(c->encode_record(&drec));
         uint8_t* ddig = a.dev.dbuf;
         uint8_t* dbase = a.dev.dbuf + round_up(B * t * 32, kChunkAlign);
         hipStream_t s = a.dev.stream;
-        HIP_TRY(hipMemcpy2DAsync(dbase, t * cs, a.in.ptr, d * cs, d * cs, B,
-                                 hipMemcpyHostToDevice, s));
+        if (!per_part) {
+            HIP_TRY(hipMemcpy2DAsync(dbase, t * cs, a.in.ptr, d * cs, d * cs, B,
+                                     hipMemcpyHostToDevice, s));
+        } else {
+            for (const PartReq* r : batch) {
+                uint8_t* dst = dbase + r->slot * t * cs;
+                if (r->in_pinned)  // d rows of L bytes from the caller's data_buf
+                    HIP_TRY(hipMemcpy2DAsync(dst, cs, r->data_buf, r->L, r->L, d,
+                                             hipMemcpyHostToDevice, s));
+                else
+                    HIP_TRY(hipMemcpyAsync(dst, a.in.ptr + r->in_off, d * cs,
+                                           hipMemcpyHostToDevice, s));
+            }
+        }
         if (fused_covers(uint32_t(d), uint32_t(p), L) && prefer_fused(B * t)) {
             FusedParams f{};
             f.base = dbase;
@@ -794,17 +928,32 @@ struct PartImpl {
             h.digests = ddig;
             HIP_TRY(launch_sha256(h, true, s));
         }
-        HIP_TRY(hipMemcpy2DAsync(a.out.ptr, p * cs, dbase + d * cs, t * cs, p * cs, B,
-                                 hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipMemcpyAsync(a.out.ptr + B * p * cs, ddig, B * t * 32, hipMemcpyDeviceToHost, s));
+        const size_t dig0 = batch[0]->item0;
+        if (!per_part) {
+            HIP_TRY(hipMemcpy2DAsync(a.out.ptr, p * cs, dbase + d * cs, t * cs, p * cs, B,
+                                     hipMemcpyDeviceToHost, s));
+        } else {
+            for (const PartReq* r : batch) {
+                const uint8_t* src = dbase + r->slot * t * cs + d * cs;
+                if (r->out_pinned)  // p rows of L bytes into the caller's parity buffer
+                    HIP_TRY(hipMemcpy2DAsync(r->parity_out, r->L, src, cs, r->L, p,
+                                             hipMemcpyDeviceToHost, s));
+                else
+                    HIP_TRY(hipMemcpyAsync(a.out.ptr + r->out_off, src, p * cs,
+                                           hipMemcpyDeviceToHost, s));
+            }
+        }
+        HIP_TRY(hipMemcpyAsync(a.out.ptr + dig0, ddig, B * t * 32, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         return CEC_OK;
     }
     static void copy_out(PartReq& r) {
         const size_t d = r.codec->d, p = r.codec->p, t = d + p, cs = cs_of(r);
-        const uint8_t* par = r.arena->out.ptr + r.slot * p * cs;
-        for (size_t i = 0; i < p; ++i) std::memcpy(r.parity_out + i * r.L, par + i * cs, r.L);
-        std::memcpy(r.digests_out, r.arena->out.ptr + r.item0 * p * cs + r.slot * t * 32, t * 32);
+        if (!r.out_pinned) {
+            const uint8_t* par = r.arena->out.ptr + r.out_off;
+            for (size_t i = 0; i < p; ++i) std::memcpy(r.parity_out + i * r.L, par + i * cs, r.L);
+        }
+        std::memcpy(r.digests_out, r.arena->out.ptr + r.item0 + r.slot * t * 32, t * 32);
     }
 };
 
@@ -830,6 +979,8 @@ int part_encode_coalesced(cec_codec* c, const uint8_t* data_buf, size_t L, uint8
     r.L = L;
     r.parity_out = parity_out;
     r.digests_out = digests_out;
+    r.in_pinned = pinned_range(data_buf, c->d * L);
+    r.out_pinned = pinned_range(parity_out, c->p * L);
     return g_part_queue.submit(&r);
 }
 
@@ -851,6 +1002,15 @@ int batch_ok(const cec_part_batch* b) {
 extern "C" {
 
 int cec_abi_version(void) { return CEC_ABI_VERSION; }
+
+const char* cec_build_info(void) {
+#ifdef CEC_AB_TOOLS
+    return "chunky_ec gfx950 ab_tools=1 (A/B attribution build: CEC_FUSED_MODE 1/2 and "
+           "CEC_SHA_VARIANT 7/8 produce wrong outputs by design; not for production)";
+#else
+    return "chunky_ec gfx950 ab_tools=0";
+#endif
+}
 
 const char* cec_status_name(int s) {
     switch (s) {
@@ -916,6 +1076,9 @@ void cec_codec_free(cec_codec* c) { delete c; }
 size_t cec_codec_data_shards(const cec_codec* c) { return c ? c->d : 0; }
 size_t cec_codec_parity_shards(const cec_codec* c) { return c ? c->p : 0; }
 size_t cec_codec_total_shards(const cec_codec* c) { return c ? c->d + c->p : 0; }
+size_t cec_codec_cached_patterns(const cec_codec* c) {
+    return c ? const_cast<cec_codec*>(c)->cached_patterns() : 0;
+}
 
 int cec_codec_matrix(const cec_codec* c, uint8_t* out, size_t out_len) {
     if (!c || !out || out_len < c->m.v.size()) return CEC_ERR_INVALID_ARGUMENT;
@@ -951,8 +1114,8 @@ int cec_encode_sep(const cec_codec* cc, const uint8_t* const* data, const size_t
     const size_t t = c->d + c->p, cs = round_up(len, kChunkAlign);
     uint32_t* drec = nullptr;
     CEC_TRY(c->encode_record(&drec));
-    ThreadCtx* ctx = nullptr;
-    CEC_TRY(thread_ctx(&ctx, t * cs));
+    CtxLease ctx;
+    CEC_TRY(ctx.acquire(t * cs));
     for (size_t j = 0; j < c->d; ++j)
         HIP_TRY(hipMemcpyAsync(ctx->dbuf + j * cs, data[j], len, hipMemcpyHostToDevice,
                                ctx->stream));
@@ -1198,26 +1361,86 @@ int cec_verify_batch(const cec_part_batch* b, size_t first_chunk, size_t n_chunk
     return CEC_OK;
 }
 
+}  // extern "C"
+
 namespace {
 
-// Side stream of the speculative decode in cec_read_batch / cec_resilver_batch (per thread and
-// device), with the fork/join events that order it against the caller's stream.
+// Side stream of the speculative decode in cec_read_batch / cec_resilver_batch, with the
+// fork/join events that order it against the caller's stream: leased per call from a bounded
+// per-device pool (see CtxPool for why not thread_local).
 struct SideCtx {
+    int device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
+    void destroy() {
+        if (stream) {
+            (void)hipStreamSynchronize(stream);
+            (void)hipStreamDestroy(stream);
+        }
+        if (fork) (void)hipEventDestroy(fork);
+        if (join) (void)hipEventDestroy(join);
+        stream = nullptr;
+        fork = join = nullptr;
+    }
 };
-thread_local std::unordered_map<int, SideCtx> t_side;
 
-int side_ctx(SideCtx** out) {
-    int dev = 0;
-    CEC_TRY(current_device(&dev));
-    SideCtx& c = t_side[dev];
-    if (!c.stream) HIP_TRY(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
-    if (!c.fork) HIP_TRY(hipEventCreateWithFlags(&c.fork, hipEventDisableTiming));
-    if (!c.join) HIP_TRY(hipEventCreateWithFlags(&c.join, hipEventDisableTiming));
-    *out = &c;
-    return CEC_OK;
+class SidePool {
+   public:
+    std::unique_ptr<SideCtx> take(int device) {
+        std::lock_guard<std::mutex> lk(mu_);
+        auto& v = idle_[device];
+        if (v.empty()) {
+            auto c = std::make_unique<SideCtx>();
+            c->device = device;
+            return c;
+        }
+        auto c = std::move(v.back());
+        v.pop_back();
+        return c;
+    }
+    void give(std::unique_ptr<SideCtx> c) {
+        if (!c) return;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            auto& v = idle_[c->device];
+            if (v.size() < kMaxIdleCtx) {
+                v.push_back(std::move(c));
+                return;
+            }
+        }
+        c->destroy();
+    }
+
+   private:
+    std::mutex mu_;
+    std::map<int, std::vector<std::unique_ptr<SideCtx>>> idle_;
+};
+
+SidePool& side_pool() {
+    static SidePool* pool = new SidePool();  // leaked: see ctx_pool()
+    return *pool;
 }
+
+class SideLease {
+   public:
+    SideLease() = default;
+    SideLease(const SideLease&) = delete;
+    SideLease& operator=(const SideLease&) = delete;
+    ~SideLease() { side_pool().give(std::move(c_)); }
+    int acquire() {
+        int dev = 0;
+        CEC_TRY(current_device(&dev));
+        c_ = side_pool().take(dev);
+        if (!c_->stream) HIP_TRY(hipStreamCreateWithFlags(&c_->stream, hipStreamNonBlocking));
+        if (!c_->fork) HIP_TRY(hipEventCreateWithFlags(&c_->fork, hipEventDisableTiming));
+        if (!c_->join) HIP_TRY(hipEventCreateWithFlags(&c_->join, hipEventDisableTiming));
+        return CEC_OK;
+    }
+    SideCtx* get() { return c_.get(); }
+
+   private:
+    std::unique_ptr<SideCtx> c_;
+};
 
 // LDS each speculative-decode block reserves (A/B knob CEC_SPEC_LDS_KIB).  100 KiB keeps decode
 // blocks off the CUs holding SHA workgroups (>= 64 KiB each) and runs one per free CU: a
@@ -1236,6 +1459,10 @@ bool read_speculate() {
     return !(e && e[0] == '0');
 }
 
+// A loaded chunk is hashed unless the caller marked it CEC_PRESENT_VERIFIED (a read retry's
+// chunks that an earlier pass already verified).
+inline bool needs_hash(uint8_t f) { return f != 0 && f != CEC_PRESENT_VERIFIED; }
+
 // DataVerifier::verify of the loaded chunks (present_host[k*t + i] != 0) of a batch: ok[item] =
 // digest matches (ok of the others is left as is).  The loaded chunks are packed into a
 // compacted item list, so a read with d of d+p chunks loaded runs d/(d+p) of the waves of a
@@ -1246,9 +1473,14 @@ int verify_loaded(const cec_part_batch* b, size_t t, const uint8_t* present_host
     const size_t n = b->n_parts * t;
     const char* knob = std::getenv("CEC_VERIFY_COMPACT");
     if (knob && knob[0] == '0') {  // A/B: strided launch with the skipped lanes
+        std::vector<uint32_t> mask(n);  // chunks to hash: loaded, not already verified
+        for (size_t i = 0; i < n; ++i) mask[i] = needs_hash(present_host[i]) ? 1u : 0u;
+        std::vector<uint8_t> bytes(n);
+        for (size_t i = 0; i < n; ++i) bytes[i] = uint8_t(mask[i]);
         uint8_t* dpresent = nullptr;
         HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&dpresent), n, s));
-        HIP_TRY(hipMemcpyAsync(dpresent, present_host, n, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(dpresent, bytes.data(), n, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipStreamSynchronize(s));  // `bytes` is pageable and local
         CEC_TRY(cec_verify_batch(b, 0, t, dpresent, expected, ok, s));
         HIP_TRY(hipFreeAsync(dpresent, s));
         return CEC_OK;
@@ -1256,7 +1488,7 @@ int verify_loaded(const cec_part_batch* b, size_t t, const uint8_t* present_host
     std::vector<uint32_t> items;
     items.reserve(n);
     for (size_t i = 0; i < n; ++i)
-        if (present_host[i]) items.push_back(uint32_t(i));
+        if (needs_hash(present_host[i])) items.push_back(uint32_t(i));
     if (items.empty()) return CEC_OK;
     const uint32_t n_items = uint32_t(items.size());
     uint32_t* ditems = nullptr;
@@ -1305,9 +1537,11 @@ int verify_then_reconstruct(const cec_codec* c, const cec_part_batch* b,
     HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&ok), n, s));
     HIP_TRY(hipMemsetAsync(ok, 0, n, s));
     // Fork point: the caller's work on s so far (the chunks).
+    SideLease lease;
     SideCtx* side = nullptr;
     if (speculate) {
-        CEC_TRY(side_ctx(&side));
+        CEC_TRY(lease.acquire());
+        side = lease.get();
         HIP_TRY(hipEventRecord(side->fork, s));
     }
     // Verification goes first so its long-lived workgroups claim their CUs (one or two per CU)
@@ -1343,6 +1577,8 @@ int verify_then_reconstruct(const cec_codec* c, const cec_part_batch* b,
     }
     (void)hipFreeAsync(ok, s);
     if (st != CEC_OK) return st;
+    for (size_t i = 0; i < n; ++i)  // verified by an earlier pass: trusted, not hashed again
+        if (present_host[i] == CEC_PRESENT_VERIFIED) verified_host[i] = 1;
     // Parts with fewer than d verified chunks cannot be decoded (the reference's read returns
     // the part short / resilver reports it).  Decode (again) the parts whose loaded chunks did
     // not all verify — or every part, without speculation.
@@ -1365,6 +1601,8 @@ int verify_then_reconstruct(const cec_codec* c, const cec_part_batch* b,
 }
 
 }  // namespace
+
+extern "C" {
 
 int cec_read_batch(const cec_codec* c, const cec_part_batch* b, const uint8_t* present,
                    const uint8_t* expected, uint8_t* verified, int* part_status, void* stream) {

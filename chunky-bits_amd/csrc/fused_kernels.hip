@@ -451,19 +451,29 @@ bool fused_enc3() {
     return !(e && e[0] == '0');
 }
 
+// CEC_FUSED_MODE: 3 = the generic-d build on every shape it covers (correct output; A/B and
+// tests against the shape builds).  Modes 1 and 2 (timing attribution, wrong outputs by design)
+// exist only in the A/B build (-DCEC_AB_TOOLS, `make ab`): the product library ignores them.
 int fused_mode() {
     const char* e = std::getenv("CEC_FUSED_MODE");
-    return e ? std::atoi(e) : 0;
+    const int m = e ? std::atoi(e) : 0;
+#ifdef CEC_AB_TOOLS
+    return m;
+#else
+    return m == 3 ? 3 : 0;
+#endif
 }
 
 template <int STEP>
 hipError_t launch_step(const FusedParams& a, hipStream_t s) {
     const int mode = fused_mode();
     if constexpr (STEP == 256) {
+#ifdef CEC_AB_TOOLS
         if (mode == 1)
             return a.p == 4 ? launch_p<4, STEP, 1, 0>(a, s) : launch_p<8, STEP, 1, 0>(a, s);
         if (mode == 2)
             return a.p == 4 ? launch_p<4, STEP, 2, 0>(a, s) : launch_p<8, STEP, 2, 0>(a, s);
+#endif
         // mode 3: the generic-d build on every shape it covers (A/B and tests against the
         // shape builds)
         if (mode != 3 && a.d == 10 && a.p == 4 && a.len % col_width(10) == 0)

@@ -2,13 +2,15 @@
 // FileWriteBuilder::write's part loop (reference src/file/writer.rs:166-231: read d*chunk_size
 // bytes per part, encode + hash each part, hand back parity and digests in order).
 //
-// A pipeline owns `depth` slots on one GPU.  Each slot has pinned host buffers (the caller
-// writes part data straight into them: no extra host copy), a device batch, and its own HIP
-// stream: H2D (one 2-D copy scattering [part][d][L] into the device's [part][d+p][L]), the fused
-// encode_hash kernel, and D2H of parity + digests are queued on the slot's stream, so the copies
-// of one slot overlap the kernels of the others.  A batch's kernel time is the per-chunk serial
-// SHA-256 time whatever its part count (sha256_kernels.hip), so several modest batches in
-// flight on separate streams (their workgroups run on disjoint CUs) keep the PCIe link busy.
+// A pipeline owns `depth` slots on one GPU.  Each slot has a device batch, its own HIP stream
+// and (unless created with CEC_PIPE_EXTERNAL) pinned host buffers the caller writes part data
+// straight into.  H2D (one 2-D copy scattering [part][d][L] into the device's [part][d+p][L]),
+// the fused encode_hash kernel, and D2H of parity + digests are queued on the slot's stream, so
+// the copies of one slot overlap the kernels of the others.  A batch's kernel time is the
+// per-chunk serial SHA-256 time whatever its part count (sha256_kernels.hip), so several modest
+// batches in flight on separate streams (their workgroups run on disjoint CUs) keep the PCIe link
+// busy.  submit_from takes the caller's own (ideally pinned: cec_host_alloc) buffers instead of
+// the slot's, so the copy engines DMA straight from / into them with no host copy at all.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -33,9 +35,31 @@ int pipe_fail(hipError_t e, const char* what) {
         if (_e != hipSuccess) return pipe_fail(_e, #expr);  \
     } while (0)
 
+// Makes `device` current for a scope and restores the caller's device on every exit path
+// (early error returns included).
+class DeviceGuard {
+   public:
+    explicit DeviceGuard(int device) {
+        err_ = hipGetDevice(&prev_);
+        if (err_ == hipSuccess && prev_ != device) {
+            err_ = hipSetDevice(device);
+            switched_ = err_ == hipSuccess;
+        }
+    }
+    ~DeviceGuard() {
+        if (switched_) (void)hipSetDevice(prev_);
+    }
+    hipError_t status() const { return err_; }
+
+   private:
+    int prev_ = 0;
+    bool switched_ = false;
+    hipError_t err_ = hipSuccess;
+};
+
 struct Slot {
-    uint8_t* h_data = nullptr;    // pinned [parts][d][L]
-    uint8_t* h_parity = nullptr;  // pinned [parts][p][L]
+    uint8_t* h_data = nullptr;    // pinned [parts][d][L] (null with CEC_PIPE_EXTERNAL)
+    uint8_t* h_parity = nullptr;  // pinned [parts][p][L] (null with CEC_PIPE_EXTERNAL)
     uint8_t* h_dig = nullptr;     // pinned [parts][d+p][32]
     uint8_t* d_buf = nullptr;     // device [parts][d+p][cs]
     uint8_t* d_dig = nullptr;     // device [parts][d+p][32]
@@ -43,6 +67,8 @@ struct Slot {
     hipEvent_t done = nullptr;
     bool in_flight = false;
     size_t n_parts = 0;
+    uint8_t* out_parity = nullptr;  // where this batch's parity / digests go
+    uint8_t* out_dig = nullptr;
 };
 
 }  // namespace
@@ -51,6 +77,7 @@ struct cec_pipeline {
     const cec_codec* codec = nullptr;
     int device = 0;
     size_t d = 0, p = 0, t = 0, L = 0, cs = 0, parts = 0;
+    bool external = false;
     std::vector<Slot> slots;
     size_t next = 0;
 
@@ -70,6 +97,44 @@ struct cec_pipeline {
         }
         (void)hipSetDevice(cur);
     }
+
+    // Queue one batch: data [n][d][L] host -> device, encode + hash, parity [n][p][L] and
+    // digests [n][d+p][32] back to host.
+    int submit(Slot& s, const uint8_t* data, size_t n_parts, uint8_t* parity, uint8_t* dig) {
+        DeviceGuard guard(device);
+        PIPE_TRY(guard.status());
+        const size_t dw = d * L, pitch = t * cs;
+        if (cs == L) {
+            PIPE_TRY(hipMemcpy2DAsync(s.d_buf, pitch, data, dw, dw, n_parts, hipMemcpyHostToDevice,
+                                      s.stream));
+        } else {  // chunk stride padded past L: one 2-D copy per data chunk column
+            for (size_t j = 0; j < d; ++j)
+                PIPE_TRY(hipMemcpy2DAsync(s.d_buf + j * cs, pitch, data + j * L, dw, L, n_parts,
+                                          hipMemcpyHostToDevice, s.stream));
+        }
+        cec_part_batch b{s.d_buf, pitch, cs, n_parts, L};
+        int st = cec_encode_hash_batch(codec, &b, s.d_dig, s.stream);
+        if (st != CEC_OK) {
+            g_pipe_error = cec_last_error();
+            return st;
+        }
+        const size_t pw = p * L;
+        if (cs == L) {
+            PIPE_TRY(hipMemcpy2DAsync(parity, pw, s.d_buf + dw, pitch, pw, n_parts,
+                                      hipMemcpyDeviceToHost, s.stream));
+        } else {
+            for (size_t i = 0; i < p; ++i)
+                PIPE_TRY(hipMemcpy2DAsync(parity + i * L, pw, s.d_buf + (d + i) * cs, pitch, L,
+                                          n_parts, hipMemcpyDeviceToHost, s.stream));
+        }
+        PIPE_TRY(hipMemcpyAsync(dig, s.d_dig, n_parts * t * 32, hipMemcpyDeviceToHost, s.stream));
+        PIPE_TRY(hipEventRecord(s.done, s.stream));
+        s.in_flight = true;
+        s.n_parts = n_parts;
+        s.out_parity = parity;
+        s.out_dig = dig;
+        return CEC_OK;
+    }
 };
 
 extern "C" {
@@ -78,7 +143,13 @@ const char* cec_pipeline_last_error(void) { return g_pipe_error.c_str(); }
 
 int cec_pipeline_new(const cec_codec* codec, size_t chunk_len, size_t parts_per_batch,
                      size_t depth, cec_pipeline** out) {
-    if (!codec || !out || chunk_len == 0 || parts_per_batch == 0 || depth == 0 || depth > 16)
+    return cec_pipeline_new_ex(codec, chunk_len, parts_per_batch, depth, 0u, out);
+}
+
+int cec_pipeline_new_ex(const cec_codec* codec, size_t chunk_len, size_t parts_per_batch,
+                        size_t depth, unsigned flags, cec_pipeline** out) {
+    if (!codec || !out || chunk_len == 0 || parts_per_batch == 0 || depth == 0 || depth > 16 ||
+        (flags & ~unsigned(CEC_PIPE_EXTERNAL)))
         return CEC_ERR_INVALID_ARGUMENT;
     *out = nullptr;
     if (cec_device_count() <= 0) return CEC_ERR_NO_DEVICE;
@@ -91,12 +162,19 @@ int cec_pipeline_new(const cec_codec* codec, size_t chunk_len, size_t parts_per_
     pl->L = chunk_len;
     pl->cs = (chunk_len + 255) / 256 * 256;
     pl->parts = parts_per_batch;
+    pl->external = (flags & CEC_PIPE_EXTERNAL) != 0;
     pl->slots.resize(depth);
     for (Slot& s : pl->slots) {
         hipError_t e = hipSuccess;
-        if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&s.h_data), pl->parts * pl->d * pl->L, hipHostMallocDefault);
-        if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&s.h_parity), pl->parts * pl->p * pl->L, hipHostMallocDefault);
-        if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&s.h_dig), pl->parts * pl->t * 32, hipHostMallocDefault);
+        auto host = [&](uint8_t** ptr, size_t bytes) {
+            if (e == hipSuccess)
+                e = hipHostMalloc(reinterpret_cast<void**>(ptr), bytes, hipHostMallocDefault);
+        };
+        if (!pl->external) {
+            host(&s.h_data, pl->parts * pl->d * pl->L);
+            host(&s.h_parity, pl->parts * pl->p * pl->L);
+        }
+        host(&s.h_dig, pl->parts * pl->t * 32);
         if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_buf), pl->parts * pl->t * pl->cs);
         if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_dig), pl->parts * pl->t * 32);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
@@ -115,7 +193,8 @@ void cec_pipeline_free(cec_pipeline* pl) { delete pl; }
 size_t cec_pipeline_depth(const cec_pipeline* pl) { return pl ? pl->slots.size() : 0; }
 
 // Next slot in round-robin order; waits for that slot's previous batch to finish, after which
-// its previous results are no longer valid.  *data receives the pinned [parts][d][L] buffer.
+// its previous results are no longer valid.  *data receives the pinned [parts][d][L] buffer
+// (null for a CEC_PIPE_EXTERNAL pipeline: use submit_from).
 int cec_pipeline_acquire(cec_pipeline* pl, size_t* slot, uint8_t** data) {
     if (!pl || !slot || !data) return CEC_ERR_INVALID_ARGUMENT;
     const size_t i = pl->next;
@@ -133,48 +212,24 @@ int cec_pipeline_acquire(cec_pipeline* pl, size_t* slot, uint8_t** data) {
 // Queue one batch of n_parts (<= parts_per_batch) parts whose data the caller wrote into the
 // slot's pinned buffer: H2D, fused encode + SHA-256 of all d+p chunks, D2H parity + digests.
 int cec_pipeline_submit(cec_pipeline* pl, size_t slot, size_t n_parts) {
-    if (!pl || slot >= pl->slots.size() || n_parts == 0 || n_parts > pl->parts)
+    if (!pl || slot >= pl->slots.size() || n_parts == 0 || n_parts > pl->parts || pl->external)
         return CEC_ERR_INVALID_ARGUMENT;
     Slot& s = pl->slots[slot];
-    int cur = 0;
-    PIPE_TRY(hipGetDevice(&cur));
-    if (cur != pl->device) PIPE_TRY(hipSetDevice(pl->device));
-    const size_t dw = pl->d * pl->L, pitch = pl->t * pl->cs;
-    if (pl->cs == pl->L) {
-        PIPE_TRY(hipMemcpy2DAsync(s.d_buf, pitch, s.h_data, dw, dw, n_parts,
-                                  hipMemcpyHostToDevice, s.stream));
-    } else {  // chunk stride padded past L: one 2-D copy per data chunk column
-        for (size_t j = 0; j < pl->d; ++j)
-            PIPE_TRY(hipMemcpy2DAsync(s.d_buf + j * pl->cs, pitch, s.h_data + j * pl->L, dw, pl->L,
-                                      n_parts, hipMemcpyHostToDevice, s.stream));
-    }
-    cec_part_batch b{s.d_buf, pitch, pl->cs, n_parts, pl->L};
-    int st = cec_encode_hash_batch(pl->codec, &b, s.d_dig, s.stream);
-    if (st != CEC_OK) {
-        g_pipe_error = cec_last_error();
-        return st;
-    }
-    const size_t pw = pl->p * pl->L;
-    if (pl->cs == pl->L) {
-        PIPE_TRY(hipMemcpy2DAsync(s.h_parity, pw, s.d_buf + dw, pitch, pw, n_parts,
-                                  hipMemcpyDeviceToHost, s.stream));
-    } else {
-        for (size_t i = 0; i < pl->p; ++i)
-            PIPE_TRY(hipMemcpy2DAsync(s.h_parity + i * pl->L, pw,
-                                      s.d_buf + (pl->d + i) * pl->cs, pitch, pl->L, n_parts,
-                                      hipMemcpyDeviceToHost, s.stream));
-    }
-    PIPE_TRY(hipMemcpyAsync(s.h_dig, s.d_dig, n_parts * pl->t * 32, hipMemcpyDeviceToHost,
-                            s.stream));
-    PIPE_TRY(hipEventRecord(s.done, s.stream));
-    s.in_flight = true;
-    s.n_parts = n_parts;
-    if (cur != pl->device) PIPE_TRY(hipSetDevice(cur));
-    return CEC_OK;
+    return pl->submit(s, s.h_data, n_parts, s.h_parity, s.h_dig);
 }
 
-// Wait for a submitted slot; *parity = pinned [parts][p][L], *digests = pinned [parts][d+p][32]
-// (chunks in order).  Valid until the slot is acquired again.
+int cec_pipeline_submit_from(cec_pipeline* pl, size_t slot, const uint8_t* data, size_t n_parts,
+                             uint8_t* parity_out, uint8_t* digests_out) {
+    if (!pl || slot >= pl->slots.size() || !data || n_parts == 0 || n_parts > pl->parts)
+        return CEC_ERR_INVALID_ARGUMENT;
+    Slot& s = pl->slots[slot];
+    if (!parity_out && !s.h_parity) return CEC_ERR_INVALID_ARGUMENT;
+    return pl->submit(s, data, n_parts, parity_out ? parity_out : s.h_parity,
+                      digests_out ? digests_out : s.h_dig);
+}
+
+// Wait for a submitted slot; *parity = [parts][p][L], *digests = [parts][d+p][32] (chunks in
+// order) where submit / submit_from put them.  Valid until the slot is acquired again.
 int cec_pipeline_wait(cec_pipeline* pl, size_t slot, const uint8_t** parity,
                       const uint8_t** digests, size_t* n_parts) {
     if (!pl || slot >= pl->slots.size()) return CEC_ERR_INVALID_ARGUMENT;
@@ -183,8 +238,8 @@ int cec_pipeline_wait(cec_pipeline* pl, size_t slot, const uint8_t** parity,
         PIPE_TRY(hipEventSynchronize(s.done));
         s.in_flight = false;
     }
-    if (parity) *parity = s.h_parity;
-    if (digests) *digests = s.h_dig;
+    if (parity) *parity = s.out_parity ? s.out_parity : s.h_parity;
+    if (digests) *digests = s.out_dig ? s.out_dig : s.h_dig;
     if (n_parts) *n_parts = s.n_parts;
     return CEC_OK;
 }
@@ -201,6 +256,8 @@ int cec_pipeline_drain(cec_pipeline* pl) {
     return CEC_OK;
 }
 
+}  // extern "C"
+
 // ------------------------------------------------------------------------------------------
 // Read pipeline (cec_read_pipeline_*): the batched form of FileReadBuilder's part loop
 // (reference src/file/reader.rs:40-75, buffered(5) reads of FilePart::read_with_context,
@@ -216,16 +273,17 @@ int cec_pipeline_drain(cec_pipeline* pl) {
 // with a chunk that failed is decoded again from its verified chunks only (or reported
 // TooFewShardsPresent when fewer than d verify) before wait() returns.
 // ------------------------------------------------------------------------------------------
-}  // extern "C"
 
 namespace {
 
 struct ReadSlot {
     uint8_t* h_chunks = nullptr;    // pinned [parts][t][L]   (caller: loaded chunk bytes)
-    uint8_t* h_present = nullptr;   // pinned [parts][t]      (caller: 1 = loaded)
+    uint8_t* h_present = nullptr;   // pinned [parts][t]      (caller: nonzero = loaded)
     uint8_t* h_expected = nullptr;  // pinned [parts][t][32]  (caller: metadata digests)
     uint8_t* h_data = nullptr;      // pinned [parts][d][L]   (result: data chunks)
     uint8_t* h_ok = nullptr;        // pinned [parts][t]      (result: verified flags)
+    uint8_t* h_hash = nullptr;      // pinned [parts][t]      chunks to hash (loaded, not
+                                    //                        CEC_PRESENT_VERIFIED)
     int* h_status = nullptr;        // host [parts]
     uint8_t* d_buf = nullptr;       // device [parts][t][cs]
     uint8_t* d_expected = nullptr;  // device [parts][t][32]
@@ -235,6 +293,8 @@ struct ReadSlot {
     bool in_flight = false;
     bool checked = false;
     size_t n_parts = 0;
+    const uint8_t* src_chunks = nullptr;  // this batch's chunk bytes (h_chunks or the caller's)
+    uint8_t* dst_data = nullptr;          // this batch's data output (h_data or the caller's)
     std::vector<uint8_t> decode_mask;  // present mask the speculative decode used
     std::vector<const uint8_t*> data_ptrs;  // [parts][d]: where each data chunk is (after wait)
 };
@@ -246,6 +306,7 @@ struct cec_read_pipeline {
     int device = 0;
     size_t d = 0, p = 0, t = 0, L = 0, cs = 0, parts = 0;
     bool rebuilt_only = false;  // CEC_READ_REBUILT_ONLY: D2H only the data chunks rebuilt
+    bool external = false;      // CEC_PIPE_EXTERNAL: no pinned chunk / data slot buffers
     std::vector<ReadSlot> slots;
     size_t next = 0;
 
@@ -259,7 +320,7 @@ struct cec_read_pipeline {
             if (s.stream) (void)hipStreamDestroy(s.stream);
             for (uint8_t* dptr : {s.d_buf, s.d_expected, s.d_flags})
                 if (dptr) (void)hipFree(dptr);
-            for (uint8_t* hptr : {s.h_chunks, s.h_present, s.h_expected, s.h_data, s.h_ok})
+            for (uint8_t* hptr : {s.h_chunks, s.h_present, s.h_expected, s.h_data, s.h_ok, s.h_hash})
                 if (hptr) (void)hipHostFree(hptr);
             delete[] s.h_status;
         }
@@ -271,7 +332,7 @@ struct cec_read_pipeline {
     }
 
     // D2H of the data chunks of part k that were not loaded (the speculative decode rebuilt
-    // them) into their h_data slots: one copy per run of consecutive missing data chunks.
+    // them) into their data slots: one copy per run of consecutive missing data chunks.
     int copy_rebuilt_back(ReadSlot& s, size_t k) const {
         const uint8_t* pr = s.h_present + k * t;
         for (size_t j = 0; j < d;) {
@@ -281,7 +342,7 @@ struct cec_read_pipeline {
             }
             size_t e = j;
             while (e < d && !pr[e]) ++e;
-            uint8_t* dst = s.h_data + (k * d + j) * L;
+            uint8_t* dst = s.dst_data + (k * d + j) * L;
             const uint8_t* src = s.d_buf + (k * t + j) * cs;
             if (cs == L)
                 PIPE_TRY(hipMemcpyAsync(dst, src, (e - j) * L, hipMemcpyDeviceToHost, s.stream));
@@ -293,18 +354,84 @@ struct cec_read_pipeline {
         return CEC_OK;
     }
 
-    // D2H of the d data chunks of parts [k0, k0 + n) into h_data.
+    // D2H of the d data chunks of parts [k0, k0 + n) into the data output.
     int copy_data_back(ReadSlot& s, size_t k0, size_t n) const {
         const size_t pitch = t * cs, dw = d * L;
         if (cs == L) {
-            PIPE_TRY(hipMemcpy2DAsync(s.h_data + k0 * dw, dw, s.d_buf + k0 * pitch, pitch, dw, n,
+            PIPE_TRY(hipMemcpy2DAsync(s.dst_data + k0 * dw, dw, s.d_buf + k0 * pitch, pitch, dw, n,
                                       hipMemcpyDeviceToHost, s.stream));
         } else {
             for (size_t j = 0; j < d; ++j)
-                PIPE_TRY(hipMemcpy2DAsync(s.h_data + k0 * dw + j * L, dw,
+                PIPE_TRY(hipMemcpy2DAsync(s.dst_data + k0 * dw + j * L, dw,
                                           s.d_buf + k0 * pitch + j * cs, pitch, L, n,
                                           hipMemcpyDeviceToHost, s.stream));
         }
+        return CEC_OK;
+    }
+
+    // Queue one batch whose present flags / expected digests are in the slot's pinned arrays.
+    int submit(ReadSlot& s, const uint8_t* chunks, size_t n_parts, uint8_t* data_out) {
+        DeviceGuard guard(device);
+        PIPE_TRY(guard.status());
+        const size_t n = n_parts * t;
+        s.src_chunks = chunks;
+        s.dst_data = data_out;
+        // loaded chunks up: one copy per run of consecutive loaded chunks of a part
+        for (size_t k = 0; k < n_parts; ++k) {
+            const uint8_t* pr = s.h_present + k * t;
+            for (size_t i = 0; i < t;) {
+                if (!pr[i]) {
+                    ++i;
+                    continue;
+                }
+                size_t j = i;
+                while (j < t && pr[j]) ++j;
+                const uint8_t* src = chunks + (k * t + i) * L;
+                uint8_t* dst = s.d_buf + (k * t + i) * cs;
+                if (cs == L)
+                    PIPE_TRY(hipMemcpyAsync(dst, src, (j - i) * L, hipMemcpyHostToDevice, s.stream));
+                else
+                    PIPE_TRY(hipMemcpy2DAsync(dst, cs, src, L, L, j - i, hipMemcpyHostToDevice,
+                                              s.stream));
+                i = j;
+            }
+        }
+        // hash every loaded chunk except those an earlier pass verified (read retries)
+        for (size_t i = 0; i < n; ++i)
+            s.h_hash[i] = s.h_present[i] != 0 && s.h_present[i] != CEC_PRESENT_VERIFIED;
+        PIPE_TRY(hipMemcpyAsync(s.d_expected, s.h_expected, n * 32, hipMemcpyHostToDevice, s.stream));
+        PIPE_TRY(hipMemcpyAsync(s.d_flags, s.h_hash, n, hipMemcpyHostToDevice, s.stream));
+        cec_part_batch b = batch(s, n_parts);
+        int st = cec_verify_batch(&b, 0, t, s.d_flags, s.d_expected, s.d_flags + n, s.stream);
+        // speculative decode from the loaded chunks; parts with fewer than d loaded are skipped
+        // (reported at wait).  Any nonzero flag means loaded, as everywhere else.
+        s.decode_mask.assign(s.h_present, s.h_present + n);
+        for (size_t k = 0; k < n_parts; ++k) {
+            const size_t loaded = size_t(std::count_if(
+                s.decode_mask.begin() + k * t, s.decode_mask.begin() + (k + 1) * t,
+                [](uint8_t f) { return f != 0; }));
+            s.h_status[k] = loaded >= d ? CEC_OK : CEC_TOO_FEW_SHARDS_PRESENT;
+            if (loaded < d)
+                std::fill(s.decode_mask.begin() + k * t, s.decode_mask.begin() + (k + 1) * t,
+                          uint8_t(1));
+        }
+        if (st == CEC_OK) st = cec_reconstruct_batch(codec, &b, s.decode_mask.data(), 1, s.stream);
+        if (st != CEC_OK) {
+            g_pipe_error = cec_last_error();
+            return st;
+        }
+        if (rebuilt_only) {
+            for (size_t k = 0; k < n_parts && st == CEC_OK; ++k)
+                if (s.h_status[k] == CEC_OK) st = copy_rebuilt_back(s, k);
+        } else {
+            st = copy_data_back(s, 0, n_parts);
+        }
+        if (st != CEC_OK) return st;
+        PIPE_TRY(hipMemcpyAsync(s.h_ok, s.d_flags + n, n, hipMemcpyDeviceToHost, s.stream));
+        PIPE_TRY(hipEventRecord(s.done, s.stream));
+        s.in_flight = true;
+        s.checked = false;
+        s.n_parts = n_parts;
         return CEC_OK;
     }
 };
@@ -319,7 +446,7 @@ int cec_read_pipeline_new(const cec_codec* codec, size_t chunk_len, size_t parts
 int cec_read_pipeline_new_ex(const cec_codec* codec, size_t chunk_len, size_t parts_per_batch,
                              size_t depth, unsigned flags, cec_read_pipeline** out) {
     if (!codec || !out || chunk_len == 0 || parts_per_batch == 0 || depth == 0 || depth > 16 ||
-        (flags & ~unsigned(CEC_READ_REBUILT_ONLY)))
+        (flags & ~unsigned(CEC_READ_REBUILT_ONLY | CEC_PIPE_EXTERNAL)))
         return CEC_ERR_INVALID_ARGUMENT;
     *out = nullptr;
     if (cec_device_count() <= 0) return CEC_ERR_NO_DEVICE;
@@ -333,6 +460,7 @@ int cec_read_pipeline_new_ex(const cec_codec* codec, size_t chunk_len, size_t pa
     pl->cs = (chunk_len + 255) / 256 * 256;
     pl->parts = parts_per_batch;
     pl->rebuilt_only = (flags & CEC_READ_REBUILT_ONLY) != 0;
+    pl->external = (flags & CEC_PIPE_EXTERNAL) != 0;
     pl->slots.resize(depth);
     const size_t P = pl->parts, t = pl->t;
     for (ReadSlot& s : pl->slots) {
@@ -343,11 +471,14 @@ int cec_read_pipeline_new_ex(const cec_codec* codec, size_t chunk_len, size_t pa
         auto dev = [&](uint8_t** ptr, size_t bytes) {
             if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(ptr), bytes);
         };
-        host(&s.h_chunks, P * t * pl->L);
+        if (!pl->external) {
+            host(&s.h_chunks, P * t * pl->L);
+            host(&s.h_data, P * pl->d * pl->L);
+        }
         host(&s.h_present, P * t);
         host(&s.h_expected, P * t * 32);
-        host(&s.h_data, P * pl->d * pl->L);
         host(&s.h_ok, P * t);
+        host(&s.h_hash, P * t);
         dev(&s.d_buf, P * t * pl->cs);
         dev(&s.d_expected, P * t * 32);
         dev(&s.d_flags, 2 * P * t);
@@ -386,65 +517,23 @@ int cec_read_pipeline_acquire(cec_read_pipeline* pl, size_t* slot, uint8_t** chu
 }
 
 int cec_read_pipeline_submit(cec_read_pipeline* pl, size_t slot, size_t n_parts) {
-    if (!pl || slot >= pl->slots.size() || n_parts == 0 || n_parts > pl->parts)
+    if (!pl || slot >= pl->slots.size() || n_parts == 0 || n_parts > pl->parts || pl->external)
         return CEC_ERR_INVALID_ARGUMENT;
     ReadSlot& s = pl->slots[slot];
-    int cur = 0;
-    PIPE_TRY(hipGetDevice(&cur));
-    if (cur != pl->device) PIPE_TRY(hipSetDevice(pl->device));
-    const size_t d = pl->d, t = pl->t, L = pl->L, cs = pl->cs, n = n_parts * t;
-    // loaded chunks up: one copy per run of consecutive loaded chunks of a part
-    for (size_t k = 0; k < n_parts; ++k) {
-        const uint8_t* pr = s.h_present + k * t;
-        for (size_t i = 0; i < t;) {
-            if (!pr[i]) {
-                ++i;
-                continue;
-            }
-            size_t j = i;
-            while (j < t && pr[j]) ++j;
-            const uint8_t* src = s.h_chunks + (k * t + i) * L;
-            uint8_t* dst = s.d_buf + (k * t + i) * cs;
-            if (cs == L)
-                PIPE_TRY(hipMemcpyAsync(dst, src, (j - i) * L, hipMemcpyHostToDevice, s.stream));
-            else
-                PIPE_TRY(hipMemcpy2DAsync(dst, cs, src, L, L, j - i, hipMemcpyHostToDevice,
-                                          s.stream));
-            i = j;
-        }
-    }
-    PIPE_TRY(hipMemcpyAsync(s.d_expected, s.h_expected, n * 32, hipMemcpyHostToDevice, s.stream));
-    PIPE_TRY(hipMemcpyAsync(s.d_flags, s.h_present, n, hipMemcpyHostToDevice, s.stream));
-    cec_part_batch b = pl->batch(s, n_parts);
-    int st = cec_verify_batch(&b, 0, t, s.d_flags, s.d_expected, s.d_flags + n, s.stream);
-    // speculative decode from the loaded chunks; parts with fewer than d loaded are skipped
-    // (reported at wait)
-    s.decode_mask.assign(s.h_present, s.h_present + n);
-    for (size_t k = 0; k < n_parts; ++k) {
-        const size_t loaded = size_t(std::count(s.decode_mask.begin() + k * t,
-                                                s.decode_mask.begin() + (k + 1) * t, uint8_t(1)));
-        s.h_status[k] = loaded >= d ? CEC_OK : CEC_TOO_FEW_SHARDS_PRESENT;
-        if (loaded < d) std::fill(s.decode_mask.begin() + k * t, s.decode_mask.begin() + (k + 1) * t, uint8_t(1));
-    }
-    if (st == CEC_OK) st = cec_reconstruct_batch(pl->codec, &b, s.decode_mask.data(), 1, s.stream);
-    if (st != CEC_OK) {
-        g_pipe_error = cec_last_error();
-        return st;
-    }
-    if (pl->rebuilt_only) {
-        for (size_t k = 0; k < n_parts && st == CEC_OK; ++k)
-            if (s.h_status[k] == CEC_OK) st = pl->copy_rebuilt_back(s, k);
-    } else {
-        st = pl->copy_data_back(s, 0, n_parts);
-    }
-    if (st != CEC_OK) return st;
-    PIPE_TRY(hipMemcpyAsync(s.h_ok, s.d_flags + n, n, hipMemcpyDeviceToHost, s.stream));
-    PIPE_TRY(hipEventRecord(s.done, s.stream));
-    s.in_flight = true;
-    s.checked = false;
-    s.n_parts = n_parts;
-    if (cur != pl->device) PIPE_TRY(hipSetDevice(cur));
-    return CEC_OK;
+    return pl->submit(s, s.h_chunks, n_parts, s.h_data);
+}
+
+int cec_read_pipeline_submit_from(cec_read_pipeline* pl, size_t slot, const uint8_t* chunks,
+                                  const uint8_t* present, const uint8_t* expected, size_t n_parts,
+                                  uint8_t* data_out) {
+    if (!pl || slot >= pl->slots.size() || !chunks || n_parts == 0 || n_parts > pl->parts)
+        return CEC_ERR_INVALID_ARGUMENT;
+    ReadSlot& s = pl->slots[slot];
+    if (!data_out && !s.h_data) return CEC_ERR_INVALID_ARGUMENT;
+    const size_t n = n_parts * pl->t;
+    if (present) std::memcpy(s.h_present, present, n);
+    if (expected) std::memcpy(s.h_expected, expected, n * 32);
+    return pl->submit(s, chunks, n_parts, data_out ? data_out : s.h_data);
 }
 
 int cec_read_pipeline_wait(cec_read_pipeline* pl, size_t slot, const uint8_t** data,
@@ -456,8 +545,10 @@ int cec_read_pipeline_wait(cec_read_pipeline* pl, size_t slot, const uint8_t** d
         s.in_flight = false;
     }
     if (!s.checked && s.n_parts) {
-        // parts whose loaded chunks did not all verify: decode again from the verified ones
         const size_t t = pl->t, d = pl->d, n = s.n_parts;
+        for (size_t i = 0; i < n * t; ++i)  // verified by an earlier pass: trusted
+            if (s.h_present[i] == CEC_PRESENT_VERIFIED) s.h_ok[i] = 1;
+        // parts whose loaded chunks did not all verify: decode again from the verified ones
         std::vector<uint8_t> mask(n * t, 1);
         std::vector<size_t> redo;
         for (size_t k = 0; k < n; ++k) {
@@ -477,9 +568,8 @@ int cec_read_pipeline_wait(cec_read_pipeline* pl, size_t slot, const uint8_t** d
             redo.push_back(k);
         }
         if (!redo.empty()) {
-            int cur = 0;
-            PIPE_TRY(hipGetDevice(&cur));
-            if (cur != pl->device) PIPE_TRY(hipSetDevice(pl->device));
+            DeviceGuard guard(pl->device);
+            PIPE_TRY(guard.status());
             cec_part_batch b = pl->batch(s, n);
             int st = cec_reconstruct_batch(pl->codec, &b, mask.data(), 1, s.stream);
             if (st != CEC_OK) {
@@ -491,23 +581,23 @@ int cec_read_pipeline_wait(cec_read_pipeline* pl, size_t slot, const uint8_t** d
                 if (st != CEC_OK) return st;
             }
             PIPE_TRY(hipStreamSynchronize(s.stream));
-            if (cur != pl->device) PIPE_TRY(hipSetDevice(cur));
         }
-        // Where each data chunk is: re-decoded parts and (without REBUILT_ONLY) every part in
-        // h_data; otherwise a loaded chunk stays in the caller's h_chunks slot (it verified:
-        // parts with a failed chunk were re-decoded) and a rebuilt one came back into h_data.
+        // Where each data chunk is: re-decoded parts and (without REBUILT_ONLY) every part in the
+        // data output; otherwise a loaded chunk stays in the chunk buffer it was read from (it
+        // verified: parts with a failed chunk were re-decoded) and a rebuilt one came back into
+        // the data output.
         std::vector<uint8_t> redone(n, 0);
         for (size_t k : redo) redone[k] = 1;
         s.data_ptrs.resize(n * d);
         for (size_t k = 0; k < n; ++k)
             for (size_t j = 0; j < d; ++j) {
                 const bool in_place = pl->rebuilt_only && !redone[k] && s.h_present[k * t + j];
-                s.data_ptrs[k * d + j] =
-                    in_place ? s.h_chunks + (k * t + j) * pl->L : s.h_data + (k * d + j) * pl->L;
+                s.data_ptrs[k * d + j] = in_place ? s.src_chunks + (k * t + j) * pl->L
+                                                  : s.dst_data + (k * d + j) * pl->L;
             }
         s.checked = true;
     }
-    if (data) *data = s.h_data;
+    if (data) *data = s.dst_data ? s.dst_data : s.h_data;
     if (verified) *verified = s.h_ok;
     if (part_status) *part_status = s.h_status;
     if (n_parts) *n_parts = s.n_parts;

@@ -234,6 +234,7 @@ __global__ __launch_bounds__(128) void sha256_split_kernel(ShaParams a) {
     }
 }
 
+#ifdef CEC_AB_TOOLS
 // ------------------------------------------------------------------------------------------
 // v3: split with balanced placement.  512-thread workgroup, one per CU (LDS ring > 80 KiB):
 // waves 0-3 producers, waves 4-7 rounds, so every SIMD carries exactly one rounds wave and one
@@ -381,9 +382,19 @@ hipError_t launch_split4(const ShaParams& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+#endif  // CEC_AB_TOOLS
+
+// CEC_SHA_VARIANT: 1 = lane kernel, 2 = split kernel (both correct; by size when unset).  The
+// experiment kernels 3-5, 7, 8 (7/8 timing attribution with wrong outputs by design) exist only
+// in the A/B build (-DCEC_AB_TOOLS): the product library treats them as unset.
 int sha_variant() {
     const char* e = std::getenv("CEC_SHA_VARIANT");
-    return e ? std::atoi(e) : 0;
+    const int v = e ? std::atoi(e) : 0;
+#ifdef CEC_AB_TOOLS
+    return v;
+#else
+    return v == 1 || v == 2 ? v : 0;
+#endif
 }
 
 // Dynamic LDS requested per lane-kernel workgroup: more than half of the 160 KiB of a CU, so
@@ -465,11 +476,15 @@ hipError_t launch_sha256(const ShaParams& a, bool vec16, hipStream_t s) {
     const int v = sha_variant();
     if (use_split(total)) return launch_split(a, vec16, s);
     if (a.items) return launch_lane(a, vec16, s);
+#ifdef CEC_AB_TOOLS
     if (v == 3 && !a.present && !a.ptrs && vec16) return launch_split4<false>(a, s);
     if (v == 4 && !a.present && !a.ptrs && vec16) return launch_split4<true>(a, s);
     if (v == 7 && !a.present && !a.ptrs && vec16) return launch_split4<true, 1>(a, s);
     if (v == 8 && !a.present && !a.ptrs && vec16) return launch_split4<true, 2>(a, s);
     if (v == 5) return launch_lane(a, vec16, s, true);
+#else
+    (void)v;
+#endif
     return launch_lane(a, vec16, s);
 }
 

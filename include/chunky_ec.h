@@ -84,6 +84,16 @@ const char* cec_status_name(int status);
 const char* cec_last_error(void);
 /* Number of visible HIP devices (0 when none; never fails). */
 int cec_device_count(void);
+/* The calling thread's current HIP device / make `device` current (host threads that drive
+ * several GPUs; every call below works on the calling thread's current device). */
+int cec_current_device(int* device);
+int cec_set_device(int device);
+/* NUMA node of a device's PCIe root (-1 when unknown). */
+int cec_device_numa_node(int device);
+/* Static build description, e.g. "chunky_ec gfx950 ab_tools=0".  The product library is always
+ * ab_tools=0: the timing-attribution kernels (wrong outputs by design) exist only in the
+ * separate A/B build used by tools/ (DESIGN.md §6.1). */
+const char* cec_build_info(void);
 
 /* ---------------------------------------------------------------------------------------- */
 /* Codec: ReedSolomon<galois_8::Field>                                                       */
@@ -100,6 +110,26 @@ size_t cec_codec_parity_shards(const cec_codec* codec);
 size_t cec_codec_total_shards(const cec_codec* codec);
 /* Copies the (d+p) x d coding matrix (row major; top d x d = identity) into out[out_len]. */
 int cec_codec_matrix(const cec_codec* codec, uint8_t* out, size_t out_len);
+/* Decode matrices cached in the codec (one per erasure pattern and mode; least recently used
+ * evicted past 4096 - the crate also bounds its decode-matrix cache). */
+size_t cec_codec_cached_patterns(const cec_codec* codec);
+
+/* ---------------------------------------------------------------------------------------- */
+/* Page-locked host memory                                                                   */
+/* ---------------------------------------------------------------------------------------- */
+
+/* The reference allocates every part's data buffer with vec![0; d*chunk_size] (writer.rs:172)
+ * and parity with vec![vec![0; L]; p] (file_part.rs:158).  Buffers from cec_host_alloc instead
+ * are page-locked and portable (any device may DMA them), with pages on the NUMA node of
+ * `device` (-1: no preference): every entry point below that takes host buffers DMAs straight
+ * from / into them and skips its staging copy.  Contents are undefined (not zeroed). */
+int cec_host_alloc(size_t bytes, int device, void** out);
+void cec_host_free(void* ptr);
+/* 1 if [ptr, ptr + bytes) lies in one page-locked allocation (cec_host_alloc, hipHostMalloc,
+ * hipHostRegister), else 0. */
+int cec_host_is_pinned(const void* ptr, size_t bytes);
+/* NUMA node holding the page at ptr (-1 when unknown). */
+int cec_host_numa_node(const void* ptr);
 
 /* ---------------------------------------------------------------------------------------- */
 /* Host-buffer API: one call per part, staged through the GPU (drop-in for the crate calls) */
@@ -190,6 +220,14 @@ int cec_reconstruct_batch(const cec_codec* codec, const cec_part_batch* batch,
 int cec_verify_batch(const cec_part_batch* batch, size_t first_chunk, size_t n_chunks,
                      const uint8_t* present, const uint8_t* expected, uint8_t* ok, void* stream);
 
+/* Present-flag value for read retries.  The reference's read drops a chunk whose hash fails and
+ * samples another (file_part.rs:92-107) until d chunks verified or none are left.  The batched
+ * reads (cec_read_batch, cec_read_pipeline_*, cec_multi_read) report such a part
+ * CEC_TOO_FEW_SHARDS_PRESENT with its verified flags; the caller loads more chunks for just
+ * those parts and submits them again, marking the chunks already verified CEC_PRESENT_VERIFIED
+ * (they are used but not hashed again) and the new ones 1.  Any other nonzero flag = loaded. */
+#define CEC_PRESENT_VERIFIED 2
+
 /* FilePart::read_with_context compute (file_part.rs:86-129) for every part: verify the loaded
  * chunks (present: HOST flags, n_parts*(d+p)) against expected (DEVICE digests, part-major,
  * chunks in order), then reconstruct_data from the first d verified chunks.  Outputs (HOST):
@@ -220,6 +258,16 @@ int cec_resilver_batch(const cec_codec* codec, const cec_part_batch* batch,
 typedef struct cec_pipeline cec_pipeline;
 int cec_pipeline_new(const cec_codec* codec, size_t chunk_len, size_t parts_per_batch,
                      size_t depth, cec_pipeline** out);
+/* Pipeline flag: no pinned part-data slot buffers; batches come from the caller's own buffers
+ * through *_submit_from (zero-copy when they are page-locked, e.g. cec_host_alloc). */
+#define CEC_PIPE_EXTERNAL 2u
+int cec_pipeline_new_ex(const cec_codec* codec, size_t chunk_len, size_t parts_per_batch,
+                        size_t depth, unsigned flags, cec_pipeline** out);
+/* As cec_pipeline_submit, with the data read from the caller's data [n_parts][d][chunk_len] and
+ * the results written to parity_out [n_parts][p][chunk_len] and digests_out [n_parts][d+p][32]
+ * (NULL: the slot's own buffers).  The buffers must stay valid until the slot's wait. */
+int cec_pipeline_submit_from(cec_pipeline* pipeline, size_t slot, const uint8_t* data,
+                             size_t n_parts, uint8_t* parity_out, uint8_t* digests_out);
 void cec_pipeline_free(cec_pipeline* pipeline);
 size_t cec_pipeline_depth(const cec_pipeline* pipeline);
 int cec_pipeline_acquire(cec_pipeline* pipeline, size_t* slot, uint8_t** data);
@@ -264,6 +312,50 @@ int cec_read_pipeline_new_ex(const cec_codec* codec, size_t chunk_len, size_t pa
  * undefined for parts whose status is not CEC_OK. */
 int cec_read_pipeline_data_chunks(cec_read_pipeline* pipeline, size_t slot,
                                   const uint8_t** ptrs);
+/* As cec_read_pipeline_submit, with the loaded chunk bytes read from the caller's chunks
+ * [n_parts][d+p][chunk_len] and the data written to data_out [n_parts][d][chunk_len] (NULL: the
+ * slot's own buffer); present / expected (NULL: the slot's arrays as filled after acquire) are
+ * copied in at submit.  chunks and data_out must stay valid until the slot is acquired again
+ * (REBUILT_ONLY data_chunks pointers may point into chunks). */
+int cec_read_pipeline_submit_from(cec_read_pipeline* pipeline, size_t slot, const uint8_t* chunks,
+                                  const uint8_t* present, const uint8_t* expected, size_t n_parts,
+                                  uint8_t* data_out);
+
+/* ---------------------------------------------------------------------------------------- */
+/* Multi-GPU part scheduler (one process, several GPUs: SURVEY.md §8e)                       */
+/* ---------------------------------------------------------------------------------------- */
+
+/* The reference writes and reads a file from one process (FileWriteBuilder::write's part loop,
+ * writer.rs:117-255; FileReadBuilder, reader.rs:32-74).  A cec_multi runs one worker thread per
+ * entry of devices[n_devices] (an ordinal may repeat: several shards on one GPU); each worker
+ * binds to its device's NUMA node and streams its share through its own pipelines of `depth`
+ * slots of parts_per_batch parts.  A job of n parts in file order gives shard g the contiguous
+ * range [g*n/G, (g+1)*n/G); every result lands at its part's own position (file order).  Jobs
+ * are asynchronous (wait with cec_multi_wait; buffers stay the caller's and must live until
+ * then) and run in submission order.  Page-locked caller buffers (cec_host_alloc) are DMA'd
+ * directly; others go through the workers' NUMA-local pinned staging. */
+typedef struct cec_multi cec_multi;
+int cec_multi_new(const cec_codec* codec, size_t chunk_len, size_t parts_per_batch, size_t depth,
+                  const int* devices, size_t n_devices, cec_multi** out);
+void cec_multi_free(cec_multi* multi);
+size_t cec_multi_shards(const cec_multi* multi);
+/* Shard g's device ordinal, its NUMA node, and the parts it has processed. */
+int cec_multi_shard_info(cec_multi* multi, size_t g, int* device, int* numa_node, uint64_t* parts);
+/* write_with_encoder's compute for n_parts parts: data [n][d][L] (each part's zero-padded
+ * data_buf) -> parity [n][p][L], digests [n][d+p][32] (chunks in order). */
+int cec_multi_encode_hash(cec_multi* multi, const uint8_t* data, size_t n_parts, uint8_t* parity,
+                          uint8_t* digests, uint64_t* job);
+/* read_with_context's compute for n_parts parts: chunks [n][d+p][L] (loaded chunk bytes; only
+ * chunks with present != 0 are read), present [n][d+p], expected [n][d+p][32] -> data [n][d][L]
+ * (the part bytes), verified [n][d+p], part_status [n] (CEC_OK / CEC_TOO_FEW_SHARDS_PRESENT).
+ * flags = CEC_READ_REBUILT_ONLY: data receives only the rebuilt data chunks and data_ptrs[n*d]
+ * (required then; optional otherwise) says where each data chunk of each part is. */
+int cec_multi_read(cec_multi* multi, const uint8_t* chunks, const uint8_t* present,
+                   const uint8_t* expected, size_t n_parts, uint8_t* data, uint8_t* verified,
+                   int* part_status, const uint8_t** data_ptrs, unsigned flags, uint64_t* job);
+/* Blocks until the job is done; returns its first error (message: cec_multi_last_error). */
+int cec_multi_wait(cec_multi* multi, uint64_t job);
+const char* cec_multi_last_error(void);
 
 /* ---------------------------------------------------------------------------------------- */
 /* Utilities for benchmarks and tests                                                        */

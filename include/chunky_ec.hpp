@@ -243,10 +243,13 @@ class ReedSolomon {
 };
 
 namespace detail {
-// Host-staged pipelines pin GiBs of host memory (~0.35 s per GiB to pin), so they are made
-// once per thread and shape and reused by every later write/read of that shape.
+// Host-staged pipelines pin GiBs of host memory (~0.35 s per GiB to pin), so the most recent one
+// of each kind is kept per thread and reused by every later write/read of the same shape on the
+// same device.  One entry per thread and kind: a new shape (or device) frees the old pipeline
+// before pinning the next, so the pinned total stays bounded by the threads that use it.
 template <typename Pipe>
 struct CachedPipe {
+    std::array<size_t, 6> key{};
     std::shared_ptr<ReedSolomon> codec;
     std::shared_ptr<Pipe> pipe;
 };
@@ -254,14 +257,17 @@ struct CachedPipe {
 template <typename Pipe, typename New, typename Free>
 CachedPipe<Pipe>& cached_pipe(size_t d, size_t p, size_t L, size_t parts, size_t depth, New make,
                               Free free_fn) {
-    using Key = std::array<size_t, 5>;
-    thread_local std::map<Key, CachedPipe<Pipe>> cache;
-    CachedPipe<Pipe>& e = cache[Key{d, p, L, parts, depth}];
-    if (!e.pipe) {
+    thread_local CachedPipe<Pipe> e;
+    int device = 0;
+    (void)cec_current_device(&device);
+    const std::array<size_t, 6> key{d, p, L, parts, depth, size_t(device)};
+    if (!e.pipe || e.key != key) {
+        e.pipe.reset();  // unpin the old slots first
         e.codec = std::make_shared<ReedSolomon>(d, p);
         Pipe* raw = nullptr;
         make(e.codec->raw(), L, parts, depth, &raw);
         e.pipe = std::shared_ptr<Pipe>(raw, free_fn);
+        e.key = key;
     }
     return e;
 }
@@ -519,8 +525,12 @@ struct FileReference {
         size_t k = 0;
         while (k < parts.size()) {
             size_t run = 1;
+            // A run shares one pipeline, so its parts must share the whole shape: the metadata
+            // allows a different d/p per part (file_part.rs:77 builds a codec per part).
             while (parts_per_batch && k + run < parts.size() &&
-                   parts[k + run].chunksize == parts[k].chunksize)
+                   parts[k + run].chunksize == parts[k].chunksize &&
+                   parts[k + run].data.size() == parts[k].data.size() &&
+                   parts[k + run].parity.size() == parts[k].parity.size())
                 ++run;
             if (run < 2) {
                 Bytes b = parts[k].read_with_context(src);

@@ -1,0 +1,372 @@
+"""GPU tests of the multi-GPU part scheduler (cec_multi_*), the zero-copy paths for
+page-locked caller buffers (cec_host_alloc, *_submit_from, per-call DMA), and the library's
+behaviour in a long-running multi-threaded host (pooled staging, bounded caches).
+
+Everything runs through the C-ABI and is compared bit for bit with the oracle / hashlib.
+"""
+import hashlib
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import oracle
+from _gen import gen_bytes
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+import chunky_ec as ce  # noqa: E402
+
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("no GPU", allow_module_level=True)
+
+
+def _write_inputs(n, d, L, seed):
+    return gen_bytes(seed, n * d * L).reshape(n, d, L)
+
+
+def _check_write(data, parity, digests, d, p):
+    for k in range(data.shape[0]):
+        st, par = oracle.encode_sep(d, p, [data[k, j] for j in range(d)])
+        assert st == 0
+        for i in range(p):
+            assert np.array_equal(parity[k, i], par[i]), (k, i)
+        chunks = [data[k, j] for j in range(d)] + par
+        for j in range(d + p):
+            assert digests[k, j].tobytes() == hashlib.sha256(chunks[j].tobytes()).digest(), (k, j)
+
+
+def _device_lists():
+    n = torch.cuda.device_count()
+    lists = [list(range(n)), [0, 0]]  # every visible device; a forced 2-shard split on one
+    if n > 1:
+        lists.append([n - 1, 0, n - 1])
+    return lists
+
+
+# ----------------------------------------------------------------------------------------------
+# Multi-GPU scheduler: write
+# ----------------------------------------------------------------------------------------------
+
+@pytest.mark.parametrize("devices", _device_lists())
+@pytest.mark.parametrize("pinned", [False, True])
+@pytest.mark.parametrize("d,p,L,n,ppb", [(10, 4, 4096, 37, 4), (3, 2, 683, 11, 3),
+                                         (20, 8, 1024, 9, 2)])
+def test_multi_encode_hash_vs_oracle(devices, pinned, d, p, L, n, ppb):
+    rs = ce.ReedSolomon(d, p)
+    m = ce.Multi(rs, L, ppb, 3, devices)
+    assert m.shards() == len(devices)
+    src = _write_inputs(n, d, L, 100 * d + L)
+    if pinned:
+        hb = [ce.HostBuffer(n * d * L, devices[0]), ce.HostBuffer(n * p * L),
+              ce.HostBuffer(n * (d + p) * 32)]
+        data, parity, dig = hb[0].view(n, d, L), hb[1].view(n, p, L), hb[2].view(n, d + p, 32)
+        assert ce.host_is_pinned(hb[0]) and ce.host_is_pinned(hb[1])
+    else:
+        data = np.empty((n, d, L), np.uint8)
+        parity = np.zeros((n, p, L), np.uint8)
+        dig = np.zeros((n, d + p, 32), np.uint8)
+        assert not ce.host_is_pinned(data)
+    data[:] = src
+    # two jobs in flight, then a third reusing the first's buffers after its wait
+    j1 = m.encode_hash(data, n, parity, dig)
+    half = n // 2
+    par2 = np.zeros((half, p, L), np.uint8)
+    dig2 = np.zeros((half, d + p, 32), np.uint8)
+    j2 = m.encode_hash(data[n - half:], half, par2, dig2)
+    m.wait(j1)
+    m.wait(j2)
+    _check_write(src, parity, dig, d, p)
+    _check_write(src[n - half:], par2, dig2, d, p)
+    # contiguous ranges: shard g processed n*(g+1)//G - n*g//G parts of each job
+    G = len(devices)
+    for g in range(G):
+        dev, numa, parts = m.shard_info(g)
+        assert dev == devices[g]
+        want = (n * (g + 1) // G - n * g // G) + (half * (g + 1) // G - half * g // G)
+        assert parts == want
+
+
+def test_multi_empty_and_tiny_jobs():
+    d, p, L = 4, 2, 256
+    rs = ce.ReedSolomon(d, p)
+    m = ce.Multi(rs, L, 2, 2, [0, 0, 0])
+    m.encode_hash_sync(np.zeros((1, d, L), np.uint8), 0, np.zeros(1, np.uint8),
+                       np.zeros(1, np.uint8))
+    # fewer parts than shards: some shards get an empty range
+    src = _write_inputs(2, d, L, 5)
+    par = np.zeros((2, p, L), np.uint8)
+    dig = np.zeros((2, d + p, 32), np.uint8)
+    m.encode_hash_sync(src.copy(), 2, par, dig)
+    _check_write(src, par, dig, d, p)
+
+
+# ----------------------------------------------------------------------------------------------
+# Multi-GPU scheduler: read (read_with_context compute)
+# ----------------------------------------------------------------------------------------------
+
+def _read_case(n, d, p, L, seed):
+    """Encoded parts, loaded sets like file_part.rs:97 (d random of d+p, or more, or fewer), a
+    few corrupted loaded chunks; expected statuses from the oracle's rules."""
+    t = d + p
+    rng = np.random.default_rng(seed)
+    data = _write_inputs(n, d, L, seed)
+    chunks = np.zeros((n, t, L), np.uint8)
+    expected = np.zeros((n, t, 32), np.uint8)
+    present = np.zeros((n, t), np.uint8)
+    ok = np.zeros((n, t), np.uint8)
+    for k in range(n):
+        st, par = oracle.encode_sep(d, p, [data[k, j] for j in range(d)])
+        full = [data[k, j] for j in range(d)] + par
+        for i in range(t):
+            chunks[k, i] = full[i]
+            expected[k, i] = np.frombuffer(hashlib.sha256(full[i].tobytes()).digest(), np.uint8)
+        kind = k % 6
+        size = {0: t, 1: d, 2: d - 1, 3: d + 1, 4: d, 5: d + 1}[kind]
+        loaded = rng.choice(t, size, replace=False)
+        present[k, loaded] = 1 if kind != 5 else 0xFF  # any nonzero flag means loaded
+        ok[k] = present[k] != 0
+        if kind in (3, 4):  # corrupt one loaded chunk
+            victim = int(loaded[0])
+            chunks[k, victim, L // 3] ^= 0x44
+            ok[k, victim] = 0
+        for i in range(t):
+            if not present[k, i]:
+                chunks[k, i] = 0
+    status = [0 if ok[k].sum() >= d else 10 for k in range(n)]
+    return data, chunks, present, expected, ok, status
+
+
+@pytest.mark.parametrize("devices", _device_lists())
+@pytest.mark.parametrize("pinned", [False, True])
+@pytest.mark.parametrize("rebuilt_only", [False, True])
+def test_multi_read_vs_oracle(devices, pinned, rebuilt_only):
+    d, p, L, n = 10, 4, 2048, 30
+    t = d + p
+    rs = ce.ReedSolomon(d, p)
+    m = ce.Multi(rs, L, 4, 2, devices)
+    data, chunks, present, expected, ok, status = _read_case(n, d, p, L, 77)
+    if pinned:
+        hb = [ce.HostBuffer(n * t * L), ce.HostBuffer(n * d * L)]
+        ch, out = hb[0].view(n, t, L), hb[1].view(n, d, L)
+        ch[:] = chunks
+        out[:] = 0
+    else:
+        ch, out = chunks.copy(), np.zeros((n, d, L), np.uint8)
+    ver = np.zeros((n, t), np.uint8)
+    st = np.zeros(n, np.int32)
+    ptrs = m.read_sync(ch, present, expected, n, out, ver, st, rebuilt_only)
+    assert list(st) == status
+    assert np.array_equal(ver, ok)
+    for k in range(n):
+        if status[k]:
+            continue
+        got = b"".join(__import__("ctypes").string_at(ptrs[k * d + j], L) for j in range(d))
+        assert got == data[k].tobytes(), k
+        if not rebuilt_only:
+            assert np.array_equal(out[k], data[k]), k
+
+
+# ----------------------------------------------------------------------------------------------
+# world-size-2 gloo: two ranks on cuda:0, each drives the HIP path for its own part range
+# ----------------------------------------------------------------------------------------------
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _rank_worker(rank, world, port, n_parts, out_q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for pth in (root, os.path.join(root, "chunky-bits_amd"), os.path.join(root, "tests")):
+        if pth not in sys.path:
+            sys.path.insert(0, pth)
+    import torch
+    import torch.distributed as dist
+    import chunky_ec as ce
+    from chunky_ec.sharding import barrier, max_over_ranks, part_range
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        d, p, L = 10, 4, 4096
+        t = d + p
+        lo, hi = part_range(n_parts, rank, world)
+        buf = torch.zeros((hi - lo, t, L), dtype=torch.uint8, device="cuda:0")
+        batch = ce.PartBatch.from_tensor(buf, L)
+        host = np.stack([gen_bytes(20_000 + k, d * L).reshape(d, L) for k in range(lo, hi)])
+        buf[:, :d].copy_(torch.from_numpy(host))
+        dig = torch.zeros((hi - lo, t, 32), dtype=torch.uint8, device="cuda:0")
+        rs = ce.ReedSolomon(d, p)
+        barrier(world)
+        ce.encode_hash_batch(rs, batch, dig.data_ptr())
+        torch.cuda.synchronize()
+        barrier(world)
+        el = max_over_ranks(float(rank + 1), world, None)
+        out_q.put((rank, lo, hi, el, buf[:, d:].cpu().numpy(), dig.cpu().numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_gloo_drives_hip_path_vs_oracle():
+    import torch.multiprocessing as mp
+    world, n_parts = 2, 11
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_worker, args=(r, world, port, n_parts, q))
+             for r in range(world)]
+    for pr in procs:
+        pr.start()
+    results = [q.get(timeout=180) for _ in range(world)]
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    covered = []
+    d, p, L = 10, 4, 4096
+    for rank, lo, hi, el, parity, dig in results:
+        assert el == 2.0  # max over ranks
+        covered.extend(range(lo, hi))
+        for k in range(lo, hi):
+            data = gen_bytes(20_000 + k, d * L).reshape(d, L)
+            st, par = oracle.encode_sep(d, p, list(data))
+            for i in range(p):
+                assert np.array_equal(parity[k - lo, i], par[i]), (rank, k, i)
+            chunks = list(data) + par
+            for j in range(d + p):
+                assert dig[k - lo, j].tobytes() == hashlib.sha256(chunks[j].tobytes()).digest()
+    assert sorted(covered) == list(range(n_parts))
+
+
+# ----------------------------------------------------------------------------------------------
+# Zero-copy pipelines and per-call DMA
+# ----------------------------------------------------------------------------------------------
+
+def test_pipeline_submit_from_pinned_and_pageable():
+    d, p, L, P = 10, 4, 4096, 6
+    rs = ce.ReedSolomon(d, p)
+    pl = ce.Pipeline(rs, L, P, 2, ce.PIPE_EXTERNAL)
+    src = _write_inputs(P, d, L, 9)
+    hin, hpar = ce.HostBuffer(P * d * L), ce.HostBuffer(P * p * L)
+    hin.view(P, d, L)[:] = src
+    dig = np.zeros((P, d + p, 32), np.uint8)
+    s0, _ = pl.acquire()
+    pl.submit_from(s0, hin.view(P, d, L), P, hpar.view(P, p, L), dig)
+    par_a, dig_a = pl.wait(s0)
+    _check_write(src, hpar.view(P, p, L), dig, d, p)
+    s1, _ = pl.acquire()
+    pageable = src.copy()
+    par2 = np.zeros((P, p, L), np.uint8)
+    pl.submit_from(s1, pageable, P, par2, None)  # digests into the slot's own buffer
+    _, dig_b = pl.wait(s1)
+    _check_write(src, par2, dig_b, d, p)
+
+
+def test_per_call_mixed_pinned_and_pageable_callers_bit_exact():
+    """cec_part_encode from page-locked buffers (DMA'd directly) and from pageable ones (staged)
+    in the same coalesced batches: every caller gets its own part's parity and digests."""
+    import ctypes
+    from concurrent.futures import ThreadPoolExecutor
+    d, p = 10, 4
+    rs = ce.ReedSolomon(d, p)
+    L = 65536
+
+    def task(i):
+        src = gen_bytes(7000 + i, d * L)
+        if i % 2:
+            hb_in, hb_out = ce.HostBuffer(d * L), ce.HostBuffer(p * L)
+            data, par = hb_in.array, hb_out.array
+            data[:] = src
+        else:
+            data, par = src.copy(), np.zeros(p * L, np.uint8)
+        dig = (ctypes.c_uint8 * (32 * (d + p)))()
+        cs = ctypes.c_size_t(0)
+        code = ce._lib.cec_part_encode(rs.handle, ctypes.cast(ce._addr(data), ce._u8p), d * L,
+                                       ctypes.cast(ce._addr(par), ce._u8p), dig, ctypes.byref(cs))
+        assert code == 0
+        _, ref, rdig = oracle.part_encode(d, p, src, d * L)
+        assert np.array_equal(par.reshape(p, L), np.stack(ref)), i
+        assert bytes(dig) == b"".join(x.tobytes() for x in rdig), i
+        return i
+
+    c0, l0 = ce.coalesce_stats()
+    with ThreadPoolExecutor(max_workers=24) as ex:
+        assert sorted(ex.map(task, range(48))) == list(range(48))
+    c1, l1 = ce.coalesce_stats()
+    assert l1 - l0 < c1 - c0
+
+
+# ----------------------------------------------------------------------------------------------
+# Long-running host: pooled staging, no per-thread leaks, product build ignores A/B modes
+# ----------------------------------------------------------------------------------------------
+
+def test_many_short_lived_threads_do_not_leak_device_memory():
+    """Tokio's blocking pool retires threads; 200 short-lived threads that each call the
+    per-call entry points must leave device memory where it was (pooled staging)."""
+    import threading
+    d, p, L = 10, 4, 8192
+    rs = ce.ReedSolomon(d, p)
+    src = gen_bytes(1, d * L).tobytes()
+
+    def body():
+        ce.Sha256Hash.from_buf(src[:1000])
+        ce.part_encode(rs, src, d * L)
+        shards = [bytearray(src[j * L:(j + 1) * L]) for j in range(d)] + [None] * p
+        rs.reconstruct(shards)  # rebuilds parity: per-call staging context
+        rs.encode_sep([src[j * L:(j + 1) * L] for j in range(d)], [bytearray(L) for _ in range(p)])
+
+    def wave(n):
+        ths = [threading.Thread(target=body) for _ in range(n)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        torch.cuda.synchronize()
+
+    wave(200)  # warm: pools and coalescing arenas reach their steady size
+    free0, _ = torch.cuda.mem_get_info()
+    wave(200)
+    wave(200)
+    free1, _ = torch.cuda.mem_get_info()
+    assert free0 - free1 <= (1 << 20), (free0 - free1)
+
+
+def test_product_build_ignores_attribution_modes(monkeypatch):
+    assert "ab_tools=0" in ce.build_info()
+    d, p, L, n = 10, 4, 4096, 20
+    for knob, val in [("CEC_FUSED_MODE", "1"), ("CEC_FUSED_MODE", "2"), ("CEC_SHA_VARIANT", "7"),
+                      ("CEC_SHA_VARIANT", "8")]:
+        monkeypatch.setenv(knob, val)
+        monkeypatch.setenv("CEC_FUSED", "1")
+        buf = torch.zeros((n, d + p, L), dtype=torch.uint8, device="cuda:0")
+        batch = ce.PartBatch.from_tensor(buf, L)
+        ce.fill_synthetic(batch, d, 3)
+        dig = torch.zeros((n, d + p, 32), dtype=torch.uint8, device="cuda:0")
+        ce.encode_hash_batch(ce.ReedSolomon(d, p), batch, dig.data_ptr())
+        torch.cuda.synchronize()
+        host, hd = buf.cpu().numpy(), dig.cpu().numpy()
+        _check_write(host[:, :d], host[:, d:], hd, d, p)
+        monkeypatch.delenv(knob)
+
+
+def test_decode_cache_is_bounded_lru():
+    d, p, L = 20, 8, 16
+    rs = ce.ReedSolomon(d, p)
+    full = [bytes([i]) * L for i in range(d + p)]
+    rng = np.random.default_rng(3)
+    seen = set()
+    while len(seen) < 4200:
+        miss = tuple(sorted(rng.choice(d + p, 3, replace=False).tolist()))
+        if miss in seen:
+            continue
+        seen.add(miss)
+        shards = [None if i in miss else bytearray(full[i]) for i in range(d + p)]
+        rs.reconstruct(shards)
+    assert rs.cached_patterns() == 4096
