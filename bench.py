@@ -52,43 +52,68 @@ CONFIGS = {
     # BASELINE.json configs[1]: the metric's workload.
     "c2": dict(d=10, p=4, chunk=1 * MiB, parts=4096, op="encode_hash",
                workload="C2: batched RS(10,4) encode_sep + SHA-256 of all 14 chunks per part, "
-                        "4096 parts x 1 MiB chunks per GPU"),
+                        "{parts} parts x {chunk} chunks per GPU"),
     # configs[2]: reconstruct, 1-4 random erasures per part (data + parity rebuilt).
     "c3": dict(d=10, p=4, chunk=1 * MiB, parts=4096, op="reconstruct",
                workload="C3: RS(10,4) reconstruct, 1-4 random erasures per part, "
-                        "4096 parts x 1 MiB chunks per GPU"),
+                        "{parts} parts x {chunk} chunks per GPU"),
+    # north_star's reconstruct target: exactly 2 random erasures per part (of the 14), the read
+    # path's reconstruct_data (file_part.rs:128) as the step, resilver's reconstruct
+    # (file_part.rs:304) timed beside it.
+    "c3e2": dict(d=10, p=4, chunk=1 * MiB, parts=4096, op="reconstruct_e2",
+                 workload="C3 2-erasure: RS(10,4) reconstruct_data with exactly 2 random erasures "
+                          "per part (reconstruct of the same parts timed beside it), {parts} parts "
+                          "x {chunk} chunks per GPU"),
     # configs[3]: wide stripe with fused per-chunk hashing.
     "c4": dict(d=20, p=8, chunk=256 * 1024, parts=4096, op="encode_hash",
                workload="C4: RS(20,8) encode_sep + SHA-256 of all 28 chunks per part, "
-                        "4096 parts x 256 KiB chunks per GPU"),
+                        "{parts} parts x {chunk} chunks per GPU"),
     # configs[4]: host-staged stream through pinned double-buffered slots (PCIe-bound);
     # --stream-gib sets the stream size (default 1 TiB split across the ranks: strong scaling).
     "c5": dict(d=10, p=4, chunk=1 * MiB, parts=256, op="stream",
-               workload="C5: 1 TiB synthetic object stream, RS(10,4) encode + SHA-256, 1 MiB "
-                        "chunks, pinned-host staged batches of 256 parts, 4 slots in flight"),
+               workload="C5: {stream} synthetic object stream, RS(10,4) encode + SHA-256, {chunk} "
+                        "chunks, pinned-host staged batches of {parts} parts, 4 slots in flight"),
     # configs[4], read side: the same stream read back through verify + repair (FileReadBuilder /
     # read_with_context batched): d random chunks loaded per part, verified, data rebuilt.
     "c5r": dict(d=10, p=4, chunk=1 * MiB, parts=256, op="read_stream",
-                workload="C5 read side: 1 TiB synthetic object stream read back, RS(10,4), d random "
-                         "chunks loaded per part, SHA-256 verify + reconstruct_data, pinned-host "
-                         "staged batches of 256 parts, 4 slots in flight, rebuilt data chunks "
-                         "back (loaded ones stay in the pinned slot)"),
+                workload="C5 read side: {stream} synthetic object stream read back, RS(10,4), d "
+                         "random chunks loaded per part, SHA-256 verify + reconstruct_data, "
+                         "pinned-host staged batches of {parts} parts, 4 slots in flight, rebuilt "
+                         "data chunks back (loaded ones stay in the pinned buffer)"),
     # configs[2], device-resident read: FilePart::read_with_context batched -- d random chunks
     # loaded per part (file_part.rs:86-122), SHA-256 verify + reconstruct_data of the missing data
     # chunks (the decode runs speculatively beside the verification).
     "c3r": dict(d=10, p=4, chunk=1 * MiB, parts=4096, op="read",
                 workload="C3 read: RS(10,4) read_with_context batched, d random chunks loaded per "
-                         "part, SHA-256 verify + reconstruct_data, 4096 parts x 1 MiB chunks per "
-                         "GPU"),
+                         "part, SHA-256 verify + reconstruct_data, {parts} parts x {chunk} chunks "
+                         "per GPU"),
     # encode only (HBM roofline of the GF kernel alone).
     "c2enc": dict(d=10, p=4, chunk=1 * MiB, parts=4096, op="encode",
-                  workload="RS(10,4) encode_sep only, 4096 parts x 1 MiB chunks per GPU"),
+                  workload="RS(10,4) encode_sep only, {parts} parts x {chunk} chunks per GPU"),
 }
+
+
+def size_label(nbytes: float) -> str:
+    for unit, k in (("TiB", 1 << 40), ("GiB", 1 << 30), ("MiB", 1 << 20), ("KiB", 1 << 10)):
+        if nbytes >= k:
+            v = nbytes / k
+            return f"{v:g} {unit}" if v == int(v) else f"{v:.3g} {unit}"
+    return f"{int(nbytes)} B"
+
+
+def workload(cfg, args, stream_bytes=None, shards=None) -> str:
+    """The config's workload text with the sizes this run actually used."""
+    text = cfg["workload"].format(parts=cfg["parts"], chunk=size_label(cfg["chunk"]),
+                                  stream=size_label(stream_bytes or 0))
+    if shards:
+        text += f"; one process, {shards} shard(s) over devices {args.devices}"
+    return text
 
 
 # bench kernel name -> rocprofv3 symbol(s); a step of concurrent kernels sums their traffic
 KERNEL_SYMBOL = {"sha256_kernel": "sha256_lane_kernel", "rs_apply_kernel": "rs_apply_kernel",
                  "rs_apply_kernel(reconstruct)": "rs_apply_var_kernel",
+                 "rs_apply_kernel(reconstruct_data)": "rs_apply_var_kernel",
                  "encode_hash_kernel": "encode_hash_kernel",
                  "read_batch(verify+decode)": ("sha256_lane_kernel", "rs_apply_var_kernel")}
 
@@ -137,6 +162,30 @@ def cpu_baseline(cfg, threads: int):
     }
 
 
+def _stream_line(args, cfg, world, n_batches, warm, el, total, extra_config, data_text, **extra):
+    d, p, L, P = cfg["d"], cfg["p"], cfg["chunk"], cfg["parts"]
+    line = {
+        "metric": f"{METRIC} [{args.config}]",
+        "value": round(total / el / 1e9, 2),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": n_batches,
+        "warmup": warm,
+        "ms_per_step": round(el / max(n_batches, 1) * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": data_text,
+        "config": dict({"workload": workload(cfg, args, total, extra_config.pop("shards", None)),
+                        "d": d, "p": p, "chunk_bytes": L, "parts_per_batch": P,
+                        "stream_bytes": total}, **extra_config),
+        "seconds": round(el, 3),
+    }
+    line.update(extra)
+    return line
+
+
 def run_stream(args, cfg, codec, world, rank, device, reduce_dev):
     """C5: host data -> pinned slot -> H2D -> fused encode+hash -> D2H parity + digests.
 
@@ -151,6 +200,8 @@ def run_stream(args, cfg, codec, world, rank, device, reduce_dev):
     lo = total_parts * rank // world
     hi = total_parts * (rank + 1) // world
     mine = hi - lo
+    if args.devices:
+        return run_stream_multi(args, cfg, codec, total_parts)
     pl = ce.Pipeline(codec, L, P, depth)
     rng = np.random.default_rng(rank)
     block = rng.integers(0, 256, size=(P, d, L), dtype=np.uint8)
@@ -180,35 +231,85 @@ def run_stream(args, cfg, codec, world, rank, device, reduce_dev):
     el = max_over_ranks(t1 - t0, world, reduce_dev)
     if rank == 0:
         total = total_parts * part_bytes
-        line = {
-            "metric": f"{METRIC} [c5]",
-            "value": round(total / el / 1e9, 2),
-            "unit": "GB/s",
-            "n_gpus": world,
-            "steps": n_batches,
-            "warmup": min(depth, n_batches),
-            "ms_per_step": round(el / max(n_batches, 1) * 1e3, 3),
-            "higher_is_better": True,
-            "scaling": "strong",
-            "vs_baseline": None,
-            "dtype": "u8",
-            "data": "synthetic host stream (pinned slots filled once, part numbers stamped)",
-            "config": {"workload": cfg["workload"], "d": d, "p": p, "chunk_bytes": L,
-                       "parts_per_batch": P, "slots": depth, "stream_bytes": total,
-                       "parallelism": f"part-range-sharded x{world}, no collective"},
-            "seconds": round(el, 3),
-        }
-        print(json.dumps(line), flush=True)
+        print(json.dumps(_stream_line(
+            args, cfg, world, n_batches, min(depth, n_batches), el, total,
+            {"slots": depth, "parallelism": f"part-range-sharded x{world}, no collective"},
+            "synthetic host stream (pinned slots filled once, part numbers stamped)")), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
+def _segments(args, cfg, shards):
+    """Parts per scheduler job and the jobs of a stream: every shard gets 2 batches per job, and
+    two jobs are in flight (the second queued while the first runs: no drain bubble)."""
+    P = cfg["parts"]
+    return 2 * P * shards
+
+
+def run_stream_multi(args, cfg, codec, total_parts):
+    """C5 through the single-process multi-GPU scheduler (cec_multi: one worker thread per
+    shard, contiguous part ranges, NUMA-local staging): page-locked source segments
+    (cec_host_alloc, filled once, part numbers stamped per job) DMA'd directly, two jobs in
+    flight."""
+    import numpy as np
+    d, p, L, P = cfg["d"], cfg["p"], cfg["chunk"], cfg["parts"]
+    t = d + p
+    devices = args.devices
+    depth = 4
+    m = ce.Multi(codec, L, P, depth, devices)
+    S = _segments(args, cfg, len(devices))
+    rng = np.random.default_rng(0)
+    segs = []
+    for _ in range(2):
+        src = ce.HostBuffer(S * d * L, devices[0])
+        par = ce.HostBuffer(S * p * L, devices[0])
+        dig = ce.HostBuffer(S * t * 32, devices[0])
+        sv = src.view(S, d, L)
+        for k in range(0, S, 64):  # fill once (64-part slabs keep the generator's memory small)
+            sv[k:k + 64] = rng.integers(0, 256, size=sv[k:k + 64].shape, dtype=np.uint8)
+        segs.append((src, par, dig))
+    n_jobs = (total_parts + S - 1) // S
+
+    def submit(i, first):
+        src, par, dig = segs[i % 2]
+        n = min(S, total_parts - first)
+        src.view(S, d, L)[:n, 0, :8] = np.arange(first, first + n, dtype=np.uint64).view(
+            np.uint8).reshape(n, 8)
+        return m.encode_hash(src, n, par, dig), n
+
+    for i in range(2):  # warmup: two jobs (pipelines, device buffers, first pinning)
+        m.wait(submit(i, 0)[0])
+    t0 = time.perf_counter()
+    jobs, first = [], 0
+    for i in range(n_jobs):
+        if len(jobs) == 2:
+            m.wait(jobs.pop(0))
+        job, n = submit(i, first)
+        jobs.append(job)
+        first += n
+    for job in jobs:
+        m.wait(job)
+    el = time.perf_counter() - t0
+    total = total_parts * d * L
+    per_shard = [m.shard_info(g) for g in range(len(devices))]
+    print(json.dumps(_stream_line(
+        args, cfg, len(set(devices)), n_jobs, 2, el, total,
+        {"slots": depth, "shards": len(devices), "parts_per_job": S,
+         "parallelism": f"single process, {len(devices)} shard(s) on devices {devices}, contiguous "
+                        "part ranges, no collective"},
+        "synthetic host stream (page-locked cec_host_alloc segments filled once, part numbers "
+        "stamped per job, DMA'd without staging)",
+        shards=[{"device": dv, "numa_node": nn, "parts": pp} for dv, nn, pp in per_shard])),
+        flush=True)
+
+
 def run_read_stream(args, cfg, codec, world, rank, device, reduce_dev):
     """C5 read side: pinned slots -> H2D of the loaded chunks -> SHA-256 verify + speculative
-    reconstruct_data -> D2H of the rebuilt data chunks (cec_read_pipeline, REBUILT_ONLY).  Every part loads d random
-    chunks of its d+p (file_part.rs:97 samples d); the chunks and their metadata digests are
-    filled into the slots once (a GPU-encoded block of parts), the loaded set changes per batch.
-    Time = first submit to last result, max over ranks; value = part data bytes delivered / s."""
+    reconstruct_data -> D2H of the rebuilt data chunks (cec_read_pipeline, REBUILT_ONLY).  Every
+    part loads d random chunks of its d+p (file_part.rs:97 samples d); the chunks and their
+    metadata digests are filled into the slots once (a GPU-encoded block of parts), the loaded
+    set changes per batch.  Time = first submit to last result, max over ranks; value = part
+    data bytes delivered / s."""
     import numpy as np
     d, p, L, P = cfg["d"], cfg["p"], cfg["chunk"], cfg["parts"]
     t = d + p
@@ -227,10 +328,6 @@ def run_read_stream(args, cfg, codec, world, rank, device, reduce_dev):
     torch.cuda.synchronize(device)
     host_blk, host_dig = blk.cpu().numpy(), dig.cpu().numpy()
     del blk, dig
-    # the loaded data chunks are already in the caller's pinned slot: only rebuilt ones come
-    # back (CEC_READ_REBUILT_ONLY); CEC_C5R_COPYALL=1 (A/B) copies all d data chunks back
-    copy_all = os.environ.get("CEC_C5R_COPYALL", "0") == "1"
-    rp = ce.ReadPipeline(codec, L, P, depth, 0 if copy_all else ce.ReadPipeline.REBUILT_ONLY)
     rng = np.random.default_rng(rank)
     masks = []
     mask_mode = os.environ.get("CEC_C5R_MASK", "random")  # dev A/B: "data" = chunks 0..d-1
@@ -239,6 +336,12 @@ def run_read_stream(args, cfg, codec, world, rank, device, reduce_dev):
         for k in range(P):
             m[k, np.arange(d) if mask_mode == "data" else rng.choice(t, d, replace=False)] = 1
         masks.append(m)
+    if args.devices:
+        return run_read_stream_multi(args, cfg, codec, total_parts, host_blk, host_dig, masks)
+    # the loaded data chunks are already in the caller's pinned slot: only rebuilt ones come
+    # back (CEC_READ_REBUILT_ONLY); CEC_C5R_COPYALL=1 (A/B) copies all d data chunks back
+    copy_all = os.environ.get("CEC_C5R_COPYALL", "0") == "1"
+    rp = ce.ReadPipeline(codec, L, P, depth, 0 if copy_all else ce.ReadPipeline.REBUILT_ONLY)
     for i in range(depth):
         slot, chunks, present, expected = rp.acquire()
         chunks[:] = host_blk
@@ -281,31 +384,91 @@ def run_read_stream(args, cfg, codec, world, rank, device, reduce_dev):
         ok = bool(ok)
     if rank == 0:
         total = total_parts * part_bytes
-        line = {
-            "metric": f"{METRIC} [c5r]",
-            "value": round(total / el / 1e9, 2),
-            "unit": "GB/s",
-            "n_gpus": world,
-            "steps": n_batches,
-            "warmup": min(depth, n_batches),
-            "ms_per_step": round(el / max(n_batches, 1) * 1e3, 3),
-            "higher_is_better": True,
-            "scaling": "strong",
-            "vs_baseline": None,
-            "dtype": "u8",
-            "data": "synthetic host stream (GPU-encoded block of parts, d random chunks loaded "
-                    "per part, loaded sets vary per batch)",
-            "config": {"workload": cfg["workload"], "d": d, "p": p, "chunk_bytes": L,
-                       "parts_per_batch": P, "slots": depth, "stream_bytes": total,
-                       "parallelism": f"part-range-sharded x{world}, no collective"},
-            "seconds": round(el, 3),
-            "undecodable_parts": bad,
-        }
+        extra = {"undecodable_parts": bad}
         if ok is not None:
-            line["check_vs_written"] = ok
-        print(json.dumps(line), flush=True)
+            extra["check_vs_written"] = ok
+        print(json.dumps(_stream_line(
+            args, cfg, world, n_batches, min(depth, n_batches), el, total,
+            {"slots": depth, "parallelism": f"part-range-sharded x{world}, no collective"},
+            "synthetic host stream (GPU-encoded block of parts, d random chunks loaded per part, "
+            "loaded sets vary per batch)", **extra)), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def run_read_stream_multi(args, cfg, codec, total_parts, host_blk, host_dig, masks):
+    """C5 read side through the multi-GPU scheduler: page-locked chunk segments (the encoded
+    block tiled, filled once), present masks varying per job, REBUILT_ONLY (loaded data chunks
+    stay where they were read), two jobs in flight."""
+    import ctypes
+
+    import numpy as np
+    d, p, L, P = cfg["d"], cfg["p"], cfg["chunk"], cfg["parts"]
+    t = d + p
+    devices = args.devices
+    depth = 4
+    m = ce.Multi(codec, L, P, depth, devices)
+    S = _segments(args, cfg, len(devices))
+    reps = S // P
+    segs = []
+    for _ in range(2):
+        ch = ce.HostBuffer(S * t * L, devices[0])
+        out = ce.HostBuffer(S * d * L, devices[0])
+        cv = ch.view(S, t, L)
+        for r in range(reps):
+            cv[r * P:(r + 1) * P] = host_blk
+        segs.append(dict(ch=ch, out=out, pres=np.zeros((S, t), np.uint8),
+                         exp=np.ascontiguousarray(np.tile(host_dig, (reps, 1, 1))),
+                         ver=np.zeros((S, t), np.uint8), st=np.zeros(S, np.int32)))
+    n_jobs = (total_parts + S - 1) // S
+    bad = 0
+
+    def submit(i, n):
+        sg = segs[i % 2]
+        for r in range(reps):
+            sg["pres"][r * P:(r + 1) * P] = masks[(i + r) % len(masks)]
+        job, ptrs = m.read(sg["ch"], sg["pres"], sg["exp"], n, sg["out"], sg["ver"], sg["st"],
+                           rebuilt_only=True)
+        return job, n, ptrs
+
+    for i in range(2):
+        j, n, _ = submit(i, S)
+        m.wait(j)
+    t0 = time.perf_counter()
+    jobs, first = [], 0
+    for i in range(n_jobs):
+        if len(jobs) == 2:
+            j, n, _ = jobs.pop(0)
+            m.wait(j)
+            bad += int((segs[(i - 2) % 2]["st"][:n] != 0).sum())
+        n = min(S, total_parts - first)
+        jobs.append(submit(i, n))
+        first += n
+    last = None
+    for q, (j, n, ptrs) in enumerate(jobs):
+        m.wait(j)
+        bad += int((segs[(n_jobs - len(jobs) + q) % 2]["st"][:n] != 0).sum())
+        last = (n, ptrs)
+    el = time.perf_counter() - t0
+    ok = None
+    if args.check and last is not None:
+        n, ptrs = last
+        ok = bad == 0 and all(
+            b"".join(ctypes.string_at(ptrs[k * d + j], L) for j in range(d)) ==
+            host_blk[k % P, :d].tobytes() for k in (0, n // 2, n - 1))
+    total = total_parts * d * L
+    extra = {"undecodable_parts": bad,
+             "shards": [dict(zip(("device", "numa_node", "parts"), m.shard_info(g)))
+                        for g in range(len(devices))]}
+    if ok is not None:
+        extra["check_vs_written"] = bool(ok)
+    print(json.dumps(_stream_line(
+        args, cfg, len(set(devices)), n_jobs, 2, el, total,
+        {"slots": depth, "shards": len(devices), "parts_per_job": S,
+         "parallelism": f"single process, {len(devices)} shard(s) on devices {devices}, contiguous "
+                        "part ranges, no collective"},
+        "synthetic host stream (page-locked segments tiled from a GPU-encoded block, d random "
+        "chunks loaded per part, REBUILT_ONLY)", **extra)), flush=True)
 
 
 def main():
@@ -322,7 +485,12 @@ def main():
     ap.add_argument("--separate", action="store_true",
                     help="encode_hash as two launches (encode kernel, then SHA-256 kernel) "
                          "instead of the fused encode_hash_kernel")
+    ap.add_argument("--devices", default=None,
+                    help="c5/c5r only: run in ONE process through the multi-GPU scheduler "
+                         "(cec_multi), one shard per listed device ordinal, e.g. 0,1,2,3 "
+                         "(repeats allowed: 0,0 = two shards on GPU 0)")
     args = ap.parse_args()
+    args.devices = [int(x) for x in args.devices.split(",")] if args.devices else None
 
     cfg = dict(CONFIGS[args.config])
     if args.parts:
@@ -359,7 +527,23 @@ def main():
     ce.fill_synthetic(batch, t, seed, stream)  # data chunks + (overwritten) parity slots
 
     present = None
-    if cfg["op"] == "reconstruct":
+    if cfg["op"] == "reconstruct_e2":
+        ce.encode_batch(codec, batch, stream)
+        # exactly 2 erasures per part, uniform over the 14 chunks (seeded); rebuilt in place
+        g = torch.Generator().manual_seed(2222 + rank)
+        pres = torch.ones((n_parts, t), dtype=torch.uint8)
+        for i in range(n_parts):
+            pres[i, torch.randperm(t, generator=g)[:2]] = 0
+        present = bytes(pres.flatten().tolist())
+        miss_data = (d - pres[:, :d].sum(1))
+        # reconstruct_data: parts with a missing data chunk read d chunks and write the missing
+        # data ones (parts missing only parity are skipped, as the crate returns early)
+        algo_data = int((miss_data > 0).sum().item()) * d * L + int(miss_data.sum().item()) * L
+        # reconstruct: every part reads d chunks and writes its 2 missing ones
+        algo_full = n_parts * (d + 2) * L
+        # the erased chunks start zeroed, so the first step really rebuilds them
+        buf.mul_(pres.to(device).view(n_parts, t, 1))
+    elif cfg["op"] == "reconstruct":
         ce.encode_batch(codec, batch, stream)
         # 1..4 random erasures per part (seeded); rebuilt in place every step
         g = torch.Generator().manual_seed(1234 + rank)
@@ -409,6 +593,12 @@ def main():
             if evs is not None:
                 evs[0].record(stream)
             ce.encode_batch(codec, batch, stream)
+            if evs is not None:
+                evs[1].record(stream)
+        elif cfg["op"] == "reconstruct_e2":
+            if evs is not None:
+                evs[0].record(stream)
+            ce.reconstruct_batch(codec, batch, present, True, stream)
             if evs is not None:
                 evs[1].record(stream)
         elif cfg["op"] == "read":
@@ -468,6 +658,28 @@ def main():
         kernels["rs_apply_kernel"] = {"ms": round(enc_ms, 4),
                                       "algorithmic_bytes": n_parts * t * L,
                                       "GBs": round(n_parts * t * L / enc_ms / 1e6, 1)}
+    elif cfg["op"] == "reconstruct_e2":
+        ms = avg_ms(0, 1)
+        kernels["rs_apply_kernel(reconstruct_data)"] = {
+            "ms": round(ms, 4), "algorithmic_bytes": algo_data,
+            "GBs": round(algo_data / ms / 1e6, 1)}
+        # reconstruct (data + parity) of the same erasure sets, timed the same way
+        evf = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(args.steps)]
+        ce.reconstruct_batch(codec, batch, present, False, stream)
+        for k in range(args.steps):
+            evf[k][0].record(stream)
+            ce.reconstruct_batch(codec, batch, present, False, stream)
+            evf[k][1].record(stream)
+        torch.cuda.synchronize(device)
+        ms_f = sum(e[0].elapsed_time(e[1]) for e in evf) / args.steps
+        full_gbs = algo_full / (ms_f / 1e3) / 1e9
+        kernels["also_reconstruct"] = {
+            "call": "reconstruct (data + parity, file_part.rs:304), same parts and erasures",
+            "ms": round(ms_f, 4), "algorithmic_bytes": algo_full,
+            "GBs": round(full_gbs, 1),
+            "roofline": {"bound": "hbm", "kernel": "rs_apply_var_kernel",
+                         "achieved": round(full_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(full_gbs / HBM_PEAK_GBS, 4)}}
     elif cfg["op"] == "read":
         # one read_batch call: verify (sha256_lane_kernel, d chunks per part) on the caller's
         # stream, the speculative decode (rs_apply_var_kernel) beside it on a side stream
@@ -483,7 +695,7 @@ def main():
         kernels["rs_apply_kernel(reconstruct)"] = {"ms": round(rec_ms, 4),
                                                    "algorithmic_bytes": algo,
                                                    "GBs": round(algo / rec_ms / 1e6, 1)}
-    dom_name = max(kernels, key=lambda k: kernels[k]["ms"])
+    dom_name = max((k for k in kernels if not k.startswith("also_")), key=lambda k: kernels[k]["ms"])
     dom = kernels[dom_name]
     achieved = dom["algorithmic_bytes"] / (dom["ms"] / 1e3) / 1e9
     traffic = measured_traffic(args.config + ("sep" if cfg["op"] == "encode_hash" and not fused
@@ -549,7 +761,7 @@ def main():
             "dtype": "u8",
             "data": "synthetic (counter-based generator on device; inputs resident in HBM)",
             "config": {
-                "workload": cfg["workload"],
+                "workload": workload(cfg, args),
                 "d": d, "p": p, "chunk_bytes": L, "parts_per_gpu": n_parts,
                 "data_bytes_per_step": total_data,
                 "parallelism": f"part-sharded x{world}, no collective",

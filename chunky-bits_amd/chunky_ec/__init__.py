@@ -107,6 +107,8 @@ _sig("cec_pipeline_submit", [_vp, ctypes.c_size_t, ctypes.c_size_t])
 _sig("cec_pipeline_wait", [_vp, ctypes.c_size_t, ctypes.POINTER(_u8p), ctypes.POINTER(_u8p),
                            _szp])
 _sig("cec_pipeline_drain", [_vp])
+_sig("cec_pipeline_query", [_vp, ctypes.c_size_t])
+_sig("cec_read_pipeline_query", [_vp, ctypes.c_size_t])
 _sig("cec_pipeline_last_error", [], ctypes.c_char_p)
 _sig("cec_read_pipeline_new", [_vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t,
                                ctypes.POINTER(_vp)])
@@ -550,6 +552,8 @@ class Pipeline:
         slot = ctypes.c_size_t(0)
         ptr = _u8p()
         _check(_lib.cec_pipeline_acquire(self._h, ctypes.byref(slot), ctypes.byref(ptr)))
+        if not ptr:  # PIPE_EXTERNAL: no slot buffer, batches come through submit_from
+            return slot.value, None
         n = self.parts * self.d * self.L
         arr = np.ctypeslib.as_array(ptr, shape=(n,)).reshape(self.parts, self.d, self.L)
         return slot.value, arr
@@ -575,6 +579,13 @@ class Pipeline:
         digests = np.ctypeslib.as_array(dig, shape=(max(k * (self.d + self.p) * 32, 1),))[
             : k * (self.d + self.p) * 32].reshape(k, self.d + self.p, 32)
         return parity, digests
+
+    def query(self, slot: int) -> bool:
+        """True when the slot's batch is complete (never blocks)."""
+        r = _lib.cec_pipeline_query(self._h, slot)
+        if r < 0 or r > 1:
+            raise Error(r)
+        return bool(r)
 
     def drain(self) -> None:
         _check(_lib.cec_pipeline_drain(self._h))
@@ -620,7 +631,8 @@ class ReadPipeline:
         _check(_lib.cec_read_pipeline_acquire(self._h, ctypes.byref(slot), ctypes.byref(ch),
                                               ctypes.byref(pr), ctypes.byref(ex)))
         P, t, L = self.parts, self.t, self.L
-        chunks = np.ctypeslib.as_array(ch, shape=(P * t * L,)).reshape(P, t, L)
+        chunks = (np.ctypeslib.as_array(ch, shape=(P * t * L,)).reshape(P, t, L) if ch
+                  else None)  # PIPE_EXTERNAL: chunks come through submit_from
         present = np.ctypeslib.as_array(pr, shape=(P * t,)).reshape(P, t)
         expected = np.ctypeslib.as_array(ex, shape=(P * t * 32,)).reshape(P, t, 32)
         return slot.value, chunks, present, expected
@@ -658,6 +670,13 @@ class ReadPipeline:
     def part_bytes(self, slot: int, n_parts: int, k: int) -> bytes:
         """Part k's d data chunks concatenated (read_with_context's output), via data_chunks."""
         return b"".join(ctypes.string_at(int(a), self.L) for a in self.data_chunks(slot, n_parts)[k])
+
+    def query(self, slot: int) -> bool:
+        """True when the slot's batch is complete (never blocks)."""
+        r = _lib.cec_read_pipeline_query(self._h, slot)
+        if r < 0 or r > 1:
+            raise Error(r)
+        return bool(r)
 
     def drain(self) -> None:
         _check(_lib.cec_read_pipeline_drain(self._h))
@@ -729,6 +748,7 @@ def set_device(device: int) -> None:
 # ---------------------------------------------------------------------------------------------
 
 PIPE_EXTERNAL = 2  # CEC_PIPE_EXTERNAL
+PRESENT_VERIFIED = 2  # CEC_PRESENT_VERIFIED: read-retry flag (loaded, verified by an earlier pass)
 
 
 class MultiError(Error):

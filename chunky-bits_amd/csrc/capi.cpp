@@ -81,7 +81,12 @@ std::deque<PendingUpload> g_pending;
 void reap_pending() {
     std::lock_guard<std::mutex> lk(g_pending_mu);
     for (auto it = g_pending.begin(); it != g_pending.end();) {
-        if (hipEventQuery(it->ev) == hipSuccess) {
+        const hipError_t e = hipEventQuery(it->ev);
+        // A query never leaves its status behind for the next launch check (hipGetLastError).
+        // Any answer but NotReady means the copy is over: done, or its stream was destroyed,
+        // which waits for the stream's work first (a pipeline or pooled side stream freed since).
+        (void)hipGetLastError();
+        if (e != hipErrorNotReady) {
             (void)hipEventDestroy(it->ev);
             it = g_pending.erase(it);
         } else {
@@ -886,7 +891,9 @@ struct PartImpl {
         } else {
             for (const PartReq* r : batch) {
                 uint8_t* dst = dbase + r->slot * t * cs;
-                if (r->in_pinned)  // d rows of L bytes from the caller's data_buf
+                if (r->in_pinned && cs == L)  // the caller's data_buf, straight
+                    HIP_TRY(hipMemcpyAsync(dst, r->data_buf, d * L, hipMemcpyHostToDevice, s));
+                else if (r->in_pinned)  // d rows of L bytes into the padded chunk stride
                     HIP_TRY(hipMemcpy2DAsync(dst, cs, r->data_buf, r->L, r->L, d,
                                              hipMemcpyHostToDevice, s));
                 else
@@ -935,7 +942,9 @@ struct PartImpl {
         } else {
             for (const PartReq* r : batch) {
                 const uint8_t* src = dbase + r->slot * t * cs + d * cs;
-                if (r->out_pinned)  // p rows of L bytes into the caller's parity buffer
+                if (r->out_pinned && cs == L)  // straight into the caller's parity buffer
+                    HIP_TRY(hipMemcpyAsync(r->parity_out, src, p * L, hipMemcpyDeviceToHost, s));
+                else if (r->out_pinned)  // p rows of L bytes out of the padded chunk stride
                     HIP_TRY(hipMemcpy2DAsync(r->parity_out, r->L, src, cs, r->L, p,
                                              hipMemcpyDeviceToHost, s));
                 else

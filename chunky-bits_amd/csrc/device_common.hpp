@@ -12,6 +12,11 @@
 
 namespace cec {
 
+// Drop a status an earlier, non-fatal HIP call left on this host thread (an event query that
+// was not ready, a pointer query on pageable memory), so the hipGetLastError() after the next
+// launch reports that launch only.
+inline void clear_stale_error() { (void)hipGetLastError(); }
+
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }

@@ -423,6 +423,7 @@ hipError_t launch_p(const FusedParams& a, hipStream_t s) {
         hipSuccess;
     if (!attr) return hipErrorInvalidValue;
     const uint32_t grid = (a.n_parts + a.parts_per_wg - 1) / a.parts_per_wg;
+    clear_stale_error();
     hipLaunchKernelGGL((encode_hash_kernel<PMAX, STEP, MODE, DT, SW, ENC3, BE>), dim3(grid),
                        dim3(64 * (SW + 4)), lds, s, a);
     return hipGetLastError();

@@ -13,13 +13,16 @@
 // pipeline of `depth` slots (pipeline.cpp, CEC_PIPE_EXTERNAL), and streams its range batch by
 // batch: caller buffers that are page-locked (cec_host_alloc) are DMA'd directly; pageable ones
 // go through the worker's own NUMA-local pinned staging.  Jobs are queued and run in submission
-// order; a worker keeps its batches in flight across job boundaries and drains only when its
-// queue runs dry, so back-to-back jobs (a streamed object) leave no bubble.
+// order; a worker keeps its batches in flight across job boundaries: with its queue empty it
+// completes batches as their events fire while watching the queue, so the next job of a stream
+// is queued behind the batches still running instead of after a drain (no bubble).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <map>
@@ -94,6 +97,44 @@ struct Staging {
     }
 };
 
+// Host threads per shard for its staging copies (CEC_MULTI_COPY_THREADS, default 4): one
+// thread's memcpy (~10 GB/s) is below the ~55 GB/s a GPU's PCIe link takes.
+size_t copy_threads() {
+    static const size_t n = [] {
+        const char* e = std::getenv("CEC_MULTI_COPY_THREADS");
+        const long v = e ? std::atol(e) : 4;
+        return size_t(std::min<long>(std::max<long>(v, 1), 32));
+    }();
+    return n;
+}
+
+// fn(i) for i in [0, n) split in contiguous ranges over copy_threads() threads (inline when the
+// work is small).
+template <typename Fn>
+void parallel_for(size_t n, size_t bytes, Fn fn) {
+    const size_t w = std::min(copy_threads(), n);
+    if (w <= 1 || bytes < (size_t(16) << 20)) {
+        for (size_t i = 0; i < n; ++i) fn(i);
+        return;
+    }
+    std::vector<std::thread> pool;
+    pool.reserve(w - 1);
+    for (size_t k = 1; k < w; ++k)
+        pool.emplace_back([&, k] {
+            for (size_t i = n * k / w; i < n * (k + 1) / w; ++i) fn(i);
+        });
+    for (size_t i = 0; i < n / w; ++i) fn(i);
+    for (auto& th : pool) th.join();
+}
+
+void parallel_copy(uint8_t* dst, const uint8_t* src, size_t n) {
+    constexpr size_t kGrain = size_t(1) << 20;
+    parallel_for((n + kGrain - 1) / kGrain, n, [&](size_t i) {
+        const size_t off = i * kGrain;
+        std::memcpy(dst + off, src + off, std::min(kGrain, n - off));
+    });
+}
+
 // A batch in flight on one slot of a shard's pipeline.
 struct InFlight {
     Job* job = nullptr;
@@ -123,6 +164,7 @@ struct Shard {
     unsigned rp_flags = 0;
     Kind active = Kind::Write;
     std::vector<InFlight> wslots, rslots;
+    std::deque<size_t> worder, rorder;  // slots in flight, oldest first
     std::vector<Staging> wstage, rstage;
     std::vector<const uint8_t*> ptrs;  // read: data chunk locations of one batch
 };
@@ -179,14 +221,15 @@ struct cec_multi {
     void finish_write(Shard& s, size_t slot) {
         InFlight& f = s.wslots[slot];
         if (!f.job) return;
+        auto wo = std::find(s.worder.begin(), s.worder.end(), slot);
+        if (wo != s.worder.end()) s.worder.erase(wo);
         const uint8_t *par = nullptr, *dig = nullptr;
         size_t got = 0;
         int st = cec_pipeline_wait(s.wp, slot, &par, &dig, &got);
         std::string err = st == CEC_OK ? std::string() : cec_pipeline_last_error();
         Job* job = f.job;
         if (st == CEC_OK) {
-            if (f.staged_out)
-                std::memcpy(job->parity + f.first * p * L, par, f.n * p * L);
+            if (f.staged_out) parallel_copy(job->parity + f.first * p * L, par, f.n * p * L);
             if (!f.direct_dig) std::memcpy(job->digests + f.first * t * 32, dig, f.n * t * 32);
         }
         s.parts.fetch_add(f.n, std::memory_order_relaxed);
@@ -198,6 +241,8 @@ struct cec_multi {
     void finish_read(Shard& s, size_t slot) {
         InFlight& f = s.rslots[slot];
         if (!f.job) return;
+        auto ro = std::find(s.rorder.begin(), s.rorder.end(), slot);
+        if (ro != s.rorder.end()) s.rorder.erase(ro);
         const uint8_t *data = nullptr, *ver = nullptr;
         const int* status = nullptr;
         size_t got = 0;
@@ -211,18 +256,20 @@ struct cec_multi {
         if (st == CEC_OK) {
             std::memcpy(job->verified + f.first * t, ver, f.n * t);
             std::memcpy(job->status + f.first, status, f.n * sizeof(int));
-            for (size_t k = 0; k < f.n; ++k)
+            const bool staged = f.staged_in || f.staged_out;
+            parallel_for(f.n, staged ? f.n * d * L : 0, [&](size_t k) {
                 for (size_t j = 0; j < d; ++j) {
                     const size_t q = (f.first + k) * d + j;
                     const uint8_t* src = s.ptrs[k * d + j];
                     uint8_t* dst = job->out_data + q * L;
-                    if (status[k] == CEC_OK && (f.staged_in || f.staged_out)) {
+                    if (status[k] == CEC_OK && staged) {
                         // staging is reused by the next batch: the bytes move to the caller
                         if (src != dst) std::memcpy(dst, src, L);
                         src = dst;
                     }
                     if (job->data_ptrs) job->data_ptrs[q] = src;
                 }
+            });
         }
         s.parts.fetch_add(f.n, std::memory_order_relaxed);
         const size_t n = f.n;
@@ -241,6 +288,25 @@ struct cec_multi {
     void drain(Shard& s) {
         drain_write(s);
         drain_read(s);
+    }
+    bool in_flight(const Shard& s) const { return !s.worder.empty() || !s.rorder.empty(); }
+
+    // Finish the oldest batch in flight if it is complete; never blocks.  False when it is still
+    // running (or nothing is in flight).
+    bool finish_oldest_if_done(Shard& s) {
+        if (!s.worder.empty()) {
+            const size_t slot = s.worder.front();
+            if (cec_pipeline_query(s.wp, slot) != 1) return false;
+            finish_write(s, slot);
+            return true;
+        }
+        if (!s.rorder.empty()) {
+            const size_t slot = s.rorder.front();
+            if (cec_read_pipeline_query(s.rp, slot) != 1) return false;
+            finish_read(s, slot);
+            return true;
+        }
+        return false;
     }
 
     void run_write(Shard& s, Job* job, size_t lo, size_t hi) {
@@ -279,7 +345,7 @@ struct cec_multi {
                 }
             }
             if (f.staged_in) {
-                std::memcpy(sg.in, src, n * dw);
+                parallel_copy(sg.in, src, n * dw);
                 src = sg.in;
             }
             st = cec_pipeline_submit_from(s.wp, slot, src, n, f.staged_out ? sg.out : par,
@@ -289,6 +355,7 @@ struct cec_multi {
                 return;
             }
             s.wslots[slot] = f;
+            s.worder.push_back(slot);
         }
     }
 
@@ -328,8 +395,12 @@ struct cec_multi {
             if (f.staged_in) {
                 // only the loaded chunks are read by the engine
                 const uint8_t* prs = job->present + first * t;
-                for (size_t i = 0; i < n * t; ++i)
-                    if (prs[i]) std::memcpy(sg.in + i * L, src + i * L, L);
+                const uint8_t* from = src;
+                uint8_t* to = sg.in;
+                parallel_for(n, n * cw, [&](size_t k) {
+                    for (size_t i = k * t; i < (k + 1) * t; ++i)
+                        if (prs[i]) std::memcpy(to + i * L, from + i * L, L);
+                });
                 src = sg.in;
             }
             st = cec_read_pipeline_submit_from(s.rp, slot, src, job->present + first * t,
@@ -340,6 +411,7 @@ struct cec_multi {
                 return;
             }
             s.rslots[slot] = f;
+            s.rorder.push_back(slot);
         }
     }
 
@@ -351,10 +423,17 @@ struct cec_multi {
             Job* job = nullptr;
             {
                 std::unique_lock<std::mutex> lk(mu);
-                if (s.queue.empty() && !stop) {
+                // Nothing queued: complete batches as they finish (polling their events, 100 us
+                // apart) while watching the queue, so a job submitted meanwhile (the next segment
+                // of a stream) is queued behind the batches still running, never behind a drain;
+                // sleep on the queue alone only when nothing is in flight.
+                while (s.queue.empty() && in_flight(s)) {
                     lk.unlock();
-                    drain(s);  // nothing queued: finish what is in flight before sleeping
+                    while (finish_oldest_if_done(s)) {
+                    }
                     lk.lock();
+                    if (!s.queue.empty() || !in_flight(s)) break;
+                    work_cv.wait_for(lk, std::chrono::microseconds(100));
                 }
                 work_cv.wait(lk, [&] { return stop || !s.queue.empty(); });
                 if (s.queue.empty()) break;  // stop requested and nothing left

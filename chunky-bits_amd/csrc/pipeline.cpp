@@ -244,6 +244,16 @@ int cec_pipeline_wait(cec_pipeline* pl, size_t slot, const uint8_t** parity,
     return CEC_OK;
 }
 
+// 1 when the slot's batch is complete (or none is in flight), 0 while it runs; never blocks.
+int cec_pipeline_query(cec_pipeline* pl, size_t slot) {
+    if (!pl || slot >= pl->slots.size()) return CEC_ERR_INVALID_ARGUMENT;
+    Slot& s = pl->slots[slot];
+    if (!s.in_flight) return 1;
+    const hipError_t e = hipEventQuery(s.done);
+    (void)hipGetLastError();
+    return e == hipErrorNotReady ? 0 : 1;
+}
+
 // Wait for every slot.
 int cec_pipeline_drain(cec_pipeline* pl) {
     if (!pl) return CEC_ERR_INVALID_ARGUMENT;
@@ -613,6 +623,15 @@ int cec_read_pipeline_data_chunks(cec_read_pipeline* pl, size_t slot, const uint
     }
     std::copy(s.data_ptrs.begin(), s.data_ptrs.end(), ptrs);
     return CEC_OK;
+}
+
+int cec_read_pipeline_query(cec_read_pipeline* pl, size_t slot) {
+    if (!pl || slot >= pl->slots.size()) return CEC_ERR_INVALID_ARGUMENT;
+    ReadSlot& s = pl->slots[slot];
+    if (!s.in_flight) return 1;
+    const hipError_t e = hipEventQuery(s.done);
+    (void)hipGetLastError();
+    return e == hipErrorNotReady ? 0 : 1;
 }
 
 int cec_read_pipeline_drain(cec_read_pipeline* pl) {

@@ -293,6 +293,7 @@ hipError_t launch_rg(const ApplyParams& a, uint32_t row_base, uint32_t groups, b
         using T = Tune<decltype(k)::value>;
         auto* kern = &rs_apply_kernel<RG, T::kVec, T::kGroup, T::kV, T::kNt>;
         if (!allow_lds(kern, a.lds_reserve)) return hipErrorInvalidValue;
+        clear_stale_error();
         hipLaunchKernelGGL(kern, grid, dim3(kApplyThreads), a.lds_reserve, s, a, tiles, row_base);
         return hipGetLastError();
     });
@@ -337,6 +338,7 @@ hipError_t launch_rs_apply_var(const ApplyParams& a, bool vec16, hipStream_t s) 
         using T = Tune<decltype(k)::value>;
         auto* kern = &rs_apply_var_kernel<T::kVec, T::kGroup, T::kV, T::kNt>;
         if (!allow_lds(kern, a.lds_reserve)) return hipErrorInvalidValue;
+        clear_stale_error();
         hipLaunchKernelGGL(kern, grid, dim3(kApplyThreads), a.lds_reserve, s, a, tiles);
         return hipGetLastError();
     });
@@ -352,6 +354,7 @@ hipError_t launch_fill(const FillParams& a, hipStream_t s) {
     uint32_t gy = uint32_t(std::min<uint64_t>(n_inst, 65535));
     const bool aligned8 = (reinterpret_cast<uintptr_t>(a.base) % 8 == 0) &&
                           (a.part_stride % 8 == 0) && (a.chunk_stride % 8 == 0);
+    clear_stale_error();
     hipLaunchKernelGGL(fill_kernel, dim3(gx, gy), dim3(256), 0, s, a, aligned8);
     return hipGetLastError();
 }

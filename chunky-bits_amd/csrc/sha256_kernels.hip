@@ -378,6 +378,7 @@ hipError_t launch_split4(const ShaParams& a, hipStream_t s) {
     if (!attr_ok) return hipErrorInvalidValue;
     const uint64_t total = uint64_t(a.n_parts) * a.n_chunks;
     dim3 grid(uint32_t((total + kS4Streams - 1) / kS4Streams));
+    clear_stale_error();
     hipLaunchKernelGGL((sha256_split4_kernel<PRIO, MODE>), grid, dim3(512), kS4Lds, s, a);
     return hipGetLastError();
 }
@@ -422,6 +423,7 @@ hipError_t launch_lane(const ShaParams& a, bool vec16, hipStream_t s, bool one_p
     // instead of a second, partly empty pass.
     const size_t lds =
         (!one_per_cu && grid.x > uint32_t(device_cus())) ? kCuReservation2 : kCuReservation;
+    clear_stale_error();
     if (vec16)
         hipLaunchKernelGGL((sha256_lane_kernel<true>), grid, dim3(kLaneThreads), lds, s, a);
     else
@@ -432,6 +434,7 @@ hipError_t launch_lane(const ShaParams& a, bool vec16, hipStream_t s, bool one_p
 hipError_t launch_split(const ShaParams& a, bool vec16, hipStream_t s) {
     const uint64_t total = a.items ? a.n_items : uint64_t(a.n_parts) * a.n_chunks;
     dim3 grid(uint32_t((total + 63) / 64));
+    clear_stale_error();
     if (vec16) hipLaunchKernelGGL((sha256_split_kernel<true, 64>), grid, dim3(128), 0, s, a);
     else hipLaunchKernelGGL((sha256_split_kernel<false, 64>), grid, dim3(128), 0, s, a);
     return hipGetLastError();

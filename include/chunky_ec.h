@@ -275,6 +275,9 @@ int cec_pipeline_submit(cec_pipeline* pipeline, size_t slot, size_t n_parts);
 int cec_pipeline_wait(cec_pipeline* pipeline, size_t slot, const uint8_t** parity,
                       const uint8_t** digests, size_t* n_parts);
 int cec_pipeline_drain(cec_pipeline* pipeline);
+/* 1 when the slot's batch is complete (or none is in flight), 0 while it is running; never
+ * blocks (for callers that multiplex pipelines).  Same for cec_read_pipeline_query. */
+int cec_pipeline_query(cec_pipeline* pipeline, size_t slot);
 const char* cec_pipeline_last_error(void);
 
 /* Host-staged READ pipeline (FileReadBuilder's part loop, reader.rs:40-75, over
@@ -299,6 +302,7 @@ int cec_read_pipeline_submit(cec_read_pipeline* pipeline, size_t slot, size_t n_
 int cec_read_pipeline_wait(cec_read_pipeline* pipeline, size_t slot, const uint8_t** data,
                            const uint8_t** verified, const int** part_status, size_t* n_parts);
 int cec_read_pipeline_drain(cec_read_pipeline* pipeline);
+int cec_read_pipeline_query(cec_read_pipeline* pipeline, size_t slot);
 /* As cec_read_pipeline_new with flags.  CEC_READ_REBUILT_ONLY: submit copies back only the data
  * chunks it rebuilt (RS(10,4) with d random chunks loaded: 2.9 of 10 per part), since the
  * loaded ones are already in the caller's pinned chunk buffer; wait's *data then holds only

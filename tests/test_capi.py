@@ -105,7 +105,7 @@ def test_read_pipeline_argument_checks_precede_device_use():
     a device a valid request reports NoDevice (no host-side fallback pipeline)."""
     import chunky_ec as ce
     rs = ce.ReedSolomon(10, 4)
-    for args in [(1 << 20, 4, 2, 2), (0, 4, 2, 0), (1 << 20, 0, 2, 0), (1 << 20, 4, 0, 0),
+    for args in [(1 << 20, 4, 2, 4), (0, 4, 2, 0), (1 << 20, 0, 2, 0), (1 << 20, 4, 0, 0),
                  (1 << 20, 4, 17, 0)]:
         with pytest.raises(ce.Error) as e:
             ce.ReadPipeline(rs, *args)
@@ -121,3 +121,53 @@ def test_synth_byte_host_mirror_is_deterministic():
     a = [ce.synth_byte(7, k, c, o) for k in range(3) for c in range(3) for o in (0, 1, 7, 8, 1000)]
     b = [ce.synth_byte(7, k, c, o) for k in range(3) for c in range(3) for o in (0, 1, 7, 8, 1000)]
     assert a == b and len(set(a)) > 10
+
+
+def test_write_pipeline_and_multi_argument_checks_precede_device_use():
+    """Shape / flag / device-list checks of cec_pipeline_new_ex and cec_multi_new come before any
+    HIP call; without a device a valid request reports NoDevice (no host-side fallback)."""
+    import chunky_ec as ce
+    rs = ce.ReedSolomon(10, 4)
+    for args in [(1 << 20, 4, 2, 1), (0, 4, 2, 0), (1 << 20, 0, 2, 0), (1 << 20, 4, 17, 0)]:
+        with pytest.raises(ce.Error) as e:
+            ce.Pipeline(rs, *args)
+        assert e.value.code == ce.ERR_INVALID_ARGUMENT, args
+    for devices in ([], list(range(65))):
+        with pytest.raises(ce.Error) as e:
+            ce.Multi(rs, 1 << 20, 4, 2, devices)
+        assert e.value.code == ce.ERR_INVALID_ARGUMENT
+    if ce.device_count() == 0:
+        with pytest.raises(ce.Error) as e:
+            ce.Multi(rs, 1 << 20, 4, 2, [0])
+        assert e.value.code == ce.ERR_NO_DEVICE
+        with pytest.raises(ce.Error) as e:
+            ce.HostBuffer(4096)
+        assert e.value.code == ce.ERR_NO_DEVICE
+
+
+def test_product_library_has_no_attribution_kernels():
+    """The A/B attribution modes (wrong outputs by design) are compiled only into the separate
+    tools/ab build: the product library reports ab_tools=0."""
+    import chunky_ec as ce
+    assert ce.build_info().startswith("chunky_ec gfx950 ab_tools=0")
+
+
+def test_decode_cache_bounded_without_device():
+    """Decode matrices are built on the host before any device use, and the codec keeps at most
+    4096 of them (least recently used evicted)."""
+    import chunky_ec as ce
+    if ce.device_count() != 0:
+        pytest.skip("host-only check (the GPU variant is in test_gpu_multi.py)")
+    rs = ce.ReedSolomon(20, 8)
+    rng = np.random.default_rng(5)
+    seen = set()
+    while len(seen) < 4200:
+        miss = tuple(sorted(rng.choice(28, 4, replace=False).tolist()))
+        if miss in seen:
+            continue
+        seen.add(miss)
+        shards = [None if i in miss else bytearray(b"x") for i in range(28)]
+        with pytest.raises(ce.Error) as e:
+            rs.reconstruct(shards)
+        assert e.value.code == ce.ERR_NO_DEVICE
+    assert rs.cached_patterns() == 4096

@@ -363,10 +363,119 @@ def test_decode_cache_is_bounded_lru():
     rng = np.random.default_rng(3)
     seen = set()
     while len(seen) < 4200:
-        miss = tuple(sorted(rng.choice(d + p, 3, replace=False).tolist()))
+        miss = tuple(sorted(rng.choice(d + p, 4, replace=False).tolist()))
         if miss in seen:
             continue
         seen.add(miss)
         shards = [None if i in miss else bytearray(full[i]) for i in range(d + p)]
         rs.reconstruct(shards)
     assert rs.cached_patterns() == 4096
+
+
+# ----------------------------------------------------------------------------------------------
+# Read retry (file_part.rs:92-107): resubmit just the undecodable parts with more chunks
+# ----------------------------------------------------------------------------------------------
+
+def test_read_retry_with_one_more_chunk_vs_oracle():
+    """Exactly d chunks loaded, one of them corrupt -> TooFewShardsPresent; the caller loads one
+    more chunk for just those parts and resubmits, marking the chunks that verified
+    CEC_PRESENT_VERIFIED (not hashed again): the part then decodes bit-exact."""
+    d, p, L, n = 10, 4, 4096 + 16, 8
+    t = d + p
+    rs = ce.ReedSolomon(d, p)
+    buf = torch.zeros((n, t, L), dtype=torch.uint8, device="cuda:0")
+    batch = ce.PartBatch.from_tensor(buf, L)
+    ce.fill_synthetic(batch, d, 99)
+    dig = torch.zeros((n, t, 32), dtype=torch.uint8, device="cuda:0")
+    ce.encode_hash_batch(rs, batch, dig.data_ptr())
+    torch.cuda.synchronize()
+    ref = buf.cpu().numpy().copy()
+    rng = np.random.default_rng(12)
+    present = np.zeros((n, t), np.uint8)
+    unloaded = {}
+    for k in range(n):
+        loaded = rng.choice(t, d, replace=False)
+        present[k, loaded] = 1
+        unloaded[k] = [i for i in range(t) if not present[k, i]]
+    host = ref.copy()
+    host[present == 0] = 0
+    bad = [1, 4, 6]
+    for k in bad:  # one corrupt loaded chunk: d - 1 verify
+        i = int(np.flatnonzero(present[k])[3])
+        host[k, i, 5] ^= 0x80
+    buf.copy_(torch.from_numpy(host))
+    verified, status = ce.read_batch(rs, batch, present.tobytes(), dig.data_ptr())
+    v = np.frombuffer(verified, np.uint8).reshape(n, t)
+    assert [k for k in range(n) if status[k] != ce.OK] == bad
+    # retry just the failed parts: verified chunks marked 2, one more chunk loaded (1)
+    sub = torch.zeros((len(bad), t, L), dtype=torch.uint8, device="cuda:0")
+    sub_dig = dig[bad].contiguous()
+    pres2 = np.zeros((len(bad), t), np.uint8)
+    sub_host = np.zeros((len(bad), t, L), np.uint8)
+    for q, k in enumerate(bad):
+        for i in range(t):
+            if v[k, i]:
+                pres2[q, i] = ce.PRESENT_VERIFIED
+                sub_host[q, i] = host[k, i]
+        extra = unloaded[k][0]
+        pres2[q, extra] = 1
+        sub_host[q, extra] = ref[k, extra]
+    sub.copy_(torch.from_numpy(sub_host))
+    sub_batch = ce.PartBatch.from_tensor(sub, L)
+    verified2, status2 = ce.read_batch(rs, sub_batch, pres2.tobytes(), sub_dig.data_ptr())
+    torch.cuda.synchronize()
+    assert status2 == [ce.OK] * len(bad)
+    v2 = np.frombuffer(verified2, np.uint8).reshape(len(bad), t)
+    got = sub.cpu().numpy()
+    for q, k in enumerate(bad):
+        assert np.array_equal(v2[q], (pres2[q] != 0).astype(np.uint8))
+        shards = [ref[k, i] if v2[q, i] else None for i in range(t)]
+        st, out = oracle.reconstruct(d, p, shards, data_only=True)
+        assert st == 0
+        for j in range(d):
+            assert np.array_equal(got[q, j], out[j]) and np.array_equal(got[q, j], ref[k, j])
+
+
+def test_multi_read_retry_pass():
+    d, p, L, n = 6, 3, 1024, 12
+    t = d + p
+    rs = ce.ReedSolomon(d, p)
+    m = ce.Multi(rs, L, 3, 2, [0, 0])
+    data = _write_inputs(n, d, L, 31)
+    chunks = np.zeros((n, t, L), np.uint8)
+    expected = np.zeros((n, t, 32), np.uint8)
+    for k in range(n):
+        st, par = oracle.encode_sep(d, p, [data[k, j] for j in range(d)])
+        full = [data[k, j] for j in range(d)] + par
+        for i in range(t):
+            chunks[k, i] = full[i]
+            expected[k, i] = np.frombuffer(hashlib.sha256(full[i].tobytes()).digest(), np.uint8)
+    good = chunks.copy()
+    present = np.zeros((n, t), np.uint8)
+    present[:, :d] = 1  # the data chunks first
+    for k in range(0, n, 3):
+        chunks[k, 2, 0] ^= 1  # corrupt: that part needs one more chunk
+    out = np.zeros((n, d, L), np.uint8)
+    ver = np.zeros((n, t), np.uint8)
+    st = np.zeros(n, np.int32)
+    m.read_sync(chunks, present, expected, n, out, ver, st)
+    failed = [k for k in range(n) if st[k]]
+    assert failed == list(range(0, n, 3))
+    f = len(failed)
+    ch2 = np.zeros((f, t, L), np.uint8)
+    pr2 = np.zeros((f, t), np.uint8)
+    for q, k in enumerate(failed):
+        pr2[q] = np.where(ver[k] != 0, ce.PRESENT_VERIFIED, 0)
+        ch2[q] = np.where(ver[k][:, None] != 0, chunks[k], 0)
+        pr2[q, d] = 1
+        ch2[q, d] = good[k, d]
+    out2 = np.zeros((f, d, L), np.uint8)
+    ver2 = np.zeros((f, t), np.uint8)
+    st2 = np.zeros(f, np.int32)
+    m.read_sync(ch2, pr2, expected[failed].copy(), f, out2, ver2, st2)
+    assert list(st2) == [0] * f
+    for q, k in enumerate(failed):
+        assert np.array_equal(out2[q], data[k])
+    for k in range(n):
+        if k not in failed:
+            assert np.array_equal(out[k], data[k])

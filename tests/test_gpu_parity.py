@@ -431,7 +431,9 @@ def test_reconstruct_batch_too_few_present_launches_nothing():
 # ----------------------------------------------------------------------------------------------
 
 @pytest.mark.slow
-@pytest.mark.parametrize("d,p,L,n_parts", [(10, 4, 1 << 20, 4096), (20, 8, 256 << 10, 2048)])
+@pytest.mark.parametrize("d,p,L,n_parts", [(10, 4, 1 << 20, 4096), (20, 8, 256 << 10, 2048),
+                                           (20, 8, 256 << 10, 4096)])  # C4 bench shape: the
+# two-SHA-wave ENC3 / big-endian-ring build at 256 KiB
 def test_full_size_encode_erase_reconstruct_roundtrip(d, p, L, n_parts):
     """C2 / C4 at full size: encode+hash, sampled parts vs oracle, then erase 1..p chunks per
     part, reconstruct, and re-hash: every digest must match the encode-time digest."""
