@@ -240,8 +240,8 @@ def run_stream(args, cfg, codec, world, rank, device, reduce_dev):
 
 
 def _segments(args, cfg, shards):
-    """Parts per scheduler job and the jobs of a stream: every shard gets 2 batches per job, and
-    two jobs are in flight (the second queued while the first runs: no drain bubble)."""
+    """Parts per scheduler job: every shard gets 2 batches per job; --jobs-in-flight jobs are
+    queued at once (the next ones queued while the first runs: no drain bubble)."""
     P = cfg["parts"]
     return 2 * P * shards
 
@@ -259,8 +259,9 @@ def run_stream_multi(args, cfg, codec, total_parts):
     m = ce.Multi(codec, L, P, depth, devices)
     S = _segments(args, cfg, len(devices))
     rng = np.random.default_rng(0)
+    J = args.jobs_in_flight
     segs = []
-    for _ in range(2):
+    for _ in range(J):
         src = ce.HostBuffer(S * d * L, devices[0])
         par = ce.HostBuffer(S * p * L, devices[0])
         dig = ce.HostBuffer(S * t * 32, devices[0])
@@ -271,18 +272,18 @@ def run_stream_multi(args, cfg, codec, total_parts):
     n_jobs = (total_parts + S - 1) // S
 
     def submit(i, first):
-        src, par, dig = segs[i % 2]
+        src, par, dig = segs[i % J]
         n = min(S, total_parts - first)
         src.view(S, d, L)[:n, 0, :8] = np.arange(first, first + n, dtype=np.uint64).view(
             np.uint8).reshape(n, 8)
         return m.encode_hash(src, n, par, dig), n
 
-    for i in range(2):  # warmup: two jobs (pipelines, device buffers, first pinning)
+    for i in range(J):  # warmup: one job per segment (pipelines, device buffers, first pinning)
         m.wait(submit(i, 0)[0])
     t0 = time.perf_counter()
     jobs, first = [], 0
     for i in range(n_jobs):
-        if len(jobs) == 2:
+        if len(jobs) == J:
             m.wait(jobs.pop(0))
         job, n = submit(i, first)
         jobs.append(job)
@@ -293,8 +294,8 @@ def run_stream_multi(args, cfg, codec, total_parts):
     total = total_parts * d * L
     per_shard = [m.shard_info(g) for g in range(len(devices))]
     print(json.dumps(_stream_line(
-        args, cfg, len(set(devices)), n_jobs, 2, el, total,
-        {"slots": depth, "shards": len(devices), "parts_per_job": S,
+        args, cfg, len(set(devices)), n_jobs, J, el, total,
+        {"slots": depth, "shards": len(devices), "parts_per_job": S, "jobs_in_flight": J,
          "parallelism": f"single process, {len(devices)} shard(s) on devices {devices}, contiguous "
                         "part ranges, no collective"},
         "synthetic host stream (page-locked cec_host_alloc segments filled once, part numbers "
@@ -410,8 +411,9 @@ def run_read_stream_multi(args, cfg, codec, total_parts, host_blk, host_dig, mas
     m = ce.Multi(codec, L, P, depth, devices)
     S = _segments(args, cfg, len(devices))
     reps = S // P
+    J = args.jobs_in_flight
     segs = []
-    for _ in range(2):
+    for _ in range(J):
         ch = ce.HostBuffer(S * t * L, devices[0])
         out = ce.HostBuffer(S * d * L, devices[0])
         cv = ch.view(S, t, L)
@@ -424,30 +426,30 @@ def run_read_stream_multi(args, cfg, codec, total_parts, host_blk, host_dig, mas
     bad = 0
 
     def submit(i, n):
-        sg = segs[i % 2]
+        sg = segs[i % J]
         for r in range(reps):
             sg["pres"][r * P:(r + 1) * P] = masks[(i + r) % len(masks)]
         job, ptrs = m.read(sg["ch"], sg["pres"], sg["exp"], n, sg["out"], sg["ver"], sg["st"],
                            rebuilt_only=True)
         return job, n, ptrs
 
-    for i in range(2):
+    for i in range(J):
         j, n, _ = submit(i, S)
         m.wait(j)
     t0 = time.perf_counter()
     jobs, first = [], 0
     for i in range(n_jobs):
-        if len(jobs) == 2:
+        if len(jobs) == J:
             j, n, _ = jobs.pop(0)
             m.wait(j)
-            bad += int((segs[(i - 2) % 2]["st"][:n] != 0).sum())
+            bad += int((segs[(i - J) % J]["st"][:n] != 0).sum())
         n = min(S, total_parts - first)
         jobs.append(submit(i, n))
         first += n
     last = None
     for q, (j, n, ptrs) in enumerate(jobs):
         m.wait(j)
-        bad += int((segs[(n_jobs - len(jobs) + q) % 2]["st"][:n] != 0).sum())
+        bad += int((segs[(n_jobs - len(jobs) + q) % J]["st"][:n] != 0).sum())
         last = (n, ptrs)
     el = time.perf_counter() - t0
     ok = None
@@ -463,8 +465,8 @@ def run_read_stream_multi(args, cfg, codec, total_parts, host_blk, host_dig, mas
     if ok is not None:
         extra["check_vs_written"] = bool(ok)
     print(json.dumps(_stream_line(
-        args, cfg, len(set(devices)), n_jobs, 2, el, total,
-        {"slots": depth, "shards": len(devices), "parts_per_job": S,
+        args, cfg, len(set(devices)), n_jobs, J, el, total,
+        {"slots": depth, "shards": len(devices), "parts_per_job": S, "jobs_in_flight": J,
          "parallelism": f"single process, {len(devices)} shard(s) on devices {devices}, contiguous "
                         "part ranges, no collective"},
         "synthetic host stream (page-locked segments tiled from a GPU-encoded block, d random "
@@ -489,6 +491,8 @@ def main():
                     help="c5/c5r only: run in ONE process through the multi-GPU scheduler "
                          "(cec_multi), one shard per listed device ordinal, e.g. 0,1,2,3 "
                          "(repeats allowed: 0,0 = two shards on GPU 0)")
+    ap.add_argument("--jobs-in-flight", type=int, default=2,
+                    help="--devices mode: scheduler jobs (segments of the stream) queued at once")
     args = ap.parse_args()
     args.devices = [int(x) for x in args.devices.split(",")] if args.devices else None
 

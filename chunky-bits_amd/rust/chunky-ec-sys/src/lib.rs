@@ -26,8 +26,18 @@ pub mod sys {
         _private: [u8; 0],
     }
 
-    /// cec_read_pipeline_new_ex flag: only rebuilt data chunks come back over PCIe.
+    #[repr(C)]
+    pub struct cec_multi {
+        _private: [u8; 0],
+    }
+
+    pub const CEC_ABI_VERSION: c_int = 1;
+    /// cec_read_pipeline_new_ex / cec_multi_read flag: only rebuilt data chunks come back.
     pub const CEC_READ_REBUILT_ONLY: std::os::raw::c_uint = 1;
+    /// cec_pipeline_new_ex / cec_read_pipeline_new_ex flag: batches come from caller buffers.
+    pub const CEC_PIPE_EXTERNAL: std::os::raw::c_uint = 2;
+    /// Present-flag value of a read retry: loaded and already verified (not hashed again).
+    pub const CEC_PRESENT_VERIFIED: u8 = 2;
 
     #[repr(C)]
     #[derive(Clone, Copy, Debug)]
@@ -208,6 +218,90 @@ pub mod sys {
             ptrs: *mut *const u8,
         ) -> c_int;
         pub fn cec_coalesce_stats(calls: *mut u64, launches: *mut u64);
+        pub fn cec_build_info() -> *const std::os::raw::c_char;
+        pub fn cec_current_device(device: *mut c_int) -> c_int;
+        pub fn cec_set_device(device: c_int) -> c_int;
+        pub fn cec_device_numa_node(device: c_int) -> c_int;
+        pub fn cec_codec_cached_patterns(codec: *const cec_codec) -> usize;
+        pub fn cec_host_alloc(bytes: usize, device: c_int, out: *mut *mut c_void) -> c_int;
+        pub fn cec_host_free(ptr: *mut c_void);
+        pub fn cec_host_is_pinned(ptr: *const c_void, bytes: usize) -> c_int;
+        pub fn cec_host_numa_node(ptr: *const c_void) -> c_int;
+        pub fn cec_pipeline_new_ex(
+            codec: *const cec_codec,
+            chunk_len: usize,
+            parts_per_batch: usize,
+            depth: usize,
+            flags: std::os::raw::c_uint,
+            out: *mut *mut cec_pipeline,
+        ) -> c_int;
+        pub fn cec_pipeline_submit_from(
+            pipeline: *mut cec_pipeline,
+            slot: usize,
+            data: *const u8,
+            n_parts: usize,
+            parity_out: *mut u8,
+            digests_out: *mut u8,
+        ) -> c_int;
+        pub fn cec_pipeline_query(pipeline: *mut cec_pipeline, slot: usize) -> c_int;
+        pub fn cec_read_pipeline_submit_from(
+            pipeline: *mut cec_read_pipeline,
+            slot: usize,
+            chunks: *const u8,
+            present: *const u8,
+            expected: *const u8,
+            n_parts: usize,
+            data_out: *mut u8,
+        ) -> c_int;
+        pub fn cec_read_pipeline_query(pipeline: *mut cec_read_pipeline, slot: usize) -> c_int;
+        pub fn cec_multi_new(
+            codec: *const cec_codec,
+            chunk_len: usize,
+            parts_per_batch: usize,
+            depth: usize,
+            devices: *const c_int,
+            n_devices: usize,
+            out: *mut *mut cec_multi,
+        ) -> c_int;
+        pub fn cec_multi_free(multi: *mut cec_multi);
+        pub fn cec_multi_shards(multi: *const cec_multi) -> usize;
+        pub fn cec_multi_shard_info(
+            multi: *mut cec_multi,
+            g: usize,
+            device: *mut c_int,
+            numa_node: *mut c_int,
+            parts: *mut u64,
+        ) -> c_int;
+        pub fn cec_multi_encode_hash(
+            multi: *mut cec_multi,
+            data: *const u8,
+            n_parts: usize,
+            parity: *mut u8,
+            digests: *mut u8,
+            job: *mut u64,
+        ) -> c_int;
+        pub fn cec_multi_read(
+            multi: *mut cec_multi,
+            chunks: *const u8,
+            present: *const u8,
+            expected: *const u8,
+            n_parts: usize,
+            data: *mut u8,
+            verified: *mut u8,
+            part_status: *mut c_int,
+            data_ptrs: *mut *const u8,
+            flags: std::os::raw::c_uint,
+            job: *mut u64,
+        ) -> c_int;
+        pub fn cec_multi_wait(multi: *mut cec_multi, job: u64) -> c_int;
+        pub fn cec_multi_last_error() -> *const std::os::raw::c_char;
+        pub fn cec_fill_synthetic(
+            batch: *const cec_part_batch,
+            n_chunks: usize,
+            seed: u64,
+            stream: *mut c_void,
+        ) -> c_int;
+        pub fn cec_synth_byte(seed: u64, part: u64, chunk: u64, offset: u64) -> u8;
     }
 }
 
@@ -220,20 +314,49 @@ pub struct EngineError {
     pub message: String,
 }
 
+impl std::fmt::Display for EngineError {
+    fn fmt(&self, f: &mut std::fmt::Formatter<'_>) -> std::fmt::Result {
+        write!(f, "chunky_ec engine error {}: {}", self.code, self.message)
+    }
+}
+
+impl std::error::Error for EngineError {}
+
 /// Error of a call through the boundary: a crate error (codes 1..13) or an engine error.
+/// Every fallible call returns it; nothing in this crate panics on an engine failure (a HIP
+/// out-of-memory inside a tokio part task surfaces as an error of that part).  The reference
+/// side gains one variant per error type it returns:
+/// `FileWriteError::Engine(EngineError)` / `FileReadError::Engine(EngineError)` with
+/// `From<CecError>`, so `?` keeps working at every call site.
 #[derive(Debug)]
 pub enum CecError {
     Erasure(Error),
     Engine(EngineError),
 }
 
-impl From<CecError> for Error {
-    /// For call sites typed `Result<_, reed_solomon_erasure::Error>`; engine errors have no
-    /// crate variant and abort loudly instead of being disguised as one.
-    fn from(e: CecError) -> Error {
-        match e {
-            CecError::Erasure(e) => e,
-            CecError::Engine(e) => panic!("chunky_ec engine error {}: {}", e.code, e.message),
+impl std::fmt::Display for CecError {
+    fn fmt(&self, f: &mut std::fmt::Formatter<'_>) -> std::fmt::Result {
+        match self {
+            CecError::Erasure(e) => write!(f, "{:?}", e),
+            CecError::Engine(e) => e.fmt(f),
+        }
+    }
+}
+
+impl std::error::Error for CecError {}
+
+impl From<Error> for CecError {
+    fn from(e: Error) -> CecError {
+        CecError::Erasure(e)
+    }
+}
+
+impl CecError {
+    /// The crate error, if this is one (engine errors have no crate variant).
+    pub fn erasure(&self) -> Option<Error> {
+        match self {
+            CecError::Erasure(e) => Some(*e),
+            CecError::Engine(_) => None,
         }
     }
 }
@@ -292,7 +415,7 @@ impl Drop for ReedSolomon {
 }
 
 impl ReedSolomon {
-    pub fn new(data_shards: usize, parity_shards: usize) -> Result<ReedSolomon, Error> {
+    pub fn new(data_shards: usize, parity_shards: usize) -> Result<ReedSolomon, CecError> {
         let mut raw = std::ptr::null_mut();
         check(unsafe { sys::cec_codec_new(data_shards, parity_shards, &mut raw) })?;
         Ok(ReedSolomon { raw })
@@ -315,7 +438,7 @@ impl ReedSolomon {
         &self,
         data: &[T],
         parity: &mut [U],
-    ) -> Result<(), Error> {
+    ) -> Result<(), CecError> {
         let dptr: Vec<*const u8> = data.iter().map(|d| d.as_ref().as_ptr()).collect();
         let dlen: Vec<usize> = data.iter().map(|d| d.as_ref().len()).collect();
         let plen: Vec<usize> = parity.iter().map(|p| p.as_ref().len()).collect();
@@ -334,7 +457,11 @@ impl ReedSolomon {
         Ok(())
     }
 
-    fn reconstruct_inner(&self, shards: &mut [Option<Vec<u8>>], data_only: bool) -> Result<(), Error> {
+    fn reconstruct_inner(
+        &self,
+        shards: &mut [Option<Vec<u8>>],
+        data_only: bool,
+    ) -> Result<(), CecError> {
         // The crate allocates missing slots zeroed at the present length; do the same so the
         // engine writes straight into the caller's Vec.
         let len = shards.iter().flatten().map(|s| s.len()).find(|&l| l > 0).unwrap_or(0);
@@ -373,12 +500,12 @@ impl ReedSolomon {
     }
 
     /// `reconstruct(&mut shards)`: rebuilds missing data and parity.
-    pub fn reconstruct(&self, shards: &mut [Option<Vec<u8>>]) -> Result<(), Error> {
+    pub fn reconstruct(&self, shards: &mut [Option<Vec<u8>>]) -> Result<(), CecError> {
         self.reconstruct_inner(shards, false)
     }
 
     /// `reconstruct_data(&mut shards)`: rebuilds missing data only.
-    pub fn reconstruct_data(&self, shards: &mut [Option<Vec<u8>>]) -> Result<(), Error> {
+    pub fn reconstruct_data(&self, shards: &mut [Option<Vec<u8>>]) -> Result<(), CecError> {
         self.reconstruct_inner(shards, true)
     }
 
@@ -387,13 +514,12 @@ impl ReedSolomon {
     }
 }
 
-/// `Sha256::digest(buf)` (sha256.rs:20-26) computed on the GPU.
-pub fn sha256(buf: &[u8]) -> [u8; 32] {
+/// `Sha256::digest(buf)` (sha256.rs:20-26) computed on the GPU.  Fallible where the CPU digest
+/// is not: an engine failure is returned, never panicked on.
+pub fn sha256(buf: &[u8]) -> Result<[u8; 32], CecError> {
     let mut out = [0u8; 32];
-    check(unsafe { sys::cec_sha256(buf.as_ptr(), buf.len(), out.as_mut_ptr()) })
-        .map_err(Error::from)
-        .expect("cec_sha256");
-    out
+    check(unsafe { sys::cec_sha256(buf.as_ptr(), buf.len(), out.as_mut_ptr()) })?;
+    Ok(out)
 }
 
 /// `FilePart::write_with_encoder`'s compute for one part: (chunksize, parity chunks, d+p digests).
@@ -401,7 +527,7 @@ pub fn part_encode(
     codec: &ReedSolomon,
     data_buf: &[u8],
     length: usize,
-) -> Result<(usize, Vec<Vec<u8>>, Vec<[u8; 32]>), Error> {
+) -> Result<(usize, Vec<Vec<u8>>, Vec<[u8; 32]>), CecError> {
     let d = codec.data_shard_count();
     let p = codec.parity_shard_count();
     let l = (length + d - 1) / d;
@@ -549,7 +675,7 @@ pub struct ReadSlotInput<'a> {
 pub struct ReadBatchResult<'a> {
     pub data: &'a [u8],
     pub verified: &'a [u8],
-    pub part_status: Vec<Result<(), Error>>,
+    pub part_status: Vec<Result<(), CecError>>,
 }
 
 impl ReadPipeline {
@@ -606,7 +732,7 @@ impl ReadPipeline {
             verified: unsafe { std::slice::from_raw_parts(ver, n * self.t) },
             part_status: codes
                 .iter()
-                .map(|&c| check(c).map_err(Error::from))
+                .map(|&c| check(c))
                 .collect(),
         })
     }
@@ -657,5 +783,202 @@ impl ReadPipeline {
                     .collect()
             })
             .collect())
+    }
+}
+
+/// Page-locked host memory (`cec_host_alloc`) placed on `device`'s NUMA node: use it for the
+/// part buffers the reference allocates with `vec![0; d * chunk_size]` (writer.rs:172) and the
+/// parity `Vec`s (file_part.rs:158), and the engine DMAs them directly (no staging copy).
+pub struct HostBuffer {
+    ptr: *mut u8,
+    len: usize,
+}
+
+unsafe impl Send for HostBuffer {}
+unsafe impl Sync for HostBuffer {}
+
+impl HostBuffer {
+    /// `len` bytes, zeroed like the reference's `vec![0; n]`; `device` < 0: no NUMA preference.
+    pub fn zeroed(len: usize, device: c_int) -> Result<HostBuffer, CecError> {
+        let mut p: *mut c_void = std::ptr::null_mut();
+        check(unsafe { sys::cec_host_alloc(len.max(1), device, &mut p) })?;
+        unsafe { std::ptr::write_bytes(p as *mut u8, 0, len) };
+        Ok(HostBuffer { ptr: p as *mut u8, len })
+    }
+}
+
+impl Drop for HostBuffer {
+    fn drop(&mut self) {
+        unsafe { sys::cec_host_free(self.ptr as *mut c_void) }
+    }
+}
+
+impl std::ops::Deref for HostBuffer {
+    type Target = [u8];
+    fn deref(&self) -> &[u8] {
+        unsafe { std::slice::from_raw_parts(self.ptr, self.len) }
+    }
+}
+
+impl std::ops::DerefMut for HostBuffer {
+    fn deref_mut(&mut self) -> &mut [u8] {
+        unsafe { std::slice::from_raw_parts_mut(self.ptr, self.len) }
+    }
+}
+
+impl AsRef<[u8]> for HostBuffer {
+    fn as_ref(&self) -> &[u8] {
+        self
+    }
+}
+
+impl AsMut<[u8]> for HostBuffer {
+    fn as_mut(&mut self) -> &mut [u8] {
+        self
+    }
+}
+
+/// Multi-GPU part scheduler (`cec_multi_*`): `FileWriteBuilder::write`'s part loop
+/// (writer.rs:117-255) and `FileReadBuilder`'s (reader.rs:32-74) over several GPUs in one
+/// process.  One worker thread per entry of `devices`; a job of n parts in file order gives
+/// shard g the contiguous range [g*n/G, (g+1)*n/G) and every result lands at its part's own
+/// position.  The blocking forms below submit one job and wait for it; the buffers are the
+/// caller's (page-locked ones, e.g. [`HostBuffer`], are DMA'd directly).
+pub struct Multi {
+    raw: *mut sys::cec_multi,
+    d: usize,
+    t: usize,
+    chunk_len: usize,
+}
+
+fn too_small(what: &str) -> CecError {
+    CecError::Engine(EngineError { code: 101, message: format!("{} buffer too small", what) })
+}
+
+unsafe impl Send for Multi {}
+unsafe impl Sync for Multi {}
+
+impl Drop for Multi {
+    fn drop(&mut self) {
+        unsafe { sys::cec_multi_free(self.raw) }
+    }
+}
+
+fn check_multi(code: c_int) -> Result<(), CecError> {
+    match check(code) {
+        Err(CecError::Engine(mut e)) => {
+            e.message = unsafe { std::ffi::CStr::from_ptr(sys::cec_multi_last_error()) }
+                .to_string_lossy()
+                .into_owned();
+            Err(CecError::Engine(e))
+        },
+        other => other,
+    }
+}
+
+impl Multi {
+    pub fn new(
+        codec: &ReedSolomon,
+        chunk_len: usize,
+        parts_per_batch: usize,
+        depth: usize,
+        devices: &[c_int],
+    ) -> Result<Multi, CecError> {
+        let mut raw = std::ptr::null_mut();
+        check_multi(unsafe {
+            sys::cec_multi_new(
+                codec.raw,
+                chunk_len,
+                parts_per_batch,
+                depth,
+                devices.as_ptr(),
+                devices.len(),
+                &mut raw,
+            )
+        })?;
+        Ok(Multi {
+            raw,
+            d: codec.data_shard_count(),
+            t: codec.total_shard_count(),
+            chunk_len,
+        })
+    }
+
+    /// write_with_encoder's compute for `n_parts` parts: `data` `[n][d][L]` ->
+    /// `parity` `[n][p][L]`, `digests` `[n][d+p][32]` (chunks in order).
+    pub fn encode_hash(
+        &self,
+        data: &[u8],
+        n_parts: usize,
+        parity: &mut [u8],
+        digests: &mut [u8],
+    ) -> Result<(), CecError> {
+        let (d, p, l) = (self.d, self.t - self.d, self.chunk_len);
+        if data.len() < n_parts * d * l {
+            return Err(too_small("data"));
+        }
+        if parity.len() < n_parts * p * l {
+            return Err(too_small("parity"));
+        }
+        if digests.len() < n_parts * self.t * 32 {
+            return Err(too_small("digests"));
+        }
+        let mut job = 0u64;
+        check_multi(unsafe {
+            sys::cec_multi_encode_hash(
+                self.raw,
+                data.as_ptr(),
+                n_parts,
+                parity.as_mut_ptr(),
+                digests.as_mut_ptr(),
+                &mut job,
+            )
+        })?;
+        check_multi(unsafe { sys::cec_multi_wait(self.raw, job) })
+    }
+
+    /// read_with_context's compute for `n_parts` parts: `chunks` `[n][d+p][L]` (loaded chunk
+    /// bytes), `present` `[n][d+p]` (0 not loaded, 1 loaded, `CEC_PRESENT_VERIFIED` already
+    /// verified by an earlier pass), `expected` `[n][d+p][32]` -> `data` `[n][d][L]`,
+    /// `verified` `[n][d+p]`; per part `Ok(())` or `Err(TooFewShardsPresent)` (load more
+    /// chunks and read that part again, file_part.rs:92-107).
+    pub fn read(
+        &self,
+        chunks: &[u8],
+        present: &[u8],
+        expected: &[u8],
+        n_parts: usize,
+        data: &mut [u8],
+        verified: &mut [u8],
+    ) -> Result<Vec<Result<(), CecError>>, CecError> {
+        let (d, t, l) = (self.d, self.t, self.chunk_len);
+        if chunks.len() < n_parts * t * l || data.len() < n_parts * d * l {
+            return Err(too_small("chunk / data"));
+        }
+        if present.len() < n_parts * t || verified.len() < n_parts * t {
+            return Err(too_small("present / verified"));
+        }
+        if expected.len() < n_parts * t * 32 {
+            return Err(too_small("expected"));
+        }
+        let mut status = vec![0 as c_int; n_parts];
+        let mut job = 0u64;
+        check_multi(unsafe {
+            sys::cec_multi_read(
+                self.raw,
+                chunks.as_ptr(),
+                present.as_ptr(),
+                expected.as_ptr(),
+                n_parts,
+                data.as_mut_ptr(),
+                verified.as_mut_ptr(),
+                status.as_mut_ptr(),
+                std::ptr::null_mut(),
+                0,
+                &mut job,
+            )
+        })?;
+        check_multi(unsafe { sys::cec_multi_wait(self.raw, job) })?;
+        Ok(status.into_iter().map(check).collect())
     }
 }

@@ -243,33 +243,74 @@ class ReedSolomon {
 };
 
 namespace detail {
-// Host-staged pipelines pin GiBs of host memory (~0.35 s per GiB to pin), so the most recent one
-// of each kind is kept per thread and reused by every later write/read of the same shape on the
-// same device.  One entry per thread and kind: a new shape (or device) frees the old pipeline
-// before pinning the next, so the pinned total stays bounded by the threads that use it.
-template <typename Pipe>
-struct CachedPipe {
-    std::array<size_t, 6> key{};
-    std::shared_ptr<ReedSolomon> codec;
-    std::shared_ptr<Pipe> pipe;
+// Multi-GPU scheduler calls keep their messages in cec_multi_last_error().
+inline void check_multi(int status) {
+    if (status == CEC_OK) return;
+    if (status >= CEC_TOO_FEW_SHARDS && status <= CEC_INVALID_INDEX)
+        throw ErasureError(static_cast<Error>(status));
+    throw EngineError(status, std::string(cec_status_name(status)) + ": " + cec_multi_last_error());
+}
+
+// Page-locked host buffer (cec_host_alloc, pages on `device`'s NUMA node), grown on demand:
+// the engine DMAs it directly.
+class PinnedBuf {
+   public:
+    PinnedBuf() = default;
+    PinnedBuf(const PinnedBuf&) = delete;
+    PinnedBuf& operator=(const PinnedBuf&) = delete;
+    ~PinnedBuf() { release(); }
+    uint8_t* reserve(size_t n, int device) {
+        if (n > cap_) {
+            release();
+            void* q = nullptr;
+            check(cec_host_alloc(n, device, &q));
+            p_ = static_cast<uint8_t*>(q);
+            cap_ = n;
+        }
+        return p_;
+    }
+    void release() {
+        if (p_) cec_host_free(p_);
+        p_ = nullptr;
+        cap_ = 0;
+    }
+
+   private:
+    uint8_t* p_ = nullptr;
+    size_t cap_ = 0;
 };
 
-template <typename Pipe, typename New, typename Free>
-CachedPipe<Pipe>& cached_pipe(size_t d, size_t p, size_t L, size_t parts, size_t depth, New make,
-                              Free free_fn) {
-    thread_local CachedPipe<Pipe> e;
-    int device = 0;
-    (void)cec_current_device(&device);
-    const std::array<size_t, 6> key{d, p, L, parts, depth, size_t(device)};
-    if (!e.pipe || e.key != key) {
-        e.pipe.reset();  // unpin the old slots first
+inline std::vector<int> devices_or_current(const std::vector<int>& devices) {
+    if (!devices.empty()) return devices;
+    int dev = 0;
+    (void)cec_current_device(&dev);
+    return {dev};
+}
+
+// The batched paths run through the multi-GPU scheduler (cec_multi: one worker thread and
+// pipeline per shard).  Its pipelines and staging pin host memory (~0.35 s per GiB), so the most
+// recent scheduler is kept per thread and reused by every later write/read of the same shape and
+// device list; a new shape frees the old one first, so the pinned total stays bounded.
+struct CachedMulti {
+    std::vector<size_t> key;
+    std::shared_ptr<ReedSolomon> codec;
+    std::shared_ptr<cec_multi> multi;
+};
+
+inline cec_multi* cached_multi(size_t d, size_t p, size_t L, size_t parts, size_t depth,
+                               const std::vector<int>& devices) {
+    thread_local CachedMulti e;
+    std::vector<size_t> key{d, p, L, parts, depth};
+    for (int dv : devices) key.push_back(size_t(dv));
+    if (!e.multi || e.key != key) {
+        e.multi.reset();
         e.codec = std::make_shared<ReedSolomon>(d, p);
-        Pipe* raw = nullptr;
-        make(e.codec->raw(), L, parts, depth, &raw);
-        e.pipe = std::shared_ptr<Pipe>(raw, free_fn);
+        cec_multi* raw = nullptr;
+        check(cec_multi_new(e.codec->raw(), L, parts, depth, devices.data(), devices.size(), &raw));
+        e.multi = std::shared_ptr<cec_multi>(raw, cec_multi_free);
         e.key = key;
     }
-    return e;
+    return e.multi.get();
 }
 }  // namespace detail
 
@@ -514,18 +555,22 @@ struct FileReference {
     std::vector<FilePart> parts;
 
     // FileReference::read: every part's data, truncated to `length` (file_reference.rs:49-56).
-    // parts_per_batch > 0: runs of parts with one chunksize go through the host-staged read
-    // pipeline (cec_read_pipeline_*: verify + rebuild for a whole batch per launch); the same
-    // bytes and the same TooFewShardsPresent failure as the per-part path.
-    Bytes read(const ChunkStore& src, size_t parts_per_batch = 0, size_t depth = 4) const {
-        Bytes out;
-        size_t total = 0;
-        for (const auto& part : parts) total += part.len_bytes();
-        out.reserve(total);
+    // parts_per_batch > 0: runs of parts of one shape go through the multi-GPU scheduler
+    // (cec_multi: a whole window of parts verified + rebuilt per launch, sharded over `devices`,
+    // default the current device) the way the reference reads (file_part.rs:86-122): d chunks
+    // loaded per part, and for a part whose loaded chunks do not all verify, more chunks loaded
+    // and the part resubmitted (CEC_PRESENT_VERIFIED marks the chunks already verified) until d
+    // verify or none are left (TooFewShardsPresent).  Same bytes and the same failure as the
+    // per-part path.
+    Bytes read(const ChunkStore& src, size_t parts_per_batch = 0, size_t depth = 4,
+               const std::vector<int>& devices = {}) const {
+        std::vector<size_t> offset(parts.size() + 1, 0);
+        for (size_t k = 0; k < parts.size(); ++k) offset[k + 1] = offset[k] + parts[k].len_bytes();
+        Bytes out(offset.back());
         size_t k = 0;
         while (k < parts.size()) {
             size_t run = 1;
-            // A run shares one pipeline, so its parts must share the whole shape: the metadata
+            // A run shares one scheduler, so its parts must share the whole shape: the metadata
             // allows a different d/p per part (file_part.rs:77 builds a codec per part).
             while (parts_per_batch && k + run < parts.size() &&
                    parts[k + run].chunksize == parts[k].chunksize &&
@@ -533,10 +578,10 @@ struct FileReference {
                    parts[k + run].parity.size() == parts[k].parity.size())
                 ++run;
             if (run < 2) {
-                Bytes b = parts[k].read_with_context(src);
-                out.insert(out.end(), b.begin(), b.end());
+                const Bytes b = parts[k].read_with_context(src);
+                std::memcpy(out.data() + offset[k], b.data(), b.size());
             } else {
-                read_run(src, k, run, parts_per_batch, depth, out);
+                read_run(src, k, run, parts_per_batch, depth, devices, out.data() + offset[k]);
             }
             k += run;
         }
@@ -555,60 +600,142 @@ struct FileReference {
     }
 
    private:
+    // One window of a run in flight: its parts, loaded chunk buffers and results.
+    struct ReadWindow {
+        size_t first = 0, n = 0;
+        uint64_t job = 0;
+        bool live = false;
+        detail::PinnedBuf chunks;  // [W][t][L] loaded chunk bytes (DMA'd directly)
+        std::vector<uint8_t> present, expected, verified;
+        std::vector<int> status;
+    };
+
+    // Parts [k0, k0 + n) (one shape) through cec_multi, two windows in flight; their bytes land
+    // at dst (part k0 + q at dst + q*d*L).
     void read_run(const ChunkStore& src, size_t k0, size_t n, size_t ppb, size_t depth,
-                  Bytes& out) const {
+                  const std::vector<int>& devices, uint8_t* dst) const {
         const FilePart& first = parts[k0];
         const size_t d = first.data.size(), t = d + first.parity.size(), L = first.chunksize;
-        auto& cached = detail::cached_pipe<cec_read_pipeline>(
-            d, t - d, L, ppb, depth,
-            [](const cec_codec* c, size_t l, size_t parts, size_t dep, cec_read_pipeline** out) {
-                detail::check_pipe(
-                    cec_read_pipeline_new_ex(c, l, parts, dep, CEC_READ_REBUILT_ONLY, out));
-            },
-            cec_read_pipeline_free);
-        cec_read_pipeline* rp = cached.pipe.get();
-        const size_t nd = cec_read_pipeline_depth(rp);
-        std::vector<std::pair<size_t, size_t>> pending(nd, {0, 0});  // slot -> (first, count)
-        std::vector<const uint8_t*> where;
-        // Called right after acquire(slot), before its chunk buffer is refilled: the loaded data
-        // chunks are read from there (only the rebuilt ones came back from the GPU).
-        auto collect = [&](size_t slot) {
-            const uint8_t *data = nullptr, *ver = nullptr;
-            const int* status = nullptr;
-            size_t got = 0;
-            detail::check(cec_read_pipeline_wait(rp, slot, &data, &ver, &status, &got));
-            for (size_t i = 0; i < got; ++i) detail::check(status[i]);
-            where.resize(got * d);
-            detail::check(cec_read_pipeline_data_chunks(rp, slot, where.data()));
-            for (const uint8_t* c : where) out.insert(out.end(), c, c + L);
-        };
-        size_t done = 0, submitted = 0;
-        const size_t per = ppb;
-        while (done < n) {
-            size_t slot = 0;
-            uint8_t *chunks = nullptr, *present = nullptr, *expected = nullptr;
-            detail::check(cec_read_pipeline_acquire(rp, &slot, &chunks, &present, &expected));
-            if (pending[slot].second) {  // this slot's previous batch: in order, oldest first
-                collect(slot);
-                done += pending[slot].second;
-                pending[slot] = {0, 0};
-            }
-            if (submitted == n) continue;
-            const size_t b = std::min(per, n - submitted);
-            // the loads (store lookups + copies into the pinned slot) run on copy_threads()
-            detail::parallel_for(b, [&](size_t q) {
-                const FilePart& part = parts[k0 + submitted + q];
+        const std::vector<int> devs = detail::devices_or_current(devices);
+        cec_multi* m = detail::cached_multi(d, t - d, L, ppb, depth, devs);
+        const size_t W = ppb * depth * devs.size();
+        thread_local ReadWindow win[2];
+        auto submit = [&](ReadWindow& w, size_t at, size_t cnt) {
+            uint8_t* ch = w.chunks.reserve(W * t * L, devs[0]);
+            w.present.assign(cnt * t, 0);
+            w.expected.resize(cnt * t * 32);
+            w.verified.assign(cnt * t, 0);
+            w.status.assign(cnt, 0);
+            // The reference loads d chunks per part (file_part.rs:86-107): the first d stored
+            // ones here (data chunks first: no rebuild when they are all there).
+            detail::parallel_for(cnt, [&](size_t q) {
+                const FilePart& part = parts[k0 + at + q];
+                size_t loaded = 0;
                 for (size_t i = 0; i < t; ++i) {
+                    std::memcpy(&w.expected[(q * t + i) * 32], part.chunk(i).hash.digest().data(), 32);
+                    if (loaded == d) continue;
                     const Bytes* bytes = src.find(part.chunk(i).hash);
-                    const bool ok = bytes && bytes->size() == L;
-                    present[q * t + i] = ok ? 1 : 0;
-                    if (ok) std::memcpy(chunks + (q * t + i) * L, bytes->data(), L);
-                    std::memcpy(expected + (q * t + i) * 32, part.chunk(i).hash.digest().data(), 32);
+                    if (!bytes || bytes->size() != L) continue;
+                    std::memcpy(ch + (q * t + i) * L, bytes->data(), L);
+                    w.present[q * t + i] = 1;
+                    ++loaded;
                 }
             });
-            detail::check(cec_read_pipeline_submit(rp, slot, b));
-            pending[slot] = {submitted, b};
-            submitted += b;
+            detail::check_multi(cec_multi_read(m, ch, w.present.data(), w.expected.data(), cnt,
+                                               dst + at * d * L, w.verified.data(),
+                                               w.status.data(), nullptr, 0, &w.job));
+            w.first = at;
+            w.n = cnt;
+            w.live = true;
+        };
+        auto collect = [&](ReadWindow& w) {
+            w.live = false;
+            detail::check_multi(cec_multi_wait(m, w.job));
+            std::vector<size_t> failed;
+            for (size_t q = 0; q < w.n; ++q)
+                if (w.status[q] != CEC_OK) failed.push_back(q);
+            if (!failed.empty()) retry(src, m, k0, d, t, L, w, failed, dst);
+        };
+        try {
+            size_t at = 0;
+            int cur = 0;
+            while (at < n || win[0].live || win[1].live) {
+                ReadWindow& w = win[cur];
+                if (w.live) collect(w);
+                if (at < n) {
+                    const size_t cnt = std::min(W, n - at);
+                    submit(w, at, cnt);
+                    at += cnt;
+                }
+                cur ^= 1;
+            }
+        } catch (...) {
+            for (auto& w : win)  // no job may still write into dst / the window buffers
+                if (w.live) {
+                    (void)cec_multi_wait(m, w.job);
+                    w.live = false;
+                }
+            throw;
+        }
+    }
+
+    // file_part.rs:92-107: a loaded chunk whose hash fails is dropped and another one is read.
+    // The failed parts of a window are resubmitted with the chunks that verified (marked
+    // CEC_PRESENT_VERIFIED: not hashed again) plus as many untried stored chunks as are missing,
+    // until they decode or no chunk is left (TooFewShardsPresent, as the reference's read).
+    void retry(const ChunkStore& src, cec_multi* m, size_t k0, size_t d, size_t t, size_t L,
+               const ReadWindow& w, const std::vector<size_t>& failed, uint8_t* dst) const {
+        const size_t f = failed.size();
+        std::vector<uint8_t> tried(f * t), good(f * t);
+        for (size_t r = 0; r < f; ++r)
+            for (size_t i = 0; i < t; ++i) {
+                tried[r * t + i] = w.present[failed[r] * t + i] != 0;
+                good[r * t + i] = w.verified[failed[r] * t + i] != 0;
+            }
+        Bytes chunks(f * t * L), data(f * d * L);
+        std::vector<uint8_t> present(f * t), expected(f * t * 32), verified(f * t);
+        std::vector<int> status(f);
+        std::vector<size_t> open(f);
+        for (size_t r = 0; r < f; ++r) open[r] = r;
+        while (!open.empty()) {
+            // build the resubmission of the still-open parts
+            std::vector<size_t> next_open;
+            const size_t g = open.size();
+            std::fill(present.begin(), present.begin() + g * t, uint8_t(0));
+            for (size_t q = 0; q < g; ++q) {
+                const size_t r = open[q];
+                const FilePart& part = parts[k0 + w.first + failed[r]];
+                size_t have = 0, added = 0;
+                for (size_t i = 0; i < t; ++i) have += good[r * t + i];
+                for (size_t i = 0; i < t; ++i) {
+                    std::memcpy(&expected[(q * t + i) * 32], part.chunk(i).hash.digest().data(), 32);
+                    const Bytes* bytes = src.find(part.chunk(i).hash);
+                    if (good[r * t + i]) {
+                        std::memcpy(&chunks[(q * t + i) * L], bytes->data(), L);
+                        present[q * t + i] = CEC_PRESENT_VERIFIED;
+                    } else if (!tried[r * t + i] && have + added < d && bytes && bytes->size() == L) {
+                        std::memcpy(&chunks[(q * t + i) * L], bytes->data(), L);
+                        present[q * t + i] = 1;
+                        tried[r * t + i] = 1;
+                        ++added;
+                    }
+                }
+                if (added == 0) throw ErasureError(Error::TooFewShardsPresent);
+            }
+            uint64_t job = 0;
+            detail::check_multi(cec_multi_read(m, chunks.data(), present.data(), expected.data(), g,
+                                               data.data(), verified.data(), status.data(),
+                                               nullptr, 0, &job));
+            detail::check_multi(cec_multi_wait(m, job));
+            for (size_t q = 0; q < g; ++q) {
+                const size_t r = open[q];
+                for (size_t i = 0; i < t; ++i) good[r * t + i] = verified[q * t + i] != 0;
+                if (status[q] == CEC_OK)
+                    std::memcpy(dst + (w.first + failed[r]) * d * L, &data[q * d * L], d * L);
+                else
+                    next_open.push_back(r);
+            }
+            open.swap(next_open);
         }
     }
 };
@@ -631,11 +758,16 @@ class FileWriteBuilder {
         return *this;
     }
 
-    // Parts per host-staged batch (cec_pipeline_*) and batches in flight; 0 = one
-    // write_with_encoder call per part (the reference's shape).
+    // Parts per batch and batches in flight per device for the batched path (the multi-GPU
+    // scheduler, cec_multi); 0 = one write_with_encoder call per part (the reference's shape).
     FileWriteBuilder& batch(size_t parts_per_batch, size_t depth = 4) {
         batch_ = parts_per_batch;
         depth_ = depth;
+        return *this;
+    }
+    // Devices the batched path shards over (one shard per entry; default: the current device).
+    FileWriteBuilder& devices(std::vector<int> devs) {
+        devices_ = std::move(devs);
         return *this;
     }
 
@@ -666,57 +798,72 @@ class FileWriteBuilder {
     size_t parity_ = 2;
     size_t batch_ = 0;
     size_t depth_ = 4;
+    std::vector<int> devices_;
 
-    // The write pipeline over `full` parts of d*chunk_size bytes: same FileParts and stored
-    // chunks as write_with_encoder part by part.
+    // The `full` parts of d*chunk_size bytes through the multi-GPU scheduler, in windows of
+    // batch * depth * shards parts with two windows in flight: same FileParts and stored chunks as
+    // write_with_encoder part by part.  The input bytes are already [part][d][L] (a full part is
+    // d*chunk_size contiguous bytes), so each window is one job straight from them; parity and
+    // digests come back into page-locked buffers.
     void write_full_parts(const ReedSolomon& encoder, const uint8_t* bytes, size_t full,
                           ChunkStore& dest, FileReference& file) const {
         (void)encoder;
-        const size_t d = data_, p = parity_, t = d + p, L = chunk_size_, per = batch_;
-        auto& cached = detail::cached_pipe<cec_pipeline>(
-            d, p, L, batch_, depth_,
-            [](const cec_codec* c, size_t l, size_t parts, size_t dep, cec_pipeline** out) {
-                detail::check_pipe(cec_pipeline_new(c, l, parts, dep, out));
-            },
-            cec_pipeline_free);
-        cec_pipeline* pl = cached.pipe.get();
-        std::vector<std::pair<size_t, size_t>> pending(cec_pipeline_depth(pl), {0, 0});
-        auto collect = [&](size_t slot) {
-            const uint8_t *parity = nullptr, *digests = nullptr;
-            size_t got = 0;
-            detail::check_pipe(cec_pipeline_wait(pl, slot, &parity, &digests, &got));
-            const size_t first = pending[slot].first;
-            for (size_t k = 0; k < got; ++k) {
+        const size_t d = data_, p = parity_, t = d + p, L = chunk_size_;
+        const std::vector<int> devs = detail::devices_or_current(devices_);
+        cec_multi* m = detail::cached_multi(d, p, L, batch_, depth_, devs);
+        const size_t W = batch_ * depth_ * devs.size();
+        struct Window {
+            size_t first = 0, n = 0;
+            uint64_t job = 0;
+            bool live = false;
+            detail::PinnedBuf parity, digests;
+        };
+        thread_local Window win[2];
+        auto collect = [&](Window& w) {
+            w.live = false;
+            detail::check_multi(cec_multi_wait(m, w.job));
+            const uint8_t* par = w.parity.reserve(W * p * L, devs[0]);
+            const uint8_t* dig = w.digests.reserve(W * t * 32, devs[0]);
+            for (size_t k = 0; k < w.n; ++k) {
                 FilePart part;
                 part.chunksize = L;
                 for (size_t i = 0; i < t; ++i) {
                     std::array<uint8_t, 32> h{};
-                    std::memcpy(h.data(), digests + (k * t + i) * 32, 32);
+                    std::memcpy(h.data(), dig + (k * t + i) * 32, 32);
                     const Chunk c{Sha256Hash(h)};
-                    const uint8_t* src = i < d ? bytes + ((first + k) * d + i) * L
-                                               : parity + (k * p + (i - d)) * L;
+                    const uint8_t* src = i < d ? bytes + ((w.first + k) * d + i) * L
+                                               : par + (k * p + (i - d)) * L;
                     dest.write_shard(c.hash, src, L);
                     (i < d ? part.data : part.parity).push_back(c);
                 }
                 file.parts.push_back(std::move(part));
             }
         };
-        size_t submitted = 0, done = 0;
-        while (done < full) {
-            size_t slot = 0;
-            uint8_t* data = nullptr;
-            detail::check_pipe(cec_pipeline_acquire(pl, &slot, &data));
-            if (pending[slot].second) {  // oldest batch first: parts stay in file order
-                collect(slot);
-                done += pending[slot].second;
-                pending[slot] = {0, 0};
+        try {
+            size_t at = 0;
+            int cur = 0;
+            while (at < full || win[0].live || win[1].live) {
+                Window& w = win[cur];
+                if (w.live) collect(w);  // oldest window first: parts stay in file order
+                if (at < full) {
+                    const size_t cnt = std::min(W, full - at);
+                    detail::check_multi(cec_multi_encode_hash(
+                        m, bytes + at * d * L, cnt, w.parity.reserve(W * p * L, devs[0]),
+                        w.digests.reserve(W * t * 32, devs[0]), &w.job));
+                    w.first = at;
+                    w.n = cnt;
+                    w.live = true;
+                    at += cnt;
+                }
+                cur ^= 1;
             }
-            if (submitted == full) continue;
-            const size_t b = std::min(per, full - submitted);
-            detail::parallel_copy(data, bytes + submitted * d * L, b * d * L);
-            detail::check_pipe(cec_pipeline_submit(pl, slot, b));
-            pending[slot] = {submitted, b};
-            submitted += b;
+        } catch (...) {
+            for (auto& w : win)  // no job may still write into the window buffers
+                if (w.live) {
+                    (void)cec_multi_wait(m, w.job);
+                    w.live = false;
+                }
+            throw;
         }
     }
 };

@@ -234,6 +234,62 @@ void test_batched_paths() {
     }
 }
 
+// The batched paths sharded over several devices in one process (cec_multi): two shards on the
+// first GPU (and one per GPU when more are visible), identical parts, chunks and bytes; a read
+// whose d loaded chunks include a corrupted one is retried with another chunk (file_part.rs:92-107).
+void test_multi_device_paths() {
+    int n_dev = cec_device_count();
+    std::vector<std::vector<int>> lists = {{0, 0}};
+    if (n_dev > 1) {
+        std::vector<int> all;
+        for (int i = 0; i < n_dev; ++i) all.push_back(i);
+        lists.push_back(all);
+    }
+    const size_t d = 10, p = 4, chunk = size_t(1) << 14, n_parts = 29;
+    const size_t length = d * chunk * (n_parts - 1) + 777;
+    const Bytes input = random_bytes(length, 4242);
+    ChunkStore per_part;
+    const auto b = FileWriteBuilder().chunk_size(chunk).data_chunks(d).parity_chunks(p);
+    const FileReference a = b.write(input, per_part);
+    for (const auto& devs : lists) {
+        ChunkStore store;
+        const FileReference c = FileWriteBuilder(b).batch(3, 2).devices(devs).write(input, store);
+        CHECK(c.parts.size() == n_parts);
+        for (size_t k = 0; k < n_parts; ++k)
+            for (size_t i = 0; i < d + p; ++i) CHECK(a.parts[k].chunk(i).hash == c.parts[k].chunk(i).hash);
+        CHECK(c.read(store, 3, 2, devs) == input);
+        // data chunk 0 corrupted in every other part: the d-chunk first pass fails its hash,
+        // the retry loads the next stored chunk
+        for (size_t k = 0; k < n_parts; k += 2) CHECK(store.corrupt(c.parts[k].data[0].hash, 9));
+        CHECK(c.read(store, 3, 2, devs) == input);
+        // and a part whose usable chunks run out
+        for (size_t i = 1; i < d + p - (d - 2); ++i) store.erase(c.parts[7].chunk(i).hash);
+        CHECK(throws_erasure([&] { c.read(store, 3, 2, devs); }, Error::TooFewShardsPresent));
+    }
+}
+
+// A FileReference whose parts have different shapes (the metadata allows a d/p per part;
+// file_part.rs:77 builds a codec per part): batched reads group only parts of one shape.
+void test_mixed_shape_read() {
+    const size_t chunk = 2048;
+    const Bytes in1 = random_bytes(3 * chunk * 4, 11), in2 = random_bytes(5 * chunk * 3 + 17, 12);
+    ChunkStore store;
+    const FileReference f1 = FileWriteBuilder().chunk_size(chunk).data_chunks(3).parity_chunks(2).write(in1, store);
+    const FileReference f2 = FileWriteBuilder().chunk_size(chunk).data_chunks(5).parity_chunks(3).write(in2, store);
+    FileReference mixed;
+    mixed.parts = f1.parts;
+    mixed.parts.insert(mixed.parts.end(), f2.parts.begin(), f2.parts.end());
+    // f2's last part is short (chunksize < chunk): its bytes are that part's d*chunksize
+    Bytes expect = in1;
+    for (const auto& part : f2.parts) {
+        const Bytes b = part.read_with_context(store);
+        expect.insert(expect.end(), b.begin(), b.end());
+    }
+    mixed.length = expect.size();
+    CHECK(mixed.read(store, 2, 2) == expect);
+    CHECK(mixed.read(store) == expect);
+}
+
 // JavaReedSolomon testOneEncode / reed-solomon-erasure test_encoding (RS(5,5)).
 void test_one_encode() {
     const ReedSolomon rs(5, 5);
@@ -336,6 +392,8 @@ const Test kTests[] = {
     {"test_cluster_digests", test_cluster_digests},
     {"test_cp_50mib", test_cp_50mib},
     {"test_batched_paths", test_batched_paths},
+    {"test_multi_device_paths", test_multi_device_paths},
+    {"test_mixed_shape_read", test_mixed_shape_read},
     {"test_one_encode", test_one_encode},
     {"test_matrix_rows", test_matrix_rows},
     {"test_errors", test_errors},

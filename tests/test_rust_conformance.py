@@ -1,0 +1,135 @@
+"""The Rust FFI crate (chunky-bits_amd/rust/chunky-ec-sys) against the C header it binds.
+
+There is no cargo in this image, so the crate is never compiled here; this is the check that is
+possible: the `extern "C"` block of src/lib.rs and include/chunky_ec.h must declare the same
+functions, with the same arity, and every parameter / return type must match in kind (pointer
+depth and constness, integer width and signedness); the `cec_part_batch` layout and the ABI
+constants must agree too.
+"""
+import os
+import re
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "chunky_ec.h")
+RUST = os.path.join(ROOT, "chunky-bits_amd", "rust", "chunky-ec-sys", "src", "lib.rs")
+
+# C base type -> canonical name shared with Rust
+C_BASE = {"size_t": "usize", "int": "c_int", "unsigned": "c_uint", "unsigned int": "c_uint",
+          "uint64_t": "u64", "uint8_t": "u8", "char": "c_char", "void": "c_void",
+          "cec_codec": "cec_codec", "cec_pipeline": "cec_pipeline",
+          "cec_read_pipeline": "cec_read_pipeline", "cec_multi": "cec_multi",
+          "cec_part_batch": "cec_part_batch"}
+
+
+def _strip_c_comments(src):
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return re.sub(r"//[^\n]*", "", src)
+
+
+def c_type(decl: str, has_name: bool = True):
+    """Canonical type of a C declarator like 'const uint8_t* const* data'."""
+    toks = re.findall(r"[A-Za-z_][A-Za-z_0-9]*|\*", decl)
+    type_words = {w for k in C_BASE for w in k.split()} | {"const"}
+    if has_name and toks and toks[-1] != "*" and toks[-1] not in type_words:
+        toks = toks[:-1]  # the parameter name
+    base_words, consts, stars = [], [False], 0
+    cur_const = False
+    for tk in toks:
+        if tk == "const":
+            cur_const = True
+        elif tk == "*":
+            consts[-1] = consts[-1] or cur_const
+            consts.append(False)
+            cur_const = False
+            stars += 1
+        else:
+            base_words.append(tk)
+    consts[-1] = consts[-1] or cur_const
+    base = C_BASE[" ".join(base_words)]
+    # consts[0]: const of the base; consts[i]: const of pointer level i (the pointee of i+1)
+    t = base
+    pointee_const = consts[0]
+    for level in range(stars):
+        t = ("ptr", pointee_const, t)
+        pointee_const = consts[level + 1]
+    return t
+
+
+def rust_type(s: str):
+    s = s.strip()
+    m = re.match(r"\*(const|mut)\s+(.*)$", s)
+    if m:
+        return ("ptr", m.group(1) == "const", rust_type(m.group(2)))
+    return s.split("::")[-1].strip()
+
+
+def header_functions():
+    src = _strip_c_comments(open(HEADER).read())
+    out = {}
+    for m in re.finditer(r"([A-Za-z_][A-Za-z_0-9 \*]*?)\b(cec_[a-z0-9_]+)\s*\(([^;{]*?)\)\s*;", src):
+        ret, name, params = m.group(1).strip(), m.group(2), m.group(3).strip()
+        if name.startswith("cec_") and ret.startswith("typedef"):
+            continue
+        ps = [] if params in ("", "void") else [p.strip() for p in params.split(",")]
+        out[name] = (c_type(ret, has_name=False), [c_type(p) for p in ps])
+    return out
+
+
+def rust_functions():
+    src = open(RUST).read()
+    block = re.search(r'extern "C"\s*\{(.*?)\n    \}', src, flags=re.S).group(1)
+    block = re.sub(r"//[^\n]*", "", block)
+    out = {}
+    for m in re.finditer(r"pub fn (cec_[a-z0-9_]+)\s*\((.*?)\)\s*(->\s*([^;]+))?;", block,
+                         flags=re.S):
+        name, params, ret = m.group(1), m.group(2), m.group(4)
+        ps = [p.strip() for p in params.split(",") if p.strip()]
+        types = [rust_type(p.split(":", 1)[1]) for p in ps]
+        out[name] = (rust_type(ret) if ret else "c_void", types)
+    return out
+
+
+def test_rust_declares_every_header_function_with_matching_types():
+    h, r = header_functions(), rust_functions()
+    assert len(h) > 60
+    assert sorted(h) == sorted(r), (sorted(set(h) - set(r)), sorted(set(r) - set(h)))
+    for name in h:
+        hret, hps = h[name]
+        rret, rps = r[name]
+        assert len(hps) == len(rps), name
+        assert hret == rret, (name, hret, rret)
+        for i, (a, b) in enumerate(zip(hps, rps)):
+            assert a == b, (name, i, a, b)
+
+
+def test_part_batch_layout_and_constants_match():
+    hsrc = _strip_c_comments(open(HEADER).read())
+    rsrc = open(RUST).read()
+    cfields = re.search(r"typedef struct cec_part_batch \{(.*?)\}", hsrc, flags=re.S).group(1)
+    cf = [(c_type(f.strip()), f.strip().split()[-1].lstrip("*")) for f in cfields.split(";")
+          if f.strip()]
+    rfields = re.search(r"pub struct cec_part_batch \{(.*?)\}", rsrc, flags=re.S).group(1)
+    rf = [(rust_type(f.split(":", 1)[1]), f.split(":", 1)[0].replace("pub", "").strip())
+          for f in rfields.split(",") if ":" in f]
+    assert [(t, n) for t, n in cf] == [(t, n) for t, n in rf]
+    for const in ("CEC_ABI_VERSION", "CEC_READ_REBUILT_ONLY", "CEC_PIPE_EXTERNAL",
+                  "CEC_PRESENT_VERIFIED"):
+        cv = re.search(rf"#define {const}\s+(\d+)u?", hsrc).group(1)
+        rv = re.search(rf"pub const {const}:[^=]+=\s*(\d+);", rsrc).group(1)
+        assert cv == rv, const
+
+
+def test_status_codes_match_the_crate_mapping():
+    """check() in lib.rs maps 1..13 onto reed_solomon_erasure::Error in the header's order."""
+    hsrc = _strip_c_comments(open(HEADER).read())
+    rsrc = open(RUST).read()
+    names = dict((int(v), k) for k, v in re.findall(r"CEC_([A-Z_]+)\s*=\s*(\d+)", hsrc))
+    for code, variant in re.findall(r"(\d+) => Error::(\w+),", rsrc):
+        camel = "".join(w.capitalize() for w in names[int(code)].split("_"))
+        assert camel == variant, (code, camel, variant)
+
+
+def test_no_panics_on_engine_errors():
+    src = open(RUST).read()
+    code = re.sub(r"//[^\n]*", "", src)
+    assert "panic!" not in code and ".expect(" not in code and ".unwrap()" not in code
