@@ -28,13 +28,21 @@ def short(name: str) -> str:
     return name[:40]
 
 
+LAUNCHES = None  # (a, b): per kernel, only its launches a..b-1 in dispatch order (--launches a:b)
+
+
 def pmc(path):
     out = collections.defaultdict(lambda: collections.defaultdict(list))
     dur = collections.defaultdict(list)
     if not os.path.exists(path):
         return out, dur
+    seen = collections.Counter()
     for r in csv.DictReader(open(path)):
         k = short(r["Kernel_Name"])
+        i = seen[(k, r["Counter_Name"])]
+        seen[(k, r["Counter_Name"])] += 1
+        if LAUNCHES and k in ("rs_apply_var_kernel",) and not LAUNCHES[0] <= i < LAUNCHES[1]:
+            continue
         out[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
         dur[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
     return out, dur
@@ -45,11 +53,17 @@ def mean(v):
 
 
 def main():
+    global LAUNCHES
     tag = sys.argv[1]
+    if "--launches" in sys.argv:  # c3e2: the reconstruct_data launches come first
+        a, b = sys.argv[sys.argv.index("--launches") + 1].split(":")
+        LAUNCHES = (int(a), int(b))
     config = sys.argv[sys.argv.index("--config") + 1] if "--config" in sys.argv else "c2"
     # FETCH_SIZE multiplier: 2 for 16 B/lane streaming reads (the guide's gfx950 calibration);
-    # 1 for 8 B/lane reads (the RS(20,p) fused build), whose 64-B requests FETCH_SIZE counts in
-    # full: r1f_c4 reports 20 895 570 KiB = 0.996 x the 21.47 GB of data the kernel reads once.
+    # 1 for the RS(20,p) fused build's 8 B/lane reads, whose two 64-B halves of a line are read
+    # one ~5 us step apart: calibrated independently by tools/ubench_fetch.hip's wide8_steps
+    # kernel, which reads a known 21.47 GB in that exact pattern and pacing and gets FETCH_SIZE =
+    # 1.000 x the bytes (profiles/r2_fetch_calibration.log; unpaced the halves merge: 1.78).
     fmult = float(sys.argv[sys.argv.index("--fetch-mult") + 1]) if "--fetch-mult" in sys.argv \
         else 2.0
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
@@ -65,7 +79,11 @@ def main():
     for r in stats:
         lines.append(f"| {short(r['Name'])} | {r['Calls']} | {float(r['AverageNs'])/1e6:.3f} | "
                      f"{float(r['MinNs'])/1e6:.3f} | {float(r['MaxNs'])/1e6:.3f} |")
-    lines += ["", "## Counters (separate `--pmc` passes; per-launch means)", "",
+    lines += ["", "## Counters (separate `--pmc` passes; per-launch means)", ""]
+    if LAUNCHES:
+        lines += [f"rs_apply_var_kernel: launches {LAUNCHES[0]}..{LAUNCHES[1] - 1} only (the "
+                  "reconstruct_data steps; the reconstruct launches timed beside them follow).", ""]
+    lines += [
               "| kernel | clock GHz (GRBM_GUI_ACTIVE/8/dur) | SQ_WAVES | VALU insts/wave | "
               f"FETCH_SIZE KiB | WRITE_SIZE KiB | HBM traffic GB ({fmult:g}xFETCH+WRITE) |",
               "|---|---|---|---|---|---|---|"]
