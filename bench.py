@@ -506,6 +506,9 @@ def main():
     ordinal = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(ordinal)
     device = torch.device("cuda", ordinal)
+    # host threads and the pinned slots of this rank on its GPU's NUMA node (the engine places
+    # its own pinned buffers there anyway; this keeps the host copies local too)
+    numa_bound = ce.bind_thread_to_device_node(ordinal)
     # RCCL ("nccl") carries only the barrier and the max-over-ranks all-reduce.
     # CEC_BENCH_BACKEND=gloo rehearses N > 1 with several ranks on one GPU.
     backend = os.environ.get("CEC_BENCH_BACKEND", "nccl")
@@ -769,6 +772,7 @@ def main():
                 "d": d, "p": p, "chunk_bytes": L, "parts_per_gpu": n_parts,
                 "data_bytes_per_step": total_data,
                 "parallelism": f"part-sharded x{world}, no collective",
+                "host_threads_numa_bound": numa_bound,
             },
             "roofline": {
                 "bound": "hbm",

@@ -132,6 +132,7 @@ _sig("cec_host_alloc", [ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(_vp)])
 _sig("cec_host_free", [_vp], None)
 _sig("cec_host_is_pinned", [_vp, ctypes.c_size_t])
 _sig("cec_host_numa_node", [_vp])
+_sig("cec_bind_thread_to_device_node", [ctypes.c_int])
 _sig("cec_pipeline_new_ex", [_vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_uint,
                              ctypes.POINTER(_vp)])
 _sig("cec_pipeline_submit_from", [_vp, ctypes.c_size_t, _vp, ctypes.c_size_t, _vp, _vp])
@@ -731,6 +732,11 @@ def host_numa_node(buf) -> int:
 
 def device_numa_node(device: int) -> int:
     return _lib.cec_device_numa_node(device)
+
+
+def bind_thread_to_device_node(device: int) -> bool:
+    """Restrict the calling thread to the CPUs of the device's NUMA node (False if impossible)."""
+    return bool(_lib.cec_bind_thread_to_device_node(device))
 
 
 def current_device() -> int:

@@ -131,6 +131,20 @@ bool bind_thread_to_device_node(int device) {
     return sched_setaffinity(0, sizeof(want), &want) == 0;
 }
 
+hipError_t host_malloc_near(void** out, size_t bytes, unsigned flags, int device) {
+    // Pages land on the device's NUMA node: prefer that node for this thread while HIP pins them
+    // (hipHostMallocNumaUser: HIP follows the thread's policy), then restore the default.
+    const int node = device >= 0 ? device_numa_node(device) : -1;
+    bool policy = false;
+    if (node >= 0 && node < 64) {
+        const unsigned long mask = 1ul << node;
+        policy = set_mempolicy_raw(kMpolPreferred, &mask, 64) == 0;
+    }
+    const hipError_t e = hipHostMalloc(out, bytes, flags | (policy ? hipHostMallocNumaUser : 0u));
+    if (policy) (void)set_mempolicy_raw(kMpolDefault, nullptr, 0);
+    return e;
+}
+
 }  // namespace cec
 
 using namespace cec;
@@ -169,18 +183,8 @@ int cec_host_alloc(size_t bytes, int device, void** out) {
         return CEC_ERR_NO_DEVICE;
     }
     if (device >= n) return CEC_ERR_INVALID_ARGUMENT;
-    // Pages land on the device's NUMA node: prefer that node for this thread while HIP pins them
-    // (hipHostMallocNumaUser: HIP follows the thread's policy), then restore the default.
-    const int node = device >= 0 ? device_numa_node(device) : -1;
-    bool policy = false;
-    if (node >= 0 && node < 64) {
-        const unsigned long mask = 1ul << node;
-        policy = set_mempolicy_raw(kMpolPreferred, &mask, 64) == 0;
-    }
     void* p = nullptr;
-    const unsigned flags = hipHostMallocPortable | (policy ? hipHostMallocNumaUser : 0u);
-    hipError_t e = hipHostMalloc(&p, bytes, flags);
-    if (policy) (void)set_mempolicy_raw(kMpolDefault, nullptr, 0);
+    const hipError_t e = host_malloc_near(&p, bytes, hipHostMallocPortable, device);
     if (e != hipSuccess) {
         (void)hipGetLastError();
         return e == hipErrorOutOfMemory ? CEC_ERR_OUT_OF_MEMORY : CEC_ERR_HIP;
@@ -203,6 +207,8 @@ void cec_host_free(void* p) {
 }
 
 int cec_host_is_pinned(const void* p, size_t bytes) { return pinned_range(p, bytes) ? 1 : 0; }
+
+int cec_bind_thread_to_device_node(int device) { return bind_thread_to_device_node(device) ? 1 : 0; }
 
 int cec_host_numa_node(const void* p) {
     // move_pages(2) in query mode (nodes == NULL) reports the node of each page.

@@ -2,6 +2,8 @@
 // per-call coalescer and the multi-GPU scheduler (hostmem.cpp).
 #pragma once
 
+#include <hip/hip_runtime.h>
+
 #include <cstddef>
 #include <cstdint>
 
@@ -17,5 +19,10 @@ int device_numa_node(int device);
 // Restrict the calling thread to the CPUs of `device`'s NUMA node (intersected with the CPUs it
 // may use now).  Returns false (and leaves the affinity alone) when that is not possible.
 bool bind_thread_to_device_node(int device);
+
+// hipHostMalloc(bytes, flags) with the pages preferred on `device`'s NUMA node (device < 0 or
+// node unknown: the default placement).  Used for every pinned buffer the engine allocates
+// itself (pipeline slots, scheduler staging) and by cec_host_alloc.
+hipError_t host_malloc_near(void** out, size_t bytes, unsigned flags, int device);
 
 }  // namespace cec

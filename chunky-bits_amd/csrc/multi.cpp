@@ -75,13 +75,14 @@ struct Staging {
         in = out = nullptr;
         in_cap = out_cap = 0;
     }
-    hipError_t reserve(size_t in_bytes, size_t out_bytes) {
+    hipError_t reserve(size_t in_bytes, size_t out_bytes, int device) {
         hipError_t e = hipSuccess;
         if (in_cap < in_bytes) {
             if (in) (void)hipHostFree(in);
             in = nullptr;
             in_cap = 0;
-            e = hipHostMalloc(reinterpret_cast<void**>(&in), in_bytes, hipHostMallocDefault);
+            e = cec::host_malloc_near(reinterpret_cast<void**>(&in), in_bytes,
+                                      hipHostMallocDefault, device);
             if (e != hipSuccess) return e;
             in_cap = in_bytes;
         }
@@ -89,7 +90,8 @@ struct Staging {
             if (out) (void)hipHostFree(out);
             out = nullptr;
             out_cap = 0;
-            e = hipHostMalloc(reinterpret_cast<void**>(&out), out_bytes, hipHostMallocDefault);
+            e = cec::host_malloc_near(reinterpret_cast<void**>(&out), out_bytes,
+                                      hipHostMallocDefault, device);
             if (e != hipSuccess) return e;
             out_cap = out_bytes;
         }
@@ -337,7 +339,8 @@ struct cec_multi {
             f.direct_dig = cec::pinned_range(dig, n * t * 32);
             Staging& sg = s.wstage[slot];
             if (f.staged_in || f.staged_out) {
-                hipError_t e = sg.reserve(f.staged_in ? P * dw : 0, f.staged_out ? P * pw : 0);
+                hipError_t e = sg.reserve(f.staged_in ? P * dw : 0, f.staged_out ? P * pw : 0,
+                                          s.device);
                 if (e != hipSuccess) {
                     finish_parts(job, hi - first, CEC_ERR_OUT_OF_MEMORY,
                                  std::string("multi staging: ") + hipGetErrorString(e));
@@ -385,7 +388,8 @@ struct cec_multi {
             f.staged_out = !cec::pinned_range(dst, n * dw);
             Staging& sg = s.rstage[slot];
             if (f.staged_in || f.staged_out) {
-                hipError_t e = sg.reserve(f.staged_in ? P * cw : 0, f.staged_out ? P * dw : 0);
+                hipError_t e = sg.reserve(f.staged_in ? P * cw : 0, f.staged_out ? P * dw : 0,
+                                          s.device);
                 if (e != hipSuccess) {
                     finish_parts(job, hi - first, CEC_ERR_OUT_OF_MEMORY,
                                  std::string("multi staging: ") + hipGetErrorString(e));

@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "chunky_ec.h"
+#include "hostmem.hpp"
 
 namespace {
 
@@ -166,9 +167,10 @@ int cec_pipeline_new_ex(const cec_codec* codec, size_t chunk_len, size_t parts_p
     pl->slots.resize(depth);
     for (Slot& s : pl->slots) {
         hipError_t e = hipSuccess;
-        auto host = [&](uint8_t** ptr, size_t bytes) {
+        auto host = [&](uint8_t** ptr, size_t bytes) {  // pinned, on the device's NUMA node
             if (e == hipSuccess)
-                e = hipHostMalloc(reinterpret_cast<void**>(ptr), bytes, hipHostMallocDefault);
+                e = cec::host_malloc_near(reinterpret_cast<void**>(ptr), bytes,
+                                          hipHostMallocDefault, pl->device);
         };
         if (!pl->external) {
             host(&s.h_data, pl->parts * pl->d * pl->L);
@@ -475,8 +477,10 @@ int cec_read_pipeline_new_ex(const cec_codec* codec, size_t chunk_len, size_t pa
     const size_t P = pl->parts, t = pl->t;
     for (ReadSlot& s : pl->slots) {
         hipError_t e = hipSuccess;
-        auto host = [&](uint8_t** ptr, size_t bytes) {
-            if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(ptr), bytes, hipHostMallocDefault);
+        auto host = [&](uint8_t** ptr, size_t bytes) {  // pinned, on the device's NUMA node
+            if (e == hipSuccess)
+                e = cec::host_malloc_near(reinterpret_cast<void**>(ptr), bytes,
+                                          hipHostMallocDefault, pl->device);
         };
         auto dev = [&](uint8_t** ptr, size_t bytes) {
             if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(ptr), bytes);

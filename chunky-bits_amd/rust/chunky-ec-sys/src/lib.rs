@@ -227,6 +227,7 @@ pub mod sys {
         pub fn cec_host_free(ptr: *mut c_void);
         pub fn cec_host_is_pinned(ptr: *const c_void, bytes: usize) -> c_int;
         pub fn cec_host_numa_node(ptr: *const c_void) -> c_int;
+        pub fn cec_bind_thread_to_device_node(device: c_int) -> c_int;
         pub fn cec_pipeline_new_ex(
             codec: *const cec_codec,
             chunk_len: usize,

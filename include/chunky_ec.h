@@ -130,6 +130,11 @@ void cec_host_free(void* ptr);
 int cec_host_is_pinned(const void* ptr, size_t bytes);
 /* NUMA node holding the page at ptr (-1 when unknown). */
 int cec_host_numa_node(const void* ptr);
+/* Restrict the calling thread to the CPUs of `device`'s NUMA node (∩ the CPUs it may use);
+ * 1 if done, 0 if not possible (node unknown, or outside this process's cpuset).  The pinned
+ * buffers the engine allocates itself (pipeline slots, scheduler staging) are placed on that
+ * node whatever the caller's affinity. */
+int cec_bind_thread_to_device_node(int device);
 
 /* ---------------------------------------------------------------------------------------- */
 /* Host-buffer API: one call per part, staged through the GPU (drop-in for the crate calls) */

@@ -171,3 +171,12 @@ def test_decode_cache_bounded_without_device():
             rs.reconstruct(shards)
         assert e.value.code == ce.ERR_NO_DEVICE
     assert rs.cached_patterns() == 4096
+
+
+def test_part_encode_rejects_length_past_data_buf():
+    """file_part.rs:150 asserts length <= data_buf.len(): the binding refuses before reading
+    past the buffer (no device needed)."""
+    import chunky_ec as ce
+    rs = ce.ReedSolomon(3, 2)
+    with pytest.raises(ValueError):
+        ce.part_encode(rs, b"abcdef", 7)
