@@ -1,11 +1,14 @@
 // End-to-end `cp` through the C++ host layer (dev tool): FileWriteBuilder::write of an in-memory
 // file into a ChunkStore (RAM stand-in for the locations), then FileReference::read back after
 // losing one data + one parity chunk per part — per-part calls (the reference's shape) vs the
-// host-staged pipelines (FileWriteBuilder::batch / read(src, parts_per_batch)).
-//   make -C chunky-bits_amd/csrc cp_bench ; tools/cp_bench [GiB]
+// batched paths (FileWriteBuilder::batch / read(src, parts_per_batch) through the multi-GPU
+// scheduler, sharded over `devices`: default the current GPU; e.g. 0,0 = two shards on GPU 0).
+//   make -C chunky-bits_amd/csrc cp_bench ; tools/cp_bench [GiB] [devices]
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <sstream>
+#include <string>
 
 #include "chunky_ec.hpp"
 
@@ -13,6 +16,12 @@ using namespace chunky_ec;
 
 int main(int argc, char** argv) {
     const double gib = argc > 1 ? std::atof(argv[1]) : 4.0;
+    std::vector<int> devices;
+    if (argc > 2) {
+        std::stringstream ss(argv[2]);
+        std::string tok;
+        while (std::getline(ss, tok, ',')) devices.push_back(std::atoi(tok.c_str()));
+    }
     const size_t d = 10, p = 4, chunk = size_t(1) << 20;
     const size_t length = size_t(gib * double(size_t(1) << 30)) / (d * chunk) * (d * chunk) + 4321;
     Bytes input(length);
@@ -32,7 +41,8 @@ int main(int argc, char** argv) {
     for (int batched = 1; batched >= 0; --batched) {
         const size_t n = batched ? length : std::min(length, size_t(64) * d * chunk);
         auto write = [&](ChunkStore& store) {
-            return batched ? FileWriteBuilder(builder).batch(256, 4).write(input.data(), n, store)
+            return batched ? FileWriteBuilder(builder).batch(128, 4).devices(devices).write(
+                                 input.data(), n, store)
                            : builder.write(input.data(), n, store);
         };
         // write path alone (shards discarded, as if written to /dev/null); the first write
@@ -51,15 +61,16 @@ int main(int argc, char** argv) {
             store.erase(part.data[3].hash);
             store.erase(part.parity[1].hash);
         }
-        if (batched) (void)f.read(store, 256, 4);  // pins the read pipeline
+        if (batched) (void)f.read(store, 128, 4, devices);  // pins the read windows
         t0 = std::chrono::steady_clock::now();
-        const Bytes back = batched ? f.read(store, 256, 4) : f.read(store);
+        const Bytes back = batched ? f.read(store, 128, 4, devices) : f.read(store);
         const double r = secs(t0);
         const bool ok = back.size() == n && std::memcmp(back.data(), input.data(), n) == 0;
-        std::printf("%-9s %6.2f GiB, %zu parts: write %6.2f GB/s (%6.2f GB/s into the RAM store), "
-                    "read with 2 holes/part %6.2f GB/s, bit-exact %s\n",
+        std::printf("%-9s %6.2f GiB, %zu parts, %zu shard(s): write %6.2f GB/s (%6.2f GB/s into "
+                    "the RAM store), read with 2 holes/part %6.2f GB/s, bit-exact %s\n",
                     batched ? "batched" : "per-part", double(n) / double(size_t(1) << 30),
-                    f.parts.size(), double(n) / w / 1e9, double(n) / w_ram / 1e9,
+                    f.parts.size(), batched ? std::max<size_t>(devices.size(), 1) : size_t(0),
+                    double(n) / w / 1e9, double(n) / w_ram / 1e9,
                     double(n) / r / 1e9, ok ? "yes" : "NO");
         std::fflush(stdout);
         if (!ok) return 1;
