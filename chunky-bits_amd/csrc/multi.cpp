@@ -475,7 +475,11 @@ struct cec_multi {
         Job* raw = job.get();
         jobs.emplace(raw->id, std::move(job));
         if (raw->n == 0) return CEC_OK;
-        for (auto& s : shards) s->queue.push_back(raw);
+        // Only shards with a non-empty range get the job: once the others have finished, the
+        // caller may free it, and a shard popping it later would read freed memory.
+        const size_t G = shards.size();
+        for (size_t g = 0; g < G; ++g)
+            if (raw->n * (g + 1) / G > raw->n * g / G) shards[g]->queue.push_back(raw);
         work_cv.notify_all();
         return CEC_OK;
     }

@@ -479,3 +479,37 @@ def test_multi_read_retry_pass():
     for k in range(n):
         if k not in failed:
             assert np.array_equal(out[k], data[k])
+
+
+def test_multi_many_tiny_jobs_fewer_parts_than_shards():
+    """Jobs smaller than the shard count leave some shards without a range: those never see the
+    job, so a caller may free it as soon as it completes (no shard touches it afterwards)."""
+    d, p, L = 4, 2, 512
+    rs = ce.ReedSolomon(d, p)
+    m = ce.Multi(rs, L, 2, 2, [0, 0, 0, 0])
+    for it in range(150):
+        n = 1 + it % 3
+        src = _write_inputs(n, d, L, 40_000 + it)
+        par = np.zeros((n, p, L), np.uint8)
+        dig = np.zeros((n, d + p, 32), np.uint8)
+        m.encode_hash_sync(src.copy(), n, par, dig)
+        if it % 25 == 0:
+            _check_write(src, par, dig, d, p)
+    with pytest.raises(ce.Error):
+        m.wait(123456789)  # unknown job
+
+
+def test_multi_freed_with_jobs_in_flight_finishes_them():
+    """Destroying the scheduler with jobs still queued completes them first (their buffers are
+    the caller's until then)."""
+    d, p, L, n = 10, 4, 4096, 12
+    rs = ce.ReedSolomon(d, p)
+    src = _write_inputs(n, d, L, 77)
+    par = np.zeros((n, p, L), np.uint8)
+    dig = np.zeros((n, d + p, 32), np.uint8)
+    m = ce.Multi(rs, L, 2, 2, [0, 0])
+    m.encode_hash(src.copy(), n, par, dig)
+    del m
+    import gc
+    gc.collect()
+    _check_write(src, par, dig, d, p)
