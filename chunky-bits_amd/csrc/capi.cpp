@@ -69,46 +69,38 @@ bool aligned16(const void* p, size_t a, size_t b) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Host buffers that must outlive an asynchronous upload: released once their event fires.
+// Host words that must outlive an asynchronous upload.  The copy from pageable memory may read
+// the words after hipMemcpyAsync returns, so they are released by a host function queued right
+// behind the copy on the same stream: it runs once the stream has passed the copy, whatever
+// happens to other streams or events.  (Round 2's first version polled an event per upload and
+// treated any answer but NotReady as done; an event recorded on a stream that was destroyed
+// meanwhile answers an error, and treating that as done freed words still being copied — a
+// GPU memory fault in the read path's decode.)
 // ------------------------------------------------------------------------------------------
-struct PendingUpload {
-    hipEvent_t ev;
-    std::vector<uint32_t> words;
-};
-std::mutex g_pending_mu;
-std::deque<PendingUpload> g_pending;
-
-void reap_pending() {
-    std::lock_guard<std::mutex> lk(g_pending_mu);
-    for (auto it = g_pending.begin(); it != g_pending.end();) {
-        const hipError_t e = hipEventQuery(it->ev);
-        // A query never leaves its status behind for the next launch check (hipGetLastError).
-        // Any answer but NotReady means the copy is over: done, or its stream was destroyed,
-        // which waits for the stream's work first (a pipeline or pooled side stream freed since).
-        (void)hipGetLastError();
-        if (e != hipErrorNotReady) {
-            (void)hipEventDestroy(it->ev);
-            it = g_pending.erase(it);
-        } else {
-            ++it;
-        }
-    }
-}
+void release_words(void* p) { delete static_cast<std::vector<uint32_t>*>(p); }
 
 // Upload `words` to a stream-ordered device allocation; the allocation is released (stream
 // ordered) by free_upload after the consumer launches.
 int upload_words(std::vector<uint32_t>&& words, hipStream_t s, uint32_t** dptr) {
-    reap_pending();
-    const size_t bytes = std::max<size_t>(words.size() * sizeof(uint32_t), 4);
-    HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(dptr), bytes, s));
-    HIP_TRY(hipMemcpyAsync(*dptr, words.data(), words.size() * sizeof(uint32_t),
-                           hipMemcpyHostToDevice, s));
-    PendingUpload pu;
-    HIP_TRY(hipEventCreateWithFlags(&pu.ev, hipEventDisableTiming));
-    HIP_TRY(hipEventRecord(pu.ev, s));
-    pu.words = std::move(words);
-    std::lock_guard<std::mutex> lk(g_pending_mu);
-    g_pending.push_back(std::move(pu));
+    auto* held = new std::vector<uint32_t>(std::move(words));
+    const size_t bytes = std::max<size_t>(held->size() * sizeof(uint32_t), 4);
+    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(dptr), bytes, s);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(*dptr, held->data(), held->size() * sizeof(uint32_t),
+                           hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) {
+        // nothing was queued that reads `held` if the copy failed to enqueue; after a failed
+        // allocation nothing was queued at all
+        delete held;
+        return hip_fail(e, "upload_words");
+    }
+    e = hipLaunchHostFunc(s, release_words, held);
+    if (e != hipSuccess) {
+        // keep the words alive: wait for the copy, then free them here
+        (void)hipStreamSynchronize(s);
+        delete held;
+        return hip_fail(e, "hipLaunchHostFunc");
+    }
     return CEC_OK;
 }
 
