@@ -520,12 +520,13 @@ struct Batch {
     std::condition_variable cv;
 };
 
-// Batches on the GPU at once (CEC_COALESCE_INFLIGHT, 1..16; default 1).  More than one lets the
-// next batch gather and copy while earlier ones run, but a leader then starts as soon as an arena
-// is free, and since a launch costs one chunk's SHA chain whatever its size, the callers split
-// into ever smaller batches that each pay it: measured on one box, interleaved
-// (profiles/r1y_percall_ab.log), 100 threads 7.1-8.2 GB/s with 1 vs 3.6-3.8 with 4, 400 threads
-// 6.9-7.9 vs 6.0-7.1.
+// Batches on the GPU at once (CEC_COALESCE_INFLIGHT, 1..16; default 2).  A second batch starts
+// while one runs only when the batch before it overflowed the cap (callers of its key were left
+// queued): otherwise a leader would start as soon as an arena is free, and since a launch costs
+// one chunk's SHA chain whatever its size, the callers would split into ever smaller batches that
+// each pay it (round 1, unconditional: 100 threads 7.1-8.2 GB/s with 1 vs 3.6-3.8 with 4,
+// profiles/r1y_percall_ab.log).  Overflowing callers (256 pageable parts vs a 1 GiB cap) then
+// copy in while the first batch runs: 13.9 -> ~26 GB/s (profiles/r2_percall/).
 // CEC_COALESCE_ADAPT=0 (A/B knob): fixed CEC_COALESCE_US window, no early exit.
 bool coalesce_adaptive() {
     static const bool on = [] {
@@ -538,7 +539,7 @@ bool coalesce_adaptive() {
 uint32_t coalesce_inflight() {
     static const uint32_t n = [] {
         const char* e = std::getenv("CEC_COALESCE_INFLIGHT");
-        const unsigned long v = e ? std::strtoul(e, nullptr, 10) : 1ul;
+        const unsigned long v = e ? std::strtoul(e, nullptr, 10) : 2ul;
         return uint32_t(std::min<unsigned long>(std::max<unsigned long>(v, 1ul), 16ul));
     }();
     return n;
@@ -567,7 +568,8 @@ class Coalescer {
                 r->phase = Phase::Finished;
                 if (++r->batch->finished == r->batch->size) r->batch->cv.notify_one();
                 break;
-            } else if (r->phase == Phase::Queued && !gathering_ && active_ < coalesce_inflight()) {
+            } else if (r->phase == Phase::Queued && !gathering_ &&
+                       (active_ == 0 || (overflow_ && active_ < coalesce_inflight()))) {
                 lead(r, lk);
                 break;
             } else {
@@ -639,6 +641,8 @@ class Coalescer {
         for (Req* q : batch) q->batch = &batch_state;
         batch_state.size = batch.size();
         last_batch_ = batch.size();
+        overflow_ = false;  // callers of this key left behind by the cap
+        for (Req* q : queue_) overflow_ = overflow_ || q->key() == key;
         if (++batches_since_peak_ >= 32) {  // forget an old burst of callers
             peak_ = callers_;
             batches_since_peak_ = 0;
@@ -719,6 +723,7 @@ class Coalescer {
     std::deque<Req*> queue_;
     bool gathering_ = false;
     uint32_t active_ = 0;
+    bool overflow_ = false;          // the last batch formed left callers of its key queued
     size_t last_batch_ = 0;
     size_t callers_ = 0;             // submit() calls in progress
     size_t peak_ = 0;                // most callers in progress at once, lately
@@ -829,6 +834,8 @@ struct PartImpl {
     // Weight against CEC_COALESCE_MAX_MIB: the cap bounds the pinned staging a batch needs; a
     // page-locked caller needs none, so its part counts a quarter (its batch is bounded by the
     // device buffer, 4x the staging cap).
+    // (A/B at 256 page-locked callers, profiles/r2_percall/pinned_cap_*: full weight 26.0 GB/s,
+    // half 23.6, quarter 24.8 — noise; the quarter keeps them in one launch.)
     static size_t cap_bytes(const PartReq& r) { return r.in_pinned ? bytes(r) / 4 : bytes(r); }
     static bool any_pinned(const std::vector<PartReq*>& batch) {
         for (const PartReq* r : batch)
