@@ -148,6 +148,11 @@ _sig("cec_multi_encode_hash", [_vp, _vp, ctypes.c_size_t, _vp, _vp,
 _sig("cec_multi_read", [_vp, _vp, _vp, _vp, ctypes.c_size_t, _vp, _vp,
                         ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint,
                         ctypes.POINTER(ctypes.c_uint64)])
+_sig("cec_multi_resilver", [_vp, _vp, _vp, _vp, ctypes.c_size_t, _vp, _vp,
+                            ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_void_p),
+                            ctypes.POINTER(ctypes.c_uint64)])
+_sig("cec_multi_verify", [_vp, _vp, _vp, _vp, ctypes.c_size_t, _vp,
+                          ctypes.POINTER(ctypes.c_uint64)])
 _sig("cec_multi_wait", [_vp, ctypes.c_uint64])
 _sig("cec_multi_last_error", [], ctypes.c_char_p)
 
@@ -755,6 +760,8 @@ def set_device(device: int) -> None:
 
 PIPE_EXTERNAL = 2  # CEC_PIPE_EXTERNAL
 PRESENT_VERIFIED = 2  # CEC_PRESENT_VERIFIED: read-retry flag (loaded, verified by an earlier pass)
+READ_RESILVER = 4  # CEC_READ_RESILVER: read-pipeline flag, FilePart::resilver's compute
+READ_VERIFY_ONLY = 8  # CEC_READ_VERIFY_ONLY: read-pipeline flag, FilePart::verify's compute
 
 
 class MultiError(Error):
@@ -825,6 +832,35 @@ class Multi:
             raise MultiError(code)
         self._keep[job.value] = (chunks, present, expected, data, verified, status, ptrs)
         return job.value, ptrs
+
+    def resilver(self, chunks, present, expected, n_parts: int, rebuilt, verified, status):
+        """FilePart::resilver's compute; returns (job, chunk_ptrs [n*(d+p)] filled at wait())."""
+        job = ctypes.c_uint64(0)
+        ptrs = (ctypes.c_void_p * max(n_parts * self.t, 1))()
+        code = _lib.cec_multi_resilver(self._h, _addr(chunks), _addr(present), _addr(expected),
+                                       n_parts, _addr(rebuilt), _addr(verified),
+                                       ctypes.cast(_addr(status), ctypes.POINTER(ctypes.c_int)),
+                                       ptrs, ctypes.byref(job))
+        if code != OK:
+            raise MultiError(code)
+        self._keep[job.value] = (chunks, present, expected, rebuilt, verified, status, ptrs)
+        return job.value, ptrs
+
+    def resilver_sync(self, chunks, present, expected, n_parts: int, rebuilt, verified, status):
+        job, ptrs = self.resilver(chunks, present, expected, n_parts, rebuilt, verified, status)
+        keep = self._keep[job]
+        self.wait(job)
+        del keep
+        return [p or 0 for p in ptrs[: n_parts * self.t]]
+
+    def verify_sync(self, chunks, present, expected, n_parts: int, verified) -> None:
+        """FilePart::verify's compute: verified[n][d+p] for every loaded chunk."""
+        job = ctypes.c_uint64(0)
+        code = _lib.cec_multi_verify(self._h, _addr(chunks), _addr(present), _addr(expected),
+                                     n_parts, _addr(verified), ctypes.byref(job))
+        if code != OK:
+            raise MultiError(code)
+        self.wait(job.value)
 
     def wait(self, job: int) -> None:
         code = _lib.cec_multi_wait(self._h, job)

@@ -58,6 +58,8 @@ struct Job {
     uint8_t* verified = nullptr;
     int* status = nullptr;
     const uint8_t** data_ptrs = nullptr;
+    bool resilver = false;  // FilePart::resilver's compute: output [n][t][L], t pointers a part
+    bool verify_only = false;  // FilePart::verify's compute: verified flags only
     // completion
     size_t remaining = 0;  // parts not yet finished (guarded by cec_multi::mu)
     int result = CEC_OK;
@@ -204,8 +206,10 @@ struct cec_multi {
         return st;
     }
 
-    int ensure_read_pipe(Shard& s, unsigned flags) {
-        const unsigned want = (flags & CEC_READ_REBUILT_ONLY) | CEC_PIPE_EXTERNAL;
+    int ensure_read_pipe(Shard& s, unsigned flags, bool resilver, bool verify_only) {
+        const unsigned want = (flags & CEC_READ_REBUILT_ONLY) | CEC_PIPE_EXTERNAL |
+                              (resilver ? CEC_READ_RESILVER : 0u) |
+                              (verify_only ? CEC_READ_VERIFY_ONLY : 0u);
         if (s.rp && s.rp_flags == want) return CEC_OK;
         if (s.rp) {
             drain_read(s);
@@ -249,20 +253,25 @@ struct cec_multi {
         const int* status = nullptr;
         size_t got = 0;
         Job* job = f.job;
+        // chunks per part in the output / pointer table: d (read) or t (resilver)
+        const size_t W = (s.rp_flags & CEC_READ_RESILVER) ? t : d;
+        const bool verify_only = (s.rp_flags & CEC_READ_VERIFY_ONLY) != 0;
         int st = cec_read_pipeline_wait(s.rp, slot, &data, &ver, &status, &got);
-        if (st == CEC_OK) {
-            s.ptrs.resize(f.n * d);
+        if (st == CEC_OK && !verify_only) {
+            s.ptrs.resize(f.n * W);
             st = cec_read_pipeline_data_chunks(s.rp, slot, s.ptrs.data());
         }
         std::string err = st == CEC_OK ? std::string() : cec_pipeline_last_error();
-        if (st == CEC_OK) {
+        if (st == CEC_OK && verify_only) {
+            std::memcpy(job->verified + f.first * t, ver, f.n * t);
+        } else if (st == CEC_OK) {
             std::memcpy(job->verified + f.first * t, ver, f.n * t);
             std::memcpy(job->status + f.first, status, f.n * sizeof(int));
             const bool staged = f.staged_in || f.staged_out;
-            parallel_for(f.n, staged ? f.n * d * L : 0, [&](size_t k) {
-                for (size_t j = 0; j < d; ++j) {
-                    const size_t q = (f.first + k) * d + j;
-                    const uint8_t* src = s.ptrs[k * d + j];
+            parallel_for(f.n, staged ? f.n * W * L : 0, [&](size_t k) {
+                for (size_t j = 0; j < W; ++j) {
+                    const size_t q = (f.first + k) * W + j;
+                    const uint8_t* src = s.ptrs[k * W + j];
                     uint8_t* dst = job->out_data + q * L;
                     if (status[k] == CEC_OK && staged) {
                         // staging is reused by the next batch: the bytes move to the caller
@@ -368,11 +377,11 @@ struct cec_multi {
     }
 
     void run_read(Shard& s, Job* job, size_t lo, size_t hi) {
-        int st = ensure_read_pipe(s, job->flags);
+        int st = ensure_read_pipe(s, job->flags, job->resilver, job->verify_only);
         if (st != CEC_OK) return finish_parts(job, hi - lo, st, g_multi_error);
         if (s.active != Kind::Read) drain_write(s);
         s.active = Kind::Read;
-        const size_t cw = t * L, dw = d * L;
+        const size_t cw = t * L, dw = (job->resilver ? t : d) * L;  // output per part
         for (size_t first = lo; first < hi; first += P) {
             const size_t n = std::min(P, hi - first);
             size_t slot = 0;
@@ -388,9 +397,9 @@ struct cec_multi {
             f.first = first;
             f.n = n;
             const uint8_t* src = job->chunks + first * cw;
-            uint8_t* dst = job->out_data + first * dw;
+            uint8_t* dst = job->verify_only ? nullptr : job->out_data + first * dw;
             f.staged_in = !cec::pinned_range(src, n * cw);
-            f.staged_out = !cec::pinned_range(dst, n * dw);
+            f.staged_out = !job->verify_only && !cec::pinned_range(dst, n * dw);
             Staging& sg = s.rstage[slot];
             if (f.staged_in || f.staged_out) {
                 hipError_t e = hipSuccess;  // every slot at once (see run_write)
@@ -577,6 +586,42 @@ int cec_multi_read(cec_multi* m, const uint8_t* chunks, const uint8_t* present,
     j->verified = verified;
     j->status = part_status;
     j->data_ptrs = data_ptrs;
+    return m->submit(std::move(j), job);
+}
+
+int cec_multi_resilver(cec_multi* m, const uint8_t* chunks, const uint8_t* present,
+                       const uint8_t* expected, size_t n_parts, uint8_t* rebuilt,
+                       uint8_t* verified, int* part_status, const uint8_t** chunk_ptrs,
+                       uint64_t* job) {
+    if (!m || !job) return CEC_ERR_INVALID_ARGUMENT;
+    if (n_parts && (!chunks || !present || !expected || !rebuilt || !verified || !part_status))
+        return CEC_ERR_INVALID_ARGUMENT;
+    auto j = std::make_unique<Job>();
+    j->kind = Kind::Read;
+    j->resilver = true;
+    j->n = n_parts;
+    j->chunks = chunks;
+    j->present = present;
+    j->expected = expected;
+    j->out_data = rebuilt;
+    j->verified = verified;
+    j->status = part_status;
+    j->data_ptrs = chunk_ptrs;
+    return m->submit(std::move(j), job);
+}
+
+int cec_multi_verify(cec_multi* m, const uint8_t* chunks, const uint8_t* present,
+                     const uint8_t* expected, size_t n_parts, uint8_t* verified, uint64_t* job) {
+    if (!m || !job) return CEC_ERR_INVALID_ARGUMENT;
+    if (n_parts && (!chunks || !present || !expected || !verified)) return CEC_ERR_INVALID_ARGUMENT;
+    auto j = std::make_unique<Job>();
+    j->kind = Kind::Read;
+    j->verify_only = true;
+    j->n = n_parts;
+    j->chunks = chunks;
+    j->present = present;
+    j->expected = expected;
+    j->verified = verified;
     return m->submit(std::move(j), job);
 }
 

@@ -318,6 +318,14 @@ struct cec_read_pipeline {
     int device = 0;
     size_t d = 0, p = 0, t = 0, L = 0, cs = 0, parts = 0;
     bool rebuilt_only = false;  // CEC_READ_REBUILT_ONLY: D2H only the data chunks rebuilt
+    // CEC_READ_RESILVER: FilePart::resilver's compute (file_part.rs:253-308): every chunk that
+    // did not verify (data AND parity) is rebuilt and comes back, in a [parts][t][L] output;
+    // the verified ones stay where they were read.
+    bool resilver = false;
+    // CEC_READ_VERIFY_ONLY: FilePart::verify's compute (file_part.rs:228-251): the loaded chunks
+    // are hashed and compared, nothing is decoded or copied back.
+    bool verify_only = false;
+    size_t out_chunks() const { return resilver ? t : d; }  // output chunks per part
     bool external = false;      // CEC_PIPE_EXTERNAL: no pinned chunk / data slot buffers
     std::vector<ReadSlot> slots;
     size_t next = 0;
@@ -362,6 +370,28 @@ struct cec_read_pipeline {
                 PIPE_TRY(hipMemcpy2DAsync(dst, L, src, cs, L, e - j, hipMemcpyDeviceToHost,
                                           s.stream));
             j = e;
+        }
+        return CEC_OK;
+    }
+
+    // Resilver: D2H of the chunks of part k whose flag in `have` is 0 (rebuilt) into their
+    // [t] output slots, one copy per run.
+    int copy_missing_back(ReadSlot& s, size_t k, const uint8_t* have) const {
+        for (size_t i = 0; i < t;) {
+            if (have[i]) {
+                ++i;
+                continue;
+            }
+            size_t e = i;
+            while (e < t && !have[e]) ++e;
+            uint8_t* dst = s.dst_data + (k * t + i) * L;
+            const uint8_t* src = s.d_buf + (k * t + i) * cs;
+            if (cs == L)
+                PIPE_TRY(hipMemcpyAsync(dst, src, (e - i) * L, hipMemcpyDeviceToHost, s.stream));
+            else
+                PIPE_TRY(hipMemcpy2DAsync(dst, L, src, cs, L, e - i, hipMemcpyDeviceToHost,
+                                          s.stream));
+            i = e;
         }
         return CEC_OK;
     }
@@ -415,6 +445,19 @@ struct cec_read_pipeline {
         PIPE_TRY(hipMemcpyAsync(s.d_flags, s.h_hash, n, hipMemcpyHostToDevice, s.stream));
         cec_part_batch b = batch(s, n_parts);
         int st = cec_verify_batch(&b, 0, t, s.d_flags, s.d_expected, s.d_flags + n, s.stream);
+        if (verify_only) {
+            if (st != CEC_OK) {
+                g_pipe_error = cec_last_error();
+                return st;
+            }
+            for (size_t k = 0; k < n_parts; ++k) s.h_status[k] = CEC_OK;
+            PIPE_TRY(hipMemcpyAsync(s.h_ok, s.d_flags + n, n, hipMemcpyDeviceToHost, s.stream));
+            PIPE_TRY(hipEventRecord(s.done, s.stream));
+            s.in_flight = true;
+            s.checked = false;
+            s.n_parts = n_parts;
+            return CEC_OK;
+        }
         // speculative decode from the loaded chunks; parts with fewer than d loaded are skipped
         // (reported at wait).  Any nonzero flag means loaded, as everywhere else.
         s.decode_mask.assign(s.h_present, s.h_present + n);
@@ -427,12 +470,17 @@ struct cec_read_pipeline {
                 std::fill(s.decode_mask.begin() + k * t, s.decode_mask.begin() + (k + 1) * t,
                           uint8_t(1));
         }
-        if (st == CEC_OK) st = cec_reconstruct_batch(codec, &b, s.decode_mask.data(), 1, s.stream);
+        if (st == CEC_OK)
+            st = cec_reconstruct_batch(codec, &b, s.decode_mask.data(), resilver ? 0 : 1,
+                                       s.stream);
         if (st != CEC_OK) {
             g_pipe_error = cec_last_error();
             return st;
         }
-        if (rebuilt_only) {
+        if (resilver) {
+            for (size_t k = 0; k < n_parts && st == CEC_OK; ++k)
+                if (s.h_status[k] == CEC_OK) st = copy_missing_back(s, k, s.h_present + k * t);
+        } else if (rebuilt_only) {
             for (size_t k = 0; k < n_parts && st == CEC_OK; ++k)
                 if (s.h_status[k] == CEC_OK) st = copy_rebuilt_back(s, k);
         } else {
@@ -458,7 +506,9 @@ int cec_read_pipeline_new(const cec_codec* codec, size_t chunk_len, size_t parts
 int cec_read_pipeline_new_ex(const cec_codec* codec, size_t chunk_len, size_t parts_per_batch,
                              size_t depth, unsigned flags, cec_read_pipeline** out) {
     if (!codec || !out || chunk_len == 0 || parts_per_batch == 0 || depth == 0 || depth > 16 ||
-        (flags & ~unsigned(CEC_READ_REBUILT_ONLY | CEC_PIPE_EXTERNAL)))
+        (flags & ~unsigned(CEC_READ_REBUILT_ONLY | CEC_PIPE_EXTERNAL | CEC_READ_RESILVER |
+                           CEC_READ_VERIFY_ONLY)) ||
+        ((flags & CEC_READ_RESILVER) && (flags & CEC_READ_VERIFY_ONLY)))
         return CEC_ERR_INVALID_ARGUMENT;
     *out = nullptr;
     if (cec_device_count() <= 0) return CEC_ERR_NO_DEVICE;
@@ -473,6 +523,8 @@ int cec_read_pipeline_new_ex(const cec_codec* codec, size_t chunk_len, size_t pa
     pl->parts = parts_per_batch;
     pl->rebuilt_only = (flags & CEC_READ_REBUILT_ONLY) != 0;
     pl->external = (flags & CEC_PIPE_EXTERNAL) != 0;
+    pl->resilver = (flags & CEC_READ_RESILVER) != 0;
+    pl->verify_only = (flags & CEC_READ_VERIFY_ONLY) != 0;
     pl->slots.resize(depth);
     const size_t P = pl->parts, t = pl->t;
     for (ReadSlot& s : pl->slots) {
@@ -487,7 +539,7 @@ int cec_read_pipeline_new_ex(const cec_codec* codec, size_t chunk_len, size_t pa
         };
         if (!pl->external) {
             host(&s.h_chunks, P * t * pl->L);
-            host(&s.h_data, P * pl->d * pl->L);
+            host(&s.h_data, P * pl->out_chunks() * pl->L);
         }
         host(&s.h_present, P * t);
         host(&s.h_expected, P * t * 32);
@@ -543,7 +595,7 @@ int cec_read_pipeline_submit_from(cec_read_pipeline* pl, size_t slot, const uint
     if (!pl || slot >= pl->slots.size() || !chunks || n_parts == 0 || n_parts > pl->parts)
         return CEC_ERR_INVALID_ARGUMENT;
     ReadSlot& s = pl->slots[slot];
-    if (!data_out && !s.h_data) return CEC_ERR_INVALID_ARGUMENT;
+    if (!data_out && !s.h_data && !pl->verify_only) return CEC_ERR_INVALID_ARGUMENT;
     const size_t n = n_parts * pl->t;
     if (present) std::memcpy(s.h_present, present, n);
     if (expected) std::memcpy(s.h_expected, expected, n * 32);
@@ -557,6 +609,12 @@ int cec_read_pipeline_wait(cec_read_pipeline* pl, size_t slot, const uint8_t** d
     if (s.in_flight) {
         PIPE_TRY(hipEventSynchronize(s.done));
         s.in_flight = false;
+    }
+    if (!s.checked && s.n_parts && pl->verify_only) {
+        for (size_t i = 0; i < s.n_parts * pl->t; ++i)  // verified by an earlier pass: trusted
+            if (s.h_present[i] == CEC_PRESENT_VERIFIED) s.h_ok[i] = 1;
+        s.data_ptrs.clear();
+        s.checked = true;
     }
     if (!s.checked && s.n_parts) {
         const size_t t = pl->t, d = pl->d, n = s.n_parts;
@@ -585,13 +643,15 @@ int cec_read_pipeline_wait(cec_read_pipeline* pl, size_t slot, const uint8_t** d
             DeviceGuard guard(pl->device);
             PIPE_TRY(guard.status());
             cec_part_batch b = pl->batch(s, n);
-            int st = cec_reconstruct_batch(pl->codec, &b, mask.data(), 1, s.stream);
+            int st = cec_reconstruct_batch(pl->codec, &b, mask.data(), pl->resilver ? 0 : 1,
+                                           s.stream);
             if (st != CEC_OK) {
                 g_pipe_error = cec_last_error();
                 return st;
             }
             for (size_t k : redo) {
-                st = pl->copy_data_back(s, k, 1);
+                st = pl->resilver ? pl->copy_missing_back(s, k, s.h_ok + k * t)
+                                  : pl->copy_data_back(s, k, 1);
                 if (st != CEC_OK) return st;
             }
             PIPE_TRY(hipStreamSynchronize(s.stream));
@@ -602,13 +662,22 @@ int cec_read_pipeline_wait(cec_read_pipeline* pl, size_t slot, const uint8_t** d
         // the data output.
         std::vector<uint8_t> redone(n, 0);
         for (size_t k : redo) redone[k] = 1;
-        s.data_ptrs.resize(n * d);
-        for (size_t k = 0; k < n; ++k)
-            for (size_t j = 0; j < d; ++j) {
-                const bool in_place = pl->rebuilt_only && !redone[k] && s.h_present[k * t + j];
-                s.data_ptrs[k * d + j] = in_place ? s.src_chunks + (k * t + j) * pl->L
-                                                  : s.dst_data + (k * d + j) * pl->L;
-            }
+        if (pl->resilver) {  // [parts][t]: verified chunks where they were read, others rebuilt
+            s.data_ptrs.resize(n * t);
+            for (size_t k = 0; k < n; ++k)
+                for (size_t i = 0; i < t; ++i)
+                    s.data_ptrs[k * t + i] = s.h_ok[k * t + i]
+                                                 ? s.src_chunks + (k * t + i) * pl->L
+                                                 : s.dst_data + (k * t + i) * pl->L;
+        } else {
+            s.data_ptrs.resize(n * d);
+            for (size_t k = 0; k < n; ++k)
+                for (size_t j = 0; j < d; ++j) {
+                    const bool in_place = pl->rebuilt_only && !redone[k] && s.h_present[k * t + j];
+                    s.data_ptrs[k * d + j] = in_place ? s.src_chunks + (k * t + j) * pl->L
+                                                      : s.dst_data + (k * d + j) * pl->L;
+                }
+        }
         s.checked = true;
     }
     if (data) *data = s.dst_data ? s.dst_data : s.h_data;

@@ -34,6 +34,10 @@ pub mod sys {
     pub const CEC_ABI_VERSION: c_int = 1;
     /// cec_read_pipeline_new_ex / cec_multi_read flag: only rebuilt data chunks come back.
     pub const CEC_READ_REBUILT_ONLY: std::os::raw::c_uint = 1;
+    /// cec_read_pipeline_new_ex flag: FilePart::resilver's compute (data and parity rebuilt).
+    pub const CEC_READ_RESILVER: std::os::raw::c_uint = 4;
+    /// cec_read_pipeline_new_ex flag: FilePart::verify's compute (hash and compare only).
+    pub const CEC_READ_VERIFY_ONLY: std::os::raw::c_uint = 8;
     /// cec_pipeline_new_ex / cec_read_pipeline_new_ex flag: batches come from caller buffers.
     pub const CEC_PIPE_EXTERNAL: std::os::raw::c_uint = 2;
     /// Present-flag value of a read retry: loaded and already verified (not hashed again).
@@ -292,6 +296,27 @@ pub mod sys {
             part_status: *mut c_int,
             data_ptrs: *mut *const u8,
             flags: std::os::raw::c_uint,
+            job: *mut u64,
+        ) -> c_int;
+        pub fn cec_multi_resilver(
+            multi: *mut cec_multi,
+            chunks: *const u8,
+            present: *const u8,
+            expected: *const u8,
+            n_parts: usize,
+            rebuilt: *mut u8,
+            verified: *mut u8,
+            part_status: *mut c_int,
+            chunk_ptrs: *mut *const u8,
+            job: *mut u64,
+        ) -> c_int;
+        pub fn cec_multi_verify(
+            multi: *mut cec_multi,
+            chunks: *const u8,
+            present: *const u8,
+            expected: *const u8,
+            n_parts: usize,
+            verified: *mut u8,
             job: *mut u64,
         ) -> c_int;
         pub fn cec_multi_wait(multi: *mut cec_multi, job: u64) -> c_int;

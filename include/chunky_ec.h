@@ -315,6 +315,18 @@ int cec_read_pipeline_query(cec_read_pipeline* pipeline, size_t slot);
 #define CEC_READ_REBUILT_ONLY 1u
 int cec_read_pipeline_new_ex(const cec_codec* codec, size_t chunk_len, size_t parts_per_batch,
                              size_t depth, unsigned flags, cec_read_pipeline** out);
+/* Read-pipeline flag: FilePart::resilver's compute (file_part.rs:253-308) instead of
+ * read_with_context's.  Every chunk that does not verify (data AND parity: missing, or loaded
+ * with a bad hash) is rebuilt from the first d verified chunks (reconstruct, not
+ * reconstruct_data) and comes back into the slot's / the caller's output, which is then
+ * [parts][d+p][chunk_len] (only the rebuilt chunks are written); cec_read_pipeline_data_chunks
+ * gives d+p pointers per part (a verified chunk where it was read, a rebuilt one in the output):
+ * what resilver writes back to storage is every chunk whose verified flag is 0. */
+#define CEC_READ_RESILVER 4u
+/* Read-pipeline flag: FilePart::verify's compute (file_part.rs:228-251): every loaded chunk is
+ * hashed and compared with its metadata digest; nothing is decoded or copied back (wait gives
+ * the verified flags; part_status is CEC_OK; data_out may be NULL). */
+#define CEC_READ_VERIFY_ONLY 8u
 /* After (or instead of) wait: ptrs[k*d + j] = the chunk_len bytes of data chunk j of part k —
  * in the slot's chunk buffer (loaded and verified, REBUILT_ONLY) or in its data buffer
  * (rebuilt, re-decoded, or without REBUILT_ONLY).  Valid until the slot is acquired again;
@@ -362,6 +374,19 @@ int cec_multi_encode_hash(cec_multi* multi, const uint8_t* data, size_t n_parts,
 int cec_multi_read(cec_multi* multi, const uint8_t* chunks, const uint8_t* present,
                    const uint8_t* expected, size_t n_parts, uint8_t* data, uint8_t* verified,
                    int* part_status, const uint8_t** data_ptrs, unsigned flags, uint64_t* job);
+/* FilePart::resilver's compute (file_part.rs:253-308) for n_parts parts: as cec_multi_read, but
+ * every chunk that does not verify (data AND parity) is rebuilt (reconstruct) into
+ * rebuilt [n][d+p][L] (the verified ones are not written there); chunk_ptrs[n*(d+p)] (nullable)
+ * says where each chunk of each part is.  What resilver writes back to storage: each chunk of a
+ * CEC_OK part whose verified flag is 0. */
+int cec_multi_resilver(cec_multi* multi, const uint8_t* chunks, const uint8_t* present,
+                       const uint8_t* expected, size_t n_parts, uint8_t* rebuilt,
+                       uint8_t* verified, int* part_status, const uint8_t** chunk_ptrs,
+                       uint64_t* job);
+/* FilePart::verify's compute for n_parts parts: verified[n][d+p] = every loaded chunk
+ * (present != 0) hashed and compared with expected; nothing is decoded. */
+int cec_multi_verify(cec_multi* multi, const uint8_t* chunks, const uint8_t* present,
+                     const uint8_t* expected, size_t n_parts, uint8_t* verified, uint64_t* job);
 /* Blocks until the job is done; returns its first error (message: cec_multi_last_error). */
 int cec_multi_wait(cec_multi* multi, uint64_t job);
 const char* cec_multi_last_error(void);

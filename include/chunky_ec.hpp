@@ -588,18 +588,108 @@ struct FileReference {
         if (length && out.size() > *length) out.resize(size_t(*length));
         return out;
     }
-    std::vector<PartReport> verify(const ChunkStore& src) const {
-        std::vector<PartReport> r;
-        for (const auto& part : parts) r.push_back(part.verify(src));
+    // FileReference::verify / resilver (file_reference.rs:78-113 over FilePart::verify /
+    // resilver, file_part.rs:228-390).  parts_per_batch > 0: runs of parts of one shape go
+    // through the multi-GPU scheduler (cec_multi_verify / cec_multi_resilver over `devices`):
+    // every stored chunk loaded, hashed against its metadata digest, and (resilver) every chunk
+    // that is missing or fails rebuilt and written back.  Same reports and the same failure
+    // (TooFewShardsPresent) as the per-part calls.
+    std::vector<PartReport> verify(const ChunkStore& src, size_t parts_per_batch = 0,
+                                   size_t depth = 4, const std::vector<int>& devices = {}) const {
+        std::vector<PartReport> r(parts.size());
+        for_runs(parts_per_batch, [&](size_t k0, size_t n) {
+            if (n < 2) r[k0] = parts[k0].verify(src);
+            else check_run(const_cast<ChunkStore&>(src), k0, n, parts_per_batch, depth, devices,
+                           false, r);
+        });
         return r;
     }
-    std::vector<PartReport> resilver(ChunkStore& dest) const {
-        std::vector<PartReport> r;
-        for (const auto& part : parts) r.push_back(part.resilver(dest));
+    std::vector<PartReport> resilver(ChunkStore& dest, size_t parts_per_batch = 0,
+                                     size_t depth = 4, const std::vector<int>& devices = {}) const {
+        std::vector<PartReport> r(parts.size());
+        for_runs(parts_per_batch, [&](size_t k0, size_t n) {
+            if (n < 2) r[k0] = parts[k0].resilver(dest);
+            else check_run(dest, k0, n, parts_per_batch, depth, devices, true, r);
+        });
         return r;
     }
 
    private:
+    // fn(k0, n) over runs of parts of one shape (whole shape: chunk size, d and p); runs of one
+    // part when batching is off.
+    template <typename Fn>
+    void for_runs(size_t parts_per_batch, Fn fn) const {
+        size_t k = 0;
+        while (k < parts.size()) {
+            size_t run = 1;
+            while (parts_per_batch && k + run < parts.size() &&
+                   parts[k + run].chunksize == parts[k].chunksize &&
+                   parts[k + run].data.size() == parts[k].data.size() &&
+                   parts[k + run].parity.size() == parts[k].parity.size())
+                ++run;
+            fn(k, run);
+            k += run;
+        }
+    }
+
+    // verify / resilver of parts [k0, k0 + n) (one shape) through cec_multi, a window of
+    // ppb * depth * shards parts at a time: every stored chunk is loaded.
+    void check_run(ChunkStore& store, size_t k0, size_t n, size_t ppb, size_t depth,
+                   const std::vector<int>& devices, bool resilver,
+                   std::vector<PartReport>& reports) const {
+        const FilePart& first = parts[k0];
+        const size_t d = first.data.size(), t = d + first.parity.size(), L = first.chunksize;
+        const std::vector<int> devs = detail::devices_or_current(devices);
+        cec_multi* m = detail::cached_multi(d, t - d, L, ppb, depth, devs);
+        const size_t W = ppb * depth * devs.size();
+        thread_local detail::PinnedBuf chunks_buf, rebuilt_buf;
+        uint8_t* chunks = chunks_buf.reserve(W * t * L, devs[0]);
+        uint8_t* rebuilt = resilver ? rebuilt_buf.reserve(W * t * L, devs[0]) : nullptr;
+        std::vector<uint8_t> present(W * t), expected(W * t * 32), verified(W * t);
+        std::vector<int> status(W);
+        for (size_t at = 0; at < n; at += W) {
+            const size_t cnt = std::min(W, n - at);
+            detail::parallel_for(cnt, [&](size_t q) {
+                const FilePart& part = parts[k0 + at + q];
+                for (size_t i = 0; i < t; ++i) {
+                    std::memcpy(&expected[(q * t + i) * 32], part.chunk(i).hash.digest().data(), 32);
+                    const Bytes* bytes = store.find(part.chunk(i).hash);
+                    const bool ok = bytes && bytes->size() == L;
+                    present[q * t + i] = ok ? 1 : 0;
+                    if (ok) std::memcpy(chunks + (q * t + i) * L, bytes->data(), L);
+                }
+            });
+            uint64_t job = 0;
+            if (resilver)
+                detail::check_multi(cec_multi_resilver(m, chunks, present.data(), expected.data(),
+                                                       cnt, rebuilt, verified.data(), status.data(),
+                                                       nullptr, &job));
+            else
+                detail::check_multi(cec_multi_verify(m, chunks, present.data(), expected.data(),
+                                                     cnt, verified.data(), &job));
+            detail::check_multi(cec_multi_wait(m, job));
+            for (size_t q = 0; q < cnt; ++q) {
+                PartReport& rep = reports[k0 + at + q];
+                rep.chunks.assign(t, LocationIntegrity::Unavailable);
+                bool missing = false;
+                for (size_t i = 0; i < t; ++i) {
+                    if (present[q * t + i])
+                        rep.chunks[i] = verified[q * t + i] ? LocationIntegrity::Valid
+                                                            : LocationIntegrity::Invalid;
+                    missing = missing || !verified[q * t + i];
+                }
+                if (!resilver || !missing) continue;
+                if (status[q] != CEC_OK) throw ErasureError(Error::TooFewShardsPresent);
+                const FilePart& part = parts[k0 + at + q];
+                for (size_t i = 0; i < t; ++i) {
+                    if (verified[q * t + i]) continue;
+                    store.write_shard(part.chunk(i).hash, rebuilt + (q * t + i) * L, L);
+                    rep.chunks[i] = LocationIntegrity::Resilvered;
+                }
+            }
+        }
+    }
+
     // One window of a run in flight: its parts, loaded chunk buffers and results.
     struct ReadWindow {
         size_t first = 0, n = 0;

@@ -268,6 +268,49 @@ void test_multi_device_paths() {
     }
 }
 
+// tests/cluster.rs:145-231 through the batched verify / resilver (cec_multi_verify /
+// cec_multi_resilver): delete data[0] and parity[0] of every part, corrupt another chunk of some
+// parts, verify reports them, resilver rebuilds exactly those chunks, verify is ideal again, and
+// the file reads back bit-exact.
+void test_batched_verify_resilver() {
+    const size_t d = 3, p = 2, chunk = 1024;
+    const Bytes input = random_bytes(d * chunk * 11 + 500, 99);
+    ChunkStore store;
+    const FileReference f =
+        FileWriteBuilder().chunk_size(chunk).data_chunks(d).parity_chunks(p).write(input, store);
+    for (const auto& devs : std::vector<std::vector<int>>{{}, {0, 0}}) {
+        for (size_t k = 0; k < f.parts.size(); ++k) {
+            store.erase(f.parts[k].data[0].hash);
+            store.erase(f.parts[k].parity[0].hash);
+            if (k % 3 == 1) CHECK(store.corrupt(f.parts[k].data[2].hash, 7));
+        }
+        auto before = f.verify(store, 4, 2, devs);
+        CHECK(before.size() == f.parts.size());
+        for (size_t k = 0; k < f.parts.size(); ++k) {
+            CHECK(!before[k].is_ideal());
+            CHECK(before[k].chunks[0] == LocationIntegrity::Unavailable);
+            CHECK(before[k].chunks[d] == LocationIntegrity::Unavailable);
+            CHECK(before[k].chunks[2] ==
+                  (k % 3 == 1 ? LocationIntegrity::Invalid : LocationIntegrity::Valid));
+        }
+        // the per-part verify reports the same
+        const auto per_part = f.verify(store);
+        for (size_t k = 0; k < f.parts.size(); ++k) CHECK(per_part[k].chunks == before[k].chunks);
+        const auto rep = f.resilver(store, 4, 2, devs);
+        for (size_t k = 0; k < f.parts.size(); ++k) {
+            CHECK(rep[k].chunks[0] == LocationIntegrity::Resilvered);
+            CHECK(rep[k].chunks[d] == LocationIntegrity::Resilvered);
+            CHECK(rep[k].chunks[2] ==
+                  (k % 3 == 1 ? LocationIntegrity::Resilvered : LocationIntegrity::Valid));
+        }
+        for (const auto& r : f.verify(store, 4, 2, devs)) CHECK(r.is_ideal());
+        CHECK(f.read(store, 4, 2, devs) == input);
+    }
+    // a part with fewer than d usable chunks: resilver fails like the per-part call
+    for (size_t i = 1; i < d + p; ++i) store.erase(f.parts[4].chunk(i).hash);
+    CHECK(throws_erasure([&] { f.resilver(store, 4, 2); }, Error::TooFewShardsPresent));
+}
+
 // A FileReference whose parts have different shapes (the metadata allows a d/p per part;
 // file_part.rs:77 builds a codec per part): batched reads group only parts of one shape.
 void test_mixed_shape_read() {
@@ -394,6 +437,7 @@ const Test kTests[] = {
     {"test_batched_paths", test_batched_paths},
     {"test_multi_device_paths", test_multi_device_paths},
     {"test_mixed_shape_read", test_mixed_shape_read},
+    {"test_batched_verify_resilver", test_batched_verify_resilver},
     {"test_one_encode", test_one_encode},
     {"test_matrix_rows", test_matrix_rows},
     {"test_errors", test_errors},

@@ -105,7 +105,8 @@ def test_read_pipeline_argument_checks_precede_device_use():
     a device a valid request reports NoDevice (no host-side fallback pipeline)."""
     import chunky_ec as ce
     rs = ce.ReedSolomon(10, 4)
-    for args in [(1 << 20, 4, 2, 4), (0, 4, 2, 0), (1 << 20, 0, 2, 0), (1 << 20, 4, 0, 0),
+    for args in [(1 << 20, 4, 2, 16), (1 << 20, 4, 2, 12), (0, 4, 2, 0), (1 << 20, 0, 2, 0),
+                 (1 << 20, 4, 0, 0),
                  (1 << 20, 4, 17, 0)]:
         with pytest.raises(ce.Error) as e:
             ce.ReadPipeline(rs, *args)

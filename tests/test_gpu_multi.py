@@ -513,3 +513,74 @@ def test_multi_freed_with_jobs_in_flight_finishes_them():
     import gc
     gc.collect()
     _check_write(src, par, dig, d, p)
+
+
+# ----------------------------------------------------------------------------------------------
+# Resilver / verify through the scheduler (FilePart::resilver / verify compute)
+# ----------------------------------------------------------------------------------------------
+
+@pytest.mark.parametrize("devices", _device_lists())
+@pytest.mark.parametrize("pinned", [False, True])
+def test_multi_resilver_and_verify_vs_oracle(devices, pinned):
+    """file_part.rs:253-308: every chunk that is missing or fails its hash is rebuilt (data AND
+    parity) from the verified ones; file_part.rs:228-251: verify reports every loaded chunk."""
+    d, p, L, n = 6, 3, 1536, 26
+    t = d + p
+    rs = ce.ReedSolomon(d, p)
+    m = ce.Multi(rs, L, 3, 2, devices)
+    data, chunks, present, expected, ok, status = _read_case(n, d, p, L, 91)
+    full = np.zeros((n, t, L), np.uint8)
+    for k in range(n):
+        st, par = oracle.encode_sep(d, p, [data[k, j] for j in range(d)])
+        full[k, :d] = data[k]
+        full[k, d:] = np.stack(par)
+    if pinned:
+        hb = [ce.HostBuffer(n * t * L), ce.HostBuffer(n * t * L)]
+        ch, rebuilt = hb[0].view(n, t, L), hb[1].view(n, t, L)
+        ch[:] = chunks
+        rebuilt[:] = 0
+    else:
+        ch, rebuilt = chunks.copy(), np.zeros((n, t, L), np.uint8)
+    ver = np.zeros((n, t), np.uint8)
+    st = np.zeros(n, np.int32)
+    ptrs = m.resilver_sync(ch, present, expected, n, rebuilt, ver, st)
+    assert list(st) == status
+    assert np.array_equal(ver, ok)
+    import ctypes
+    for k in range(n):
+        if status[k]:
+            continue
+        for i in range(t):
+            got = ctypes.string_at(ptrs[k * t + i], L)
+            assert got == full[k, i].tobytes(), (k, i)  # every chunk, verified or rebuilt
+            if not ok[k, i]:
+                assert np.array_equal(rebuilt[k, i], full[k, i]), (k, i)
+    ver2 = np.zeros((n, t), np.uint8)
+    m.verify_sync(ch, present, expected, n, ver2)
+    assert np.array_equal(ver2, ok)
+
+
+def test_read_pipeline_resilver_flag_vs_oracle():
+    d, p, L, P = 4, 3, 2048 + 16, 10
+    t = d + p
+    rs = ce.ReedSolomon(d, p)
+    rp = ce.ReadPipeline(rs, L, P, 2, ce.READ_RESILVER)
+    data, chunks, present, expected, ok, status = _read_case(P, d, p, L, 13)
+    slot, c, pr, ex = rp.acquire()
+    c[:] = chunks
+    pr[:] = present
+    ex[:] = expected
+    rp.submit(slot, P)
+    out, ver, stt = rp.wait(slot)
+    assert list(stt) == status
+    assert np.array_equal(ver, ok)
+    import ctypes
+    ptrs = (ctypes.c_void_p * (P * t))()
+    assert ce._lib.cec_read_pipeline_data_chunks(rp._h, slot, ptrs) == 0
+    for k in range(P):
+        if status[k]:
+            continue
+        st, par = oracle.encode_sep(d, p, [data[k, j] for j in range(d)])
+        want = [data[k, j] for j in range(d)] + par
+        for i in range(t):
+            assert ctypes.string_at(ptrs[k * t + i], L) == want[i].tobytes(), (k, i)

@@ -113,7 +113,7 @@ def test_part_batch_layout_and_constants_match():
           for f in rfields.split(",") if ":" in f]
     assert [(t, n) for t, n in cf] == [(t, n) for t, n in rf]
     for const in ("CEC_ABI_VERSION", "CEC_READ_REBUILT_ONLY", "CEC_PIPE_EXTERNAL",
-                  "CEC_PRESENT_VERIFIED"):
+                  "CEC_PRESENT_VERIFIED", "CEC_READ_RESILVER", "CEC_READ_VERIFY_ONLY"):
         cv = re.search(rf"#define {const}\s+(\d+)u?", hsrc).group(1)
         rv = re.search(rf"pub const {const}:[^=]+=\s*(\d+);", rsrc).group(1)
         assert cv == rv, const
