@@ -273,7 +273,7 @@ void test_multi_device_paths() {
 // parts, verify reports them, resilver rebuilds exactly those chunks, verify is ideal again, and
 // the file reads back bit-exact.
 void test_batched_verify_resilver() {
-    const size_t d = 3, p = 2, chunk = 1024;
+    const size_t d = 3, p = 3, chunk = 1024;  // 2 lost + 1 corrupt leaves exactly d
     const Bytes input = random_bytes(d * chunk * 11 + 500, 99);
     ChunkStore store;
     const FileReference f =
