@@ -342,6 +342,9 @@ def run_read_stream(args, cfg, codec, world, rank, device, reduce_dev):
     # the loaded data chunks are already in the caller's pinned slot: only rebuilt ones come
     # back (CEC_READ_REBUILT_ONLY); CEC_C5R_COPYALL=1 (A/B) copies all d data chunks back
     copy_all = os.environ.get("CEC_C5R_COPYALL", "0") == "1"
+    if os.environ.get("CEC_C5R_PACKED", "0") == "1":
+        return run_read_stream_packed(args, cfg, codec, world, rank, reduce_dev, lo, hi,
+                                      total_parts, host_blk, host_dig, masks[:4], copy_all)
     rp = ce.ReadPipeline(codec, L, P, depth, 0 if copy_all else ce.ReadPipeline.REBUILT_ONLY)
     for i in range(depth):
         slot, chunks, present, expected = rp.acquire()
@@ -393,6 +396,79 @@ def run_read_stream(args, cfg, codec, world, rank, device, reduce_dev):
             {"slots": depth, "parallelism": f"part-range-sharded x{world}, no collective"},
             "synthetic host stream (GPU-encoded block of parts, d random chunks loaded per part, "
             "loaded sets vary per batch)", **extra)), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def run_read_stream_packed(args, cfg, codec, world, rank, reduce_dev, lo, hi, total_parts,
+                           host_blk, host_dig, masks, copy_all):
+    """c5r with the loaded chunks of each batch packed back to back (part by part, ascending
+    chunk index: what a reader fetching a part's chunks in turn writes) and submitted with
+    cec_read_pipeline_submit_packed: one upload per batch.  One page-locked packed buffer per
+    loaded-set pattern (filled once, as the slots are in the unpacked form); outputs into
+    page-locked per-slot buffers."""
+    import numpy as np
+    d, p, L, P = cfg["d"], cfg["p"], cfg["chunk"], cfg["parts"]
+    t = d + p
+    depth = 4
+    mine = hi - lo
+    flags = ce.PIPE_EXTERNAL | (0 if copy_all else ce.ReadPipeline.REBUILT_ONLY)
+    rp = ce.ReadPipeline(codec, L, P, depth, flags)
+    packs = []
+    for m in masks:
+        buf = ce.HostBuffer(int(m.sum()) * L)
+        view = buf.array.reshape(-1, L)
+        view[:] = host_blk.reshape(P * t, L)[np.flatnonzero(m.reshape(-1))]
+        packs.append(buf)
+    outs = [ce.HostBuffer(P * d * L) for _ in range(depth)]
+    expected = np.ascontiguousarray(host_dig)
+    n_batches = (mine + P - 1) // P
+
+    def submit(i, n):
+        m = masks[i % len(masks)]
+        slot, _, _, _ = rp.acquire()
+        rp.submit_packed(slot, packs[i % len(masks)], m, expected, n, outs[slot])
+        return slot
+
+    for i in range(min(depth, n_batches)):  # warmup
+        submit(i, P)
+    rp.drain()
+    barrier(world)
+    t0 = time.perf_counter()
+    part, bad = lo, 0
+    order = []
+    for i in range(n_batches):
+        if i >= depth:
+            _, _, status = rp.wait(order[i - depth])
+            bad += int((status != 0).sum())
+        n = min(P, hi - part)
+        order.append(submit(i, n))
+        part += n
+    for slot in order[-depth:]:
+        _, _, status = rp.wait(slot)
+        bad += int((status != 0).sum())
+    rp.drain()
+    barrier(world)
+    t1 = time.perf_counter()
+    el = max_over_ranks(t1 - t0, world, reduce_dev)
+    ok = None
+    if args.check and rank == 0:
+        slot = order[-1]
+        _, _, status = rp.wait(slot)
+        n_last = int(status.shape[0])
+        ok = bad == 0
+        for k in (0, n_last // 2, n_last - 1):
+            ok = ok and rp.part_bytes(slot, n_last, k) == host_blk[k, :d].tobytes()
+        ok = bool(ok)
+    if rank == 0:
+        extra = {"undecodable_parts": bad, "packed_upload": True}
+        if ok is not None:
+            extra["check_vs_written"] = ok
+        print(json.dumps(_stream_line(
+            args, cfg, world, n_batches, min(depth, n_batches), el, total_parts * d * L,
+            {"slots": depth, "parallelism": f"part-range-sharded x{world}, no collective"},
+            "synthetic host stream (GPU-encoded block of parts, d random chunks loaded per part "
+            "and packed back to back, 4 loaded-set patterns cycling)", **extra)), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

@@ -137,6 +137,7 @@ _sig("cec_pipeline_new_ex", [_vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_siz
                              ctypes.POINTER(_vp)])
 _sig("cec_pipeline_submit_from", [_vp, ctypes.c_size_t, _vp, ctypes.c_size_t, _vp, _vp])
 _sig("cec_read_pipeline_submit_from", [_vp, ctypes.c_size_t, _vp, _vp, _vp, ctypes.c_size_t, _vp])
+_sig("cec_read_pipeline_submit_packed", [_vp, ctypes.c_size_t, _vp, _vp, _vp, ctypes.c_size_t, _vp])
 _sig("cec_multi_new", [_vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t,
                        ctypes.POINTER(ctypes.c_int), ctypes.c_size_t, ctypes.POINTER(_vp)])
 _sig("cec_multi_free", [_vp], None)
@@ -649,6 +650,14 @@ class ReadPipeline:
     def submit_from(self, slot: int, chunks, present, expected, n_parts: int, data=None) -> None:
         """Batch from the caller's buffers (page-locked ones are DMA'd directly)."""
         _check(_lib.cec_read_pipeline_submit_from(
+            self._h, slot, _addr(chunks), _addr(present), _addr(expected), n_parts,
+            _addr(data) if data is not None else None))
+
+    def submit_packed(self, slot: int, chunks, present, expected, n_parts: int,
+                      data=None) -> None:
+        """Batch whose loaded chunks are packed back to back in (part, chunk index) order
+        (cec_read_pipeline_submit_packed): one upload per batch."""
+        _check(_lib.cec_read_pipeline_submit_packed(
             self._h, slot, _addr(chunks), _addr(present), _addr(expected), n_parts,
             _addr(data) if data is not None else None))
 

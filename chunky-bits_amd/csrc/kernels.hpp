@@ -96,6 +96,22 @@ bool use_split(uint64_t chunks);
 int device_cus();  // CUs of the current device
 hipError_t launch_fill(const FillParams& a, hipStream_t s);
 
+// Packed <-> batch chunk moves (move_kernels.hip): packed chunk j (len bytes at packed + j*len)
+// is batch chunk ids[j] = k*t + i (at batch + k*part_stride + i*chunk_stride); to_batch = 1
+// scatters packed -> batch, 0 gathers batch -> packed.  Device memory on both sides.
+struct MoveParams {
+    uint8_t* batch;
+    uint64_t part_stride;
+    uint64_t chunk_stride;
+    uint32_t t;
+    uint8_t* packed;
+    uint64_t len;
+    const uint32_t* ids;
+    uint32_t n;
+    uint32_t to_batch;
+};
+hipError_t launch_move_chunks(const MoveParams& a, hipStream_t s);
+
 // Host mirror of the device generator (cec_synth_byte).
 uint8_t synth_byte(uint64_t seed, uint64_t part, uint64_t chunk, uint64_t offset);
 

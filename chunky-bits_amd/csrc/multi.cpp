@@ -414,19 +414,28 @@ struct cec_multi {
                 }
             }
             if (f.staged_in) {
-                // only the loaded chunks are read by the engine
+                // only the loaded chunks are staged, packed back to back (part by part, index
+                // ascending): the batch then goes up as one copy (submit_packed)
                 const uint8_t* prs = job->present + first * t;
+                std::vector<size_t> at(n + 1, 0);
+                for (size_t k = 0; k < n; ++k)
+                    at[k + 1] = at[k] + size_t(std::count_if(prs + k * t, prs + (k + 1) * t,
+                                                             [](uint8_t x) { return x != 0; }));
                 const uint8_t* from = src;
                 uint8_t* to = sg.in;
                 parallel_for(n, n * cw, [&](size_t k) {
+                    size_t pos = at[k];
                     for (size_t i = k * t; i < (k + 1) * t; ++i)
-                        if (prs[i]) std::memcpy(to + i * L, from + i * L, L);
+                        if (prs[i]) std::memcpy(to + (pos++) * L, from + i * L, L);
                 });
-                src = sg.in;
+                st = cec_read_pipeline_submit_packed(s.rp, slot, sg.in, prs,
+                                                     job->expected + first * t * 32, n,
+                                                     f.staged_out ? sg.out : dst);
+            } else {
+                st = cec_read_pipeline_submit_from(s.rp, slot, src, job->present + first * t,
+                                                   job->expected + first * t * 32, n,
+                                                   f.staged_out ? sg.out : dst);
             }
-            st = cec_read_pipeline_submit_from(s.rp, slot, src, job->present + first * t,
-                                               job->expected + first * t * 32, n,
-                                               f.staged_out ? sg.out : dst);
             if (st != CEC_OK) {
                 finish_parts(job, hi - first, st, cec_pipeline_last_error());
                 return;

@@ -20,6 +20,7 @@
 
 #include "chunky_ec.h"
 #include "hostmem.hpp"
+#include "kernels.hpp"
 
 namespace {
 
@@ -300,6 +301,9 @@ struct ReadSlot {
     uint8_t* d_buf = nullptr;       // device [parts][t][cs]
     uint8_t* d_expected = nullptr;  // device [parts][t][32]
     uint8_t* d_flags = nullptr;     // device [parts][t] present, then [parts][t] ok
+    uint8_t* d_pack = nullptr;      // device [parts*t][L]  packed upload (submit_packed; lazy)
+    uint32_t* h_ids = nullptr;      // pinned [parts*t]     batch position of packed chunk j
+    uint32_t* d_ids = nullptr;      // device [parts*t]
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
     bool in_flight = false;
@@ -309,6 +313,7 @@ struct ReadSlot {
     uint8_t* dst_data = nullptr;          // this batch's data output (h_data or the caller's)
     std::vector<uint8_t> decode_mask;  // present mask the speculative decode used
     std::vector<const uint8_t*> data_ptrs;  // [parts][d]: where each data chunk is (after wait)
+    std::vector<size_t> src_off;  // [parts][t]: byte offset of a loaded chunk in src_chunks
 };
 
 }  // namespace
@@ -338,8 +343,11 @@ struct cec_read_pipeline {
             if (s.stream) (void)hipStreamSynchronize(s.stream);
             if (s.done) (void)hipEventDestroy(s.done);
             if (s.stream) (void)hipStreamDestroy(s.stream);
-            for (uint8_t* dptr : {s.d_buf, s.d_expected, s.d_flags})
+            for (void* dptr : {static_cast<void*>(s.d_buf), static_cast<void*>(s.d_expected),
+                               static_cast<void*>(s.d_flags), static_cast<void*>(s.d_pack),
+                               static_cast<void*>(s.d_ids)})
                 if (dptr) (void)hipFree(dptr);
+            if (s.h_ids) (void)hipHostFree(s.h_ids);
             for (uint8_t* hptr : {s.h_chunks, s.h_present, s.h_expected, s.h_data, s.h_ok, s.h_hash})
                 if (hptr) (void)hipHostFree(hptr);
             delete[] s.h_status;
@@ -355,6 +363,27 @@ struct cec_read_pipeline {
     // them) into their data slots: one copy per run of consecutive missing data chunks.
     int copy_rebuilt_back(ReadSlot& s, size_t k) const {
         const uint8_t* pr = s.h_present + k * t;
+        static const bool span = [] {
+            const char* e = std::getenv("CEC_READ_D2H_SPAN");
+            return e && e[0] == '1';
+        }();
+        if (span) {  // A/B: one copy from the first to the last rebuilt data chunk
+            size_t lo = d, hi = 0;
+            for (size_t j = 0; j < d; ++j)
+                if (!pr[j]) {
+                    lo = std::min(lo, j);
+                    hi = j + 1;
+                }
+            if (lo >= hi) return CEC_OK;
+            uint8_t* dst = s.dst_data + (k * d + lo) * L;
+            const uint8_t* src = s.d_buf + (k * t + lo) * cs;
+            if (cs == L)
+                PIPE_TRY(hipMemcpyAsync(dst, src, (hi - lo) * L, hipMemcpyDeviceToHost, s.stream));
+            else
+                PIPE_TRY(hipMemcpy2DAsync(dst, L, src, cs, L, hi - lo, hipMemcpyDeviceToHost,
+                                          s.stream));
+            return CEC_OK;
+        }
         for (size_t j = 0; j < d;) {
             if (pr[j]) {
                 ++j;
@@ -412,12 +441,54 @@ struct cec_read_pipeline {
     }
 
     // Queue one batch whose present flags / expected digests are in the slot's pinned arrays.
-    int submit(ReadSlot& s, const uint8_t* chunks, size_t n_parts, uint8_t* data_out) {
+    // Device / pinned buffers of the packed upload, made on a slot's first packed batch.
+    int ensure_packed(ReadSlot& s) const {
+        if (s.d_pack) return CEC_OK;
+        const size_t n = parts * t;
+        hipError_t e = hipMalloc(reinterpret_cast<void**>(&s.d_ids), n * sizeof(uint32_t));
+        if (e == hipSuccess)
+            e = cec::host_malloc_near(reinterpret_cast<void**>(&s.h_ids), n * sizeof(uint32_t),
+                                      hipHostMallocDefault, device);
+        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_pack), n * L);
+        return e == hipSuccess ? CEC_OK : pipe_fail(e, "read pipeline packed buffers");
+    }
+
+    // packed: `chunks` holds the loaded chunks back to back (part by part, ascending chunk
+    // index), uploaded with ONE copy and placed by the move kernel; else chunk (k, i) is at
+    // chunks + (k*t + i)*L and goes up with one copy per run of consecutive loaded chunks.
+    int submit(ReadSlot& s, const uint8_t* chunks, size_t n_parts, uint8_t* data_out,
+               bool packed = false) {
         DeviceGuard guard(device);
         PIPE_TRY(guard.status());
+        if (s.in_flight) {  // the slot's pinned arrays may still be read by its last batch
+            PIPE_TRY(hipEventSynchronize(s.done));
+            s.in_flight = false;
+        }
         const size_t n = n_parts * t;
         s.src_chunks = chunks;
         s.dst_data = data_out;
+        s.src_off.resize(n);
+        if (packed) {
+            const int est = ensure_packed(s);
+            if (est != CEC_OK) return est;
+            size_t m = 0;
+            for (size_t x = 0; x < n; ++x)
+                if (s.h_present[x]) {
+                    s.h_ids[m] = uint32_t(x);
+                    s.src_off[x] = m * L;
+                    ++m;
+                }
+            if (m) {
+                PIPE_TRY(hipMemcpyAsync(s.d_pack, chunks, m * L, hipMemcpyHostToDevice, s.stream));
+                PIPE_TRY(hipMemcpyAsync(s.d_ids, s.h_ids, m * sizeof(uint32_t),
+                                        hipMemcpyHostToDevice, s.stream));
+                cec::MoveParams mv{s.d_buf, t * cs, cs, uint32_t(t), s.d_pack, L, s.d_ids,
+                                   uint32_t(m), 1u};
+                PIPE_TRY(cec::launch_move_chunks(mv, s.stream));
+            }
+            return submit_compute(s, n_parts);
+        }
+        for (size_t x = 0; x < n; ++x) s.src_off[x] = x * L;
         // loaded chunks up: one copy per run of consecutive loaded chunks of a part
         for (size_t k = 0; k < n_parts; ++k) {
             const uint8_t* pr = s.h_present + k * t;
@@ -438,6 +509,11 @@ struct cec_read_pipeline {
                 i = j;
             }
         }
+        return submit_compute(s, n_parts);
+    }
+
+    int submit_compute(ReadSlot& s, size_t n_parts) {
+        const size_t n = n_parts * t;
         // hash every loaded chunk except those an earlier pass verified (read retries)
         for (size_t i = 0; i < n; ++i)
             s.h_hash[i] = s.h_present[i] != 0 && s.h_present[i] != CEC_PRESENT_VERIFIED;
@@ -596,10 +672,35 @@ int cec_read_pipeline_submit_from(cec_read_pipeline* pl, size_t slot, const uint
         return CEC_ERR_INVALID_ARGUMENT;
     ReadSlot& s = pl->slots[slot];
     if (!data_out && !s.h_data && !pl->verify_only) return CEC_ERR_INVALID_ARGUMENT;
+    if (s.in_flight) {  // the flags below are read by the slot's last batch until it completes
+        DeviceGuard guard(pl->device);
+        PIPE_TRY(guard.status());
+        PIPE_TRY(hipEventSynchronize(s.done));
+        s.in_flight = false;
+    }
     const size_t n = n_parts * pl->t;
     if (present) std::memcpy(s.h_present, present, n);
     if (expected) std::memcpy(s.h_expected, expected, n * 32);
     return pl->submit(s, chunks, n_parts, data_out ? data_out : s.h_data);
+}
+
+int cec_read_pipeline_submit_packed(cec_read_pipeline* pl, size_t slot, const uint8_t* chunks,
+                                    const uint8_t* present, const uint8_t* expected,
+                                    size_t n_parts, uint8_t* data_out) {
+    if (!pl || slot >= pl->slots.size() || !chunks || n_parts == 0 || n_parts > pl->parts)
+        return CEC_ERR_INVALID_ARGUMENT;
+    ReadSlot& s = pl->slots[slot];
+    if (!data_out && !s.h_data && !pl->verify_only) return CEC_ERR_INVALID_ARGUMENT;
+    if (s.in_flight) {  // the flags below are read by the slot's last batch until it completes
+        DeviceGuard guard(pl->device);
+        PIPE_TRY(guard.status());
+        PIPE_TRY(hipEventSynchronize(s.done));
+        s.in_flight = false;
+    }
+    const size_t n = n_parts * pl->t;
+    if (present) std::memcpy(s.h_present, present, n);
+    if (expected) std::memcpy(s.h_expected, expected, n * 32);
+    return pl->submit(s, chunks, n_parts, data_out ? data_out : s.h_data, true);
 }
 
 int cec_read_pipeline_wait(cec_read_pipeline* pl, size_t slot, const uint8_t** data,
@@ -667,14 +768,14 @@ int cec_read_pipeline_wait(cec_read_pipeline* pl, size_t slot, const uint8_t** d
             for (size_t k = 0; k < n; ++k)
                 for (size_t i = 0; i < t; ++i)
                     s.data_ptrs[k * t + i] = s.h_ok[k * t + i]
-                                                 ? s.src_chunks + (k * t + i) * pl->L
+                                                 ? s.src_chunks + s.src_off[k * t + i]
                                                  : s.dst_data + (k * t + i) * pl->L;
         } else {
             s.data_ptrs.resize(n * d);
             for (size_t k = 0; k < n; ++k)
                 for (size_t j = 0; j < d; ++j) {
                     const bool in_place = pl->rebuilt_only && !redone[k] && s.h_present[k * t + j];
-                    s.data_ptrs[k * d + j] = in_place ? s.src_chunks + (k * t + j) * pl->L
+                    s.data_ptrs[k * d + j] = in_place ? s.src_chunks + s.src_off[k * t + j]
                                                       : s.dst_data + (k * d + j) * pl->L;
                 }
         }

@@ -258,6 +258,15 @@ pub mod sys {
             n_parts: usize,
             data_out: *mut u8,
         ) -> c_int;
+        pub fn cec_read_pipeline_submit_packed(
+            pipeline: *mut cec_read_pipeline,
+            slot: usize,
+            chunks: *const u8,
+            present: *const u8,
+            expected: *const u8,
+            n_parts: usize,
+            data_out: *mut u8,
+        ) -> c_int;
         pub fn cec_read_pipeline_query(pipeline: *mut cec_read_pipeline, slot: usize) -> c_int;
         pub fn cec_multi_new(
             codec: *const cec_codec,

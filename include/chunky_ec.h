@@ -341,6 +341,16 @@ int cec_read_pipeline_data_chunks(cec_read_pipeline* pipeline, size_t slot,
 int cec_read_pipeline_submit_from(cec_read_pipeline* pipeline, size_t slot, const uint8_t* chunks,
                                   const uint8_t* present, const uint8_t* expected, size_t n_parts,
                                   uint8_t* data_out);
+/* As cec_read_pipeline_submit_from with the loaded chunks PACKED: `chunks` holds exactly the
+ * chunks whose present flag is nonzero (CEC_PRESENT_VERIFIED included), chunk_len bytes each,
+ * back to back — part by part, ascending chunk index within a part — the order a reader that
+ * fetches a part's chunks one after the other produces them (file_part.rs:86-107).  The batch
+ * then goes up as ONE copy (per-run copies of randomly loaded chunks cost the copy engines
+ * ~11 us each) and a device kernel places each chunk.  Outputs, data_chunks pointers (which may
+ * point into `chunks`) and lifetimes as cec_read_pipeline_submit_from. */
+int cec_read_pipeline_submit_packed(cec_read_pipeline* pipeline, size_t slot,
+                                    const uint8_t* chunks, const uint8_t* present,
+                                    const uint8_t* expected, size_t n_parts, uint8_t* data_out);
 
 /* ---------------------------------------------------------------------------------------- */
 /* Multi-GPU part scheduler (one process, several GPUs: SURVEY.md §8e)                       */

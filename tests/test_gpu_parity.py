@@ -638,6 +638,96 @@ def test_read_pipeline_matches_read_with_context(d, p, L, parts, depth, batches,
     rp.drain()
 
 
+@pytest.mark.parametrize("d,p,L,parts,depth,batches", [
+    (10, 4, 4096, 12, 3, 5),
+    (3, 2, 683, 9, 2, 3),         # odd chunk length: byte-wise placement kernel
+])
+@pytest.mark.parametrize("flags", [0, ce.ReadPipeline.REBUILT_ONLY])
+@pytest.mark.parametrize("pinned", [False, True])
+def test_read_pipeline_packed_submit(d, p, L, parts, depth, batches, flags, pinned):
+    """cec_read_pipeline_submit_packed: the loaded chunks back to back in (part, index) order,
+    one upload per batch and the move kernel placing them.  Same loaded sets and corruption as
+    the unpacked test; data, flags and statuses as the oracle's rules give them, and the
+    REBUILT_ONLY data_chunks pointers of loaded chunks point into the packed buffer."""
+    t = d + p
+    rs = ce.ReedSolomon(d, p)
+    rp = ce.ReadPipeline(rs, L, parts, depth, flags | ce.PIPE_EXTERNAL)
+    rng = np.random.default_rng(d * 31 + L)
+    pending, want, keep = {}, {}, {}
+    outs = [ce.HostBuffer(parts * d * L) for _ in range(depth)]
+
+    def check(b, slot):
+        data, ver, status = rp.wait(slot)
+        exp_data, exp_ok, exp_status, packed, loaded_of = want[b]
+        assert list(status) == exp_status, b
+        assert np.array_equal(ver, exp_ok), b
+        ptrs = rp.data_chunks(slot, len(exp_status))
+        base = packed.ptr if pinned else packed.ctypes.data
+        for k, st in enumerate(exp_status):
+            if st != 0:
+                continue
+            assert rp.part_bytes(slot, len(exp_status), k) == exp_data[k].tobytes(), (b, k)
+            if flags and exp_ok[k].sum() == len(loaded_of[k]):  # no redo: loaded data in place
+                for j in range(d):
+                    if j in loaded_of[k]:
+                        pos = loaded_of[k][j]
+                        assert int(ptrs[k, j]) == base + pos * L, (b, k, j)
+
+    for b in range(batches):
+        slot, _, present, expected = rp.acquire()
+        if slot in pending:
+            check(pending[slot], slot)
+        n = parts if b % 2 == 0 else parts - 1
+        exp_data, exp_ok, exp_status, pieces, loaded_of = [], np.zeros((n, t), np.uint8), [], [], []
+        present_arr = np.zeros((n, t), np.uint8)
+        expected_arr = np.zeros((n, t, 32), np.uint8)
+        pos = 0
+        for k in range(n):
+            dat = gen_bytes(5000 + 97 * b + k, d * L).reshape(d, L)
+            st, par = oracle.encode_sep(d, p, list(dat))
+            full = [dat[j].copy() for j in range(d)] + [x.copy() for x in par]
+            for i in range(t):
+                expected_arr[k, i] = np.frombuffer(hashlib.sha256(full[i].tobytes()).digest(),
+                                                   np.uint8)
+            kind = (k + b) % 5
+            if kind == 0:
+                loaded = list(range(t))
+            elif kind == 1:
+                loaded = sorted(rng.choice(t, d, replace=False).tolist())
+            elif kind == 2:
+                loaded = sorted(rng.choice(t, d - 1, replace=False).tolist())
+            else:
+                loaded = sorted(rng.choice(t, d + 1 if kind == 3 else d, replace=False).tolist())
+            present_arr[k, loaded] = 1
+            ok = present_arr[k].copy()
+            if kind >= 3:
+                victim = next((i for i in loaded if i < d), loaded[0])
+                full[victim][L // 2] ^= 0x5A
+                ok[victim] = 0
+            where = {}
+            for i in loaded:
+                pieces.append(full[i])
+                where[i] = pos
+                pos += 1
+            loaded_of.append(where)
+            exp_ok[k] = ok
+            exp_status.append(0 if ok.sum() >= d else 10)
+            exp_data.append(dat)
+        flat = np.concatenate(pieces) if pieces else np.zeros(0, np.uint8)
+        if pinned:
+            packed = ce.HostBuffer(max(flat.size, 1))
+            packed.array[: flat.size] = flat
+        else:
+            packed = flat
+        rp.submit_packed(slot, packed, present_arr, expected_arr, n, outs[slot])
+        keep[slot] = packed
+        pending[slot] = b
+        want[b] = (exp_data, exp_ok, exp_status, packed, loaded_of)
+    for slot, b in pending.items():
+        check(b, slot)
+    rp.drain()
+
+
 # ----------------------------------------------------------------------------------------------
 # Verify / read / resilver (FilePart::verify, read_with_context, resilver compute)
 # ----------------------------------------------------------------------------------------------
