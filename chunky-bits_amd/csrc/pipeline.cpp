@@ -363,27 +363,6 @@ struct cec_read_pipeline {
     // them) into their data slots: one copy per run of consecutive missing data chunks.
     int copy_rebuilt_back(ReadSlot& s, size_t k) const {
         const uint8_t* pr = s.h_present + k * t;
-        static const bool span = [] {
-            const char* e = std::getenv("CEC_READ_D2H_SPAN");
-            return e && e[0] == '1';
-        }();
-        if (span) {  // A/B: one copy from the first to the last rebuilt data chunk
-            size_t lo = d, hi = 0;
-            for (size_t j = 0; j < d; ++j)
-                if (!pr[j]) {
-                    lo = std::min(lo, j);
-                    hi = j + 1;
-                }
-            if (lo >= hi) return CEC_OK;
-            uint8_t* dst = s.dst_data + (k * d + lo) * L;
-            const uint8_t* src = s.d_buf + (k * t + lo) * cs;
-            if (cs == L)
-                PIPE_TRY(hipMemcpyAsync(dst, src, (hi - lo) * L, hipMemcpyDeviceToHost, s.stream));
-            else
-                PIPE_TRY(hipMemcpy2DAsync(dst, L, src, cs, L, hi - lo, hipMemcpyDeviceToHost,
-                                          s.stream));
-            return CEC_OK;
-        }
         for (size_t j = 0; j < d;) {
             if (pr[j]) {
                 ++j;
