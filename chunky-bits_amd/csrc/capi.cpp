@@ -69,38 +69,131 @@ bool aligned16(const void* p, size_t a, size_t b) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Host words that must outlive an asynchronous upload.  The copy from pageable memory may read
-// the words after hipMemcpyAsync returns, so they are released by a host function queued right
-// behind the copy on the same stream: it runs once the stream has passed the copy, whatever
-// happens to other streams or events.  (Round 2's first version polled an event per upload and
-// treated any answer but NotReady as done; an event recorded on a stream that was destroyed
-// meanwhile answers an error, and treating that as done freed words still being copied — a
-// GPU memory fault in the read path's decode.)
+// Small per-launch device buffers (decode pattern records, verify item lists, flag arrays).
+//
+// Not hipMallocAsync / hipFreeAsync: on this ROCm, stream work queued behind a hipFreeAsync of a
+// buffer a kernel was still reading did not reliably wait for that kernel — read and resilver
+// batches came back with chunks the decode had not yet (re)written, timing-dependent (the C++
+// mirror's batched verify/resilver and streamed reads, 4 of 4 runs; with the frees removed, 0
+// of 2).  Instead a process-wide pool of device buffers, each with a page-locked host mirror
+// and an event: a buffer is handed out only once the event recorded after its last use has
+// completed, the words go up from the mirror (a truly asynchronous copy, no host lifetime to
+// manage), and its release records the event on the stream of the work that used it.
 // ------------------------------------------------------------------------------------------
-void release_words(void* p) { delete static_cast<std::vector<uint32_t>*>(p); }
+class ScratchPool {
+   public:
+    struct Buf {
+        int device = 0;
+        uint8_t* dev = nullptr;
+        uint8_t* host = nullptr;  // page-locked mirror of the same size
+        size_t cap = 0;
+        hipEvent_t done = nullptr;
+        bool in_use = false;   // handed out, release not called yet
+        bool pending = false;  // released: `done` marks the end of its last use
+    };
 
-// Upload `words` to a stream-ordered device allocation; the allocation is released (stream
-// ordered) by free_upload after the consumer launches.
-int upload_words(std::vector<uint32_t>&& words, hipStream_t s, uint32_t** dptr) {
-    auto* held = new std::vector<uint32_t>(std::move(words));
-    const size_t bytes = std::max<size_t>(held->size() * sizeof(uint32_t), 4);
-    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(dptr), bytes, s);
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(*dptr, held->data(), held->size() * sizeof(uint32_t),
-                           hipMemcpyHostToDevice, s);
-    if (e != hipSuccess) {
-        // nothing was queued that reads `held` if the copy failed to enqueue; after a failed
-        // allocation nothing was queued at all
-        delete held;
-        return hip_fail(e, "upload_words");
+    // A buffer of >= bytes on `device` whose last use has completed.
+    hipError_t acquire(int device, size_t bytes, Buf** out) {
+        std::lock_guard<std::mutex> lk(mu_);
+        Buf* best = nullptr;
+        for (Buf* b : bufs_) {
+            if (b->device != device || b->in_use) continue;
+            if (b->pending) {
+                const hipError_t q = hipEventQuery(b->done);
+                if (q == hipErrorNotReady) {
+                    (void)hipGetLastError();
+                    continue;
+                }
+                if (q != hipSuccess) {  // unknown state (e.g. its stream was destroyed): wait
+                    (void)hipGetLastError();
+                    if (hipEventSynchronize(b->done) != hipSuccess) {
+                        (void)hipGetLastError();
+                        continue;  // never reused
+                    }
+                }
+                b->pending = false;
+            }
+            if (b->cap >= bytes && (!best || b->cap < best->cap)) best = b;
+        }
+        if (!best) {
+            auto* b = new Buf();
+            b->device = device;
+            b->cap = std::max<size_t>(size_t(64) << 10, size_t(1) << (64 - __builtin_clzll(bytes | 1)));
+            hipError_t e = hipMalloc(reinterpret_cast<void**>(&b->dev), b->cap);
+            if (e == hipSuccess)
+                e = hipHostMalloc(reinterpret_cast<void**>(&b->host), b->cap, hipHostMallocDefault);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&b->done, hipEventDisableTiming);
+            if (e != hipSuccess) {
+                (void)hipGetLastError();
+                if (b->dev) (void)hipFree(b->dev);
+                if (b->host) (void)hipHostFree(b->host);
+                delete b;
+                return e;
+            }
+            bufs_.push_back(b);
+            best = b;
+        }
+        best->in_use = true;
+        *out = best;
+        return hipSuccess;
     }
-    e = hipLaunchHostFunc(s, release_words, held);
-    if (e != hipSuccess) {
-        // keep the words alive: wait for the copy, then free them here
-        (void)hipStreamSynchronize(s);
-        delete held;
-        return hip_fail(e, "hipLaunchHostFunc");
+
+    // The work that uses `b` has been queued on `s`: reusable once it completes.
+    void release(Buf* b, hipStream_t s) {
+        const hipError_t e = hipEventRecord(b->done, s);
+        if (e != hipSuccess) {  // no marker: wait for the stream instead
+            (void)hipGetLastError();
+            (void)hipStreamSynchronize(s);
+            (void)hipGetLastError();
+        }
+        std::lock_guard<std::mutex> lk(mu_);
+        b->pending = e == hipSuccess;
+        b->in_use = false;
     }
+
+   private:
+    std::mutex mu_;
+    std::vector<Buf*> bufs_;  // never freed: the pool lives as long as the process
+};
+
+ScratchPool& scratch_pool() {
+    static auto* pool = new ScratchPool();
+    return *pool;
+}
+
+// One scratch buffer for the launches of one call: acquire, fill / upload, launch, and the
+// destructor releases it on the stream those launches went to (error paths included).
+class Scratch {
+   public:
+    Scratch() = default;
+    Scratch(const Scratch&) = delete;
+    Scratch& operator=(const Scratch&) = delete;
+    ~Scratch() {
+        if (buf_) scratch_pool().release(buf_, stream_);
+    }
+    int acquire(size_t bytes, hipStream_t s) {
+        int dev = 0;
+        CEC_TRY(current_device(&dev));
+        HIP_TRY(scratch_pool().acquire(dev, bytes, &buf_));
+        stream_ = s;
+        return CEC_OK;
+    }
+    uint8_t* dev() const { return buf_->dev; }
+    uint8_t* host() const { return buf_->host; }
+
+   private:
+    ScratchPool::Buf* buf_ = nullptr;
+    hipStream_t stream_ = nullptr;
+};
+
+// Upload `words` into `sc` (acquired here) on stream s; *dptr = their device copy.
+int upload_words(const std::vector<uint32_t>& words, hipStream_t s, Scratch& sc, uint32_t** dptr) {
+    const size_t bytes = std::max<size_t>(words.size() * sizeof(uint32_t), 4);
+    CEC_TRY(sc.acquire(bytes, s));
+    std::memcpy(sc.host(), words.data(), words.size() * sizeof(uint32_t));
+    HIP_TRY(hipMemcpyAsync(sc.dev(), sc.host(), words.size() * sizeof(uint32_t),
+                           hipMemcpyHostToDevice, s));
+    *dptr = reinterpret_cast<uint32_t*>(sc.dev());
     return CEC_OK;
 }
 
@@ -1317,7 +1410,8 @@ static int reconstruct_batch(const cec_codec* cc, const cec_part_batch* b, const
     }
     hipStream_t s = static_cast<hipStream_t>(stream);
     uint32_t* dwords = nullptr;
-    CEC_TRY(upload_words(std::move(words), s, &dwords));
+    Scratch scratch;  // released on s behind the launches below
+    CEC_TRY(upload_words(words, s, scratch, &dwords));
     const bool vec = aligned16(b->base, b->part_stride, b->chunk_stride);
     int status = CEC_OK;
     for (size_t i = 0; i < launches.size() && status == CEC_OK; ++i) {
@@ -1337,8 +1431,6 @@ static int reconstruct_batch(const cec_codec* cc, const cec_part_batch* b, const
                                          : launch_rs_apply_var(a, vec, s);
         if (e != hipSuccess) status = hip_fail(e, "launch_rs_apply");
     }
-    hipError_t e = hipFreeAsync(dwords, s);
-    if (status == CEC_OK && e != hipSuccess) status = hip_fail(e, "hipFreeAsync");
     return status;
 }
 
@@ -1485,12 +1577,11 @@ int verify_loaded(const cec_part_batch* b, size_t t, const uint8_t* present_host
         for (size_t i = 0; i < n; ++i) mask[i] = needs_hash(present_host[i]) ? 1u : 0u;
         std::vector<uint8_t> bytes(n);
         for (size_t i = 0; i < n; ++i) bytes[i] = uint8_t(mask[i]);
-        uint8_t* dpresent = nullptr;
-        HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&dpresent), n, s));
-        HIP_TRY(hipMemcpyAsync(dpresent, bytes.data(), n, hipMemcpyHostToDevice, s));
-        HIP_TRY(hipStreamSynchronize(s));  // `bytes` is pageable and local
-        CEC_TRY(cec_verify_batch(b, 0, t, dpresent, expected, ok, s));
-        HIP_TRY(hipFreeAsync(dpresent, s));
+        Scratch sc;
+        CEC_TRY(sc.acquire(n, s));
+        std::memcpy(sc.host(), bytes.data(), n);
+        HIP_TRY(hipMemcpyAsync(sc.dev(), sc.host(), n, hipMemcpyHostToDevice, s));
+        CEC_TRY(cec_verify_batch(b, 0, t, sc.dev(), expected, ok, s));
         return CEC_OK;
     }
     std::vector<uint32_t> items;
@@ -1500,7 +1591,8 @@ int verify_loaded(const cec_part_batch* b, size_t t, const uint8_t* present_host
     if (items.empty()) return CEC_OK;
     const uint32_t n_items = uint32_t(items.size());
     uint32_t* ditems = nullptr;
-    CEC_TRY(upload_words(std::move(items), s, &ditems));
+    Scratch sc;  // released on s behind the verification launch
+    CEC_TRY(upload_words(items, s, sc, &ditems));
     ShaParams h{};
     h.base = b->base;
     h.part_stride = b->part_stride;
@@ -1514,9 +1606,7 @@ int verify_loaded(const cec_part_batch* b, size_t t, const uint8_t* present_host
     h.items = ditems;
     h.n_items = n_items;
     hipError_t e = launch_sha256(h, aligned16(b->base, b->part_stride, b->chunk_stride), s);
-    const hipError_t f = hipFreeAsync(ditems, s);
     if (e != hipSuccess) return hip_fail(e, "launch_sha256 (verify)");
-    if (f != hipSuccess) return hip_fail(f, "hipFreeAsync");
     return CEC_OK;
 }
 
@@ -1541,8 +1631,9 @@ int verify_then_reconstruct(const cec_codec* c, const cec_part_batch* b,
     const size_t d = c->d, t = c->d + c->p, n = b->n_parts * t;
     if (n > 0xFFFFFFFFull) return CEC_ERR_INVALID_ARGUMENT;
     const bool speculate = read_speculate();
-    uint8_t* ok = nullptr;  // device verification flags
-    HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&ok), n, s));
+    Scratch ok_buf;  // device verification flags, released on s behind the readback
+    CEC_TRY(ok_buf.acquire(n, s));
+    uint8_t* ok = ok_buf.dev();
     HIP_TRY(hipMemsetAsync(ok, 0, n, s));
     // Fork point: the caller's work on s so far (the chunks).
     SideLease lease;
@@ -1583,7 +1674,6 @@ int verify_then_reconstruct(const cec_codec* c, const cec_part_batch* b,
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) st = hip_fail(e, "verify readback");
     }
-    (void)hipFreeAsync(ok, s);
     if (st != CEC_OK) return st;
     for (size_t i = 0; i < n; ++i)  // verified by an earlier pass: trusted, not hashed again
         if (present_host[i] == CEC_PRESENT_VERIFIED) verified_host[i] = 1;

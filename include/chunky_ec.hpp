@@ -29,6 +29,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <map>
 #include <memory>
 #include <optional>
@@ -564,9 +565,34 @@ struct FileReference {
     // per-part path.
     Bytes read(const ChunkStore& src, size_t parts_per_batch = 0, size_t depth = 4,
                const std::vector<int>& devices = {}) const {
-        std::vector<size_t> offset(parts.size() + 1, 0);
-        for (size_t k = 0; k < parts.size(); ++k) offset[k + 1] = offset[k] + parts[k].len_bytes();
-        Bytes out(offset.back());
+        uint64_t total = 0;
+        for (const FilePart& part : parts) total += part.len_bytes();
+        if (length && *length < total) total = *length;
+        Bytes out(static_cast<size_t>(total));
+        size_t at = 0;
+        read_to(
+            src,
+            [&](const uint8_t* p, size_t n) {
+                detail::parallel_copy(out.data() + at, p, n);
+                at += n;
+            },
+            parts_per_batch, depth, devices);
+        return out;
+    }
+    // FileReadBuilder's reader (reader.rs:40-75) as a stream: the file's bytes in order (the
+    // last part truncated to `length`, file_reference.rs:49-56) handed to sink(bytes, n) piece by
+    // piece — a batched window of parts at a time, straight from the page-locked buffer the
+    // GPU's output landed in (valid during the call only).  Same bytes and failures as read().
+    template <typename Sink>
+    void read_to(const ChunkStore& src, Sink&& sink, size_t parts_per_batch = 0, size_t depth = 4,
+                 const std::vector<int>& devices = {}) const {
+        uint64_t left = std::numeric_limits<uint64_t>::max();
+        if (length) left = *length;
+        auto emit = [&](const uint8_t* p, size_t n) {
+            const size_t m = size_t(std::min<uint64_t>(n, left));
+            if (m) sink(p, m);
+            left -= m;
+        };
         size_t k = 0;
         while (k < parts.size()) {
             size_t run = 1;
@@ -579,14 +605,12 @@ struct FileReference {
                 ++run;
             if (run < 2) {
                 const Bytes b = parts[k].read_with_context(src);
-                std::memcpy(out.data() + offset[k], b.data(), b.size());
+                emit(b.data(), b.size());
             } else {
-                read_run(src, k, run, parts_per_batch, depth, devices, out.data() + offset[k]);
+                read_run(src, k, run, parts_per_batch, depth, devices, emit);
             }
             k += run;
         }
-        if (length && out.size() > *length) out.resize(size_t(*length));
-        return out;
     }
     // FileReference::verify / resilver (file_reference.rs:78-113 over FilePart::verify /
     // resilver, file_part.rs:228-390).  parts_per_batch > 0: runs of parts of one shape go
@@ -696,22 +720,29 @@ struct FileReference {
         uint64_t job = 0;
         bool live = false;
         detail::PinnedBuf chunks;  // [W][t][L] loaded chunk bytes (DMA'd directly)
+        detail::PinnedBuf out;     // [W][d][L] the parts' data (DMA'd directly)
         std::vector<uint8_t> present, expected, verified;
         std::vector<int> status;
     };
+    static constexpr size_t kMaxReadWindows = 8;
 
-    // Parts [k0, k0 + n) (one shape) through cec_multi, two windows in flight; their bytes land
-    // at dst (part k0 + q at dst + q*d*L).
+    // Parts [k0, k0 + n) (one shape) through cec_multi in windows of one pipeline batch per
+    // shard (ppb x shards parts), up to `depth` windows in flight, so loading the next windows
+    // overlaps the GPU work and the output of the earlier ones; each window's data goes to
+    // emit() in file order.
+    template <typename Emit>
     void read_run(const ChunkStore& src, size_t k0, size_t n, size_t ppb, size_t depth,
-                  const std::vector<int>& devices, uint8_t* dst) const {
+                  const std::vector<int>& devices, Emit& emit) const {
         const FilePart& first = parts[k0];
         const size_t d = first.data.size(), t = d + first.parity.size(), L = first.chunksize;
         const std::vector<int> devs = detail::devices_or_current(devices);
         cec_multi* m = detail::cached_multi(d, t - d, L, ppb, depth, devs);
-        const size_t W = ppb * depth * devs.size();
-        thread_local ReadWindow win[2];
+        const size_t W = ppb * devs.size();
+        const size_t nwin = std::min(std::max<size_t>(depth, 2), kMaxReadWindows);
+        thread_local std::array<ReadWindow, kMaxReadWindows> win;
         auto submit = [&](ReadWindow& w, size_t at, size_t cnt) {
             uint8_t* ch = w.chunks.reserve(W * t * L, devs[0]);
+            uint8_t* out = w.out.reserve(W * d * L, devs[0]);
             w.present.assign(cnt * t, 0);
             w.expected.resize(cnt * t * 32);
             w.verified.assign(cnt * t, 0);
@@ -732,8 +763,8 @@ struct FileReference {
                 }
             });
             detail::check_multi(cec_multi_read(m, ch, w.present.data(), w.expected.data(), cnt,
-                                               dst + at * d * L, w.verified.data(),
-                                               w.status.data(), nullptr, 0, &w.job));
+                                               out, w.verified.data(), w.status.data(), nullptr, 0,
+                                               &w.job));
             w.first = at;
             w.n = cnt;
             w.live = true;
@@ -744,23 +775,25 @@ struct FileReference {
             std::vector<size_t> failed;
             for (size_t q = 0; q < w.n; ++q)
                 if (w.status[q] != CEC_OK) failed.push_back(q);
-            if (!failed.empty()) retry(src, m, k0, d, t, L, w, failed, dst);
+            uint8_t* out = w.out.reserve(W * d * L, devs[0]);
+            if (!failed.empty()) retry(src, m, k0, d, t, L, w, failed, out);
+            emit(out, w.n * d * L);
         };
         try {
             size_t at = 0;
-            int cur = 0;
-            while (at < n || win[0].live || win[1].live) {
-                ReadWindow& w = win[cur];
+            for (size_t i = 0; at < n || std::any_of(win.begin(), win.begin() + nwin,
+                                                     [](const ReadWindow& w) { return w.live; });
+                 ++i) {
+                ReadWindow& w = win[i % nwin];  // windows are collected in submission order
                 if (w.live) collect(w);
                 if (at < n) {
                     const size_t cnt = std::min(W, n - at);
                     submit(w, at, cnt);
                     at += cnt;
                 }
-                cur ^= 1;
             }
         } catch (...) {
-            for (auto& w : win)  // no job may still write into dst / the window buffers
+            for (auto& w : win)  // no job may still write into the window buffers
                 if (w.live) {
                     (void)cec_multi_wait(m, w.job);
                     w.live = false;
@@ -773,8 +806,9 @@ struct FileReference {
     // The failed parts of a window are resubmitted with the chunks that verified (marked
     // CEC_PRESENT_VERIFIED: not hashed again) plus as many untried stored chunks as are missing,
     // until they decode or no chunk is left (TooFewShardsPresent, as the reference's read).
+    // The rebuilt data of window part q goes to out + q*d*L.
     void retry(const ChunkStore& src, cec_multi* m, size_t k0, size_t d, size_t t, size_t L,
-               const ReadWindow& w, const std::vector<size_t>& failed, uint8_t* dst) const {
+               const ReadWindow& w, const std::vector<size_t>& failed, uint8_t* out) const {
         const size_t f = failed.size();
         std::vector<uint8_t> tried(f * t), good(f * t);
         for (size_t r = 0; r < f; ++r)
@@ -821,7 +855,7 @@ struct FileReference {
                 const size_t r = open[q];
                 for (size_t i = 0; i < t; ++i) good[r * t + i] = verified[q * t + i] != 0;
                 if (status[q] == CEC_OK)
-                    std::memcpy(dst + (w.first + failed[r]) * d * L, &data[q * d * L], d * L);
+                    std::memcpy(out + failed[r] * d * L, &data[q * d * L], d * L);
                 else
                     next_open.push_back(r);
             }

@@ -227,6 +227,25 @@ void test_batched_paths() {
         if (p >= 3) CHECK(batched.corrupt(c.parts[3].data[0].hash, 5));
         CHECK(c.read(batched, 8, 3) == input);
         CHECK(c.read(batched) == input);
+        // streamed (reader.rs:40-75): the same bytes in order, piece by piece, the last part cut
+        // at the file length; depth 1..5 windows in flight (2..5 rings)
+        for (size_t depth : {1, 3, 5}) {
+            Bytes streamed;
+            size_t pieces = 0;
+            c.read_to(batched, [&](const uint8_t* q, size_t m) {
+                streamed.insert(streamed.end(), q, q + m);
+                ++pieces;
+            }, 4, depth);
+            if (streamed != input) {
+                size_t bad = 0;
+                while (bad < std::min(streamed.size(), input.size()) && streamed[bad] == input[bad]) ++bad;
+                std::printf("  streamed read, depth %zu: %zu of %zu bytes, first difference at %zu "
+                            "(part %zu)\n", depth, streamed.size(), input.size(), bad,
+                            bad / (d * chunk));
+            }
+            CHECK(streamed == input);
+            CHECK(pieces >= 2);
+        }
         // a part with fewer than d usable chunks fails like the per-part read
         for (size_t i = 2; i < d + p; ++i) batched.erase(c.parts[5].chunk(i).hash);
         CHECK(batched.corrupt(c.parts[5].chunk(0).hash, 1));
@@ -303,7 +322,16 @@ void test_batched_verify_resilver() {
             CHECK(rep[k].chunks[2] ==
                   (k % 3 == 1 ? LocationIntegrity::Resilvered : LocationIntegrity::Valid));
         }
-        for (const auto& r : f.verify(store, 4, 2, devs)) CHECK(r.is_ideal());
+        {
+            const auto after = f.verify(store, 4, 2, devs);
+            for (size_t k = 0; k < after.size(); ++k)
+                if (!after[k].is_ideal())
+                    for (size_t i = 0; i < d + p; ++i)
+                        if (after[k].chunks[i] != LocationIntegrity::Valid)
+                            std::printf("  after resilver (%zu devices): part %zu chunk %zu state %d\n",
+                                        devs.size(), k, i, int(after[k].chunks[i]));
+            for (const auto& r : after) CHECK(r.is_ideal());
+        }
         CHECK(f.read(store, 4, 2, devs) == input);
     }
     // a part with fewer than d usable chunks: resilver fails like the per-part call
