@@ -3,9 +3,12 @@ kernels and copies finish in microseconds and any missing stream dependency show
 whose speculative decode must be redone (a corrupted loaded chunk), several scheduler jobs
 queued at once.  Every returned byte is checked against the written data.
 
-This is the shape that exposed a race in round 2 (work queued behind a hipFreeAsync of the decode
-patterns did not wait for the decode): the C++ mirror's batched verify/resilver failed 4 of 4
-runs until per-launch metadata moved to the event-recycled scratch pool.
+Round 2 found a race on this path (work queued behind a hipFreeAsync of the decode patterns did
+not reliably wait for the decode): the C++ mirror's batched verify/resilver (a plain C++ process)
+failed 4 of 4 runs until per-launch metadata moved to the event-recycled scratch pool
+(DESIGN.md §4.9).  These Python cases, run against the old allocator in this (torch) process,
+did not reproduce it (profiles/r2_fix/stress/); they stay as ordering coverage next to the
+mirror case, which does.
 """
 import ctypes
 import hashlib
