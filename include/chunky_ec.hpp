@@ -725,6 +725,12 @@ struct FileReference {
         std::vector<int> status;
     };
     static constexpr size_t kMaxReadWindows = 8;
+    // The windows (and their page-locked buffers) of this thread, shared by every read_run
+    // instantiation: a thread_local inside the template would pin a new set per sink type.
+    static std::array<ReadWindow, kMaxReadWindows>& read_windows() {
+        thread_local std::array<ReadWindow, kMaxReadWindows> win;
+        return win;
+    }
 
     // Parts [k0, k0 + n) (one shape) through cec_multi in windows of one pipeline batch per
     // shard (ppb x shards parts), up to `depth` windows in flight, so loading the next windows
@@ -739,7 +745,7 @@ struct FileReference {
         cec_multi* m = detail::cached_multi(d, t - d, L, ppb, depth, devs);
         const size_t W = ppb * devs.size();
         const size_t nwin = std::min(std::max<size_t>(depth, 2), kMaxReadWindows);
-        thread_local std::array<ReadWindow, kMaxReadWindows> win;
+        std::array<ReadWindow, kMaxReadWindows>& win = read_windows();
         auto submit = [&](ReadWindow& w, size_t at, size_t cnt) {
             uint8_t* ch = w.chunks.reserve(W * t * L, devs[0]);
             uint8_t* out = w.out.reserve(W * d * L, devs[0]);
