@@ -284,18 +284,54 @@ bool allow_lds(K kernel, uint32_t bytes) {
                                hipFuncAttributeMaxDynamicSharedMemorySize, int(bytes)) == hipSuccess;
 }
 
+// A dispatch's grid is at most 2^32 - 1 work-items (the AQL packet's 32-bit grid size): with
+// kApplyThreads per block, at most this many blocks.  Larger batches (many parts of long chunks,
+// e.g. 4096 x 64 MiB) are split over several launches of whole parts.
+constexpr uint64_t kMaxApplyBlocks = 0xFFFFFFFFull / kApplyThreads;
+// CEC_APPLY_MAX_BLOCKS (test knob, read per launch) lowers the limit so the split is exercised
+// at test sizes; results are identical either way.
+uint64_t max_apply_blocks() {
+    const char* e = std::getenv("CEC_APPLY_MAX_BLOCKS");
+    const unsigned long long v = e ? std::strtoull(e, nullptr, 10) : 0ull;
+    return v ? std::min<uint64_t>(v, kMaxApplyBlocks) : kMaxApplyBlocks;
+}
+
+// fn(sub) for launches of at most max_parts parts each: part ranges [p0, p0 + n) as a base
+// offset (parts addressed directly) or as offsets into the listed part_ids / part_pat.
+template <typename Fn>
+hipError_t for_part_ranges(const ApplyParams& a, uint64_t max_parts, Fn fn) {
+    for (uint64_t p0 = 0; p0 < a.n_parts; p0 += max_parts) {
+        ApplyParams b = a;
+        b.n_parts = uint32_t(std::min<uint64_t>(max_parts, a.n_parts - p0));
+        if (a.part_ids) {
+            b.part_ids = a.part_ids + p0;
+            if (a.part_pat) b.part_pat = a.part_pat + p0;
+        } else {
+            b.base = a.base + p0 * a.part_stride;
+        }
+        const hipError_t e = fn(b);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
 template <int RG>
 hipError_t launch_rg(const ApplyParams& a, uint32_t row_base, uint32_t groups, bool vec16,
                      hipStream_t s) {
-    const uint32_t tiles = uint32_t((a.len + kApplyTile - 1) / kApplyTile);
-    const dim3 grid(a.n_parts * tiles, groups);
-    return dispatch_apply(vec16, [&](auto k) {
-        using T = Tune<decltype(k)::value>;
-        auto* kern = &rs_apply_kernel<RG, T::kVec, T::kGroup, T::kV, T::kNt>;
-        if (!allow_lds(kern, a.lds_reserve)) return hipErrorInvalidValue;
-        clear_stale_error();
-        hipLaunchKernelGGL(kern, grid, dim3(kApplyThreads), a.lds_reserve, s, a, tiles, row_base);
-        return hipGetLastError();
+    const uint64_t tiles = (a.len + kApplyTile - 1) / kApplyTile;
+    const uint64_t max_blocks = max_apply_blocks();
+    if (tiles > max_blocks) return hipErrorInvalidValue;
+    return for_part_ranges(a, max_blocks / tiles, [&](const ApplyParams& b) {
+        const dim3 grid(uint32_t(b.n_parts * tiles), groups);
+        return dispatch_apply(vec16, [&](auto k) {
+            using T = Tune<decltype(k)::value>;
+            auto* kern = &rs_apply_kernel<RG, T::kVec, T::kGroup, T::kV, T::kNt>;
+            if (!allow_lds(kern, b.lds_reserve)) return hipErrorInvalidValue;
+            clear_stale_error();
+            hipLaunchKernelGGL(kern, grid, dim3(kApplyThreads), b.lds_reserve, s, b,
+                               uint32_t(tiles), row_base);
+            return hipGetLastError();
+        });
     });
 }
 
@@ -332,15 +368,20 @@ hipError_t launch_rs_apply(const ApplyParams& a, bool vec16, hipStream_t s) {
 hipError_t launch_rs_apply_var(const ApplyParams& a, bool vec16, hipStream_t s) {
     if (a.n_parts == 0 || a.len == 0) return hipSuccess;
     if (!a.part_ids || !a.part_pat) return hipErrorInvalidValue;
-    const uint32_t tiles = uint32_t((a.len + kApplyTile - 1) / kApplyTile);
-    const dim3 grid(a.n_parts * tiles);
-    return dispatch_apply(vec16, [&](auto k) {
-        using T = Tune<decltype(k)::value>;
-        auto* kern = &rs_apply_var_kernel<T::kVec, T::kGroup, T::kV, T::kNt>;
-        if (!allow_lds(kern, a.lds_reserve)) return hipErrorInvalidValue;
-        clear_stale_error();
-        hipLaunchKernelGGL(kern, grid, dim3(kApplyThreads), a.lds_reserve, s, a, tiles);
-        return hipGetLastError();
+    const uint64_t tiles = (a.len + kApplyTile - 1) / kApplyTile;
+    const uint64_t max_blocks = max_apply_blocks();
+    if (tiles > max_blocks) return hipErrorInvalidValue;
+    return for_part_ranges(a, max_blocks / tiles, [&](const ApplyParams& b) {
+        const dim3 grid(uint32_t(b.n_parts * tiles));
+        return dispatch_apply(vec16, [&](auto k) {
+            using T = Tune<decltype(k)::value>;
+            auto* kern = &rs_apply_var_kernel<T::kVec, T::kGroup, T::kV, T::kNt>;
+            if (!allow_lds(kern, b.lds_reserve)) return hipErrorInvalidValue;
+            clear_stale_error();
+            hipLaunchKernelGGL(kern, grid, dim3(kApplyThreads), b.lds_reserve, s, b,
+                               uint32_t(tiles));
+            return hipGetLastError();
+        });
     });
 }
 

@@ -898,3 +898,74 @@ def test_resilver_batch_random_patterns_with_corruption(speculate, monkeypatch):
             continue
         assert status[k] == ce.OK
         assert np.array_equal(got[k], ref[k]), k
+
+
+@pytest.mark.slow
+def test_chunk_longer_than_4gib_encode_and_reconstruct():
+    """ChunkSize allows chunks up to 2^32 bytes (cluster/sized_int.rs:139): byte offsets past
+    32 bits.  RS(2,1) with L = 4 GiB + 4 KiB + 48 (not a multiple of the kernels' 16 KiB column
+    range): encode, then lose data chunk 0 and rebuild it.  GF coding is column-local, so
+    windows at the start, across the 2^32 boundary and at the end are checked against the
+    oracle run on just those windows."""
+    d, p = 2, 1
+    L = (1 << 32) + 4096 + 48
+    need = (d + p) * L
+    free, _ = torch.cuda.mem_get_info()
+    if free < need + (2 << 30):
+        pytest.skip("not enough device memory")
+    rs = ce.ReedSolomon(d, p)
+    buf = torch.empty((1, d + p, L), dtype=torch.uint8, device=DEV)
+    batch = ce.PartBatch.from_tensor(buf, L)
+    ce.fill_synthetic(batch, d, 77)
+    ce.encode_batch(rs, batch)
+    torch.cuda.synchronize()
+    windows = [(0, 8192), ((1 << 32) - 4096, 8192), (L - 8192, 8192)]
+
+    def check_windows():
+        for off, w in windows:
+            host = buf[0, :, off:off + w].cpu().numpy()
+            st, par = oracle.encode_sep(d, p, [host[j] for j in range(d)])
+            assert st == 0
+            assert np.array_equal(host[d], par[0]), off
+
+    check_windows()
+    want = [buf[0, 0, off:off + w].cpu().numpy().copy() for off, w in windows]
+    buf[0, 0].zero_()
+    present = np.array([0, 1, 1], np.uint8)
+    ce.reconstruct_batch(rs, batch, present.tobytes(), True)
+    torch.cuda.synchronize()
+    for (off, w), v in zip(windows, want):
+        assert np.array_equal(buf[0, 0, off:off + w].cpu().numpy(), v), off
+    check_windows()
+    del buf
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("max_blocks", ["7", "64", "1000"])
+def test_apply_launch_split_over_part_ranges(monkeypatch, max_blocks):
+    """A dispatch holds at most 2^32-1 work-items, so encode / reconstruct batches of more
+    blocks than that are split into launches over whole part ranges (rs_kernels.hip).  The test
+    knob CEC_APPLY_MAX_BLOCKS lowers the limit to force splits at test size (here 4 tiles per
+    part): every byte must match the unsplit launch."""
+    d, p, L, n = 10, 4, 4 * 16384 + 100, 37
+    t = d + p
+    rs = ce.ReedSolomon(d, p)
+    buf = torch.zeros((n, t, L + 12), dtype=torch.uint8, device=DEV)
+    batch = ce.PartBatch.from_tensor(buf, L)
+    ce.fill_synthetic(batch, d, 4242)
+    ce.encode_batch(rs, batch)
+    torch.cuda.synchronize()
+    ref = buf.clone()
+    rng = np.random.default_rng(int(max_blocks))
+    present = np.ones((n, t), np.uint8)
+    for k in range(n):
+        present[k, rng.choice(t, int(rng.integers(1, p + 1)), replace=False)] = 0
+    monkeypatch.setenv("CEC_APPLY_MAX_BLOCKS", max_blocks)
+    buf[:, d:] = 0
+    ce.encode_batch(rs, batch)  # encode split
+    torch.cuda.synchronize()
+    assert torch.equal(buf, ref)
+    buf[~torch.from_numpy(present).to(DEV).bool()] = 0
+    ce.reconstruct_batch(rs, batch, present.tobytes(), False)  # reconstruct split (var kernel)
+    torch.cuda.synchronize()
+    assert torch.equal(buf, ref)
