@@ -656,8 +656,25 @@ struct FileReference {
         }
     }
 
-    // verify / resilver of parts [k0, k0 + n) (one shape) through cec_multi, a window of
-    // ppb * depth * shards parts at a time: every stored chunk is loaded.
+    // One verify / resilver window in flight.
+    struct CheckWindow {
+        size_t first = 0, n = 0;
+        uint64_t job = 0;
+        bool live = false;
+        detail::PinnedBuf chunks;   // [W][t][L] every stored chunk (DMA'd directly)
+        detail::PinnedBuf rebuilt;  // [W][t][L] resilver: the rebuilt chunks
+        std::vector<uint8_t> present, expected, verified;
+        std::vector<int> status;
+    };
+    static std::array<CheckWindow, 8>& check_windows() {
+        thread_local std::array<CheckWindow, 8> win;
+        return win;
+    }
+
+    // verify / resilver of parts [k0, k0 + n) (one shape) through cec_multi: windows of one
+    // pipeline batch per shard (ppb x shards parts), up to `depth` in flight, so loading the next
+    // windows overlaps the GPU work; every stored chunk is loaded, reports (and resilver's
+    // write-backs) are made window by window in file order.
     void check_run(ChunkStore& store, size_t k0, size_t n, size_t ppb, size_t depth,
                    const std::vector<int>& devices, bool resilver,
                    std::vector<PartReport>& reports) const {
@@ -665,52 +682,81 @@ struct FileReference {
         const size_t d = first.data.size(), t = d + first.parity.size(), L = first.chunksize;
         const std::vector<int> devs = detail::devices_or_current(devices);
         cec_multi* m = detail::cached_multi(d, t - d, L, ppb, depth, devs);
-        const size_t W = ppb * depth * devs.size();
-        thread_local detail::PinnedBuf chunks_buf, rebuilt_buf;
-        uint8_t* chunks = chunks_buf.reserve(W * t * L, devs[0]);
-        uint8_t* rebuilt = resilver ? rebuilt_buf.reserve(W * t * L, devs[0]) : nullptr;
-        std::vector<uint8_t> present(W * t), expected(W * t * 32), verified(W * t);
-        std::vector<int> status(W);
-        for (size_t at = 0; at < n; at += W) {
-            const size_t cnt = std::min(W, n - at);
+        const size_t W = ppb * devs.size();
+        std::array<CheckWindow, 8>& win = check_windows();
+        const size_t nwin = std::min<size_t>(std::max<size_t>(depth, 2), win.size());
+        auto submit = [&](CheckWindow& w, size_t at, size_t cnt) {
+            uint8_t* chunks = w.chunks.reserve(W * t * L, devs[0]);
+            uint8_t* rebuilt = resilver ? w.rebuilt.reserve(W * t * L, devs[0]) : nullptr;
+            w.present.assign(cnt * t, 0);
+            w.expected.resize(cnt * t * 32);
+            w.verified.assign(cnt * t, 0);
+            w.status.assign(cnt, 0);
             detail::parallel_for(cnt, [&](size_t q) {
                 const FilePart& part = parts[k0 + at + q];
                 for (size_t i = 0; i < t; ++i) {
-                    std::memcpy(&expected[(q * t + i) * 32], part.chunk(i).hash.digest().data(), 32);
+                    std::memcpy(&w.expected[(q * t + i) * 32], part.chunk(i).hash.digest().data(), 32);
                     const Bytes* bytes = store.find(part.chunk(i).hash);
                     const bool ok = bytes && bytes->size() == L;
-                    present[q * t + i] = ok ? 1 : 0;
+                    w.present[q * t + i] = ok ? 1 : 0;
                     if (ok) std::memcpy(chunks + (q * t + i) * L, bytes->data(), L);
                 }
             });
-            uint64_t job = 0;
             if (resilver)
-                detail::check_multi(cec_multi_resilver(m, chunks, present.data(), expected.data(),
-                                                       cnt, rebuilt, verified.data(), status.data(),
-                                                       nullptr, &job));
+                detail::check_multi(cec_multi_resilver(m, chunks, w.present.data(), w.expected.data(),
+                                                       cnt, rebuilt, w.verified.data(),
+                                                       w.status.data(), nullptr, &w.job));
             else
-                detail::check_multi(cec_multi_verify(m, chunks, present.data(), expected.data(),
-                                                     cnt, verified.data(), &job));
-            detail::check_multi(cec_multi_wait(m, job));
-            for (size_t q = 0; q < cnt; ++q) {
-                PartReport& rep = reports[k0 + at + q];
+                detail::check_multi(cec_multi_verify(m, chunks, w.present.data(), w.expected.data(),
+                                                     cnt, w.verified.data(), &w.job));
+            w.first = at;
+            w.n = cnt;
+            w.live = true;
+        };
+        auto collect = [&](CheckWindow& w) {
+            w.live = false;
+            detail::check_multi(cec_multi_wait(m, w.job));
+            const uint8_t* rebuilt = resilver ? w.rebuilt.reserve(W * t * L, devs[0]) : nullptr;
+            for (size_t q = 0; q < w.n; ++q) {
+                PartReport& rep = reports[k0 + w.first + q];
                 rep.chunks.assign(t, LocationIntegrity::Unavailable);
                 bool missing = false;
                 for (size_t i = 0; i < t; ++i) {
-                    if (present[q * t + i])
-                        rep.chunks[i] = verified[q * t + i] ? LocationIntegrity::Valid
-                                                            : LocationIntegrity::Invalid;
-                    missing = missing || !verified[q * t + i];
+                    if (w.present[q * t + i])
+                        rep.chunks[i] = w.verified[q * t + i] ? LocationIntegrity::Valid
+                                                              : LocationIntegrity::Invalid;
+                    missing = missing || !w.verified[q * t + i];
                 }
                 if (!resilver || !missing) continue;
-                if (status[q] != CEC_OK) throw ErasureError(Error::TooFewShardsPresent);
-                const FilePart& part = parts[k0 + at + q];
+                if (w.status[q] != CEC_OK) throw ErasureError(Error::TooFewShardsPresent);
+                const FilePart& part = parts[k0 + w.first + q];
                 for (size_t i = 0; i < t; ++i) {
-                    if (verified[q * t + i]) continue;
+                    if (w.verified[q * t + i]) continue;
                     store.write_shard(part.chunk(i).hash, rebuilt + (q * t + i) * L, L);
                     rep.chunks[i] = LocationIntegrity::Resilvered;
                 }
             }
+        };
+        try {
+            size_t at = 0;
+            for (size_t i = 0; at < n || std::any_of(win.begin(), win.begin() + nwin,
+                                                     [](const CheckWindow& w) { return w.live; });
+                 ++i) {
+                CheckWindow& w = win[i % nwin];  // collected in submission order
+                if (w.live) collect(w);
+                if (at < n) {
+                    const size_t cnt = std::min(W, n - at);
+                    submit(w, at, cnt);
+                    at += cnt;
+                }
+            }
+        } catch (...) {
+            for (auto& w : win)  // no job may still write into the window buffers
+                if (w.live) {
+                    (void)cec_multi_wait(m, w.job);
+                    w.live = false;
+                }
+            throw;
         }
     }
 

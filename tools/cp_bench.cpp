@@ -57,6 +57,10 @@ int main(int argc, char** argv) {
         t0 = std::chrono::steady_clock::now();
         const FileReference f = write(store);
         const double w_ram = secs(t0);
+        if (batched) {  // pins the verify / resilver windows (nothing to rebuild yet)
+            (void)f.resilver(store, 128, 4, devices);
+            (void)f.verify(store, 128, 4, devices);
+        }
         for (const auto& part : f.parts) {
             store.erase(part.data[3].hash);
             store.erase(part.parity[1].hash);
@@ -76,13 +80,26 @@ int main(int argc, char** argv) {
             f.read_to(store, [&](const uint8_t*, size_t m) { at += m; });
         const double r_sink = secs(t0);
         ok = ok && at == n;
+        // resilver (rebuild the two lost chunks of every part and write them back), then verify
+        // (every stored chunk hashed)
+        t0 = std::chrono::steady_clock::now();
+        const auto rep = batched ? f.resilver(store, 128, 4, devices) : f.resilver(store);
+        const double rs = secs(t0);
+        t0 = std::chrono::steady_clock::now();
+        const auto ver = batched ? f.verify(store, 128, 4, devices) : f.verify(store);
+        const double vs = secs(t0);
+        for (const auto& r : ver) ok = ok && r.is_ideal();
+        for (const auto& r : rep)
+            ok = ok && r.chunks[3] == LocationIntegrity::Resilvered &&
+                 r.chunks[d + 1] == LocationIntegrity::Resilvered;
         std::printf("%-9s %6.2f GiB, %zu parts, %zu shard(s): write %6.2f GB/s (%6.2f GB/s into "
                     "the RAM store), read with 2 holes/part %6.2f GB/s (%6.2f GB/s streamed to a "
-                    "sink), bit-exact %s\n",
+                    "sink), resilver %6.2f GB/s, verify %6.2f GB/s, bit-exact %s\n",
                     batched ? "batched" : "per-part", double(n) / double(size_t(1) << 30),
                     f.parts.size(), batched ? std::max<size_t>(devices.size(), 1) : size_t(0),
                     double(n) / w / 1e9, double(n) / w_ram / 1e9,
-                    double(n) / r / 1e9, double(n) / r_sink / 1e9, ok ? "yes" : "NO");
+                    double(n) / r / 1e9, double(n) / r_sink / 1e9, double(n) / rs / 1e9,
+                    double(n) / vs / 1e9, ok ? "yes" : "NO");
         std::fflush(stdout);
         if (!ok) return 1;
     }
