@@ -64,6 +64,55 @@ __global__ void stream_kernel(uint8_t* base, uint32_t tiles_per_part, size_t cs)
     }
 }
 
+// Reconstruct-shaped pattern: the D inputs read, W (< P) outputs written (a 2-erasure
+// reconstruct_data writes 1-2 data chunks per part).
+template <int V, bool NT, int W>
+__global__ void stream_w_kernel(uint8_t* base, uint32_t tiles_per_part, size_t cs) {
+    const uint32_t part = blockIdx.x / tiles_per_part;
+    const uint32_t tile = blockIdx.x - part * tiles_per_part;
+    uint8_t* pb = base + size_t(part) * T * cs;
+    const size_t x = size_t(tile) * blockDim.x * 16 * V + size_t(threadIdx.x) * 16;
+    v4u acc[V];
+    for (int u = 0; u < V; ++u) acc[u] = v4u{0, 0, 0, 0};
+    v4u in[D][V];
+#pragma unroll
+    for (int j = 0; j < D; ++j)
+#pragma unroll
+        for (int u = 0; u < V; ++u) in[j][u] = ld<NT>(pb + j * cs + x + size_t(u) * blockDim.x * 16);
+#pragma unroll
+    for (int j = 0; j < D; ++j)
+#pragma unroll
+        for (int u = 0; u < V; ++u) acc[u] ^= in[j][u];
+#pragma unroll
+    for (int r = 0; r < W; ++r)
+#pragma unroll
+        for (int u = 0; u < V; ++u)
+            st<NT>(pb + (D + r) * cs + x + size_t(u) * blockDim.x * 16, acc[u] + v4u{unsigned(r), 0u, 0u, 0u});
+}
+
+template <int V, bool NT, int W>
+void run_w(uint8_t* base, uint32_t parts, int threads) {
+    const uint32_t tiles = uint32_t(L / (size_t(threads) * 16 * V));
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    float best = 1e30f;
+    for (int r = 0; r < 6; ++r) {
+        CK(hipEventRecord(a));
+        hipLaunchKernelGGL((stream_w_kernel<V, NT, W>), dim3(parts * tiles), dim3(threads), 0, 0,
+                           base, tiles, L);
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        float ms;
+        CK(hipEventElapsedTime(&ms, a, b));
+        if (r && ms < best) best = ms;
+    }
+    const double bytes = double(parts) * (D + W) * L;
+    printf("reads %d + writes %d  V %d NT %d threads %4d : %8.3f ms  %7.0f GB/s\n", D, W, V,
+           int(NT), threads, best, bytes / best / 1e6);
+    fflush(stdout);
+}
+
 // Read-only (14 streams) / write-only (14 streams) ceilings of the same layout.
 template <bool NT>
 __global__ void read_kernel(const uint8_t* base, uint32_t tiles_per_part, uint32_t* sink) {
@@ -172,6 +221,17 @@ int main(int argc, char** argv) {
     uint8_t* base;
     CK(hipMalloc(&base, size_t(parts) * T * (L + max_pad)));
     CK(hipMemset(base, 1, size_t(parts) * T * (L + max_pad)));
+    if (argc > 2 && argv[2][0] == 'w') {  // reconstruct-shaped ceilings: 10 reads + W writes
+        run_w<2, true, 1>(base, parts, 256);
+        run_w<2, true, 2>(base, parts, 256);
+        run_w<2, true, 3>(base, parts, 256);
+        run_w<2, true, 4>(base, parts, 256);
+        run_w<4, true, 2>(base, parts, 256);
+        run_w<1, true, 2>(base, parts, 256);
+        run_w<2, false, 2>(base, parts, 256);
+        run_w<2, true, 2>(base, parts, 512);
+        return 0;
+    }
     if (argc > 2 && argv[2][0] == 'p') {  // chunk-stride pad sweep of the best shapes
         for (size_t pad : {size_t(0), size_t(256), size_t(1024), size_t(4096), size_t(8192 + 256),
                            size_t(65536), max_pad}) {
