@@ -94,7 +94,7 @@ class ScratchPool {
 
     // A buffer of >= bytes on `device` whose last use has completed.
     hipError_t acquire(int device, size_t bytes, Buf** out) {
-        std::lock_guard<std::mutex> lk(mu_);
+        std::unique_lock<std::mutex> lk(mu_);
         Buf* best = nullptr;
         for (Buf* b : bufs_) {
             if (b->device != device || b->in_use) continue;
@@ -115,26 +115,31 @@ class ScratchPool {
             }
             if (b->cap >= bytes && (!best || b->cap < best->cap)) best = b;
         }
-        if (!best) {
-            auto* b = new Buf();
-            b->device = device;
-            b->cap = std::max<size_t>(size_t(64) << 10, size_t(1) << (64 - __builtin_clzll(bytes | 1)));
-            hipError_t e = hipMalloc(reinterpret_cast<void**>(&b->dev), b->cap);
-            if (e == hipSuccess)
-                e = hipHostMalloc(reinterpret_cast<void**>(&b->host), b->cap, hipHostMallocDefault);
-            if (e == hipSuccess) e = hipEventCreateWithFlags(&b->done, hipEventDisableTiming);
-            if (e != hipSuccess) {
-                (void)hipGetLastError();
-                if (b->dev) (void)hipFree(b->dev);
-                if (b->host) (void)hipHostFree(b->host);
-                delete b;
-                return e;
-            }
-            bufs_.push_back(b);
-            best = b;
+        if (best) {
+            best->in_use = true;
+            *out = best;
+            return hipSuccess;
         }
-        best->in_use = true;
-        *out = best;
+        // None free: a new buffer, made outside the lock (allocations are slow).
+        lk.unlock();
+        auto* b = new Buf();
+        b->device = device;
+        b->cap = std::max<size_t>(size_t(64) << 10, size_t(1) << (64 - __builtin_clzll(bytes | 1)));
+        hipError_t e = hipMalloc(reinterpret_cast<void**>(&b->dev), b->cap);
+        if (e == hipSuccess)
+            e = hipHostMalloc(reinterpret_cast<void**>(&b->host), b->cap, hipHostMallocDefault);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&b->done, hipEventDisableTiming);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            if (b->dev) (void)hipFree(b->dev);
+            if (b->host) (void)hipHostFree(b->host);
+            delete b;
+            return e;
+        }
+        b->in_use = true;
+        lk.lock();
+        bufs_.push_back(b);
+        *out = b;
         return hipSuccess;
     }
 
