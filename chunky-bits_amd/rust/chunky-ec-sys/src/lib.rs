@@ -754,6 +754,37 @@ impl ReadPipeline {
         check_pipe(unsafe { sys::cec_read_pipeline_submit(self.raw, slot, n_parts) })
     }
 
+    /// A batch whose loaded chunks the reader appended back to back (part by part, ascending
+    /// chunk index): `chunks` holds exactly the chunks whose `present` flag is nonzero, each
+    /// `chunk_len` bytes, and goes up as one copy (`cec_read_pipeline_submit_packed`).
+    ///
+    /// # Safety
+    /// `chunks` must stay alive and unmodified until `slot` is acquired again: the copy is
+    /// asynchronous and `data_chunks` may point into it.
+    pub unsafe fn submit_packed(
+        &mut self,
+        slot: usize,
+        chunks: &[u8],
+        present: &[u8],
+        expected: &[u8],
+        n_parts: usize,
+    ) -> Result<(), CecError> {
+        let n = n_parts * self.t;
+        let loaded = present.iter().take(n).filter(|&&f| f != 0).count();
+        if present.len() < n || expected.len() < n * 32 || chunks.len() < loaded * self.chunk_len {
+            return Err(too_small("submit_packed"));
+        }
+        check_pipe(sys::cec_read_pipeline_submit_packed(
+            self.raw,
+            slot,
+            chunks.as_ptr(),
+            present.as_ptr(),
+            expected.as_ptr(),
+            n_parts,
+            std::ptr::null_mut(),
+        ))
+    }
+
     pub fn wait(&mut self, slot: usize) -> Result<ReadBatchResult<'_>, CecError> {
         let (mut data, mut ver) = (std::ptr::null(), std::ptr::null());
         let mut status: *const c_int = std::ptr::null();
