@@ -298,9 +298,14 @@ struct CachedMulti {
     std::shared_ptr<cec_multi> multi;
 };
 
+inline CachedMulti& cached_multi_entry() {
+    thread_local CachedMulti e;
+    return e;
+}
+
 inline cec_multi* cached_multi(size_t d, size_t p, size_t L, size_t parts, size_t depth,
                                const std::vector<int>& devices) {
-    thread_local CachedMulti e;
+    CachedMulti& e = cached_multi_entry();
     std::vector<size_t> key{d, p, L, parts, depth};
     for (int dv : devices) key.push_back(size_t(dv));
     if (!e.multi || e.key != key) {
@@ -551,7 +556,10 @@ struct FilePart {
 };
 
 // file::FileReference: total length + parts (the metadata document).
+void release_thread_buffers();
+
 struct FileReference {
+    friend void release_thread_buffers();
     std::optional<uint64_t> length;
     std::vector<FilePart> parts;
 
@@ -968,6 +976,19 @@ class FileWriteBuilder {
     }
     FileReference write(const Bytes& b, ChunkStore& dest) const { return write(b.data(), b.size(), dest); }
 
+   public:
+    // The page-locked windows of the calling thread's batched writes (see release_thread_buffers).
+    struct WriteWindow {
+        size_t first = 0, n = 0;
+        uint64_t job = 0;
+        bool live = false;
+        detail::PinnedBuf parity, digests;
+    };
+    static std::array<WriteWindow, 2>& write_windows() {
+        thread_local std::array<WriteWindow, 2> win;
+        return win;
+    }
+
    private:
     size_t chunk_size_ = size_t(1) << 20;
     size_t data_ = 3;
@@ -988,14 +1009,8 @@ class FileWriteBuilder {
         const std::vector<int> devs = detail::devices_or_current(devices_);
         cec_multi* m = detail::cached_multi(d, p, L, batch_, depth_, devs);
         const size_t W = batch_ * depth_ * devs.size();
-        struct Window {
-            size_t first = 0, n = 0;
-            uint64_t job = 0;
-            bool live = false;
-            detail::PinnedBuf parity, digests;
-        };
-        thread_local Window win[2];
-        auto collect = [&](Window& w) {
+        std::array<WriteWindow, 2>& win = write_windows();
+        auto collect = [&](WriteWindow& w) {
             w.live = false;
             detail::check_multi(cec_multi_wait(m, w.job));
             const uint8_t* par = w.parity.reserve(W * p * L, devs[0]);
@@ -1019,7 +1034,7 @@ class FileWriteBuilder {
             size_t at = 0;
             int cur = 0;
             while (at < full || win[0].live || win[1].live) {
-                Window& w = win[cur];
+                WriteWindow& w = win[cur];
                 if (w.live) collect(w);  // oldest window first: parts stay in file order
                 if (at < full) {
                     const size_t cnt = std::min(W, full - at);
@@ -1043,6 +1058,27 @@ class FileWriteBuilder {
         }
     }
 };
+
+// The batched paths keep, per thread, the most recent scheduler and the page-locked windows of
+// the last writes / reads / verifies (reused by the next call: pinning costs ~0.35 s per GiB).
+// A thread that is done with large files can hand them back here; the next batched call makes
+// them again.  Must not be called while that thread has a batched call running (it never does
+// by construction: the calls are synchronous).
+inline void release_thread_buffers() {
+    for (auto& w : FileWriteBuilder::write_windows()) {
+        w.parity.release();
+        w.digests.release();
+    }
+    for (auto& w : FileReference::read_windows()) {
+        w.chunks.release();
+        w.out.release();
+    }
+    for (auto& w : FileReference::check_windows()) {
+        w.chunks.release();
+        w.rebuilt.release();
+    }
+    detail::cached_multi_entry() = detail::CachedMulti{};
+}
 
 }  // namespace chunky_ec
 

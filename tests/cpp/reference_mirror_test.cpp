@@ -333,6 +333,10 @@ void test_batched_verify_resilver() {
             for (const auto& r : after) CHECK(r.is_ideal());
         }
         CHECK(f.read(store, 4, 2, devs) == input);
+        // the thread's scheduler and page-locked windows handed back: the next call remakes them
+        release_thread_buffers();
+        CHECK(f.read(store, 4, 2, devs) == input);
+        for (const auto& r : f.verify(store, 4, 2, devs)) CHECK(r.is_ideal());
     }
     // a part with fewer than d usable chunks: resilver fails like the per-part call
     for (size_t i = 1; i < d + p; ++i) store.erase(f.parts[4].chunk(i).hash);
