@@ -422,14 +422,18 @@ struct cec_read_pipeline {
     // Queue one batch whose present flags / expected digests are in the slot's pinned arrays.
     // Device / pinned buffers of the packed upload, made on a slot's first packed batch.
     int ensure_packed(ReadSlot& s) const {
-        if (s.d_pack) return CEC_OK;
         const size_t n = parts * t;
-        hipError_t e = hipMalloc(reinterpret_cast<void**>(&s.d_ids), n * sizeof(uint32_t));
-        if (e == hipSuccess)
+        hipError_t e = hipSuccess;  // each buffer made once (a failed call leaves the others)
+        if (!s.d_ids) e = hipMalloc(reinterpret_cast<void**>(&s.d_ids), n * sizeof(uint32_t));
+        if (e == hipSuccess && !s.h_ids)
             e = cec::host_malloc_near(reinterpret_cast<void**>(&s.h_ids), n * sizeof(uint32_t),
                                       hipHostMallocDefault, device);
-        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_pack), n * L);
-        return e == hipSuccess ? CEC_OK : pipe_fail(e, "read pipeline packed buffers");
+        if (e == hipSuccess && !s.d_pack) e = hipMalloc(reinterpret_cast<void**>(&s.d_pack), n * L);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            return pipe_fail(e, "read pipeline packed buffers");
+        }
+        return CEC_OK;
     }
 
     // packed: `chunks` holds the loaded chunks back to back (part by part, ascending chunk
