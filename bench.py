@@ -194,7 +194,7 @@ def run_stream(args, cfg, codec, world, rank, device, reduce_dev):
     GPU work is data-independent).  Time = first submit to last result, max over ranks."""
     import numpy as np
     d, p, L, P = cfg["d"], cfg["p"], cfg["chunk"], cfg["parts"]
-    depth = 4
+    depth = int(os.environ.get("CEC_STREAM_DEPTH", "4"))  # slots in flight (A/B knob)
     part_bytes = d * L
     total_parts = int(args.stream_gib * (1 << 30)) // part_bytes
     lo = total_parts * rank // world
@@ -255,7 +255,7 @@ def run_stream_multi(args, cfg, codec, total_parts):
     d, p, L, P = cfg["d"], cfg["p"], cfg["chunk"], cfg["parts"]
     t = d + p
     devices = args.devices
-    depth = 4
+    depth = int(os.environ.get("CEC_STREAM_DEPTH", "4"))  # slots in flight (A/B knob)
     m = ce.Multi(codec, L, P, depth, devices)
     S = _segments(args, cfg, len(devices))
     rng = np.random.default_rng(0)
@@ -314,7 +314,7 @@ def run_read_stream(args, cfg, codec, world, rank, device, reduce_dev):
     import numpy as np
     d, p, L, P = cfg["d"], cfg["p"], cfg["chunk"], cfg["parts"]
     t = d + p
-    depth = 4
+    depth = int(os.environ.get("CEC_STREAM_DEPTH", "4"))  # slots in flight (A/B knob)
     part_bytes = d * L
     total_parts = int(args.stream_gib * (1 << 30)) // part_bytes
     lo = total_parts * rank // world
@@ -410,7 +410,7 @@ def run_read_stream_packed(args, cfg, codec, world, rank, reduce_dev, lo, hi, to
     import numpy as np
     d, p, L, P = cfg["d"], cfg["p"], cfg["chunk"], cfg["parts"]
     t = d + p
-    depth = 4
+    depth = int(os.environ.get("CEC_STREAM_DEPTH", "4"))  # slots in flight (A/B knob)
     mine = hi - lo
     flags = ce.PIPE_EXTERNAL | (0 if copy_all else ce.ReadPipeline.REBUILT_ONLY)
     rp = ce.ReadPipeline(codec, L, P, depth, flags)
@@ -483,7 +483,7 @@ def run_read_stream_multi(args, cfg, codec, total_parts, host_blk, host_dig, mas
     d, p, L, P = cfg["d"], cfg["p"], cfg["chunk"], cfg["parts"]
     t = d + p
     devices = args.devices
-    depth = 4
+    depth = int(os.environ.get("CEC_STREAM_DEPTH", "4"))  # slots in flight (A/B knob)
     m = ce.Multi(codec, L, P, depth, devices)
     S = _segments(args, cfg, len(devices))
     reps = S // P

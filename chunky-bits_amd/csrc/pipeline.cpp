@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -25,6 +26,11 @@
 namespace {
 
 thread_local std::string g_pipe_error;
+
+bool env_flag(const char* name, bool dflt) {
+    const char* v = std::getenv(name);
+    return v && *v ? std::strcmp(v, "0") != 0 : dflt;
+}
 
 int pipe_fail(hipError_t e, const char* what) {
     g_pipe_error = std::string(what) + ": " + hipGetErrorString(e);
@@ -306,6 +312,10 @@ struct ReadSlot {
     uint32_t* d_ids = nullptr;      // device [parts*t]
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
+    // side stream (decode + rebuilt D2H beside the verification) and its fork / join events;
+    // uploaded: the shared upload stream's event this slot's compute waits for (made lazily)
+    hipStream_t side = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr, uploaded = nullptr;
     bool in_flight = false;
     bool checked = false;
     size_t n_parts = 0;
@@ -332,6 +342,13 @@ struct cec_read_pipeline {
     bool verify_only = false;
     size_t out_chunks() const { return resilver ? t : d; }  // output chunks per part
     bool external = false;      // CEC_PIPE_EXTERNAL: no pinned chunk / data slot buffers
+    // A/B knobs (read once at creation): CEC_READ_SIDE=1 runs the speculative decode and the
+    // rebuilt chunks' D2H on a per-slot side stream beside the verification; CEC_READ_UPSTREAM=1
+    // queues every slot's uploads on one pipeline-wide stream (batches go up one after another
+    // in submission order instead of sharing the link).
+    bool side_decode = false;
+    bool shared_upload = false;
+    hipStream_t up = nullptr;
     std::vector<ReadSlot> slots;
     size_t next = 0;
 
@@ -339,10 +356,14 @@ struct cec_read_pipeline {
         int cur = 0;
         if (hipGetDevice(&cur) != hipSuccess) return;
         (void)hipSetDevice(device);
+        if (up) (void)hipStreamSynchronize(up);
         for (ReadSlot& s : slots) {
             if (s.stream) (void)hipStreamSynchronize(s.stream);
-            if (s.done) (void)hipEventDestroy(s.done);
+            if (s.side) (void)hipStreamSynchronize(s.side);
+            for (hipEvent_t ev : {s.done, s.fork, s.join, s.uploaded})
+                if (ev) (void)hipEventDestroy(ev);
             if (s.stream) (void)hipStreamDestroy(s.stream);
+            if (s.side) (void)hipStreamDestroy(s.side);
             for (void* dptr : {static_cast<void*>(s.d_buf), static_cast<void*>(s.d_expected),
                                static_cast<void*>(s.d_flags), static_cast<void*>(s.d_pack),
                                static_cast<void*>(s.d_ids)})
@@ -352,6 +373,7 @@ struct cec_read_pipeline {
                 if (hptr) (void)hipHostFree(hptr);
             delete[] s.h_status;
         }
+        if (up) (void)hipStreamDestroy(up);
         (void)hipSetDevice(cur);
     }
 
@@ -361,7 +383,7 @@ struct cec_read_pipeline {
 
     // D2H of the data chunks of part k that were not loaded (the speculative decode rebuilt
     // them) into their data slots: one copy per run of consecutive missing data chunks.
-    int copy_rebuilt_back(ReadSlot& s, size_t k) const {
+    int copy_rebuilt_back(ReadSlot& s, size_t k, hipStream_t stream) const {
         const uint8_t* pr = s.h_present + k * t;
         for (size_t j = 0; j < d;) {
             if (pr[j]) {
@@ -373,10 +395,10 @@ struct cec_read_pipeline {
             uint8_t* dst = s.dst_data + (k * d + j) * L;
             const uint8_t* src = s.d_buf + (k * t + j) * cs;
             if (cs == L)
-                PIPE_TRY(hipMemcpyAsync(dst, src, (e - j) * L, hipMemcpyDeviceToHost, s.stream));
+                PIPE_TRY(hipMemcpyAsync(dst, src, (e - j) * L, hipMemcpyDeviceToHost, stream));
             else
                 PIPE_TRY(hipMemcpy2DAsync(dst, L, src, cs, L, e - j, hipMemcpyDeviceToHost,
-                                          s.stream));
+                                          stream));
             j = e;
         }
         return CEC_OK;
@@ -384,7 +406,7 @@ struct cec_read_pipeline {
 
     // Resilver: D2H of the chunks of part k whose flag in `have` is 0 (rebuilt) into their
     // [t] output slots, one copy per run.
-    int copy_missing_back(ReadSlot& s, size_t k, const uint8_t* have) const {
+    int copy_missing_back(ReadSlot& s, size_t k, const uint8_t* have, hipStream_t stream) const {
         for (size_t i = 0; i < t;) {
             if (have[i]) {
                 ++i;
@@ -395,26 +417,26 @@ struct cec_read_pipeline {
             uint8_t* dst = s.dst_data + (k * t + i) * L;
             const uint8_t* src = s.d_buf + (k * t + i) * cs;
             if (cs == L)
-                PIPE_TRY(hipMemcpyAsync(dst, src, (e - i) * L, hipMemcpyDeviceToHost, s.stream));
+                PIPE_TRY(hipMemcpyAsync(dst, src, (e - i) * L, hipMemcpyDeviceToHost, stream));
             else
                 PIPE_TRY(hipMemcpy2DAsync(dst, L, src, cs, L, e - i, hipMemcpyDeviceToHost,
-                                          s.stream));
+                                          stream));
             i = e;
         }
         return CEC_OK;
     }
 
     // D2H of the d data chunks of parts [k0, k0 + n) into the data output.
-    int copy_data_back(ReadSlot& s, size_t k0, size_t n) const {
+    int copy_data_back(ReadSlot& s, size_t k0, size_t n, hipStream_t stream) const {
         const size_t pitch = t * cs, dw = d * L;
         if (cs == L) {
             PIPE_TRY(hipMemcpy2DAsync(s.dst_data + k0 * dw, dw, s.d_buf + k0 * pitch, pitch, dw, n,
-                                      hipMemcpyDeviceToHost, s.stream));
+                                      hipMemcpyDeviceToHost, stream));
         } else {
             for (size_t j = 0; j < d; ++j)
                 PIPE_TRY(hipMemcpy2DAsync(s.dst_data + k0 * dw + j * L, dw,
                                           s.d_buf + k0 * pitch + j * cs, pitch, L, n,
-                                          hipMemcpyDeviceToHost, s.stream));
+                                          hipMemcpyDeviceToHost, stream));
         }
         return CEC_OK;
     }
@@ -436,6 +458,35 @@ struct cec_read_pipeline {
         return CEC_OK;
     }
 
+    // The shared upload stream, the slot's side stream and the events that order them (A/B
+    // knobs; made on first use).
+    int ensure_streams(ReadSlot& s) {
+        hipError_t e = hipSuccess;
+        if (shared_upload && !up) e = hipStreamCreateWithFlags(&up, hipStreamNonBlocking);
+        if (e == hipSuccess && shared_upload && !s.uploaded)
+            e = hipEventCreateWithFlags(&s.uploaded, hipEventDisableTiming);
+        if (e == hipSuccess && side_decode && !s.side)
+            e = hipStreamCreateWithFlags(&s.side, hipStreamNonBlocking);
+        if (e == hipSuccess && side_decode && !s.fork)
+            e = hipEventCreateWithFlags(&s.fork, hipEventDisableTiming);
+        if (e == hipSuccess && side_decode && !s.join)
+            e = hipEventCreateWithFlags(&s.join, hipEventDisableTiming);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            return pipe_fail(e, "read pipeline streams");
+        }
+        return CEC_OK;
+    }
+
+    // Stream the uploads of slot s go on, and the hand-over to its compute stream.
+    hipStream_t upload_stream(ReadSlot& s) const { return shared_upload ? up : s.stream; }
+    int uploads_done(ReadSlot& s) const {
+        if (!shared_upload) return CEC_OK;
+        PIPE_TRY(hipEventRecord(s.uploaded, up));
+        PIPE_TRY(hipStreamWaitEvent(s.stream, s.uploaded, 0));
+        return CEC_OK;
+    }
+
     // packed: `chunks` holds the loaded chunks back to back (part by part, ascending chunk
     // index), uploaded with ONE copy and placed by the move kernel; else chunk (k, i) is at
     // chunks + (k*t + i)*L and goes up with one copy per run of consecutive loaded chunks.
@@ -451,6 +502,9 @@ struct cec_read_pipeline {
         s.src_chunks = chunks;
         s.dst_data = data_out;
         s.src_off.resize(n);
+        const int sst = ensure_streams(s);
+        if (sst != CEC_OK) return sst;
+        const hipStream_t us = upload_stream(s);
         if (packed) {
             const int est = ensure_packed(s);
             if (est != CEC_OK) return est;
@@ -462,9 +516,11 @@ struct cec_read_pipeline {
                     ++m;
                 }
             if (m) {
-                PIPE_TRY(hipMemcpyAsync(s.d_pack, chunks, m * L, hipMemcpyHostToDevice, s.stream));
+                PIPE_TRY(hipMemcpyAsync(s.d_pack, chunks, m * L, hipMemcpyHostToDevice, us));
                 PIPE_TRY(hipMemcpyAsync(s.d_ids, s.h_ids, m * sizeof(uint32_t),
-                                        hipMemcpyHostToDevice, s.stream));
+                                        hipMemcpyHostToDevice, us));
+                const int ust = uploads_done(s);
+                if (ust != CEC_OK) return ust;
                 cec::MoveParams mv{s.d_buf, t * cs, cs, uint32_t(t), s.d_pack, L, s.d_ids,
                                    uint32_t(m), 1u};
                 PIPE_TRY(cec::launch_move_chunks(mv, s.stream));
@@ -485,13 +541,14 @@ struct cec_read_pipeline {
                 const uint8_t* src = chunks + (k * t + i) * L;
                 uint8_t* dst = s.d_buf + (k * t + i) * cs;
                 if (cs == L)
-                    PIPE_TRY(hipMemcpyAsync(dst, src, (j - i) * L, hipMemcpyHostToDevice, s.stream));
+                    PIPE_TRY(hipMemcpyAsync(dst, src, (j - i) * L, hipMemcpyHostToDevice, us));
                 else
-                    PIPE_TRY(hipMemcpy2DAsync(dst, cs, src, L, L, j - i, hipMemcpyHostToDevice,
-                                              s.stream));
+                    PIPE_TRY(hipMemcpy2DAsync(dst, cs, src, L, L, j - i, hipMemcpyHostToDevice, us));
                 i = j;
             }
         }
+        const int ust = uploads_done(s);
+        if (ust != CEC_OK) return ust;
         return submit_compute(s, n_parts);
     }
 
@@ -503,6 +560,14 @@ struct cec_read_pipeline {
         PIPE_TRY(hipMemcpyAsync(s.d_expected, s.h_expected, n * 32, hipMemcpyHostToDevice, s.stream));
         PIPE_TRY(hipMemcpyAsync(s.d_flags, s.h_hash, n, hipMemcpyHostToDevice, s.stream));
         cec_part_batch b = batch(s, n_parts);
+        // decode (and its D2H) on the side stream when enabled: it reads only loaded chunks and
+        // writes only chunks that were not loaded, as the verification beside it reads
+        const bool fork = side_decode && !verify_only;
+        const hipStream_t dstream = fork ? s.side : s.stream;
+        if (fork) {
+            PIPE_TRY(hipEventRecord(s.fork, s.stream));
+            PIPE_TRY(hipStreamWaitEvent(s.side, s.fork, 0));
+        }
         int st = cec_verify_batch(&b, 0, t, s.d_flags, s.d_expected, s.d_flags + n, s.stream);
         if (verify_only) {
             if (st != CEC_OK) {
@@ -531,21 +596,26 @@ struct cec_read_pipeline {
         }
         if (st == CEC_OK)
             st = cec_reconstruct_batch(codec, &b, s.decode_mask.data(), resilver ? 0 : 1,
-                                       s.stream);
+                                       dstream);
         if (st != CEC_OK) {
             g_pipe_error = cec_last_error();
             return st;
         }
         if (resilver) {
             for (size_t k = 0; k < n_parts && st == CEC_OK; ++k)
-                if (s.h_status[k] == CEC_OK) st = copy_missing_back(s, k, s.h_present + k * t);
+                if (s.h_status[k] == CEC_OK)
+                    st = copy_missing_back(s, k, s.h_present + k * t, dstream);
         } else if (rebuilt_only) {
             for (size_t k = 0; k < n_parts && st == CEC_OK; ++k)
-                if (s.h_status[k] == CEC_OK) st = copy_rebuilt_back(s, k);
+                if (s.h_status[k] == CEC_OK) st = copy_rebuilt_back(s, k, dstream);
         } else {
-            st = copy_data_back(s, 0, n_parts);
+            st = copy_data_back(s, 0, n_parts, dstream);
         }
         if (st != CEC_OK) return st;
+        if (fork) {
+            PIPE_TRY(hipEventRecord(s.join, s.side));
+            PIPE_TRY(hipStreamWaitEvent(s.stream, s.join, 0));
+        }
         PIPE_TRY(hipMemcpyAsync(s.h_ok, s.d_flags + n, n, hipMemcpyDeviceToHost, s.stream));
         PIPE_TRY(hipEventRecord(s.done, s.stream));
         s.in_flight = true;
@@ -584,6 +654,8 @@ int cec_read_pipeline_new_ex(const cec_codec* codec, size_t chunk_len, size_t pa
     pl->external = (flags & CEC_PIPE_EXTERNAL) != 0;
     pl->resilver = (flags & CEC_READ_RESILVER) != 0;
     pl->verify_only = (flags & CEC_READ_VERIFY_ONLY) != 0;
+    pl->side_decode = env_flag("CEC_READ_SIDE", false);
+    pl->shared_upload = env_flag("CEC_READ_UPSTREAM", false);
     pl->slots.resize(depth);
     const size_t P = pl->parts, t = pl->t;
     for (ReadSlot& s : pl->slots) {
@@ -734,8 +806,8 @@ int cec_read_pipeline_wait(cec_read_pipeline* pl, size_t slot, const uint8_t** d
                 return st;
             }
             for (size_t k : redo) {
-                st = pl->resilver ? pl->copy_missing_back(s, k, s.h_ok + k * t)
-                                  : pl->copy_data_back(s, k, 1);
+                st = pl->resilver ? pl->copy_missing_back(s, k, s.h_ok + k * t, s.stream)
+                                  : pl->copy_data_back(s, k, 1, s.stream);
                 if (st != CEC_OK) return st;
             }
             PIPE_TRY(hipStreamSynchronize(s.stream));
