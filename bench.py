@@ -239,6 +239,44 @@ def run_stream(args, cfg, codec, world, rank, device, reduce_dev):
         dist.destroy_process_group()
 
 
+def end_to_end(codec, d, p, L, gib, world, rank, reduce_dev):
+    """North-star's PCIe-bound end-to-end figure beside the device-resident headline: the same
+    RS(10,4) encode + SHA-256 with the parts starting in page-locked host memory and parity +
+    digests landing back in it (cec_pipeline, C5's 256-part batches, 4 slots), `gib` GiB per
+    rank (weak scaling like the headline), max over ranks.  Not `value` (that is HBM-resident)."""
+    import numpy as np
+    P, depth = CONFIGS["c5"]["parts"], 4
+    n_parts = max(depth * P, int(gib * (1 << 30)) // (d * L))
+    pl = ce.Pipeline(codec, L, P, depth)
+    block = np.random.default_rng(0xE2E + rank).integers(0, 256, size=(P, d, L), dtype=np.uint8)
+    for _ in range(depth):
+        _, data = pl.acquire()
+        data[:] = block
+    for _ in range(depth):  # warmup: one batch per slot
+        slot, _ = pl.acquire()
+        pl.submit(slot, P)
+    pl.drain()
+    barrier(world)
+    t0 = time.perf_counter()
+    part = 0
+    n_batches = (n_parts + P - 1) // P
+    for _ in range(n_batches):
+        slot, data = pl.acquire()
+        n = min(P, n_parts - part)
+        data[:n, 0, :8] = np.arange(part, part + n, dtype=np.uint64).view(np.uint8).reshape(n, 8)
+        pl.submit(slot, n)
+        part += n
+    pl.drain()
+    barrier(world)
+    el = max_over_ranks(time.perf_counter() - t0, world, reduce_dev)
+    del pl
+    total = n_parts * d * L * world
+    return {"value": round(total / el / 1e9, 2), "unit": "GB/s", "bound": "pcie",
+            "stream_bytes": total, "seconds": round(el, 3),
+            "path": "page-locked host parts -> H2D -> encode_hash_kernel -> D2H parity + digests "
+                    f"(cec_pipeline, {P}-part batches, {depth} slots), {gib:g} GiB per GPU"}
+
+
 def _segments(args, cfg, shards):
     """Parts per scheduler job: every shard gets 2 batches per job; --jobs-in-flight jobs are
     queued at once (the next ones queued while the first runs: no drain bubble)."""
@@ -557,6 +595,8 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--parts", type=int, default=None, help="override parts per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--e2e-gib", type=float, default=32.0,
+                    help="c2: GiB per GPU of the PCIe-bound end-to-end figure (0 = skip)")
     ap.add_argument("--check", action="store_true", help="verify a sampled part vs the oracle")
     ap.add_argument("--stream-gib", type=float, default=1024.0,
                     help="c5: total stream size in GiB across all ranks")
@@ -827,6 +867,11 @@ def main():
             ok = ok and all(hashlib.sha256(host[j].tobytes()).digest() == dg[j].tobytes()
                             for j in range(t))
 
+    # every rank streams its own share (barriers inside): the PCIe-inclusive figure
+    e2e = None
+    if args.config == "c2" and args.e2e_gib > 0 and not args.separate:
+        e2e = end_to_end(codec, d, p, L, args.e2e_gib, world, rank, reduce_dev)
+
     if rank == 0:
         total_data = data_bytes * world
         value = total_data / step_s / 1e9
@@ -863,6 +908,8 @@ def main():
         }
         if valu is not None:
             line["valu_roofline"] = valu
+        if e2e is not None:
+            line["end_to_end"] = e2e
         if ok is not None:
             line["check_vs_oracle"] = bool(ok)
         if world == 1 and not args.no_cpu_baseline and cfg["op"] in ("encode_hash", "encode"):

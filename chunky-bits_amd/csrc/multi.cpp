@@ -273,10 +273,11 @@ struct cec_multi {
                     const size_t q = (f.first + k) * W + j;
                     const uint8_t* src = s.ptrs[k * W + j];
                     uint8_t* dst = job->out_data + q * L;
-                    if (status[k] == CEC_OK && staged) {
-                        // staging is reused by the next batch: the bytes move to the caller
-                        if (src != dst) std::memcpy(dst, src, L);
-                        src = dst;
+                    if (staged) {
+                        // staging is reused by the next batch: the bytes move to the caller (a
+                        // part that could not be decoded has no bytes: its pointers are null)
+                        if (status[k] == CEC_OK && src != dst) std::memcpy(dst, src, L);
+                        src = status[k] == CEC_OK ? dst : nullptr;
                     }
                     if (job->data_ptrs) job->data_ptrs[q] = src;
                 }

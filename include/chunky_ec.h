@@ -380,7 +380,8 @@ int cec_multi_encode_hash(cec_multi* multi, const uint8_t* data, size_t n_parts,
  * chunks with present != 0 are read), present [n][d+p], expected [n][d+p][32] -> data [n][d][L]
  * (the part bytes), verified [n][d+p], part_status [n] (CEC_OK / CEC_TOO_FEW_SHARDS_PRESENT).
  * flags = CEC_READ_REBUILT_ONLY: data receives only the rebuilt data chunks and data_ptrs[n*d]
- * (required then; optional otherwise) says where each data chunk of each part is. */
+ * (required then; optional otherwise) says where each data chunk of each part is (null for a
+ * part that is not CEC_OK when its bytes went through the scheduler's own staging). */
 int cec_multi_read(cec_multi* multi, const uint8_t* chunks, const uint8_t* present,
                    const uint8_t* expected, size_t n_parts, uint8_t* data, uint8_t* verified,
                    int* part_status, const uint8_t** data_ptrs, unsigned flags, uint64_t* job);
