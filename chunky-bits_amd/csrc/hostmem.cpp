@@ -66,10 +66,14 @@ std::string read_line(const std::string& path) {
     return line;
 }
 
-// set_mempolicy(2) without libnuma.
-constexpr int kMpolDefault = 0, kMpolPreferred = 1;
+// set_mempolicy(2) / get_mempolicy(2) without libnuma.
+constexpr int kMpolPreferred = 1;
+constexpr unsigned long kMaxNodes = 1024;  // node mask bits saved / restored
 long set_mempolicy_raw(int mode, const unsigned long* mask, unsigned long maxnode) {
     return syscall(SYS_set_mempolicy, mode, mask, maxnode);
+}
+long get_mempolicy_raw(int* mode, unsigned long* mask, unsigned long maxnode) {
+    return syscall(SYS_get_mempolicy, mode, mask, maxnode, nullptr, 0ul);
 }
 
 }  // namespace
@@ -133,15 +137,19 @@ bool bind_thread_to_device_node(int device) {
 
 hipError_t host_malloc_near(void** out, size_t bytes, unsigned flags, int device) {
     // Pages land on the device's NUMA node: prefer that node for this thread while HIP pins them
-    // (hipHostMallocNumaUser: HIP follows the thread's policy), then restore the default.
+    // (hipHostMallocNumaUser: HIP follows the thread's policy), then restore the thread's own
+    // policy (a caller under `numactl --membind` keeps it).
     const int node = device >= 0 ? device_numa_node(device) : -1;
+    constexpr size_t kWords = kMaxNodes / (8 * sizeof(unsigned long));
+    unsigned long saved_mask[kWords] = {};
+    int saved_mode = 0;
     bool policy = false;
-    if (node >= 0 && node < 64) {
+    if (node >= 0 && node < 64 && get_mempolicy_raw(&saved_mode, saved_mask, kMaxNodes) == 0) {
         const unsigned long mask = 1ul << node;
         policy = set_mempolicy_raw(kMpolPreferred, &mask, 64) == 0;
     }
     const hipError_t e = hipHostMalloc(out, bytes, flags | (policy ? hipHostMallocNumaUser : 0u));
-    if (policy) (void)set_mempolicy_raw(kMpolDefault, nullptr, 0);
+    if (policy) (void)set_mempolicy_raw(saved_mode, saved_mask, kMaxNodes);
     return e;
 }
 
