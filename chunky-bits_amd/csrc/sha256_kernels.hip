@@ -383,6 +383,145 @@ hipError_t launch_split4(const ShaParams& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------------------------------------
+// v5: the v3 split with per-pair hand-over counters in LDS instead of workgroup barriers.  A
+// rounds wave waits only for ITS producer's block (produced[pair] > b) and a producer only for
+// its slot to be consumed (consumed[pair] >= b - 1, two slots), so the four pairs of a CU no
+// longer lock-step each other at every block.  Waits spin with s_sleep and give up after
+// ~2^20 polls (a wave that gave up stops waiting and runs to its end: wrong digests, never a
+// hang); in a correct run a wait lasts at most about one block.
+// ------------------------------------------------------------------------------------------
+constexpr size_t kS5Ring = size_t(2) * 256 * kKwRow;  // words
+constexpr size_t kS5Lds = kS5Ring * 4 + 64;
+
+__device__ __forceinline__ void s5_wait_ge(const uint32_t* c, uint32_t target, bool& dead) {
+    uint32_t spins = 0;
+    while (!dead) {
+        const uint32_t v = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const volatile uint32_t*>(c));
+        if (v >= target) break;
+        if (++spins > (1u << 20)) dead = true;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ void s5_publish(uint32_t* c, uint32_t v) {
+    // this wave's ring writes / reads are done before the counter moves (LDS only: global
+    // prefetches stay in flight)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    *reinterpret_cast<volatile uint32_t*>(c) = v;
+}
+
+template <bool PRIO>
+__global__ __launch_bounds__(512) void sha256_split5_kernel(ShaParams a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s5[];
+    uint32_t* cnt = s5 + kS5Ring;  // [0, 4) produced blocks per pair, [4, 8) consumed
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t pair = wave & 3u;
+    const bool producer = wave < 4u;
+    if (threadIdx.x < 8u) cnt[threadIdx.x] = 0u;
+    __syncthreads();
+    const uint32_t slot_lane = pair * 64u + lane;
+    const uint32_t item = blockIdx.x * kS4Streams + pair * kS4Spw + lane;
+    const bool valid = lane < kS4Spw && item < a.n_parts * a.n_chunks;
+    const uint32_t src_item = valid ? item : blockIdx.x * kS4Streams;
+    const uint64_t len = a.len;
+    const uint64_t nfull = len >> 6;
+    const uint32_t rem = uint32_t(len - 64 * nfull);
+    const uint32_t tb = tail_blocks(rem);
+    const uint32_t nb = uint32_t(nfull) + tb;
+    const uint8_t* p = nullptr;
+    uint64_t dummy;
+    item_source(a, src_item, p, dummy);
+    bool dead = false;
+    if (producer) {
+        auto produce = [&](uint32_t w[16], uint32_t b) {
+            if (b >= 2) s5_wait_ge(&cnt[4 + pair], b - 1, dead);
+            uint32_t* row = &s5[((b & 1u) * 256u + slot_lane) * kKwRow];
+#pragma unroll
+            for (int i = 0; i < 64; i += 4) {
+                uint32_t v[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    v[k] = (i + k < 16 ? w[i + k] : schedule_next(w, i + k)) + kK[i + k];
+                *reinterpret_cast<uint4*>(row + i) = make_uint4(v[0], v[1], v[2], v[3]);
+            }
+            s5_publish(&cnt[pair], b + 1);
+        };
+        auto load = [&](uint4 q[4], uint64_t blk) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) q[i] = gload16(p + 64 * blk + 16 * i);
+        };
+        uint4 qa[4], qb[4];
+        const uint32_t nf = uint32_t(nfull);
+        if (nf) load(qa, 0);
+#pragma unroll 1
+        for (uint32_t b = 0; b < nf; b += 2) {
+            load(qb, min(b + 1, nf - 1));
+            {
+                uint32_t w[16];
+                block_words(qa, w);
+                produce(w, b);
+            }
+            if (b + 1 < nf) {
+                load(qa, min(b + 2, nf - 1));
+                uint32_t w[16];
+                block_words(qb, w);
+                produce(w, b + 1);
+            }
+        }
+#pragma unroll 1
+        for (uint32_t t = 0; t < tb; ++t) {
+            uint32_t w[16];
+            tail_words(p + 64 * nfull, rem, t, tb, len * 8, w);
+            produce(w, nf + t);
+        }
+    } else {
+        if (PRIO) __builtin_amdgcn_s_setprio(1);
+        uint32_t st[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) st[i] = kH0[i];
+#pragma unroll 1
+        for (uint32_t b = 0; b < nb; ++b) {
+            s5_wait_ge(&cnt[pair], b + 1, dead);
+            const uint32_t* row = &s5[((b & 1u) * 256u + slot_lane) * kKwRow];
+            uint32_t x0 = st[0], x1 = st[1], x2 = st[2], x3 = st[3];
+            uint32_t x4 = st[4], x5 = st[5], x6 = st[6], x7 = st[7];
+#pragma unroll
+            for (int i = 0; i < 64; i += 4) {
+                const uint4 v = *reinterpret_cast<const uint4*>(row + i);
+                round_split(x0, x1, x2, x3, x4, x5, x6, x7, v.x);
+                round_split(x0, x1, x2, x3, x4, x5, x6, x7, v.y);
+                round_split(x0, x1, x2, x3, x4, x5, x6, x7, v.z);
+                round_split(x0, x1, x2, x3, x4, x5, x6, x7, v.w);
+            }
+            st[0] += x0;
+            st[1] += x1;
+            st[2] += x2;
+            st[3] += x3;
+            st[4] += x4;
+            st[5] += x5;
+            st[6] += x6;
+            st[7] += x7;
+            s5_publish(&cnt[4 + pair], b + 1);
+        }
+        if (valid) finish_item(a, item, st);
+    }
+}
+
+template <bool PRIO>
+hipError_t launch_split5(const ShaParams& a, hipStream_t s) {
+    static const bool attr_ok =
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&sha256_split5_kernel<PRIO>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, int(kS5Lds)) == hipSuccess;
+    if (!attr_ok) return hipErrorInvalidValue;
+    const uint64_t total = uint64_t(a.n_parts) * a.n_chunks;
+    dim3 grid(uint32_t((total + kS4Streams - 1) / kS4Streams));
+    clear_stale_error();
+    hipLaunchKernelGGL((sha256_split5_kernel<PRIO>), grid, dim3(512), kS5Lds, s, a);
+    return hipGetLastError();
+}
+
 #endif  // CEC_AB_TOOLS
 
 // CEC_SHA_VARIANT: 1 = lane kernel, 2 = split kernel (both correct; by size when unset).  The
@@ -485,6 +624,8 @@ hipError_t launch_sha256(const ShaParams& a, bool vec16, hipStream_t s) {
     if (v == 7 && !a.present && !a.ptrs && vec16) return launch_split4<true, 1>(a, s);
     if (v == 8 && !a.present && !a.ptrs && vec16) return launch_split4<true, 2>(a, s);
     if (v == 5) return launch_lane(a, vec16, s, true);
+    if (v == 9 && !a.present && !a.ptrs && vec16) return launch_split5<false>(a, s);
+    if (v == 10 && !a.present && !a.ptrs && vec16) return launch_split5<true>(a, s);
 #else
     (void)v;
 #endif
