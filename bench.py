@@ -851,6 +851,16 @@ def main():
                 "basis": f"SHA-256: {SHA_VALU_PER_BLOCK} VALU/64-B block/lane, "
                          f"{SHA_SIMD_CYCLES:.2f} SIMD cycles/inst saturated, "
                          f"{MI355X_SIMDS} SIMDs x {MI355X_CLOCK_GHZ} GHz"}
+        # The design's own bound: one SHA wave per SIMD issues at most one VALU op per 4 cycles
+        # (MI355X_MICROARCH.md, one wave alone), and a chunk's chain is serial, so the step can
+        # take no less than blocks x ops x 4 cycles; at the nominal clock (the chip held
+        # 2.36-2.38 GHz under this load, profiles/r2f_c2_summary.md, so this reads low).
+        floor_ms = blocks * SHA_VALU_PER_BLOCK * 4 / (MI355X_CLOCK_GHZ * 1e9) * 1e3
+        if n_parts * hashed <= MI355X_SIMDS * 64:  # one SHA wave per SIMD (C2, c3r; not C4)
+            valu["lone_wave_issue_floor"] = {
+                "ms": round(floor_ms, 2), "frac": round(floor_ms / sha_ms, 4),
+                "basis": f"{blocks} blocks per chunk x {SHA_VALU_PER_BLOCK} VALU x 4 cycles per "
+                         f"instruction of one wave alone, {MI355X_CLOCK_GHZ} GHz"}
 
     ok = None
     if args.check and rank == 0 and cfg["op"] == "read":
