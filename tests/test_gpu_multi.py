@@ -337,7 +337,12 @@ def test_many_short_lived_threads_do_not_leak_device_memory():
     wave(200)
     wave(200)
     free1, _ = torch.cuda.mem_get_info()
-    assert free0 - free1 <= (1 << 20), (free0 - free1)
+    # A per-thread leak costs >= 1 MiB of staging per retired thread: >= 400 MiB over these 400
+    # threads.  What may still grow is bounded and timing-dependent: a coalescing arena whose
+    # batch gathered more callers than in the warm-up wave (<= 200 parts x 14 x 8 KiB ~ 22 MiB,
+    # in 1 MiB steps; one repeat run saw +2 MiB) and scratch buffers for a higher peak of
+    # concurrent launches (64 KiB each).
+    assert free0 - free1 <= (32 << 20), (free0 - free1)
 
 
 def test_product_build_ignores_attribution_modes(monkeypatch):
