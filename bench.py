@@ -31,7 +31,8 @@ import torch  # noqa: E402  (import before chunky_ec: one HIP runtime)
 import torch.distributed as dist  # noqa: E402
 
 import chunky_ec as ce  # noqa: E402
-from chunky_ec.sharding import barrier, dist_env, max_over_ranks, rank_seed  # noqa: E402
+from chunky_ec.sharding import (all_ranks_ok, barrier, dist_env, max_over_ranks,  # noqa: E402
+                                rank_seed)
 
 METRIC = "RS(10,4) encode+sha256 GB/s per node at 1/2/4/8 GPUs; % of HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md); 5.79 TB/s measured
@@ -253,7 +254,7 @@ def end_to_end(codec, d, p, L, gib, world, rank, reduce_dev):
         pl, err = ce.Pipeline(codec, L, P, depth), None
     except Exception as e:  # noqa: BLE001 (reported in the line)
         pl, err = None, f"{type(e).__name__}: {e}"
-    if -max_over_ranks(-(0.0 if pl is None else 1.0), world, reduce_dev) < 1.0:
+    if not all_ranks_ok(pl is not None, world, reduce_dev):
         del pl
         return {"value": None, "unit": "GB/s", "bound": "pcie",
                 "skipped": err or "another rank could not allocate its page-locked slots"}

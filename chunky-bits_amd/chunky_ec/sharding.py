@@ -28,6 +28,13 @@ def max_over_ranks(x: float, world: int, device=None) -> float:
     return float(t.item())
 
 
+def all_ranks_ok(ok: bool, world: int, device=None) -> bool:
+    """True on every rank iff `ok` holds on every rank (a collective: every rank must call it).
+    Lets the ranks skip an optional step together when one of them cannot run it, so no rank is
+    left waiting in that step's barriers."""
+    return -max_over_ranks(-(1.0 if ok else 0.0), world, device) >= 1.0
+
+
 def barrier(world: int) -> None:
     if world > 1:
         import torch.distributed as dist

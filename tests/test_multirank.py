@@ -34,7 +34,7 @@ def _part_digests(part, d, p, L):
 def _worker(rank, world, port, n_parts, out_q):
     import torch
     import torch.distributed as dist
-    from chunky_ec.sharding import barrier, max_over_ranks
+    from chunky_ec.sharding import all_ranks_ok, barrier, max_over_ranks
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -43,9 +43,12 @@ def _worker(rank, world, port, n_parts, out_q):
         res = {k: _part_digests(k, 3, 2, 257) for k in range(lo, hi)}
         barrier(world)
         t = max_over_ranks(float(rank + 1) * 0.5, world, torch.device("cpu"))
+        # bench.py's optional end-to-end step: skipped on every rank when one rank cannot run it
+        ok_all = all_ranks_ok(True, world)
+        ok_one_fails = all_ranks_ok(rank != world - 1, world)
         gathered = [None] * world
         dist.all_gather_object(gathered, res)
-        out_q.put((rank, t, gathered))
+        out_q.put((rank, t, gathered, ok_all, ok_one_fails))
     finally:
         dist.destroy_process_group()
 
@@ -74,8 +77,9 @@ def test_two_rank_gloo_sharding_matches_single_process():
         pr.join(timeout=60)
         assert pr.exitcode == 0
     single = {k: _part_digests(k, 3, 2, 257) for k in range(n_parts)}
-    for rank, t, gathered in results:
+    for rank, t, gathered, ok_all, ok_one_fails in results:
         assert t == pytest.approx(1.0)  # max over ranks of (rank+1)*0.5
+        assert ok_all and not ok_one_fails
         merged = {}
         for part_map in gathered:
             assert not (set(merged) & set(part_map))  # disjoint ownership
