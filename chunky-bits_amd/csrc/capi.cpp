@@ -918,8 +918,22 @@ struct PartReq : ReqBase {
     // Page-locked caller buffers (cec_host_alloc): DMA'd directly, no copy-in / copy-out.
     bool in_pinned = false, out_pinned = false;
     size_t out_off = 0;                 // parity offset in the pinned output staging
+    // Early upload (CEC_COALESCE_EARLY_H2D): the caller queues its own part's H2D right after its
+    // copy-in, so the uploads overlap the other callers' copies instead of following them all.
+    bool early = false;
+    uint8_t* dev_dst = nullptr;         // this part's place in the device batch
+    hipStream_t stream = nullptr;       // the batch's stream
+    hipError_t early_err = hipSuccess;
     CoalesceKey key() const { return {codec, L, device}; }
 };
+
+bool coalesce_early_h2d() {
+    static const bool on = [] {
+        const char* e = std::getenv("CEC_COALESCE_EARLY_H2D");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
 
 // Pinned layout: input [part][d][cs] (staged parts only, at in_off), output [part][p][cs]
 // (staged parts only, at out_off) then digests [part][d+p][32]; device batch [part][d+p][cs]
@@ -964,13 +978,39 @@ struct PartImpl {
         CEC_TRY(a.in.reserve(std::max<size_t>(in_bytes, 1), coalesce_max_bytes()));
         CEC_TRY(a.out.reserve(out_bytes + B * t * 32,
                               coalesce_max_bytes() / d * p + coalesce_max_bytes() / cs * t * 32));
-        return ctx_reserve(a.dev, round_up(B * t * 32, kChunkAlign) + B * t * cs);
+        CEC_TRY(ctx_reserve(a.dev, round_up(B * t * 32, kChunkAlign) + B * t * cs));
+        const bool early = coalesce_early_h2d();
+        uint8_t* dbase = a.dev.dbuf + round_up(B * t * 32, kChunkAlign);
+        for (PartReq* r : batch) {
+            r->early = early;
+            r->dev_dst = dbase + r->slot * t * cs;
+            r->stream = a.dev.stream;
+            r->early_err = hipSuccess;
+        }
+        return CEC_OK;
+    }
+    // This part's upload into the device batch (from the caller's page-locked buffer or from its
+    // copy in the pinned staging).
+    static hipError_t upload(PartReq& r) {
+        const size_t d = r.codec->d, cs = cs_of(r);
+        if (r.in_pinned && cs == r.L)
+            return hipMemcpyAsync(r.dev_dst, r.data_buf, d * r.L, hipMemcpyHostToDevice, r.stream);
+        if (r.in_pinned)
+            return hipMemcpy2DAsync(r.dev_dst, cs, r.data_buf, r.L, r.L, d, hipMemcpyHostToDevice,
+                                    r.stream);
+        return hipMemcpyAsync(r.dev_dst, r.arena->in.ptr + r.in_off, d * cs, hipMemcpyHostToDevice,
+                              r.stream);
     }
     static void copy_in(PartReq& r) {
-        if (r.in_pinned) return;
-        const size_t d = r.codec->d, cs = cs_of(r);
-        uint8_t* dst = r.arena->in.ptr + r.in_off;
-        for (size_t j = 0; j < d; ++j) std::memcpy(dst + j * cs, r.data_buf + j * r.L, r.L);
+        if (!r.in_pinned) {
+            const size_t d = r.codec->d, cs = cs_of(r);
+            uint8_t* dst = r.arena->in.ptr + r.in_off;
+            for (size_t j = 0; j < d; ++j) std::memcpy(dst + j * cs, r.data_buf + j * r.L, r.L);
+        }
+        if (r.early) {
+            r.early_err = upload(r);
+            if (r.early_err != hipSuccess) (void)hipGetLastError();
+        }
     }
     static int run(std::vector<PartReq*>& batch, Arena& a) {
         cec_codec* c = batch[0]->codec;
@@ -982,21 +1022,13 @@ struct PartImpl {
         uint8_t* ddig = a.dev.dbuf;
         uint8_t* dbase = a.dev.dbuf + round_up(B * t * 32, kChunkAlign);
         hipStream_t s = a.dev.stream;
-        if (!per_part) {
+        if (batch[0]->early) {  // every caller queued its own upload after its copy-in
+            for (const PartReq* r : batch) HIP_TRY(r->early_err);
+        } else if (!per_part) {
             HIP_TRY(hipMemcpy2DAsync(dbase, t * cs, a.in.ptr, d * cs, d * cs, B,
                                      hipMemcpyHostToDevice, s));
         } else {
-            for (const PartReq* r : batch) {
-                uint8_t* dst = dbase + r->slot * t * cs;
-                if (r->in_pinned && cs == L)  // the caller's data_buf, straight
-                    HIP_TRY(hipMemcpyAsync(dst, r->data_buf, d * L, hipMemcpyHostToDevice, s));
-                else if (r->in_pinned)  // d rows of L bytes into the padded chunk stride
-                    HIP_TRY(hipMemcpy2DAsync(dst, cs, r->data_buf, r->L, r->L, d,
-                                             hipMemcpyHostToDevice, s));
-                else
-                    HIP_TRY(hipMemcpyAsync(dst, a.in.ptr + r->in_off, d * cs,
-                                           hipMemcpyHostToDevice, s));
-            }
+            for (PartReq* r : batch) HIP_TRY(upload(*r));  // pinned ones straight from the caller
         }
         if (fused_covers(uint32_t(d), uint32_t(p), L) && prefer_fused(B * t)) {
             FusedParams f{};
