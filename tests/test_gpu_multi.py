@@ -591,3 +591,18 @@ def test_read_pipeline_resilver_flag_vs_oracle():
         want = [data[k, j] for j in range(d)] + par
         for i in range(t):
             assert ctypes.string_at(ptrs[k * t + i], L) == want[i].tobytes(), (k, i)
+
+
+@pytest.mark.parametrize("knobs", [{"CEC_READ_SIDE": "1"}, {"CEC_READ_UPSTREAM": "1"},
+                                   {"CEC_READ_SIDE": "1", "CEC_READ_UPSTREAM": "1"}])
+def test_read_pipeline_stream_knobs_bit_exact(monkeypatch, knobs):
+    """The read pipeline's A/B stream layouts (decode + rebuilt downloads on a side stream; every
+    upload on one shared stream; both) are in the product library: read, packed read and
+    resilver batches under each must give the default's results (oracle / written bytes)."""
+    import test_gpu_parity as tp
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)  # read when a pipeline is created
+    for flags in (0, ce.ReadPipeline.REBUILT_ONLY):
+        tp.test_read_pipeline_matches_read_with_context(10, 4, 4096, 12, 3, 5, flags)
+        tp.test_read_pipeline_packed_submit(10, 4, 4096, 12, 3, 5, flags, True)
+    test_read_pipeline_resilver_flag_vs_oracle()
