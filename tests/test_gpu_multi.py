@@ -305,6 +305,21 @@ def test_per_call_mixed_pinned_and_pageable_callers_bit_exact():
     assert l1 - l0 < c1 - c0
 
 
+def test_per_call_early_upload_knob_bit_exact():
+    """CEC_COALESCE_EARLY_H2D=1 (every caller queues its own part's upload after its copy-in) is
+    read once per process, so the mixed pinned / pageable per-call case runs in a child process
+    with it set."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = ("import sys; sys.path.insert(0, %r); import conftest, torch, test_gpu_multi as m; "
+            "m.test_per_call_mixed_pinned_and_pageable_callers_bit_exact(); print('ok')" % here)
+    env = dict(os.environ, CEC_COALESCE_EARLY_H2D="1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
+
+
 # ----------------------------------------------------------------------------------------------
 # Long-running host: pooled staging, no per-thread leaks, product build ignores A/B modes
 # ----------------------------------------------------------------------------------------------
