@@ -582,7 +582,19 @@ struct PinnedBuf {
 struct Arena {
     StageCtx dev;  // stream + device staging
     PinnedBuf in, out;
+    // CEC_COALESCE_EARLY_D2H: the parity comes back on a side stream as soon as the encode is
+    // done, beside the SHA-256 chains (made on first use; arenas live as long as the process)
+    hipStream_t side = nullptr;
+    hipEvent_t encoded = nullptr, parity_down = nullptr;
 };
+
+bool coalesce_early_d2h() {  // default on (profiles/r2_early_d2h/); =0 for A/B
+    static const bool on = [] {
+        const char* e = std::getenv("CEC_COALESCE_EARLY_D2H");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
 
 struct CoalesceKey {
     const void* codec;
@@ -1030,6 +1042,35 @@ struct PartImpl {
         } else {
             for (PartReq* r : batch) HIP_TRY(upload(*r));  // pinned ones straight from the caller
         }
+        // the parity of every part back to its caller (or the staging) on stream `q`
+        auto parity_down = [&](hipStream_t q) -> int {
+            if (!per_part) {
+                HIP_TRY(hipMemcpy2DAsync(a.out.ptr, p * cs, dbase + d * cs, t * cs, p * cs, B,
+                                         hipMemcpyDeviceToHost, q));
+                return CEC_OK;
+            }
+            for (const PartReq* r : batch) {
+                const uint8_t* src = dbase + r->slot * t * cs + d * cs;
+                if (r->out_pinned && cs == L)  // straight into the caller's parity buffer
+                    HIP_TRY(hipMemcpyAsync(r->parity_out, src, p * L, hipMemcpyDeviceToHost, q));
+                else if (r->out_pinned)  // p rows of L bytes out of the padded chunk stride
+                    HIP_TRY(hipMemcpy2DAsync(r->parity_out, r->L, src, cs, r->L, p,
+                                             hipMemcpyDeviceToHost, q));
+                else
+                    HIP_TRY(hipMemcpyAsync(a.out.ptr + r->out_off, src, p * cs,
+                                           hipMemcpyDeviceToHost, q));
+            }
+            return CEC_OK;
+        };
+        bool parity_sent = false;
+        // an error return after the side-stream download was queued must not leave it writing
+        // into the callers' buffers: wait for it on every exit
+        struct SideWait {
+            hipStream_t q = nullptr;
+            ~SideWait() {
+                if (q) (void)hipStreamSynchronize(q);
+            }
+        } side_wait;
         if (fused_covers(uint32_t(d), uint32_t(p), L) && prefer_fused(B * t)) {
             FusedParams f{};
             f.base = dbase;
@@ -1053,6 +1094,18 @@ struct PartImpl {
             ap.d = uint32_t(d);
             ap.n_rows = uint32_t(p);
             HIP_TRY(launch_rs_apply(ap, true, s));
+            if (coalesce_early_d2h()) {  // parity down beside the SHA-256 chains (both only read)
+                if (!a.side) HIP_TRY(hipStreamCreateWithFlags(&a.side, hipStreamNonBlocking));
+                if (!a.encoded) HIP_TRY(hipEventCreateWithFlags(&a.encoded, hipEventDisableTiming));
+                if (!a.parity_down)
+                    HIP_TRY(hipEventCreateWithFlags(&a.parity_down, hipEventDisableTiming));
+                HIP_TRY(hipEventRecord(a.encoded, s));
+                HIP_TRY(hipStreamWaitEvent(a.side, a.encoded, 0));
+                side_wait.q = a.side;
+                CEC_TRY(parity_down(a.side));
+                HIP_TRY(hipEventRecord(a.parity_down, a.side));
+                parity_sent = true;
+            }
             ShaParams h{};
             h.base = dbase;
             h.part_stride = t * cs;
@@ -1065,22 +1118,8 @@ struct PartImpl {
             HIP_TRY(launch_sha256(h, true, s));
         }
         const size_t dig0 = batch[0]->item0;
-        if (!per_part) {
-            HIP_TRY(hipMemcpy2DAsync(a.out.ptr, p * cs, dbase + d * cs, t * cs, p * cs, B,
-                                     hipMemcpyDeviceToHost, s));
-        } else {
-            for (const PartReq* r : batch) {
-                const uint8_t* src = dbase + r->slot * t * cs + d * cs;
-                if (r->out_pinned && cs == L)  // straight into the caller's parity buffer
-                    HIP_TRY(hipMemcpyAsync(r->parity_out, src, p * L, hipMemcpyDeviceToHost, s));
-                else if (r->out_pinned)  // p rows of L bytes out of the padded chunk stride
-                    HIP_TRY(hipMemcpy2DAsync(r->parity_out, r->L, src, cs, r->L, p,
-                                             hipMemcpyDeviceToHost, s));
-                else
-                    HIP_TRY(hipMemcpyAsync(a.out.ptr + r->out_off, src, p * cs,
-                                           hipMemcpyDeviceToHost, s));
-            }
-        }
+        if (parity_sent) HIP_TRY(hipStreamWaitEvent(s, a.parity_down, 0));
+        else CEC_TRY(parity_down(s));
         HIP_TRY(hipMemcpyAsync(a.out.ptr + dig0, ddig, B * t * 32, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         return CEC_OK;
