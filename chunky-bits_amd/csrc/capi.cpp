@@ -585,7 +585,7 @@ struct Arena {
     // CEC_COALESCE_EARLY_D2H: the parity comes back on a side stream as soon as the encode is
     // done, beside the SHA-256 chains (made on first use; arenas live as long as the process)
     hipStream_t side = nullptr;
-    hipEvent_t encoded = nullptr, parity_down = nullptr;
+    hipEvent_t encoded = nullptr;
 };
 
 bool coalesce_early_d2h() {  // default on (profiles/r2_early_d2h/); =0 for A/B
@@ -678,8 +678,13 @@ class Coalescer {
                 r->phase = Phase::Finished;
                 if (++r->batch->finished == r->batch->size) r->batch->cv.notify_one();
                 break;
-            } else if (r->phase == Phase::Queued && !gathering_ &&
+            } else if (r->phase == Phase::Queued && r->batch == nullptr && !gathering_ &&
                        (active_ == 0 || (overflow_ && active_ < coalesce_inflight()))) {
+                // r->batch: a caller already taken into a batch stays Queued until its leader
+                // has prepared the arena (lock released meanwhile); woken in that window (a
+                // wake-up sent before the batch formed) it must not lead a batch of its own, or
+                // it never copies in and its leader waits forever — seen with two batches in
+                // flight at 256 pageable callers.
                 lead(r, lk);
                 break;
             } else {
@@ -759,11 +764,16 @@ class Coalescer {
         }
         Arena* arena = take_arena(key.device);
         gathering_ = false;
+        if (coalesce_trace())
+            std::fprintf(stderr, "[cec coalesce] lead arena %p: %zu callers, %u active, %zu queued\n",
+                         (void*)arena, batch.size(), active_, queue_.size());
         wake_next();  // the next batch can gather while this one runs
         lk.unlock();
         const auto t0 = std::chrono::steady_clock::now();
         auto t1 = t0, t2 = t0, t3 = t0;
         int st = Impl::prepare(batch, *arena);
+        if (coalesce_trace())
+            std::fprintf(stderr, "[cec coalesce] arena %p: prepared (%d)\n", (void*)arena, st);
         if (st == CEC_OK) {
             lk.lock();
             batch_state.staged = 1;  // the leader's own copy, done below
@@ -778,6 +788,8 @@ class Coalescer {
             lk.lock();
             batch_state.cv.wait(lk, [&] { return batch_state.staged == batch_state.size; });
             lk.unlock();
+            if (coalesce_trace())
+                std::fprintf(stderr, "[cec coalesce] arena %p: staged\n", (void*)arena);
             t2 = std::chrono::steady_clock::now();
             g_launches.fetch_add(1, std::memory_order_relaxed);
             st = Impl::run(batch, *arena);
@@ -1094,17 +1106,11 @@ struct PartImpl {
             ap.d = uint32_t(d);
             ap.n_rows = uint32_t(p);
             HIP_TRY(launch_rs_apply(ap, true, s));
-            if (coalesce_early_d2h()) {  // parity down beside the SHA-256 chains (both only read)
+            const bool early = coalesce_early_d2h();
+            if (early) {
                 if (!a.side) HIP_TRY(hipStreamCreateWithFlags(&a.side, hipStreamNonBlocking));
                 if (!a.encoded) HIP_TRY(hipEventCreateWithFlags(&a.encoded, hipEventDisableTiming));
-                if (!a.parity_down)
-                    HIP_TRY(hipEventCreateWithFlags(&a.parity_down, hipEventDisableTiming));
                 HIP_TRY(hipEventRecord(a.encoded, s));
-                HIP_TRY(hipStreamWaitEvent(a.side, a.encoded, 0));
-                side_wait.q = a.side;
-                CEC_TRY(parity_down(a.side));
-                HIP_TRY(hipEventRecord(a.parity_down, a.side));
-                parity_sent = true;
             }
             ShaParams h{};
             h.base = dbase;
@@ -1116,12 +1122,24 @@ struct PartImpl {
             h.n_chunks = uint32_t(t);
             h.digests = ddig;
             HIP_TRY(launch_sha256(h, true, s));
+            if (early) {
+                // Parity down beside the SHA-256 chains (both only read the batch).  The host
+                // waits for the encode and only then queues the download: no stream waits on
+                // another stream's event, since with more streams than the process's hardware
+                // queues (GPU_MAX_HW_QUEUES) two streams can share a queue, and cross-stream
+                // waits in shared in-order queues can wait on each other (a 256-caller run
+                // hung with the device-side form).
+                HIP_TRY(hipEventSynchronize(a.encoded));
+                side_wait.q = a.side;
+                CEC_TRY(parity_down(a.side));
+                parity_sent = true;
+            }
         }
         const size_t dig0 = batch[0]->item0;
-        if (parity_sent) HIP_TRY(hipStreamWaitEvent(s, a.parity_down, 0));
-        else CEC_TRY(parity_down(s));
+        if (!parity_sent) CEC_TRY(parity_down(s));
         HIP_TRY(hipMemcpyAsync(a.out.ptr + dig0, ddig, B * t * 32, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
+        if (parity_sent) HIP_TRY(hipStreamSynchronize(a.side));
         return CEC_OK;
     }
     static void copy_out(PartReq& r) {

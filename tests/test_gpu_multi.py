@@ -320,6 +320,45 @@ def test_per_call_early_upload_knob_bit_exact():
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
 
 
+def _overflow_callers_child():
+    """Run in a child with a small CEC_COALESCE_MAX_MIB: 48 pageable callers x 4 calls, so
+    nearly every batch overflows the cap and two batches are in flight over and over."""
+    from concurrent.futures import ThreadPoolExecutor
+    d, p, L = 10, 4, 65536
+    rs = ce.ReedSolomon(d, p)
+
+    def task(i):
+        src = gen_bytes(9000 + i, d * L)
+        _, ref, rdig = oracle.part_encode(d, p, src, d * L)
+        for _ in range(4):
+            ep = ce.part_encode(rs, src.tobytes(), d * L)
+            assert b"".join(ep.parity) == np.asarray(ref).tobytes(), i
+            assert [str(h) for h in ep.hashes] == [bytes(x).hex() for x in np.asarray(rdig)], i
+        return i
+
+    c0, l0 = ce.coalesce_stats()
+    with ThreadPoolExecutor(max_workers=48) as ex:
+        assert sorted(ex.map(task, range(48))) == list(range(48))
+    c1, l1 = ce.coalesce_stats()
+    assert c1 - c0 == 192 and l1 - l0 > 192 // 8
+
+
+def test_per_call_two_batches_in_flight_never_strand_a_caller():
+    """Regression: with two batches in flight (the overflow rule), a caller already taken into
+    a batch that was woken before the batch formed once led a batch of its own, so its first
+    leader waited forever for its copy-in (percall_bench, 256 pageable callers).  A child
+    process with a 2 MiB batch cap overflows on nearly every batch; it must finish, bit-exact."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = ("import sys; sys.path.insert(0, %r); import conftest, torch, test_gpu_multi as m; "
+            "m._overflow_callers_child(); print('ok')" % here)
+    env = dict(os.environ, CEC_COALESCE_MAX_MIB="2")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
+
+
 # ----------------------------------------------------------------------------------------------
 # Long-running host: pooled staging, no per-thread leaks, product build ignores A/B modes
 # ----------------------------------------------------------------------------------------------
