@@ -206,3 +206,27 @@ def test_verify_resilver_verify_mode_switches(devices):
     windows(lambda at, c: m.verify_sync(chunks.view(n, t, L)[at:at + c], present[at:at + c].copy(),
                                         dig[at:at + c].copy(), c, ver3[at:at + c]))
     assert ver3.all()
+
+
+def test_concurrent_read_batches_on_many_streams():
+    """16 host threads call cec_read_batch at once, each on its own stream (each read forks its
+    speculative decode onto a pooled side stream and joins it back): many more streams than
+    the process's hardware queues, cross-stream event waits in flight together.  Every read
+    rebuilds its parts bit-exact and none waits forever (tools/stress_read_batch.py, the same
+    at 48 threads)."""
+    import os
+    import sys
+    import types
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "tools"))
+    import stress_read_batch as srb
+    import threading
+    errors = []
+    args = types.SimpleNamespace(iters=5)
+    ths = [threading.Thread(target=srb.worker, args=(i, args, errors)) for i in range(16)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join(timeout=100)
+    assert not any(th.is_alive() for th in ths), "a read never finished"
+    assert not errors, errors
