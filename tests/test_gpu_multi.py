@@ -343,6 +343,48 @@ def _overflow_callers_child():
     assert c1 - c0 == 192 and l1 - l0 > 192 // 8
 
 
+def _mixed_keys_child():
+    """Child with a small batch cap: callers of three coalescing keys at once (RS(10,4) at
+    64 KiB chunks, RS(3,2) at 683-byte chunks, and plain SHA-256 of odd lengths), so batches of
+    one key overflow while callers of the others wait behind them."""
+    import hashlib
+    from concurrent.futures import ThreadPoolExecutor
+    codecs = {(10, 4): ce.ReedSolomon(10, 4), (3, 2): ce.ReedSolomon(3, 2)}
+
+    def task(i):
+        kind = i % 3
+        for it in range(3):
+            if kind == 2:
+                buf = gen_bytes(11000 + 7 * i + it, 1000 + 37 * i)
+                h = ce.Sha256Hash.from_buf(buf.tobytes())
+                assert str(h) == hashlib.sha256(buf.tobytes()).hexdigest(), i
+                continue
+            d, p, L = (10, 4, 65536) if kind == 0 else (3, 2, 683)
+            src = gen_bytes(12000 + 7 * i + it, d * L)
+            ep = ce.part_encode(codecs[(d, p)], src.tobytes(), d * L)
+            _, ref, rdig = oracle.part_encode(d, p, src, d * L)
+            assert b"".join(ep.parity) == np.asarray(ref).tobytes(), i
+            assert [str(h) for h in ep.hashes] == [bytes(x).hex() for x in np.asarray(rdig)], i
+        return i
+
+    with ThreadPoolExecutor(max_workers=60) as ex:
+        assert sorted(ex.map(task, range(60))) == list(range(60))
+
+
+def test_per_call_mixed_keys_under_overflow():
+    """Three coalescing keys at once under a 1 MiB batch cap (child process): every caller
+    finishes with its own bit-exact result."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = ("import sys; sys.path.insert(0, %r); import conftest, torch, test_gpu_multi as m; "
+            "m._mixed_keys_child(); print('ok')" % here)
+    env = dict(os.environ, CEC_COALESCE_MAX_MIB="1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
+
+
 def test_per_call_two_batches_in_flight_never_strand_a_caller():
     """Regression: with two batches in flight (the overflow rule), a caller already taken into
     a batch that was woken before the batch formed once led a batch of its own, so its first
