@@ -230,3 +230,43 @@ def test_concurrent_read_batches_on_many_streams():
         th.join(timeout=100)
     assert not any(th.is_alive() for th in ths), "a read never finished"
     assert not errors, errors
+
+
+def test_scheduler_jobs_from_many_threads():
+    """8 host threads submit and wait for their own write jobs on ONE scheduler (two shards on
+    cuda:0) at the same time, pageable and page-locked buffers mixed: every job gets its own
+    parts' parity and digests (the scheduler's job queue and completion are shared)."""
+    import threading
+    d, p, L = 10, 4, 4096
+    t = d + p
+    rs = ce.ReedSolomon(d, p)
+    m = ce.Multi(rs, L, 4, 2, [0, 0])
+    errors = []
+
+    def worker(w):
+        try:
+            for it in range(4):
+                n = 5 + (w + it) % 7
+                data, dig_ref = _parts(d, p, L, n, 300 + 10 * w + it)
+                if (w + it) % 2:
+                    hb = [ce.HostBuffer(n * d * L), ce.HostBuffer(n * p * L),
+                          ce.HostBuffer(n * t * 32)]
+                    src, par, dg = hb[0].view(n, d, L), hb[1].view(n, p, L), hb[2].view(n, t, 32)
+                    src[:] = data[:, :d]
+                else:
+                    src = np.ascontiguousarray(data[:, :d])
+                    par = np.zeros((n, p, L), np.uint8)
+                    dg = np.zeros((n, t, 32), np.uint8)
+                m.wait(m.encode_hash(src, n, par, dg))
+                assert np.array_equal(par, data[:, d:]), (w, it)
+                assert np.array_equal(dg, dig_ref), (w, it)
+        except Exception as e:  # noqa: BLE001
+            errors.append(f"{w}: {e!r}")
+
+    ths = [threading.Thread(target=worker, args=(w,)) for w in range(8)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join(timeout=100)
+    assert not any(th.is_alive() for th in ths), "a job never finished"
+    assert not errors, errors
