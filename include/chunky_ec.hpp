@@ -26,12 +26,15 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <limits>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <optional>
 #include <stdexcept>
 #include <string>
@@ -464,8 +467,11 @@ struct FilePart {
     // write_with_encoder (file_part.rs:137-225): L = ceil(length/d); data chunk j =
     // data_buf[L*j .. L*(j+1)] (data_buf zero padded to d*L, writer.rs:172); parity from
     // encode_sep; every chunk hashed, in order, and written to `dest` under its hash.
+    // dest_mu (optional): held while the chunks go into `dest` (several parts written at once,
+    // FileWriteBuilder::concurrency); the GPU work runs outside it.
     static FilePart write_with_encoder(const ReedSolomon& encoder, ChunkStore& dest,
-                                       const Bytes& data_buf, size_t length) {
+                                       const Bytes& data_buf, size_t length,
+                                       std::mutex* dest_mu = nullptr) {
         const size_t d = encoder.data_shard_count(), p = encoder.parity_shard_count();
         if (length > data_buf.size()) throw std::invalid_argument("length > data_buf.len()");
         const size_t L = (length + d - 1) / d;
@@ -477,6 +483,8 @@ struct FilePart {
                                       digests.data(), &chunksize));
         FilePart part;
         part.chunksize = chunksize;
+        std::unique_lock<std::mutex> lk;
+        if (dest_mu) lk = std::unique_lock<std::mutex>(*dest_mu);
         for (size_t i = 0; i < d + p; ++i) {
             std::array<uint8_t, 32> h{};
             std::memcpy(h.data(), &digests[32 * i], 32);
@@ -941,6 +949,14 @@ class FileWriteBuilder {
         parity_ = n;
         return *this;
     }
+    // Part tasks in flight for the per-part path (writer.rs:106-110 `concurrency`, default 10,
+    // semaphore at :130; write() requires > 1 like writer.rs:128): that many parts are encoded
+    // and hashed at once, so their per-call GPU work shares coalesced launches (DESIGN.md §4.7:
+    // raise it to >= 64 for the swap to pay).  Parts still come out in file order.
+    FileWriteBuilder& concurrency(size_t n) {
+        concurrency_ = n;
+        return *this;
+    }
 
     // Parts per batch and batches in flight per device for the batched path (the multi-GPU
     // scheduler, cec_multi); 0 = one write_with_encoder call per part (the reference's shape).
@@ -956,6 +972,7 @@ class FileWriteBuilder {
     }
 
     FileReference write(const uint8_t* bytes, size_t n, ChunkStore& dest) const {
+        if (concurrency_ <= 1) throw std::invalid_argument("concurrency must be > 1");  // :128
         const ReedSolomon encoder(data_, parity_);  // writer.rs:131
         FileReference file;
         const size_t part_cap = data_ * chunk_size_;
@@ -965,11 +982,38 @@ class FileWriteBuilder {
             write_full_parts(encoder, bytes, full, dest, file);
             off = full * part_cap;
         }
-        for (; off < n; off += part_cap) {
-            const size_t bytes_read = std::min(part_cap, n - off);
+        std::vector<size_t> offs;
+        for (; off < n; off += part_cap) offs.push_back(off);
+        auto one_part = [&](size_t k, std::mutex* mu) {
+            const size_t bytes_read = std::min(part_cap, n - offs[k]);
             Bytes data_buf(part_cap, 0);  // vec![0; data * chunk_size] (writer.rs:172)
-            std::memcpy(data_buf.data(), bytes + off, bytes_read);
-            file.parts.push_back(FilePart::write_with_encoder(encoder, dest, data_buf, bytes_read));
+            std::memcpy(data_buf.data(), bytes + offs[k], bytes_read);
+            return FilePart::write_with_encoder(encoder, dest, data_buf, bytes_read, mu);
+        };
+        const size_t workers = std::min(concurrency_, offs.size());
+        if (workers <= 1) {
+            for (size_t k = 0; k < offs.size(); ++k) file.parts.push_back(one_part(k, nullptr));
+        } else {  // `workers` part tasks at once (writer.rs:200-210), results in file order
+            std::vector<FilePart> parts(offs.size());
+            std::mutex dest_mu, err_mu;
+            std::atomic<size_t> next{0};
+            std::exception_ptr err;
+            auto task = [&] {
+                for (size_t k; (k = next.fetch_add(1)) < offs.size();) {
+                    try {
+                        parts[k] = one_part(k, &dest_mu);
+                    } catch (...) {  // the first failure is the write's; stop taking parts
+                        std::lock_guard<std::mutex> lk(err_mu);
+                        if (!err) err = std::current_exception();
+                        next.store(offs.size());
+                    }
+                }
+            };
+            std::vector<std::thread> pool;
+            for (size_t w = 0; w < workers; ++w) pool.emplace_back(task);
+            for (auto& th : pool) th.join();
+            if (err) std::rethrow_exception(err);
+            for (auto& part : parts) file.parts.push_back(std::move(part));
         }
         file.length = n;
         return file;
@@ -995,6 +1039,7 @@ class FileWriteBuilder {
     size_t parity_ = 2;
     size_t batch_ = 0;
     size_t depth_ = 4;
+    size_t concurrency_ = 10;  // the reference's default (writer.rs:56)
     std::vector<int> devices_;
 
     // The `full` parts of d*chunk_size bytes through the multi-GPU scheduler, in windows of

@@ -197,6 +197,35 @@ void test_cp_50mib() {
     CHECK(f.read(store) == input);
 }
 
+// FileWriteBuilder::concurrency (writer.rs:106-130): 2 and 64 part tasks at once give the
+// same FileParts, in file order, and the same stored chunks as the default 10; 1 is refused like
+// the reference's assert.
+void test_write_concurrency() {
+    const size_t length = size_t(40) << 20;
+    const Bytes input = random_bytes(length, 77);
+    const auto b = FileWriteBuilder().chunk_size(size_t(1) << 18).data_chunks(10).parity_chunks(4);
+    ChunkStore s10, s2, s64;
+    const FileReference f10 = FileWriteBuilder(b).write(input, s10);
+    const FileReference f2 = FileWriteBuilder(b).concurrency(2).write(input, s2);
+    const FileReference f64 = FileWriteBuilder(b).concurrency(64).write(input, s64);
+    CHECK(f10.parts.size() == 16 && f2.parts.size() == 16 && f64.parts.size() == 16);
+    for (size_t k = 0; k < f10.parts.size(); ++k)
+        for (size_t i = 0; i < 14; ++i) {
+            CHECK(f10.parts[k].chunk(i).hash == f2.parts[k].chunk(i).hash);
+            CHECK(f10.parts[k].chunk(i).hash == f64.parts[k].chunk(i).hash);
+        }
+    CHECK(s10.size() == s2.size() && s10.size() == s64.size());
+    CHECK(f64.read(s64) == input);
+    bool refused = false;
+    try {
+        ChunkStore s1;
+        FileWriteBuilder(b).concurrency(1).write(input, s1);
+    } catch (const std::invalid_argument&) {
+        refused = true;
+    }
+    CHECK(refused);
+}
+
 // The host-staged pipelines behind FileWriteBuilder::batch and FileReference::read(src, n):
 // identical FileParts, identical stored chunks, identical bytes read back (with holes).
 void test_batched_paths() {
@@ -466,6 +495,7 @@ const Test kTests[] = {
     {"test_resilver", test_resilver},
     {"test_cluster_digests", test_cluster_digests},
     {"test_cp_50mib", test_cp_50mib},
+    {"test_write_concurrency", test_write_concurrency},
     {"test_batched_paths", test_batched_paths},
     {"test_multi_device_paths", test_multi_device_paths},
     {"test_mixed_shape_read", test_mixed_shape_read},
