@@ -30,7 +30,9 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <exception>
+#include <future>
 #include <limits>
 #include <map>
 #include <memory>
@@ -284,6 +286,22 @@ class PinnedBuf {
     size_t cap_ = 0;
 };
 
+// fn(k) for k in [0, n) with at most `window` calls in flight, sink(k, result) in order of k —
+// the reference's `buffered(window)` / FuturesOrdered over part futures.  A call's exception
+// reaches the caller at its turn (the calls still in flight finish first).
+template <typename Fn, typename Sink>
+void ordered_concurrent(size_t n, size_t window, Fn fn, Sink sink) {
+    using R = decltype(fn(size_t(0)));
+    std::deque<std::future<R>> q;
+    size_t next = 0, done = 0;
+    window = std::max<size_t>(window, 1);
+    while (done < n) {
+        while (next < n && q.size() < window) q.push_back(std::async(std::launch::async, fn, next++));
+        sink(done++, q.front().get());
+        q.pop_front();
+    }
+}
+
 inline std::vector<int> devices_or_current(const std::vector<int>& devices) {
     if (!devices.empty()) return devices;
     int dev = 0;
@@ -521,14 +539,18 @@ struct FilePart {
 
     // resilver (file_part.rs:253-390): verify, reconstruct every missing/invalid chunk (data
     // and parity) and write it back under its hash.  Rebuilt chunks report Resilvered.
-    PartReport resilver(ChunkStore& dest) const {
+    // dest_mu (optional): held while reading from and writing to `dest` (several parts resilvered
+    // at once, FileReference::resilver); the GPU work runs outside it.
+    PartReport resilver(ChunkStore& dest, std::mutex* dest_mu = nullptr) const {
         PartReport rep;
-        Shards all = load_verified(dest, &rep);
+        Shards all = load_verified(dest, &rep, dest_mu);
         bool any_missing = false;
         for (const auto& s : all) any_missing = any_missing || !s;
         if (!any_missing) return rep;
         const ReedSolomon r(data.size(), parity.size());
         r.reconstruct(all);
+        std::unique_lock<std::mutex> lk;
+        if (dest_mu) lk = std::unique_lock<std::mutex>(*dest_mu);
         for (size_t i = 0; i < all.size(); ++i) {
             if (rep.chunks[i] == LocationIntegrity::Valid) continue;
             dest.write_shard(chunk(i).hash, *all[i]);
@@ -540,13 +562,18 @@ struct FilePart {
     const Chunk& chunk(size_t i) const { return i < data.size() ? data[i] : parity[i - data.size()]; }
 
    private:
-    Shards load_verified(const ChunkStore& src, PartReport* rep) const {
+    Shards load_verified(const ChunkStore& src, PartReport* rep,
+                         std::mutex* src_mu = nullptr) const {
         const size_t t = data.size() + parity.size();
         Shards all(t);
         std::vector<const Bytes*> loaded;
         std::vector<size_t> idx;
+        {
+            std::unique_lock<std::mutex> lk;
+            if (src_mu) lk = std::unique_lock<std::mutex>(*src_mu);
+            for (size_t i = 0; i < t; ++i) all[i] = src.read(chunk(i).hash);
+        }
         for (size_t i = 0; i < t; ++i) {
-            all[i] = src.read(chunk(i).hash);
             if (all[i]) {
                 loaded.push_back(&*all[i]);
                 idx.push_back(i);
@@ -570,6 +597,10 @@ struct FileReference {
     friend void release_thread_buffers();
     std::optional<uint64_t> length;
     std::vector<FilePart> parts;
+    // Part futures in flight on the per-part paths, as the reference: FileReadBuilder's default
+    // buffer (reader.rs), verify's FuturesOrdered over every part (capped here at 64 threads),
+    // resilver's buffered(10).
+    static constexpr size_t kReadBuffer = 5, kVerifyBuffer = 64, kResilverBuffer = 10;
 
     // FileReference::read: every part's data, truncated to `length` (file_reference.rs:49-56).
     // parts_per_batch > 0: runs of parts of one shape go through the multi-GPU scheduler
@@ -609,6 +640,12 @@ struct FileReference {
             if (m) sink(p, m);
             left -= m;
         };
+        if (!parts_per_batch) {  // FileReadBuilder: part reads buffered(5) (reader.rs:63)
+            detail::ordered_concurrent(
+                parts.size(), kReadBuffer, [&](size_t k) { return parts[k].read_with_context(src); },
+                [&](size_t, const Bytes& b) { emit(b.data(), b.size()); });
+            return;
+        }
         size_t k = 0;
         while (k < parts.size()) {
             size_t run = 1;
@@ -637,6 +674,12 @@ struct FileReference {
     std::vector<PartReport> verify(const ChunkStore& src, size_t parts_per_batch = 0,
                                    size_t depth = 4, const std::vector<int>& devices = {}) const {
         std::vector<PartReport> r(parts.size());
+        if (!parts_per_batch) {  // every part at once (FuturesOrdered, file_reference.rs:78-86)
+            detail::ordered_concurrent(
+                parts.size(), kVerifyBuffer, [&](size_t k) { return parts[k].verify(src); },
+                [&](size_t k, PartReport rep) { r[k] = std::move(rep); });
+            return r;
+        }
         for_runs(parts_per_batch, [&](size_t k0, size_t n) {
             if (n < 2) r[k0] = parts[k0].verify(src);
             else check_run(const_cast<ChunkStore&>(src), k0, n, parts_per_batch, depth, devices,
@@ -647,6 +690,14 @@ struct FileReference {
     std::vector<PartReport> resilver(ChunkStore& dest, size_t parts_per_batch = 0,
                                      size_t depth = 4, const std::vector<int>& devices = {}) const {
         std::vector<PartReport> r(parts.size());
+        if (!parts_per_batch) {  // buffered(10) (file_reference.rs:103-110)
+            std::mutex dest_mu;
+            detail::ordered_concurrent(
+                parts.size(), kResilverBuffer,
+                [&](size_t k) { return parts[k].resilver(dest, &dest_mu); },
+                [&](size_t k, PartReport rep) { r[k] = std::move(rep); });
+            return r;
+        }
         for_runs(parts_per_batch, [&](size_t k0, size_t n) {
             if (n < 2) r[k0] = parts[k0].resilver(dest);
             else check_run(dest, k0, n, parts_per_batch, depth, devices, true, r);
