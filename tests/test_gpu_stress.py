@@ -270,3 +270,76 @@ def test_scheduler_jobs_from_many_threads():
         th.join(timeout=100)
     assert not any(th.is_alive() for th in ths), "a job never finished"
     assert not errors, errors
+
+
+def test_mixed_workload_in_one_process():
+    """Every tier at once in one process: a scheduler write stream (two shards on cuda:0), 24
+    per-call part_encode callers, 6 threads of device-batch reads on their own streams and a
+    read pipeline — each checked bit-exact, none left waiting."""
+    import os
+    import sys
+    import threading
+    import types
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "tools"))
+    import stress_read_batch as srb
+    d, p, L = 10, 4, 8192
+    t = d + p
+    rs = ce.ReedSolomon(d, p)
+    errors = []
+
+    def guard(fn, name):
+        def run():
+            try:
+                fn()
+            except Exception as e:  # noqa: BLE001
+                errors.append(f"{name}: {e!r}")
+        return run
+
+    def scheduler_stream():
+        m = ce.Multi(rs, L, 4, 2, [0, 0])
+        for it in range(6):
+            n = 9 + it
+            full, dig_ref = _parts(d, p, L, n, 700 + it)
+            src = np.ascontiguousarray(full[:, :d])
+            par = np.zeros((n, p, L), np.uint8)
+            dg = np.zeros((n, t, 32), np.uint8)
+            m.wait(m.encode_hash(src, n, par, dg))
+            assert np.array_equal(par, full[:, d:]) and np.array_equal(dg, dig_ref), it
+
+    def per_call(i):
+        def run():
+            src = np.random.default_rng(900 + i).integers(0, 256, d * L, dtype=np.uint8)
+            _, ref, _ = oracle.part_encode(d, p, src, d * L)
+            for _ in range(3):
+                ep = ce.part_encode(rs, src.tobytes(), d * L)
+                assert b"".join(ep.parity) == np.asarray(ref).tobytes(), i
+        return run
+
+    def pipeline_reads():
+        rp = ce.ReadPipeline(rs, L, 6, 2, 0)
+        full, dig_ref = _parts(d, p, L, 6, 800)
+        for it in range(6):
+            slot, chunks, present, expected = rp.acquire()
+            chunks[:] = full
+            expected[:] = dig_ref
+            present[:] = 0
+            for k in range(6):
+                present[k, [(k + it + j) % t for j in range(d)]] = 1
+            rp.submit(slot, 6)
+            _, _, st = rp.wait(slot)
+            assert not any(st), it
+            for k in range(6):
+                assert rp.part_bytes(slot, 6, k) == full[k, :d].tobytes(), (it, k)
+
+    ths = [threading.Thread(target=guard(scheduler_stream, "scheduler"))]
+    ths += [threading.Thread(target=guard(per_call(i), f"per-call {i}")) for i in range(24)]
+    args = types.SimpleNamespace(iters=4)
+    ths += [threading.Thread(target=srb.worker, args=(100 + i, args, errors)) for i in range(6)]
+    ths += [threading.Thread(target=guard(pipeline_reads, "read pipeline"))]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join(timeout=150)
+    assert not any(th.is_alive() for th in ths), "a tier never finished"
+    assert not errors, errors
