@@ -31,8 +31,8 @@ import torch  # noqa: E402  (import before chunky_ec: one HIP runtime)
 import torch.distributed as dist  # noqa: E402
 
 import chunky_ec as ce  # noqa: E402
-from chunky_ec.sharding import (all_ranks_ok, barrier, dist_env, max_over_ranks,  # noqa: E402
-                                rank_seed)
+from chunky_ec.sharding import (all_ranks_ok, barrier, dist_env, gather_rows,  # noqa: E402
+                                max_over_ranks, rank_seed)
 
 METRIC = "RS(10,4) encode+sha256 GB/s per node at 1/2/4/8 GPUs; % of HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md); 5.79 TB/s measured
@@ -119,21 +119,69 @@ KERNEL_SYMBOL = {"sha256_kernel": "sha256_lane_kernel", "rs_apply_kernel": "rs_a
                  "read_batch(verify+decode)": ("sha256_lane_kernel", "rs_apply_var_kernel")}
 
 
-def measured_traffic(config: str, kernel: str, full_size: bool):
+def measured_traffic(config: str, kernel: str, full_size: bool, with_source: bool = False):
     """HBM bytes per launch of `kernel` from the committed PMC runs (profiles/traffic.json,
     written by profiles/summarize.py from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes
-    with the gfx950 x2 FETCH_SIZE correction), or None when this workload was not profiled."""
+    with the gfx950 x2 FETCH_SIZE correction), or None when this workload was not profiled.
+    with_source: (bytes, "the summary file it comes from") -- a committed measurement of the
+    same kernel and workload, not a measurement of this run."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
+    none = (None, None) if with_source else None
     if not full_size or not os.path.exists(path):
-        return None
+        return none
     table = json.load(open(path)).get(config, {})
     syms = KERNEL_SYMBOL.get(kernel, kernel)
     entries = [table.get(k) for k in ((syms,) if isinstance(syms, str) else syms)]
-    return sum(e["bytes_per_launch"] for e in entries) if all(entries) else None
+    if not all(entries):
+        return none
+    total = sum(e["bytes_per_launch"] for e in entries)
+    if not with_source:
+        return total
+    return total, "committed PMC run (not this run): " + ", ".join(
+        sorted({e.get("source", "profiles/traffic.json") for e in entries}))
 
 
-def cpu_baseline(cfg, threads: int):
-    """Oracle restatement of the crate path timed on this host (rank 0, N=1 only)."""
+def cpu_quota():
+    """CPUs this process may use: (affinity count, cgroup v2 cpu.max quota in CPUs or None)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = round(int(q) / int(period), 2)
+    except (OSError, ValueError):
+        pass
+    return aff, quota
+
+
+def host_info():
+    """The host the run is on (diagnoses host-bound end-to-end figures and stragglers)."""
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    nodes = [n for n in os.listdir("/sys/devices/system/node") if n.startswith("node")] \
+        if os.path.isdir("/sys/devices/system/node") else []
+    mem = None
+    try:
+        for line in open("/proc/meminfo"):
+            if line.startswith("MemTotal"):
+                mem = round(int(line.split()[1]) / (1 << 20), 1)
+    except OSError:
+        pass
+    aff, quota = cpu_quota()
+    return {"cpu": model, "logical_cpus": os.cpu_count(), "affinity_cpus": aff,
+            "cgroup_cpu_quota": quota, "numa_nodes": len(nodes), "mem_gib": mem}
+
+
+def cpu_baseline(cfg, threads: int, cores_total: int, cores_avail: int, quota):
+    """Oracle restatement of the crate path timed on this host (rank 0, N=1 only), with the
+    process's full CPU affinity (the caller restores it: the bench binds its main thread to
+    GPU0's NUMA node, and the baseline's threads would inherit that mask)."""
     import oracle
     d, p, L = cfg["d"], cfg["p"], cfg["chunk"]
     hashed = cfg["op"] != "encode"
@@ -153,10 +201,18 @@ def cpu_baseline(cfg, threads: int):
         "value": round(gbs, 3),
         "unit": "GB/s",
         "cores": threads,
+        "threads": threads,
+        "cores_used": min(threads, cores_avail, int(quota) if quota else cores_avail),
+        "cores_avail": cores_avail,
+        "cores_total": cores_total,
+        "cgroup_cpu_quota": quota,
         "kind": "port",
         "sample": f"{total} parts of RS({d},{p}) x {L // 1024} KiB "
                   f"({'encode_sep + sha256 of all chunks' if hashed else 'encode_sep'}), "
-                  f"{threads} threads, one part per task; {sec:.2f} s wall; "
+                  f"{threads} threads on {cores_avail} CPUs of the process's affinity "
+                  f"({cores_total} logical CPUs on the host"
+                  f"{f', cgroup quota {quota} CPUs' if quota else ''}), one part per task; "
+                  f"{sec:.2f} s wall; "
                   f"SHA-NI={'yes' if oracle.has_shani() else 'no'}",
         "single_core": {"value": round(n1 * d * L / sec1 / 1e9, 3), "unit": "GB/s",
                         "sample": f"{n1} parts on 1 thread; {sec1:.2f} s"},
@@ -240,51 +296,281 @@ def run_stream(args, cfg, codec, world, rank, device, reduce_dev):
         dist.destroy_process_group()
 
 
-def end_to_end(codec, d, p, L, gib, world, rank, reduce_dev):
+class HostCopier:
+    """`threads` host threads copying part-sized slices (numpy releases the GIL for the copy):
+    the caller's reader filling its part buffers (writer.rs:170-197 reads each part's
+    d*chunk_size bytes into `data_buf`)."""
+
+    def __init__(self, threads: int):
+        from concurrent.futures import ThreadPoolExecutor
+        self.threads = threads
+        self.pool = ThreadPoolExecutor(threads)
+
+    def copy(self, dst, src) -> None:
+        """dst[k] = src[k] for the leading (part) axis, split over the threads."""
+        n, T = len(src), self.threads
+
+        def job(i):
+            a, b = n * i // T, n * (i + 1) // T
+            if a < b:
+                dst[a:b] = src[a:b]
+        for f in [self.pool.submit(job, i) for i in range(T)]:
+            f.result()
+
+    def close(self) -> None:
+        self.pool.shutdown()
+
+
+def source_ring(n_parts, d, L, seed, copier):
+    """A pageable [n_parts][d][L] source of distinct parts (the file the reader reads): a
+    random 64 MiB block tiled with `copier`'s threads (first touch in parallel), then each
+    part's first 8 bytes set to its ring index.  Not timed."""
+    import numpy as np
+    ring = np.empty((n_parts, d, L), np.uint8)
+    blk = np.random.default_rng(seed).integers(0, 256, size=(max(1, (64 << 20) // (d * L)), d, L),
+                                                dtype=np.uint8)
+    for k in range(0, n_parts, len(blk)):
+        m = min(len(blk), n_parts - k)
+        copier.copy(ring[k:k + m], blk[:m])
+    ring[:, 0, :8] = np.arange(n_parts, dtype=np.uint64).view(np.uint8).reshape(n_parts, 8)
+    return ring
+
+
+def end_to_end(codec, d, p, L, gib, world, rank, reduce_dev, host_threads, device_ordinal):
     """North-star's PCIe-bound end-to-end figure beside the device-resident headline: the same
-    RS(10,4) encode + SHA-256 with the parts starting in page-locked host memory and parity +
-    digests landing back in it (cec_pipeline, C5's 256-part batches, 4 slots), `gib` GiB per
-    rank (weak scaling like the headline), max over ranks.  Not `value` (that is HBM-resident)."""
+    RS(10,4) encode + SHA-256 with the parts produced in host memory, parity + digests landing
+    back in it, `gib` GiB per rank (weak scaling like the headline), max over ranks.  Not
+    `value` (that is HBM-resident).  Three forms, each timed on its own:
+
+    value (`reader_to_pinned`): every batch's part bytes are copied, inside the timed region, by
+      `host_threads` threads from a pageable source ring (2x the slots' bytes, so every copy
+      reads DRAM) into the pinned slot -- the reference's reader filling `data_buf`
+      (writer.rs:170-197) when `data_buf` is the engine's page-locked slot -- then H2D, the
+      fused kernel (or, for these 256-part batches, encode + split SHA), D2H (cec_pipeline,
+      256-part batches, 4 slots in flight);
+    `scheduler_pageable`: the `cp` path of a single process -- the same pageable ring handed to
+      the multi-GPU scheduler (cec_multi, one shard on this rank's GPU), whose own NUMA-local
+      copy threads stage it;
+    `pcie_link`: the slots filled once and re-sent (8 bytes per part stamped): the link alone,
+      no host production (round 2's figure)."""
     import numpy as np
     P, depth = CONFIGS["c5"]["parts"], 4
     n_parts = max(depth * P, int(gib * (1 << 30)) // (d * L))
-    # ~10 GiB of page-locked slots per rank: if any rank cannot get them, every rank skips the
-    # figure together (no rank may be left waiting in a barrier) and the headline still prints
+    n_batches = (n_parts + P - 1) // P
+    ring_parts = 2 * depth * P
+    # ~10 GiB page-locked slots + a 20 GiB pageable ring per rank: if any rank cannot get them,
+    # every rank skips the figure together (no rank may be left waiting in a barrier) and the
+    # headline still prints
+    copier = HostCopier(host_threads)
     try:
         pl, err = ce.Pipeline(codec, L, P, depth), None
+        ring = source_ring(ring_parts, d, L, 0xE2E + rank, copier)
     except Exception as e:  # noqa: BLE001 (reported in the line)
-        pl, err = None, f"{type(e).__name__}: {e}"
+        pl, ring, err = None, None, f"{type(e).__name__}: {e}"
     if not all_ranks_ok(pl is not None, world, reduce_dev):
-        del pl
+        del pl, ring
+        copier.close()
         return {"value": None, "unit": "GB/s", "bound": "pcie",
-                "skipped": err or "another rank could not allocate its page-locked slots"}
-    block = np.random.default_rng(0xE2E + rank).integers(0, 256, size=(P, d, L), dtype=np.uint8)
-    for _ in range(depth):
-        _, data = pl.acquire()
-        data[:] = block
-    for _ in range(depth):  # warmup: one batch per slot
-        slot, _ = pl.acquire()
-        pl.submit(slot, P)
-    pl.drain()
-    barrier(world)
-    t0 = time.perf_counter()
-    part = 0
-    n_batches = (n_parts + P - 1) // P
-    for _ in range(n_batches):
-        slot, data = pl.acquire()
-        n = min(P, n_parts - part)
-        data[:n, 0, :8] = np.arange(part, part + n, dtype=np.uint64).view(np.uint8).reshape(n, 8)
-        pl.submit(slot, n)
-        part += n
-    pl.drain()
-    barrier(world)
-    el = max_over_ranks(time.perf_counter() - t0, world, reduce_dev)
+                "skipped": err or "another rank could not allocate its slots / source ring"}
+    stamp = np.arange(n_parts, dtype=np.uint64).view(np.uint8).reshape(n_parts, 8)
+
+    def timed(fill):
+        for _ in range(depth):  # warmup: one batch per slot
+            slot, data = pl.acquire()
+            fill(data, 0, P)
+            pl.submit(slot, P)
+        pl.drain()
+        barrier(world)
+        t0 = time.perf_counter()
+        part = 0
+        for _ in range(n_batches):
+            slot, data = pl.acquire()
+            n = min(P, n_parts - part)
+            fill(data, part, n)
+            pl.submit(slot, n)
+            part += n
+        pl.drain()
+        barrier(world)
+        return time.perf_counter() - t0
+
+    def from_ring(data, part, n):  # the reader: part bytes from the pageable source
+        r = part % ring_parts
+        m = min(n, ring_parts - r)
+        copier.copy(data[:m], ring[r:r + m])
+        if m < n:
+            copier.copy(data[m:n], ring[:n - m])
+        data[:n, 0, :8] = stamp[part:part + n]
+
+    def stamp_only(data, part, n):
+        data[:n, 0, :8] = stamp[part:part + n]
+
+    # parity / digests of the last batch against the oracle would need the CPU path; the
+    # ring-fed batches are checked for the property that holds at any size instead: every
+    # digest of a data chunk equals SHA-256 of the ring bytes it was copied from (sampled)
+    loc_ring = timed(from_ring)
+    el_ring = max_over_ranks(loc_ring, world, reduce_dev)
+    _, dg = pl.wait((n_batches - 1) % depth)
+    import hashlib
+    first = (n_batches - 1) * P
+    k = min(len(dg), n_parts - first) - 1
+    src = ring[(first + k) % ring_parts, 1]  # chunk 1: not stamped
+    ring_ok = bool(dg[k, 1].tobytes() == hashlib.sha256(src.tobytes()).digest())
+    loc_link = timed(stamp_only)
+    el_link = max_over_ranks(loc_link, world, reduce_dev)
     del pl
     total = n_parts * d * L * world
-    return {"value": round(total / el / 1e9, 2), "unit": "GB/s", "bound": "pcie",
-            "stream_bytes": total, "seconds": round(el, 3),
-            "path": "page-locked host parts -> H2D -> encode_hash_kernel -> D2H parity + digests "
-                    f"(cec_pipeline, {P}-part batches, {depth} slots), {gib:g} GiB per GPU"}
+    mine = n_parts * d * L
+    res = {
+        # this rank's own rates (the N > 1 line's `ranks` array; removed before printing)
+        "_local": (mine / loc_ring / 1e9, mine / loc_link / 1e9),
+        "value": round(total / el_ring / 1e9, 2), "unit": "GB/s", "bound": "pcie + host copy",
+        "form": "reader_to_pinned",
+        "stream_bytes": total, "seconds": round(el_ring, 3),
+        "host_threads": host_threads,
+        "host_copy_GBs": round(total / el_ring / 1e9, 2),
+        # host DRAM traffic of the form: the copy reads the ring and writes the slot, the H2D
+        # reads the slot, the D2H writes parity (p/d of the data) + 32-B digests per chunk
+        "host_dram_GBs": round(total * (3 + p / d) / el_ring / 1e9, 1),
+        "sampled_digest_matches_source": ring_ok,
+        "path": f"pageable source ring ({ring_parts} distinct parts, {size_label(ring.nbytes)}) "
+                f"-> {host_threads} host threads copy each batch into a page-locked slot -> H2D "
+                f"-> encode + SHA-256 -> D2H parity + digests (cec_pipeline, {P}-part batches, "
+                f"{depth} slots), {gib:g} GiB per GPU",
+        "pcie_link": {
+            "value": round(total / el_link / 1e9, 2), "unit": "GB/s", "seconds": round(el_link, 3),
+            "path": "the same pipeline with its slots filled ONCE and re-sent (8 bytes per part "
+                    "stamped): the PCIe link with no host production"},
+    }
+    # the scheduler's pageable path (what `cp` through the C++ FileWriteBuilder batch takes)
+    try:
+        res["scheduler_pageable"] = scheduler_pageable(codec, d, p, L, ring, n_parts, world,
+                                                       reduce_dev, device_ordinal)
+    except Exception as e:  # noqa: BLE001 (reported in the line)
+        res["scheduler_pageable"] = {"value": None, "skipped": f"{type(e).__name__}: {e}"}
+    copier.close()
+    return res
+
+
+def scheduler_pageable(codec, d, p, L, ring, n_parts, world, reduce_dev, device_ordinal):
+    """cec_multi with one shard on this rank's GPU, fed the pageable ring (two 512-part jobs in
+    flight; the scheduler's own copy threads stage the bytes), page-locked parity / digest
+    outputs.  Every rank streams its own n_parts."""
+    P, depth = CONFIGS["c5"]["parts"], 4
+    t = d + p
+    ring_parts = len(ring)
+    S, J = 2 * P, 2
+    m = ce.Multi(codec, L, P, depth, [device_ordinal])
+    outs = [(ce.HostBuffer(S * p * L, device_ordinal), ce.HostBuffer(S * t * 32, device_ordinal))
+            for _ in range(J)]
+    n_jobs = (n_parts + S - 1) // S
+
+    def submit(i, first):
+        par, dig = outs[i % J]
+        n = min(S, n_parts - first)
+        r = first % ring_parts
+        n = min(n, ring_parts - r)  # a job never wraps the ring
+        return m.encode_hash(ring[r:r + n], n, par, dig), n
+
+    for i in range(J):  # warmup: pins the shard's staging on its first pageable job
+        m.wait(submit(i, i * S)[0])
+    barrier(world)
+    t0 = time.perf_counter()
+    jobs, first, i = [], 0, 0
+    while first < n_parts:
+        if len(jobs) == J:
+            m.wait(jobs.pop(0))
+        job, n = submit(i, first)
+        jobs.append(job)
+        first += n
+        i += 1
+    for job in jobs:
+        m.wait(job)
+    barrier(world)
+    el = max_over_ranks(time.perf_counter() - t0, world, reduce_dev)
+    total = n_parts * d * L * world
+    copy_threads = int(os.environ.get("CEC_MULTI_COPY_THREADS", "4"))
+    del m, outs
+    return {"value": round(total / el / 1e9, 2), "unit": "GB/s", "seconds": round(el, 3),
+            "copy_threads": copy_threads,
+            "path": f"pageable source ring -> cec_multi (1 shard on device {device_ordinal}, its "
+                    f"{copy_threads} NUMA-local copy threads stage into page-locked slots) -> "
+                    f"H2D -> encode + SHA-256 -> D2H into page-locked outputs; {S}-part jobs, "
+                    f"{J} in flight"}
+
+
+def two_erasures(n_parts: int, t: int, rank: int):
+    """north_star's reconstruct case: exactly 2 erasures per part, uniform over the t chunks
+    (seeded, the c3e2 config's sets).  Returns the present mask as a uint8 [n][t] tensor."""
+    g = torch.Generator().manual_seed(2222 + rank)
+    pres = torch.ones((n_parts, t), dtype=torch.uint8)
+    for i in range(n_parts):
+        pres[i, torch.randperm(t, generator=g)[:2]] = 0
+    return pres
+
+
+def reconstruct_data_bytes(pres, d: int, L: int) -> int:
+    """Algorithmic bytes of reconstruct_data over `pres`: parts with a missing data chunk read d
+    chunks and write the missing data ones; parts missing only parity are skipped (the crate
+    returns early)."""
+    miss = d - pres[:, :d].sum(1)
+    return int((miss > 0).sum().item()) * d * L + int(miss.sum().item()) * L
+
+
+def north_star_block(codec, batch, buf, digests, stream, device, rank, d, p, L, steps):
+    """north_star's two numeric targets, timed on the headline's own buffer right after it:
+    RS(10,4) encode (file_part.rs:161-165) and 2-erasure reconstruct_data (file_part.rs:128)
+    over every part, each launch bracketed by HIP events on `stream` (1 warmup launch, then
+    `steps`), as a fraction of the 8 TB/s HBM peak.  After the rebuild, every data chunk is
+    verified on the GPU against the digest the headline computed for it."""
+    n = batch.n_parts
+    t = d + p
+    out = {}
+
+    def time_launches(fn):
+        fn()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(steps)]
+        for a, b in evs:
+            a.record(stream)
+            fn()
+            b.record(stream)
+        torch.cuda.synchronize(device)
+        return sum(a.elapsed_time(b) for a, b in evs) / steps
+
+    def entry(call, kernel, ms, algo, cfgkey):
+        gbs = algo / (ms / 1e3) / 1e9
+        tr, src = measured_traffic(cfgkey, kernel, True, with_source=True)
+        return {"call": call, "kernel": kernel, "ms": round(ms, 4), "algorithmic_bytes": algo,
+                "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(gbs / HBM_PEAK_GBS, 4), "target_frac": 0.60,
+                "meets_target": gbs / HBM_PEAK_GBS >= 0.60,
+                "traffic": tr, "traffic_source": src}
+
+    ms = time_launches(lambda: ce.encode_batch(codec, batch, stream))
+    out["encode"] = entry("encode_sep (cec_encode_batch), every part: read d, write p chunks",
+                          "rs_apply_kernel", ms, n * t * L, "c2enc")
+    pres = two_erasures(n, t, rank)
+    present = bytes(pres.flatten().tolist())
+    buf.mul_(pres.to(device).view(n, t, 1))  # the erased chunks start zeroed
+    ms = time_launches(lambda: ce.reconstruct_batch(codec, batch, present, True, stream))
+    out["reconstruct_data_2_erasures"] = entry(
+        "reconstruct_data (cec_reconstruct_batch, data_only), exactly 2 random erasures of the "
+        f"{t} chunks per part (c3e2's sets): parts with a missing data chunk read d, write the "
+        "missing data chunks", "rs_apply_var_kernel", ms, reconstruct_data_bytes(pres, d, L),
+        "c3e2")
+    # size-independent check: every rebuilt (and every untouched) data chunk hashes to the
+    # digest the headline step computed before the erasure
+    exp = digests[:, :d].contiguous()
+    ok = torch.zeros((n, d), dtype=torch.uint8, device=device)
+    ce.verify_batch(batch, 0, d, exp.data_ptr(), ok.data_ptr(), stream=stream)
+    torch.cuda.synchronize(device)
+    out["rebuilt_data_verified"] = bool(ok.all().item())
+    out["basis"] = ("HIP events on the launch stream, average of the timed launches; algorithmic "
+                    "bytes per SURVEY.md §8d (encode (d+p)·L per part, reconstruct_data (d+k)·L per "
+                    "part with a missing data chunk); traffic = committed PMC bytes per launch of "
+                    "the same kernel on the same workload (traffic_source), not measured in this "
+                    "run")
+    return out
 
 
 def _segments(args, cfg, shards):
@@ -608,6 +894,8 @@ def main():
     ap.add_argument("--e2e-gib", type=float, default=64.0,
                     help="c2: GiB per GPU of the PCIe-bound end-to-end figure (0 = skip)")
     ap.add_argument("--check", action="store_true", help="verify a sampled part vs the oracle")
+    ap.add_argument("--no-north-star", action="store_true",
+                    help="c2: skip the encode-only / 2-erasure reconstruct_data block")
     ap.add_argument("--stream-gib", type=float, default=1024.0,
                     help="c5: total stream size in GiB across all ranks")
     ap.add_argument("--separate", action="store_true",
@@ -632,9 +920,17 @@ def main():
     ordinal = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(ordinal)
     device = torch.device("cuda", ordinal)
+    # the process's own CPU set, before the NUMA binding below narrows the main thread's (the
+    # CPU baseline runs with it restored)
+    full_affinity = os.sched_getaffinity(0)
     # host threads and the pinned slots of this rank on its GPU's NUMA node (the engine places
     # its own pinned buffers there anyway; this keeps the host copies local too)
     numa_bound = ce.bind_thread_to_device_node(ordinal)
+    numa_node = ce.device_numa_node(ordinal)
+    rank_cpus = len(os.sched_getaffinity(0))
+    # host threads of this rank's end-to-end reader: half its CPUs (the rest run the engine's
+    # own threads), 8 at most
+    e2e_threads = int(os.environ.get("CEC_E2E_THREADS", "0")) or max(1, min(8, rank_cpus // 2))
     # RCCL ("nccl") carries only the barrier and the max-over-ranks all-reduce.
     # CEC_BENCH_BACKEND=gloo rehearses N > 1 with several ranks on one GPU.
     backend = os.environ.get("CEC_BENCH_BACKEND", "nccl")
@@ -663,15 +959,9 @@ def main():
     if cfg["op"] == "reconstruct_e2":
         ce.encode_batch(codec, batch, stream)
         # exactly 2 erasures per part, uniform over the 14 chunks (seeded); rebuilt in place
-        g = torch.Generator().manual_seed(2222 + rank)
-        pres = torch.ones((n_parts, t), dtype=torch.uint8)
-        for i in range(n_parts):
-            pres[i, torch.randperm(t, generator=g)[:2]] = 0
+        pres = two_erasures(n_parts, t, rank)
         present = bytes(pres.flatten().tolist())
-        miss_data = (d - pres[:, :d].sum(1))
-        # reconstruct_data: parts with a missing data chunk read d chunks and write the missing
-        # data ones (parts missing only parity are skipped, as the crate returns early)
-        algo_data = int((miss_data > 0).sum().item()) * d * L + int(miss_data.sum().item()) * L
+        algo_data = reconstruct_data_bytes(pres, d, L)
         # reconstruct: every part reads d chunks and writes its 2 missing ones
         algo_full = n_parts * (d + 2) * L
         # the erased chunks start zeroed, so the first step really rebuilds them
@@ -831,9 +1121,9 @@ def main():
     dom_name = max((k for k in kernels if not k.startswith("also_")), key=lambda k: kernels[k]["ms"])
     dom = kernels[dom_name]
     achieved = dom["algorithmic_bytes"] / (dom["ms"] / 1e3) / 1e9
-    traffic = measured_traffic(args.config + ("sep" if cfg["op"] == "encode_hash" and not fused
-                                              else ""),
-                               dom_name, n_parts == CONFIGS[args.config]["parts"])
+    traffic, traffic_src = measured_traffic(
+        args.config + ("sep" if cfg["op"] == "encode_hash" and not fused else ""),
+        dom_name, n_parts == CONFIGS[args.config]["parts"], with_source=True)
 
     valu = None
     if cfg["op"] in ("encode_hash", "read"):
@@ -887,10 +1177,33 @@ def main():
             ok = ok and all(hashlib.sha256(host[j].tobytes()).digest() == dg[j].tobytes()
                             for j in range(t))
 
+    # north_star's two >= 60 % targets on the same buffer (C2 only)
+    nstar = None
+    if args.config == "c2" and not args.separate and not args.no_north_star:
+        nstar = north_star_block(codec, batch, buf, digests, stream, device, rank, d, p, L,
+                                 args.steps)
+    del buf, digests  # the end-to-end forms below use their own buffers
+    torch.cuda.empty_cache()
+
     # every rank streams its own share (barriers inside): the PCIe-inclusive figure
     e2e = None
     if args.config == "c2" and args.e2e_gib > 0 and not args.separate:
-        e2e = end_to_end(codec, d, p, L, args.e2e_gib, world, rank, reduce_dev)
+        e2e = end_to_end(codec, d, p, L, args.e2e_gib, world, rank, reduce_dev, e2e_threads,
+                         ordinal)
+
+    # per-rank figures for the N > 1 line (a straggler or a cross-NUMA placement must be
+    # visible from the line alone)
+    ranks = None
+    if world > 1:
+        e2e_v, link_v = (e2e or {}).get("_local") or (0.0, 0.0)
+        rows = gather_rows([ordinal, numa_node, 1.0 if numa_bound else 0.0, rank_cpus,
+                            local_s * 1e3, e2e_v, link_v], world, reduce_dev)
+        ranks = [{"rank": r, "device": int(row[0]), "numa_node": int(row[1]),
+                  "host_threads_numa_bound": bool(row[2]), "cpus": int(row[3]),
+                  "step_ms": round(row[4], 3),
+                  "end_to_end_GBs": round(row[5], 2) if row[5] else None,
+                  "pcie_link_GBs": round(row[6], 2) if row[6] else None}
+                 for r, row in enumerate(rows)]
 
     if rank == 0:
         total_data = data_bytes * world
@@ -923,18 +1236,33 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
+                "traffic_source": traffic_src,
             },
             "kernels": kernels,
         }
         if valu is not None:
             line["valu_roofline"] = valu
+        if nstar is not None:
+            line["north_star"] = nstar
         if e2e is not None:
+            e2e.pop("_local", None)
             line["end_to_end"] = e2e
+        if ranks is not None:
+            steps_ms = [r["step_ms"] for r in ranks]
+            line["ranks"] = ranks
+            line["step_ms_over_ranks"] = {"max": round(max(steps_ms), 3),
+                                          "mean": round(sum(steps_ms) / len(steps_ms), 3),
+                                          "min": round(min(steps_ms), 3)}
         if ok is not None:
             line["check_vs_oracle"] = bool(ok)
+        line["host"] = host_info()
         if world == 1 and not args.no_cpu_baseline and cfg["op"] in ("encode_hash", "encode"):
-            threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-            line["cpu_baseline"] = cpu_baseline(cfg, threads)
+            # the process's full CPU set (the main thread was bound to GPU0's NUMA node above)
+            os.sched_setaffinity(0, full_affinity)
+            avail, quota = len(full_affinity), cpu_quota()[1]
+            threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, avail)
+            line["cpu_baseline"] = cpu_baseline(cfg, threads, os.cpu_count() or avail, avail,
+                                                quota)
         print(json.dumps(line), flush=True)
 
     if world > 1:

@@ -65,6 +65,11 @@ def _sig(name, argtypes, restype=ctypes.c_int):
 
 
 _sig("cec_abi_version", [])
+# the include/chunky_ec.h this binding mirrors (2: CEC_PRESENT_VERIFIED = 0x80)
+ABI_VERSION = 2
+if _lib.cec_abi_version() != ABI_VERSION:
+    raise ImportError(f"chunky_ec: {LIB_PATH} has ABI {_lib.cec_abi_version()}, this binding "
+                      f"needs {ABI_VERSION}; rebuild with `make -C chunky-bits_amd/csrc`")
 _sig("cec_status_name", [ctypes.c_int], ctypes.c_char_p)
 _sig("cec_last_error", [], ctypes.c_char_p)
 _sig("cec_device_count", [])
@@ -714,15 +719,24 @@ def _addr(buf) -> int:
 
 class HostBuffer:
     """Page-locked, portable host memory from cec_host_alloc (pages on `device`'s NUMA node).
-    ``.array`` is a writable numpy uint8 view; the memory is freed with the object."""
+    ``.array`` is a writable numpy uint8 view.  Every view holds a reference to the HostBuffer
+    (through its base buffer), so the memory is freed only once the object AND all views of it
+    are gone: ``HostBuffer(n).view(a, b)`` is safe to keep."""
 
     def __init__(self, nbytes: int, device: int = -1):
-        import numpy as np
         h = _vp()
         _check(_lib.cec_host_alloc(nbytes, device, ctypes.byref(h)))
         self.ptr = h.value
         self.nbytes = nbytes
-        self.array = np.ctypeslib.as_array(ctypes.cast(h, _u8p), shape=(nbytes,))
+
+    @property
+    def array(self):
+        import numpy as np
+        if not self.ptr:
+            raise ValueError("HostBuffer already freed")
+        raw = (ctypes.c_uint8 * self.nbytes).from_address(self.ptr)
+        raw._owner = self  # the numpy view's base is `raw`: it keeps this buffer alive
+        return np.frombuffer(raw, dtype=np.uint8)
 
     def view(self, *shape):
         return self.array.reshape(*shape)
@@ -730,7 +744,6 @@ class HostBuffer:
     def __del__(self, _free=_lib.cec_host_free):
         p = getattr(self, "ptr", None)
         if p:
-            self.array = None
             _free(p)
             self.ptr = None
 
@@ -768,7 +781,7 @@ def set_device(device: int) -> None:
 # ---------------------------------------------------------------------------------------------
 
 PIPE_EXTERNAL = 2  # CEC_PIPE_EXTERNAL
-PRESENT_VERIFIED = 2  # CEC_PRESENT_VERIFIED: read-retry flag (loaded, verified by an earlier pass)
+PRESENT_VERIFIED = 0x80  # CEC_PRESENT_VERIFIED: read-retry flag (loaded, verified by an earlier pass)
 READ_RESILVER = 4  # CEC_READ_RESILVER: read-pipeline flag, FilePart::resilver's compute
 READ_VERIFY_ONLY = 8  # CEC_READ_VERIFY_ONLY: read-pipeline flag, FilePart::verify's compute
 

@@ -28,6 +28,20 @@ def max_over_ranks(x: float, world: int, device=None) -> float:
     return float(t.item())
 
 
+def gather_rows(row, world: int, device=None):
+    """Every rank's `row` (a list of floats of the same length on every rank), in rank order, on
+    every rank (a collective: every rank must call it).  A SUM all-reduce of a [world][k] zero
+    tensor with each rank's own row filled in, so it works on gloo and on RCCL alike."""
+    if world == 1:
+        return [list(map(float, row))]
+    import torch
+    import torch.distributed as dist
+    t = torch.zeros((world, len(row)), dtype=torch.float64, device=device)
+    t[dist.get_rank()] = torch.tensor(list(map(float, row)), dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t.cpu().tolist()
+
+
 def all_ranks_ok(ok: bool, world: int, device=None) -> bool:
     """True on every rank iff `ok` holds on every rank (a collective: every rank must call it).
     Lets the ranks skip an optional step together when one of them cannot run it, so no rank is

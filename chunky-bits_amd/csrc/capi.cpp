@@ -207,7 +207,7 @@ int upload_words(const std::vector<uint32_t>& words, hipStream_t s, Scratch& sc,
 // bounded per-device pool (not thread_local: the reference calls the crate from tokio's
 // blocking pool, whose threads come and go, file_part.rs:128,161 / any.rs:19-24, so per-thread
 // resources would leak with every retired thread).  At most kMaxIdleCtx contexts per device
-// stay alive between calls; idle buffers above kMaxIdleBytes are freed when returned.
+// stay alive between calls, holding at most kMaxIdleBytes of device buffers together.
 // ------------------------------------------------------------------------------------------
 struct StageCtx {
     int device = 0;
@@ -242,11 +242,16 @@ int ctx_reserve(StageCtx& c, size_t device_bytes) {
 }
 
 constexpr size_t kMaxIdleCtx = 8;
-constexpr size_t kMaxIdleBytes = size_t(64) << 20;
+// Device bytes idle contexts may hold per device.  Bounding the total (not each buffer) keeps a
+// steady stream of large per-call requests (e.g. RS(10,4) at 8 MiB chunks: 112 MiB per part)
+// from paying a hipMalloc + a device-synchronizing hipFree on every call.
+constexpr size_t kMaxIdleBytes = size_t(1) << 30;
 
 class CtxPool {
    public:
-    std::unique_ptr<StageCtx> take(int device) {
+    // An idle context of `device` whose buffer already holds `device_bytes` (the smallest such),
+    // else the one with the largest buffer (grown by ctx_reserve), else a new one.
+    std::unique_ptr<StageCtx> take(int device, size_t device_bytes) {
         std::lock_guard<std::mutex> lk(mu_);
         auto& v = idle_[device];
         if (v.empty()) {
@@ -254,29 +259,50 @@ class CtxPool {
             c->device = device;
             return c;
         }
-        auto c = std::move(v.back());
-        v.pop_back();
+        size_t best = 0;
+        for (size_t i = 1; i < v.size(); ++i) {
+            const size_t a = v[i]->dcap, b = v[best]->dcap;
+            const bool fits_a = a >= device_bytes, fits_b = b >= device_bytes;
+            if (fits_a != fits_b ? fits_a : (fits_a ? a < b : a > b)) best = i;
+        }
+        auto c = std::move(v[best]);
+        v.erase(v.begin() + std::ptrdiff_t(best));
+        idle_bytes_[device] -= c->dcap;
         return c;
     }
     // The caller's current device is the context's (leases never cross devices).
     void give(std::unique_ptr<StageCtx> c) {
         if (!c) return;
         if (c->stream) (void)hipStreamSynchronize(c->stream);
-        if (c->dcap > kMaxIdleBytes) c->release_buffer();
+        bool drop_buffer = false;
         {
             std::lock_guard<std::mutex> lk(mu_);
             auto& v = idle_[c->device];
             if (v.size() < kMaxIdleCtx) {
-                v.push_back(std::move(c));
-                return;
+                size_t& held = idle_bytes_[c->device];
+                if (held + c->dcap <= kMaxIdleBytes) {
+                    held += c->dcap;
+                    v.push_back(std::move(c));
+                    return;
+                }
+                drop_buffer = true;  // over the budget: keep the stream, free the buffer below
             }
         }
-        c->destroy();
+        if (!drop_buffer) {
+            c->destroy();
+            return;
+        }
+        c->release_buffer();
+        std::lock_guard<std::mutex> lk(mu_);
+        auto& v = idle_[c->device];
+        if (v.size() < kMaxIdleCtx) v.push_back(std::move(c));
+        // (else another thread filled the pool meanwhile: c's stream is destroyed with it)
     }
 
    private:
     std::mutex mu_;
     std::map<int, std::vector<std::unique_ptr<StageCtx>>> idle_;
+    std::map<int, size_t> idle_bytes_;
 };
 
 // Leaked on purpose: destroying HIP objects from a static destructor races the runtime's own
@@ -296,7 +322,7 @@ class CtxLease {
     int acquire(size_t device_bytes) {
         int dev = 0;
         CEC_TRY(current_device(&dev));
-        c_ = ctx_pool().take(dev);
+        c_ = ctx_pool().take(dev, device_bytes);
         return ctx_reserve(*c_, device_bytes);
     }
     StageCtx* operator->() { return c_.get(); }
@@ -1123,13 +1149,15 @@ struct PartImpl {
             h.digests = ddig;
             HIP_TRY(launch_sha256(h, true, s));
             if (early) {
-                // Parity down beside the SHA-256 chains (both only read the batch).  The host
-                // waits for the encode and only then queues the download: no stream waits on
-                // another stream's event, since with more streams than the process's hardware
-                // queues (GPU_MAX_HW_QUEUES) two streams can share a queue, and cross-stream
-                // waits in shared in-order queues can wait on each other (a 256-caller run
-                // hung with the device-side form).
-                HIP_TRY(hipEventSynchronize(a.encoded));
+                // Parity down beside the SHA-256 chains (both only read the batch): the side
+                // stream waits on the device for the encode's event.  A wait on an event that
+                // was recorded before the wait is queued cannot deadlock, even when two streams
+                // share one in-order hardware queue (more streams than GPU_MAX_HW_QUEUES): the
+                // event's marker precedes the waiting packet in any queue order.  (Round 2 had
+                // the host block on the event here, blaming a 256-caller hang on such waits;
+                // that hang was the stranded-caller race fixed below, and the host hand-over
+                // build hung the same way before that fix.)
+                HIP_TRY(hipStreamWaitEvent(a.side, a.encoded, 0));
                 side_wait.q = a.side;
                 CEC_TRY(parity_down(a.side));
                 parity_sent = true;
@@ -1729,7 +1757,10 @@ int verify_then_reconstruct(const cec_codec* c, const cec_part_batch* b,
     CEC_TRY(ok_buf.acquire(n, s));
     uint8_t* ok = ok_buf.dev();
     HIP_TRY(hipMemsetAsync(ok, 0, n, s));
-    // Fork point: the caller's work on s so far (the chunks).
+    // Fork point: the caller's work on s so far (the chunks).  The side stream waits for it and
+    // s later waits for the side stream's join, each on an event recorded before the wait is
+    // queued: safe in shared in-order hardware queues (the rule of the coalescer's early parity
+    // download above).
     SideLease lease;
     SideCtx* side = nullptr;
     if (speculate) {

@@ -224,7 +224,7 @@ int cec_host_numa_node(const void* p) {
                                          ~uintptr_t(sysconf(_SC_PAGESIZE) - 1));
     int status = -1;
     if (syscall(SYS_move_pages, 0, 1ul, &page, nullptr, &status, 0) != 0) return -1;
-    return status;
+    return status >= 0 ? status : -1;  // a page not resident / not mapped: -ENOENT, -EFAULT
 }
 
 }  // extern "C"

@@ -31,7 +31,7 @@ pub mod sys {
         _private: [u8; 0],
     }
 
-    pub const CEC_ABI_VERSION: c_int = 1;
+    pub const CEC_ABI_VERSION: c_int = 2;
     /// cec_read_pipeline_new_ex / cec_multi_read flag: only rebuilt data chunks come back.
     pub const CEC_READ_REBUILT_ONLY: std::os::raw::c_uint = 1;
     /// cec_read_pipeline_new_ex flag: FilePart::resilver's compute (data and parity rebuilt).
@@ -41,7 +41,7 @@ pub mod sys {
     /// cec_pipeline_new_ex / cec_read_pipeline_new_ex flag: batches come from caller buffers.
     pub const CEC_PIPE_EXTERNAL: std::os::raw::c_uint = 2;
     /// Present-flag value of a read retry: loaded and already verified (not hashed again).
-    pub const CEC_PRESENT_VERIFIED: u8 = 2;
+    pub const CEC_PRESENT_VERIFIED: u8 = 0x80;
 
     #[repr(C)]
     #[derive(Clone, Copy, Debug)]

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define CEC_ABI_VERSION 1
+#define CEC_ABI_VERSION 2  /* 2: CEC_PRESENT_VERIFIED moved from 2 to 0x80 */
 
 typedef enum cec_status {
     CEC_OK = 0,
@@ -230,8 +230,10 @@ int cec_verify_batch(const cec_part_batch* batch, size_t first_chunk, size_t n_c
  * reads (cec_read_batch, cec_read_pipeline_*, cec_multi_read) report such a part
  * CEC_TOO_FEW_SHARDS_PRESENT with its verified flags; the caller loads more chunks for just
  * those parts and submits them again, marking the chunks already verified CEC_PRESENT_VERIFIED
- * (they are used but not hashed again) and the new ones 1.  Any other nonzero flag = loaded. */
-#define CEC_PRESENT_VERIFIED 2
+ * (they are used but not hashed again) and the new ones 1.  Any other nonzero flag = loaded and
+ * hashed.  ABI 2 moved the value from 2 to 0x80: in ABI 1 a caller passing 2 for "loaded" (or
+ * summing / OR-ing small flags) silently skipped verification; 0x80 does not arise that way. */
+#define CEC_PRESENT_VERIFIED 0x80
 
 /* FilePart::read_with_context compute (file_part.rs:86-129) for every part: verify the loaded
  * chunks (present: HOST flags, n_parts*(d+p)) against expected (DEVICE digests, part-major,

@@ -459,10 +459,15 @@ struct Chunk {
 
 enum class LocationIntegrity { Valid, Invalid, Unavailable, Resilvered };
 
-// VerifyPartReport / ResilverPartReport (file_part.rs:392-520), reduced to per-chunk status.
+// VerifyPartReport / ResilverPartReport (file_part.rs:392-520, 671-676), reduced to per-chunk
+// status.  write_error: ResilverPartReport::write_error — the reconstruct failure of this part
+// (TooFewShardsPresent when fewer than d chunks verified, file_part.rs:296-308); the other parts
+// of the file are still resilvered.
 struct PartReport {
     std::vector<LocationIntegrity> chunks;  // d data then p parity
+    std::optional<Error> write_error;
     bool is_ideal() const {
+        if (write_error) return false;
         for (auto c : chunks)
             if (c != LocationIntegrity::Valid && c != LocationIntegrity::Resilvered) return false;
         return true;
@@ -548,7 +553,12 @@ struct FilePart {
         for (const auto& s : all) any_missing = any_missing || !s;
         if (!any_missing) return rep;
         const ReedSolomon r(data.size(), parity.size());
-        r.reconstruct(all);
+        try {
+            r.reconstruct(all);
+        } catch (const ErasureError& e) {  // recorded in the report, as write_error
+            rep.write_error = e.error();
+            return rep;
+        }
         std::unique_lock<std::mutex> lk;
         if (dest_mu) lk = std::unique_lock<std::mutex>(*dest_mu);
         for (size_t i = 0; i < all.size(); ++i) {
@@ -669,8 +679,9 @@ struct FileReference {
     // resilver, file_part.rs:228-390).  parts_per_batch > 0: runs of parts of one shape go
     // through the multi-GPU scheduler (cec_multi_verify / cec_multi_resilver over `devices`):
     // every stored chunk loaded, hashed against its metadata digest, and (resilver) every chunk
-    // that is missing or fails rebuilt and written back.  Same reports and the same failure
-    // (TooFewShardsPresent) as the per-part calls.
+    // that is missing or fails rebuilt and written back.  Same reports as the per-part calls: a
+    // part that cannot be rebuilt gets write_error (TooFewShardsPresent) in its report and the
+    // remaining parts are still resilvered (file_reference.rs:103-110 collects every report).
     std::vector<PartReport> verify(const ChunkStore& src, size_t parts_per_batch = 0,
                                    size_t depth = 4, const std::vector<int>& devices = {}) const {
         std::vector<PartReport> r(parts.size());
@@ -795,7 +806,10 @@ struct FileReference {
                     missing = missing || !w.verified[q * t + i];
                 }
                 if (!resilver || !missing) continue;
-                if (w.status[q] != CEC_OK) throw ErasureError(Error::TooFewShardsPresent);
+                if (w.status[q] != CEC_OK) {  // this part's write_error; the others go on
+                    rep.write_error = Error::TooFewShardsPresent;
+                    continue;
+                }
                 const FilePart& part = parts[k0 + w.first + q];
                 for (size_t i = 0; i < t; ++i) {
                     if (w.verified[q * t + i]) continue;

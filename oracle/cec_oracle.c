@@ -28,7 +28,7 @@
  *   src/file/hash/sha256.rs:20-26.  A scalar restatement plus an x86 SHA-NI variant (sha2 0.9.9
  *   dispatches to SHA-NI through `cpufeatures` when present), used only for the CPU baseline.
  *
- * Pinning (tests/test_oracle_kat.py): the reference's own KAT sha256("Hello World")
+ * Pinning (tests/test_oracle.py): the reference's own KAT sha256("Hello World")
  * (tests/hash.rs:3-4), hashlib (OpenSSL FIPS 180-4) on many lengths, and the crate's /
  * JavaReedSolomon's published known-answer tests (galois mul/exp values and the RS(5,5)
  * "one encode" vector) — those come from the crate's test-suite, which is not in this

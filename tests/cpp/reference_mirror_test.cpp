@@ -367,9 +367,20 @@ void test_batched_verify_resilver() {
         CHECK(f.read(store, 4, 2, devs) == input);
         for (const auto& r : f.verify(store, 4, 2, devs)) CHECK(r.is_ideal());
     }
-    // a part with fewer than d usable chunks: resilver fails like the per-part call
+    // a part with fewer than d usable chunks: its report carries the reconstruct error
+    // (ResilverPartReport::write_error) and the other parts are still resilvered, batched and
+    // per part alike
     for (size_t i = 1; i < d + p; ++i) store.erase(f.parts[4].chunk(i).hash);
-    CHECK(throws_erasure([&] { f.resilver(store, 4, 2); }, Error::TooFewShardsPresent));
+    for (const size_t ppb : {size_t(4), size_t(0)}) {
+        store.erase(f.parts[7].data[1].hash);  // a repairable hole in another part
+        const auto rep = f.resilver(store, ppb, 2);
+        CHECK(rep.size() == f.parts.size());
+        CHECK(rep[4].write_error && *rep[4].write_error == Error::TooFewShardsPresent);
+        CHECK(rep[4].count(LocationIntegrity::Resilvered) == 0 && !rep[4].is_ideal());
+        CHECK(!rep[7].write_error && rep[7].chunks[1] == LocationIntegrity::Resilvered);
+        for (size_t k = 0; k < f.parts.size(); ++k)
+            if (k != 4) CHECK(!rep[k].write_error && rep[k].is_ideal());
+    }
 }
 
 // A FileReference whose parts have different shapes (the metadata allows a d/p per part;

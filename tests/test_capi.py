@@ -56,7 +56,7 @@ def test_status_codes_match_crate_order():
              "InvalidShardFlags", "InvalidIndex"]
     for code, name in enumerate(names):
         assert ce.status_name(code) == name
-    assert ce.abi_version() == 1
+    assert ce.abi_version() == ce.ABI_VERSION == 2
 
 
 @pytest.mark.parametrize("d,p", [(1, 1), (3, 2), (10, 4), (20, 8), (5, 5), (17, 3), (128, 128),

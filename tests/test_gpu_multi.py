@@ -702,3 +702,35 @@ def test_read_pipeline_stream_knobs_bit_exact(monkeypatch, knobs):
         tp.test_read_pipeline_matches_read_with_context(10, 4, 4096, 12, 3, 5, flags)
         tp.test_read_pipeline_packed_submit(10, 4, 4096, 12, 3, 5, flags, True)
     test_read_pipeline_resilver_flag_vs_oracle()
+
+
+# ----------------------------------------------------------------------------------------------
+# HostBuffer views keep their page-locked memory alive
+# ----------------------------------------------------------------------------------------------
+
+def test_host_buffer_view_outlives_its_owner():
+    """A view of a HostBuffer that was dropped keeps the buffer (and its page-locked memory)
+    alive; the memory is freed only once the last view is gone.  Used to be a use-after-free:
+    the view's base was a bare ctypes pointer."""
+    import gc
+    import weakref
+    n = 1 << 20
+    hb = ce.HostBuffer(n)
+    owner = weakref.ref(hb)
+    v = hb.view(256, 4096)
+    v2 = ce.HostBuffer(n).array  # a temporary: only its view is kept
+    del hb
+    gc.collect()
+    assert owner() is not None
+    assert ce.host_is_pinned(v) and ce.host_is_pinned(v2)
+    v[:] = 7
+    v2[:] = 9
+    others = [ce.HostBuffer(n) for _ in range(4)]  # would reuse freed pinned pages
+    for o in others:
+        o.array[:] = 0
+    assert int(v.min()) == int(v.max()) == 7 and int(v2.min()) == int(v2.max()) == 9
+    # the engine DMAs it: the buffer's bytes go through a per-call SHA-256
+    assert str(ce.Sha256Hash.from_buf(v)) == hashlib.sha256(bytes(v)).hexdigest()
+    del v
+    gc.collect()
+    assert owner() is None

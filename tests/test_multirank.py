@@ -34,7 +34,7 @@ def _part_digests(part, d, p, L):
 def _worker(rank, world, port, n_parts, out_q):
     import torch
     import torch.distributed as dist
-    from chunky_ec.sharding import all_ranks_ok, barrier, max_over_ranks
+    from chunky_ec.sharding import all_ranks_ok, barrier, gather_rows, max_over_ranks
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -46,9 +46,11 @@ def _worker(rank, world, port, n_parts, out_q):
         # bench.py's optional end-to-end step: skipped on every rank when one rank cannot run it
         ok_all = all_ranks_ok(True, world)
         ok_one_fails = all_ranks_ok(rank != world - 1, world)
+        # bench.py's per-rank array: each rank's own row, in rank order, on every rank
+        rows = gather_rows([rank, 10.0 * rank + 0.5, hi - lo], world)
         gathered = [None] * world
         dist.all_gather_object(gathered, res)
-        out_q.put((rank, t, gathered, ok_all, ok_one_fails))
+        out_q.put((rank, t, gathered, ok_all, ok_one_fails, rows))
     finally:
         dist.destroy_process_group()
 
@@ -64,8 +66,10 @@ def test_part_range_partitions_exactly():
             assert seen == list(range(n))
 
 
-def test_two_rank_gloo_sharding_matches_single_process():
-    world, n_parts = 2, 9
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_gloo_sharding_matches_single_process(world):
+    """World sizes 2, 4 and 8 (the driver's 1/2/4/8-GPU runs use the same helpers over RCCL)."""
+    n_parts = 9 if world == 2 else 19  # 19 over 8 ranks: ragged ranges (2 or 3 parts each)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -77,9 +81,12 @@ def test_two_rank_gloo_sharding_matches_single_process():
         pr.join(timeout=60)
         assert pr.exitcode == 0
     single = {k: _part_digests(k, 3, 2, 257) for k in range(n_parts)}
-    for rank, t, gathered, ok_all, ok_one_fails in results:
-        assert t == pytest.approx(1.0)  # max over ranks of (rank+1)*0.5
+    for rank, t, gathered, ok_all, ok_one_fails, rows in results:
+        assert t == pytest.approx(0.5 * world)  # max over ranks of (rank+1)*0.5
         assert ok_all and not ok_one_fails
+        assert rows == [[float(r), 10.0 * r + 0.5,
+                         float(part_range(n_parts, r, world)[1] - part_range(n_parts, r, world)[0])]
+                        for r in range(world)]
         merged = {}
         for part_map in gathered:
             assert not (set(merged) & set(part_map))  # disjoint ownership

@@ -114,9 +114,9 @@ def test_part_batch_layout_and_constants_match():
     assert [(t, n) for t, n in cf] == [(t, n) for t, n in rf]
     for const in ("CEC_ABI_VERSION", "CEC_READ_REBUILT_ONLY", "CEC_PIPE_EXTERNAL",
                   "CEC_PRESENT_VERIFIED", "CEC_READ_RESILVER", "CEC_READ_VERIFY_ONLY"):
-        cv = re.search(rf"#define {const}\s+(\d+)u?", hsrc).group(1)
-        rv = re.search(rf"pub const {const}:[^=]+=\s*(\d+);", rsrc).group(1)
-        assert cv == rv, const
+        cv = re.search(rf"#define {const}\s+(0x[0-9a-fA-F]+|\d+)u?", hsrc).group(1)
+        rv = re.search(rf"pub const {const}:[^=]+=\s*(0x[0-9a-fA-F]+|\d+);", rsrc).group(1)
+        assert int(cv, 0) == int(rv, 0), const
 
 
 def test_status_codes_match_the_crate_mapping():
