@@ -804,6 +804,29 @@ def test_read_batch_restores_data_and_reports_undecodable_parts(speculate, monke
         assert torch.equal(got[k, :d], want[k, :d]), k   # data chunks are the read's output
 
 
+def test_read_batch_present_flag_values():
+    """ABI 2: only CEC_PRESENT_VERIFIED (0x80) marks a loaded chunk as trusted (used, not hashed
+    again).  Any other nonzero flag -- 2 included, the ABI-1 value of the trusted mark -- means
+    loaded and hashed, so a corrupt chunk flagged 2 (or 3, or 0xFF) is caught."""
+    d, p, L, n = 4, 2, 1024, 4
+    rs, buf, batch, dig = _encoded_batch(d, p, L, n, 47)
+    t = d + p
+    ref = buf.clone()
+    present = np.ones((n, t), dtype=np.uint8)
+    for k, flag in enumerate([2, 3, 0xFF, ce.PRESENT_VERIFIED]):
+        present[k, 1] = flag
+        buf[k, 1, 5] ^= 0x40  # the flagged chunk is corrupt
+    verified, status = ce.read_batch(rs, batch, present.tobytes(), dig.data_ptr())
+    torch.cuda.synchronize()
+    v = np.frombuffer(verified, np.uint8).reshape(n, t)
+    for k in range(3):  # hashed: fails, dropped, data chunk 1 rebuilt from the other 5
+        assert v[k, 1] == 0 and status[k] == ce.OK, k
+        assert torch.equal(buf[k, :d].cpu(), ref[k, :d].cpu()), k
+    # trusted without hashing: reported verified and used as loaded (the caller vouched for it)
+    assert v[3, 1] == 1 and status[3] == ce.OK
+    assert ce.PRESENT_VERIFIED == 0x80 and ce.abi_version() == 2
+
+
 @pytest.mark.parametrize("variant", ["1", "2"])  # compacted item list in both SHA kernels
 @pytest.mark.parametrize("speculate", ["1", "0"])
 def test_read_batch_random_patterns_vs_oracle(speculate, variant, monkeypatch):
