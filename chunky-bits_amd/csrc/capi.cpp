@@ -614,6 +614,18 @@ struct Arena {
     hipEvent_t encoded = nullptr;
 };
 
+// How the early parity download waits for the encode: on the device (the side stream waits on
+// the encode's event, default) or on the host (the leader blocks on the event, then queues the
+// copy: CEC_COALESCE_D2H_WAIT=host, the round-2 form, kept for the A/B).  Both are deadlock-free
+// (see the wait itself); which is faster is a measurement.
+bool coalesce_d2h_host_wait() {
+    static const bool host = [] {
+        const char* e = std::getenv("CEC_COALESCE_D2H_WAIT");
+        return e && std::strcmp(e, "host") == 0;
+    }();
+    return host;
+}
+
 bool coalesce_early_d2h() {  // default on (profiles/r2_early_d2h/); =0 for A/B
     static const bool on = [] {
         const char* e = std::getenv("CEC_COALESCE_EARLY_D2H");
@@ -1157,7 +1169,10 @@ struct PartImpl {
                 // the host block on the event here, blaming a 256-caller hang on such waits;
                 // that hang was the stranded-caller race fixed below, and the host hand-over
                 // build hung the same way before that fix.)
-                HIP_TRY(hipStreamWaitEvent(a.side, a.encoded, 0));
+                if (coalesce_d2h_host_wait())
+                    HIP_TRY(hipEventSynchronize(a.encoded));
+                else
+                    HIP_TRY(hipStreamWaitEvent(a.side, a.encoded, 0));
                 side_wait.q = a.side;
                 CEC_TRY(parity_down(a.side));
                 parity_sent = true;

@@ -36,8 +36,9 @@ def trace_groups(path):
         return g
     for r in csv.DictReader(open(path)):
         k = short(r["Kernel_Name"])
-        g[(k, int(r["Grid_Size"]))].append((int(r["End_Timestamp"]) -
-                                            int(r["Start_Timestamp"])) / 1e6)
+        grid = int(r["Grid_Size"]) if "Grid_Size" in r else \
+            int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
+        g[(k, grid)].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
     return g
 
 
