@@ -541,9 +541,10 @@ def north_star_block(codec, batch, buf, digests, stream, device, rank, d, p, L, 
         gbs = algo / (ms / 1e3) / 1e9
         # this command's own PMC run (the c2 entries: profiles/summarize_shapes.py keeps the
         # full-size launch of each kernel), else the kernel's own config
-        tr, src = measured_traffic("c2", kernel, True, with_source=True)
+        full = n == CONFIGS["c2"]["parts"]  # the profiled workload; else no committed figure
+        tr, src = measured_traffic("c2", kernel, full, with_source=True)
         if tr is None:
-            tr, src = measured_traffic(cfgkey, kernel, True, with_source=True)
+            tr, src = measured_traffic(cfgkey, kernel, full, with_source=True)
         return {"call": call, "kernel": kernel, "ms": round(ms, 4), "algorithmic_bytes": algo,
                 "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(gbs / HBM_PEAK_GBS, 4), "target_frac": 0.60,
