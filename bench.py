@@ -442,11 +442,8 @@ def end_to_end(codec, d, p, L, gib, world, rank, reduce_dev, host_threads, devic
                     "stamped): the PCIe link with no host production"},
     }
     # the scheduler's pageable path (what `cp` through the C++ FileWriteBuilder batch takes)
-    try:
-        res["scheduler_pageable"] = scheduler_pageable(codec, d, p, L, ring, n_parts, world,
-                                                       reduce_dev, device_ordinal)
-    except Exception as e:  # noqa: BLE001 (reported in the line)
-        res["scheduler_pageable"] = {"value": None, "skipped": f"{type(e).__name__}: {e}"}
+    res["scheduler_pageable"] = scheduler_pageable(codec, d, p, L, ring, n_parts, world,
+                                                   reduce_dev, device_ordinal)
     copier.close()
     return res
 
@@ -459,10 +456,18 @@ def scheduler_pageable(codec, d, p, L, ring, n_parts, world, reduce_dev, device_
     t = d + p
     ring_parts = len(ring)
     S, J = 2 * P, 2
-    m = ce.Multi(codec, L, P, depth, [device_ordinal])
-    outs = [(ce.HostBuffer(S * p * L, device_ordinal), ce.HostBuffer(S * t * 32, device_ordinal))
-            for _ in range(J)]
-    n_jobs = (n_parts + S - 1) // S
+    # every rank must reach the barriers below, or none: a rank that cannot build its scheduler
+    # makes every rank skip this form together
+    try:
+        m, err = ce.Multi(codec, L, P, depth, [device_ordinal]), None
+        outs = [(ce.HostBuffer(S * p * L, device_ordinal),
+                 ce.HostBuffer(S * t * 32, device_ordinal)) for _ in range(J)]
+    except Exception as e:  # noqa: BLE001 (reported in the line)
+        m, outs, err = None, None, f"{type(e).__name__}: {e}"
+    if not all_ranks_ok(err is None, world, reduce_dev):
+        del m, outs
+        return {"value": None, "unit": "GB/s",
+                "skipped": err or "another rank could not build its scheduler"}
 
     def submit(i, first):
         par, dig = outs[i % J]
