@@ -14,6 +14,13 @@
 // reader is finished by then), "same" (Q allocated on A: stream order).  Per trial it prints
 // whether Q == P and how many words the reader saw change.  Any nonzero count means freed memory
 // was handed out and written while a kernel queued before the free was still reading it.
+//
+// Mode "join" is round 2's read-path shape itself: a side stream B waits on a fork event of A,
+// allocates its metadata words with hipMallocAsync, uploads them, queues a host function that
+// releases the host copy, runs a ~10 ms writer kernel (reading the words, writing an output
+// buffer), frees the words with hipFreeAsync and records a join event; A waits on the join and
+// copies the output to the host.  Any output word missing means A's copy ran before B's kernel
+// finished although A waited on B's join.
 //   hipcc --offload-arch=gfx950 -O3 tools/repro_free_async.hip -o tools/repro_free_async
 #include <hip/hip_runtime.h>
 
@@ -46,10 +53,67 @@ __global__ void reader(const uint32_t* p, size_t n, uint32_t expect, int reps, u
     bad[tid] = miss;
 }
 
+// Writes out[i] = words[i % nw] + r for r = 0..reps-1 (the last pass leaves words[i % nw] +
+// reps - 1): slow on purpose, reading the metadata words throughout.
+__global__ void writer(const uint32_t* words, size_t nw, uint32_t* out, size_t n, int reps) {
+    const size_t tid = size_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    const size_t stride = size_t(gridDim.x) * blockDim.x;
+    for (int r = 0; r < reps; ++r)
+        for (size_t i = tid; i < n; i += stride)
+            __builtin_nontemporal_store(__builtin_nontemporal_load(words + i % nw) + uint32_t(r),
+                                        out + i);
+}
+
+void release_host(void* p) { delete static_cast<std::vector<uint32_t>*>(p); }
+
+int run_join(int trials, int reps) {
+    const size_t n = size_t(1) << 22, nw = 4096;
+    hipStream_t A, B;
+    CK(hipStreamCreateWithFlags(&A, hipStreamNonBlocking));
+    CK(hipStreamCreateWithFlags(&B, hipStreamNonBlocking));
+    hipEvent_t fork, join;
+    CK(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+    CK(hipEventCreateWithFlags(&join, hipEventDisableTiming));
+    uint32_t* out = nullptr;
+    CK(hipMalloc(&out, n * sizeof(uint32_t)));
+    std::vector<uint32_t> host(n);
+    int bad_trials = 0;
+    for (int k = 0; k < trials; ++k) {
+        CK(hipMemsetAsync(out, 0, n * sizeof(uint32_t), A));
+        CK(hipEventRecord(fork, A));
+        CK(hipStreamWaitEvent(B, fork, 0));
+        auto* words = new std::vector<uint32_t>(nw);
+        for (size_t i = 0; i < nw; ++i) (*words)[i] = uint32_t(k * 7919 + i) | 1u;
+        uint32_t* dw = nullptr;
+        CK(hipMallocAsync(reinterpret_cast<void**>(&dw), nw * sizeof(uint32_t), B));
+        CK(hipMemcpyAsync(dw, words->data(), nw * sizeof(uint32_t), hipMemcpyHostToDevice, B));
+        std::vector<uint32_t> expect(*words);
+        CK(hipLaunchHostFunc(B, release_host, words));
+        hipLaunchKernelGGL(writer, dim3(kBlocks), dim3(kThreads), 0, B, dw, nw, out, n, reps);
+        CK(hipGetLastError());
+        CK(hipFreeAsync(dw, B));
+        CK(hipEventRecord(join, B));
+        CK(hipStreamWaitEvent(A, join, 0));
+        CK(hipMemcpyAsync(host.data(), out, n * sizeof(uint32_t), hipMemcpyDeviceToHost, A));
+        CK(hipStreamSynchronize(A));
+        size_t wrong = 0;
+        for (size_t i = 0; i < n; ++i) wrong += host[i] != expect[i % nw] + uint32_t(reps - 1);
+        bad_trials += wrong != 0;
+        printf("mode join        trial %2d: output words not yet written when A copied: %zu\n", k,
+               wrong);
+        fflush(stdout);
+        CK(hipStreamSynchronize(B));
+    }
+    printf("mode join: %d trials, output incomplete in %d\n", trials, bad_trials);
+    CK(hipFree(out));
+    return bad_trials ? 3 : 0;
+}
+
 int main(int argc, char** argv) {
     const char* mode = argc > 1 ? argv[1] : "independent";
     const int trials = argc > 2 ? atoi(argv[2]) : 20;
     const int reps = argc > 3 ? atoi(argv[3]) : 64;
+    if (!strcmp(mode, "join")) return run_join(trials, reps);
     const size_t n = size_t(1) << 22;  // 16 MiB of words
     const size_t bytes = n * sizeof(uint32_t);
     hipStream_t A, B;
