@@ -41,16 +41,54 @@
 
 constexpr int kThreads = 256, kBlocks = 1024;
 
-// Every thread re-reads its words of p `reps` times and stores its own mismatch count (a plain
-// per-thread vector store: no atomics).
+// Every thread re-reads its words of p `reps` times and stores its own mismatch count and the
+// last wrong value it saw, and the count over its FIRST pass alone (plain per-thread vector
+// stores: no atomics).
 __global__ void reader(const uint32_t* p, size_t n, uint32_t expect, int reps, uint32_t* bad) {
     const size_t tid = size_t(blockIdx.x) * blockDim.x + threadIdx.x;
     const size_t stride = size_t(gridDim.x) * blockDim.x;
-    uint32_t miss = 0;
+    const size_t nt = stride;
+    uint32_t miss = 0, first = 0, seen = expect;
     for (int r = 0; r < reps; ++r)
-        for (size_t i = tid; i < n; i += stride)
-            miss += __builtin_nontemporal_load(p + i) != expect;
+        for (size_t i = tid; i < n; i += stride) {
+            const uint32_t v = __builtin_nontemporal_load(p + i);
+            if (v != expect) {
+                ++miss;
+                first += r == 0;
+                seen = v;
+            }
+        }
     bad[tid] = miss;
+    bad[nt + tid] = first;
+    bad[2 * nt + tid] = seen;
+}
+
+// The fill as a kernel on the stream (REPRO_FILL=kernel) instead of hipMemsetD32Async.
+__global__ void fill(uint32_t* p, size_t n, uint32_t v) {
+    const size_t stride = size_t(gridDim.x) * blockDim.x;
+    for (size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) p[i] = v;
+}
+
+bool g_fill_kernel = false;
+
+void fill_async(uint32_t* p, uint32_t v, size_t n, hipStream_t s) {
+    if (g_fill_kernel) {
+        hipLaunchKernelGGL(fill, dim3(1024), dim3(256), 0, s, p, n, v);
+        CK(hipGetLastError());
+    } else {
+        CK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p), int(v), n, s));
+    }
+}
+
+// Host buffers: pageable std::vector (default) or page-locked (REPRO_PINNED=1).
+template <typename T>
+T* host_buf(size_t n) {
+    if (getenv("REPRO_PINNED") && getenv("REPRO_PINNED")[0] == '1') {
+        void* p = nullptr;
+        CK(hipHostMalloc(&p, n * sizeof(T), hipHostMallocDefault));
+        return static_cast<T*>(p);
+    }
+    return new T[n];
 }
 
 // Writes out[i] = words[i % nw] + r for r = 0..reps-1 (the last pass leaves words[i % nw] +
@@ -76,10 +114,10 @@ int run_join(int trials, int reps) {
     CK(hipEventCreateWithFlags(&join, hipEventDisableTiming));
     uint32_t* out = nullptr;
     CK(hipMalloc(&out, n * sizeof(uint32_t)));
-    std::vector<uint32_t> host(n);
+    uint32_t* host = host_buf<uint32_t>(n);
     int bad_trials = 0;
     for (int k = 0; k < trials; ++k) {
-        CK(hipMemsetAsync(out, 0, n * sizeof(uint32_t), A));
+        fill_async(out, 0u, n, A);
         CK(hipEventRecord(fork, A));
         CK(hipStreamWaitEvent(B, fork, 0));
         auto* words = new std::vector<uint32_t>(nw);
@@ -94,13 +132,15 @@ int run_join(int trials, int reps) {
         CK(hipFreeAsync(dw, B));
         CK(hipEventRecord(join, B));
         CK(hipStreamWaitEvent(A, join, 0));
-        CK(hipMemcpyAsync(host.data(), out, n * sizeof(uint32_t), hipMemcpyDeviceToHost, A));
+        CK(hipMemcpyAsync(host, out, n * sizeof(uint32_t), hipMemcpyDeviceToHost, A));
         CK(hipStreamSynchronize(A));
-        size_t wrong = 0;
-        for (size_t i = 0; i < n; ++i) wrong += host[i] != expect[i % nw] + uint32_t(reps - 1);
+        size_t wrong = 0, at = 0;
+        for (size_t i = 0; i < n; ++i)
+            if (host[i] != expect[i % nw] + uint32_t(reps - 1) && !wrong++) at = i;
         bad_trials += wrong != 0;
-        printf("mode join        trial %2d: output words not yet written when A copied: %zu\n", k,
-               wrong);
+        printf("mode join        trial %2d: output words not yet written when A copied: %zu "
+               "(first at %zu: %08x, expected %08x)\n", k, wrong, at, host[at],
+               expect[at % nw] + uint32_t(reps - 1));
         fflush(stdout);
         CK(hipStreamSynchronize(B));
     }
@@ -113,6 +153,9 @@ int main(int argc, char** argv) {
     const char* mode = argc > 1 ? argv[1] : "independent";
     const int trials = argc > 2 ? atoi(argv[2]) : 20;
     const int reps = argc > 3 ? atoi(argv[3]) : 64;
+    g_fill_kernel = getenv("REPRO_FILL") && !strcmp(getenv("REPRO_FILL"), "kernel");
+    printf("fill: %s, host buffers: %s\n", g_fill_kernel ? "kernel" : "hipMemsetD32Async",
+           getenv("REPRO_PINNED") && getenv("REPRO_PINNED")[0] == '1' ? "page-locked" : "pageable");
     if (!strcmp(mode, "join")) return run_join(trials, reps);
     const size_t n = size_t(1) << 22;  // 16 MiB of words
     const size_t bytes = n * sizeof(uint32_t);
@@ -125,14 +168,14 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&t1));
     uint32_t* bad = nullptr;
     const size_t nt = size_t(kThreads) * kBlocks;
-    CK(hipMalloc(&bad, nt * sizeof(uint32_t)));
-    std::vector<uint32_t> host(nt);
+    CK(hipMalloc(&bad, 3 * nt * sizeof(uint32_t)));
+    uint32_t* host = host_buf<uint32_t>(3 * nt);
     int reused = 0, corrupted = 0;
     for (int k = 0; k < trials; ++k) {
         uint32_t *P = nullptr, *Q = nullptr;
-        CK(hipMemsetAsync(bad, 0, nt * sizeof(uint32_t), A));
+        CK(hipMemsetAsync(bad, 0, 3 * nt * sizeof(uint32_t), A));
         CK(hipMallocAsync(reinterpret_cast<void**>(&P), bytes, A));
-        CK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(P), 0xA5A5A5A5u, n, A));
+        fill_async(P, 0xA5A5A5A5u, n, A);
         CK(hipEventRecord(t0, A));
         hipLaunchKernelGGL(reader, dim3(kBlocks), dim3(kThreads), 0, A, P, n, 0xA5A5A5A5u, reps,
                            bad);
@@ -147,19 +190,25 @@ int main(int argc, char** argv) {
             qs = A;
         }
         CK(hipMallocAsync(reinterpret_cast<void**>(&Q), bytes, qs));
-        CK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(Q), 0x5A5A5A5Au, n, qs));
+        fill_async(Q, 0x5A5A5A5Au, n, qs);
         CK(hipFreeAsync(Q, qs));
         CK(hipStreamSynchronize(A));
         CK(hipStreamSynchronize(B));
-        CK(hipMemcpy(host.data(), bad, nt * sizeof(uint32_t), hipMemcpyDeviceToHost));
-        unsigned long long miss = 0;
-        for (uint32_t v : host) miss += v;
+        CK(hipMemcpy(host, bad, 3 * nt * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        unsigned long long miss = 0, first = 0;
+        uint32_t seen = 0xA5A5A5A5u;
+        for (size_t i = 0; i < nt; ++i) {
+            miss += host[i];
+            first += host[nt + i];
+            if (host[2 * nt + i] != 0xA5A5A5A5u) seen = host[2 * nt + i];
+        }
         float ms = 0;
         CK(hipEventElapsedTime(&ms, t0, t1));
         reused += P == Q;
         corrupted += miss != 0;
-        printf("mode %-11s trial %2d: reader %.1f ms, Q %s P, words changed under the reader: "
-               "%llu\n", mode, k, ms, P == Q ? "==" : "!=", miss);
+        printf("mode %-11s trial %2d: P %p Q %p, reader %.1f ms, wrong words seen: %llu (first "
+               "pass %llu, a wrong value: %08x)\n", mode, k, static_cast<void*>(P),
+               static_cast<void*>(Q), ms, miss, first, seen);
         fflush(stdout);
     }
     printf("mode %s: %d trials, Q reused P's address %d times, reader saw changed words in %d\n",
