@@ -70,6 +70,9 @@ __global__ void fill(uint32_t* p, size_t n, uint32_t v) {
 }
 
 bool g_fill_kernel = false;
+// REPRO_FREE=late: free only after the streams are synchronized (control); default: the free is
+// queued right behind the work that uses the memory, as stream-ordered allocation allows.
+bool g_free_late = false;
 
 void fill_async(uint32_t* p, uint32_t v, size_t n, hipStream_t s) {
     if (g_fill_kernel) {
@@ -129,7 +132,7 @@ int run_join(int trials, int reps) {
         CK(hipLaunchHostFunc(B, release_host, words));
         hipLaunchKernelGGL(writer, dim3(kBlocks), dim3(kThreads), 0, B, dw, nw, out, n, reps);
         CK(hipGetLastError());
-        CK(hipFreeAsync(dw, B));
+        if (!g_free_late) CK(hipFreeAsync(dw, B));
         CK(hipEventRecord(join, B));
         CK(hipStreamWaitEvent(A, join, 0));
         CK(hipMemcpyAsync(host, out, n * sizeof(uint32_t), hipMemcpyDeviceToHost, A));
@@ -138,6 +141,10 @@ int run_join(int trials, int reps) {
         for (size_t i = 0; i < n; ++i)
             if (host[i] != expect[i % nw] + uint32_t(reps - 1) && !wrong++) at = i;
         bad_trials += wrong != 0;
+        if (g_free_late) {
+            CK(hipStreamSynchronize(B));
+            CK(hipFreeAsync(dw, B));
+        }
         printf("mode join        trial %2d: output words not yet written when A copied: %zu "
                "(first at %zu: %08x, expected %08x)\n", k, wrong, at, host[at],
                expect[at % nw] + uint32_t(reps - 1));
@@ -154,6 +161,16 @@ int main(int argc, char** argv) {
     const int trials = argc > 2 ? atoi(argv[2]) : 20;
     const int reps = argc > 3 ? atoi(argv[3]) : 64;
     g_fill_kernel = getenv("REPRO_FILL") && !strcmp(getenv("REPRO_FILL"), "kernel");
+    g_free_late = getenv("REPRO_FREE") && !strcmp(getenv("REPRO_FREE"), "late");
+    // REPRO_THRESHOLD=max: the default pool keeps freed memory (never trims it at sync points)
+    if (getenv("REPRO_THRESHOLD") && !strcmp(getenv("REPRO_THRESHOLD"), "max")) {
+        hipMemPool_t pool;
+        CK(hipDeviceGetDefaultMemPool(&pool, 0));
+        uint64_t thr = ~uint64_t(0);
+        CK(hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr));
+    }
+    printf("free: %s, pool release threshold: %s\n", g_free_late ? "after sync" : "stream-ordered",
+           getenv("REPRO_THRESHOLD") ? getenv("REPRO_THRESHOLD") : "default");
     printf("fill: %s, host buffers: %s\n", g_fill_kernel ? "kernel" : "hipMemsetD32Async",
            getenv("REPRO_PINNED") && getenv("REPRO_PINNED")[0] == '1' ? "page-locked" : "pageable");
     if (!strcmp(mode, "join")) return run_join(trials, reps);
@@ -181,7 +198,7 @@ int main(int argc, char** argv) {
                            bad);
         CK(hipGetLastError());
         CK(hipEventRecord(t1, A));
-        CK(hipFreeAsync(P, A));
+        if (!g_free_late) CK(hipFreeAsync(P, A));
         hipStream_t qs = B;
         if (!strcmp(mode, "event")) {
             CK(hipEventRecord(freed, A));
@@ -191,9 +208,13 @@ int main(int argc, char** argv) {
         }
         CK(hipMallocAsync(reinterpret_cast<void**>(&Q), bytes, qs));
         fill_async(Q, 0x5A5A5A5Au, n, qs);
-        CK(hipFreeAsync(Q, qs));
+        if (!g_free_late) CK(hipFreeAsync(Q, qs));
         CK(hipStreamSynchronize(A));
         CK(hipStreamSynchronize(B));
+        if (g_free_late) {
+            CK(hipFreeAsync(P, A));
+            CK(hipFreeAsync(Q, qs));
+        }
         CK(hipMemcpy(host, bad, 3 * nt * sizeof(uint32_t), hipMemcpyDeviceToHost));
         unsigned long long miss = 0, first = 0;
         uint32_t seen = 0xA5A5A5A5u;
