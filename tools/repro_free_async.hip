@@ -156,6 +156,60 @@ int run_join(int trials, int reps) {
     return bad_trials ? 3 : 0;
 }
 
+// Mode "fresh": every trial gets newly mapped device memory -- hipMalloc (REPRO_ALLOC=sync) or
+// hipMallocAsync after trimming the default pool to 0 (REPRO_ALLOC=async, the default) -- fills
+// it with a kernel right away and runs the reader.  Wrong words in a later pass of the reader
+// (the first pass right) mean the memory changed under a kernel that was the only user of it:
+// e.g. the driver's clear of a fresh allocation landing after the user's first writes.
+int run_fresh(int trials, int reps) {
+    const size_t n = size_t(1) << 22, bytes = n * sizeof(uint32_t);
+    const bool sync_alloc = getenv("REPRO_ALLOC") && !strcmp(getenv("REPRO_ALLOC"), "sync");
+    hipStream_t A;
+    CK(hipStreamCreateWithFlags(&A, hipStreamNonBlocking));
+    hipMemPool_t pool;
+    CK(hipDeviceGetDefaultMemPool(&pool, 0));
+    uint32_t* bad = nullptr;
+    const size_t nt = size_t(kThreads) * kBlocks;
+    CK(hipMalloc(&bad, 3 * nt * sizeof(uint32_t)));
+    uint32_t* host = host_buf<uint32_t>(3 * nt);
+    int corrupted = 0;
+    for (int k = 0; k < trials; ++k) {
+        uint32_t* P = nullptr;
+        CK(hipMemsetAsync(bad, 0, 3 * nt * sizeof(uint32_t), A));
+        if (sync_alloc) {
+            CK(hipMalloc(reinterpret_cast<void**>(&P), bytes));
+        } else {
+            CK(hipMemPoolTrimTo(pool, 0));
+            CK(hipMallocAsync(reinterpret_cast<void**>(&P), bytes, A));
+        }
+        fill_async(P, 0xA5A5A5A5u, n, A);
+        hipLaunchKernelGGL(reader, dim3(kBlocks), dim3(kThreads), 0, A, P, n, 0xA5A5A5A5u, reps,
+                           bad);
+        CK(hipGetLastError());
+        CK(hipStreamSynchronize(A));
+        CK(hipMemcpy(host, bad, 3 * nt * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        unsigned long long miss = 0, first = 0;
+        uint32_t seen = 0xA5A5A5A5u;
+        for (size_t i = 0; i < nt; ++i) {
+            miss += host[i];
+            first += host[nt + i];
+            if (host[2 * nt + i] != 0xA5A5A5A5u) seen = host[2 * nt + i];
+        }
+        corrupted += miss != 0;
+        printf("mode fresh (%s) trial %2d: P %p, wrong words seen: %llu (first pass %llu, a wrong "
+               "value: %08x)\n", sync_alloc ? "hipMalloc" : "hipMallocAsync after trim", k,
+               static_cast<void*>(P), miss, first, seen);
+        fflush(stdout);
+        if (sync_alloc) CK(hipFree(P));
+        else CK(hipFreeAsync(P, A));
+        CK(hipStreamSynchronize(A));
+    }
+    printf("mode fresh (%s): %d trials, reader saw changed words in %d\n",
+           sync_alloc ? "hipMalloc" : "hipMallocAsync after trim", trials, corrupted);
+    CK(hipFree(bad));
+    return corrupted ? 3 : 0;
+}
+
 int main(int argc, char** argv) {
     const char* mode = argc > 1 ? argv[1] : "independent";
     const int trials = argc > 2 ? atoi(argv[2]) : 20;
@@ -174,6 +228,7 @@ int main(int argc, char** argv) {
     printf("fill: %s, host buffers: %s\n", g_fill_kernel ? "kernel" : "hipMemsetD32Async",
            getenv("REPRO_PINNED") && getenv("REPRO_PINNED")[0] == '1' ? "page-locked" : "pageable");
     if (!strcmp(mode, "join")) return run_join(trials, reps);
+    if (!strcmp(mode, "fresh")) return run_fresh(trials, reps);
     const size_t n = size_t(1) << 22;  // 16 MiB of words
     const size_t bytes = n * sizeof(uint32_t);
     hipStream_t A, B;
