@@ -71,11 +71,15 @@ bool aligned16(const void* p, size_t a, size_t b) {
 // ------------------------------------------------------------------------------------------
 // Small per-launch device buffers (decode pattern records, verify item lists, flag arrays).
 //
-// Not hipMallocAsync / hipFreeAsync: on this ROCm, stream work queued behind a hipFreeAsync of a
-// buffer a kernel was still reading did not reliably wait for that kernel — read and resilver
-// batches came back with chunks the decode had not yet (re)written, timing-dependent (the C++
-// mirror's batched verify/resilver and streamed reads, 4 of 4 runs; with the frees removed, 0
-// of 2).  Instead a process-wide pool of device buffers, each with a page-locked host mirror
+// Not hipMallocAsync / hipFreeAsync: with them, read and resilver batches came back with chunks
+// the decode had not (re)written (round 2: the C++ mirror's batched verify/resilver and streamed
+// reads, 4 of 4 runs).  tools/repro_free_async.hip shows why, with no engine code: on this
+// ROCm, memory hipMallocAsync maps fresh (the default pool trimmed) is, on some boxes and every
+// other allocation, zeroed AFTER the stream's first writes to it -- a kernel that filled it reads
+// zeros on its later passes, and metadata words uploaded into it read as zeros (round 2's
+// fork/join read shape loses whole outputs the same way, with the free queued behind the work
+// or only after a sync).  hipMalloc'd memory never showed it (profiles/r3_repro/).
+// Instead a process-wide pool of device buffers, each with a page-locked host mirror
 // and an event: a buffer is handed out only once the event recorded after its last use has
 // completed, the words go up from the mirror (a truly asynchronous copy, no host lifetime to
 // manage), and its release records the event on the stream of the work that used it.

@@ -17,7 +17,7 @@
 //
 // Mode "join" is round 2's read-path shape itself: a side stream B waits on a fork event of A,
 // allocates its metadata words with hipMallocAsync, uploads them, queues a host function that
-// releases the host copy, runs a ~10 ms writer kernel (reading the words, writing an output
+// releases the host copy, runs a slow writer kernel (reading the words, writing an output
 // buffer), frees the words with hipFreeAsync and records a join event; A waits on the join and
 // copies the output to the host.  Any output word missing means A's copy ran before B's kernel
 // finished although A waited on B's join.
