@@ -64,6 +64,66 @@ __global__ void stream_kernel(uint8_t* base, uint32_t tiles_per_part, size_t cs)
     }
 }
 
+// Loads and stores with separate cache policies (round 3): NTL non-temporal loads, NTS
+// non-temporal stores; XCD=true maps blocks so that each of the 8 XCDs (blocks are dealt to them
+// round-robin) walks its own contiguous run of parts.
+template <int V, bool NTL, bool NTS, bool XCD>
+__global__ void stream_mix_kernel(uint8_t* base, uint32_t tiles_per_part, uint32_t n_blocks) {
+    uint32_t b = blockIdx.x;
+    if (XCD) {  // block b runs on XCD b % 8: give XCD x the blocks [x*n/8, (x+1)*n/8)
+        const uint32_t per = n_blocks / 8;
+        b = (b % 8) * per + b / 8;
+    }
+    const uint32_t part = b / tiles_per_part;
+    const uint32_t tile = b - part * tiles_per_part;
+    uint8_t* pb = base + size_t(part) * T * L;
+    const size_t x = size_t(tile) * blockDim.x * 16 * V + size_t(threadIdx.x) * 16;
+    v4u acc[V];
+    for (int u = 0; u < V; ++u) acc[u] = v4u{0, 0, 0, 0};
+    v4u in[D][V];
+#pragma unroll
+    for (int j = 0; j < D; ++j)
+#pragma unroll
+        for (int u = 0; u < V; ++u) in[j][u] = ld<NTL>(pb + j * L + x + size_t(u) * blockDim.x * 16);
+#pragma unroll
+    for (int j = 0; j < D; ++j)
+#pragma unroll
+        for (int u = 0; u < V; ++u) acc[u] ^= in[j][u];
+#pragma unroll
+    for (int r = 0; r < P; ++r)
+#pragma unroll
+        for (int u = 0; u < V; ++u)
+            st<NTS>(pb + (D + r) * L + x + size_t(u) * blockDim.x * 16,
+                    acc[u] + v4u{unsigned(r), unsigned(r), unsigned(r), unsigned(r)});
+}
+
+template <int V, bool NTL, bool NTS, bool XCD>
+void run_mix(uint8_t* base, uint32_t parts) {
+    const uint32_t tiles = uint32_t(L / (size_t(256) * 16 * V));
+    const uint32_t n = parts * tiles;
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    float best = 1e30f, sum = 0;
+    for (int r = 0; r < 8; ++r) {
+        CK(hipEventRecord(a));
+        hipLaunchKernelGGL((stream_mix_kernel<V, NTL, NTS, XCD>), dim3(n), dim3(256), 0, 0, base,
+                           tiles, n);
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        float ms;
+        CK(hipEventElapsedTime(&ms, a, b));
+        if (r) {
+            sum += ms;
+            if (ms < best) best = ms;
+        }
+    }
+    const double bytes = double(parts) * T * L;
+    printf("mix V %d nt-load %d nt-store %d xcd-map %d : best %8.3f ms %7.0f GB/s, mean %7.0f GB/s\n",
+           V, int(NTL), int(NTS), int(XCD), best, bytes / best / 1e6, bytes / (sum / 7) / 1e6);
+    fflush(stdout);
+}
+
 // Reconstruct-shaped pattern: the D inputs read, W (< P) outputs written (a 2-erasure
 // reconstruct_data writes 1-2 data chunks per part).
 template <int V, bool NT, int W>
@@ -230,6 +290,19 @@ int main(int argc, char** argv) {
         run_w<1, true, 2>(base, parts, 256);
         run_w<2, false, 2>(base, parts, 256);
         run_w<2, true, 2>(base, parts, 512);
+        return 0;
+    }
+    if (argc > 2 && argv[2][0] == 'm') {  // load / store policies and XCD-aware block mapping
+        for (int rep = 0; rep < 2; ++rep) {
+            run_mix<2, true, true, false>(base, parts);
+            run_mix<2, true, false, false>(base, parts);
+            run_mix<2, false, true, false>(base, parts);
+            run_mix<2, false, false, false>(base, parts);
+            run_mix<2, true, true, true>(base, parts);
+            run_mix<2, true, false, true>(base, parts);
+            run_mix<4, true, true, false>(base, parts);
+            run_mix<4, true, false, false>(base, parts);
+        }
         return 0;
     }
     if (argc > 2 && argv[2][0] == 'p') {  // chunk-stride pad sweep of the best shapes
