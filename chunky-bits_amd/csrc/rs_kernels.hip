@@ -160,14 +160,30 @@ __device__ __forceinline__ void apply_tile(const ApplyParams& a, cu32* pat, uint
     }
 }
 
+// XCD-aware block order.  The dispatcher deals a grid's blocks to the 8 XCDs round-robin (block
+// b to XCD b % 8), so in launch order neighbouring tiles of a part land on different XCDs and
+// every XCD streams a slice of every part at once.  Renumbering so that XCD x runs the contiguous
+// range [x*q + min(x, r), ...) of the n blocks (q = n / 8, r = n % 8: a bijection for any n)
+// gives each XCD whole runs of parts instead.  For the 10-read / 4-write stream of an RS(10,4)
+// encode with no GF work this lifts the chip from 5.72-5.74 to 6.26-6.27 TB/s
+// (tools/ubench_stream.hip mode m, profiles/r3_full/ubench_mix.log).
+constexpr uint32_t kXcds = 8;
+
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t n) {
+    const uint32_t x = b % kXcds, i = b / kXcds, q = n / kXcds, r = n % kXcds;
+    return x * q + (x < r ? x : r) + i;
+}
+
 // grid.x = n_parts * tiles_per_part (one 16 KiB column tile of one part per block),
-// grid.y = row groups of exactly RG output rows starting at row_base.
+// grid.y = row groups of exactly RG output rows starting at row_base.  xcd: block order of
+// xcd_block (else launch order).
 template <int RG, bool VEC, int GROUP, int V, bool NT>
 __global__ __launch_bounds__(kApplyThreads) void rs_apply_kernel(ApplyParams a,
                                                                  uint32_t tiles_per_part,
-                                                                 uint32_t row_base) {
-    const uint32_t lp = blockIdx.x / tiles_per_part;
-    const uint32_t tile = blockIdx.x - lp * tiles_per_part;
+                                                                 uint32_t row_base, bool xcd) {
+    const uint32_t bx = xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint32_t lp = bx / tiles_per_part;
+    const uint32_t tile = bx - lp * tiles_per_part;
     const uint32_t part = a.part_ids ? as_const(a.part_ids)[lp] : lp;
     cu32* pat = as_const(a.pat) + (a.part_pat ? as_const(a.part_pat)[lp] : 0u);
     apply_tile<RG, VEC, GROUP, V, NT>(a, pat, part, tile, a.n_rows, row_base + blockIdx.y * RG);
@@ -178,9 +194,11 @@ __global__ __launch_bounds__(kApplyThreads) void rs_apply_kernel(ApplyParams a,
 // to the exact-RG body, so no row is predicated inside the inner loop.
 template <bool VEC, int GROUP, int V, bool NT>
 __global__ __launch_bounds__(kApplyThreads) void rs_apply_var_kernel(ApplyParams a,
-                                                                     uint32_t tiles_per_part) {
-    const uint32_t lp = blockIdx.x / tiles_per_part;
-    const uint32_t tile = blockIdx.x - lp * tiles_per_part;
+                                                                     uint32_t tiles_per_part,
+                                                                     bool xcd) {
+    const uint32_t bx = xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint32_t lp = bx / tiles_per_part;
+    const uint32_t tile = bx - lp * tiles_per_part;
     const uint32_t part = as_const(a.part_ids)[lp];
     cu32* pat = as_const(a.pat) + as_const(a.part_pat)[lp];
     switch (pat[0]) {
@@ -250,6 +268,13 @@ int apply_tune() {
     if (!e) return 1;
     return (std::strstr(e, "nt") ? 1 : 0) | (std::strstr(e, "g8") ? 2 : 0) |
            (std::strstr(e, "v1") ? 4 : 0);
+}
+
+// CEC_APPLY_XCD (A/B knob, read per launch; unset = 1): 0 launches the apply kernels' blocks in
+// plain launch order instead of the XCD-aware order (xcd_block).
+bool apply_xcd() {
+    const char* e = std::getenv("CEC_APPLY_XCD");
+    return !(e && e[0] == '0');
 }
 
 // Launch KERNEL<PRE... VEC, GROUP, V, NT> as picked by the tuning knob; layouts that are not
@@ -329,7 +354,7 @@ hipError_t launch_rg(const ApplyParams& a, uint32_t row_base, uint32_t groups, b
             if (!allow_lds(kern, b.lds_reserve)) return hipErrorInvalidValue;
             clear_stale_error();
             hipLaunchKernelGGL(kern, grid, dim3(kApplyThreads), b.lds_reserve, s, b,
-                               uint32_t(tiles), row_base);
+                               uint32_t(tiles), row_base, apply_xcd());
             return hipGetLastError();
         });
     });
@@ -379,7 +404,7 @@ hipError_t launch_rs_apply_var(const ApplyParams& a, bool vec16, hipStream_t s) 
             if (!allow_lds(kern, b.lds_reserve)) return hipErrorInvalidValue;
             clear_stale_error();
             hipLaunchKernelGGL(kern, grid, dim3(kApplyThreads), b.lds_reserve, s, b,
-                               uint32_t(tiles));
+                               uint32_t(tiles), apply_xcd());
             return hipGetLastError();
         });
     });
