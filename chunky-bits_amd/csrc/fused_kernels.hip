@@ -36,6 +36,43 @@ constexpr uint32_t kShaLanes = 256;   // SHA lanes of the one-wave-per-SIMD buil
 constexpr uint32_t kEncThreads = 256;  // 4 encoder waves in every build
 constexpr int kMaxFusedData = 16;  // generic build: d <= 16 (RS(20,p) has its own build)
 
+// 4x4 byte transpose: r_k byte i = a_i byte k.  acc words hold, per data byte position, the
+// products of all parity rows (row r in byte r); the transpose turns 4 byte positions into one
+// output word per row.  8 v_perm per 4 words.
+__device__ __forceinline__ void transpose4(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3,
+                                           uint32_t r[4]) {
+    const uint32_t t01 = perm(a1, a0, 0x05010400u), t23 = perm(a3, a2, 0x05010400u);
+    const uint32_t u01 = perm(a1, a0, 0x07030602u), u23 = perm(a3, a2, 0x07030602u);
+    r[0] = perm(t23, t01, 0x05040100u);
+    r[1] = perm(t23, t01, 0x07060302u);
+    r[2] = perm(u23, u01, 0x05040100u);
+    r[3] = perm(u23, u01, 0x07060302u);
+}
+
+// Byte k of w times E (E = 4 or 8): one SDWA shift (src1_sel picks the byte, zero-extended).
+// The compiler's own form is v_bfe + v_lshl_add (two ops, one of them half-rate).
+template <int E>
+__device__ __forceinline__ uint32_t byte_scaled(uint32_t w, int k) {
+    static_assert(E == 4 || E == 8, "entry size");
+    uint32_t r;
+    if (E == 4) {
+        switch (k) {
+            case 0: asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(r) : "v"(w)); break;
+            case 1: asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(w)); break;
+            case 2: asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(w)); break;
+            default: asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(w)); break;
+        }
+    } else {
+        switch (k) {
+            case 0: asm("v_lshlrev_b32_sdwa %0, 3, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(r) : "v"(w)); break;
+            case 1: asm("v_lshlrev_b32_sdwa %0, 3, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(w)); break;
+            case 2: asm("v_lshlrev_b32_sdwa %0, 3, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(w)); break;
+            default: asm("v_lshlrev_b32_sdwa %0, 3, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(w)); break;
+        }
+    }
+    return r;
+}
+
 constexpr int col_width(int dmax) { return dmax > kMaxFusedData ? 8 : 16; }
 
 // NW words (NW*4 bytes) of one column: a full 16- or 8-byte load, or the n < NW*4 bytes of a

@@ -21,9 +21,6 @@ struct ApplyParams {
     uint32_t n_parts;
     uint32_t d;
     uint32_t n_rows;  // n_out shared by every pattern of this launch
-    // rs_apply_var launches (n_rows == 0): the largest row count among the listed patterns
-    // (0 = unknown: up to 8).  Picks the LDS path's 4- or 8-byte table entries.
-    uint32_t max_rows;
     // Dynamic LDS each workgroup reserves (never touched; 0 = none).  Above 64 KiB a block
     // cannot share a CU with a SHA-256 lane-kernel workgroup (>= 64 KiB reserved each), which
     // keeps a decode running beside a verification off the SHA waves' SIMDs.

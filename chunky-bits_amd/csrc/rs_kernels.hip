@@ -215,213 +215,6 @@ __global__ __launch_bounds__(kApplyThreads) void rs_apply_var_kernel(ApplyParams
 }
 
 // ------------------------------------------------------------------------------------------
-// LDS product-table path (aligned layouts, d <= 32).
-//
-// The v_perm multiply above costs ~25-30 VALU per data dword for RS(10,4) (3 half-rate v_perm
-// + an xor per row, plus the selectors), which keeps the VALU ~70 % busy at the HBM rate.  Here
-// each block first builds, in LDS, one table per input j: entry x (E = 4 bytes for <= 4 rows, 8
-// for <= 8) packs coef[r][j] (x) x for every row r of the block's row group.  A data byte then
-// costs one SDWA address op + one ds_read, and inputs in pairs fold into the accumulators with
-// one full-rate xor3: ~7 VALU per data dword, plus a 4x4 byte transpose per output word (the
-// accumulators hold, per byte position, all rows).  Tables are built once per block from the
-// pattern record's coefficient tables (256 threads = 256 byte values), so blocks take 64 KiB
-// column tiles to amortize them.
-// ------------------------------------------------------------------------------------------
-
-constexpr uint64_t kLdsTile = 65536;  // bytes of one part's column range per block (LDS path)
-
-template <int RG, int E>
-__device__ __forceinline__ void build_tables(uint8_t* tabs, cu32* tab, uint32_t tab_stride,
-                                             uint32_t d) {
-    static_assert(RG <= E, "rows per entry");
-    const uint32_t x = threadIdx.x;  // kApplyThreads == 256 byte values
-    const Sel sx = selectors(x);
-#pragma unroll 1
-    for (uint32_t j = 0; j < d; ++j) {
-        uint32_t lo = 0u, hi = 0u;
-        cu32* tj = tab + size_t(j) * tab_stride;
-#pragma unroll
-        for (int r = 0; r < RG; ++r) {
-            cu32* c = tj + r * kTabWords;
-            const uint32_t prod = gmul(sx, c[0], c[1], c[2], c[3], c[4]) & 0xFFu;
-            if (r < 4) lo |= prod << (8 * r);
-            else hi |= prod << (8 * (r - 4));
-        }
-        uint32_t* e = reinterpret_cast<uint32_t*>(tabs + (size_t(j) * 256 + x) * E);
-        e[0] = lo;
-        if (E == 8) e[1] = hi;
-    }
-}
-
-// Entry of input slot j for the byte k of word w: lo (and hi for E == 8) halves.  j is an
-// unrolled loop index, so its table offset folds into the ds_read's instruction offset.
-template <int E>
-__device__ __forceinline__ uint2 lookup(const uint8_t* tabs, int j, uint32_t w, int k) {
-    const uint8_t* t = tabs + size_t(j) * 256 * E + byte_scaled<E>(w, k);
-    if (E == 4) return make_uint2(*reinterpret_cast<const uint32_t*>(t), 0u);
-    return *reinterpret_cast<const uint2*>(t);
-}
-
-// V full 16-byte columns (x + c*kSpan) of a part, every input through the LDS tables.
-template <int RG, int E, int DMAX, int GROUP, int V>
-__device__ __forceinline__ void apply_column_lds(uint8_t* pbase, uint64_t cs, uint64_t x,
-                                                 uint32_t d, cu32* in_idx, cu32* out_idx,
-                                                 const uint8_t* tabs) {
-    static_assert(GROUP % 2 == 0 && DMAX % GROUP == 0, "inputs go in pairs");
-    uint32_t lo[V][16], hi[V][16];
-#pragma unroll
-    for (int c = 0; c < V; ++c)
-#pragma unroll
-        for (int b = 0; b < 16; ++b) lo[c][b] = hi[c][b] = 0u;
-#pragma unroll
-    for (int j0 = 0; j0 < DMAX; j0 += GROUP) {
-        if (uint32_t(j0) >= d) break;  // block-uniform
-        uint4 v[GROUP][V];
-#pragma unroll
-        for (int u = 0; u < GROUP; ++u) {
-#pragma unroll
-            for (int c = 0; c < V; ++c) v[u][c] = make_uint4(0u, 0u, 0u, 0u);
-            if (uint32_t(j0 + u) < d) {
-                const uint8_t* src = pbase + uint64_t(in_idx[j0 + u]) * cs + x;
-#pragma unroll
-                for (int c = 0; c < V; ++c) v[u][c] = ld16<true>(src + c * kSpan);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < GROUP; u += 2) {
-            // block-uniform branches around whole loops, so the ds_reads of a loop issue back to
-            // back (a branch per lookup would wait for each one)
-            if (uint32_t(j0 + u + 1) < d) {
-#pragma unroll
-                for (int c = 0; c < V; ++c) {
-                    const uint32_t w0[4] = {v[u][c].x, v[u][c].y, v[u][c].z, v[u][c].w};
-                    const uint32_t w1[4] = {v[u + 1][c].x, v[u + 1][c].y, v[u + 1][c].z,
-                                            v[u + 1][c].w};
-#pragma unroll
-                    for (int b = 0; b < 16; ++b) {
-                        const uint2 e0 = lookup<E>(tabs, j0 + u, w0[b >> 2], b & 3);
-                        const uint2 e1 = lookup<E>(tabs, j0 + u + 1, w1[b >> 2], b & 3);
-                        lo[c][b] = xor3(lo[c][b], e0.x, e1.x);
-                        if (E == 8) hi[c][b] = xor3(hi[c][b], e0.y, e1.y);
-                    }
-                }
-            } else if (uint32_t(j0 + u) < d) {
-#pragma unroll
-                for (int c = 0; c < V; ++c) {
-                    const uint32_t w0[4] = {v[u][c].x, v[u][c].y, v[u][c].z, v[u][c].w};
-#pragma unroll
-                    for (int b = 0; b < 16; ++b) {
-                        const uint2 e0 = lookup<E>(tabs, j0 + u, w0[b >> 2], b & 3);
-                        lo[c][b] ^= e0.x;
-                        if (E == 8) hi[c][b] ^= e0.y;
-                    }
-                }
-            }
-        }
-    }
-#pragma unroll
-    for (int c = 0; c < V; ++c) {
-        uint32_t out[8][4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            uint32_t r4[4];
-            transpose4(lo[c][4 * q], lo[c][4 * q + 1], lo[c][4 * q + 2], lo[c][4 * q + 3], r4);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) out[r][q] = r4[r];
-            if (E == 8) {
-                transpose4(hi[c][4 * q], hi[c][4 * q + 1], hi[c][4 * q + 2], hi[c][4 * q + 3], r4);
-#pragma unroll
-                for (int r = 0; r < 4; ++r) out[4 + r][q] = r4[r];
-            }
-        }
-#pragma unroll
-        for (int r = 0; r < RG; ++r)
-            st16<true>(pbase + uint64_t(out_idx[r]) * cs + x + c * kSpan,
-                       make_uint4(out[r][0], out[r][1], out[r][2], out[r][3]));
-    }
-}
-
-// One kLdsTile column range of one part for rows [row0, row0 + RG) of its n_out-row pattern:
-// tables, then the full columns through them and a ragged end (if any) through the byte-granular
-// v_perm path.  Every thread of the block reaches the table barrier.
-template <int RG, int E, int DMAX, int GROUP, int V>
-__device__ __forceinline__ void apply_tile_lds(const ApplyParams& a, cu32* pat, uint32_t part,
-                                               uint32_t tile, uint32_t n_out, uint32_t row0,
-                                               uint8_t* tabs) {
-    const uint32_t d = a.d;
-    cu32* in_idx = pat + 1;
-    cu32* out_idx = pat + 1 + d + row0;
-    cu32* tab = pat + 1 + d + n_out + size_t(row0) * kTabWords;
-    const uint32_t tab_stride = n_out * kTabWords;
-    build_tables<RG, E>(tabs, tab, tab_stride, d);
-    __syncthreads();
-    uint8_t* pbase = a.base + uint64_t(part) * a.part_stride;
-    const uint64_t len = a.len;
-    const uint64_t cs = a.chunk_stride;
-    const uint64_t t0 = uint64_t(tile) * kLdsTile;
-    const uint64_t t1 = t0 + kLdsTile < len ? t0 + kLdsTile : len;
-#pragma unroll 1
-    for (uint64_t xb = t0; xb < t1; xb += kSpan * V) {  // block-uniform
-        const uint64_t x = xb + uint64_t(threadIdx.x) * 16u;
-        if (xb + kSpan * V <= len) {
-            apply_column_lds<RG, E, DMAX, GROUP, V>(pbase, cs, x, d, in_idx, out_idx, tabs);
-        } else {
-#pragma unroll 1
-            for (uint64_t xc = x; xc < t1 && xc < xb + kSpan * V; xc += kSpan)
-                apply_column<RG, false, 4, 1, false>(pbase, cs, xc, len - xc, d, tab_stride,
-                                                     in_idx, out_idx, tab);
-        }
-    }
-}
-
-// The tables live in static LDS (sized for DMAX inputs): fixed addresses, so an input's table
-// base is a ds_read instruction offset.  Dynamic LDS (lds_reserve beyond it) is only reserved.
-template <int RG, int DMAX>
-__global__ __launch_bounds__(kApplyThreads) void rs_apply_lds_kernel(ApplyParams a,
-                                                                     uint32_t tiles_per_part,
-                                                                     uint32_t row_base, bool xcd) {
-    __shared__ __attribute__((aligned(16))) uint8_t tabs[DMAX * 256 * (RG <= 4 ? 4 : 8)];
-    const uint32_t bx = xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
-    const uint32_t lp = bx / tiles_per_part;
-    const uint32_t tile = bx - lp * tiles_per_part;
-    const uint32_t part = a.part_ids ? as_const(a.part_ids)[lp] : lp;
-    cu32* pat = as_const(a.pat) + (a.part_pat ? as_const(a.part_pat)[lp] : 0u);
-    apply_tile_lds<RG, (RG <= 4 ? 4 : 8), DMAX, 4, 2>(a, pat, part, tile, a.n_rows,
-                                                     row_base + blockIdx.y * RG, tabs);
-}
-
-// MAXRG: the launch's largest row count class (4: every pattern has <= 4 rows, 4-byte entries
-// and a register budget for 4 rows; 8: up to 8).
-template <int DMAX, int MAXRG>
-__global__ __launch_bounds__(kApplyThreads) void rs_apply_var_lds_kernel(ApplyParams a,
-                                                                         uint32_t tiles_per_part,
-                                                                         bool xcd) {
-    __shared__ __attribute__((aligned(16))) uint8_t tabs[DMAX * 256 * (MAXRG <= 4 ? 4 : 8)];
-    const uint32_t bx = xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
-    const uint32_t lp = bx / tiles_per_part;
-    const uint32_t tile = bx - lp * tiles_per_part;
-    const uint32_t part = as_const(a.part_ids)[lp];
-    cu32* pat = as_const(a.pat) + as_const(a.part_pat)[lp];
-    switch (pat[0]) {
-        case 1: apply_tile_lds<1, 4, DMAX, 4, 2>(a, pat, part, tile, 1, 0, tabs); break;
-        case 2: apply_tile_lds<2, 4, DMAX, 4, 2>(a, pat, part, tile, 2, 0, tabs); break;
-        case 3: apply_tile_lds<3, 4, DMAX, 4, 2>(a, pat, part, tile, 3, 0, tabs); break;
-        case 4: apply_tile_lds<4, 4, DMAX, 4, 2>(a, pat, part, tile, 4, 0, tabs); break;
-        default:
-            if (MAXRG > 4) {
-                switch (pat[0]) {
-                    case 5: apply_tile_lds<5, 8, DMAX, 4, 2>(a, pat, part, tile, 5, 0, tabs); break;
-                    case 6: apply_tile_lds<6, 8, DMAX, 4, 2>(a, pat, part, tile, 6, 0, tabs); break;
-                    case 7: apply_tile_lds<7, 8, DMAX, 4, 2>(a, pat, part, tile, 7, 0, tabs); break;
-                    case 8: apply_tile_lds<8, 8, DMAX, 4, 2>(a, pat, part, tile, 8, 0, tabs); break;
-                    default: break;  // the host routes n_out > 8 to row-group launches
-                }
-            }
-            break;
-    }
-}
-
-// ------------------------------------------------------------------------------------------
 // Synthetic data
 // ------------------------------------------------------------------------------------------
 
@@ -547,44 +340,9 @@ hipError_t for_part_ranges(const ApplyParams& a, uint64_t max_parts, Fn fn) {
     return hipSuccess;
 }
 
-// CEC_APPLY_LDS (A/B knob, read per launch; unset = 1): 0 keeps every launch on the v_perm
-// multiply instead of the LDS product tables.
-bool apply_lds() {
-    const char* e = std::getenv("CEC_APPLY_LDS");
-    return !(e && e[0] == '0');
-}
-
-constexpr uint32_t kLdsMaxData = 32;  // inputs the LDS path takes (tables: d * 256 * E bytes)
-
-// The LDS path serves 16-byte-aligned layouts with d <= 32 under the default tuning.
-bool use_lds(const ApplyParams& a, bool vec16) {
-    return vec16 && a.d <= kLdsMaxData && apply_lds() && apply_tune() == 1;
-}
-
-template <int RG>
-hipError_t launch_rg_lds(const ApplyParams& a, uint32_t row_base, uint32_t groups,
-                         hipStream_t s) {
-    const uint64_t tiles = (a.len + kLdsTile - 1) / kLdsTile;
-    const uint64_t max_blocks = max_apply_blocks();
-    if (tiles > max_blocks) return hipErrorInvalidValue;
-    // static tables: DMAX * 256 * E bytes; dynamic LDS only for what lds_reserve asks beyond them
-    const uint32_t tabs = (a.d <= 16 ? 16u : 32u) * 256u * (RG <= 4 ? 4u : 8u);
-    const uint32_t lds = a.lds_reserve > tabs ? a.lds_reserve - tabs : 0u;
-    return for_part_ranges(a, max_blocks / tiles, [&](const ApplyParams& b) {
-        const dim3 grid(uint32_t(b.n_parts * tiles), groups);
-        auto* kern = b.d <= 16 ? &rs_apply_lds_kernel<RG, 16> : &rs_apply_lds_kernel<RG, 32>;
-        if (!allow_lds(kern, lds)) return hipErrorInvalidValue;
-        clear_stale_error();
-        hipLaunchKernelGGL(kern, grid, dim3(kApplyThreads), lds, s, b, uint32_t(tiles), row_base,
-                           apply_xcd());
-        return hipGetLastError();
-    });
-}
-
 template <int RG>
 hipError_t launch_rg(const ApplyParams& a, uint32_t row_base, uint32_t groups, bool vec16,
                      hipStream_t s) {
-    if (use_lds(a, vec16)) return launch_rg_lds<RG>(a, row_base, groups, s);
     const uint64_t tiles = (a.len + kApplyTile - 1) / kApplyTile;
     const uint64_t max_blocks = max_apply_blocks();
     if (tiles > max_blocks) return hipErrorInvalidValue;
@@ -635,26 +393,6 @@ hipError_t launch_rs_apply(const ApplyParams& a, bool vec16, hipStream_t s) {
 hipError_t launch_rs_apply_var(const ApplyParams& a, bool vec16, hipStream_t s) {
     if (a.n_parts == 0 || a.len == 0) return hipSuccess;
     if (!a.part_ids || !a.part_pat) return hipErrorInvalidValue;
-    if (use_lds(a, vec16)) {
-        const uint64_t tiles = (a.len + kLdsTile - 1) / kLdsTile;
-        const uint64_t max_blocks = max_apply_blocks();
-        if (tiles > max_blocks) return hipErrorInvalidValue;
-        // patterns of up to 4 rows: 4-byte entries and the smaller register budget; else 8
-        const bool wide = a.max_rows == 0 || a.max_rows > 4;
-        const uint32_t tabs = (a.d <= 16 ? 16u : 32u) * 256u * (wide ? 8u : 4u);
-        const uint32_t lds = a.lds_reserve > tabs ? a.lds_reserve - tabs : 0u;
-        return for_part_ranges(a, max_blocks / tiles, [&](const ApplyParams& b) {
-            auto* kern = wide ? (b.d <= 16 ? &rs_apply_var_lds_kernel<16, 8>
-                                           : &rs_apply_var_lds_kernel<32, 8>)
-                              : (b.d <= 16 ? &rs_apply_var_lds_kernel<16, 4>
-                                           : &rs_apply_var_lds_kernel<32, 4>);
-            if (!allow_lds(kern, lds)) return hipErrorInvalidValue;
-            clear_stale_error();
-            hipLaunchKernelGGL(kern, dim3(uint32_t(b.n_parts * tiles)), dim3(kApplyThreads), lds,
-                               s, b, uint32_t(tiles), apply_xcd());
-            return hipGetLastError();
-        });
-    }
     const uint64_t tiles = (a.len + kApplyTile - 1) / kApplyTile;
     const uint64_t max_blocks = max_apply_blocks();
     if (tiles > max_blocks) return hipErrorInvalidValue;
