@@ -35,7 +35,7 @@ namespace {
 using namespace gf;
 
 constexpr int kApplyThreads = 256;
-constexpr uint64_t kApplyTile = 16384;  // bytes of one part's column range per block
+constexpr uint64_t kApplyTile = 16384;  // default bytes of one part's column range per block
 constexpr uint64_t kSpan = uint64_t(kApplyThreads) * 16u;  // bytes per block per column step
 constexpr uint32_t kMaxApplyRows = 8;
 
@@ -134,7 +134,8 @@ __device__ __forceinline__ void apply_column(uint8_t* pbase, uint64_t cs, uint64
 // (ragged end, unaligned layouts) the byte-granular single-column path.
 template <int RG, bool VEC, int GROUP, int V, bool NT>
 __device__ __forceinline__ void apply_tile(const ApplyParams& a, cu32* pat, uint32_t part,
-                                           uint32_t tile, uint32_t n_out, uint32_t row0) {
+                                           uint32_t tile, uint32_t n_out, uint32_t row0,
+                                           uint32_t tile_bytes) {
     const uint32_t d = a.d;
     cu32* in_idx = pat + 1;
     cu32* out_idx = pat + 1 + d + row0;
@@ -143,8 +144,8 @@ __device__ __forceinline__ void apply_tile(const ApplyParams& a, cu32* pat, uint
     uint8_t* pbase = a.base + uint64_t(part) * a.part_stride;
     const uint64_t len = a.len;
     const uint64_t cs = a.chunk_stride;
-    const uint64_t t0 = uint64_t(tile) * kApplyTile;
-    const uint64_t t1 = t0 + kApplyTile < len ? t0 + kApplyTile : len;
+    const uint64_t t0 = uint64_t(tile) * tile_bytes;
+    const uint64_t t1 = t0 + tile_bytes < len ? t0 + tile_bytes : len;
 #pragma unroll 1
     for (uint64_t xb = t0; xb < t1; xb += kSpan * V) {  // block-uniform
         const uint64_t x = xb + uint64_t(threadIdx.x) * 16u;
@@ -180,13 +181,15 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t n) {
 template <int RG, bool VEC, int GROUP, int V, bool NT>
 __global__ __launch_bounds__(kApplyThreads) void rs_apply_kernel(ApplyParams a,
                                                                  uint32_t tiles_per_part,
-                                                                 uint32_t row_base, bool xcd) {
+                                                                 uint32_t row_base, bool xcd,
+                                                                 uint32_t tile_bytes) {
     const uint32_t bx = xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
     const uint32_t lp = bx / tiles_per_part;
     const uint32_t tile = bx - lp * tiles_per_part;
     const uint32_t part = a.part_ids ? as_const(a.part_ids)[lp] : lp;
     cu32* pat = as_const(a.pat) + (a.part_pat ? as_const(a.part_pat)[lp] : 0u);
-    apply_tile<RG, VEC, GROUP, V, NT>(a, pat, part, tile, a.n_rows, row_base + blockIdx.y * RG);
+    apply_tile<RG, VEC, GROUP, V, NT>(a, pat, part, tile, a.n_rows, row_base + blockIdx.y * RG,
+                                      tile_bytes);
 }
 
 // Reconstruct with mixed erasure counts in ONE launch: every listed part's pattern carries its
@@ -195,21 +198,21 @@ __global__ __launch_bounds__(kApplyThreads) void rs_apply_kernel(ApplyParams a,
 template <bool VEC, int GROUP, int V, bool NT>
 __global__ __launch_bounds__(kApplyThreads) void rs_apply_var_kernel(ApplyParams a,
                                                                      uint32_t tiles_per_part,
-                                                                     bool xcd) {
+                                                                     bool xcd, uint32_t tile_bytes) {
     const uint32_t bx = xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
     const uint32_t lp = bx / tiles_per_part;
     const uint32_t tile = bx - lp * tiles_per_part;
     const uint32_t part = as_const(a.part_ids)[lp];
     cu32* pat = as_const(a.pat) + as_const(a.part_pat)[lp];
     switch (pat[0]) {
-        case 1: apply_tile<1, VEC, GROUP, V, NT>(a, pat, part, tile, 1, 0); break;
-        case 2: apply_tile<2, VEC, GROUP, V, NT>(a, pat, part, tile, 2, 0); break;
-        case 3: apply_tile<3, VEC, GROUP, V, NT>(a, pat, part, tile, 3, 0); break;
-        case 4: apply_tile<4, VEC, GROUP, V, NT>(a, pat, part, tile, 4, 0); break;
-        case 5: apply_tile<5, VEC, GROUP, V, NT>(a, pat, part, tile, 5, 0); break;
-        case 6: apply_tile<6, VEC, GROUP, V, NT>(a, pat, part, tile, 6, 0); break;
-        case 7: apply_tile<7, VEC, GROUP, V, NT>(a, pat, part, tile, 7, 0); break;
-        case 8: apply_tile<8, VEC, GROUP, V, NT>(a, pat, part, tile, 8, 0); break;
+        case 1: apply_tile<1, VEC, GROUP, V, NT>(a, pat, part, tile, 1, 0, tile_bytes); break;
+        case 2: apply_tile<2, VEC, GROUP, V, NT>(a, pat, part, tile, 2, 0, tile_bytes); break;
+        case 3: apply_tile<3, VEC, GROUP, V, NT>(a, pat, part, tile, 3, 0, tile_bytes); break;
+        case 4: apply_tile<4, VEC, GROUP, V, NT>(a, pat, part, tile, 4, 0, tile_bytes); break;
+        case 5: apply_tile<5, VEC, GROUP, V, NT>(a, pat, part, tile, 5, 0, tile_bytes); break;
+        case 6: apply_tile<6, VEC, GROUP, V, NT>(a, pat, part, tile, 6, 0, tile_bytes); break;
+        case 7: apply_tile<7, VEC, GROUP, V, NT>(a, pat, part, tile, 7, 0, tile_bytes); break;
+        case 8: apply_tile<8, VEC, GROUP, V, NT>(a, pat, part, tile, 8, 0, tile_bytes); break;
         default: break;  // the host routes n_out > 8 to row-group launches
     }
 }
@@ -275,6 +278,14 @@ int apply_tune() {
 bool apply_xcd() {
     const char* e = std::getenv("CEC_APPLY_XCD");
     return !(e && e[0] == '0');
+}
+
+// CEC_APPLY_TILE (A/B knob, read per launch): bytes of one part's column range per block, a
+// multiple of 8 KiB (one full two-column step of a block) up to 256 KiB; default kApplyTile.
+uint64_t apply_tile_bytes() {
+    const char* e = std::getenv("CEC_APPLY_TILE");
+    const unsigned long long v = e ? std::strtoull(e, nullptr, 10) : 0ull;
+    return v && v % 8192 == 0 && v <= (256u << 10) ? v : kApplyTile;
 }
 
 // Launch KERNEL<PRE... VEC, GROUP, V, NT> as picked by the tuning knob; layouts that are not
@@ -343,7 +354,8 @@ hipError_t for_part_ranges(const ApplyParams& a, uint64_t max_parts, Fn fn) {
 template <int RG>
 hipError_t launch_rg(const ApplyParams& a, uint32_t row_base, uint32_t groups, bool vec16,
                      hipStream_t s) {
-    const uint64_t tiles = (a.len + kApplyTile - 1) / kApplyTile;
+    const uint64_t tb = apply_tile_bytes();
+    const uint64_t tiles = (a.len + tb - 1) / tb;
     const uint64_t max_blocks = max_apply_blocks();
     if (tiles > max_blocks) return hipErrorInvalidValue;
     return for_part_ranges(a, max_blocks / tiles, [&](const ApplyParams& b) {
@@ -354,7 +366,7 @@ hipError_t launch_rg(const ApplyParams& a, uint32_t row_base, uint32_t groups, b
             if (!allow_lds(kern, b.lds_reserve)) return hipErrorInvalidValue;
             clear_stale_error();
             hipLaunchKernelGGL(kern, grid, dim3(kApplyThreads), b.lds_reserve, s, b,
-                               uint32_t(tiles), row_base, apply_xcd());
+                               uint32_t(tiles), row_base, apply_xcd(), uint32_t(tb));
             return hipGetLastError();
         });
     });
@@ -393,7 +405,8 @@ hipError_t launch_rs_apply(const ApplyParams& a, bool vec16, hipStream_t s) {
 hipError_t launch_rs_apply_var(const ApplyParams& a, bool vec16, hipStream_t s) {
     if (a.n_parts == 0 || a.len == 0) return hipSuccess;
     if (!a.part_ids || !a.part_pat) return hipErrorInvalidValue;
-    const uint64_t tiles = (a.len + kApplyTile - 1) / kApplyTile;
+    const uint64_t tb = apply_tile_bytes();
+    const uint64_t tiles = (a.len + tb - 1) / tb;
     const uint64_t max_blocks = max_apply_blocks();
     if (tiles > max_blocks) return hipErrorInvalidValue;
     return for_part_ranges(a, max_blocks / tiles, [&](const ApplyParams& b) {
@@ -404,7 +417,7 @@ hipError_t launch_rs_apply_var(const ApplyParams& a, bool vec16, hipStream_t s) 
             if (!allow_lds(kern, b.lds_reserve)) return hipErrorInvalidValue;
             clear_stale_error();
             hipLaunchKernelGGL(kern, grid, dim3(kApplyThreads), b.lds_reserve, s, b,
-                               uint32_t(tiles), apply_xcd());
+                               uint32_t(tiles), apply_xcd(), uint32_t(tb));
             return hipGetLastError();
         });
     });
