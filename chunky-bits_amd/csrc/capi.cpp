@@ -354,6 +354,7 @@ struct cec_codec {
     size_t d = 0, p = 0;
     ByteMatrix m;                  // (d+p) x d
     std::vector<uint32_t> enc;     // pattern record: parity rows over the d data chunks
+    bool bs = false;               // parity rows = a compiled bit-sliced shape (bs_encode_matches)
     std::mutex mu;
     std::unordered_map<int, uint32_t*> dev_enc;  // encode record per device
     // Decode records, least recently used first out once kDecCacheCap patterns are cached (every
@@ -1147,7 +1148,8 @@ struct PartImpl {
             ap.n_parts = uint32_t(B);
             ap.d = uint32_t(d);
             ap.n_rows = uint32_t(p);
-            HIP_TRY(launch_rs_apply(ap, true, s));
+            ap.std_encode = c->bs ? 1u : 0u;
+            HIP_TRY(launch_rs_encode(ap, true, s));
             const bool early = coalesce_early_d2h();
             if (early) {
                 if (!a.side) HIP_TRY(hipStreamCreateWithFlags(&a.side, hipStreamNonBlocking));
@@ -1310,6 +1312,8 @@ int cec_codec_new(size_t d, size_t p, cec_codec** out) {
     }
     c->enc.resize(pattern_words(d, p));
     write_pattern(c->enc.data(), d, in_idx, out_idx, rows);
+    c->bs = d <= 0xFFFFFFFFull && p <= 0xFFFFFFFFull &&
+            bs_encode_matches(uint32_t(d), uint32_t(p), rows.v.data());
     *out = c.release();
     return CEC_OK;
 }
@@ -1370,7 +1374,8 @@ int cec_encode_sep(const cec_codec* cc, const uint8_t* const* data, const size_t
     a.n_parts = 1;
     a.d = uint32_t(c->d);
     a.n_rows = uint32_t(c->p);
-    HIP_TRY(launch_rs_apply(a, true, ctx->stream));
+    a.std_encode = c->bs ? 1u : 0u;
+    HIP_TRY(launch_rs_encode(a, true, ctx->stream));
     for (size_t i = 0; i < c->p; ++i)
         HIP_TRY(hipMemcpyAsync(parity[i], ctx->dbuf + (c->d + i) * cs, len,
                                hipMemcpyDeviceToHost, ctx->stream));
@@ -1434,7 +1439,8 @@ int cec_encode_batch(const cec_codec* cc, const cec_part_batch* b, void* stream)
     a.n_parts = uint32_t(b->n_parts);
     a.d = uint32_t(c->d);
     a.n_rows = uint32_t(c->p);
-    HIP_TRY(launch_rs_apply(a, aligned16(b->base, b->part_stride, b->chunk_stride),
+    a.std_encode = c->bs ? 1u : 0u;
+    HIP_TRY(launch_rs_encode(a, aligned16(b->base, b->part_stride, b->chunk_stride),
                             static_cast<hipStream_t>(stream)));
     return CEC_OK;
 }

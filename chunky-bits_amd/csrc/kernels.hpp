@@ -25,6 +25,10 @@ struct ApplyParams {
     // cannot share a CU with a SHA-256 lane-kernel workgroup (>= 64 KiB reserved each), which
     // keeps a decode running beside a verification off the SHA waves' SIMDs.
     uint32_t lds_reserve;
+    // Nonzero: `pat` is the codec's encode record (inputs 0..d-1, outputs d..d+p-1) and its
+    // matrix equals gfc::Shape<d, p> (bs_encode_matches), so launch_rs_encode may take the
+    // bit-sliced kernel of that shape.
+    uint32_t std_encode;
 };
 
 // SHA-256 of n_parts * n_chunks chunks.  Strided mode: chunk (k, first_chunk + c) at
@@ -81,6 +85,12 @@ struct FusedParams {
 };
 
 hipError_t launch_rs_apply(const ApplyParams& a, bool vec16, hipStream_t s);
+// encode_sep over a batch: the bit-sliced kernel of the shape when a.std_encode, the layout is
+// 16-byte aligned and (d, p) is one of the compiled shapes; launch_rs_apply otherwise.
+hipError_t launch_rs_encode(const ApplyParams& a, bool vec16, hipStream_t s);
+// Whether a codec's parity rows (p x d bytes, row-major) are those of a compiled bit-sliced
+// shape (the compile-time construction of gf_const.hpp, compared byte for byte).
+bool bs_encode_matches(uint32_t d, uint32_t p, const uint8_t* parity_rows);
 // Listed parts whose patterns carry their own row count (1..max_var_rows()), one launch;
 // a.n_rows is ignored.
 hipError_t launch_rs_apply_var(const ApplyParams& a, bool vec16, hipStream_t s);

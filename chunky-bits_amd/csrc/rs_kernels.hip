@@ -26,6 +26,7 @@
 
 #include "device_common.hpp"
 #include "gf256.hpp"
+#include "gf_const.hpp"
 #include "gf_device.hpp"
 #include "kernels.hpp"
 
@@ -218,6 +219,177 @@ __global__ __launch_bounds__(kApplyThreads) void rs_apply_var_kernel(ApplyParams
 }
 
 // ------------------------------------------------------------------------------------------
+// Bit-sliced encode for the common shapes: RS(d, p) with the parity rows compile-time constants.
+//
+// The v_perm multiply above costs, per data dword, 3 selector ops plus 3 half-rate v_perm and
+// 2 xors per parity row: for RS(10,4) about 84 SIMD cycles per 64 data dwords, against ~39 for
+// the HBM stream (the encode was co-bound).  Bit-sliced, the same multiply is a
+// fixed XOR network: a lane's 32 bytes of one input (its two 16-byte columns) are transposed
+// into 8 bit planes (plane i = bit i of all 32 bytes; 12 two-word bit swaps, 48 full-rate ops),
+// output plane o of row r is the XOR of the input planes i with bit o of c[r][j]*2^i set
+// (gf_const.hpp kBits, about half of them), and the 8 planes of each row are transposed back.
+// With the matrix known at compile time the network is straight-line v_bitop3 xor3s: RS(10,4)
+// ≈ 17 full-rate ops per data dword (6 transpose in, 9 xor, 2.4 transpose out), about half the
+// v_perm form.  Loads and stores are the rs_apply ones (non-temporal, two 16-byte columns 4 KiB
+// apart per lane, XCD-aware block order); ragged tails take the v_perm byte path.
+// ------------------------------------------------------------------------------------------
+
+// bitop3 select: m ? x : y per bit.
+__device__ __forceinline__ uint32_t bsel(uint32_t m, uint32_t x, uint32_t y) {
+    return __builtin_amdgcn_bitop3_b32(m, x, y, 0xCA);
+}
+
+// Swap bit k (k & S set) of a with bit k - S of b, in every byte.
+template <int S>
+__device__ __forceinline__ void swap_bits(uint32_t& a, uint32_t& b) {
+    constexpr uint32_t lo = S == 1 ? 0x55555555u : S == 2 ? 0x33333333u : 0x0F0F0F0Fu;
+    constexpr uint32_t hi = lo << S;
+    const uint32_t na = bsel(hi, b << S, a);
+    const uint32_t nb = bsel(lo, a >> S, b);
+    a = na;
+    b = nb;
+}
+
+// 8x8 bit transpose in each byte lane of 8 words: bit k of byte m of w[j] <-> bit j of byte m of
+// w[k].  Each stage swaps one bit of the word index with the same bit of the bit index, so the
+// three commute and the whole is an involution (the same network maps planes back to bytes).
+__device__ __forceinline__ void transpose8(uint32_t (&w)[8]) {
+    swap_bits<1>(w[0], w[1]);
+    swap_bits<1>(w[2], w[3]);
+    swap_bits<1>(w[4], w[5]);
+    swap_bits<1>(w[6], w[7]);
+    swap_bits<2>(w[0], w[2]);
+    swap_bits<2>(w[1], w[3]);
+    swap_bits<2>(w[4], w[6]);
+    swap_bits<2>(w[5], w[7]);
+    swap_bits<4>(w[0], w[4]);
+    swap_bits<4>(w[1], w[5]);
+    swap_bits<4>(w[2], w[6]);
+    swap_bits<4>(w[3], w[7]);
+}
+
+constexpr int kBsGroup = 2;  // inputs per network step (terms pair across both into xor3s)
+
+// Input words of inputs J0 .. J0 + kBsGroup: a lane's two 16-byte columns (x, x + kSpan).
+template <int D, int J0>
+__device__ __forceinline__ void bs_load(uint32_t (&w)[kBsGroup][8], const uint8_t* pbase,
+                                        uint64_t cs, uint64_t x, cu32* in_idx) {
+#pragma unroll
+    for (int u = 0; u < kBsGroup; ++u) {
+        if (J0 + u < D) {
+            const uint8_t* src = pbase + uint64_t(in_idx[J0 + u]) * cs + x;
+            const uint4 c0 = ld16<true>(src), c1 = ld16<true>(src + kSpan);
+            w[u][0] = c0.x, w[u][1] = c0.y, w[u][2] = c0.z, w[u][3] = c0.w;
+            w[u][4] = c1.x, w[u][5] = c1.y, w[u][6] = c1.z, w[u][7] = c1.w;
+        }
+    }
+}
+
+// acc[r][o] ^= the planes of inputs J0 .. J0 + kBsGroup that feed bit o of row r, two per xor3.
+template <int D, int P, int J0>
+__device__ __forceinline__ void bs_group(uint32_t (&acc)[P][8], uint32_t (&w)[kBsGroup][8]) {
+    using S = gfc::Shape<D, P>;
+#pragma unroll
+    for (int u = 0; u < kBsGroup; ++u)
+        if (J0 + u < D) transpose8(w[u]);
+#pragma unroll
+    for (int r = 0; r < P; ++r) {
+#pragma unroll
+        for (int o = 0; o < 8; ++o) {
+            uint32_t pend = 0;
+            bool has = false;
+#pragma unroll
+            for (int u = 0; u < kBsGroup; ++u) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    if (J0 + u < D && ((S::kBits.m[r][J0 + u < D ? J0 + u : 0][o] >> i) & 1)) {
+                        if (has) {
+                            acc[r][o] = xor3(acc[r][o], pend, w[u][i]);
+                            has = false;
+                        } else {
+                            pend = w[u][i];
+                            has = true;
+                        }
+                    }
+                }
+            }
+            if (has) acc[r][o] ^= pend;
+        }
+    }
+}
+
+// Groups J0, J0 + kBsGroup, ... with the next group's loads issued before this group's network.
+template <int D, int P, int J0>
+struct BsSteps {
+    __device__ static __forceinline__ void run(uint32_t (&acc)[P][8],
+                                               uint32_t (&w)[2][kBsGroup][8],
+                                               const uint8_t* pbase, uint64_t cs, uint64_t x,
+                                               cu32* in_idx) {
+        constexpr int buf = (J0 / kBsGroup) & 1;
+        if constexpr (J0 + kBsGroup < D) bs_load<D, J0 + kBsGroup>(w[buf ^ 1], pbase, cs, x, in_idx);
+        bs_group<D, P, J0>(acc, w[buf]);
+        if constexpr (J0 + kBsGroup < D)
+            BsSteps<D, P, J0 + kBsGroup>::run(acc, w, pbase, cs, x, in_idx);
+    }
+};
+
+// Two full 16-byte columns (x, x + kSpan) of every parity row of one part.
+template <int D, int P>
+__device__ __forceinline__ void bs_column(uint8_t* pbase, uint64_t cs, uint64_t x, cu32* in_idx,
+                                          cu32* out_idx) {
+    uint32_t acc[P][8];
+#pragma unroll
+    for (int r = 0; r < P; ++r)
+#pragma unroll
+        for (int o = 0; o < 8; ++o) acc[r][o] = 0u;
+    uint32_t w[2][kBsGroup][8];
+    bs_load<D, 0>(w[0], pbase, cs, x, in_idx);
+    BsSteps<D, P, 0>::run(acc, w, pbase, cs, x, in_idx);
+#pragma unroll
+    for (int r = 0; r < P; ++r) {
+        transpose8(acc[r]);
+        uint8_t* dst = pbase + uint64_t(out_idx[r]) * cs + x;
+        st16<true>(dst, make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]));
+        st16<true>(dst + kSpan, make_uint4(acc[r][4], acc[r][5], acc[r][6], acc[r][7]));
+    }
+}
+
+// grid.x = n_parts * tiles_per_part, as rs_apply_kernel; the pattern record is the codec's
+// encode record (its indices; its v_perm tables serve the ragged tail).  The host launches this
+// only for 16-byte aligned layouts whose run-time matrix equals gfc::Shape<D, P> (checked once
+// per codec, bs_encode_matches).
+template <int D, int P>
+__global__ __launch_bounds__(kApplyThreads) void rs_encode_bs_kernel(ApplyParams a,
+                                                                     uint32_t tiles_per_part,
+                                                                     bool xcd, uint32_t tile_bytes) {
+    const uint32_t bx = xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint32_t lp = bx / tiles_per_part;
+    const uint32_t tile = bx - lp * tiles_per_part;
+    const uint32_t part = a.part_ids ? as_const(a.part_ids)[lp] : lp;
+    cu32* pat = as_const(a.pat);
+    cu32* in_idx = pat + 1;
+    cu32* out_idx = pat + 1 + D;
+    cu32* tab = pat + 1 + D + P;
+    uint8_t* pbase = a.base + uint64_t(part) * a.part_stride;
+    const uint64_t len = a.len;
+    const uint64_t cs = a.chunk_stride;
+    const uint64_t t0 = uint64_t(tile) * tile_bytes;
+    const uint64_t t1 = t0 + tile_bytes < len ? t0 + tile_bytes : len;
+#pragma unroll 1
+    for (uint64_t xb = t0; xb < t1; xb += 2 * kSpan) {  // block-uniform
+        const uint64_t x = xb + uint64_t(threadIdx.x) * 16u;
+        if (xb + 2 * kSpan <= len) {
+            bs_column<D, P>(pbase, cs, x, in_idx, out_idx);
+        } else {
+#pragma unroll 1
+            for (uint64_t xc = x; xc < t1 && xc < xb + 2 * kSpan; xc += kSpan)
+                apply_column<P, false, 4, 1, false>(pbase, cs, xc, len - xc, D, P * kTabWords,
+                                                    in_idx, out_idx, tab);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // Synthetic data
 // ------------------------------------------------------------------------------------------
 
@@ -386,7 +558,66 @@ hipError_t launch_rows(const ApplyParams& a, uint32_t rg, uint32_t row_base, uin
     }
 }
 
+// CEC_APPLY_BS (A/B knob, read per launch; unset = 1): 0 sends the compiled shapes' encodes to
+// the v_perm kernel too.
+bool apply_bs() {
+    const char* e = std::getenv("CEC_APPLY_BS");
+    return !(e && e[0] == '0');
+}
+
+template <int D, int P>
+hipError_t launch_bs(const ApplyParams& a, hipStream_t s) {
+    const uint64_t tb = apply_tile_bytes();
+    const uint64_t tiles = (a.len + tb - 1) / tb;
+    const uint64_t max_blocks = max_apply_blocks();
+    if (tiles > max_blocks) return hipErrorInvalidValue;
+    return for_part_ranges(a, max_blocks / tiles, [&](const ApplyParams& b) {
+        auto* kern = &rs_encode_bs_kernel<D, P>;
+        if (!allow_lds(kern, b.lds_reserve)) return hipErrorInvalidValue;
+        clear_stale_error();
+        hipLaunchKernelGGL(kern, dim3(uint32_t(b.n_parts * tiles)), dim3(kApplyThreads),
+                           b.lds_reserve, s, b, uint32_t(tiles), apply_xcd(), uint32_t(tb));
+        return hipGetLastError();
+    });
+}
+
+// The compiled bit-sliced shapes: the reference's example clusters (RS(3,2), examples/*.yaml)
+// and the bench configurations (RS(10,4), RS(20,8)).
+template <typename Fn>
+bool with_bs_shape(uint32_t d, uint32_t p, Fn&& fn) {
+    if (d == 3 && p == 2) return fn(gfc::Shape<3, 2>{}, std::integral_constant<int, 3>{},
+                                    std::integral_constant<int, 2>{});
+    if (d == 10 && p == 4) return fn(gfc::Shape<10, 4>{}, std::integral_constant<int, 10>{},
+                                     std::integral_constant<int, 4>{});
+    if (d == 20 && p == 8) return fn(gfc::Shape<20, 8>{}, std::integral_constant<int, 20>{},
+                                     std::integral_constant<int, 8>{});
+    return false;
+}
+
 }  // namespace
+
+bool bs_encode_matches(uint32_t d, uint32_t p, const uint8_t* parity_rows) {
+    return with_bs_shape(d, p, [&](auto shape, auto, auto) {
+        using S = decltype(shape);
+        for (uint32_t r = 0; r < p; ++r)
+            for (uint32_t j = 0; j < d; ++j)
+                if (S::kMat.c[r][j] != parity_rows[r * d + j]) return false;
+        return true;
+    });
+}
+
+hipError_t launch_rs_encode(const ApplyParams& a, bool vec16, hipStream_t s) {
+    if (a.n_parts == 0 || a.n_rows == 0 || a.len == 0) return hipSuccess;
+    if (a.std_encode && vec16 && !a.part_pat && apply_bs()) {
+        hipError_t e = hipErrorInvalidValue;
+        const bool shaped = with_bs_shape(a.d, a.n_rows, [&](auto, auto dd, auto pp) {
+            e = launch_bs<decltype(dd)::value, decltype(pp)::value>(a, s);
+            return true;
+        });
+        if (shaped) return e;
+    }
+    return launch_rs_apply(a, vec16, s);
+}
 
 // Rows are processed in groups of kMaxApplyRows (8) plus one remainder group, so every kernel
 // instance handles exactly RG rows (no per-row predicate in the inner loop).

@@ -4,6 +4,8 @@
 set -o pipefail
 T=gpurun_out/r3_tile_ab
 mkdir -p $T
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 150 --timeout-method thread > $T/pytest_gpu.log 2>&1 || { tail -30 $T/pytest_gpu.log; exit 1; }
+tail -1 $T/pytest_gpu.log
 for tb in 8192 65536; do
   CEC_APPLY_TILE=$tb timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fuzz.py -m gpu -x -q --timeout 150 --timeout-method thread -k "encode or reconstruct or apply or read or fuzz" > $T/pytest_tile$tb.log 2>&1 || { tail -30 $T/pytest_tile$tb.log; exit 1; }
   echo "tile $tb: $(tail -1 $T/pytest_tile$tb.log)"
