@@ -116,10 +116,21 @@ def workload(cfg, args, stream_bytes=None, shards=None) -> str:
 
 # bench kernel name -> rocprofv3 symbol(s); a step of concurrent kernels sums their traffic
 KERNEL_SYMBOL = {"sha256_kernel": "sha256_lane_kernel", "rs_apply_kernel": "rs_apply_kernel",
+                 "rs_encode_bs_kernel": "rs_encode_bs_kernel",
                  "rs_apply_kernel(reconstruct)": "rs_apply_var_kernel",
                  "rs_apply_kernel(reconstruct_data)": "rs_apply_var_kernel",
                  "encode_hash_kernel": "encode_hash_kernel",
                  "read_batch(verify+decode)": ("sha256_lane_kernel", "rs_apply_var_kernel")}
+
+
+# Shapes with a compiled bit-sliced encoder (rs_kernels.hip with_bs_shape / launch_rs_encode).
+BS_SHAPES = {(3, 2), (10, 4), (20, 8)}
+
+
+def encode_kernel(d: int, p: int) -> str:
+    """The kernel cec_encode_batch launches for RS(d, p) at a 16-byte aligned layout."""
+    bs = (d, p) in BS_SHAPES and os.environ.get("CEC_APPLY_BS", "1")[:1] != "0"
+    return "rs_encode_bs_kernel" if bs else "rs_apply_kernel"
 
 
 def measured_traffic(config: str, kernel: str, full_size: bool, with_source: bool = False):
@@ -561,7 +572,7 @@ def north_star_block(codec, batch, buf, digests, stream, device, rank, d, p, L, 
 
     ms = time_launches(lambda: ce.encode_batch(codec, batch, stream))
     out["encode"] = entry("encode_sep (cec_encode_batch), every part: read d, write p chunks",
-                          "rs_apply_kernel", ms, n * t * L, "c2enc")
+                          encode_kernel(d, p), ms, n * t * L, "c2enc")
     pres = two_erasures(n, t, rank)
     present = bytes(pres.flatten().tolist())
     buf.mul_(pres.to(device).view(n, t, 1))  # the erased chunks start zeroed
@@ -1083,17 +1094,17 @@ def main():
                                          "GBs": round((n_parts * t * (L + 32)) / ms / 1e6, 1)}
     elif cfg["op"] == "encode_hash":
         enc_ms, sha_ms = avg_ms(0, 1), avg_ms(1, 2)
-        kernels["rs_apply_kernel"] = {"ms": round(enc_ms, 4),
-                                      "algorithmic_bytes": n_parts * t * L,
-                                      "GBs": round(n_parts * t * L / enc_ms / 1e6, 1)}
+        kernels[encode_kernel(d, t - d)] = {"ms": round(enc_ms, 4),
+                                            "algorithmic_bytes": n_parts * t * L,
+                                            "GBs": round(n_parts * t * L / enc_ms / 1e6, 1)}
         kernels["sha256_kernel"] = {"ms": round(sha_ms, 4),
                                     "algorithmic_bytes": n_parts * t * (L + 32),
                                     "GBs": round(n_parts * t * (L + 32) / sha_ms / 1e6, 1)}
     elif cfg["op"] == "encode":
         enc_ms = avg_ms(0, 1)
-        kernels["rs_apply_kernel"] = {"ms": round(enc_ms, 4),
-                                      "algorithmic_bytes": n_parts * t * L,
-                                      "GBs": round(n_parts * t * L / enc_ms / 1e6, 1)}
+        kernels[encode_kernel(d, t - d)] = {"ms": round(enc_ms, 4),
+                                            "algorithmic_bytes": n_parts * t * L,
+                                            "GBs": round(n_parts * t * L / enc_ms / 1e6, 1)}
     elif cfg["op"] == "reconstruct_e2":
         ms = avg_ms(0, 1)
         kernels["rs_apply_kernel(reconstruct_data)"] = {

@@ -453,11 +453,16 @@ bool apply_xcd() {
 }
 
 // CEC_APPLY_TILE (A/B knob, read per launch): bytes of one part's column range per block, a
-// multiple of 8 KiB (one full two-column step of a block) up to 256 KiB; default kApplyTile.
-uint64_t apply_tile_bytes() {
+// multiple of 8 KiB (one full two-column step of a block) up to 256 KiB; default `def`:
+// kApplyTile for the v_perm kernels, kBsTile for the bit-sliced encoder.  Measured interleaved
+// on one box (profiles/r3_tile2_ab/, 8 vs 16 KiB): bit-sliced C2 encode 9.56 vs 9.69 ms, RS(20,8)
+// encode 4.89-4.91 vs 5.20; c3e2 7.97 vs 8.08, but C3 (1-4 rows, data + parity) 9.90-10.00 vs
+// 9.48-9.51, so the v_perm kernels keep 16 KiB.
+constexpr uint64_t kBsTile = 8192;
+uint64_t apply_tile_bytes(uint64_t def = kApplyTile) {
     const char* e = std::getenv("CEC_APPLY_TILE");
     const unsigned long long v = e ? std::strtoull(e, nullptr, 10) : 0ull;
-    return v && v % 8192 == 0 && v <= (256u << 10) ? v : kApplyTile;
+    return v && v % 8192 == 0 && v <= (256u << 10) ? v : def;
 }
 
 // Launch KERNEL<PRE... VEC, GROUP, V, NT> as picked by the tuning knob; layouts that are not
@@ -567,7 +572,7 @@ bool apply_bs() {
 
 template <int D, int P>
 hipError_t launch_bs(const ApplyParams& a, hipStream_t s) {
-    const uint64_t tb = apply_tile_bytes();
+    const uint64_t tb = apply_tile_bytes(kBsTile);
     const uint64_t tiles = (a.len + tb - 1) / tb;
     const uint64_t max_blocks = max_apply_blocks();
     if (tiles > max_blocks) return hipErrorInvalidValue;

@@ -21,7 +21,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def short(name: str) -> str:
-    for k in ("rs_apply_var_kernel", "rs_apply_kernel", "sha256_lane_kernel", "sha256_split_kernel", "fill_kernel",
+    for k in ("rs_apply_var_kernel", "rs_apply_kernel", "rs_encode_bs_kernel", "sha256_lane_kernel", "sha256_split_kernel", "fill_kernel",
               "encode_hash_kernel", "copyBuffer"):
         if k in name:
             return k
@@ -106,14 +106,14 @@ def main():
         lines.append(f"| {k} | {ghz:.2f} | {waves:.0f} | {vpw:.0f} | {f:.0f} | {w:.0f} | "
                      f"{tb/1e9 if tb else float('nan'):.2f} |")
         if tb and k in ("rs_apply_kernel", "rs_apply_var_kernel", "sha256_lane_kernel",
-                        "encode_hash_kernel"):
+                        "encode_hash_kernel", "rs_encode_bs_kernel"):
             traffic.setdefault(config, {})[k] = {
                 "bytes_per_launch": int(tb),
                 "fetch_kib": f, "write_kib": w,
                 # x2 measured for both read patterns (tools/ubench_fetch.hip,
                 # profiles/r1y_fetch_calibration.log): coalesced 16 B/lane and per-lane streams
                 "calibrated": k in ("rs_apply_kernel", "rs_apply_var_kernel", "encode_hash_kernel",
-                                    "sha256_lane_kernel") or fmult != 2.0,
+                                    "sha256_lane_kernel", "rs_encode_bs_kernel") or fmult != 2.0,
                 "fetch_mult": fmult,
                 "source": f"profiles/{tag}_summary.md",
             }

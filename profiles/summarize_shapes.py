@@ -22,7 +22,7 @@ from summarize import short  # noqa: E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 TRAFFIC_KERNELS = ("rs_apply_kernel", "rs_apply_var_kernel", "sha256_lane_kernel",
-                   "encode_hash_kernel")
+                   "encode_hash_kernel", "rs_encode_bs_kernel")
 
 
 def mean(v):

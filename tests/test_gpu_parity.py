@@ -992,3 +992,32 @@ def test_apply_launch_split_over_part_ranges(monkeypatch, max_blocks):
     ce.reconstruct_batch(rs, batch, present.tobytes(), False)  # reconstruct split (var kernel)
     torch.cuda.synchronize()
     assert torch.equal(buf, ref)
+
+
+@pytest.mark.parametrize("d,p", [(3, 2), (10, 4), (20, 8)])
+@pytest.mark.parametrize("L", [16, 8192, 8192 + 16, 3 * 8192 - 16, 16384 + 5, 65536 + 4096])
+def test_bitsliced_encode_matches_vperm_and_oracle(monkeypatch, d, p, L):
+    """The compiled shapes' encode takes the bit-sliced kernel (rs_encode_bs_kernel: full
+    8 KiB column steps bit-sliced, the ragged rest through the v_perm byte path).  Every byte
+    must equal the v_perm kernel's (CEC_APPLY_BS=0) and, on sampled parts, the oracle's."""
+    t, n = d + p, 9
+    cstride = (L + 15) // 16 * 16 + 32  # 16-byte aligned, not a power of two
+    rs = ce.ReedSolomon(d, p)
+    buf = torch.zeros((n, t, cstride), dtype=torch.uint8, device=DEV)
+    batch = ce.PartBatch.from_tensor(buf, L)
+    ce.fill_synthetic(batch, d, 9000 + L)
+    ce.encode_batch(rs, batch)
+    torch.cuda.synchronize()
+    got = buf.clone()
+    monkeypatch.setenv("CEC_APPLY_BS", "0")
+    buf[:, d:] = 0
+    ce.encode_batch(rs, batch)
+    torch.cuda.synchronize()
+    assert torch.equal(got, buf)
+    assert not got[:, d:, L:].any()  # nothing written past the chunk
+    host = got.cpu().numpy()
+    for k in (0, n - 1):
+        st, par = oracle.encode_sep(d, p, [host[k, j, :L] for j in range(d)])
+        assert st == 0
+        for i in range(p):
+            assert np.array_equal(host[k, d + i, :L], par[i]), (k, i)
