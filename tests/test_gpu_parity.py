@@ -964,12 +964,13 @@ def test_chunk_longer_than_4gib_encode_and_reconstruct():
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("max_blocks", ["7", "64", "1000"])
+@pytest.mark.parametrize("max_blocks", ["9", "64", "1000"])
 def test_apply_launch_split_over_part_ranges(monkeypatch, max_blocks):
     """A dispatch holds at most 2^32-1 work-items, so encode / reconstruct batches of more
     blocks than that are split into launches over whole part ranges (rs_kernels.hip).  The test
-    knob CEC_APPLY_MAX_BLOCKS lowers the limit to force splits at test size (here 4 tiles per
-    part): every byte must match the unsplit launch."""
+    knob CEC_APPLY_MAX_BLOCKS lowers the limit to force splits at test size (here 9 tiles per
+    part for the bit-sliced encoder's 8 KiB tiles, 5 for the v_perm reconstruct's 16 KiB; the
+    smallest value is one part per launch for both): every byte must match the unsplit launch."""
     d, p, L, n = 10, 4, 4 * 16384 + 100, 37
     t = d + p
     rs = ce.ReedSolomon(d, p)

@@ -17,6 +17,8 @@ for c in c5 c5r; do
 done
 CEC_MULTI_COPY_THREADS=8 timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-north-star > $T/bench_c2_copy8.log 2>&1 || exit 1
 timeout -k 10 120 ./tools/ubench_stream 4096 m > $T/ubench_mix.log 2>&1 || exit 1
+timeout -k 10 120 ./tools/ubench_stream 4096 x > $T/ubench_w_xcd.log 2>&1 || exit 1
+cat $T/ubench_w_xcd.log
 cat $T/ubench_mix.log
 grep -v amdgpu.ids $T/smoke.log
 for c in c2 c2enc c3 c3e2 c3r c4 c5 c5r c2_copy8; do grep -o '"value": [0-9.]*\|"ms_per_step": [0-9.]*\|"frac": [0-9.]*\|"check[a-z_]*": [a-z]*' $T/bench_$c.log | tr '\n' ' '; echo " $c"; done

@@ -126,10 +126,15 @@ void run_mix(uint8_t* base, uint32_t parts) {
 
 // Reconstruct-shaped pattern: the D inputs read, W (< P) outputs written (a 2-erasure
 // reconstruct_data writes 1-2 data chunks per part).
-template <int V, bool NT, int W>
+template <int V, bool NT, int W, bool XCD = false>
 __global__ void stream_w_kernel(uint8_t* base, uint32_t tiles_per_part, size_t cs) {
-    const uint32_t part = blockIdx.x / tiles_per_part;
-    const uint32_t tile = blockIdx.x - part * tiles_per_part;
+    uint32_t b = blockIdx.x;
+    if (XCD) {  // as stream_mix_kernel: XCD x walks the blocks [x*n/8, (x+1)*n/8)
+        const uint32_t per = gridDim.x / 8;
+        b = (b % 8) * per + b / 8;
+    }
+    const uint32_t part = b / tiles_per_part;
+    const uint32_t tile = b - part * tiles_per_part;
     uint8_t* pb = base + size_t(part) * T * cs;
     const size_t x = size_t(tile) * blockDim.x * 16 * V + size_t(threadIdx.x) * 16;
     v4u acc[V];
@@ -150,7 +155,7 @@ __global__ void stream_w_kernel(uint8_t* base, uint32_t tiles_per_part, size_t c
             st<NT>(pb + (D + r) * cs + x + size_t(u) * blockDim.x * 16, acc[u] + v4u{unsigned(r), 0u, 0u, 0u});
 }
 
-template <int V, bool NT, int W>
+template <int V, bool NT, int W, bool XCD = false>
 void run_w(uint8_t* base, uint32_t parts, int threads) {
     const uint32_t tiles = uint32_t(L / (size_t(threads) * 16 * V));
     hipEvent_t a, b;
@@ -159,7 +164,7 @@ void run_w(uint8_t* base, uint32_t parts, int threads) {
     float best = 1e30f;
     for (int r = 0; r < 6; ++r) {
         CK(hipEventRecord(a));
-        hipLaunchKernelGGL((stream_w_kernel<V, NT, W>), dim3(parts * tiles), dim3(threads), 0, 0,
+        hipLaunchKernelGGL((stream_w_kernel<V, NT, W, XCD>), dim3(parts * tiles), dim3(threads), 0, 0,
                            base, tiles, L);
         CK(hipEventRecord(b));
         CK(hipEventSynchronize(b));
@@ -168,8 +173,8 @@ void run_w(uint8_t* base, uint32_t parts, int threads) {
         if (r && ms < best) best = ms;
     }
     const double bytes = double(parts) * (D + W) * L;
-    printf("reads %d + writes %d  V %d NT %d threads %4d : %8.3f ms  %7.0f GB/s\n", D, W, V,
-           int(NT), threads, best, bytes / best / 1e6);
+    printf("reads %d + writes %d  V %d NT %d threads %4d xcd-map %d : %8.3f ms  %7.0f GB/s\n", D, W,
+           V, int(NT), threads, int(XCD), best, bytes / best / 1e6);
     fflush(stdout);
 }
 
@@ -290,6 +295,17 @@ int main(int argc, char** argv) {
         run_w<1, true, 2>(base, parts, 256);
         run_w<2, false, 2>(base, parts, 256);
         run_w<2, true, 2>(base, parts, 512);
+        return 0;
+    }
+    if (argc > 2 && argv[2][0] == 'x') {  // reconstruct-shaped ceilings with the XCD-aware order
+        for (int rep = 0; rep < 2; ++rep) {
+            run_w<2, true, 1, false>(base, parts, 256);
+            run_w<2, true, 1, true>(base, parts, 256);
+            run_w<2, true, 2, false>(base, parts, 256);
+            run_w<2, true, 2, true>(base, parts, 256);
+            run_w<2, true, 4, false>(base, parts, 256);
+            run_w<2, true, 4, true>(base, parts, 256);
+        }
         return 0;
     }
     if (argc > 2 && argv[2][0] == 'm') {  // load / store policies and XCD-aware block mapping
