@@ -1531,10 +1531,12 @@ static int reconstruct_batch(const cec_codec* cc, const cec_part_batch* b, const
     // part's row count; wider patterns get a row-group launch per row count.
     std::vector<uint32_t> words;
     std::map<uint32_t, std::pair<std::vector<uint32_t>, std::vector<uint32_t>>> buckets;
+    uint32_t var_rows = 0;  // the shared launch's widest pattern: its kernel's row class
     for (auto& kv : groups) {
         auto rec = c->decode_record(kv.first);
         const uint32_t n_out = (*rec)[0];
         if (n_out == 0) continue;  // data_only: only parity missing, nothing to do
+        if (n_out <= max_var_rows()) var_rows = std::max(var_rows, n_out);
         const uint32_t off = uint32_t(words.size());
         words.insert(words.end(), rec->begin(), rec->end());
         auto& bk = buckets[n_out <= max_var_rows() ? 0u : n_out];  // 0 = the shared launch
@@ -1572,7 +1574,7 @@ static int reconstruct_batch(const cec_codec* cc, const cec_part_batch* b, const
         a.part_pat = dwords + launches[i].ids + launches[i].count;
         a.n_parts = uint32_t(launches[i].count);
         a.d = uint32_t(d);
-        a.n_rows = launches[i].n_out;
+        a.n_rows = launches[i].n_out ? launches[i].n_out : var_rows;
         a.lds_reserve = lds_reserve;
         hipError_t e = launches[i].n_out ? launch_rs_apply(a, vec, s)
                                          : launch_rs_apply_var(a, vec, s);

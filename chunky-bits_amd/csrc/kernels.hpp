@@ -20,7 +20,7 @@ struct ApplyParams {
     const uint32_t* part_pat;
     uint32_t n_parts;
     uint32_t d;
-    uint32_t n_rows;  // n_out shared by every pattern of this launch
+    uint32_t n_rows;  // n_out shared by every pattern of this launch (var launch: the largest)
     // Dynamic LDS each workgroup reserves (never touched; 0 = none).  Above 64 KiB a block
     // cannot share a CU with a SHA-256 lane-kernel workgroup (>= 64 KiB reserved each), which
     // keeps a decode running beside a verification off the SHA waves' SIMDs.

@@ -162,6 +162,113 @@ __device__ __forceinline__ void apply_tile(const ApplyParams& a, cu32* pat, uint
     }
 }
 
+// ---- compile-time d: the same multiply with every input's loads issued one group ahead ----
+// With d a run-time value the column loop above waits for each group's loads before it multiplies
+// (`unroll 1`, no prefetch across groups).  For the compiled input counts (rs_apply_var_kernel's
+// CDG instantiations) the loop unrolls at compile time and group J0 + G's loads go out before
+// group J0's multiplies, as in the bit-sliced encoder.
+template <int D, int G, int J0, int V>
+__device__ __forceinline__ void vp_load(uint4 (&v)[G][V], const uint8_t* pbase, uint64_t cs,
+                                        uint64_t x, cu32* in_idx) {
+#pragma unroll
+    for (int u = 0; u < G; ++u)
+        if (J0 + u < D) {
+            const uint8_t* src = pbase + uint64_t(in_idx[J0 + u]) * cs + x;
+#pragma unroll
+            for (int c = 0; c < V; ++c) v[u][c] = ld16<true>(src + c * kSpan);
+        }
+}
+
+template <int D, int RG, int G, int J0, int V>
+__device__ __forceinline__ void vp_mul(uint32_t (&acc)[RG][V][4], uint4 (&v)[G][V], cu32* tab,
+                                       uint32_t tab_stride) {
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+        if (J0 + u < D) {
+            cu32* tj = tab + size_t(J0 + u) * tab_stride;
+#pragma unroll
+            for (int c = 0; c < V; ++c) {
+                const Sel s0 = selectors(v[u][c].x), s1 = selectors(v[u][c].y),
+                          s2 = selectors(v[u][c].z), s3 = selectors(v[u][c].w);
+#pragma unroll
+                for (int r = 0; r < RG; ++r) {
+                    cu32* t = tj + r * kTabWords;
+                    const uint32_t t0 = t[0], t1 = t[1], t2 = t[2], t3 = t[3], t4 = t[4];
+                    acc[r][c][0] ^= gmul(s0, t0, t1, t2, t3, t4);
+                    acc[r][c][1] ^= gmul(s1, t0, t1, t2, t3, t4);
+                    acc[r][c][2] ^= gmul(s2, t0, t1, t2, t3, t4);
+                    acc[r][c][3] ^= gmul(s3, t0, t1, t2, t3, t4);
+                }
+            }
+        }
+    }
+}
+
+template <int D, int RG, int G, int J0, int V>
+struct VpSteps {
+    __device__ static __forceinline__ void run(uint32_t (&acc)[RG][V][4], uint4 (&v)[2][G][V],
+                                               const uint8_t* pbase, uint64_t cs, uint64_t x,
+                                               cu32* in_idx, cu32* tab, uint32_t tab_stride) {
+        constexpr int buf = (J0 / G) & 1;
+        if constexpr (J0 + G < D) vp_load<D, G, J0 + G, V>(v[buf ^ 1], pbase, cs, x, in_idx);
+        vp_mul<D, RG, G, J0, V>(acc, v[buf], tab, tab_stride);
+        if constexpr (J0 + G < D)
+            VpSteps<D, RG, G, J0 + G, V>::run(acc, v, pbase, cs, x, in_idx, tab, tab_stride);
+    }
+};
+
+// apply_column<RG, true, ., V, true> for d == D.
+template <int D, int RG, int G, int V>
+__device__ __forceinline__ void vp_column(uint8_t* pbase, uint64_t cs, uint64_t x,
+                                          uint32_t tab_stride, cu32* in_idx, cu32* out_idx,
+                                          cu32* tab) {
+    uint32_t acc[RG][V][4];
+#pragma unroll
+    for (int r = 0; r < RG; ++r)
+#pragma unroll
+        for (int c = 0; c < V; ++c) acc[r][c][0] = acc[r][c][1] = acc[r][c][2] = acc[r][c][3] = 0u;
+    uint4 v[2][G][V];
+    vp_load<D, G, 0, V>(v[0], pbase, cs, x, in_idx);
+    VpSteps<D, RG, G, 0, V>::run(acc, v, pbase, cs, x, in_idx, tab, tab_stride);
+#pragma unroll
+    for (int r = 0; r < RG; ++r) {
+        uint8_t* dst = pbase + uint64_t(out_idx[r]) * cs + x;
+#pragma unroll
+        for (int c = 0; c < V; ++c)
+            st16<true>(dst + c * kSpan,
+                       make_uint4(acc[r][c][0], acc[r][c][1], acc[r][c][2], acc[r][c][3]));
+    }
+}
+
+// apply_tile with d == D (aligned layout, non-temporal, two columns per lane): full steps take
+// vp_column, the ragged end the byte path.
+template <int D, int RG, int G>
+__device__ __forceinline__ void apply_tile_cd(const ApplyParams& a, cu32* pat, uint32_t part,
+                                              uint32_t tile, uint32_t n_out, uint32_t tile_bytes) {
+    constexpr int V = 2;
+    cu32* in_idx = pat + 1;
+    cu32* out_idx = pat + 1 + D;
+    cu32* tab = pat + 1 + D + n_out;
+    const uint32_t tab_stride = n_out * kTabWords;
+    uint8_t* pbase = a.base + uint64_t(part) * a.part_stride;
+    const uint64_t len = a.len;
+    const uint64_t cs = a.chunk_stride;
+    const uint64_t t0 = uint64_t(tile) * tile_bytes;
+    const uint64_t t1 = t0 + tile_bytes < len ? t0 + tile_bytes : len;
+#pragma unroll 1
+    for (uint64_t xb = t0; xb < t1; xb += kSpan * V) {  // block-uniform
+        const uint64_t x = xb + uint64_t(threadIdx.x) * 16u;
+        if (xb + kSpan * V <= len) {
+            vp_column<D, RG, G, V>(pbase, cs, x, tab_stride, in_idx, out_idx, tab);
+        } else {
+#pragma unroll 1
+            for (uint64_t xc = x; xc < t1 && xc < xb + kSpan * V; xc += kSpan)
+                apply_column<RG, false, 4, 1, false>(pbase, cs, xc, len - xc, D, tab_stride,
+                                                     in_idx, out_idx, tab);
+        }
+    }
+}
+
 // XCD-aware block order.  The dispatcher deals a grid's blocks to the 8 XCDs round-robin (block
 // b to XCD b % 8), so in launch order neighbouring tiles of a part land on different XCDs and
 // every XCD streams a slice of every part at once.  Renumbering so that XCD x runs the contiguous
@@ -194,9 +301,20 @@ __global__ __launch_bounds__(kApplyThreads) void rs_apply_kernel(ApplyParams a,
 }
 
 // Reconstruct with mixed erasure counts in ONE launch: every listed part's pattern carries its
-// own row count n_out (1..8, the record's first word); each block branches (block-uniformly)
-// to the exact-RG body, so no row is predicated inside the inner loop.
-template <bool VEC, int GROUP, int V, bool NT>
+// own row count n_out (1..MAXRG, the record's first word); each block branches (block-uniformly)
+// to the exact-RG body, so no row is predicated inside the inner loop.  MAXRG is the batch's
+// largest row count rounded up to 2, 4 or 8 (host side): the kernel's register allocation is the
+// widest body's, so a 2-erasure batch compiled for 8 rows would run at half the occupancy.
+// CD > 0 (aligned non-temporal builds only): the batch's d equals CD (host-checked), every tile
+// takes apply_tile_cd with loads CDG inputs ahead.
+template <int RG, int MAXRG, typename F>
+__device__ __forceinline__ void rg_dispatch(uint32_t n, F&& f) {
+    if (n == RG) f(std::integral_constant<int, RG>{});
+    else if constexpr (RG < MAXRG) rg_dispatch<RG + 1, MAXRG>(n, f);
+    // n > MAXRG or 0: never listed (the host routes n_out > 8 to row-group launches)
+}
+
+template <bool VEC, int GROUP, int V, bool NT, int MAXRG, int CD = 0, int CDG = 0>
 __global__ __launch_bounds__(kApplyThreads) void rs_apply_var_kernel(ApplyParams a,
                                                                      uint32_t tiles_per_part,
                                                                      bool xcd, uint32_t tile_bytes) {
@@ -205,17 +323,15 @@ __global__ __launch_bounds__(kApplyThreads) void rs_apply_var_kernel(ApplyParams
     const uint32_t tile = bx - lp * tiles_per_part;
     const uint32_t part = as_const(a.part_ids)[lp];
     cu32* pat = as_const(a.pat) + as_const(a.part_pat)[lp];
-    switch (pat[0]) {
-        case 1: apply_tile<1, VEC, GROUP, V, NT>(a, pat, part, tile, 1, 0, tile_bytes); break;
-        case 2: apply_tile<2, VEC, GROUP, V, NT>(a, pat, part, tile, 2, 0, tile_bytes); break;
-        case 3: apply_tile<3, VEC, GROUP, V, NT>(a, pat, part, tile, 3, 0, tile_bytes); break;
-        case 4: apply_tile<4, VEC, GROUP, V, NT>(a, pat, part, tile, 4, 0, tile_bytes); break;
-        case 5: apply_tile<5, VEC, GROUP, V, NT>(a, pat, part, tile, 5, 0, tile_bytes); break;
-        case 6: apply_tile<6, VEC, GROUP, V, NT>(a, pat, part, tile, 6, 0, tile_bytes); break;
-        case 7: apply_tile<7, VEC, GROUP, V, NT>(a, pat, part, tile, 7, 0, tile_bytes); break;
-        case 8: apply_tile<8, VEC, GROUP, V, NT>(a, pat, part, tile, 8, 0, tile_bytes); break;
-        default: break;  // the host routes n_out > 8 to row-group launches
-    }
+    rg_dispatch<1, MAXRG>(pat[0], [&](auto rg) {
+        constexpr int RG = decltype(rg)::value;
+        if constexpr (CD > 0) {
+            static_assert(VEC && V == 2 && NT, "compile-time d: aligned non-temporal build");
+            apply_tile_cd<CD, RG, CDG>(a, pat, part, tile, RG, tile_bytes);
+        } else {
+            apply_tile<RG, VEC, GROUP, V, NT>(a, pat, part, tile, RG, 0, tile_bytes);
+        }
+    });
 }
 
 // ------------------------------------------------------------------------------------------
@@ -452,6 +568,21 @@ bool apply_xcd() {
     return !(e && e[0] == '0');
 }
 
+// CEC_APPLY_RGCLS (A/B knob, read per launch; unset = 1): 0 runs every reconstruct batch on the
+// var kernel compiled for 8 rows instead of the batch's row class (2, 4 or 8).
+bool apply_rg_classes() {
+    const char* e = std::getenv("CEC_APPLY_RGCLS");
+    return !(e && e[0] == '0');
+}
+
+// CEC_APPLY_CD (A/B knob, read per launch): 0 = run-time d everywhere; 2, 5 or 10 = for d == 10
+// reconstruct batches, the compile-time-d var kernel with loads that many inputs ahead.
+int apply_cd_group() {
+    const char* e = std::getenv("CEC_APPLY_CD");
+    const int v = e ? std::atoi(e) : 0;
+    return v == 2 || v == 5 || v == 10 ? v : 0;
+}
+
 // CEC_APPLY_TILE (A/B knob, read per launch): bytes of one part's column range per block, a
 // multiple of 8 KiB (one full two-column step of a block) up to 256 KiB; default `def`:
 // kApplyTile for the v_perm kernels, kBsTile for the bit-sliced encoder.  Measured interleaved
@@ -638,28 +769,60 @@ hipError_t launch_rs_apply(const ApplyParams& a, bool vec16, hipStream_t s) {
 }
 
 // Listed parts (part_ids / part_pat) whose patterns have 1..kMaxApplyRows rows each: one launch.
+// a.n_rows = the largest row count in the batch (0: unknown, up to kMaxApplyRows).
 hipError_t launch_rs_apply_var(const ApplyParams& a, bool vec16, hipStream_t s) {
     if (a.n_parts == 0 || a.len == 0) return hipSuccess;
     if (!a.part_ids || !a.part_pat) return hipErrorInvalidValue;
+    if (a.n_rows > kMaxApplyRows) return hipErrorInvalidValue;
     const uint64_t tb = apply_tile_bytes();
     const uint64_t tiles = (a.len + tb - 1) / tb;
     const uint64_t max_blocks = max_apply_blocks();
     if (tiles > max_blocks) return hipErrorInvalidValue;
+    const int cdg = apply_cd_group();
+    const uint32_t rows = a.n_rows ? a.n_rows : kMaxApplyRows;
+    const int cls = !apply_rg_classes() ? 8 : rows <= 2 ? 2 : rows <= 4 ? 4 : 8;  // MAXRG
     return for_part_ranges(a, max_blocks / tiles, [&](const ApplyParams& b) {
         const dim3 grid(uint32_t(b.n_parts * tiles));
-        return dispatch_apply(vec16, [&](auto k) {
-            using T = Tune<decltype(k)::value>;
-            auto* kern = &rs_apply_var_kernel<T::kVec, T::kGroup, T::kV, T::kNt>;
+        auto go = [&](auto* kern) {
             if (!allow_lds(kern, b.lds_reserve)) return hipErrorInvalidValue;
             clear_stale_error();
             hipLaunchKernelGGL(kern, grid, dim3(kApplyThreads), b.lds_reserve, s, b,
                                uint32_t(tiles), apply_xcd(), uint32_t(tb));
             return hipGetLastError();
+        };
+        auto by_class = [&](auto k2, auto k4, auto k8) {
+            return cls == 2 ? go(k2) : cls == 4 ? go(k4) : go(k8);
+        };
+        if (vec16 && apply_tune() == 1 && b.d == 10 && cdg) {
+            switch (cdg) {
+                case 2: return by_class(&rs_apply_var_kernel<true, 4, 2, true, 2, 10, 2>,
+                                        &rs_apply_var_kernel<true, 4, 2, true, 4, 10, 2>,
+                                        &rs_apply_var_kernel<true, 4, 2, true, 8, 10, 2>);
+                case 5: return by_class(&rs_apply_var_kernel<true, 4, 2, true, 2, 10, 5>,
+                                        &rs_apply_var_kernel<true, 4, 2, true, 4, 10, 5>,
+                                        &rs_apply_var_kernel<true, 4, 2, true, 8, 10, 5>);
+                default: return by_class(&rs_apply_var_kernel<true, 4, 2, true, 2, 10, 10>,
+                                         &rs_apply_var_kernel<true, 4, 2, true, 4, 10, 10>,
+                                         &rs_apply_var_kernel<true, 4, 2, true, 8, 10, 10>);
+            }
+        }
+        return dispatch_apply(vec16, [&](auto k) {
+            using T = Tune<decltype(k)::value>;
+            // the default build (nt) and the byte-granular one get the row classes; the other
+            // tuning codes are A/B builds at the full 8 rows
+            constexpr bool classes = decltype(k)::value == 1 || decltype(k)::value == -1;
+            if constexpr (classes)
+                return by_class(&rs_apply_var_kernel<T::kVec, T::kGroup, T::kV, T::kNt, 2>,
+                                &rs_apply_var_kernel<T::kVec, T::kGroup, T::kV, T::kNt, 4>,
+                                &rs_apply_var_kernel<T::kVec, T::kGroup, T::kV, T::kNt, 8>);
+            else
+                return go(&rs_apply_var_kernel<T::kVec, T::kGroup, T::kV, T::kNt, 8>);
         });
     });
 }
 
 uint32_t max_var_rows() { return kMaxApplyRows; }
+
 
 hipError_t launch_fill(const FillParams& a, hipStream_t s) {
     const uint64_t n_inst = uint64_t(a.n_parts) * a.n_chunks;
