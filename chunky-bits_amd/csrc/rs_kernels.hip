@@ -568,6 +568,26 @@ bool apply_xcd() {
     return !(e && e[0] == '0');
 }
 
+// Residency cap.  The GF kernels stream 10-28 chunks per part 1 MiB (chunk stride) apart, and on
+// MI355X they run faster with FEWER blocks in flight than their registers allow: interleaved on
+// one box (profiles/r3_occ_ab/), RS(10,4) bit-sliced encode 9.53 ms at 2 blocks (= waves per
+// SIMD) per CU vs 9.88 at its register-bound 6; 2-erasure reconstruct_data 8.11 at 2 vs 8.26 at
+// 3 (the 8-row build) and 8.57 at 6 (the 2-row build); C3 (1-4 rows) 9.58 at 3 vs 10.15 at 2;
+// RS(20,8) encode no different (3 by registers).  The cap is an unused LDS reservation (160 KiB
+// per CU), on top of any the caller asked for, and only for grids of at least kCapMinBlocks
+// blocks (the device-resident batches it was measured on; the host pipelines' 256-part batches
+// share the chip with SHA-256 kernels and keep the register-bound occupancy).
+// CEC_APPLY_BLOCKS_PER_CU (A/B knob, read per launch): n > 0 caps every apply launch at n blocks
+// per CU, 0 turns the cap off; unset = the per-kernel default `def_cap` (0 = none).
+constexpr uint64_t kCapMinBlocks = 65536;
+uint32_t apply_lds(uint32_t reserve, int def_cap, uint64_t n_blocks) {
+    const char* e = std::getenv("CEC_APPLY_BLOCKS_PER_CU");
+    int n = e ? std::atoi(e) : (n_blocks >= kCapMinBlocks ? def_cap : 0);
+    if (n <= 0 || n > 16) return reserve;
+    const uint32_t lds = 163840u / uint32_t(n + 1) + 2048u;  // floor(160 KiB / lds) == n
+    return std::max(reserve, lds);
+}
+
 // CEC_APPLY_RGCLS (A/B knob, read per launch; unset = 1): 0 runs every reconstruct batch on the
 // var kernel compiled for 8 rows instead of the batch's row class (2, 4 or 8).
 bool apply_rg_classes() {
@@ -671,9 +691,10 @@ hipError_t launch_rg(const ApplyParams& a, uint32_t row_base, uint32_t groups, b
         return dispatch_apply(vec16, [&](auto k) {
             using T = Tune<decltype(k)::value>;
             auto* kern = &rs_apply_kernel<RG, T::kVec, T::kGroup, T::kV, T::kNt>;
-            if (!allow_lds(kern, b.lds_reserve)) return hipErrorInvalidValue;
+            const uint32_t lds = apply_lds(b.lds_reserve, 0, uint64_t(grid.x) * groups);
+            if (!allow_lds(kern, lds)) return hipErrorInvalidValue;
             clear_stale_error();
-            hipLaunchKernelGGL(kern, grid, dim3(kApplyThreads), b.lds_reserve, s, b,
+            hipLaunchKernelGGL(kern, grid, dim3(kApplyThreads), lds, s, b,
                                uint32_t(tiles), row_base, apply_xcd(), uint32_t(tb));
             return hipGetLastError();
         });
@@ -709,10 +730,13 @@ hipError_t launch_bs(const ApplyParams& a, hipStream_t s) {
     if (tiles > max_blocks) return hipErrorInvalidValue;
     return for_part_ranges(a, max_blocks / tiles, [&](const ApplyParams& b) {
         auto* kern = &rs_encode_bs_kernel<D, P>;
-        if (!allow_lds(kern, b.lds_reserve)) return hipErrorInvalidValue;
+        const uint64_t n_blocks = b.n_parts * tiles;
+        // measured for RS(10,4) (2 blocks per CU); the other shapes keep their occupancy
+        const uint32_t lds = apply_lds(b.lds_reserve, D == 10 && P == 4 ? 2 : 0, n_blocks);
+        if (!allow_lds(kern, lds)) return hipErrorInvalidValue;
         clear_stale_error();
-        hipLaunchKernelGGL(kern, dim3(uint32_t(b.n_parts * tiles)), dim3(kApplyThreads),
-                           b.lds_reserve, s, b, uint32_t(tiles), apply_xcd(), uint32_t(tb));
+        hipLaunchKernelGGL(kern, dim3(uint32_t(n_blocks)), dim3(kApplyThreads), lds, s, b,
+                           uint32_t(tiles), apply_xcd(), uint32_t(tb));
         return hipGetLastError();
     });
 }
@@ -783,10 +807,12 @@ hipError_t launch_rs_apply_var(const ApplyParams& a, bool vec16, hipStream_t s) 
     const int cls = !apply_rg_classes() ? 8 : rows <= 2 ? 2 : rows <= 4 ? 4 : 8;  // MAXRG
     return for_part_ranges(a, max_blocks / tiles, [&](const ApplyParams& b) {
         const dim3 grid(uint32_t(b.n_parts * tiles));
+        // 2-row class: 2 blocks per CU, 4-row class: 3, 8-row: by registers (3)
+        const uint32_t lds = apply_lds(b.lds_reserve, cls == 2 ? 2 : cls == 4 ? 3 : 0, grid.x);
         auto go = [&](auto* kern) {
-            if (!allow_lds(kern, b.lds_reserve)) return hipErrorInvalidValue;
+            if (!allow_lds(kern, lds)) return hipErrorInvalidValue;
             clear_stale_error();
-            hipLaunchKernelGGL(kern, grid, dim3(kApplyThreads), b.lds_reserve, s, b,
+            hipLaunchKernelGGL(kern, grid, dim3(kApplyThreads), lds, s, b,
                                uint32_t(tiles), apply_xcd(), uint32_t(tb));
             return hipGetLastError();
         };

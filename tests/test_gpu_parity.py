@@ -412,6 +412,32 @@ def test_reconstruct_batch_random_patterns(d, p, L, data_only):
                 assert out[i].tobytes() == got[k, i].tobytes()
 
 
+@pytest.mark.parametrize("d,p,max_miss", [(10, 4, 1), (10, 4, 2), (10, 4, 3), (20, 8, 5),
+                                          (20, 8, 8)])
+def test_reconstruct_row_classes(d, p, max_miss):
+    """The shared reconstruct launch compiles its kernel for the batch's widest pattern rounded
+    up to 2, 4 or 8 rows (rs_kernels.hip launch_rs_apply_var): batches whose widest pattern sits
+    on each side of a class boundary rebuild every chunk bit-exact, data + parity."""
+    n_parts, t, L = 64, d + p, 2 * 8192 + 48
+    buf, batch = _device_parts(n_parts, t, L, None, seed=d * 100 + max_miss)
+    rs = ce.ReedSolomon(d, p)
+    ce.encode_batch(rs, batch)
+    ref = buf.clone()
+    rng = np.random.default_rng(max_miss)
+    present = np.ones((n_parts, t), dtype=np.uint8)
+    for k in range(n_parts):
+        present[k, rng.choice(t, 1 + k % max_miss, replace=False)] = 0
+    buf[~torch.from_numpy(present).to(DEV).bool()] = 0
+    ce.reconstruct_batch(rs, batch, present.tobytes(), False)
+    torch.cuda.synchronize()
+    assert torch.equal(buf, ref)
+    want = ref.cpu().numpy()
+    k = n_parts - 1
+    shards = [want[k, i].tobytes() if present[k, i] else None for i in range(t)]
+    st, out = oracle.reconstruct(d, p, shards, data_only=False)
+    assert st == 0 and all(out[i].tobytes() == want[k, i].tobytes() for i in range(t))
+
+
 def test_reconstruct_batch_too_few_present_launches_nothing():
     d, p, L = 3, 2, 256
     buf, batch = _device_parts(4, d + p, L, None, seed=9)
