@@ -595,12 +595,14 @@ bool apply_rg_classes() {
     return !(e && e[0] == '0');
 }
 
-// CEC_APPLY_CD (A/B knob, read per launch): 0 = run-time d everywhere; 2, 5 or 10 = for d == 10
-// reconstruct batches, the compile-time-d var kernel with loads that many inputs ahead.
-int apply_cd_group() {
+// CEC_APPLY_CD (A/B knob, read per launch; unset = 1): for d == 10 reconstruct batches, the
+// compile-time-d var kernel (apply_tile_cd, loads 5 inputs ahead); 0 = the run-time-d kernel.
+// Interleaved on one box with the residency caps (profiles/r3_cap_ab/): c3e2 8.07-8.09 vs
+// 8.12-8.14 ms, C3 9.64-9.68 vs 9.71-9.75 (groups of 2 and 10 measured the same as 5 without
+// the caps, profiles/r3_cd_ab/).
+bool apply_cd() {
     const char* e = std::getenv("CEC_APPLY_CD");
-    const int v = e ? std::atoi(e) : 0;
-    return v == 2 || v == 5 || v == 10 ? v : 0;
+    return !(e && e[0] == '0');
 }
 
 // CEC_APPLY_TILE (A/B knob, read per launch): bytes of one part's column range per block, a
@@ -802,7 +804,7 @@ hipError_t launch_rs_apply_var(const ApplyParams& a, bool vec16, hipStream_t s) 
     const uint64_t tiles = (a.len + tb - 1) / tb;
     const uint64_t max_blocks = max_apply_blocks();
     if (tiles > max_blocks) return hipErrorInvalidValue;
-    const int cdg = apply_cd_group();
+    const bool cd = apply_cd();
     const uint32_t rows = a.n_rows ? a.n_rows : kMaxApplyRows;
     const int cls = !apply_rg_classes() ? 8 : rows <= 2 ? 2 : rows <= 4 ? 4 : 8;  // MAXRG
     return for_part_ranges(a, max_blocks / tiles, [&](const ApplyParams& b) {
@@ -819,19 +821,10 @@ hipError_t launch_rs_apply_var(const ApplyParams& a, bool vec16, hipStream_t s) 
         auto by_class = [&](auto k2, auto k4, auto k8) {
             return cls == 2 ? go(k2) : cls == 4 ? go(k4) : go(k8);
         };
-        if (vec16 && apply_tune() == 1 && b.d == 10 && cdg) {
-            switch (cdg) {
-                case 2: return by_class(&rs_apply_var_kernel<true, 4, 2, true, 2, 10, 2>,
-                                        &rs_apply_var_kernel<true, 4, 2, true, 4, 10, 2>,
-                                        &rs_apply_var_kernel<true, 4, 2, true, 8, 10, 2>);
-                case 5: return by_class(&rs_apply_var_kernel<true, 4, 2, true, 2, 10, 5>,
-                                        &rs_apply_var_kernel<true, 4, 2, true, 4, 10, 5>,
-                                        &rs_apply_var_kernel<true, 4, 2, true, 8, 10, 5>);
-                default: return by_class(&rs_apply_var_kernel<true, 4, 2, true, 2, 10, 10>,
-                                         &rs_apply_var_kernel<true, 4, 2, true, 4, 10, 10>,
-                                         &rs_apply_var_kernel<true, 4, 2, true, 8, 10, 10>);
-            }
-        }
+        if (vec16 && apply_tune() == 1 && b.d == 10 && cd)
+            return by_class(&rs_apply_var_kernel<true, 4, 2, true, 2, 10, 5>,
+                            &rs_apply_var_kernel<true, 4, 2, true, 4, 10, 5>,
+                            &rs_apply_var_kernel<true, 4, 2, true, 8, 10, 5>);
         return dispatch_apply(vec16, [&](auto k) {
             using T = Tune<decltype(k)::value>;
             // the default build (nt) and the byte-granular one get the row classes; the other
