@@ -607,10 +607,11 @@ bool apply_cd() {
 
 // CEC_APPLY_TILE (A/B knob, read per launch): bytes of one part's column range per block, a
 // multiple of 8 KiB (one full two-column step of a block) up to 256 KiB; default `def`:
-// kApplyTile for the v_perm kernels, kBsTile for the bit-sliced encoder.  Measured interleaved
-// on one box (profiles/r3_tile2_ab/, 8 vs 16 KiB): bit-sliced C2 encode 9.56 vs 9.69 ms, RS(20,8)
-// encode 4.89-4.91 vs 5.20; c3e2 7.97 vs 8.08, but C3 (1-4 rows, data + parity) 9.90-10.00 vs
-// 9.48-9.51, so the v_perm kernels keep 16 KiB.
+// kApplyTile for rs_apply_kernel, kBsTile for the bit-sliced encoder and the mixed-pattern
+// reconstruct.  Measured interleaved on one box with the residency caps
+// (profiles/r3_tilecap_ab/, 8 / 16 / 32 KiB): RS(10,4) bit-sliced encode 9.46 / 9.72 / 9.86 ms,
+// c3e2 7.89 / 7.96 / 8.39, C3 9.20 / 9.35 / 9.61.  (Without the caps C3 had preferred 16 KiB,
+// profiles/r3_tile2_ab/.)
 constexpr uint64_t kBsTile = 8192;
 uint64_t apply_tile_bytes(uint64_t def = kApplyTile) {
     const char* e = std::getenv("CEC_APPLY_TILE");
@@ -800,7 +801,7 @@ hipError_t launch_rs_apply_var(const ApplyParams& a, bool vec16, hipStream_t s) 
     if (a.n_parts == 0 || a.len == 0) return hipSuccess;
     if (!a.part_ids || !a.part_pat) return hipErrorInvalidValue;
     if (a.n_rows > kMaxApplyRows) return hipErrorInvalidValue;
-    const uint64_t tb = apply_tile_bytes();
+    const uint64_t tb = apply_tile_bytes(kBsTile);  // 8 KiB with the caps (see kBsTile)
     const uint64_t tiles = (a.len + tb - 1) / tb;
     const uint64_t max_blocks = max_apply_blocks();
     if (tiles > max_blocks) return hipErrorInvalidValue;

@@ -20,3 +20,5 @@ for rep in 1 2 3; do
     run "t${tile}_$rep" c3 CEC_APPLY_TILE=$tile
   done
 done
+timeout -k 10 120 ./tools/ubench_stream 4096 c > $T/ubench_caps.log 2>&1 || exit 1
+cat $T/ubench_caps.log

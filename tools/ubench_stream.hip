@@ -98,7 +98,12 @@ __global__ void stream_mix_kernel(uint8_t* base, uint32_t tiles_per_part, uint32
 }
 
 template <int V, bool NTL, bool NTS, bool XCD>
-void run_mix(uint8_t* base, uint32_t parts) {
+void run_mix(uint8_t* base, uint32_t parts, int cap = 0) {
+    // cap > 0: at most `cap` 256-thread blocks per CU (an unused LDS reservation, 160 KiB per CU)
+    const uint32_t lds = cap > 0 ? 163840u / uint32_t(cap + 1) + 2048u : 0u;
+    if (lds > 65536)
+        CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&stream_mix_kernel<V, NTL, NTS, XCD>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
     const uint32_t tiles = uint32_t(L / (size_t(256) * 16 * V));
     const uint32_t n = parts * tiles;
     hipEvent_t a, b;
@@ -107,7 +112,7 @@ void run_mix(uint8_t* base, uint32_t parts) {
     float best = 1e30f, sum = 0;
     for (int r = 0; r < 8; ++r) {
         CK(hipEventRecord(a));
-        hipLaunchKernelGGL((stream_mix_kernel<V, NTL, NTS, XCD>), dim3(n), dim3(256), 0, 0, base,
+        hipLaunchKernelGGL((stream_mix_kernel<V, NTL, NTS, XCD>), dim3(n), dim3(256), lds, 0, base,
                            tiles, n);
         CK(hipEventRecord(b));
         CK(hipEventSynchronize(b));
@@ -119,8 +124,8 @@ void run_mix(uint8_t* base, uint32_t parts) {
         }
     }
     const double bytes = double(parts) * T * L;
-    printf("mix V %d nt-load %d nt-store %d xcd-map %d : best %8.3f ms %7.0f GB/s, mean %7.0f GB/s\n",
-           V, int(NTL), int(NTS), int(XCD), best, bytes / best / 1e6, bytes / (sum / 7) / 1e6);
+    printf("mix V %d nt-load %d nt-store %d xcd-map %d cap %d : best %8.3f ms %7.0f GB/s, mean %7.0f GB/s\n",
+           V, int(NTL), int(NTS), int(XCD), cap, best, bytes / best / 1e6, bytes / (sum / 7) / 1e6);
     fflush(stdout);
 }
 
@@ -156,7 +161,11 @@ __global__ void stream_w_kernel(uint8_t* base, uint32_t tiles_per_part, size_t c
 }
 
 template <int V, bool NT, int W, bool XCD = false>
-void run_w(uint8_t* base, uint32_t parts, int threads) {
+void run_w(uint8_t* base, uint32_t parts, int threads, int cap = 0) {
+    const uint32_t lds = cap > 0 ? 163840u / uint32_t(cap + 1) + 2048u : 0u;
+    if (lds > 65536)
+        CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&stream_w_kernel<V, NT, W, XCD>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
     const uint32_t tiles = uint32_t(L / (size_t(threads) * 16 * V));
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
@@ -164,7 +173,7 @@ void run_w(uint8_t* base, uint32_t parts, int threads) {
     float best = 1e30f;
     for (int r = 0; r < 6; ++r) {
         CK(hipEventRecord(a));
-        hipLaunchKernelGGL((stream_w_kernel<V, NT, W, XCD>), dim3(parts * tiles), dim3(threads), 0, 0,
+        hipLaunchKernelGGL((stream_w_kernel<V, NT, W, XCD>), dim3(parts * tiles), dim3(threads), lds, 0,
                            base, tiles, L);
         CK(hipEventRecord(b));
         CK(hipEventSynchronize(b));
@@ -173,8 +182,8 @@ void run_w(uint8_t* base, uint32_t parts, int threads) {
         if (r && ms < best) best = ms;
     }
     const double bytes = double(parts) * (D + W) * L;
-    printf("reads %d + writes %d  V %d NT %d threads %4d xcd-map %d : %8.3f ms  %7.0f GB/s\n", D, W,
-           V, int(NT), threads, int(XCD), best, bytes / best / 1e6);
+    printf("reads %d + writes %d  V %d NT %d threads %4d xcd-map %d cap %d : %8.3f ms  %7.0f GB/s\n",
+           D, W, V, int(NT), threads, int(XCD), cap, best, bytes / best / 1e6);
     fflush(stdout);
 }
 
@@ -305,6 +314,16 @@ int main(int argc, char** argv) {
             run_w<2, true, 2, true>(base, parts, 256);
             run_w<2, true, 4, false>(base, parts, 256);
             run_w<2, true, 4, true>(base, parts, 256);
+        }
+        return 0;
+    }
+    if (argc > 2 && argv[2][0] == 'c') {  // residency caps (blocks per CU) on the best mix shape
+        for (int rep = 0; rep < 2; ++rep) {
+            for (int cap : {0, 1, 2, 3, 4, 6}) run_mix<2, true, true, true>(base, parts, cap);
+            for (int cap : {0, 2, 3}) {
+                run_w<2, true, 1, true>(base, parts, 256, cap);
+                run_w<2, true, 2, true>(base, parts, 256, cap);
+            }
         }
         return 0;
     }
