@@ -805,7 +805,10 @@ hipError_t launch_rs_apply_var(const ApplyParams& a, bool vec16, hipStream_t s) 
     const uint64_t tiles = (a.len + tb - 1) / tb;
     const uint64_t max_blocks = max_apply_blocks();
     if (tiles > max_blocks) return hipErrorInvalidValue;
-    const bool cd = apply_cd();
+    // not under a caller's LDS reservation: the read path's decode beside the SHA-256
+    // verification (capi.cpp decode_lds) loses with it (c3r 44.0-44.5 vs 42.6-42.8 ms,
+    // profiles/r3_c3r_ab/): its loads run ahead into the SHA chains' bandwidth
+    const bool cd = apply_cd() && a.lds_reserve == 0;
     const uint32_t rows = a.n_rows ? a.n_rows : kMaxApplyRows;
     const int cls = !apply_rg_classes() ? 8 : rows <= 2 ? 2 : rows <= 4 ? 4 : 8;  // MAXRG
     return for_part_ranges(a, max_blocks / tiles, [&](const ApplyParams& b) {
