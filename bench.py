@@ -597,6 +597,96 @@ def north_star_block(codec, batch, buf, digests, stream, device, rank, d, p, L, 
     return out
 
 
+def c3_erasures(n_parts: int, t: int, p: int, rank: int):
+    """The c3 config's erasure sets: 1..p random erasures per part (seeded)."""
+    g = torch.Generator().manual_seed(1234 + rank)
+    pres = torch.ones((n_parts, t), dtype=torch.uint8)
+    k = torch.randint(1, p + 1, (n_parts,), generator=g)
+    for i in range(n_parts):
+        pres[i, torch.randperm(t, generator=g)[: int(k[i])]] = 0
+    return pres
+
+
+def baseline_configs_block(codec, batch, buf, digests, stream, device, rank, d, p, L, steps):
+    """BASELINE.json's other device-resident configurations in the default line, so the driver's
+    run observes them too: configs[2] (C3: RS(10,4) reconstruct with 1-4 random erasures per
+    part, data + parity, file_part.rs:304) on the headline's buffer, and configs[3] (C4: RS(20,8),
+    4 096 parts x 256 KiB, fused encode + SHA-256 of all 28 chunks) on a buffer of its own.
+    Each is checked size-independently on the GPU: after the rebuild every chunk (C3) / after an
+    erase-and-rebuild round trip every chunk (C4) hashes to the digest its encode step computed."""
+    n, t = batch.n_parts, d + p
+    out = {}
+
+    def timed(fn):
+        fn()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(steps)]
+        for a, b in evs:
+            a.record(stream)
+            fn()
+            b.record(stream)
+        torch.cuda.synchronize(device)
+        return sum(a.elapsed_time(b) for a, b in evs) / steps
+
+    def verified(bt, dg, nchunks, nparts):
+        ok = torch.zeros((nparts, nchunks), dtype=torch.uint8, device=device)
+        ce.verify_batch(bt, 0, nchunks, dg.data_ptr(), ok.data_ptr(), stream=stream)
+        torch.cuda.synchronize(device)
+        return bool(ok.all().item())
+
+    # C3: restore the parity north_star's data-only rebuild left erased, then 1-4 erasures
+    ce.encode_batch(codec, batch, stream)
+    pres = c3_erasures(n, t, p, rank)
+    present = bytes(pres.flatten().tolist())
+    buf.mul_(pres.to(device).view(n, t, 1))
+    ms = timed(lambda: ce.reconstruct_batch(codec, batch, present, False, stream))
+    touched = int((pres.sum(1) < t).sum().item())
+    algo = touched * d * L + int((t - pres.sum(1)).sum().item()) * L
+    gbs = algo / (ms / 1e3) / 1e9
+    tr, src = measured_traffic("c3", "rs_apply_kernel(reconstruct)", n == CONFIGS["c3"]["parts"],
+                               with_source=True)
+    out["c3_reconstruct"] = {
+        "config": "BASELINE configs[2]: RS(10,4) reconstruct (data + parity), 1-4 random erasures "
+                  f"per part, {n} parts x {size_label(L)}", "kernel": "rs_apply_var_kernel",
+        "ms": round(ms, 4), "algorithmic_bytes": algo, "achieved": round(gbs, 1),
+        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+        "traffic": tr, "traffic_source": src,
+        "rebuilt_verified": verified(batch, digests, t, n)}
+
+    # C4: RS(20,8) x 256 KiB, fused encode + SHA-256, then an 8-erasure round trip
+    c4 = CONFIGS["c4"]
+    d4, p4, L4, n4 = c4["d"], c4["p"], c4["chunk"], c4["parts"]
+    t4 = d4 + p4
+    codec4 = ce.ReedSolomon(d4, p4)
+    buf4 = torch.empty((n4, t4, L4), dtype=torch.uint8, device=device)
+    dig4 = torch.empty((n4, t4, 32), dtype=torch.uint8, device=device)
+    b4 = ce.PartBatch.from_tensor(buf4, L4)
+    ce.fill_synthetic(b4, t4, rank_seed(0xC4C4, rank), stream)
+    ms = timed(lambda: ce.encode_hash_batch(codec4, b4, dig4.data_ptr(), stream))
+    data_gbs = n4 * d4 * L4 / (ms / 1e3) / 1e9
+    hbm = n4 * t4 * (L4 + 32) / (ms / 1e3) / 1e9
+    g = torch.Generator().manual_seed(2828 + rank)
+    pres4 = torch.ones((n4, t4), dtype=torch.uint8)
+    for i in range(n4):
+        pres4[i, torch.randperm(t4, generator=g)[:p4]] = 0
+    buf4.mul_(pres4.to(device).view(n4, t4, 1))
+    ce.reconstruct_batch(codec4, b4, bytes(pres4.flatten().tolist()), False, stream)
+    tr, src = measured_traffic("c4", "encode_hash_kernel", True, with_source=True)
+    out["c4_encode_hash"] = {
+        "config": f"BASELINE configs[3] per GPU: RS(20,8), {n4} parts x {size_label(L4)}, fused "
+                  "encode + SHA-256 of all 28 chunks", "kernel": "encode_hash_kernel",
+        "ms": round(ms, 4), "value": round(data_gbs, 2), "unit": "GB/s of data",
+        "hbm_achieved": round(hbm, 1), "hbm_frac": round(hbm / HBM_PEAK_GBS, 4),
+        "traffic": tr, "traffic_source": src,
+        "round_trip_verified": verified(b4, dig4, t4, n4),
+        "round_trip": "8 random erasures of 28 per part, reconstruct (data + parity), every "
+                      "chunk re-hashed against the fused step's digests"}
+    del buf4, dig4
+    out["basis"] = ("HIP events on the launch stream, average of the timed launches after one "
+                    "warmup; algorithmic bytes per SURVEY.md §8d")
+    return out
+
+
 def _segments(args, cfg, shards):
     """Parts per scheduler job: every shard gets 2 batches per job; --jobs-in-flight jobs are
     queued at once (the next ones queued while the first runs: no drain bubble)."""
@@ -993,12 +1083,7 @@ def main():
     elif cfg["op"] == "reconstruct":
         ce.encode_batch(codec, batch, stream)
         # 1..4 random erasures per part (seeded); rebuilt in place every step
-        g = torch.Generator().manual_seed(1234 + rank)
-        pres = torch.ones((n_parts, t), dtype=torch.uint8)
-        k = torch.randint(1, p + 1, (n_parts,), generator=g)
-        for i in range(n_parts):
-            idx = torch.randperm(t, generator=g)[: int(k[i])]
-            pres[i, idx] = 0
+        pres = c3_erasures(n_parts, t, p, rank)
         present = bytes(pres.flatten().tolist())
         missing_bytes = int((t - pres.sum(1)).sum().item()) * L
     elif cfg["op"] == "read":
@@ -1206,6 +1291,11 @@ def main():
     if args.config == "c2" and not args.separate and not args.no_north_star:
         nstar = north_star_block(codec, batch, buf, digests, stream, device, rank, d, p, L,
                                  args.steps)
+    others = None
+    if (args.config == "c2" and not args.separate and not args.no_north_star
+            and n_parts == CONFIGS["c2"]["parts"]):
+        others = baseline_configs_block(codec, batch, buf, digests, stream, device, rank, d, p,
+                                        L, args.steps)
     del buf, digests  # the end-to-end forms below use their own buffers
     torch.cuda.empty_cache()
 
@@ -1268,6 +1358,8 @@ def main():
             line["valu_roofline"] = valu
         if nstar is not None:
             line["north_star"] = nstar
+        if others is not None:
+            line["baseline_configs"] = others
         if e2e is not None:
             e2e.pop("_local", None)
             line["end_to_end"] = e2e

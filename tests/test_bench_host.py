@@ -50,6 +50,15 @@ def test_two_erasures_exactly_two_per_part_and_bytes():
     assert bench.reconstruct_data_bytes(pres, d, L) == want
 
 
+def test_c3_erasures_one_to_p_per_part_and_seeded():
+    pres = bench.c3_erasures(200, 14, 4, 0)
+    miss = 14 - pres.sum(1)
+    assert ((miss >= 1) & (miss <= 4)).all()
+    assert set(miss.tolist()) == {1, 2, 3, 4}
+    assert bench.c3_erasures(200, 14, 4, 0).equal(pres)  # the c3 config's sets
+    assert not bench.c3_erasures(200, 14, 4, 1).equal(pres)  # per-rank seed
+
+
 def test_host_report_and_quota():
     info = bench.host_info()
     assert info["logical_cpus"] == os.cpu_count()
