@@ -371,8 +371,11 @@ def end_to_end(codec, d, p, L, gib, world, rank, reduce_dev, host_threads, devic
     P, depth = CONFIGS["c5"]["parts"], 4
     n_parts = max(depth * P, int(gib * (1 << 30)) // (d * L))
     n_batches = (n_parts + P - 1) // P
-    ring_parts = 2 * depth * P
-    # ~10 GiB page-locked slots + a 20 GiB pageable ring per rank: if any rank cannot get them,
+    # 2x the slots' part count at N = 1 (20 GiB); at N > 1 every rank of the node holds its own
+    # ring, slots and scheduler staging at once, so the ring shrinks to 2 batches (5 GiB, still
+    # 20x a socket's L3: every copy reads DRAM) to keep the node's host memory near 20 GiB per GPU
+    ring_parts = 2 * depth * P if world == 1 else 2 * P
+    # ~14 GiB page-locked slots + the pageable ring per rank: if any rank cannot get them,
     # every rank skips the figure together (no rank may be left waiting in a barrier) and the
     # headline still prints
     copier = HostCopier(host_threads)
