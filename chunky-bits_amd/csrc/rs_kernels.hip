@@ -15,11 +15,12 @@
 // Coefficient tables are wave-uniform and come in through scalar loads (s_load), so a row costs
 // 3 v_perm + ~1.5 xor per data dword, with no LDS traffic and no bank conflicts.
 //
-// Memory shape: a block owns a 16 KiB column range of one part; each lane moves V 16-byte
-// columns per input per step (V = 2: two 1 KiB-per-wave loads per input in flight) with
-// non-temporal loads and stores (every byte is touched once).  That is the best of the
-// streaming-ceiling sweep of this 10-read/4-write pattern with no GF work at all
-// (tools/ubench_stream.hip: 5.79 TB/s) and the best rs_apply variant (5.57 TB/s, C2 encode).
+// Memory shape: a block owns a 16 KiB (rs_apply_kernel) or 8 KiB (bit-sliced encoder, mixed-
+// pattern reconstruct) column range of one part; each lane moves V 16-byte columns per input per
+// step (V = 2: two 1 KiB-per-wave loads per input in flight) with non-temporal loads and stores
+// (every byte is touched once), blocks in an XCD-aware order, and on large grids a residency cap
+// of 2-3 blocks per CU (apply_lds).  RS(10,4) encode streams 6.40 TB/s and 2-erasure
+// reconstruct_data 5.96 TB/s.
 #include <cstdlib>
 #include <cstring>
 #include <type_traits>
