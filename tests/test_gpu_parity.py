@@ -456,6 +456,52 @@ def test_reconstruct_batch_too_few_present_launches_nothing():
 # Full BASELINE shapes: size-independent properties
 # ----------------------------------------------------------------------------------------------
 
+def test_large_grid_capped_paths_ragged_length():
+    """The paths that only large grids take (>= 65 536 blocks: residency caps, rs_kernels.hip
+    apply_lds) at a ragged length (full 8 KiB bit-sliced steps + the v_perm byte tail): the
+    bit-sliced encode must reproduce the fused kernel's parity byte for byte, the 2-row
+    (data-only, 2 erasures) and 4-row (1-4 erasures, data + parity) reconstruct classes with
+    the compile-time-d loop must rebuild chunks that hash to the fused step's digests, and a
+    sampled part must match the oracle."""
+    d, p, n_parts = 10, 4, 640
+    L = (1 << 20) - 4096 + 48  # 128 tiles of 8 KiB, the last one ragged: 81 920 blocks
+    t = d + p
+    buf = torch.empty((n_parts, t, L), dtype=torch.uint8, device=DEV)
+    batch = ce.PartBatch.from_tensor(buf, L)
+    ce.fill_synthetic(batch, t, 5151)
+    rs = ce.ReedSolomon(d, p)
+    dig = torch.empty((n_parts, t, 32), dtype=torch.uint8, device=DEV)
+    ce.encode_hash_batch(rs, batch, dig.data_ptr())
+    torch.cuda.synchronize()
+    ref = buf.clone()
+    buf[:, d:] = 0
+    ce.encode_batch(rs, batch)  # the bit-sliced kernel under the cap
+    torch.cuda.synchronize()
+    assert torch.equal(buf, ref)
+    k = n_parts // 3
+    host = ref[k].cpu().numpy()
+    st, par = oracle.encode_sep(d, p, [host[j] for j in range(d)])
+    assert st == 0 and all(np.array_equal(host[d + i], par[i]) for i in range(p))
+    rng = np.random.default_rng(51)
+    for data_only, lo, hi in ((True, 2, 2), (False, 1, p)):
+        present = np.ones((n_parts, t), dtype=np.uint8)
+        for j in range(n_parts):
+            present[j, rng.choice(t, int(rng.integers(lo, hi + 1)), replace=False)] = 0
+        buf[~torch.from_numpy(present).to(DEV).bool()] = 0
+        ce.reconstruct_batch(rs, batch, present.tobytes(), data_only)
+        torch.cuda.synchronize()
+        if data_only:
+            assert torch.equal(buf[:, :d], ref[:, :d])
+            buf.copy_(ref)
+        else:
+            dig2 = torch.empty_like(dig)
+            ce.sha256_batch(batch, 0, t, dig2.data_ptr())
+            torch.cuda.synchronize()
+            assert torch.equal(dig, dig2) and torch.equal(buf, ref)
+    del buf, ref
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.slow
 @pytest.mark.parametrize("d,p,L,n_parts", [(10, 4, 1 << 20, 4096), (20, 8, 256 << 10, 2048),
                                            (20, 8, 256 << 10, 4096)])  # C4 bench shape: the
