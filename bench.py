@@ -1313,13 +1313,18 @@ def main():
     ranks = None
     if world > 1:
         e2e_v, link_v = (e2e or {}).get("_local") or (0.0, 0.0)
+        # each rank's own north_star fractions (the block runs on every rank, on its own GPU)
+        ns_enc = (nstar or {}).get("encode", {}).get("frac") or 0.0
+        ns_rec = (nstar or {}).get("reconstruct_data_2_erasures", {}).get("frac") or 0.0
         rows = gather_rows([ordinal, numa_node, 1.0 if numa_bound else 0.0, rank_cpus,
-                            local_s * 1e3, e2e_v, link_v], world, reduce_dev)
+                            local_s * 1e3, e2e_v, link_v, ns_enc, ns_rec], world, reduce_dev)
         ranks = [{"rank": r, "device": int(row[0]), "numa_node": int(row[1]),
                   "host_threads_numa_bound": bool(row[2]), "cpus": int(row[3]),
                   "step_ms": round(row[4], 3),
                   "end_to_end_GBs": round(row[5], 2) if row[5] else None,
-                  "pcie_link_GBs": round(row[6], 2) if row[6] else None}
+                  "pcie_link_GBs": round(row[6], 2) if row[6] else None,
+                  "north_star_encode_frac": round(row[7], 4) if row[7] else None,
+                  "north_star_reconstruct_data_frac": round(row[8], 4) if row[8] else None}
                  for r, row in enumerate(rows)]
 
     if rank == 0:
