@@ -317,6 +317,15 @@ int main(int argc, char** argv) {
         }
         return 0;
     }
+    if (argc > 2 && argv[2][0] == 'v') {  // bytes per lane x residency cap
+        for (int rep = 0; rep < 2; ++rep)
+            for (int cap : {1, 2, 3, 4}) {
+                run_mix<1, true, true, true>(base, parts, cap);
+                run_mix<2, true, true, true>(base, parts, cap);
+                run_mix<4, true, true, true>(base, parts, cap);
+            }
+        return 0;
+    }
     if (argc > 2 && argv[2][0] == 'c') {  // residency caps (blocks per CU) on the best mix shape
         for (int rep = 0; rep < 2; ++rep) {
             for (int cap : {0, 1, 2, 3, 4, 6}) run_mix<2, true, true, true>(base, parts, cap);
