@@ -378,6 +378,7 @@ def test_sha256_batch_subrange(variant, monkeypatch):
 @pytest.mark.parametrize("data_only", [False, True])
 @pytest.mark.parametrize("d,p,L", [(10, 4, 16384), (3, 2, 683), (20, 8, 4096 + 5),
                                    (10, 4, 12368),   # partial last 8 KiB step (2-column path)
+                                   (10, 6, 3 * 8192 + 16),  # compile-time d=10, 8-row class
                                    (6, 10, 1024)])   # up to 10 rows: shared + row-group launches
 def test_reconstruct_batch_random_patterns(d, p, L, data_only):
     n_parts, t = 96, d + p
