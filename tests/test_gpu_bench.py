@@ -1,0 +1,54 @@
+"""bench.py's JSON contract on the GPU, at a small size (a subprocess, as the driver runs it):
+one line with the BASELINE metric, the roofline / VALU-roofline / north_star blocks and the CPU
+baseline, every GPU-side check in it true.  The full-size line is the driver's own run."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("no GPU", allow_module_level=True)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(*args):
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], cwd=ROOT,
+                         capture_output=True, text=True, timeout=150)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [x for x in out.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_default_line_contract_small():
+    base = json.load(open(os.path.join(ROOT, "BASELINE.json")))
+    line = _run("--parts", "256", "--steps", "2", "--warmup", "1", "--e2e-gib", "0")
+    assert line["metric"] == base["metric"]
+    assert line["unit"] == "GB/s" and line["n_gpus"] == 1 and line["steps"] == 2
+    assert line["higher_is_better"] is True and line["scaling"] == "weak"
+    assert line["dtype"] == "u8" and line["value"] > 0 and line["ms_per_step"] > 0
+    assert line["config"]["parts_per_gpu"] == 256 and line["config"]["d"] == 10
+    rf = line["roofline"]
+    assert rf["bound"] == "hbm" and rf["kernel"] == "encode_hash_kernel" and 0 < rf["frac"] < 1
+    assert line["valu_roofline"]["bound"] == "valu"
+    ns = line["north_star"]
+    assert ns["rebuilt_data_verified"] is True
+    assert ns["encode"]["kernel"] == "rs_encode_bs_kernel" and ns["encode"]["frac"] > 0
+    assert ns["reconstruct_data_2_erasures"]["frac"] > 0
+    cb = line["cpu_baseline"]
+    assert cb["value"] > 0 and cb["kind"] == "port" and cb["cores"] >= 1
+    assert "baseline_configs" not in line  # full-size only (the driver's run)
+
+
+def test_reconstruct_config_line_small():
+    line = _run("--config", "c3e2", "--parts", "128", "--steps", "2", "--warmup", "1",
+                "--check", "--no-cpu-baseline")
+    assert line["check_vs_oracle"] is True
+    assert line["roofline"]["kernel"] == "rs_apply_kernel(reconstruct_data)"
+    assert line["kernels"]["also_reconstruct"]["ms"] > 0
