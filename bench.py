@@ -91,6 +91,9 @@ CONFIGS = {
     # encode only (HBM roofline of the GF kernel alone).
     "c2enc": dict(d=10, p=4, chunk=1 * MiB, parts=4096, op="encode",
                   workload="RS(10,4) encode_sep only, {parts} parts x {chunk} chunks per GPU"),
+    # the reference's example clusters' shape (RS(3,2), examples/*.yaml) as a device batch.
+    "c1enc": dict(d=3, p=2, chunk=1 * MiB, parts=8192, op="encode",
+                  workload="RS(3,2) encode_sep only, {parts} parts x {chunk} chunks per GPU"),
     # the C4 shape's encode alone (RS(20,8), 256 KiB chunks).
     "c4enc": dict(d=20, p=8, chunk=256 * 1024, parts=4096, op="encode",
                   workload="RS(20,8) encode_sep only, {parts} parts x {chunk} chunks per GPU"),

@@ -735,8 +735,10 @@ hipError_t launch_bs(const ApplyParams& a, hipStream_t s) {
     return for_part_ranges(a, max_blocks / tiles, [&](const ApplyParams& b) {
         auto* kern = &rs_encode_bs_kernel<D, P>;
         const uint64_t n_blocks = b.n_parts * tiles;
-        // measured for RS(10,4) (2 blocks per CU); the other shapes keep their occupancy
-        const uint32_t lds = apply_lds(b.lds_reserve, D == 10 && P == 4 ? 2 : 0, n_blocks);
+        // measured per shape: RS(10,4) 2 blocks per CU, RS(3,2) 3 (6.71 vs 6.92-7.23 ms for 8 192
+        // parts x 1 MiB, profiles/r3_c1enc_ab/), RS(20,8) its register-bound 3
+        const int cap = D == 10 && P == 4 ? 2 : D == 3 && P == 2 ? 3 : 0;
+        const uint32_t lds = apply_lds(b.lds_reserve, cap, n_blocks);
         if (!allow_lds(kern, lds)) return hipErrorInvalidValue;
         clear_stale_error();
         hipLaunchKernelGGL(kern, dim3(uint32_t(n_blocks)), dim3(kApplyThreads), lds, s, b,
