@@ -1010,6 +1010,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--parts", type=int, default=None, help="override parts per GPU")
+    ap.add_argument("--shape", default=None, help="d,p override for the encode-only configs")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e-gib", type=float, default=64.0,
                     help="c2: GiB per GPU of the PCIe-bound end-to-end figure (0 = skip)")
@@ -1033,6 +1034,13 @@ def main():
     cfg = dict(CONFIGS[args.config])
     if args.parts:
         cfg["parts"] = args.parts
+    if args.shape:  # A/B of other (d, p) on the encode configs
+        if cfg["op"] != "encode":
+            ap.error("--shape applies to the encode-only configs")
+        cfg["d"], cfg["p"] = (int(x) for x in args.shape.split(","))
+        cfg["workload"] = cfg["workload"].replace(
+            "RS(10,4)", f"RS({cfg['d']},{cfg['p']})").replace(
+            "RS(3,2)", f"RS({cfg['d']},{cfg['p']})").replace("RS(20,8)", f"RS({cfg['d']},{cfg['p']})")
     world, rank, local = dist_env()
     if world != args.gpus and rank == 0:
         print(f"note: WORLD_SIZE={world} but --gpus={args.gpus}", file=sys.stderr)
@@ -1238,7 +1246,7 @@ def main():
     achieved = dom["algorithmic_bytes"] / (dom["ms"] / 1e3) / 1e9
     traffic, traffic_src = measured_traffic(
         args.config + ("sep" if cfg["op"] == "encode_hash" and not fused else ""),
-        dom_name, n_parts == CONFIGS[args.config]["parts"], with_source=True)
+        dom_name, n_parts == CONFIGS[args.config]["parts"] and not args.shape, with_source=True)
 
     valu = None
     if cfg["op"] in ("encode_hash", "read"):
