@@ -695,7 +695,10 @@ hipError_t launch_rg(const ApplyParams& a, uint32_t row_base, uint32_t groups, b
         return dispatch_apply(vec16, [&](auto k) {
             using T = Tune<decltype(k)::value>;
             auto* kern = &rs_apply_kernel<RG, T::kVec, T::kGroup, T::kV, T::kNt>;
-            const uint32_t lds = apply_lds(b.lds_reserve, 0, uint64_t(grid.x) * groups);
+            // 1-3 rows: 3 blocks per CU (RS(2,1) / RS(4,2) / RS(8,2) / RS(6,3) encode 1-2 %
+            // faster than by registers, profiles/r3_vperm_shapes_ab/); 4+ rows: no gain
+            const uint32_t lds =
+                apply_lds(b.lds_reserve, RG <= 3 ? 3 : 0, uint64_t(grid.x) * groups);
             if (!allow_lds(kern, lds)) return hipErrorInvalidValue;
             clear_stale_error();
             hipLaunchKernelGGL(kern, grid, dim3(kApplyThreads), lds, s, b,
