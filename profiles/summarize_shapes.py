@@ -5,6 +5,11 @@ one row per (kernel, grid size), and merge the full-size launch of each kernel (
 into profiles/traffic.json under --config (read by bench.py).
 
     python profiles/summarize_shapes.py <tag> [--config c2] [--fetch-mult 2]
+                                        [--grid encode_hash_kernel=131072,...]
+
+--grid names the launch shape to merge for a kernel when its largest grid is not the config's
+(the default line also runs BASELINE's C3 / C4 configurations: C4's fused kernel and C3's
+reconstruct have larger grids than the C2 launches the c2 entries describe).
 
 Durations come from the kernel trace (run_kernel_trace.csv, every dispatch); counters from the
 separate --pmc passes, matched to the same (kernel, grid).  HBM traffic per launch, as
@@ -60,6 +65,11 @@ def main():
     config = sys.argv[sys.argv.index("--config") + 1] if "--config" in sys.argv else "c2"
     fmult = float(sys.argv[sys.argv.index("--fetch-mult") + 1]) if "--fetch-mult" in sys.argv \
         else 2.0
+    pick = {}
+    if "--grid" in sys.argv:
+        for kv in sys.argv[sys.argv.index("--grid") + 1].split(","):
+            k, g = kv.split("=")
+            pick[k] = int(g)
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
     tr = trace_groups(os.path.join(src, "trace", "run_kernel_trace.csv"))
     sq, sq_dur = pmc_groups(os.path.join(src, "pmc_sq", "run_counter_collection.csv"))
@@ -70,7 +80,8 @@ def main():
     lines = [f"# rocprofv3 summary `{tag}` ({config})", "",
              f"Command: `{cmd}` on one MI355X (gfx950), profiled by `profiles/collect.sh`; raw "
              f"CSVs under `profiles/{tag}/`.  One row per kernel and grid size: the same kernel "
-             "runs at the full C2 shape and at the end-to-end forms' 256-part batches.", "",
+             "runs at the full C2 shape, at the end-to-end forms' 256-part batches and (the default "
+             "line) at BASELINE's C3 / C4 shapes.", "",
              "## Kernel trace (`--kernel-trace --stats`), per dispatch shape", "",
              "| kernel | grid (work-items) | calls | avg ms | min ms | max ms |",
              "|---|---|---|---|---|---|"]
@@ -101,7 +112,8 @@ def main():
         tb = (fmult * f + w) * 1024 if f == f and w == w else None
         lines.append(f"| {k} | {grid} | {ghz:.2f} | {waves:.0f} | {vpw:.0f} | {f:.0f} | {w:.0f} | "
                      f"{tb / 1e9 if tb else float('nan'):.2f} |")
-        if tb and k in TRAFFIC_KERNELS and grid > biggest.get(k, (0, None))[0]:
+        chosen = grid == pick[k] if k in pick else grid > biggest.get(k, (0, None))[0]
+        if tb and k in TRAFFIC_KERNELS and chosen:
             biggest[k] = (grid, {"bytes_per_launch": int(tb), "fetch_kib": f, "write_kib": w,
                                  "grid": grid, "calibrated": True, "fetch_mult": fmult,
                                  "source": f"profiles/{tag}_summary.md"})
