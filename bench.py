@@ -31,8 +31,9 @@ import torch  # noqa: E402  (import before chunky_ec: one HIP runtime)
 import torch.distributed as dist  # noqa: E402
 
 import chunky_ec as ce  # noqa: E402
+from chunky_ec.readstream import ReadRepairStream  # noqa: E402
 from chunky_ec.sharding import (all_ranks_ok, barrier, dist_env, gather_rows,  # noqa: E402
-                                max_over_ranks, rank_seed)
+                                max_over_ranks, part_range, rank_seed)
 
 METRIC = "RS(10,4) encode+sha256 GB/s per node at 1/2/4/8 GPUs; % of HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md); 5.79 TB/s measured
@@ -69,18 +70,23 @@ CONFIGS = {
     "c4": dict(d=20, p=8, chunk=256 * 1024, parts=4096, op="encode_hash",
                workload="C4: RS(20,8) encode_sep + SHA-256 of all 28 chunks per part, "
                         "{parts} parts x {chunk} chunks per GPU"),
-    # configs[4]: host-staged stream through pinned double-buffered slots (PCIe-bound);
+    # configs[4]: a host-produced stream through pinned double-buffered slots (PCIe-bound);
     # --stream-gib sets the stream size (default 1 TiB split across the ranks: strong scaling).
     "c5": dict(d=10, p=4, chunk=1 * MiB, parts=256, op="stream",
                workload="C5: {stream} synthetic object stream, RS(10,4) encode + SHA-256, {chunk} "
-                        "chunks, pinned-host staged batches of {parts} parts, 4 slots in flight"),
-    # configs[4], read side: the same stream read back through verify + repair (FileReadBuilder /
-    # read_with_context batched): d random chunks loaded per part, verified, data rebuilt.
+                        "chunks, every part copied from a pageable source ring into pinned-host "
+                        "staged batches of {parts} parts inside the timed region, 4 slots in "
+                        "flight"),
+    # configs[4], verify/repair side: the same stream read back through FileReadBuilder /
+    # read_with_context batched with its retry rule: d random chunks fetched per part from a
+    # pageable ring of stored chunks, a seeded fraction of them damaged, SHA-256 verify, data
+    # rebuilt, parts with a rejected chunk retried with another one (file_part.rs:92-107).
     "c5r": dict(d=10, p=4, chunk=1 * MiB, parts=256, op="read_stream",
-                workload="C5 read side: {stream} synthetic object stream read back, RS(10,4), d "
-                         "random chunks loaded per part, SHA-256 verify + reconstruct_data, "
-                         "pinned-host staged batches of {parts} parts, 4 slots in flight, rebuilt "
-                         "data chunks back (loaded ones stay in the pinned buffer)"),
+                workload="C5 verify/repair: {stream} synthetic object stream read back, RS(10,4), "
+                         "d random chunks per part fetched from a pageable ring of stored chunks "
+                         "into pinned-host staged batches of {parts} parts inside the timed "
+                         "region, damaged chunks rejected by SHA-256 verify and retried, "
+                         "reconstruct_data, 4 slots in flight"),
     # configs[2], device-resident read: FilePart::read_with_context batched -- d random chunks
     # loaded per part (file_part.rs:86-122), SHA-256 verify + reconstruct_data of the missing data
     # chunks (the decode runs speculatively beside the verification).
@@ -236,6 +242,199 @@ def cpu_baseline(cfg, threads: int, cores_total: int, cores_avail: int, quota):
     }
 
 
+class HostCopier:
+    """`threads` host threads working on part ranges (numpy releases the GIL for the copies):
+    the caller's reader filling its part buffers (writer.rs:170-197 reads each part's
+    d*chunk_size bytes into `data_buf`; read_with_context loads a part's chunks,
+    file_part.rs:86-107)."""
+
+    def __init__(self, threads: int):
+        from concurrent.futures import ThreadPoolExecutor
+        self.threads = threads
+        self.pool = ThreadPoolExecutor(threads)
+
+    def map(self, fn, n: int) -> None:
+        """fn(a, b) over [0, n) split into `threads` contiguous ranges, run in parallel."""
+        T = self.threads
+        futs = [self.pool.submit(fn, n * i // T, n * (i + 1) // T) for i in range(T)
+                if n * i // T < n * (i + 1) // T]
+        for f in futs:
+            f.result()
+
+    def copy(self, dst, src) -> None:
+        """dst[k] = src[k] for the leading (part) axis, split over the threads."""
+        def job(a, b):
+            dst[a:b] = src[a:b]
+        self.map(job, len(src))
+
+    def close(self) -> None:
+        self.pool.shutdown()
+
+
+def source_ring(n_parts, d, L, seed, copier):
+    """A pageable [n_parts][d][L] source of distinct parts (the file the reader reads): a
+    random 64 MiB block tiled with `copier`'s threads (first touch in parallel), then each
+    part's first 8 bytes set to its ring index.  Not timed."""
+    import numpy as np
+    ring = np.empty((n_parts, d, L), np.uint8)
+    blk = np.random.default_rng(seed).integers(0, 256, size=(max(1, (64 << 20) // (d * L)), d, L),
+                                                dtype=np.uint8)
+    for k in range(0, n_parts, len(blk)):
+        m = min(len(blk), n_parts - k)
+        copier.copy(ring[k:k + m], blk[:m])
+    ring[:, 0, :8] = np.arange(n_parts, dtype=np.uint64).view(np.uint8).reshape(n_parts, 8)
+    return ring
+
+
+def part_stamps(first: int, n: int):
+    """[n][8] bytes: the global part numbers [first, first + n) as little-endian u64."""
+    import numpy as np
+    return np.arange(first, first + n, dtype=np.uint64).view(np.uint8).reshape(n, 8)
+
+
+def ring_reader(ring, copier):
+    """fill(data, part, n): the reader producing parts [part, part + n) into a pinned slot --
+    each part's bytes copied by `copier`'s threads from the pageable ring (part k is ring part
+    k mod len(ring)), its first 8 bytes then set to its global part number, so every part of
+    the stream differs."""
+    R = len(ring)
+
+    def fill(data, part, n):
+        r = part % R
+        m = min(n, R - r)
+        copier.copy(data[:m], ring[r:r + m])
+        if m < n:
+            copier.copy(data[m:n], ring[:n - m])
+        data[:n, 0, :8] = part_stamps(part, n)
+    return fill
+
+
+def ring_part_digests(ring, part: int):
+    """SHA-256 of the d data chunks of stream part `part` as ring_reader produced it."""
+    import hashlib
+    src = ring[part % len(ring)].copy()
+    src[0, :8] = part_stamps(part, 1)[0]
+    return [hashlib.sha256(c.tobytes()).digest() for c in src]
+
+
+def timed_write(pl, fill, first: int, n_parts: int, world: int):
+    """FileWriteBuilder::write's part loop through `pl` (cec_pipeline): parts [first, first +
+    n_parts) produced by fill() into each acquired slot, then H2D, encode + SHA-256, D2H.  One
+    untimed warmup batch per slot, barrier, the timed stream, drain, barrier.  Returns (local
+    seconds, the slot of the last batch, its part count)."""
+    P, depth = pl.parts, pl.depth
+    for _ in range(depth):
+        slot, data = pl.acquire()
+        fill(data, first, P)
+        pl.submit(slot, P)
+    pl.drain()
+    barrier(world)
+    t0 = time.perf_counter()
+    part, end, last = first, first + n_parts, (0, 0)
+    while part < end:
+        slot, data = pl.acquire()
+        n = min(P, end - part)
+        fill(data, part, n)
+        pl.submit(slot, n)
+        part += n
+        last = (slot, n)
+    pl.drain()
+    barrier(world)
+    return (time.perf_counter() - t0,) + last
+
+
+def write_check(pl, ring, slot: int, n: int, last_part: int):
+    """The size-independent check of a ring-fed write stream: the digests of every data chunk of
+    the first and last part of the last batch equal SHA-256 of the bytes the reader produced."""
+    _, dg = pl.wait(slot)
+    ok = True
+    for k in (0, n - 1):
+        want = ring_part_digests(ring, last_part - (n - 1) + k)
+        ok = ok and all(dg[k, j].tobytes() == want[j] for j in range(len(want)))
+    return bool(ok)
+
+
+def encoded_ring(codec, d, p, L, n_parts, seed, device, P=256):
+    """The stored chunks the read streams fetch from: a pageable [n_parts][d+p][L] ring of
+    encoded parts and their metadata digests [n_parts][d+p][32], made on the GPU P parts at a
+    time (synthetic data, fused encode + SHA-256) and copied down.  Not timed."""
+    import numpy as np
+    t = d + p
+    ring = np.empty((n_parts, t, L), np.uint8)
+    dig = np.empty((n_parts, t, 32), np.uint8)
+    blk = torch.empty((P, t, L), dtype=torch.uint8, device=device)
+    dg = torch.empty((P, t, 32), dtype=torch.uint8, device=device)
+    batch = ce.PartBatch.from_tensor(blk, L)
+    for b0 in range(0, n_parts, P):
+        m = min(P, n_parts - b0)
+        ce.fill_synthetic(batch, d, seed + b0)
+        ce.encode_hash_batch(codec, batch, dg.data_ptr())
+        torch.cuda.synchronize(device)
+        torch.from_numpy(ring[b0:b0 + m]).copy_(blk[:m])
+        torch.from_numpy(dig[b0:b0 + m]).copy_(dg[:m])
+    del blk, dg
+    return ring, dig
+
+
+def timed_read_repair(codec, ring, ring_dig, L, P, depth, first, n_parts, world, corrupt,
+                      copier, seed, n_samples=3):
+    """FileReadBuilder over parts [first, first + n_parts) with read_with_context's retries
+    (chunky_ec.readstream over cec_read_pipeline, REBUILT_ONLY): each part loads d random
+    chunks of its d+p, copied by `copier`'s threads from the pageable ring of stored chunks
+    (stream part k is ring part k mod len(ring)) into the pinned slot; a seeded `corrupt`
+    fraction of the fresh loads comes back with a flipped byte (the location served bad bytes);
+    the GPU verifies every fresh chunk against the metadata digest, decodes the missing data
+    chunks, and a part whose load failed verification is retried with one more chunk
+    (file_part.rs:92-107).  One untimed warmup pass of `depth` batches, then the timed stream.
+    Returns (local seconds, stats dict, sampled output checks)."""
+    import numpy as np
+    d = codec.data_shard_count()
+    R = len(ring)
+    rp = ce.ReadPipeline(codec, L, P, depth, ce.ReadPipeline.REBUILT_ONLY)
+    crng = np.random.default_rng(seed)
+    damaged = [0]
+
+    def fetch(chunks, rows):
+        def job(a, b):
+            for k, part, flags in rows[a:b]:
+                r = part % R
+                for j in np.flatnonzero(flags):
+                    chunks[k, j] = ring[r, j]
+        copier.map(job, len(rows))
+        if corrupt > 0:  # fresh reads only: a re-sent verified chunk is the bytes that verified
+            for k, _, flags in rows:
+                fresh = np.flatnonzero(flags == 1)
+                for j in fresh[crng.random(len(fresh)) < corrupt]:
+                    chunks[k, j, int(crng.integers(L))] ^= 0xA5
+                    damaged[0] += 1
+
+    checks = []
+    sample_at = {first, first + n_parts // 2, first + n_parts - 1}
+    retried_checked = [0]
+
+    def on_part(slot, nb, k, part, attempts):
+        # the part's d data chunks (loaded ones where they were read, rebuilt ones from the
+        # D2H) must equal the stored data chunks: sampled parts plus the first retried ones
+        if part in sample_at or (attempts > 1 and retried_checked[0] < n_samples):
+            retried_checked[0] += attempts > 1
+            checks.append({"part": int(part), "attempts": int(attempts),
+                           "ok": rp.part_bytes(slot, nb, k) == ring[part % R, :d].tobytes()})
+
+    warm = ReadRepairStream(rp, fetch, lambda ids: ring_dig[ids % R], seed=seed + 1)
+    warm.run(first, min(n_parts, depth * P))
+    damaged[0] = 0
+    barrier(world)
+    t0 = time.perf_counter()
+    st = ReadRepairStream(rp, fetch, lambda ids: ring_dig[ids % R], seed=seed + 2,
+                          on_part=on_part).run(first, n_parts)
+    barrier(world)
+    el = time.perf_counter() - t0
+    del rp
+    stats = st.as_dict()
+    stats["damaged_loads"] = damaged[0]
+    return el, stats, checks
+
+
 def _stream_line(args, cfg, world, n_batches, warm, el, total, extra_config, data_text, **extra):
     d, p, L, P = cfg["d"], cfg["p"], cfg["chunk"], cfg["parts"]
     line = {
@@ -260,104 +459,91 @@ def _stream_line(args, cfg, world, n_batches, warm, el, total, extra_config, dat
     return line
 
 
-def run_stream(args, cfg, codec, world, rank, device, reduce_dev):
-    """C5: host data -> pinned slot -> H2D -> fused encode+hash -> D2H parity + digests.
+def _rank_threads(world):
+    """Host threads for a rank's reader: half the CPUs its main thread may use, 8 at most."""
+    return int(os.environ.get("CEC_E2E_THREADS", "0")) or max(
+        1, min(8, len(os.sched_getaffinity(0)) // 2))
 
-    The stream's bytes come from the slots' pinned buffers, filled once with synthetic data; each
-    submitted part gets its global part number stamped into its first 8 bytes (parts differ; the
-    GPU work is data-independent).  Time = first submit to last result, max over ranks."""
-    import numpy as np
+
+def run_stream(args, cfg, codec, world, rank, device, reduce_dev):
+    """C5 (BASELINE configs[4], write side): a `--stream-gib` object stream, split into
+    contiguous part ranges over the ranks (strong scaling), each rank's parts produced inside
+    the timed region by host threads copying from a pageable source ring into the pinned slots
+    (ring_reader), then H2D -> fused encode + SHA-256 -> D2H of parity + digests (cec_pipeline,
+    `depth` slots).  Time = first submit to last result, max over ranks."""
     d, p, L, P = cfg["d"], cfg["p"], cfg["chunk"], cfg["parts"]
     depth = int(os.environ.get("CEC_STREAM_DEPTH", "4"))  # slots in flight (A/B knob)
-    part_bytes = d * L
-    total_parts = int(args.stream_gib * (1 << 30)) // part_bytes
-    lo = total_parts * rank // world
-    hi = total_parts * (rank + 1) // world
-    mine = hi - lo
+    total_parts = int(args.stream_gib * (1 << 30)) // (d * L)
+    lo, hi = part_range(total_parts, rank, world)
     if args.devices:
         return run_stream_multi(args, cfg, codec, total_parts)
+    threads = _rank_threads(world)
+    copier = HostCopier(threads)
+    ring_parts = 2 * depth * P if world == 1 else 2 * P
+    ring = source_ring(ring_parts, d, L, 0xC5 + rank, copier)
     pl = ce.Pipeline(codec, L, P, depth)
-    rng = np.random.default_rng(rank)
-    block = rng.integers(0, 256, size=(P, d, L), dtype=np.uint8)
-    slots = []
-    for _ in range(depth):
-        slot, data = pl.acquire()
-        data[:] = block
-        slots.append(slot)
-    n_batches = (mine + P - 1) // P
-    # warmup: one batch per slot
-    for i in range(min(depth, n_batches)):
-        slot, data = pl.acquire()
-        pl.submit(slot, P)
-    pl.drain()
-    barrier(world)
-    t0 = time.perf_counter()
-    part = lo
-    for i in range(n_batches):
-        slot, data = pl.acquire()
-        n = min(P, hi - part)
-        data[:n, 0, :8] = np.arange(part, part + n, dtype=np.uint64).view(np.uint8).reshape(n, 8)
-        pl.submit(slot, n)
-        part += n
-    pl.drain()
-    barrier(world)
-    t1 = time.perf_counter()
-    el = max_over_ranks(t1 - t0, world, reduce_dev)
+    loc, slot, n = timed_write(pl, ring_reader(ring, copier), lo, hi - lo, world)
+    ok = write_check(pl, ring, slot, n, hi - 1) if hi > lo else True
+    ok = all_ranks_ok(ok, world, reduce_dev)
+    el = max_over_ranks(loc, world, reduce_dev)
+    del pl
+    copier.close()
     if rank == 0:
-        total = total_parts * part_bytes
+        total = total_parts * d * L
         print(json.dumps(_stream_line(
-            args, cfg, world, n_batches, min(depth, n_batches), el, total,
-            {"slots": depth, "parallelism": f"part-range-sharded x{world}, no collective"},
-            "synthetic host stream (pinned slots filled once, part numbers stamped)")), flush=True)
+            args, cfg, world, (hi - lo + P - 1) // P, depth, el, total,
+            {"slots": depth, "host_threads": threads,
+             "parallelism": f"part-range-sharded x{world}, no collective"},
+            f"synthetic host stream: every part copied inside the timed region by {threads} host "
+            f"threads from a pageable source ring ({ring_parts} distinct parts, "
+            f"{size_label(ring.nbytes)}) into the pinned slot, global part number stamped",
+            check_digests_vs_source=ok)), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-class HostCopier:
-    """`threads` host threads copying part-sized slices (numpy releases the GIL for the copy):
-    the caller's reader filling its part buffers (writer.rs:170-197 reads each part's
-    d*chunk_size bytes into `data_buf`)."""
-
-    def __init__(self, threads: int):
-        from concurrent.futures import ThreadPoolExecutor
-        self.threads = threads
-        self.pool = ThreadPoolExecutor(threads)
-
-    def copy(self, dst, src) -> None:
-        """dst[k] = src[k] for the leading (part) axis, split over the threads."""
-        n, T = len(src), self.threads
-
-        def job(i):
-            a, b = n * i // T, n * (i + 1) // T
-            if a < b:
-                dst[a:b] = src[a:b]
-        for f in [self.pool.submit(job, i) for i in range(T)]:
-            f.result()
-
-    def close(self) -> None:
-        self.pool.shutdown()
-
-
-def source_ring(n_parts, d, L, seed, copier):
-    """A pageable [n_parts][d][L] source of distinct parts (the file the reader reads): a
-    random 64 MiB block tiled with `copier`'s threads (first touch in parallel), then each
-    part's first 8 bytes set to its ring index.  Not timed."""
-    import numpy as np
-    ring = np.empty((n_parts, d, L), np.uint8)
-    blk = np.random.default_rng(seed).integers(0, 256, size=(max(1, (64 << 20) // (d * L)), d, L),
-                                                dtype=np.uint8)
-    for k in range(0, n_parts, len(blk)):
-        m = min(len(blk), n_parts - k)
-        copier.copy(ring[k:k + m], blk[:m])
-    ring[:, 0, :8] = np.arange(n_parts, dtype=np.uint64).view(np.uint8).reshape(n_parts, 8)
-    return ring
+def run_read_stream(args, cfg, codec, world, rank, device, reduce_dev):
+    """C5 (BASELINE configs[4], verify/repair side): the stream read back through
+    FileReadBuilder / read_with_context batched with retries (timed_read_repair): d random
+    chunks per part fetched inside the timed region from a pageable ring of stored chunks, a
+    seeded --corrupt fraction of the fetched chunks damaged, every fetched chunk SHA-256-verified
+    on the GPU, missing data rebuilt, failed parts retried with another chunk.  Contiguous part
+    ranges over the ranks (strong scaling); value = part data bytes delivered / s, max over
+    ranks."""
+    d, p, L, P = cfg["d"], cfg["p"], cfg["chunk"], cfg["parts"]
+    depth = int(os.environ.get("CEC_STREAM_DEPTH", "4"))  # slots in flight (A/B knob)
+    total_parts = int(args.stream_gib * (1 << 30)) // (d * L)
+    lo, hi = part_range(total_parts, rank, world)
+    threads = _rank_threads(world)
+    copier = HostCopier(threads)
+    ring, ring_dig = encoded_ring(codec, d, p, L, 2 * P, rank_seed(0xC5C5, rank), device, P)
+    loc, stats, checks = timed_read_repair(codec, ring, ring_dig, L, P, depth, lo, hi - lo,
+                                           world, args.corrupt, copier, 0x5EED + rank)
+    ok = all(c["ok"] for c in checks) and stats["undecodable_parts"] == 0
+    ok = all_ranks_ok(ok, world, reduce_dev)
+    el = max_over_ranks(loc, world, reduce_dev)
+    copier.close()
+    if rank == 0:
+        total = total_parts * d * L
+        print(json.dumps(_stream_line(
+            args, cfg, world, stats["batches"], depth, el, total,
+            {"slots": depth, "host_threads": threads, "corrupt_frac": args.corrupt,
+             "parallelism": f"part-range-sharded x{world}, no collective"},
+            f"synthetic stored chunks: a pageable ring of {len(ring)} GPU-encoded parts "
+            f"({size_label(ring.nbytes)}); d random chunks per part copied inside the timed "
+            f"region by {threads} host threads into the pinned slot, {args.corrupt:g} of the "
+            "fetched chunks damaged (seeded), failed parts retried",
+            read_repair=stats, check_vs_stored=ok, checks=checks)), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
-def end_to_end(codec, d, p, L, gib, world, rank, reduce_dev, host_threads, device_ordinal):
-    """North-star's PCIe-bound end-to-end figure beside the device-resident headline: the same
+def end_to_end(codec, d, p, L, gib, world, rank, reduce_dev, host_threads, device_ordinal,
+               device, corrupt):
+    """North-star's PCIe-bound end-to-end figures beside the device-resident headline: the same
     RS(10,4) encode + SHA-256 with the parts produced in host memory, parity + digests landing
     back in it, `gib` GiB per rank (weak scaling like the headline), max over ranks.  Not
-    `value` (that is HBM-resident).  Three forms, each timed on its own:
+    `value` (that is HBM-resident).  Each form is timed on its own:
 
     value (`reader_to_pinned`): every batch's part bytes are copied, inside the timed region, by
       `host_threads` threads from a pageable source ring (2x the slots' bytes, so every copy
@@ -365,15 +551,16 @@ def end_to_end(codec, d, p, L, gib, world, rank, reduce_dev, host_threads, devic
       (writer.rs:170-197) when `data_buf` is the engine's page-locked slot -- then H2D, the
       fused kernel (or, for these 256-part batches, encode + split SHA), D2H (cec_pipeline,
       256-part batches, 4 slots in flight);
+    `read_repair`: the read side of the same stream (timed_read_repair): d random chunks per
+      part fetched from a pageable ring of stored chunks, `corrupt` of them damaged, verified on
+      the GPU, missing data rebuilt, failed parts retried with another chunk;
     `scheduler_pageable`: the `cp` path of a single process -- the same pageable ring handed to
       the multi-GPU scheduler (cec_multi, one shard on this rank's GPU), whose own NUMA-local
       copy threads stage it;
     `pcie_link`: the slots filled once and re-sent (8 bytes per part stamped): the link alone,
       no host production (round 2's figure)."""
-    import numpy as np
     P, depth = CONFIGS["c5"]["parts"], 4
     n_parts = max(depth * P, int(gib * (1 << 30)) // (d * L))
-    n_batches = (n_parts + P - 1) // P
     # 2x the slots' part count at N = 1 (20 GiB); at N > 1 every rank of the node holds its own
     # ring, slots and scheduler staging at once, so the ring shrinks to 2 batches (5 GiB, still
     # 20x a socket's L3: every copy reads DRAM) to keep the node's host memory near 20 GiB per GPU
@@ -392,50 +579,16 @@ def end_to_end(codec, d, p, L, gib, world, rank, reduce_dev, host_threads, devic
         copier.close()
         return {"value": None, "unit": "GB/s", "bound": "pcie",
                 "skipped": err or "another rank could not allocate its slots / source ring"}
-    stamp = np.arange(n_parts, dtype=np.uint64).view(np.uint8).reshape(n_parts, 8)
-
-    def timed(fill):
-        for _ in range(depth):  # warmup: one batch per slot
-            slot, data = pl.acquire()
-            fill(data, 0, P)
-            pl.submit(slot, P)
-        pl.drain()
-        barrier(world)
-        t0 = time.perf_counter()
-        part = 0
-        for _ in range(n_batches):
-            slot, data = pl.acquire()
-            n = min(P, n_parts - part)
-            fill(data, part, n)
-            pl.submit(slot, n)
-            part += n
-        pl.drain()
-        barrier(world)
-        return time.perf_counter() - t0
-
-    def from_ring(data, part, n):  # the reader: part bytes from the pageable source
-        r = part % ring_parts
-        m = min(n, ring_parts - r)
-        copier.copy(data[:m], ring[r:r + m])
-        if m < n:
-            copier.copy(data[m:n], ring[:n - m])
-        data[:n, 0, :8] = stamp[part:part + n]
 
     def stamp_only(data, part, n):
-        data[:n, 0, :8] = stamp[part:part + n]
+        data[:n, 0, :8] = part_stamps(part, n)
 
-    # parity / digests of the last batch against the oracle would need the CPU path; the
-    # ring-fed batches are checked for the property that holds at any size instead: every
-    # digest of a data chunk equals SHA-256 of the ring bytes it was copied from (sampled)
-    loc_ring = timed(from_ring)
+    loc_ring, slot, n = timed_write(pl, ring_reader(ring, copier), 0, n_parts, world)
     el_ring = max_over_ranks(loc_ring, world, reduce_dev)
-    _, dg = pl.wait((n_batches - 1) % depth)
-    import hashlib
-    first = (n_batches - 1) * P
-    k = min(len(dg), n_parts - first) - 1
-    src = ring[(first + k) % ring_parts, 1]  # chunk 1: not stamped
-    ring_ok = bool(dg[k, 1].tobytes() == hashlib.sha256(src.tobytes()).digest())
-    loc_link = timed(stamp_only)
+    # the ring-fed batches are checked for the property that holds at any size: the digests of
+    # the data chunks equal SHA-256 of the bytes the reader produced (sampled)
+    ring_ok = write_check(pl, ring, slot, n, n_parts - 1)
+    loc_link = timed_write(pl, stamp_only, 0, n_parts, world)[0]
     el_link = max_over_ranks(loc_link, world, reduce_dev)
     del pl
     total = n_parts * d * L * world
@@ -464,8 +617,46 @@ def end_to_end(codec, d, p, L, gib, world, rank, reduce_dev, host_threads, devic
     # the scheduler's pageable path (what `cp` through the C++ FileWriteBuilder batch takes)
     res["scheduler_pageable"] = scheduler_pageable(codec, d, p, L, ring, n_parts, world,
                                                    reduce_dev, device_ordinal)
+    del ring
+    res["read_repair"] = read_repair_form(codec, d, p, L, n_parts, world, rank, reduce_dev,
+                                          copier, device, corrupt)
     copier.close()
     return res
+
+
+def read_repair_form(codec, d, p, L, n_parts, world, rank, reduce_dev, copier, device, corrupt):
+    """end_to_end's read side: n_parts per rank through timed_read_repair (2 batches of stored
+    parts in the ring: 7 GiB, every fetch reads DRAM)."""
+    P, depth = CONFIGS["c5r"]["parts"], 4
+    try:
+        ring, ring_dig = encoded_ring(codec, d, p, L, 2 * P, rank_seed(0xE2ED, rank), device, P)
+        loc, stats, checks = timed_read_repair(codec, ring, ring_dig, L, P, depth, 0, n_parts,
+                                               world, corrupt, copier, 0xE2E5 + rank)
+        err = None
+    except Exception as e:  # noqa: BLE001 (reported in the line)
+        loc, stats, checks, ring, err = 0.0, None, [], None, f"{type(e).__name__}: {e}"
+    # every rank reaches this collective (a failing rank's barriers were never entered by the
+    # others only if it failed before the first one: allocation, the usual case)
+    if not all_ranks_ok(err is None, world, reduce_dev):
+        return {"value": None, "unit": "GB/s",
+                "skipped": err or "another rank could not run its read stream"}
+    el = max_over_ranks(loc, world, reduce_dev)
+    total = n_parts * d * L * world
+    ok = all(c["ok"] for c in checks) and stats["undecodable_parts"] == 0
+    return {"value": round(total / el / 1e9, 2), "unit": "GB/s of part data delivered",
+            "_local": n_parts * d * L / loc / 1e9,
+            "seconds": round(el, 3), "stream_bytes": total, "corrupt_frac": corrupt,
+            "retries": stats["retried_parts"], "retry_batches": stats["retry_batches"],
+            "rejected_chunks": stats["rejected_chunks"], "damaged_loads": stats["damaged_loads"],
+            "undecodable_parts": stats["undecodable_parts"], "batches": stats["batches"],
+            "chunks_loaded": stats["chunks_loaded"],
+            "sampled_parts_equal_stored": ok, "checks": checks,
+            "path": f"pageable ring of {len(ring)} stored parts ({size_label(ring.nbytes)}) -> "
+                    f"{copier.threads} host threads copy d random chunks per part into a "
+                    "page-locked slot, a seeded fraction of them damaged -> H2D -> SHA-256 "
+                    "verify + reconstruct_data -> D2H of the rebuilt data chunks; parts with a "
+                    "rejected chunk resubmitted with their verified chunks (CEC_PRESENT_VERIFIED) "
+                    f"and one more (cec_read_pipeline, {P}-part batches, {depth} slots)"}
 
 
 def scheduler_pageable(codec, d, p, L, ring, n_parts, world, reduce_dev, device_ordinal):
@@ -523,6 +714,62 @@ def scheduler_pageable(codec, d, p, L, ring, n_parts, world, reduce_dev, device_
                     f"{J} in flight"}
 
 
+def snapshot_parts(buf, digests, parts):
+    """Host copies of whole parts (every chunk) of a device batch, and their digests: the
+    default line's full-size buffers, checked against the oracle after the timed work."""
+    return [(int(k), buf[k].cpu().numpy(), None if digests is None else digests[k].cpu().numpy())
+            for k in parts]
+
+
+def check_vs_oracle(snap, d, p):
+    """cpu_baseline leg: the sampled parts of the default line's own buffers against the CPU
+    restatement of the reference crates (oracle.encode_sep, the galois_8 table path) and
+    hashlib SHA-256:
+      headline        -- the fused encode_hash_kernel's parity and all d+p digests (C2);
+      north_star      -- the parity the north_star encode (bit-sliced kernel) rewrote;
+      c3_reconstruct  -- every chunk after C3's 1-4 erasures were rebuilt (data + parity);
+      c4_encode_hash  -- RS(20,8) parity + 28 digests of the fused kernel (C4's buffer);
+      c4_round_trip   -- the same C4 parts after 8 erasures and reconstruct."""
+    import hashlib
+
+    import numpy as np
+    import oracle
+    res = {}
+
+    def parity_ok(part, dd, pp):
+        st, par = oracle.encode_sep(dd, pp, [part[j] for j in range(dd)])
+        return st == 0 and all(np.array_equal(par[i], part[dd + i]) for i in range(pp))
+
+    def digests_ok(part, dg):
+        return all(hashlib.sha256(part[i].tobytes()).digest() == dg[i].tobytes()
+                   for i in range(len(part)))
+
+    head = {k: part for k, part, _ in snap["headline"]}
+    res["headline"] = all(parity_ok(part, d, p) and digests_ok(part, dg)
+                          for _, part, dg in snap["headline"])
+    if "north_star_encode" in snap:
+        res["north_star_encode"] = all(np.array_equal(part[d:], head[k][d:]) and
+                                       parity_ok(part, d, p)
+                                       for k, part, _ in snap["north_star_encode"])
+    if "c3_reconstruct" in snap:
+        res["c3_reconstruct"] = all(np.array_equal(part, head[k]) and parity_ok(part, d, p)
+                                    for k, part, _ in snap["c3_reconstruct"])
+    if "c4_encode_hash" in snap:
+        c4 = CONFIGS["c4"]
+        d4, p4 = c4["d"], c4["p"]
+        first = {k: part for k, part, _ in snap["c4_encode_hash"]}
+        res["c4_encode_hash"] = all(parity_ok(part, d4, p4) and digests_ok(part, dg)
+                                    for _, part, dg in snap["c4_encode_hash"])
+        if "c4_round_trip" in snap:
+            res["c4_round_trip"] = all(np.array_equal(part, first[k])
+                                       for k, part, _ in snap["c4_round_trip"])
+    return {"ok": all(res.values()), "checks": res, "parts": list(snap["parts"]),
+            "erased_in_c3": {str(k): v for k, v in snap.get("c3_erased", {}).items()},
+            "basis": "whole parts (all chunks) copied from the buffers that produced value, "
+                     "north_star and baseline_configs, compared with oracle.encode_sep (CPU "
+                     "restatement of reed-solomon-erasure 4.0.2 galois_8) and hashlib SHA-256"}
+
+
 def two_erasures(n_parts: int, t: int, rank: int):
     """north_star's reconstruct case: exactly 2 erasures per part, uniform over the t chunks
     (seeded, the c3e2 config's sets).  Returns the present mask as a uint8 [n][t] tensor."""
@@ -541,7 +788,8 @@ def reconstruct_data_bytes(pres, d: int, L: int) -> int:
     return int((miss > 0).sum().item()) * d * L + int(miss.sum().item()) * L
 
 
-def north_star_block(codec, batch, buf, digests, stream, device, rank, d, p, L, steps):
+def north_star_block(codec, batch, buf, digests, stream, device, rank, d, p, L, steps,
+                     snap=None):
     """north_star's two numeric targets, timed on the headline's own buffer right after it:
     RS(10,4) encode (file_part.rs:161-165) and 2-erasure reconstruct_data (file_part.rs:128)
     over every part, each launch bracketed by HIP events on `stream` (1 warmup launch, then
@@ -579,6 +827,8 @@ def north_star_block(codec, batch, buf, digests, stream, device, rank, d, p, L, 
     ms = time_launches(lambda: ce.encode_batch(codec, batch, stream))
     out["encode"] = entry("encode_sep (cec_encode_batch), every part: read d, write p chunks",
                           encode_kernel(d, p), ms, n * t * L, "c2enc")
+    if snap is not None:  # the parity this encode kernel wrote, for the oracle check
+        snap["north_star_encode"] = snapshot_parts(buf, None, snap["parts"])
     pres = two_erasures(n, t, rank)
     present = bytes(pres.flatten().tolist())
     buf.mul_(pres.to(device).view(n, t, 1))  # the erased chunks start zeroed
@@ -613,7 +863,8 @@ def c3_erasures(n_parts: int, t: int, p: int, rank: int):
     return pres
 
 
-def baseline_configs_block(codec, batch, buf, digests, stream, device, rank, d, p, L, steps):
+def baseline_configs_block(codec, batch, buf, digests, stream, device, rank, d, p, L, steps,
+                           snap=None):
     """BASELINE.json's other device-resident configurations in the default line, so the driver's
     run observes them too: configs[2] (C3: RS(10,4) reconstruct with 1-4 random erasures per
     part, data + parity, file_part.rs:304) on the headline's buffer, and configs[3] (C4: RS(20,8),
@@ -646,6 +897,10 @@ def baseline_configs_block(codec, batch, buf, digests, stream, device, rank, d, 
     present = bytes(pres.flatten().tolist())
     buf.mul_(pres.to(device).view(n, t, 1))
     ms = timed(lambda: ce.reconstruct_batch(codec, batch, present, False, stream))
+    if snap is not None:  # every chunk after the rebuild (each sampled part lost 1-4 of them)
+        snap["c3_reconstruct"] = snapshot_parts(buf, None, snap["parts"])
+        snap["c3_erased"] = {k: [int(i) for i in (pres[k] == 0).nonzero().flatten()]
+                             for k in snap["parts"]}
     touched = int((pres.sum(1) < t).sum().item())
     algo = touched * d * L + int((t - pres.sum(1)).sum().item()) * L
     gbs = algo / (ms / 1e3) / 1e9
@@ -669,6 +924,8 @@ def baseline_configs_block(codec, batch, buf, digests, stream, device, rank, d, 
     b4 = ce.PartBatch.from_tensor(buf4, L4)
     ce.fill_synthetic(b4, t4, rank_seed(0xC4C4, rank), stream)
     ms = timed(lambda: ce.encode_hash_batch(codec4, b4, dig4.data_ptr(), stream))
+    if snap is not None:  # RS(20,8) parity + all 28 digests of the fused kernel
+        snap["c4_encode_hash"] = snapshot_parts(buf4, dig4, (0, n4 - 1))
     data_gbs = n4 * d4 * L4 / (ms / 1e3) / 1e9
     hbm = n4 * t4 * (L4 + 32) / (ms / 1e3) / 1e9
     g = torch.Generator().manual_seed(2828 + rank)
@@ -677,11 +934,14 @@ def baseline_configs_block(codec, batch, buf, digests, stream, device, rank, d, 
         pres4[i, torch.randperm(t4, generator=g)[:p4]] = 0
     buf4.mul_(pres4.to(device).view(n4, t4, 1))
     ce.reconstruct_batch(codec4, b4, bytes(pres4.flatten().tolist()), False, stream)
+    if snap is not None:  # the same parts after 8 erasures and reconstruct
+        snap["c4_round_trip"] = snapshot_parts(buf4, None, (0, n4 - 1))
     tr, src = measured_traffic("c4", "encode_hash_kernel", True, with_source=True)
     out["c4_encode_hash"] = {
         "config": f"BASELINE configs[3] per GPU: RS(20,8), {n4} parts x {size_label(L4)}, fused "
                   "encode + SHA-256 of all 28 chunks", "kernel": "encode_hash_kernel",
         "ms": round(ms, 4), "value": round(data_gbs, 2), "unit": "GB/s of data",
+        "data_bytes": n4 * d4 * L4,
         "hbm_achieved": round(hbm, 1), "hbm_frac": round(hbm / HBM_PEAK_GBS, 4),
         "traffic": tr, "traffic_source": src,
         "round_trip_verified": verified(b4, dig4, t4, n4),
@@ -702,37 +962,30 @@ def _segments(args, cfg, shards):
 
 def run_stream_multi(args, cfg, codec, total_parts):
     """C5 through the single-process multi-GPU scheduler (cec_multi: one worker thread per
-    shard, contiguous part ranges, NUMA-local staging): page-locked source segments
-    (cec_host_alloc, filled once, part numbers stamped per job) DMA'd directly, two jobs in
-    flight."""
-    import numpy as np
+    shard, contiguous part ranges, NUMA-local staging): each job hands the scheduler a range of
+    a pageable source ring of distinct parts (one job's worth, read cyclically); the shards' own
+    copy threads stage the bytes into page-locked slots inside the timed region; parity and
+    digests land in page-locked outputs.  --jobs-in-flight jobs queued at once."""
     d, p, L, P = cfg["d"], cfg["p"], cfg["chunk"], cfg["parts"]
     t = d + p
     devices = args.devices
     depth = int(os.environ.get("CEC_STREAM_DEPTH", "4"))  # slots in flight (A/B knob)
     m = ce.Multi(codec, L, P, depth, devices)
     S = _segments(args, cfg, len(devices))
-    rng = np.random.default_rng(0)
     J = args.jobs_in_flight
-    segs = []
-    for _ in range(J):
-        src = ce.HostBuffer(S * d * L, devices[0])
-        par = ce.HostBuffer(S * p * L, devices[0])
-        dig = ce.HostBuffer(S * t * 32, devices[0])
-        sv = src.view(S, d, L)
-        for k in range(0, S, 64):  # fill once (64-part slabs keep the generator's memory small)
-            sv[k:k + 64] = rng.integers(0, 256, size=sv[k:k + 64].shape, dtype=np.uint8)
-        segs.append((src, par, dig))
+    copier = HostCopier(_rank_threads(1))
+    ring = source_ring(S, d, L, 0xC5, copier)
+    copier.close()
+    outs = [(ce.HostBuffer(S * p * L, devices[0]), ce.HostBuffer(S * t * 32, devices[0]))
+            for _ in range(J)]
     n_jobs = (total_parts + S - 1) // S
 
     def submit(i, first):
-        src, par, dig = segs[i % J]
+        par, dig = outs[i % J]
         n = min(S, total_parts - first)
-        src.view(S, d, L)[:n, 0, :8] = np.arange(first, first + n, dtype=np.uint64).view(
-            np.uint8).reshape(n, 8)
-        return m.encode_hash(src, n, par, dig), n
+        return m.encode_hash(ring[:n], n, par, dig), n
 
-    for i in range(J):  # warmup: one job per segment (pipelines, device buffers, first pinning)
+    for i in range(J):  # warmup: one job per output buffer (pipelines, staging, first pinning)
         m.wait(submit(i, 0)[0])
     t0 = time.perf_counter()
     jobs, first = [], 0
@@ -752,255 +1005,64 @@ def run_stream_multi(args, cfg, codec, total_parts):
         {"slots": depth, "shards": len(devices), "parts_per_job": S, "jobs_in_flight": J,
          "parallelism": f"single process, {len(devices)} shard(s) on devices {devices}, contiguous "
                         "part ranges, no collective"},
-        "synthetic host stream (page-locked cec_host_alloc segments filled once, part numbers "
-        "stamped per job, DMA'd without staging)",
+        f"synthetic host stream: a pageable source ring of {S} distinct parts "
+        f"({size_label(ring.nbytes)}) read cyclically, staged by the scheduler's copy threads "
+        "inside the timed region",
         shards=[{"device": dv, "numa_node": nn, "parts": pp} for dv, nn, pp in per_shard])),
         flush=True)
 
 
-def run_read_stream(args, cfg, codec, world, rank, device, reduce_dev):
-    """C5 read side: pinned slots -> H2D of the loaded chunks -> SHA-256 verify + speculative
-    reconstruct_data -> D2H of the rebuilt data chunks (cec_read_pipeline, REBUILT_ONLY).  Every
-    part loads d random chunks of its d+p (file_part.rs:97 samples d); the chunks and their
-    metadata digests are filled into the slots once (a GPU-encoded block of parts), the loaded
-    set changes per batch.  Time = first submit to last result, max over ranks; value = part
-    data bytes delivered / s."""
-    import numpy as np
-    d, p, L, P = cfg["d"], cfg["p"], cfg["chunk"], cfg["parts"]
-    t = d + p
-    depth = int(os.environ.get("CEC_STREAM_DEPTH", "4"))  # slots in flight (A/B knob)
-    part_bytes = d * L
-    total_parts = int(args.stream_gib * (1 << 30)) // part_bytes
-    lo = total_parts * rank // world
-    hi = total_parts * (rank + 1) // world
-    mine = hi - lo
-    # one encoded block of P parts (data + parity + digests) from the GPU
-    blk = torch.empty((P, t, L), dtype=torch.uint8, device=device)
-    batch = ce.PartBatch.from_tensor(blk, L)
-    ce.fill_synthetic(batch, d, rank_seed(0xC5, rank))
-    dig = torch.empty((P, t, 32), dtype=torch.uint8, device=device)
-    ce.encode_hash_batch(codec, batch, dig.data_ptr())
-    torch.cuda.synchronize(device)
-    host_blk, host_dig = blk.cpu().numpy(), dig.cpu().numpy()
-    del blk, dig
-    rng = np.random.default_rng(rank)
-    masks = []
-    mask_mode = os.environ.get("CEC_C5R_MASK", "random")  # dev A/B: "data" = chunks 0..d-1
-    for _ in range(8):  # d random loaded chunks per part, a few distinct batch patterns
-        m = np.zeros((P, t), np.uint8)
-        for k in range(P):
-            m[k, np.arange(d) if mask_mode == "data" else rng.choice(t, d, replace=False)] = 1
-        masks.append(m)
-    if args.devices:
-        return run_read_stream_multi(args, cfg, codec, total_parts, host_blk, host_dig, masks)
-    # the loaded data chunks are already in the caller's pinned slot: only rebuilt ones come
-    # back (CEC_READ_REBUILT_ONLY); CEC_C5R_COPYALL=1 (A/B) copies all d data chunks back
-    copy_all = os.environ.get("CEC_C5R_COPYALL", "0") == "1"
-    if os.environ.get("CEC_C5R_PACKED", "0") == "1":
-        return run_read_stream_packed(args, cfg, codec, world, rank, reduce_dev, lo, hi,
-                                      total_parts, host_blk, host_dig, masks[:4], copy_all)
-    rp = ce.ReadPipeline(codec, L, P, depth, 0 if copy_all else ce.ReadPipeline.REBUILT_ONLY)
-    for i in range(depth):
-        slot, chunks, present, expected = rp.acquire()
-        chunks[:] = host_blk
-        expected[:] = host_dig
-    n_batches = (mine + P - 1) // P
-    for i in range(min(depth, n_batches)):  # warmup
-        slot, chunks, present, expected = rp.acquire()
-        present[:] = masks[i % len(masks)]
-        rp.submit(slot, P)
-    rp.drain()
-    barrier(world)
-    t0 = time.perf_counter()
-    part = lo
-    bad = 0
-    for i in range(n_batches):
-        slot, chunks, present, expected = rp.acquire()
-        if i >= depth:
-            _, _, status = rp.wait(slot)
-            bad += int((status != 0).sum())
-        n = min(P, hi - part)
-        present[:n] = masks[i % len(masks)][:n]
-        rp.submit(slot, n)
-        part += n
-    for i in range(depth):
-        _, _, status = rp.wait(i)
-        bad += int((status != 0).sum())
-    rp.drain()
-    barrier(world)
-    t1 = time.perf_counter()
-    el = max_over_ranks(t1 - t0, world, reduce_dev)
-    ok = None
-    if args.check and rank == 0:
-        # the last batch's data must equal the encoded block's data chunks
-        slot = (n_batches - 1) % depth
-        data, ver, status = rp.wait(slot)
-        n_last = int(data.shape[0])
-        ok = bad == 0
-        for k in (0, n_last // 2, n_last - 1):
-            ok = ok and rp.part_bytes(slot, n_last, k) == host_blk[k, :d].tobytes()
-        ok = bool(ok)
-    if rank == 0:
-        total = total_parts * part_bytes
-        extra = {"undecodable_parts": bad}
-        if ok is not None:
-            extra["check_vs_written"] = ok
-        print(json.dumps(_stream_line(
-            args, cfg, world, n_batches, min(depth, n_batches), el, total,
-            {"slots": depth, "parallelism": f"part-range-sharded x{world}, no collective"},
-            "synthetic host stream (GPU-encoded block of parts, d random chunks loaded per part, "
-            "loaded sets vary per batch)", **extra)), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+RANK_FIELDS = ("device", "numa_node", "host_threads_numa_bound", "cpus", "step_ms",
+               "end_to_end_GBs", "pcie_link_GBs", "north_star_encode_frac",
+               "north_star_reconstruct_data_frac", "c3_reconstruct_frac", "c3_algorithmic_bytes",
+               "c3_ms", "c4_ms", "c4_data_bytes", "read_repair_GBs")
 
 
-def run_read_stream_packed(args, cfg, codec, world, rank, reduce_dev, lo, hi, total_parts,
-                           host_blk, host_dig, masks, copy_all):
-    """c5r with the loaded chunks of each batch packed back to back (part by part, ascending
-    chunk index: what a reader fetching a part's chunks in turn writes) and submitted with
-    cec_read_pipeline_submit_packed: one upload per batch.  One page-locked packed buffer per
-    loaded-set pattern (filled once, as the slots are in the unpacked form); outputs into
-    page-locked per-slot buffers."""
-    import numpy as np
-    d, p, L, P = cfg["d"], cfg["p"], cfg["chunk"], cfg["parts"]
-    t = d + p
-    depth = int(os.environ.get("CEC_STREAM_DEPTH", "4"))  # slots in flight (A/B knob)
-    mine = hi - lo
-    flags = ce.PIPE_EXTERNAL | (0 if copy_all else ce.ReadPipeline.REBUILT_ONLY)
-    rp = ce.ReadPipeline(codec, L, P, depth, flags)
-    packs = []
-    for m in masks:
-        buf = ce.HostBuffer(int(m.sum()) * L)
-        view = buf.array.reshape(-1, L)
-        view[:] = host_blk.reshape(P * t, L)[np.flatnonzero(m.reshape(-1))]
-        packs.append(buf)
-    outs = [ce.HostBuffer(P * d * L) for _ in range(depth)]
-    expected = np.ascontiguousarray(host_dig)
-    n_batches = (mine + P - 1) // P
-
-    def submit(i, n):
-        m = masks[i % len(masks)]
-        slot, _, _, _ = rp.acquire()
-        rp.submit_packed(slot, packs[i % len(masks)], m, expected, n, outs[slot])
-        return slot
-
-    for i in range(min(depth, n_batches)):  # warmup
-        submit(i, P)
-    rp.drain()
-    barrier(world)
-    t0 = time.perf_counter()
-    part, bad = lo, 0
-    order = []
-    for i in range(n_batches):
-        if i >= depth:
-            _, _, status = rp.wait(order[i - depth])
-            bad += int((status != 0).sum())
-        n = min(P, hi - part)
-        order.append(submit(i, n))
-        part += n
-    for slot in order[-depth:]:
-        _, _, status = rp.wait(slot)
-        bad += int((status != 0).sum())
-    rp.drain()
-    barrier(world)
-    t1 = time.perf_counter()
-    el = max_over_ranks(t1 - t0, world, reduce_dev)
-    ok = None
-    if args.check and rank == 0:
-        slot = order[-1]
-        _, _, status = rp.wait(slot)
-        n_last = int(status.shape[0])
-        ok = bad == 0
-        for k in (0, n_last // 2, n_last - 1):
-            ok = ok and rp.part_bytes(slot, n_last, k) == host_blk[k, :d].tobytes()
-        ok = bool(ok)
-    if rank == 0:
-        extra = {"undecodable_parts": bad, "packed_upload": True}
-        if ok is not None:
-            extra["check_vs_written"] = ok
-        print(json.dumps(_stream_line(
-            args, cfg, world, n_batches, min(depth, n_batches), el, total_parts * d * L,
-            {"slots": depth, "parallelism": f"part-range-sharded x{world}, no collective"},
-            "synthetic host stream (GPU-encoded block of parts, d random chunks loaded per part "
-            "and packed back to back, 4 loaded-set patterns cycling)", **extra)), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+def rank_row(r: int, row) -> dict:
+    """One rank's gathered figures (gather_rows order = RANK_FIELDS) as the line's `ranks` entry;
+    a figure the rank did not produce (0) is None."""
+    out = {"rank": r}
+    for name, v in zip(RANK_FIELDS, row):
+        if name in ("device", "numa_node", "cpus", "c3_algorithmic_bytes", "c4_data_bytes"):
+            out[name] = int(v)
+        elif name == "host_threads_numa_bound":
+            out[name] = bool(v)
+        elif name == "step_ms":
+            out[name] = round(v, 3)
+        elif name.endswith("_frac"):
+            out[name] = round(v, 4) if v else None
+        else:
+            out[name] = round(v, 4) if v else None
+    return out
 
 
-def run_read_stream_multi(args, cfg, codec, total_parts, host_blk, host_dig, masks):
-    """C5 read side through the multi-GPU scheduler: page-locked chunk segments (the encoded
-    block tiled, filled once), present masks varying per job, REBUILT_ONLY (loaded data chunks
-    stay where they were read), two jobs in flight."""
-    import ctypes
-
-    import numpy as np
-    d, p, L, P = cfg["d"], cfg["p"], cfg["chunk"], cfg["parts"]
-    t = d + p
-    devices = args.devices
-    depth = int(os.environ.get("CEC_STREAM_DEPTH", "4"))  # slots in flight (A/B knob)
-    m = ce.Multi(codec, L, P, depth, devices)
-    S = _segments(args, cfg, len(devices))
-    reps = S // P
-    J = args.jobs_in_flight
-    segs = []
-    for _ in range(J):
-        ch = ce.HostBuffer(S * t * L, devices[0])
-        out = ce.HostBuffer(S * d * L, devices[0])
-        cv = ch.view(S, t, L)
-        for r in range(reps):
-            cv[r * P:(r + 1) * P] = host_blk
-        segs.append(dict(ch=ch, out=out, pres=np.zeros((S, t), np.uint8),
-                         exp=np.ascontiguousarray(np.tile(host_dig, (reps, 1, 1))),
-                         ver=np.zeros((S, t), np.uint8), st=np.zeros(S, np.int32)))
-    n_jobs = (total_parts + S - 1) // S
-    bad = 0
-
-    def submit(i, n):
-        sg = segs[i % J]
-        for r in range(reps):
-            sg["pres"][r * P:(r + 1) * P] = masks[(i + r) % len(masks)]
-        job, ptrs = m.read(sg["ch"], sg["pres"], sg["exp"], n, sg["out"], sg["ver"], sg["st"],
-                           rebuilt_only=True)
-        return job, n, ptrs
-
-    for i in range(J):
-        j, n, _ = submit(i, S)
-        m.wait(j)
-    t0 = time.perf_counter()
-    jobs, first = [], 0
-    for i in range(n_jobs):
-        if len(jobs) == J:
-            j, n, _ = jobs.pop(0)
-            m.wait(j)
-            bad += int((segs[(i - J) % J]["st"][:n] != 0).sum())
-        n = min(S, total_parts - first)
-        jobs.append(submit(i, n))
-        first += n
-    last = None
-    for q, (j, n, ptrs) in enumerate(jobs):
-        m.wait(j)
-        bad += int((segs[(n_jobs - len(jobs) + q) % J]["st"][:n] != 0).sum())
-        last = (n, ptrs)
-    el = time.perf_counter() - t0
-    ok = None
-    if args.check and last is not None:
-        n, ptrs = last
-        ok = bad == 0 and all(
-            b"".join(ctypes.string_at(ptrs[k * d + j], L) for j in range(d)) ==
-            host_blk[k % P, :d].tobytes() for k in (0, n // 2, n - 1))
-    total = total_parts * d * L
-    extra = {"undecodable_parts": bad,
-             "shards": [dict(zip(("device", "numa_node", "parts"), m.shard_info(g)))
-                        for g in range(len(devices))]}
-    if ok is not None:
-        extra["check_vs_written"] = bool(ok)
-    print(json.dumps(_stream_line(
-        args, cfg, len(set(devices)), n_jobs, J, el, total,
-        {"slots": depth, "shards": len(devices), "parts_per_job": S, "jobs_in_flight": J,
-         "parallelism": f"single process, {len(devices)} shard(s) on devices {devices}, contiguous "
-                        "part ranges, no collective"},
-        "synthetic host stream (page-locked segments tiled from a GPU-encoded block, d random "
-        "chunks loaded per part, REBUILT_ONLY)", **extra)), flush=True)
+def node_figures(ranks) -> dict:
+    """BASELINE configs[2] and configs[3] at node level from the per-rank rows: each rank's GPU
+    runs its own C3 / C4 batch, so the node figure is the data of all ranks over the slowest
+    rank's time (C4: sum of data bytes / max ms), and the fractions are the weakest rank's
+    (min over ranks).  None when a rank did not run the block."""
+    out = {"ranks": len(ranks)}
+    if all(r.get("c4_ms") for r in ranks):
+        c4_ms = max(r["c4_ms"] for r in ranks)
+        c4_bytes = sum(r["c4_data_bytes"] for r in ranks)
+        out["c4_encode_hash"] = {
+            "value": round(c4_bytes / (c4_ms / 1e3) / 1e9, 2), "unit": "GB/s of data per node",
+            "data_bytes": c4_bytes, "max_ms": c4_ms,
+            "basis": "configs[3] sharded across the node's GPUs: sum over ranks of each GPU's "
+                     "RS(20,8) batch data / the slowest rank's fused encode + SHA-256 time"}
+    if all(r.get("c3_ms") for r in ranks):
+        c3_ms = max(r["c3_ms"] for r in ranks)
+        c3_bytes = sum(r["c3_algorithmic_bytes"] for r in ranks)
+        out["c3_reconstruct"] = {
+            "achieved": round(c3_bytes / (c3_ms / 1e3) / 1e9, 1), "unit": "GB/s per node",
+            "min_frac": min(r["c3_reconstruct_frac"] for r in ranks),
+            "basis": "algorithmic bytes of every rank's reconstruct / the slowest rank's time; "
+                     "min_frac = the weakest GPU's fraction of its own 8 TB/s"}
+    for key in ("north_star_encode_frac", "north_star_reconstruct_data_frac"):
+        vals = [r.get(key) for r in ranks]
+        if all(vals):
+            out["min_" + key] = min(vals)
+    return out
 
 
 def main():
@@ -1022,14 +1084,18 @@ def main():
     ap.add_argument("--separate", action="store_true",
                     help="encode_hash as two launches (encode kernel, then SHA-256 kernel) "
                          "instead of the fused encode_hash_kernel")
+    ap.add_argument("--corrupt", type=float, default=0.01,
+                    help="c5r / end_to_end.read_repair: fraction of fetched chunks damaged")
     ap.add_argument("--devices", default=None,
-                    help="c5/c5r only: run in ONE process through the multi-GPU scheduler "
+                    help="c5 only: run in ONE process through the multi-GPU scheduler "
                          "(cec_multi), one shard per listed device ordinal, e.g. 0,1,2,3 "
                          "(repeats allowed: 0,0 = two shards on GPU 0)")
     ap.add_argument("--jobs-in-flight", type=int, default=2,
                     help="--devices mode: scheduler jobs (segments of the stream) queued at once")
     args = ap.parse_args()
     args.devices = [int(x) for x in args.devices.split(",")] if args.devices else None
+    if args.devices and args.config != "c5":
+        ap.error("--devices applies to c5 (the scheduler's write stream)")
 
     cfg = dict(CONFIGS[args.config])
     if args.parts:
@@ -1049,16 +1115,18 @@ def main():
     torch.cuda.set_device(ordinal)
     device = torch.device("cuda", ordinal)
     # the process's own CPU set, before the NUMA binding below narrows the main thread's (the
-    # CPU baseline runs with it restored)
+    # CPU baseline runs with it restored; the line's `host` block reports it)
     full_affinity = os.sched_getaffinity(0)
+    host = host_info()
     # host threads and the pinned slots of this rank on its GPU's NUMA node (the engine places
     # its own pinned buffers there anyway; this keeps the host copies local too)
     numa_bound = ce.bind_thread_to_device_node(ordinal)
     numa_node = ce.device_numa_node(ordinal)
     rank_cpus = len(os.sched_getaffinity(0))
+    host["rank_cpus_after_numa_bind"] = rank_cpus
     # host threads of this rank's end-to-end reader: half its CPUs (the rest run the engine's
     # own threads), 8 at most
-    e2e_threads = int(os.environ.get("CEC_E2E_THREADS", "0")) or max(1, min(8, rank_cpus // 2))
+    e2e_threads = _rank_threads(world)
     # RCCL ("nccl") carries only the barrier and the max-over-ranks all-reduce.
     # CEC_BENCH_BACKEND=gloo rehearses N > 1 with several ranks on one GPU.
     backend = os.environ.get("CEC_BENCH_BACKEND", "nccl")
@@ -1300,16 +1368,22 @@ def main():
             ok = ok and all(hashlib.sha256(host[j].tobytes()).digest() == dg[j].tobytes()
                             for j in range(t))
 
+    # sampled whole parts of the buffers behind value / north_star / baseline_configs, checked
+    # against the oracle in the cpu_baseline leg (N = 1, after every timed region)
+    snap = None
+    if (args.config == "c2" and fused and world == 1 and not args.no_cpu_baseline):
+        snap = {"parts": (0, n_parts // 2, n_parts - 1)}
+        snap["headline"] = snapshot_parts(buf, digests, snap["parts"])
     # north_star's two >= 60 % targets on the same buffer (C2 only)
     nstar = None
     if args.config == "c2" and not args.separate and not args.no_north_star:
         nstar = north_star_block(codec, batch, buf, digests, stream, device, rank, d, p, L,
-                                 args.steps)
+                                 args.steps, snap)
     others = None
     if (args.config == "c2" and not args.separate and not args.no_north_star
             and n_parts == CONFIGS["c2"]["parts"]):
         others = baseline_configs_block(codec, batch, buf, digests, stream, device, rank, d, p,
-                                        L, args.steps)
+                                        L, args.steps, snap)
     del buf, digests  # the end-to-end forms below use their own buffers
     torch.cuda.empty_cache()
 
@@ -1317,26 +1391,26 @@ def main():
     e2e = None
     if args.config == "c2" and args.e2e_gib > 0 and not args.separate:
         e2e = end_to_end(codec, d, p, L, args.e2e_gib, world, rank, reduce_dev, e2e_threads,
-                         ordinal)
+                         ordinal, device, args.corrupt)
 
     # per-rank figures for the N > 1 line (a straggler or a cross-NUMA placement must be
     # visible from the line alone)
-    ranks = None
+    ranks = node = None
     if world > 1:
         e2e_v, link_v = (e2e or {}).get("_local") or (0.0, 0.0)
-        # each rank's own north_star fractions (the block runs on every rank, on its own GPU)
+        rr_v = ((e2e or {}).get("read_repair") or {}).get("_local") or 0.0
+        # each rank's own north_star / C3 / C4 figures (the blocks run on every rank, on its
+        # own GPU)
         ns_enc = (nstar or {}).get("encode", {}).get("frac") or 0.0
         ns_rec = (nstar or {}).get("reconstruct_data_2_erasures", {}).get("frac") or 0.0
-        rows = gather_rows([ordinal, numa_node, 1.0 if numa_bound else 0.0, rank_cpus,
-                            local_s * 1e3, e2e_v, link_v, ns_enc, ns_rec], world, reduce_dev)
-        ranks = [{"rank": r, "device": int(row[0]), "numa_node": int(row[1]),
-                  "host_threads_numa_bound": bool(row[2]), "cpus": int(row[3]),
-                  "step_ms": round(row[4], 3),
-                  "end_to_end_GBs": round(row[5], 2) if row[5] else None,
-                  "pcie_link_GBs": round(row[6], 2) if row[6] else None,
-                  "north_star_encode_frac": round(row[7], 4) if row[7] else None,
-                  "north_star_reconstruct_data_frac": round(row[8], 4) if row[8] else None}
-                 for r, row in enumerate(rows)]
+        c3 = (others or {}).get("c3_reconstruct", {})
+        c4 = (others or {}).get("c4_encode_hash", {})
+        row = [ordinal, numa_node, 1.0 if numa_bound else 0.0, rank_cpus, local_s * 1e3, e2e_v,
+               link_v, ns_enc, ns_rec, c3.get("frac") or 0.0, c3.get("algorithmic_bytes") or 0,
+               c3.get("ms") or 0.0, c4.get("ms") or 0.0, c4.get("data_bytes") or 0, rr_v]
+        rows = gather_rows(row, world, reduce_dev)
+        ranks = [rank_row(r, row) for r, row in enumerate(rows)]
+        node = node_figures(ranks)
 
     if rank == 0:
         total_data = data_bytes * world
@@ -1381,16 +1455,23 @@ def main():
             line["baseline_configs"] = others
         if e2e is not None:
             e2e.pop("_local", None)
+            (e2e.get("read_repair") or {}).pop("_local", None)
             line["end_to_end"] = e2e
         if ranks is not None:
             steps_ms = [r["step_ms"] for r in ranks]
             line["ranks"] = ranks
+            line["node"] = node
             line["step_ms_over_ranks"] = {"max": round(max(steps_ms), 3),
                                           "mean": round(sum(steps_ms) / len(steps_ms), 3),
                                           "min": round(min(steps_ms), 3)}
         if ok is not None:
             line["check_vs_oracle"] = bool(ok)
-        line["host"] = host_info()
+        line["host"] = host
+        if snap is not None:
+            # the oracle leg (after every timed region): the sampled full-size parts
+            detail = check_vs_oracle(snap, d, p)
+            line["check_vs_oracle"] = detail["ok"]
+            line["check_vs_oracle_detail"] = detail
         if world == 1 and not args.no_cpu_baseline and cfg["op"] in ("encode_hash", "encode"):
             # the process's full CPU set (the main thread was bound to GPU0's NUMA node above)
             os.sched_setaffinity(0, full_affinity)

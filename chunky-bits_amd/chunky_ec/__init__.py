@@ -552,6 +552,7 @@ class Pipeline:
         self.d, self.p = codec.data_shard_count(), codec.parity_shard_count()
         self.L = chunk_len
         self.parts = parts_per_batch
+        self.depth = depth
 
     def __del__(self, _free=_lib.cec_pipeline_free):
         h = getattr(self, "_h", None)
@@ -629,6 +630,7 @@ class ReadPipeline:
         self.t = self.d + self.p
         self.L = chunk_len
         self.parts = parts_per_batch
+        self.depth = depth
 
     def __del__(self, _free=_lib.cec_read_pipeline_free):
         h = getattr(self, "_h", None)

@@ -1,0 +1,180 @@
+"""FileReadBuilder's part loop over a ReadPipeline, with read_with_context's retry rule.
+
+The reference reads a part by sampling chunks at random until d of them verify
+(src/file/file_part.rs:86-107: each of the d futures draws an untried chunk, reads it and keeps
+it only if its sha256 matches the metadata; a chunk that fails is dropped and another is drawn),
+then rebuilds the missing data chunks (file_part.rs:123-129).  FileReadBuilder streams the parts
+in file order (src/file/reader.rs:40-75).
+
+:class:`ReadRepairStream` runs that loop batched over a :class:`chunky_ec.ReadPipeline` (pinned
+slots, `depth` batches in flight):
+
+* a new part loads d chunks drawn at random from its d+p;
+* a part the pipeline reports ``TooFewShardsPresent`` (one of its loaded chunks failed the
+  hash) is queued for a retry: its verified chunks are loaded again flagged
+  ``CEC_PRESENT_VERIFIED`` (used, not hashed again) plus as many untried chunks, drawn at random,
+  as it is short of d; retries go out as batches of their own, interleaved with new parts;
+* a part with fewer than d chunks left to try is undecodable (the reference's read fails with
+  ``TooFewShardsPresent`` there; the stream counts it and goes on).
+
+The caller supplies the storage side: ``fetch(chunks, rows)`` copies the chunk bytes into the
+slot's pinned [parts][d+p][L] array for every (row, part id, flags) in ``rows``, for each chunk
+whose flag is nonzero.  A chunk flagged 1 is a fresh read (it may come back corrupted: that is
+what the retries are for); one flagged ``CEC_PRESENT_VERIFIED`` must be the bytes that verified
+before (the reference keeps a verified chunk in memory, file_part.rs:102-104).
+``digests(part_ids)`` returns the metadata digests [n][d+p][32].  Host bookkeeping only; all
+hashing and decoding runs in the pipeline's HIP kernels.
+"""
+from __future__ import annotations
+
+from collections import deque
+from dataclasses import dataclass, field
+from typing import Callable, Deque, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import OK, PRESENT_VERIFIED, TOO_FEW_SHARDS_PRESENT, Error
+
+
+@dataclass
+class _Part:
+    part: int                 # part id (file order)
+    tried: np.ndarray         # [t] bool: chunks loaded by any pass so far
+    good: np.ndarray          # [t] bool: chunks that verified
+    attempts: int = 1         # submissions of this part so far
+
+
+@dataclass
+class ReadRepairStats:
+    parts: int = 0              # parts read back (decoded) successfully
+    batches: int = 0            # batches submitted (new + retry)
+    retry_batches: int = 0      # batches made of retried parts only
+    retried_parts: int = 0      # part resubmissions (a part retried twice counts twice)
+    rejected_chunks: int = 0    # loaded chunks whose sha256 did not match the metadata
+    undecodable_parts: int = 0  # parts left with fewer than d chunks to try
+    chunks_loaded: int = 0      # chunk loads (first loads, retry loads and re-sent verified ones)
+    undecodable: List[int] = field(default_factory=list)  # their part ids (first 64)
+
+    def as_dict(self) -> dict:
+        out = dict(self.__dict__)
+        out["undecodable"] = list(self.undecodable)
+        return out
+
+
+class ReadRepairStream:
+    """Batched read_with_context with retries over `rp` (a ReadPipeline or anything with its
+    acquire / submit / wait / drain and `parts`, `d`, `t` attributes)."""
+
+    def __init__(self, rp, fetch: Callable[[np.ndarray, Sequence[Tuple[int, int, np.ndarray]]], None],
+                 digests: Callable[[np.ndarray], np.ndarray], seed: int = 0,
+                 on_part: Optional[Callable[[int, int, int, int, int], None]] = None):
+        self.rp = rp
+        self.fetch = fetch
+        self.digests = digests
+        self.rng = np.random.default_rng(seed)
+        # on_part(slot, n_parts_in_batch, row, part id, attempts): called for every part that
+        # decoded, while its output is valid (before the slot is acquired again)
+        self.on_part = on_part
+        self.P, self.d, self.t = rp.parts, rp.d, rp.t
+        self.depth = rp.depth
+        self.stats = ReadRepairStats()
+        self._retry: Deque[_Part] = deque()
+        self._inflight: Deque[Tuple[int, List[_Part], np.ndarray]] = deque()
+
+    # -- batch building -------------------------------------------------------------------------
+
+    def _new_parts(self, first: int, n: int) -> Tuple[List[_Part], np.ndarray]:
+        """Parts [first, first + n): d chunks each, drawn uniformly without replacement."""
+        t, d = self.t, self.d
+        pick = np.argsort(self.rng.random((n, t)), axis=1)[:, :d]
+        present = np.zeros((n, t), np.uint8)
+        np.put_along_axis(present, pick, 1, axis=1)
+        parts = [_Part(first + k, present[k] != 0, np.zeros(t, bool)) for k in range(n)]
+        return parts, present
+
+    def _retry_parts(self) -> Tuple[List[_Part], np.ndarray]:
+        """Up to P queued retries: verified chunks re-sent as PRESENT_VERIFIED plus untried ones
+        drawn at random up to d; parts that cannot reach d are counted undecodable."""
+        t, d = self.t, self.d
+        parts, rows = [], []
+        while self._retry and len(parts) < self.P:
+            e = self._retry.popleft()
+            need = d - int(e.good.sum())
+            untried = np.flatnonzero(~e.tried)
+            if need <= 0 or len(untried) < need:
+                # need <= 0 cannot come back from the pipeline (d verified chunks decode); fewer
+                # untried chunks than needed: the reference's read runs out of chunks here
+                self.stats.undecodable_parts += 1
+                if len(self.stats.undecodable) < 64:
+                    self.stats.undecodable.append(e.part)
+                continue
+            new = self.rng.choice(untried, need, replace=False)
+            row = np.where(e.good, PRESENT_VERIFIED, 0).astype(np.uint8)
+            row[new] = 1
+            e.tried[new] = True
+            parts.append(e)
+            rows.append(row)
+        present = np.stack(rows) if rows else np.zeros((0, t), np.uint8)
+        return parts, present
+
+    def _submit(self, parts: List[_Part], present: np.ndarray) -> None:
+        n = len(parts)
+        slot, chunks, pres, expected = self.rp.acquire()
+        pres[:n] = present
+        ids = np.fromiter((e.part for e in parts), dtype=np.int64, count=n)
+        expected[:n] = self.digests(ids)
+        self.fetch(chunks, [(k, int(ids[k]), present[k]) for k in range(n)])
+        self.rp.submit(slot, n)
+        self.stats.batches += 1
+        self.stats.chunks_loaded += int(np.count_nonzero(present))
+        self._inflight.append((slot, parts, present))
+
+    # -- results --------------------------------------------------------------------------------
+
+    def _collect(self) -> None:
+        slot, parts, present = self._inflight.popleft()
+        _, ver, status = self.rp.wait(slot)
+        n = len(parts)
+        for k in range(n):
+            st = int(status[k])
+            e = parts[k]
+            if st == OK:
+                self.stats.parts += 1
+                if self.on_part is not None:
+                    self.on_part(slot, n, k, e.part, e.attempts)
+                continue
+            if st != TOO_FEW_SHARDS_PRESENT:
+                raise Error(st)
+            loaded = present[k] != 0
+            ok = ver[k] != 0
+            self.stats.rejected_chunks += int(np.count_nonzero(loaded & ~ok))
+            e.good = ok.copy()
+            e.attempts += 1
+            self.stats.retried_parts += 1
+            self._retry.append(e)
+
+    # -- driver ---------------------------------------------------------------------------------
+
+    def run(self, first: int, n_parts: int) -> ReadRepairStats:
+        """Read parts [first, first + n_parts) to the end, retries included; returns the stats."""
+        nxt, end = first, first + n_parts
+        while nxt < end or self._retry or self._inflight:
+            # a slot is reused round-robin: collect the oldest batch before its slot is acquired
+            if len(self._inflight) == self.depth:
+                self._collect()
+            if len(self._retry) >= self.P or (nxt >= end and self._retry):
+                parts, present = self._retry_parts()
+                if parts:
+                    self._submit(parts, present)
+                    self.stats.retry_batches += 1
+                continue
+            if nxt < end:
+                n = min(self.P, end - nxt)
+                parts, present = self._new_parts(nxt, n)
+                self._submit(parts, present)
+                nxt += n
+                continue
+            if self._inflight:
+                self._collect()
+        self.rp.drain()
+        return self.stats

@@ -72,3 +72,118 @@ def test_measured_traffic_names_its_source():
     assert tr and tr > 0 and src.startswith("committed PMC run (not this run): profiles/")
     assert bench.measured_traffic("c2", "encode_hash_kernel", False, with_source=True) == \
         (None, None)
+
+
+class _FakeWritePipeline:
+    """cec_pipeline's slot contract on the CPU: acquire -> [P][d][L] slot, submit hashes the
+    data chunks (hashlib), wait -> (parity placeholder, digests [n][d][32])."""
+
+    def __init__(self, d, L, parts, depth):
+        self.d, self.L, self.parts, self.depth = d, L, parts, depth
+        self.slots = [np.zeros((parts, d, L), np.uint8) for _ in range(depth)]
+        self.dig = [None] * depth
+        self.next = 0
+        self.seen = []
+
+    def acquire(self):
+        i = self.next
+        self.next = (self.next + 1) % self.depth
+        return i, self.slots[i]
+
+    def submit(self, slot, n):
+        import hashlib
+        data = self.slots[slot][:n]
+        self.seen.append(data[:, 0, :8].copy().view(np.uint64).ravel().tolist())
+        self.dig[slot] = np.array([[np.frombuffer(hashlib.sha256(c.tobytes()).digest(), np.uint8)
+                                    for c in part] for part in data])
+
+    def wait(self, slot):
+        return None, self.dig[slot]
+
+    def drain(self):
+        pass
+
+
+def test_ring_reader_stream_stamps_every_part_and_checks_digests():
+    c = bench.HostCopier(3)
+    try:
+        d, L, P, depth = 3, 512, 4, 2
+        ring = bench.source_ring(5, d, L, 9, c)  # 5 ring parts: the stream wraps the ring
+        pl = _FakeWritePipeline(d, L, P, depth)
+        el, slot, n = bench.timed_write(pl, bench.ring_reader(ring, c), 100, 11, 1)
+        assert el >= 0 and n == 11 - 2 * P
+        # warmup batches first, then parts 100..110 in order, each stamped with its number
+        timed = [x for batch in pl.seen[depth:] for x in batch]
+        assert timed == list(range(100, 111))
+        assert bench.write_check(pl, ring, slot, n, 110)
+        # the check sees a wrong digest
+        pl.dig[slot][0, 1, 0] ^= 1
+        assert not bench.write_check(pl, ring, slot, n, 110)
+        # part k's bytes are ring part k mod 5 with its stamp
+        want = ring[107 % 5].copy()
+        want[0, :8] = bench.part_stamps(107, 1)[0]
+        import hashlib
+        assert bench.ring_part_digests(ring, 107) == [hashlib.sha256(x.tobytes()).digest()
+                                                      for x in want]
+    finally:
+        c.close()
+
+
+def test_host_copier_map_covers_range_once():
+    c = bench.HostCopier(4)
+    try:
+        seen = []
+        c.map(lambda a, b: seen.extend(range(a, b)), 10)
+        assert sorted(seen) == list(range(10))
+        c.map(lambda a, b: seen.append((a, b)), 0)  # nothing to do
+        assert len(seen) == 10
+    finally:
+        c.close()
+
+
+def test_check_vs_oracle_catches_a_wrong_byte():
+    """The default line's oracle leg on small parts: good parts pass every check; one flipped
+    parity byte / digest byte / rebuilt byte fails the matching check."""
+    import hashlib
+    import oracle
+    d, p, L = 10, 4, 1000
+    rng = np.random.default_rng(3)
+    parts, digs = [], []
+    for _ in range(3):
+        data = rng.integers(0, 256, size=(d, L), dtype=np.uint8)
+        st, par = oracle.encode_sep(d, p, list(data))
+        part = np.concatenate([data, np.stack(par)])
+        parts.append(part)
+        digs.append(np.array([np.frombuffer(hashlib.sha256(x.tobytes()).digest(), np.uint8)
+                              for x in part]))
+    ks = (0, 5, 9)
+    snap = {"parts": ks, "headline": [(k, parts[i], digs[i]) for i, k in enumerate(ks)],
+            "north_star_encode": [(k, parts[i].copy(), None) for i, k in enumerate(ks)],
+            "c3_reconstruct": [(k, parts[i].copy(), None) for i, k in enumerate(ks)]}
+    res = bench.check_vs_oracle(snap, d, p)
+    assert res["ok"] and all(res["checks"].values())
+    snap["north_star_encode"][1][1][d + 2, 7] ^= 1
+    snap["c3_reconstruct"][2][1][3, 0] ^= 1
+    res = bench.check_vs_oracle(snap, d, p)
+    assert not res["ok"]
+    assert res["checks"] == {"headline": True, "north_star_encode": False,
+                             "c3_reconstruct": False}
+    snap["headline"][0][2][4, 0] ^= 1
+    assert not bench.check_vs_oracle(snap, d, p)["checks"]["headline"]
+
+
+def test_node_figures_from_rank_rows():
+    rows = [[r, 0, 1, 64, 40.0 + r, 50.0, 55.0, 0.8, 0.74, 0.74 - 0.01 * r, 4e10, 7.0 + r,
+             14.0 + r, 21474836480, 40.0] for r in range(4)]
+    ranks = [bench.rank_row(r, row) for r, row in enumerate(rows)]
+    assert ranks[2]["c4_ms"] == 16.0 and ranks[3]["c3_reconstruct_frac"] == 0.71
+    node = bench.node_figures(ranks)
+    assert node["c4_encode_hash"]["data_bytes"] == 4 * 21474836480
+    assert node["c4_encode_hash"]["value"] == round(4 * 21474836480 / 0.017 / 1e9, 2)
+    assert node["c3_reconstruct"]["min_frac"] == 0.71
+    assert node["c3_reconstruct"]["achieved"] == round(4 * 4e10 / 0.010 / 1e9, 1)
+    assert node["min_north_star_encode_frac"] == 0.8
+    # a rank without the blocks (0 -> None): no node figure rather than a wrong one
+    rows[1][12] = 0
+    assert "c4_encode_hash" not in bench.node_figures(
+        [bench.rank_row(r, row) for r, row in enumerate(rows)])

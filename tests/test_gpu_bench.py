@@ -52,3 +52,40 @@ def test_reconstruct_config_line_small():
     assert line["check_vs_oracle"] is True
     assert line["roofline"]["kernel"] == "rs_apply_kernel(reconstruct_data)"
     assert line["kernels"]["also_reconstruct"]["ms"] > 0
+
+
+def test_default_line_checks_vs_oracle_small():
+    """The default line's oracle leg on its own buffers (headline fused kernel + north_star's
+    bit-sliced re-encode at this size; C3 / C4 parts join at full size)."""
+    line = _run("--parts", "64", "--steps", "1", "--warmup", "1", "--e2e-gib", "0")
+    assert line["check_vs_oracle"] is True
+    det = line["check_vs_oracle_detail"]["checks"]
+    assert det["headline"] is True and det["north_star_encode"] is True
+
+
+def test_end_to_end_read_repair_small():
+    """end_to_end at 3 GiB: the ring-fed write form and the read_repair form with 2 % damaged
+    fetches, every damaged chunk rejected and its part retried, nothing undecodable."""
+    line = _run("--parts", "64", "--steps", "1", "--warmup", "1", "--e2e-gib", "3",
+                "--no-north-star", "--no-cpu-baseline", "--corrupt", "0.02")
+    e2e = line["end_to_end"]
+    assert e2e["value"] > 0 and e2e["sampled_digest_matches_source"] is True
+    rr = e2e["read_repair"]
+    assert rr["value"] > 0 and rr["sampled_parts_equal_stored"] is True
+    assert rr["undecodable_parts"] == 0 and rr["retries"] > 0
+    assert rr["rejected_chunks"] == rr["damaged_loads"] > 0
+    assert any(c["attempts"] > 1 for c in rr["checks"])
+
+
+def test_stream_configs_small():
+    """C5 and its verify/repair side at 4 GiB, fed from the pageable rings inside the timed
+    region."""
+    line = _run("--config", "c5", "--stream-gib", "4")
+    assert line["check_digests_vs_source"] is True and line["value"] > 0
+    assert line["config"]["stream_bytes"] == (4 << 30) // (10 << 20) * (10 << 20)
+    line = _run("--config", "c5r", "--stream-gib", "4", "--corrupt", "0.02")
+    rr = line["read_repair"]
+    assert line["check_vs_stored"] is True and line["value"] > 0
+    assert rr["undecodable_parts"] == 0 and rr["retried_parts"] > 0
+    assert rr["rejected_chunks"] == rr["damaged_loads"] > 0
+    assert rr["parts"] == (4 << 30) // (10 << 20)

@@ -48,9 +48,16 @@ def _worker(rank, world, port, n_parts, out_q):
         ok_one_fails = all_ranks_ok(rank != world - 1, world)
         # bench.py's per-rank array: each rank's own row, in rank order, on every rank
         rows = gather_rows([rank, 10.0 * rank + 0.5, hi - lo], world)
+        # bench.py's N > 1 line: each rank's C3 / C4 figures in the RANK_FIELDS row, the node's
+        # configs[2] / configs[3] figures computed from the gathered rows on every rank
+        import bench
+        row = [rank, 0, 1, 8, 40.0, 50.0, 55.0, 0.8, 0.74, 0.7 + 0.01 * rank, 1e9 * (rank + 1),
+               5.0 + rank, 10.0 + rank, (rank + 1) * 1e9, 30.0]
+        node = bench.node_figures([bench.rank_row(r, x) for r, x in
+                                   enumerate(gather_rows(row, world))])
         gathered = [None] * world
         dist.all_gather_object(gathered, res)
-        out_q.put((rank, t, gathered, ok_all, ok_one_fails, rows))
+        out_q.put((rank, t, gathered, ok_all, ok_one_fails, rows, node))
     finally:
         dist.destroy_process_group()
 
@@ -81,7 +88,13 @@ def test_gloo_sharding_matches_single_process(world):
         pr.join(timeout=60)
         assert pr.exitcode == 0
     single = {k: _part_digests(k, 3, 2, 257) for k in range(n_parts)}
-    for rank, t, gathered, ok_all, ok_one_fails, rows in results:
+    for rank, t, gathered, ok_all, ok_one_fails, rows, node in results:
+        # node C4 = all ranks' data over the slowest rank's time; C3 min frac = rank 0's
+        c4 = node["c4_encode_hash"]
+        assert c4["data_bytes"] == sum((r + 1) * 1e9 for r in range(world))
+        assert c4["max_ms"] == 10.0 + world - 1
+        assert c4["value"] == round(c4["data_bytes"] / ((10.0 + world - 1) / 1e3) / 1e9, 2)
+        assert node["c3_reconstruct"]["min_frac"] == 0.7 and node["ranks"] == world
         assert t == pytest.approx(0.5 * world)  # max over ranks of (rank+1)*0.5
         assert ok_all and not ok_one_fails
         assert rows == [[float(r), 10.0 * r + 0.5,
