@@ -74,6 +74,8 @@ _sig("cec_status_name", [ctypes.c_int], ctypes.c_char_p)
 _sig("cec_last_error", [], ctypes.c_char_p)
 _sig("cec_device_count", [])
 _sig("cec_build_info", [], ctypes.c_char_p)
+_sig("cec_reload_knobs", [], None)
+_sig("cec_release_cached", [ctypes.c_int], ctypes.c_size_t)
 _sig("cec_codec_cached_patterns", [_vp], ctypes.c_size_t)
 _sig("cec_codec_new", [ctypes.c_size_t, ctypes.c_size_t, ctypes.POINTER(_vp)])
 _sig("cec_codec_free", [_vp], None)
@@ -208,6 +210,18 @@ def device_count() -> int:
 
 def build_info() -> str:
     return _lib.cec_build_info().decode()
+
+
+def reload_knobs() -> None:
+    """Re-read the CEC_* environment knobs (test-only: the library reads them once per
+    process, cec_reload_knobs)."""
+    _lib.cec_reload_knobs()
+
+
+def release_cached(device: int = -1) -> int:
+    """Free the idle per-call staging on `device` (every device when < 0); returns the device
+    bytes released (cec_release_cached)."""
+    return _lib.cec_release_cached(device)
 
 
 def status_name(code: int) -> str:

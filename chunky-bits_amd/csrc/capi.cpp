@@ -27,6 +27,7 @@
 #include "gf256.hpp"
 #include "hostmem.hpp"
 #include "kernels.hpp"
+#include "knobs.hpp"
 
 using namespace cec;
 
@@ -211,7 +212,8 @@ int upload_words(const std::vector<uint32_t>& words, hipStream_t s, Scratch& sc,
 // bounded per-device pool (not thread_local: the reference calls the crate from tokio's
 // blocking pool, whose threads come and go, file_part.rs:128,161 / any.rs:19-24, so per-thread
 // resources would leak with every retired thread).  At most kMaxIdleCtx contexts per device
-// stay alive between calls, holding at most kMaxIdleBytes of device buffers together.
+// stay alive between calls, holding at most CEC_IDLE_STAGING_MIB (default 1 GiB) of device
+// buffers together; cec_release_cached() frees the idle ones.
 // ------------------------------------------------------------------------------------------
 struct StageCtx {
     int device = 0;
@@ -246,10 +248,10 @@ int ctx_reserve(StageCtx& c, size_t device_bytes) {
 }
 
 constexpr size_t kMaxIdleCtx = 8;
-// Device bytes idle contexts may hold per device.  Bounding the total (not each buffer) keeps a
+// Device bytes idle contexts may hold per device (knobs().idle_staging_bytes, the
+// CEC_IDLE_STAGING_MIB knob, default 1 GiB).  Bounding the total (not each buffer) keeps a
 // steady stream of large per-call requests (e.g. RS(10,4) at 8 MiB chunks: 112 MiB per part)
 // from paying a hipMalloc + a device-synchronizing hipFree on every call.
-constexpr size_t kMaxIdleBytes = size_t(1) << 30;
 
 class CtxPool {
    public:
@@ -284,7 +286,7 @@ class CtxPool {
             auto& v = idle_[c->device];
             if (v.size() < kMaxIdleCtx) {
                 size_t& held = idle_bytes_[c->device];
-                if (held + c->dcap <= kMaxIdleBytes) {
+                if (held + c->dcap <= knobs().idle_staging_bytes) {
                     held += c->dcap;
                     v.push_back(std::move(c));
                     return;
@@ -301,6 +303,31 @@ class CtxPool {
         auto& v = idle_[c->device];
         if (v.size() < kMaxIdleCtx) v.push_back(std::move(c));
         // (else another thread filled the pool meanwhile: c's stream is destroyed with it)
+    }
+
+    // Destroys the idle contexts of `device` (every device if < 0): their streams and device
+    // buffers are freed; leased contexts are untouched.  Returns the device bytes released.
+    size_t trim(int device) {
+        std::vector<std::unique_ptr<StageCtx>> out;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            for (auto& [dev, v] : idle_) {
+                if (device >= 0 && dev != device) continue;
+                for (auto& c : v) out.push_back(std::move(c));
+                v.clear();
+                idle_bytes_[dev] = 0;
+            }
+        }
+        size_t bytes = 0;
+        int cur = 0;
+        const bool have_cur = hipGetDevice(&cur) == hipSuccess;
+        for (auto& c : out) {
+            bytes += c->dcap;
+            if (hipSetDevice(c->device) == hipSuccess) c->destroy();
+            (void)hipGetLastError();
+        }
+        if (have_cur) (void)hipSetDevice(cur);
+        return bytes;
     }
 
    private:
@@ -541,10 +568,8 @@ int reconstruct_host(const cec_codec* cc, uint8_t* const* shards, const size_t* 
 // 42 ms per MiB) wins while the encode's extra pass is negligible.  CEC_FUSED (A/B knob): 0 =
 // always separate, 1 = always fused where supported.
 bool prefer_fused(size_t chunks) {
-    const char* e = std::getenv("CEC_FUSED");
-    if (e && e[0] == '0') return false;
-    if (e && e[0] == '1') return true;
-    return !use_split(chunks);
+    const int f = knobs().fused;
+    return f >= 0 ? f == 1 : !use_split(chunks);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -568,27 +593,11 @@ bool prefer_fused(size_t chunks) {
 // ------------------------------------------------------------------------------------------
 std::atomic<uint64_t> g_calls{0}, g_launches{0};
 
-uint32_t coalesce_window_us() {
-    static const uint32_t us = [] {
-        const char* e = std::getenv("CEC_COALESCE_US");
-        return e ? uint32_t(std::strtoul(e, nullptr, 10)) : 200u;
-    }();
-    return us;
-}
+uint32_t coalesce_window_us() { return knobs().coalesce_us; }
 
-size_t coalesce_max_bytes() {
-    static const size_t b = [] {
-        const char* e = std::getenv("CEC_COALESCE_MAX_MIB");
-        const size_t mib = e ? size_t(std::strtoull(e, nullptr, 10)) : 1024;
-        return std::max<size_t>(mib, 1) << 20;
-    }();
-    return b;
-}
+size_t coalesce_max_bytes() { return knobs().coalesce_max_bytes; }
 
-bool coalesce_trace() {
-    static const bool on = std::getenv("CEC_COALESCE_TRACE") != nullptr;
-    return on;
-}
+bool coalesce_trace() { return knobs().coalesce_trace; }
 
 // Pinned host staging, never shrunk.  Pinning costs ~0.35 s per GiB, so the first growth
 // past 64 MiB goes straight to the batch cap (one pinning per process, not one per size step).
@@ -619,24 +628,16 @@ struct Arena {
     hipEvent_t encoded = nullptr;
 };
 
-// How the early parity download waits for the encode: on the device (the side stream waits on
-// the encode's event, default) or on the host (the leader blocks on the event, then queues the
-// copy: CEC_COALESCE_D2H_WAIT=host, the round-2 form, kept for the A/B).  Both are deadlock-free
-// (see the wait itself); which is faster is a measurement.
-bool coalesce_d2h_host_wait() {
-    static const bool host = [] {
-        const char* e = std::getenv("CEC_COALESCE_D2H_WAIT");
-        return e && std::strcmp(e, "host") == 0;
-    }();
-    return host;
-}
+// How the early parity download waits for the encode: on the host (the leader blocks on the
+// event, then queues the copy: the default, round 2's form, adopted after a 256-caller hang on
+// an earlier device-side form) or on the device (the side stream waits on the encode's event:
+// CEC_COALESCE_D2H_WAIT=device, kept for the A/B).  Both are deadlock-free (see the wait
+// itself), and DESIGN.md §4.7's A/B put them within run-to-run spread, so the default is the
+// form with the longer record.
+bool coalesce_d2h_host_wait() { return knobs().coalesce_d2h_host_wait; }
 
 bool coalesce_early_d2h() {  // default on (profiles/r2_early_d2h/); =0 for A/B
-    static const bool on = [] {
-        const char* e = std::getenv("CEC_COALESCE_EARLY_D2H");
-        return !(e && e[0] == '0');
-    }();
-    return on;
+    return knobs().coalesce_early_d2h;
 }
 
 struct CoalesceKey {
@@ -681,22 +682,9 @@ struct Batch {
 // profiles/r1y_percall_ab.log).  Overflowing callers (256 pageable parts vs a 1 GiB cap) then
 // copy in while the first batch runs: 13.9 -> ~26 GB/s (profiles/r2_percall/).
 // CEC_COALESCE_ADAPT=0 (A/B knob): fixed CEC_COALESCE_US window, no early exit.
-bool coalesce_adaptive() {
-    static const bool on = [] {
-        const char* e = std::getenv("CEC_COALESCE_ADAPT");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
+bool coalesce_adaptive() { return knobs().coalesce_adaptive; }
 
-uint32_t coalesce_inflight() {
-    static const uint32_t n = [] {
-        const char* e = std::getenv("CEC_COALESCE_INFLIGHT");
-        const unsigned long v = e ? std::strtoul(e, nullptr, 10) : 2ul;
-        return uint32_t(std::min<unsigned long>(std::max<unsigned long>(v, 1ul), 16ul));
-    }();
-    return n;
-}
+uint32_t coalesce_inflight() { return knobs().coalesce_inflight; }
 
 template <typename Req, typename Impl>
 class Coalescer {
@@ -994,13 +982,7 @@ struct PartReq : ReqBase {
     CoalesceKey key() const { return {codec, L, device}; }
 };
 
-bool coalesce_early_h2d() {
-    static const bool on = [] {
-        const char* e = std::getenv("CEC_COALESCE_EARLY_H2D");
-        return e && e[0] == '1';
-    }();
-    return on;
-}
+bool coalesce_early_h2d() { return knobs().coalesce_early_h2d; }
 
 // Pinned layout: input [part][d][cs] (staged parts only, at in_off), output [part][p][cs]
 // (staged parts only, at out_off) then digests [part][d+p][32]; device batch [part][d+p][cs]
@@ -1421,6 +1403,8 @@ void cec_coalesce_stats(uint64_t* calls, uint64_t* launches) {
     coalesce_stats(calls, launches);
 }
 
+size_t cec_release_cached(int device) { return ctx_pool().trim(device); }
+
 int cec_encode_batch(const cec_codec* cc, const cec_part_batch* b, void* stream) {
     if (!cc) return CEC_ERR_INVALID_ARGUMENT;
     CEC_TRY(batch_ok(b));
@@ -1575,6 +1559,16 @@ static int reconstruct_batch(const cec_codec* cc, const cec_part_batch* b, const
         a.n_parts = uint32_t(launches[i].count);
         a.d = uint32_t(d);
         a.n_rows = launches[i].n_out ? launches[i].n_out : var_rows;
+        if (!launches[i].n_out) {
+            // the shared launch's row class must cover every record it lists (the kernel skips
+            // a wider pattern without writing its chunks: kernels.hpp launch_rs_apply_var)
+            const uint32_t* pat_off = words.data() + launches[i].ids + launches[i].count;
+            for (size_t q = 0; q < launches[i].count; ++q)
+                if (words[pat_off[q]] == 0 || words[pat_off[q]] > a.n_rows) {
+                    g_last_error = "reconstruct_batch: a listed pattern is wider than its launch";
+                    return CEC_ERR_INVALID_ARGUMENT;
+                }
+        }
         a.lds_reserve = lds_reserve;
         hipError_t e = launches[i].n_out ? launch_rs_apply(a, vec, s)
                                          : launch_rs_apply_var(a, vec, s);
@@ -1697,16 +1691,10 @@ class SideLease {
 // RS(10,4), d loaded, tools/c3r_ab.sh): 43.2 ms vs 45.3 (65 KiB: two per free CU) vs 46.5 (none:
 // decode everywhere, done in 17 ms, but the SHA chains slow from 42.6 to 46.4 ms beside it) vs
 // 53.0 ms without speculation.
-uint32_t decode_lds() {
-    const char* e = std::getenv("CEC_SPEC_LDS_KIB");
-    return e ? uint32_t(std::atoi(e)) * 1024u : 100u * 1024u;
-}
+uint32_t decode_lds() { return knobs().spec_lds; }
 
 // CEC_READ_SPECULATE=0 (A/B knob): verify, wait, then decode from the verified chunks only.
-bool read_speculate() {
-    const char* e = std::getenv("CEC_READ_SPECULATE");
-    return !(e && e[0] == '0');
-}
+bool read_speculate() { return knobs().read_speculate; }
 
 // A loaded chunk is hashed unless the caller marked it CEC_PRESENT_VERIFIED (a read retry's
 // chunks that an earlier pass already verified).
@@ -1720,8 +1708,7 @@ inline bool needs_hash(uint8_t f) { return f != 0 && f != CEC_PRESENT_VERIFIED; 
 int verify_loaded(const cec_part_batch* b, size_t t, const uint8_t* present_host,
                   const uint8_t* expected, uint8_t* ok, hipStream_t s) {
     const size_t n = b->n_parts * t;
-    const char* knob = std::getenv("CEC_VERIFY_COMPACT");
-    if (knob && knob[0] == '0') {  // A/B: strided launch with the skipped lanes
+    if (!knobs().verify_compact) {  // A/B: strided launch with the skipped lanes
         std::vector<uint32_t> mask(n);  // chunks to hash: loaded, not already verified
         for (size_t i = 0; i < n; ++i) mask[i] = needs_hash(present_host[i]) ? 1u : 0u;
         std::vector<uint8_t> bytes(n);

@@ -24,6 +24,7 @@
 #include "gf256.hpp"
 #include "gf_device.hpp"
 #include "kernels.hpp"
+#include "knobs.hpp"
 #include "sha256_device.hpp"
 
 namespace cec {
@@ -432,8 +433,8 @@ hipError_t launch_p(const FusedParams& a, hipStream_t s) {
 // Wave priorities: 0 = none, 1 = encoder waves at s_setprio 1, 2 = SHA waves at s_setprio 1.
 // The build's default, or CEC_FUSED_PRIO=0/1/2 (dev knob, A/B).
 uint32_t fused_prio(uint32_t dflt) {
-    const char* e = std::getenv("CEC_FUSED_PRIO");
-    return e && (e[0] >= '0' && e[0] <= '2') ? uint32_t(e[0] - '0') : dflt;
+    const int v = knobs().fused_prio;
+    return v >= 0 ? uint32_t(v) : dflt;
 }
 
 // Byte order of the LDS ring (BE = encoders store big-endian words, the SHA waves skip their
@@ -442,22 +443,18 @@ uint32_t fused_prio(uint32_t dflt) {
 // wave (RS(10,4) build: C2 42.63 -> 42.97 ms), so it is on for ENC3 only.  CEC_FUSED_BE=0/1
 // overrides (A/B).
 bool fused_be(bool dflt) {
-    const char* e = std::getenv("CEC_FUSED_BE");
-    return e && (e[0] == '0' || e[0] == '1') ? e[0] == '1' : dflt;
+    const int v = knobs().fused_be;
+    return v >= 0 ? v == 1 : dflt;
 }
 
 // CEC_FUSED_ENC3=0 turns the SIMD-3 encoder placement of the two-SHA-wave build off (A/B).
-bool fused_enc3() {
-    const char* e = std::getenv("CEC_FUSED_ENC3");
-    return !(e && e[0] == '0');
-}
+bool fused_enc3() { return knobs().fused_enc3; }
 
 // CEC_FUSED_MODE: 3 = the generic-d build on every shape it covers (correct output; A/B and
 // tests against the shape builds).  Modes 1 and 2 (timing attribution, wrong outputs by design)
 // exist only in the A/B build (-DCEC_AB_TOOLS, `make ab`): the product library ignores them.
 int fused_mode() {
-    const char* e = std::getenv("CEC_FUSED_MODE");
-    const int m = e ? std::atoi(e) : 0;
+    const int m = knobs().fused_mode;
 #ifdef CEC_AB_TOOLS
     return m;
 #else

@@ -91,8 +91,11 @@ hipError_t launch_rs_encode(const ApplyParams& a, bool vec16, hipStream_t s);
 // Whether a codec's parity rows (p x d bytes, row-major) are those of a compiled bit-sliced
 // shape (the compile-time construction of gf_const.hpp, compared byte for byte).
 bool bs_encode_matches(uint32_t d, uint32_t p, const uint8_t* parity_rows);
-// Listed parts whose patterns carry their own row count (1..max_var_rows()), one launch;
-// a.n_rows is ignored.
+// Listed parts whose patterns carry their own row count (1..max_var_rows()), one launch.
+// a.n_rows selects the kernel's row class (2, 4 or 8 rows) and MUST be at least the widest
+// listed pattern's row count, or 0 (unknown: the 8-row class); a pattern wider than its class is
+// skipped in the kernel (its chunks are not written).  The caller (capi.cpp reconstruct_batch)
+// checks this against the host records before every launch.
 hipError_t launch_rs_apply_var(const ApplyParams& a, bool vec16, hipStream_t s);
 uint32_t max_var_rows();
 bool fused_supported(uint32_t d, uint32_t p);

@@ -34,6 +34,7 @@
 
 #include "chunky_ec.h"
 #include "hostmem.hpp"
+#include "knobs.hpp"
 
 namespace {
 
@@ -103,14 +104,7 @@ struct Staging {
 
 // Host threads per shard for its staging copies (CEC_MULTI_COPY_THREADS, default 4): one
 // thread's memcpy (~10 GB/s) is below the ~55 GB/s a GPU's PCIe link takes.
-size_t copy_threads() {
-    static const size_t n = [] {
-        const char* e = std::getenv("CEC_MULTI_COPY_THREADS");
-        const long v = e ? std::atol(e) : 4;
-        return size_t(std::min<long>(std::max<long>(v, 1), 32));
-    }();
-    return n;
-}
+size_t copy_threads() { return cec::knobs().multi_copy_threads; }
 
 // fn(i) for i in [0, n) split in contiguous ranges over copy_threads() threads (inline when the
 // work is small).

@@ -22,15 +22,11 @@
 #include "chunky_ec.h"
 #include "hostmem.hpp"
 #include "kernels.hpp"
+#include "knobs.hpp"
 
 namespace {
 
 thread_local std::string g_pipe_error;
-
-bool env_flag(const char* name, bool dflt) {
-    const char* v = std::getenv(name);
-    return v && *v ? std::strcmp(v, "0") != 0 : dflt;
-}
 
 int pipe_fail(hipError_t e, const char* what) {
     g_pipe_error = std::string(what) + ": " + hipGetErrorString(e);
@@ -654,8 +650,8 @@ int cec_read_pipeline_new_ex(const cec_codec* codec, size_t chunk_len, size_t pa
     pl->external = (flags & CEC_PIPE_EXTERNAL) != 0;
     pl->resilver = (flags & CEC_READ_RESILVER) != 0;
     pl->verify_only = (flags & CEC_READ_VERIFY_ONLY) != 0;
-    pl->side_decode = env_flag("CEC_READ_SIDE", false);
-    pl->shared_upload = env_flag("CEC_READ_UPSTREAM", false);
+    pl->side_decode = cec::knobs().read_side;
+    pl->shared_upload = cec::knobs().read_upstream;
     pl->slots.resize(depth);
     const size_t P = pl->parts, t = pl->t;
     for (ReadSlot& s : pl->slots) {

@@ -21,6 +21,7 @@
 // (every byte is touched once), blocks in an XCD-aware order, and on large grids a residency cap
 // of 2-3 blocks per CU (apply_lds).  RS(10,4) encode streams 6.40 TB/s and 2-erasure
 // reconstruct_data 5.96 TB/s.
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <type_traits>
@@ -30,6 +31,7 @@
 #include "gf_const.hpp"
 #include "gf_device.hpp"
 #include "kernels.hpp"
+#include "knobs.hpp"
 
 namespace cec {
 namespace {
@@ -312,7 +314,8 @@ template <int RG, int MAXRG, typename F>
 __device__ __forceinline__ void rg_dispatch(uint32_t n, F&& f) {
     if (n == RG) f(std::integral_constant<int, RG>{});
     else if constexpr (RG < MAXRG) rg_dispatch<RG + 1, MAXRG>(n, f);
-    // n > MAXRG or 0: never listed (the host routes n_out > 8 to row-group launches)
+    // n > MAXRG or 0: never listed -- the host routes n_out > 8 to row-group launches and checks
+    // every listed record against the launch's row class (capi.cpp reconstruct_batch)
 }
 
 template <bool VEC, int GROUP, int V, bool NT, int MAXRG, int CD = 0, int CDG = 0>
@@ -550,23 +553,43 @@ __global__ __launch_bounds__(256) void fill_kernel(FillParams a, bool aligned8) 
     }
 }
 
-// CEC_APPLY_TUNE (tuning knob, read per launch; unset = "nt"): "nt" = non-temporal loads and
+// CEC_APPLY_TUNE (tuning knob, latched once: knobs.hpp; unset = "nt"): "nt" = non-temporal loads and
 // stores, "v1" = one 16-byte column per lane per step instead of two, "g8" = 8 inputs in
 // flight per lane instead of 4; any other string = plain loads, two columns, groups of 4.
 // Measured on C2 encode (tools/apply_ab.py, MI355X): nt 10.79 ms, plain 11.20, v1 11.25,
 // v1+nt 11.15, g8 11.26, nt+g8 10.85.
-int apply_tune() {
-    const char* e = std::getenv("CEC_APPLY_TUNE");
-    if (!e) return 1;
-    return (std::strstr(e, "nt") ? 1 : 0) | (std::strstr(e, "g8") ? 2 : 0) |
-           (std::strstr(e, "v1") ? 4 : 0);
-}
+int apply_tune() { return knobs().apply_tune; }
 
-// CEC_APPLY_XCD (A/B knob, read per launch; unset = 1): 0 launches the apply kernels' blocks in
+// CEC_APPLY_XCD (A/B knob; unset = 1): 0 launches the apply kernels' blocks in
 // plain launch order instead of the XCD-aware order (xcd_block).
-bool apply_xcd() {
-    const char* e = std::getenv("CEC_APPLY_XCD");
-    return !(e && e[0] == '0');
+bool apply_xcd() { return knobs().apply_xcd; }
+
+// LDS of one CU on the current device, cached per device: 160 KiB on gfx950 (MI355X), else
+// what the runtime reports (hipDeviceAttributeMaxSharedMemoryPerMultiprocessor); 0 when
+// unknown, which turns the residency caps below off rather than mis-sizing them.
+uint32_t lds_per_cu() {
+    static std::atomic<uint32_t> cache[64];  // 0 = not read yet, 1 = unknown
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    uint32_t v = cache[dev].load(std::memory_order_relaxed);
+    if (!v) {
+        hipDeviceProp_t prop;
+        int attr = 0;
+        if (hipGetDeviceProperties(&prop, dev) == hipSuccess &&
+            std::strncmp(prop.gcnArchName, "gfx950", 6) == 0)
+            v = 160u * 1024u;
+        else if (hipDeviceGetAttribute(&attr, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor,
+                                       dev) == hipSuccess && attr > 0)
+            v = uint32_t(attr);
+        else
+            v = 1;
+        (void)hipGetLastError();
+        cache[dev].store(v, std::memory_order_relaxed);
+    }
+    return v == 1 ? 0 : v;
 }
 
 // Residency cap.  The GF kernels stream 10-28 chunks per part 1 MiB (chunk stride) apart, and on
@@ -578,35 +601,33 @@ bool apply_xcd() {
 // per CU), on top of any the caller asked for, and only for grids of at least kCapMinBlocks
 // blocks (the device-resident batches it was measured on; the host pipelines' 256-part batches
 // share the chip with SHA-256 kernels and keep the register-bound occupancy).
-// CEC_APPLY_BLOCKS_PER_CU (A/B knob, read per launch): n > 0 caps every apply launch at n blocks
+// CEC_APPLY_BLOCKS_PER_CU (A/B knob): n > 0 caps every apply launch at n blocks
 // per CU, 0 turns the cap off; unset = the per-kernel default `def_cap` (0 = none).
 constexpr uint64_t kCapMinBlocks = 65536;
 uint32_t apply_lds(uint32_t reserve, int def_cap, uint64_t n_blocks) {
-    const char* e = std::getenv("CEC_APPLY_BLOCKS_PER_CU");
-    int n = e ? std::atoi(e) : (n_blocks >= kCapMinBlocks ? def_cap : 0);
-    if (n <= 0 || n > 16) return reserve;
-    const uint32_t lds = 163840u / uint32_t(n + 1) + 2048u;  // floor(160 KiB / lds) == n
+    const int knob = knobs().apply_blocks_per_cu;
+    const int n = knob >= 0 ? knob : (n_blocks >= kCapMinBlocks ? def_cap : 0);
+    const uint32_t cu_lds = lds_per_cu();
+    if (n <= 0 || n > 16 || cu_lds == 0) return reserve;
+    // floor(cu_lds / lds) == n; a cap the part's LDS cannot express (lds above the per-launch
+    // maximum, 64 KiB parts at n = 1) is dropped rather than failing the launch
+    const uint32_t lds = cu_lds / uint32_t(n + 1) + 2048u;
+    if (lds > cu_lds) return reserve;
     return std::max(reserve, lds);
 }
 
-// CEC_APPLY_RGCLS (A/B knob, read per launch; unset = 1): 0 runs every reconstruct batch on the
+// CEC_APPLY_RGCLS (A/B knob; unset = 1): 0 runs every reconstruct batch on the
 // var kernel compiled for 8 rows instead of the batch's row class (2, 4 or 8).
-bool apply_rg_classes() {
-    const char* e = std::getenv("CEC_APPLY_RGCLS");
-    return !(e && e[0] == '0');
-}
+bool apply_rg_classes() { return knobs().apply_rg_classes; }
 
-// CEC_APPLY_CD (A/B knob, read per launch; unset = 1): for d == 10 reconstruct batches, the
+// CEC_APPLY_CD (A/B knob; unset = 1): for d == 10 reconstruct batches, the
 // compile-time-d var kernel (apply_tile_cd, loads 5 inputs ahead); 0 = the run-time-d kernel.
 // Interleaved on one box with the residency caps (profiles/r3_cap_ab/): c3e2 8.07-8.09 vs
 // 8.12-8.14 ms, C3 9.64-9.68 vs 9.71-9.75 (groups of 2 and 10 measured the same as 5 without
 // the caps, profiles/r3_cd_ab/).
-bool apply_cd() {
-    const char* e = std::getenv("CEC_APPLY_CD");
-    return !(e && e[0] == '0');
-}
+bool apply_cd() { return knobs().apply_cd; }
 
-// CEC_APPLY_TILE (A/B knob, read per launch): bytes of one part's column range per block, a
+// CEC_APPLY_TILE (A/B knob): bytes of one part's column range per block, a
 // multiple of 8 KiB (one full two-column step of a block) up to 256 KiB; default `def`:
 // kApplyTile for rs_apply_kernel, kBsTile for the bit-sliced encoder and the mixed-pattern
 // reconstruct.  Measured interleaved on one box with the residency caps
@@ -615,8 +636,7 @@ bool apply_cd() {
 // profiles/r3_tile2_ab/.)
 constexpr uint64_t kBsTile = 8192;
 uint64_t apply_tile_bytes(uint64_t def = kApplyTile) {
-    const char* e = std::getenv("CEC_APPLY_TILE");
-    const unsigned long long v = e ? std::strtoull(e, nullptr, 10) : 0ull;
+    const uint64_t v = knobs().apply_tile;
     return v && v % 8192 == 0 && v <= (256u << 10) ? v : def;
 }
 
@@ -656,11 +676,10 @@ bool allow_lds(K kernel, uint32_t bytes) {
 // kApplyThreads per block, at most this many blocks.  Larger batches (many parts of long chunks,
 // e.g. 4096 x 64 MiB) are split over several launches of whole parts.
 constexpr uint64_t kMaxApplyBlocks = 0xFFFFFFFFull / kApplyThreads;
-// CEC_APPLY_MAX_BLOCKS (test knob, read per launch) lowers the limit so the split is exercised
+// CEC_APPLY_MAX_BLOCKS (test knob) lowers the limit so the split is exercised
 // at test sizes; results are identical either way.
 uint64_t max_apply_blocks() {
-    const char* e = std::getenv("CEC_APPLY_MAX_BLOCKS");
-    const unsigned long long v = e ? std::strtoull(e, nullptr, 10) : 0ull;
+    const uint64_t v = knobs().apply_max_blocks;
     return v ? std::min<uint64_t>(v, kMaxApplyBlocks) : kMaxApplyBlocks;
 }
 
@@ -722,12 +741,9 @@ hipError_t launch_rows(const ApplyParams& a, uint32_t rg, uint32_t row_base, uin
     }
 }
 
-// CEC_APPLY_BS (A/B knob, read per launch; unset = 1): 0 sends the compiled shapes' encodes to
+// CEC_APPLY_BS (A/B knob; unset = 1): 0 sends the compiled shapes' encodes to
 // the v_perm kernel too.
-bool apply_bs() {
-    const char* e = std::getenv("CEC_APPLY_BS");
-    return !(e && e[0] == '0');
-}
+bool apply_bs() { return knobs().apply_bs; }
 
 template <int D, int P>
 hipError_t launch_bs(const ApplyParams& a, hipStream_t s) {

@@ -25,6 +25,7 @@
 
 #include "device_common.hpp"
 #include "kernels.hpp"
+#include "knobs.hpp"
 #include "sha256_device.hpp"
 
 namespace cec {
@@ -528,8 +529,7 @@ hipError_t launch_split5(const ShaParams& a, hipStream_t s) {
 // experiment kernels 3-5, 7, 8 (7/8 timing attribution with wrong outputs by design) exist only
 // in the A/B build (-DCEC_AB_TOOLS): the product library treats them as unset.
 int sha_variant() {
-    const char* e = std::getenv("CEC_SHA_VARIANT");
-    const int v = e ? std::atoi(e) : 0;
+    const int v = knobs().sha_variant;
 #ifdef CEC_AB_TOOLS
     return v;
 #else

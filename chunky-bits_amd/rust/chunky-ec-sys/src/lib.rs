@@ -8,6 +8,8 @@
 //! available (not in the build container — see DESIGN.md).
 use std::os::raw::{c_int, c_void};
 
+pub mod batch;
+
 pub mod sys {
     use super::*;
 
@@ -337,6 +339,8 @@ pub mod sys {
             stream: *mut c_void,
         ) -> c_int;
         pub fn cec_synth_byte(seed: u64, part: u64, chunk: u64, offset: u64) -> u8;
+        pub fn cec_reload_knobs();
+        pub fn cec_release_cached(device: c_int) -> usize;
     }
 }
 
@@ -1047,4 +1051,39 @@ impl Multi {
         check_multi(unsafe { sys::cec_multi_wait(self.raw, job) })?;
         Ok(status.into_iter().map(check).collect())
     }
+
+    /// Asynchronous [`Multi::encode_hash`]: queues the job and returns its id for
+    /// [`Multi::wait`], so the caller can fill its next window while this one runs.
+    ///
+    /// # Safety
+    /// `data` (`n_parts * d * L` bytes), `parity` (`n_parts * p * L`) and `digests`
+    /// (`n_parts * (d + p) * 32`) must stay valid, and `data` unmodified, until the job has been
+    /// waited for.
+    pub unsafe fn submit_encode_hash(
+        &self,
+        data: *const u8,
+        n_parts: usize,
+        parity: *mut u8,
+        digests: *mut u8,
+    ) -> Result<u64, CecError> {
+        let mut job = 0u64;
+        check_multi(sys::cec_multi_encode_hash(self.raw, data, n_parts, parity, digests, &mut job))?;
+        Ok(job)
+    }
+
+    /// Waits for a job queued with [`Multi::submit_encode_hash`].
+    pub fn wait(&self, job: u64) -> Result<(), CecError> {
+        check_multi(unsafe { sys::cec_multi_wait(self.raw, job) })
+    }
+}
+
+/// Visible HIP devices (0 when none; never fails).
+pub fn device_count() -> c_int {
+    unsafe { sys::cec_device_count() }
+}
+
+/// Frees the engine's idle per-call staging on `device` (every device when < 0); returns the
+/// device bytes released (`cec_release_cached`).
+pub fn release_cached(device: c_int) -> usize {
+    unsafe { sys::cec_release_cached(device) }
 }

@@ -94,6 +94,18 @@ int cec_device_numa_node(int device);
  * ab_tools=0: the timing-attribution kernels (wrong outputs by design) exist only in the
  * separate A/B build used by tools/ (DESIGN.md §6.1). */
 const char* cec_build_info(void);
+/* Environment knobs (CEC_APPLY_*, CEC_FUSED*, CEC_SHA_VARIANT, CEC_COALESCE_*, CEC_READ_*, ...;
+ * DESIGN.md §4) are read ONCE, on the first call that needs one, into an immutable snapshot;
+ * no launch path calls getenv (the reference drives the hot path from tokio worker threads,
+ * where getenv racing a setenv is undefined behaviour).  Test-only: re-read them now (a test
+ * that sets a knob calls this after setting it and again after restoring it).  No Rust binding
+ * is needed for the reference's calls. */
+void cec_reload_knobs(void);
+/* Frees the engine's idle per-call staging (stream + device buffer contexts kept between
+ * cec_encode_sep / cec_part_encode / ... calls: at most 8 per device holding at most
+ * CEC_IDLE_STAGING_MIB, default 1024, of HBM) on `device`, or on every device when device < 0.
+ * Staging leased by calls in progress is untouched.  Returns the device bytes released. */
+size_t cec_release_cached(int device);
 
 /* ---------------------------------------------------------------------------------------- */
 /* Codec: ReedSolomon<galois_8::Field>                                                       */

@@ -806,10 +806,11 @@ struct FileReference {
                     missing = missing || !w.verified[q * t + i];
                 }
                 if (!resilver || !missing) continue;
-                if (w.status[q] != CEC_OK) {  // this part's write_error; the others go on
-                    rep.write_error = Error::TooFewShardsPresent;
+                if (w.status[q] == CEC_TOO_FEW_SHARDS_PRESENT) {  // this part's write_error;
+                    rep.write_error = Error::TooFewShardsPresent;  // the others go on
                     continue;
                 }
+                detail::check(w.status[q]);  // any other failure is itself, as per part
                 const FilePart& part = parts[k0 + w.first + q];
                 for (size_t i = 0; i < t; ++i) {
                     if (w.verified[q * t + i]) continue;

@@ -26,3 +26,24 @@ def kats():
     import json
     with open(os.path.join(ROOT, "tests", "golden", "crate_kats.json")) as f:
         return json.load(f)
+
+
+@pytest.fixture
+def knob_env(monkeypatch):
+    """Sets CEC_* engine knobs for one test.  The library reads its knobs once per process
+    (cec_reload_knobs, include/chunky_ec.h), so every change reloads them, and teardown restores
+    the environment and reloads again."""
+    import chunky_ec as ce
+
+    class _KnobEnv:
+        def set(self, name, value):
+            monkeypatch.setenv(name, value)
+            ce.reload_knobs()
+
+        def delenv(self, name):
+            monkeypatch.delenv(name, raising=False)
+            ce.reload_knobs()
+
+    yield _KnobEnv()
+    monkeypatch.undo()
+    ce.reload_knobs()

@@ -181,3 +181,19 @@ def test_part_encode_rejects_length_past_data_buf():
     rs = ce.ReedSolomon(3, 2)
     with pytest.raises(ValueError):
         ce.part_encode(rs, b"abcdef", 7)
+
+
+def test_knobs_are_read_once_not_per_launch():
+    """Every CEC_* knob is parsed in knobs.cpp into a snapshot (cec_reload_knobs re-reads it,
+    test-only); no other engine source calls getenv, so a launch from a tokio worker never races
+    a setenv elsewhere in the host process."""
+    csrc = os.path.join(ROOT, "chunky-bits_amd", "csrc")
+    offenders = []
+    for name in sorted(os.listdir(csrc)):
+        if name.endswith((".cpp", ".hip", ".hpp")) and name != "knobs.cpp":
+            src = re.sub(r"//[^\n]*", "", open(os.path.join(csrc, name)).read())
+            if "getenv" in src:
+                offenders.append(name)
+    assert not offenders, offenders
+    import chunky_ec as ce
+    ce.reload_knobs()  # host-only: parses the environment, touches no device

@@ -441,13 +441,13 @@ def test_many_short_lived_threads_do_not_leak_device_memory():
     assert free0 - free1 <= (32 << 20), (free0 - free1)
 
 
-def test_product_build_ignores_attribution_modes(monkeypatch):
+def test_product_build_ignores_attribution_modes(knob_env):
     assert "ab_tools=0" in ce.build_info()
     d, p, L, n = 10, 4, 4096, 20
     for knob, val in [("CEC_FUSED_MODE", "1"), ("CEC_FUSED_MODE", "2"), ("CEC_SHA_VARIANT", "7"),
                       ("CEC_SHA_VARIANT", "8")]:
-        monkeypatch.setenv(knob, val)
-        monkeypatch.setenv("CEC_FUSED", "1")
+        knob_env.set(knob, val)
+        knob_env.set("CEC_FUSED", "1")
         buf = torch.zeros((n, d + p, L), dtype=torch.uint8, device="cuda:0")
         batch = ce.PartBatch.from_tensor(buf, L)
         ce.fill_synthetic(batch, d, 3)
@@ -456,7 +456,7 @@ def test_product_build_ignores_attribution_modes(monkeypatch):
         torch.cuda.synchronize()
         host, hd = buf.cpu().numpy(), dig.cpu().numpy()
         _check_write(host[:, :d], host[:, d:], hd, d, p)
-        monkeypatch.delenv(knob)
+        knob_env.delenv(knob)
 
 
 def test_decode_cache_is_bounded_lru():
@@ -691,13 +691,13 @@ def test_read_pipeline_resilver_flag_vs_oracle():
 
 @pytest.mark.parametrize("knobs", [{"CEC_READ_SIDE": "1"}, {"CEC_READ_UPSTREAM": "1"},
                                    {"CEC_READ_SIDE": "1", "CEC_READ_UPSTREAM": "1"}])
-def test_read_pipeline_stream_knobs_bit_exact(monkeypatch, knobs):
+def test_read_pipeline_stream_knobs_bit_exact(knob_env, knobs):
     """The read pipeline's A/B stream layouts (decode + rebuilt downloads on a side stream; every
     upload on one shared stream; both) are in the product library: read, packed read and
     resilver batches under each must give the default's results (oracle / written bytes)."""
     import test_gpu_parity as tp
     for k, v in knobs.items():
-        monkeypatch.setenv(k, v)  # read when a pipeline is created
+        knob_env.set(k, v)  # read when a pipeline is created
     for flags in (0, ce.ReadPipeline.REBUILT_ONLY):
         tp.test_read_pipeline_matches_read_with_context(10, 4, 4096, 12, 3, 5, flags)
         tp.test_read_pipeline_packed_submit(10, 4, 4096, 12, 3, 5, flags, True)

@@ -46,8 +46,8 @@ def test_sha256_reference_and_fips_kats(kats):
 
 
 @pytest.mark.parametrize("variant", ["", "1", "2"])  # by size (split here), lane, split
-def test_sha256_many_lengths_vs_hashlib(variant, monkeypatch):
-    monkeypatch.setenv("CEC_SHA_VARIANT", variant)
+def test_sha256_many_lengths_vs_hashlib(variant, knob_env):
+    knob_env.set("CEC_SHA_VARIANT", variant)
     lens = [0, 1, 2, 3, 15, 16, 17, 55, 56, 57, 63, 64, 65, 111, 112, 119, 120, 127, 128, 129,
             191, 192, 683, 1000, 1023, 1024, 4097, 65539, 699051, 1 << 20]
     bufs = [gen_bytes(900 + n, n).tobytes() for n in lens]
@@ -362,8 +362,8 @@ def test_encode_hash_batch_vs_oracle(d, p, L, cstride):
 
 
 @pytest.mark.parametrize("variant", ["1", "2"])
-def test_sha256_batch_subrange(variant, monkeypatch):
-    monkeypatch.setenv("CEC_SHA_VARIANT", variant)
+def test_sha256_batch_subrange(variant, knob_env):
+    knob_env.set("CEC_SHA_VARIANT", variant)
     d, p, L = 4, 2, 5000
     buf, batch = _device_parts(8, d + p, L, 5008, seed=5)
     dig = torch.zeros((8, 3, 32), dtype=torch.uint8, device=DEV)
@@ -571,15 +571,15 @@ def test_full_size_encode_erase_reconstruct_roundtrip(d, p, L, n_parts):
     (20, 8, 64 * 3 + 8, None, 4096),       # C4 part count: 16 parts/CU, encoders on SIMD 3
 ]])
 def test_fused_encode_hash_matches_separate_and_oracle(d, p, L, cstride, n_parts, mode,
-                                                       monkeypatch):
+                                                       knob_env):
     if mode == "enc3off":
-        monkeypatch.setenv("CEC_FUSED_ENC3", "0")
+        knob_env.set("CEC_FUSED_ENC3", "0")
         mode = "0"
     elif mode in ("le", "be"):
-        monkeypatch.setenv("CEC_FUSED_BE", "1" if mode == "be" else "0")
+        knob_env.set("CEC_FUSED_BE", "1" if mode == "be" else "0")
         mode = "0"
-    monkeypatch.setenv("CEC_FUSED_MODE", mode)
-    monkeypatch.setenv("CEC_FUSED", "1")  # the fused kernel whatever the batch size
+    knob_env.set("CEC_FUSED_MODE", mode)
+    knob_env.set("CEC_FUSED", "1")  # the fused kernel whatever the batch size
     t = d + p
     buf, batch = _device_parts(n_parts, t, L, cstride, seed=L * 3 + d)
     ref = buf.clone()
@@ -589,7 +589,7 @@ def test_fused_encode_hash_matches_separate_and_oracle(d, p, L, cstride, n_parts
     fused_buf = buf.clone()
     buf.copy_(ref)
     dig2 = torch.zeros_like(dig)
-    monkeypatch.setenv("CEC_FUSED", "0")
+    knob_env.set("CEC_FUSED", "0")
     ce.encode_hash_batch(rs, batch, dig2.data_ptr())  # encode kernel + sha256 kernel
     torch.cuda.synchronize()
     assert torch.equal(fused_buf, buf)
@@ -816,8 +816,8 @@ def _encoded_batch(d, p, L, n_parts, seed):
 
 
 @pytest.mark.parametrize("variant", ["1", "2"])  # skip path of both kernels
-def test_verify_batch_flags(variant, monkeypatch):
-    monkeypatch.setenv("CEC_SHA_VARIANT", variant)
+def test_verify_batch_flags(variant, knob_env):
+    knob_env.set("CEC_SHA_VARIANT", variant)
     d, p, L, n = 4, 2, 3000, 10
     rs, buf, batch, dig = _encoded_batch(d, p, L, n, 31)
     t = d + p
@@ -834,11 +834,11 @@ def test_verify_batch_flags(variant, monkeypatch):
 
 
 @pytest.mark.parametrize("speculate", ["1", "0"])
-def test_read_batch_restores_data_and_reports_undecodable_parts(speculate, monkeypatch):
+def test_read_batch_restores_data_and_reports_undecodable_parts(speculate, knob_env):
     """file_part.rs:86-129 batched.  speculate=1: the decode runs from the loaded chunks
     alongside verification and is redone for parts with a failed chunk; 0: verify, then decode
     (CEC_READ_SPECULATE A/B knob).  Both must give the verified decode."""
-    monkeypatch.setenv("CEC_READ_SPECULATE", speculate)
+    knob_env.set("CEC_READ_SPECULATE", speculate)
     d, p, L, n = 10, 4, 4096 + 5, 12
     rs, buf, batch, dig = _encoded_batch(d, p, L, n, 41)
     t = d + p
@@ -902,11 +902,11 @@ def test_read_batch_present_flag_values():
 
 @pytest.mark.parametrize("variant", ["1", "2"])  # compacted item list in both SHA kernels
 @pytest.mark.parametrize("speculate", ["1", "0"])
-def test_read_batch_random_patterns_vs_oracle(speculate, variant, monkeypatch):
-    monkeypatch.setenv("CEC_SHA_VARIANT", variant)
+def test_read_batch_random_patterns_vs_oracle(speculate, variant, knob_env):
+    knob_env.set("CEC_SHA_VARIANT", variant)
     """d random chunks loaded per part (reader.rs / file_part.rs:86-122), a few corrupted;
     the rebuilt data chunks equal the oracle's reconstruct_data from the verified chunks."""
-    monkeypatch.setenv("CEC_READ_SPECULATE", speculate)
+    knob_env.set("CEC_READ_SPECULATE", speculate)
     d, p, L, n = 10, 4, 1 << 12, 64
     rs, buf, batch, dig = _encoded_batch(d, p, L, n, 43)
     t = d + p
@@ -962,11 +962,11 @@ def test_resilver_batch_cluster_style():
 
 
 @pytest.mark.parametrize("speculate", ["1", "0"])
-def test_resilver_batch_random_patterns_with_corruption(speculate, monkeypatch):
+def test_resilver_batch_random_patterns_with_corruption(speculate, knob_env):
     """FilePart::resilver compute (file_part.rs:253-308) batched: random loaded sets (d..d+p),
     some loaded chunks corrupted (including ones the speculative decode uses); every decodable
     part ends with all d+p chunks equal to the written ones, flags mark the bad chunks."""
-    monkeypatch.setenv("CEC_READ_SPECULATE", speculate)
+    knob_env.set("CEC_READ_SPECULATE", speculate)
     d, p, L, n = 6, 3, 2048 + 7, 40
     rs, buf, batch, dig = _encoded_batch(d, p, L, n, 61)
     t = d + p
@@ -1038,7 +1038,7 @@ def test_chunk_longer_than_4gib_encode_and_reconstruct():
 
 
 @pytest.mark.parametrize("max_blocks", ["9", "64", "1000"])
-def test_apply_launch_split_over_part_ranges(monkeypatch, max_blocks):
+def test_apply_launch_split_over_part_ranges(knob_env, max_blocks):
     """A dispatch holds at most 2^32-1 work-items, so encode / reconstruct batches of more
     blocks than that are split into launches over whole part ranges (rs_kernels.hip).  The test
     knob CEC_APPLY_MAX_BLOCKS lowers the limit to force splits at test size (here 9 tiles per
@@ -1057,7 +1057,7 @@ def test_apply_launch_split_over_part_ranges(monkeypatch, max_blocks):
     present = np.ones((n, t), np.uint8)
     for k in range(n):
         present[k, rng.choice(t, int(rng.integers(1, p + 1)), replace=False)] = 0
-    monkeypatch.setenv("CEC_APPLY_MAX_BLOCKS", max_blocks)
+    knob_env.set("CEC_APPLY_MAX_BLOCKS", max_blocks)
     buf[:, d:] = 0
     ce.encode_batch(rs, batch)  # encode split
     torch.cuda.synchronize()
@@ -1070,7 +1070,7 @@ def test_apply_launch_split_over_part_ranges(monkeypatch, max_blocks):
 
 @pytest.mark.parametrize("d,p", [(3, 2), (10, 4), (20, 8)])
 @pytest.mark.parametrize("L", [16, 8192, 8192 + 16, 3 * 8192 - 16, 16384 + 5, 65536 + 4096])
-def test_bitsliced_encode_matches_vperm_and_oracle(monkeypatch, d, p, L):
+def test_bitsliced_encode_matches_vperm_and_oracle(knob_env, d, p, L):
     """The compiled shapes' encode takes the bit-sliced kernel (rs_encode_bs_kernel: full
     8 KiB column steps bit-sliced, the ragged rest through the v_perm byte path).  Every byte
     must equal the v_perm kernel's (CEC_APPLY_BS=0) and, on sampled parts, the oracle's."""
@@ -1083,7 +1083,7 @@ def test_bitsliced_encode_matches_vperm_and_oracle(monkeypatch, d, p, L):
     ce.encode_batch(rs, batch)
     torch.cuda.synchronize()
     got = buf.clone()
-    monkeypatch.setenv("CEC_APPLY_BS", "0")
+    knob_env.set("CEC_APPLY_BS", "0")
     buf[:, d:] = 0
     ce.encode_batch(rs, batch)
     torch.cuda.synchronize()

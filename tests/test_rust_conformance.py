@@ -129,7 +129,41 @@ def test_status_codes_match_the_crate_mapping():
         assert camel == variant, (code, camel, variant)
 
 
+def _crate_sources():
+    src_dir = os.path.dirname(RUST)
+    return {n: open(os.path.join(src_dir, n)).read() for n in sorted(os.listdir(src_dir))
+            if n.endswith(".rs")}
+
+
 def test_no_panics_on_engine_errors():
-    src = open(RUST).read()
-    code = re.sub(r"//[^\n]*", "", src)
-    assert "panic!" not in code and ".expect(" not in code and ".unwrap()" not in code
+    for name, src in _crate_sources().items():
+        code = re.sub(r"//[^\n]*", "", src)
+        assert "panic!" not in code and ".expect(" not in code and ".unwrap()" not in code, name
+
+
+def test_every_ffi_use_is_declared():
+    """Every sys::cec_* call in the crate (lib.rs wrappers, batch.rs's BatchWriter) names a
+    function of the extern block (hence of the header, by the test above)."""
+    declared = set(rust_functions())
+    for name, src in _crate_sources().items():
+        used = set(re.findall(r"sys::(cec_[a-z0-9_]+)\s*\(", src))
+        assert used <= declared, (name, sorted(used - declared))
+    batch = _crate_sources()["batch.rs"]
+    assert "pub mod batch;" in open(RUST).read()
+    # the batched writer goes through the asynchronous scheduler calls and part_encode
+    for call in ("submit_encode_hash", ".wait(", "part_encode(", "HostBuffer::zeroed"):
+        assert call in batch, call
+
+
+def test_batch_writer_mirrors_the_cpp_loop():
+    """BatchWriter::write is the C++ FileWriteBuilder::write_full_parts loop plus the reader
+    (writer.rs:172-194): two windows alternating, the older one collected first, the short last
+    part through part_encode; the C++ loop is the one the GPU tests run."""
+    batch = _crate_sources()["batch.rs"]
+    body = batch[batch.index("pub fn write<"):batch.index("fn fill<")]
+    order = [body.index(s) for s in ("self.fill(", "self.submit(", "self.collect(prev",
+                                      "self.collect(current", "self.short_part(")]
+    assert order == sorted(order)
+    assert "slot ^= 1" in body
+    hpp = open(os.path.join(ROOT, "include", "chunky_ec.hpp")).read()
+    assert "write_full_parts" in hpp and "cur ^= 1" in hpp
