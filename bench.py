@@ -1117,13 +1117,13 @@ def main():
     # the process's own CPU set, before the NUMA binding below narrows the main thread's (the
     # CPU baseline runs with it restored; the line's `host` block reports it)
     full_affinity = os.sched_getaffinity(0)
-    host = host_info()
+    host_report = host_info()
     # host threads and the pinned slots of this rank on its GPU's NUMA node (the engine places
     # its own pinned buffers there anyway; this keeps the host copies local too)
     numa_bound = ce.bind_thread_to_device_node(ordinal)
     numa_node = ce.device_numa_node(ordinal)
     rank_cpus = len(os.sched_getaffinity(0))
-    host["rank_cpus_after_numa_bind"] = rank_cpus
+    host_report["rank_cpus_after_numa_bind"] = rank_cpus
     # host threads of this rank's end-to-end reader: half its CPUs (the rest run the engine's
     # own threads), 8 at most
     e2e_threads = _rank_threads(world)
@@ -1466,7 +1466,7 @@ def main():
                                           "min": round(min(steps_ms), 3)}
         if ok is not None:
             line["check_vs_oracle"] = bool(ok)
-        line["host"] = host
+        line["host"] = host_report
         if snap is not None:
             # the oracle leg (after every timed region): the sampled full-size parts
             detail = check_vs_oracle(snap, d, p)
