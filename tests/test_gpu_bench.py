@@ -43,7 +43,12 @@ def test_default_line_contract_small():
     assert ns["reconstruct_data_2_erasures"]["frac"] > 0
     cb = line["cpu_baseline"]
     assert cb["value"] > 0 and cb["kind"] == "port" and cb["cores"] >= 1
-    assert "baseline_configs" not in line  # full-size only (the driver's run)
+    bc = line["baseline_configs"]  # C3 on the headline's buffer, C4 scaled to 256 parts
+    assert bc["c3_reconstruct"]["rebuilt_verified"] is True
+    assert bc["c4_encode_hash"]["round_trip_verified"] is True
+    assert bc["c4_encode_hash"]["traffic"] is None  # no committed PMC figure at this size
+    assert line["check_vs_oracle"] is True
+    assert all(line["check_vs_oracle_detail"]["checks"].values())
 
 
 def test_reconstruct_config_line_small():
