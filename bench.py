@@ -377,7 +377,7 @@ def encoded_ring(codec, d, p, L, n_parts, seed, device, P=256):
 
 
 def timed_read_repair(codec, ring, ring_dig, L, P, depth, first, n_parts, world, corrupt,
-                      copier, seed, n_samples=3):
+                      copier, seed, n_samples=3, rp=None):
     """FileReadBuilder over parts [first, first + n_parts) with read_with_context's retries
     (chunky_ec.readstream over cec_read_pipeline, REBUILT_ONLY): each part loads d random
     chunks of its d+p, copied by `copier`'s threads from the pageable ring of stored chunks
@@ -390,7 +390,8 @@ def timed_read_repair(codec, ring, ring_dig, L, P, depth, first, n_parts, world,
     import numpy as np
     d = codec.data_shard_count()
     R = len(ring)
-    rp = ce.ReadPipeline(codec, L, P, depth, ce.ReadPipeline.REBUILT_ONLY)
+    if rp is None:
+        rp = ce.ReadPipeline(codec, L, P, depth, ce.ReadPipeline.REBUILT_ONLY)
     crng = np.random.default_rng(seed)
     damaged = [0]
 
@@ -628,18 +629,19 @@ def read_repair_form(codec, d, p, L, n_parts, world, rank, reduce_dev, copier, d
     """end_to_end's read side: n_parts per rank through timed_read_repair (2 batches of stored
     parts in the ring: 7 GiB, every fetch reads DRAM)."""
     P, depth = CONFIGS["c5r"]["parts"], 4
+    # allocations first (the ring of stored parts, ~24 GiB of page-locked slots): if any rank
+    # cannot get them every rank skips the form together, before any barrier of the stream
     try:
         ring, ring_dig = encoded_ring(codec, d, p, L, 2 * P, rank_seed(0xE2ED, rank), device, P)
-        loc, stats, checks = timed_read_repair(codec, ring, ring_dig, L, P, depth, 0, n_parts,
-                                               world, corrupt, copier, 0xE2E5 + rank)
-        err = None
+        rp, err = ce.ReadPipeline(codec, L, P, depth, ce.ReadPipeline.REBUILT_ONLY), None
     except Exception as e:  # noqa: BLE001 (reported in the line)
-        loc, stats, checks, ring, err = 0.0, None, [], None, f"{type(e).__name__}: {e}"
-    # every rank reaches this collective (a failing rank's barriers were never entered by the
-    # others only if it failed before the first one: allocation, the usual case)
+        ring, rp, err = None, None, f"{type(e).__name__}: {e}"
     if not all_ranks_ok(err is None, world, reduce_dev):
         return {"value": None, "unit": "GB/s",
-                "skipped": err or "another rank could not run its read stream"}
+                "skipped": err or "another rank could not allocate its read stream"}
+    loc, stats, checks = timed_read_repair(codec, ring, ring_dig, L, P, depth, 0, n_parts, world,
+                                           corrupt, copier, 0xE2E5 + rank, rp=rp)
+    del rp
     el = max_over_ranks(loc, world, reduce_dev)
     total = n_parts * d * L * world
     ok = all(c["ok"] for c in checks) and stats["undecodable_parts"] == 0
