@@ -35,6 +35,7 @@ def main():
     for r in range(args.rounds + 1):
         for v in variants:
             os.environ["CEC_APPLY_TUNE"] = v
+            ce.reload_knobs()  # the library reads its knobs once per process
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s)
             ce.encode_batch(rs, batch, s)

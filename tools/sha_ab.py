@@ -40,6 +40,7 @@ def main():
     for r in range(args.rounds + 1):
         for v in variants:
             os.environ["CEC_SHA_VARIANT"] = str(v)
+            ce.reload_knobs()  # the library reads its knobs once per process
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             if args.encode_first:
                 ce.encode_batch(codec, ce.PartBatch(batch.base, batch.part_stride,
