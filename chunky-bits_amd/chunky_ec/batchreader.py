@@ -1,0 +1,176 @@
+"""FileReadBuilder's reader batched over the multi-GPU scheduler, with read_with_context's retry
+rule, parts handed out in file order: the Python twin of the Rust crate's
+``chunky_ec_sys::batch::BatchReader`` (chunky-bits_amd/rust/chunky-ec-sys/src/batch.rs) and of
+the C++ ``FileReference::read_run`` / ``retry`` (include/chunky_ec.hpp), step for step, so the
+loop the Rust side would run is executed and tested on the GPU (tests/test_gpu_batchreader.py).
+
+The reference reads a part by loading chunks until d of them verify (src/file/file_part.rs:
+86-107), rebuilds the missing data chunks (:123-129) and FileReadBuilder yields the parts in file
+order (src/file/reader.rs:40-75).  :class:`BatchReader` loads a window of
+``parts_per_batch * len(devices)`` parts at a time -- for each part the first d chunks its
+``fetch`` returns (data chunks first, so an intact part needs no rebuild) -- into a page-locked
+buffer and submits the window as one scheduler job (verify every loaded chunk, rebuild the data
+chunks; parts split over the GPUs in contiguous ranges) while it loads the next window.  A part
+whose loaded chunks do not all verify is resubmitted with the chunks that verified flagged
+``CEC_PRESENT_VERIFIED`` (used, not hashed again) and as many untried chunks as it is short of d,
+until it decodes; a part that runs out of chunks fails the read with TooFewShardsPresent, as the
+reference's does.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable, List, Optional
+
+import numpy as np
+
+from . import OK, PRESENT_VERIFIED, TOO_FEW_SHARDS_PRESENT, Error, HostBuffer, Multi, ReedSolomon
+
+
+@dataclass
+class _Window:
+    slot: int
+    job: int
+    first: int
+    n: int
+
+
+class BatchReader:
+    def __init__(self, data: int, parity: int, chunk_size: int, parts_per_batch: int, depth: int,
+                 devices: List[int]):
+        self.codec = ReedSolomon(data, parity)  # file_part.rs:77
+        self.multi = Multi(self.codec, chunk_size, parts_per_batch, depth, devices)
+        self.d, self.p, self.t, self.L = data, parity, data + parity, chunk_size
+        self.window = parts_per_batch * max(len(devices), 1)
+        dev0 = devices[0] if devices else -1
+        W, t, L = self.window, self.t, chunk_size
+        self.chunks = [HostBuffer(W * t * L, dev0) for _ in range(2)]
+        self.out = [HostBuffer(W * data * L, dev0) for _ in range(2)]
+        self.present = [np.zeros((W, t), np.uint8) for _ in range(2)]
+        self.expected = [np.zeros((W, t, 32), np.uint8) for _ in range(2)]
+        self.verified = [np.zeros((W, t), np.uint8) for _ in range(2)]
+        self.status = [np.zeros(W, np.int32) for _ in range(2)]
+        self.retries = 0  # part resubmissions (a part retried twice counts twice)
+
+    def read(self, n_parts: int, fetch: Callable[[int, int], Optional[bytes]],
+             digests: Callable[[int], np.ndarray], sink: Callable[[int, List[memoryview]], None]):
+        """Parts 0..n_parts-1: ``fetch(part, chunk)`` returns the stored chunk's bytes (None if
+        no location has it), ``digests(part)`` its metadata digests [d+p][32]; ``sink(part,
+        data_chunks)`` gets the d data chunks of every part, in file order."""
+        at = slot = 0
+        pending: Optional[_Window] = None
+        while True:
+            cur = None
+            if at < n_parts:
+                cnt = min(self.window, n_parts - at)
+                try:
+                    self._load(slot, at, cnt, fetch, digests)
+                    cur = _Window(slot, self._submit(slot, cnt), at, cnt)
+                except BaseException:
+                    self._drain(pending)
+                    raise
+                at += cnt
+            if pending is not None:  # the older window first: file order
+                prev, pending = pending, None
+                try:
+                    self._collect(prev, fetch, sink)
+                except BaseException:
+                    self._drain(cur)
+                    raise
+            if cur is None:
+                return
+            pending = cur
+            slot ^= 1
+
+    def _load(self, slot, first, cnt, fetch, digests):
+        """The first d chunks each part's fetch returns (file_part.rs:86-107 loads d), with
+        every chunk's metadata digest."""
+        d, t, L = self.d, self.t, self.L
+        ch = self.chunks[slot].view(self.window, t, L)
+        pres, exp = self.present[slot], self.expected[slot]
+        pres[:cnt] = 0
+        for q in range(cnt):
+            exp[q] = digests(first + q)
+            loaded = 0
+            for i in range(t):
+                if loaded == d:
+                    break
+                b = fetch(first + q, i)
+                if b is None or len(b) != L:
+                    continue
+                ch[q, i] = np.frombuffer(b, np.uint8)
+                pres[q, i] = 1
+                loaded += 1
+
+    def _submit(self, slot, cnt) -> int:
+        job, _ = self.multi.read(self.chunks[slot], self.present[slot], self.expected[slot], cnt,
+                                 self.out[slot], self.verified[slot], self.status[slot])
+        return job
+
+    def _collect(self, w: _Window, fetch, sink):
+        self.multi.wait(w.job)
+        st = self.status[w.slot]
+        failed = [q for q in range(w.n) if st[q] != OK]
+        if failed:
+            self._retry(w, failed, fetch)
+        d, L = self.d, self.L
+        out = memoryview(self.out[w.slot].array)
+        for q in range(w.n):
+            sink(w.first + q, [out[(q * d + j) * L:(q * d + j + 1) * L] for j in range(d)])
+
+    def _retry(self, w: _Window, failed, fetch):
+        """file_part.rs:92-107: the failed parts go again with the chunks that verified
+        (PRESENT_VERIFIED, taken from the window's buffer: the bytes that verified) plus untried
+        ones up to d, until each decodes or runs out of chunks."""
+        d, t, L = self.d, self.t, self.L
+        ch = self.chunks[w.slot].view(self.window, t, L)
+        pres, ver = self.present[w.slot], self.verified[w.slot]
+        out = self.out[w.slot].view(self.window, d, L)
+        tried = {q: pres[q] != 0 for q in failed}
+        good = {q: ver[q] != 0 for q in failed}
+        keep = {q: ch[q].copy() for q in failed}  # bytes of every chunk loaded so far
+        f = len(failed)
+        r_chunks, r_out = HostBuffer(f * t * L), HostBuffer(f * d * L)
+        rc, ro = r_chunks.view(f, t, L), r_out.view(f, d, L)
+        r_pres, r_exp = np.zeros((f, t), np.uint8), np.zeros((f, t, 32), np.uint8)
+        r_ver, r_st = np.zeros((f, t), np.uint8), np.zeros(f, np.int32)
+        open_ = list(failed)
+        while open_:
+            g = len(open_)
+            r_pres[:g] = 0
+            for s, q in enumerate(open_):
+                r_exp[s] = self.expected[w.slot][q]
+                have = int(good[q].sum())
+                added = 0
+                for i in range(t):
+                    if good[q][i]:
+                        rc[s, i] = keep[q][i]
+                        r_pres[s, i] = PRESENT_VERIFIED
+                    elif not tried[q][i] and have + added < d:
+                        tried[q][i] = True
+                        b = fetch(w.first + q, i)
+                        if b is None or len(b) != L:
+                            continue
+                        keep[q][i] = np.frombuffer(b, np.uint8)
+                        rc[s, i] = keep[q][i]
+                        r_pres[s, i] = 1
+                        added += 1
+                if added == 0:
+                    raise Error(TOO_FEW_SHARDS_PRESENT)
+            job, _ = self.multi.read(r_chunks, r_pres, r_exp, g, r_out, r_ver, r_st)
+            self.multi.wait(job)
+            self.retries += g
+            still = []
+            for s, q in enumerate(open_):
+                good[q] = r_ver[s] != 0
+                if r_st[s] == OK:
+                    out[q] = ro[s]
+                else:
+                    still.append(q)
+            open_ = still
+
+    def _drain(self, w: Optional[_Window]) -> None:
+        if w is not None:
+            try:
+                self.multi.wait(w.job)
+            except Exception:  # noqa: BLE001 (the error being raised is the caller's)
+                pass
