@@ -274,3 +274,298 @@ impl BatchWriter {
         }
     }
 }
+
+// ---------------------------------------------------------------------------------------------
+// Reads
+// ---------------------------------------------------------------------------------------------
+
+/// Failure of [`BatchReader::read`]: the engine's (a part that runs out of chunks is
+/// `CecError::Erasure(Error::TooFewShardsPresent)`, as the reference's read fails), or the
+/// sink's own error.
+#[derive(Debug)]
+pub enum BatchReadError<E> {
+    Engine(CecError),
+    Sink(E),
+}
+
+/// A read window submitted to the scheduler and not yet handed to the sink.
+struct LiveRead {
+    slot: usize,
+    job: u64,
+    first: usize,
+    n: usize,
+}
+
+/// `FileReadBuilder`'s reader (reader.rs:40-75) batched over the multi-GPU scheduler with
+/// `read_with_context`'s retry rule (file_part.rs:86-129), parts handed out in file order.
+///
+/// For each part of a window of `parts_per_batch * devices.len()` parts it loads the first d
+/// chunks `fetch` returns (data chunks first, so an intact part needs no rebuild) into a
+/// page-locked buffer, and submits the window as one scheduler job: every loaded chunk verified
+/// against its metadata digest, the data chunks rebuilt.  It loads the next window while that one
+/// runs.  A part whose loaded chunks do not all verify goes again with the chunks that verified
+/// (`CEC_PRESENT_VERIFIED`: used, not hashed again) and as many untried chunks as it is short of
+/// d, until it decodes or runs out of chunks.  `include/chunky_ec.hpp`'s
+/// `FileReference::read_run` / `retry` is the same loop in C++ and
+/// `chunky-bits_amd/chunky_ec/batchreader.py` its Python twin; both are tested on the GPU.
+pub struct BatchReader {
+    // declared (so dropped) first: the scheduler refers to the codec and the windows
+    multi: Multi,
+    codec: ReedSolomon,
+    d: usize,
+    t: usize,
+    chunk_size: usize,
+    window: usize,
+    chunks: [HostBuffer; 2],
+    out: [HostBuffer; 2],
+    present: [Vec<u8>; 2],
+    expected: [Vec<u8>; 2],
+    verified: [Vec<u8>; 2],
+    status: [Vec<c_int>; 2],
+    retries: u64,
+}
+
+impl BatchReader {
+    /// A reader of RS(`data`, `parity`) parts of `chunk_size`-byte chunks on `devices`.
+    pub fn new(
+        data: usize,
+        parity: usize,
+        chunk_size: usize,
+        parts_per_batch: usize,
+        depth: usize,
+        devices: &[c_int],
+    ) -> Result<BatchReader, CecError> {
+        let codec = ReedSolomon::new(data, parity)?;  // file_part.rs:77
+        let multi = Multi::new(&codec, chunk_size, parts_per_batch, depth, devices)?;
+        let window = parts_per_batch * devices.len().max(1);
+        let dev0 = devices.first().copied().unwrap_or(-1);
+        let t = data + parity;
+        let buf = |n: usize| HostBuffer::zeroed(n, dev0);
+        Ok(BatchReader {
+            chunks: [buf(window * t * chunk_size)?, buf(window * t * chunk_size)?],
+            out: [buf(window * data * chunk_size)?, buf(window * data * chunk_size)?],
+            present: [vec![0u8; window * t], vec![0u8; window * t]],
+            expected: [vec![0u8; window * t * 32], vec![0u8; window * t * 32]],
+            verified: [vec![0u8; window * t], vec![0u8; window * t]],
+            status: [vec![0; window], vec![0; window]],
+            multi,
+            codec,
+            d: data,
+            t,
+            chunk_size,
+            window,
+            retries: 0,
+        })
+    }
+
+    /// Part resubmissions so far (a part retried twice counts twice).
+    pub fn retries(&self) -> u64 {
+        self.retries
+    }
+
+    /// The codec the parts were written with (`FilePart`'s d and p).
+    pub fn codec(&self) -> &ReedSolomon {
+        &self.codec
+    }
+
+    /// Parts `0..n_parts` of a file: `digests` holds the metadata digests, `n_parts * (d + p)`
+    /// of them, part by part (`FilePart::data` then `parity`); `fetch(part, chunk)` returns the
+    /// stored chunk's bytes, or `None` when no location has it (`Location::read_with_context`
+    /// over the chunk's locations, file_part.rs:100-107); `sink(part, data_chunks)` gets the d
+    /// data chunks of every part in file order, valid during the call.
+    pub fn read<F, S, E>(
+        &mut self,
+        n_parts: usize,
+        digests: &[[u8; 32]],
+        mut fetch: F,
+        mut sink: S,
+    ) -> Result<(), BatchReadError<E>>
+    where
+        F: FnMut(usize, usize) -> Option<Vec<u8>>,
+        S: FnMut(usize, &[&[u8]]) -> Result<(), E>,
+    {
+        if digests.len() < n_parts * self.t {
+            return Err(BatchReadError::Engine(crate::too_small("digests")));
+        }
+        let mut at = 0usize;
+        let mut slot = 0usize;
+        let mut pending: Option<LiveRead> = None;
+        loop {
+            let mut current = None;
+            if at < n_parts {
+                let cnt = self.window.min(n_parts - at);
+                self.load(slot, at, cnt, digests, &mut fetch);
+                match unsafe { self.submit(slot, cnt) } {
+                    Ok(job) => current = Some(LiveRead { slot, job, first: at, n: cnt }),
+                    Err(e) => {
+                        self.drain(pending.take());
+                        return Err(BatchReadError::Engine(e));
+                    },
+                }
+                at += cnt;
+            }
+            // the older window's parts go out first: file order
+            if let Some(prev) = pending.take() {
+                if let Err(e) = self.collect(prev, &mut fetch, &mut sink) {
+                    self.drain(current);
+                    return Err(e);
+                }
+            }
+            match current {
+                None => return Ok(()),
+                Some(c) => pending = Some(c),
+            }
+            slot ^= 1;
+        }
+    }
+
+    /// The first d chunks `fetch` returns for each part of window `slot` (file_part.rs:86-107
+    /// loads d), and every chunk's metadata digest.
+    fn load<F>(&mut self, slot: usize, first: usize, cnt: usize, digests: &[[u8; 32]], fetch: &mut F)
+    where
+        F: FnMut(usize, usize) -> Option<Vec<u8>>,
+    {
+        let (d, t, l) = (self.d, self.t, self.chunk_size);
+        let ch: &mut [u8] = &mut self.chunks[slot];
+        let pres = &mut self.present[slot];
+        let exp = &mut self.expected[slot];
+        for q in 0..cnt {
+            let mut loaded = 0usize;
+            for i in 0..t {
+                let x = q * t + i;
+                exp[x * 32..(x + 1) * 32].copy_from_slice(&digests[(first + q) * t + i]);
+                pres[x] = 0;
+                if loaded == d {
+                    continue;
+                }
+                if let Some(b) = fetch(first + q, i) {
+                    if b.len() == l {
+                        ch[x * l..(x + 1) * l].copy_from_slice(&b);
+                        pres[x] = 1;
+                        loaded += 1;
+                    }
+                }
+            }
+        }
+    }
+
+    /// Queues the verify + rebuild of the first `cnt` parts of window `slot`.
+    ///
+    /// # Safety
+    /// The window's buffers are not touched again until the job is collected or drained.
+    unsafe fn submit(&mut self, slot: usize, cnt: usize) -> Result<u64, CecError> {
+        let chunks = self.chunks[slot].as_ptr();
+        let present = self.present[slot].as_ptr();
+        let expected = self.expected[slot].as_ptr();
+        let out = self.out[slot].as_mut_ptr();
+        let verified = self.verified[slot].as_mut_ptr();
+        let status = self.status[slot].as_mut_ptr();
+        self.multi.submit_read(chunks, present, expected, cnt, out, verified, status)
+    }
+
+    /// Waits for a window's job, retries its failed parts, then hands its parts to the sink.
+    fn collect<F, S, E>(&mut self, w: LiveRead, fetch: &mut F, sink: &mut S) -> Result<(), BatchReadError<E>>
+    where
+        F: FnMut(usize, usize) -> Option<Vec<u8>>,
+        S: FnMut(usize, &[&[u8]]) -> Result<(), E>,
+    {
+        self.multi.wait(w.job).map_err(BatchReadError::Engine)?;
+        let failed: Vec<usize> = (0..w.n).filter(|&q| self.status[w.slot][q] != 0).collect();
+        if !failed.is_empty() {
+            self.retry(&w, &failed, fetch).map_err(BatchReadError::Engine)?;
+        }
+        let (d, l) = (self.d, self.chunk_size);
+        let out: &[u8] = &self.out[w.slot];
+        for q in 0..w.n {
+            let data: Vec<&[u8]> = (0..d).map(|j| &out[(q * d + j) * l..(q * d + j + 1) * l]).collect();
+            sink(w.first + q, &data).map_err(BatchReadError::Sink)?;
+        }
+        Ok(())
+    }
+
+    /// file_part.rs:92-107: the failed parts go again with the chunks that verified (flagged
+    /// `CEC_PRESENT_VERIFIED`, taken from the window's buffer: the bytes that verified) plus
+    /// untried ones up to d, until each decodes; a part with no untried chunk left fails the read.
+    fn retry<F>(&mut self, w: &LiveRead, failed: &[usize], fetch: &mut F) -> Result<(), CecError>
+    where
+        F: FnMut(usize, usize) -> Option<Vec<u8>>,
+    {
+        let (d, t, l) = (self.d, self.t, self.chunk_size);
+        let f = failed.len();
+        let mut tried = vec![false; f * t];
+        let mut good = vec![false; f * t];
+        let mut keep = vec![0u8; f * t * l];  // bytes of every chunk loaded so far
+        {
+            let ch: &[u8] = &self.chunks[w.slot];
+            for (r, &q) in failed.iter().enumerate() {
+                for i in 0..t {
+                    tried[r * t + i] = self.present[w.slot][q * t + i] != 0;
+                    good[r * t + i] = self.verified[w.slot][q * t + i] != 0;
+                }
+                keep[r * t * l..(r + 1) * t * l].copy_from_slice(&ch[q * t * l..(q + 1) * t * l]);
+            }
+        }
+        let dev0 = -1;
+        let mut r_chunks = HostBuffer::zeroed(f * t * l, dev0)?;
+        let mut r_out = HostBuffer::zeroed(f * d * l, dev0)?;
+        let mut r_pres = vec![0u8; f * t];
+        let mut r_exp = vec![0u8; f * t * 32];
+        let mut r_ver = vec![0u8; f * t];
+        let mut open: Vec<usize> = (0..f).collect();
+        while !open.is_empty() {
+            let g = open.len();
+            for (s, &r) in open.iter().enumerate() {
+                let q = failed[r];
+                r_exp[s * t * 32..(s + 1) * t * 32]
+                    .copy_from_slice(&self.expected[w.slot][q * t * 32..(q + 1) * t * 32]);
+                let have = (0..t).filter(|&i| good[r * t + i]).count();
+                let mut added = 0usize;
+                for i in 0..t {
+                    let (x, y) = (r * t + i, s * t + i);
+                    r_pres[y] = 0;
+                    if good[x] {
+                        r_chunks[y * l..(y + 1) * l].copy_from_slice(&keep[x * l..(x + 1) * l]);
+                        r_pres[y] = crate::sys::CEC_PRESENT_VERIFIED;
+                    } else if !tried[x] && have + added < d {
+                        tried[x] = true;
+                        if let Some(b) = fetch(w.first + q, i) {
+                            if b.len() == l {
+                                keep[x * l..(x + 1) * l].copy_from_slice(&b);
+                                r_chunks[y * l..(y + 1) * l].copy_from_slice(&b);
+                                r_pres[y] = 1;
+                                added += 1;
+                            }
+                        }
+                    }
+                }
+                if added == 0 {
+                    return Err(CecError::Erasure(crate::Error::TooFewShardsPresent));
+                }
+            }
+            let status = self.multi.read(&r_chunks, &r_pres, &r_exp, g, &mut r_out, &mut r_ver)?;
+            self.retries += g as u64;
+            let mut still = Vec::new();
+            let out: &mut [u8] = &mut self.out[w.slot];
+            for (s, &r) in open.iter().enumerate() {
+                let q = failed[r];
+                for i in 0..t {
+                    good[r * t + i] = r_ver[s * t + i] != 0;
+                }
+                if status[s].is_ok() {
+                    out[q * d * l..(q + 1) * d * l].copy_from_slice(&r_out[s * d * l..(s + 1) * d * l]);
+                } else {
+                    still.push(r);
+                }
+            }
+            open = still;
+        }
+        Ok(())
+    }
+
+    /// Waits for a window's job without handing out its parts (error paths).
+    fn drain(&self, w: Option<LiveRead>) {
+        if let Some(w) = w {
+            let _ = self.multi.wait(w.job);
+        }
+    }
+}

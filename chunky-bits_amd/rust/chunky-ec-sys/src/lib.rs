@@ -921,7 +921,7 @@ pub struct Multi {
     chunk_len: usize,
 }
 
-fn too_small(what: &str) -> CecError {
+pub(crate) fn too_small(what: &str) -> CecError {
     CecError::Engine(EngineError { code: 101, message: format!("{} buffer too small", what) })
 }
 
@@ -1071,7 +1071,42 @@ impl Multi {
         Ok(job)
     }
 
-    /// Waits for a job queued with [`Multi::submit_encode_hash`].
+    /// Asynchronous [`Multi::read`] (data of every part back, no `data_ptrs`): queues the job
+    /// and returns its id for [`Multi::wait`].
+    ///
+    /// # Safety
+    /// `chunks` (`n_parts * (d + p) * L` bytes), `present` / `verified` (`n_parts * (d + p)`),
+    /// `expected` (`n_parts * (d + p) * 32`), `data` (`n_parts * d * L`) and `status`
+    /// (`n_parts`) must stay valid, and the inputs unmodified, until the job has been waited for.
+    #[allow(clippy::too_many_arguments)]
+    pub unsafe fn submit_read(
+        &self,
+        chunks: *const u8,
+        present: *const u8,
+        expected: *const u8,
+        n_parts: usize,
+        data: *mut u8,
+        verified: *mut u8,
+        status: *mut c_int,
+    ) -> Result<u64, CecError> {
+        let mut job = 0u64;
+        check_multi(sys::cec_multi_read(
+            self.raw,
+            chunks,
+            present,
+            expected,
+            n_parts,
+            data,
+            verified,
+            status,
+            std::ptr::null_mut(),
+            0,
+            &mut job,
+        ))?;
+        Ok(job)
+    }
+
+    /// Waits for a job queued with [`Multi::submit_encode_hash`] or [`Multi::submit_read`].
     pub fn wait(&self, job: u64) -> Result<(), CecError> {
         check_multi(unsafe { sys::cec_multi_wait(self.raw, job) })
     }

@@ -167,3 +167,22 @@ def test_batch_writer_mirrors_the_cpp_loop():
     assert "slot ^= 1" in body
     hpp = open(os.path.join(ROOT, "include", "chunky_ec.hpp")).read()
     assert "write_full_parts" in hpp and "cur ^= 1" in hpp
+
+
+def test_batch_reader_mirrors_the_cpp_and_python_loops():
+    """BatchReader::read is the C++ read_run / retry loop (and chunky_ec/batchreader.py, its
+    GPU-tested Python twin): load a window (first d fetched chunks per part), submit it, hand
+    the older window out first; failed parts retried with PRESENT_VERIFIED chunks plus untried
+    ones until they decode, TooFewShardsPresent when none is left."""
+    batch = _crate_sources()["batch.rs"]
+    body = batch[batch.index("pub fn read<"):batch.index("    fn load<")]
+    order = [body.index(s) for s in ("self.load(", "self.submit(", "self.collect(prev")]
+    assert order == sorted(order) and "slot ^= 1" in body
+    retry = batch[batch.index("    fn retry<"):batch.index("    fn drain(&self, w: Option<LiveRead>)")]
+    for s in ("CEC_PRESENT_VERIFIED", "have + added < d", "TooFewShardsPresent",
+              "self.multi.read("):
+        assert s in retry, s
+    py = open(os.path.join(ROOT, "chunky-bits_amd", "chunky_ec", "batchreader.py")).read()
+    for s in ("def _load", "def _submit", "def _collect", "def _retry", "have + added < d",
+              "PRESENT_VERIFIED", "TOO_FEW_SHARDS_PRESENT"):
+        assert s in py, s
