@@ -1470,12 +1470,13 @@ def main():
         if ok is not None:
             line["check_vs_oracle"] = bool(ok)
         line["host"] = host_report
-        if snap is not None:
-            # the oracle leg (after every timed region): the sampled full-size parts
-            detail = check_vs_oracle(snap, d, p)
-            line["check_vs_oracle"] = detail["ok"]
-            line["check_vs_oracle_detail"] = detail
         if world == 1 and not args.no_cpu_baseline and cfg["op"] in ("encode_hash", "encode"):
+            # the cpu_baseline leg (after every timed region), the one place the bench runs the
+            # oracle: first the sampled full-size parts of this run's buffers against it
+            if snap is not None:
+                detail = check_vs_oracle(snap, d, p)
+                line["check_vs_oracle"] = detail["ok"]
+                line["check_vs_oracle_detail"] = detail
             # the process's full CPU set (the main thread was bound to GPU0's NUMA node above)
             os.sched_setaffinity(0, full_affinity)
             avail, quota = len(full_affinity), cpu_quota()[1]
