@@ -129,8 +129,9 @@ class BatchReader:
         good = {q: ver[q] != 0 for q in failed}
         keep = {q: ch[q].copy() for q in failed}  # bytes of every chunk loaded so far
         f = len(failed)
-        r_chunks, r_out = HostBuffer(f * t * L), HostBuffer(f * d * L)
-        rc, ro = r_chunks.view(f, t, L), r_out.view(f, d, L)
+        # pageable (the scheduler stages them): pinning a retry buffer per window would cost more
+        # than the few parts it carries (~0.35 s per GiB)
+        rc, ro = np.zeros((f, t, L), np.uint8), np.zeros((f, d, L), np.uint8)
         r_pres, r_exp = np.zeros((f, t), np.uint8), np.zeros((f, t, 32), np.uint8)
         r_ver, r_st = np.zeros((f, t), np.uint8), np.zeros(f, np.int32)
         open_ = list(failed)
@@ -156,7 +157,7 @@ class BatchReader:
                         added += 1
                 if added == 0:
                     raise Error(TOO_FEW_SHARDS_PRESENT)
-            job, _ = self.multi.read(r_chunks, r_pres, r_exp, g, r_out, r_ver, r_st)
+            job, _ = self.multi.read(rc, r_pres, r_exp, g, ro, r_ver, r_st)
             self.multi.wait(job)
             self.retries += g
             still = []

@@ -505,9 +505,10 @@ impl BatchReader {
                 keep[r * t * l..(r + 1) * t * l].copy_from_slice(&ch[q * t * l..(q + 1) * t * l]);
             }
         }
-        let dev0 = -1;
-        let mut r_chunks = HostBuffer::zeroed(f * t * l, dev0)?;
-        let mut r_out = HostBuffer::zeroed(f * d * l, dev0)?;
+        // pageable (the scheduler stages them): pinning a retry buffer per window would cost more
+        // than the few parts it carries (~0.35 s per GiB)
+        let mut r_chunks = vec![0u8; f * t * l];
+        let mut r_out = vec![0u8; f * d * l];
         let mut r_pres = vec![0u8; f * t];
         let mut r_exp = vec![0u8; f * t * 32];
         let mut r_ver = vec![0u8; f * t];
