@@ -649,6 +649,7 @@ def read_repair_form(codec, d, p, L, n_parts, world, rank, reduce_dev, copier, d
             "_local": n_parts * d * L / loc / 1e9,
             "seconds": round(el, 3), "stream_bytes": total, "corrupt_frac": corrupt,
             "retries": stats["retried_parts"], "retry_batches": stats["retry_batches"],
+            "mixed_batches": stats["mixed_batches"],
             "rejected_chunks": stats["rejected_chunks"], "damaged_loads": stats["damaged_loads"],
             "undecodable_parts": stats["undecodable_parts"], "batches": stats["batches"],
             "chunks_loaded": stats["chunks_loaded"],
@@ -657,8 +658,9 @@ def read_repair_form(codec, d, p, L, n_parts, world, rank, reduce_dev, copier, d
                     f"{copier.threads} host threads copy d random chunks per part into a "
                     "page-locked slot, a seeded fraction of them damaged -> H2D -> SHA-256 "
                     "verify + reconstruct_data -> D2H of the rebuilt data chunks; parts with a "
-                    "rejected chunk resubmitted with their verified chunks (CEC_PRESENT_VERIFIED) "
-                    f"and one more (cec_read_pipeline, {P}-part batches, {depth} slots)"}
+                    "rejected chunk resubmitted in the next batch, ahead of its new parts, with "
+                    "their verified chunks (CEC_PRESENT_VERIFIED) and one more "
+                    f"(cec_read_pipeline, {P}-part batches, {depth} slots)"}
 
 
 def scheduler_pageable(codec, d, p, L, ring, n_parts, world, reduce_dev, device_ordinal):

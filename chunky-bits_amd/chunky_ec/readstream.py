@@ -13,7 +13,7 @@ slots, `depth` batches in flight):
 * a part the pipeline reports ``TooFewShardsPresent`` (one of its loaded chunks failed the
   hash) is queued for a retry: its verified chunks are loaded again flagged
   ``CEC_PRESENT_VERIFIED`` (used, not hashed again) plus as many untried chunks, drawn at random,
-  as it is short of d; retries go out as batches of their own, interleaved with new parts;
+  as it is short of d; the next batch carries the queued retries ahead of its new parts;
 * a part with fewer than d chunks left to try is undecodable (the reference's read fails with
   ``TooFewShardsPresent`` there; the stream counts it and goes on).
 
@@ -48,7 +48,8 @@ class _Part:
 class ReadRepairStats:
     parts: int = 0              # parts read back (decoded) successfully
     batches: int = 0            # batches submitted (new + retry)
-    retry_batches: int = 0      # batches made of retried parts only
+    retry_batches: int = 0      # batches made of retried parts only (after the last new part)
+    mixed_batches: int = 0      # batches carrying retried parts ahead of new ones
     retried_parts: int = 0      # part resubmissions (a part retried twice counts twice)
     rejected_chunks: int = 0    # loaded chunks whose sha256 did not match the metadata
     undecodable_parts: int = 0  # parts left with fewer than d chunks to try
@@ -156,23 +157,31 @@ class ReadRepairStream:
     # -- driver ---------------------------------------------------------------------------------
 
     def run(self, first: int, n_parts: int) -> ReadRepairStats:
-        """Read parts [first, first + n_parts) to the end, retries included; returns the stats."""
+        """Read parts [first, first + n_parts) to the end, retries included; returns the stats.
+
+        Every batch takes the queued retries first and fills the rest with new parts, so a retried
+        part goes out in the next batch and batches stay full (a batch costs about one SHA-256
+        chain of time whatever its size); only after the last new part do batches of retries
+        alone go out."""
         nxt, end = first, first + n_parts
         while nxt < end or self._retry or self._inflight:
             # a slot is reused round-robin: collect the oldest batch before its slot is acquired
             if len(self._inflight) == self.depth:
                 self._collect()
-            if len(self._retry) >= self.P or (nxt >= end and self._retry):
+            if nxt < end or self._retry:
                 parts, present = self._retry_parts()
+                room = self.P - len(parts)
+                if nxt < end and room > 0:
+                    n = min(room, end - nxt)
+                    new, new_present = self._new_parts(nxt, n)
+                    nxt += n
+                    if parts:
+                        self.stats.mixed_batches += 1
+                    parts, present = parts + new, np.concatenate([present, new_present])
+                elif parts:
+                    self.stats.retry_batches += 1
                 if parts:
                     self._submit(parts, present)
-                    self.stats.retry_batches += 1
-                continue
-            if nxt < end:
-                n = min(self.P, end - nxt)
-                parts, present = self._new_parts(nxt, n)
-                self._submit(parts, present)
-                nxt += n
                 continue
             if self._inflight:
                 self._collect()

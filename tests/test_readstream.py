@@ -113,9 +113,14 @@ def test_read_repair_stream_rebuilds_every_part(corrupt):
     assert s.rejected_chunks == len(bad_loads)
     assert sum(attempts.values()) - len(attempts) <= s.retried_parts
     if corrupt == 0.0:
-        assert s.retried_parts == 0 and s.retry_batches == 0 and s.undecodable_parts == 0
+        assert s.retried_parts == 0 and s.retry_batches == 0 and s.mixed_batches == 0
+        assert s.undecodable_parts == 0 and s.batches == (n + P - 1) // P
     else:
-        assert s.retried_parts > 0 and s.retry_batches > 0
+        # retries ride in the next batch ahead of new parts: every batch but the trailing
+        # retry-only ones is full
+        assert s.retried_parts > 0 and s.mixed_batches > 0
+        sizes = [len(rows) for _, rows in fp.submitted]
+        assert all(k == P for k in sizes[:s.batches - s.retry_batches - 1])
     # the load rule: first loads are d distinct chunks; a retry re-sends the verified chunks as
     # PRESENT_VERIFIED and adds exactly (d - verified) chunks never tried before
     for _, rows in fp.submitted:
