@@ -195,3 +195,54 @@ def test_golden_cluster_parts(golden):
                                           len(piece))
         assert cs == part["chunksize"]
         assert [bytes(x).hex() for x in dig] == part["sha256"]
+
+
+def _gf_tables():
+    """GF(2^8) with polynomial 0x11D and generator 2, built here from the definition (the field
+    galois_8's build.rs generates), independent of the oracle's C tables."""
+    exp, log = [0] * 512, [0] * 256
+    x = 1
+    for i in range(255):
+        exp[i] = x
+        log[x] = i
+        x <<= 1
+        if x & 0x100:
+            x ^= 0x11D
+    for i in range(255, 512):
+        exp[i] = exp[i - 255]
+    return exp, log
+
+
+def test_coding_matrix_by_lagrange_interpolation():
+    """M = V·inv(V_top) with V[r][c] = r^c means: parity row i, column j is the j-th Lagrange basis
+    polynomial over the points 0..d-1 evaluated at the point d+i (the systematic code evaluates
+    the polynomial through the d data values at d..d+p-1).  Computed here in pure Python from
+    the field definition -- a second derivation of the coding matrix, by interpolation instead of
+    the oracle's Gauss-Jordan inversion -- for the hot-path shapes and the Appendix A rows."""
+    exp, log = _gf_tables()
+
+    def mul(a, b):
+        return 0 if a == 0 or b == 0 else exp[log[a] + log[b]]
+
+    def div(a, b):
+        return 0 if a == 0 else exp[log[a] - log[b] + 255]
+
+    def lagrange_row(d, x):
+        row = []
+        for j in range(d):
+            num = den = 1
+            for m in range(d):
+                if m != j:
+                    num = mul(num, x ^ m)   # (x - m) in characteristic 2
+                    den = mul(den, j ^ m)
+            row.append(div(num, den))
+        return row
+
+    for d, p in [(3, 2), (10, 4), (20, 8), (5, 5), (4, 2), (17, 3), (1, 1), (128, 128)]:
+        m = oracle.coding_matrix(d, p)
+        for i in range(p):
+            assert list(m[d + i]) == lagrange_row(d, d + i), (d, p, i)
+    # SURVEY.md Appendix A
+    assert lagrange_row(3, 3) == [1, 1, 1] and lagrange_row(3, 4) == [15, 8, 6]
+    assert lagrange_row(10, 10) == [129, 150, 175, 184, 210, 196, 254, 232, 3, 2]
+    assert lagrange_row(10, 12) == [191, 214, 98, 10, 6, 111, 223, 183, 5, 4]
