@@ -23,6 +23,7 @@ import yaml
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "golden"))
 import make_format_fixture as fx  # noqa: E402  (test infrastructure: slicing + oracle)
+from _gen import gen_bytes  # noqa: E402
 
 YAML = os.path.join(HERE, "golden", "c1_file_reference.yaml")
 RUN = os.path.join(HERE, "golden", "c1_reference_run.json")
@@ -121,3 +122,48 @@ def test_engine_device_batch_matches_reference_format():
             assert ref["parts"][k]["chunksize"] == L
             want = [c["sha256"] for c in ref["parts"][k]["data"] + ref["parts"][k]["parity"]]
             assert [got[q, i].tobytes().hex() for i in range(t)] == want, k
+
+
+# --- the engine's own store, read back by the reference (tests/golden/make_dropin_record.py) ---
+
+DROPIN_YAML = os.path.join(HERE, "golden", "dropin_file_reference.yaml")
+DROPIN_RUN = os.path.join(HERE, "golden", "dropin_reference_run.json")
+
+
+def test_reference_reader_reads_the_engines_repaired_store():
+    """tools/dropin_cp_repair.py wrote a 22 MiB file through the batched writer on the GPU,
+    deleted / damaged five chunk files, read it back through the batched reader and repaired
+    the store through the scheduler's resilver; the reference's python/chunky-bits.py then read
+    the engine's FileReference and chunk files: exit 0, no digest mismatch, stdout = the input
+    (and its control with one flipped byte was caught)."""
+    run = json.load(open(DROPIN_RUN))
+    gpu = run["gpu_side"]
+    assert run["returncode"] == 0 and run["stderr"] == ""
+    data = gen_bytes(gpu["seed"], gpu["length"])
+    assert run["stdout_len"] == gpu["length"]
+    assert run["stdout_sha256"] == gpu["input_sha256"] == hashlib.sha256(data.tobytes()).hexdigest()
+    assert gpu["cat_equals_input"] is True and gpu["read_retries"] >= 1
+    assert sorted(map(tuple, gpu["repaired"])) == sorted(map(tuple, gpu["deleted"] +
+                                                             [gpu["corrupted"]]))
+    c = run["corrupted_control"]
+    assert c["stderr_lines"] == 1 and c["stderr_names_the_chunk"] and c["stdout_sha256_differs"]
+
+
+def test_engines_store_equals_the_oracle_file_reference():
+    """The FileReference the GPU wrote -- chunk sizes, data digests AND parity digests -- equals
+    the oracle's for the same input: the engine's parity bytes (batched writer for the full
+    parts, cec_part_encode for the short last one) match the CPU restatement of the crate on
+    every part of this file."""
+    ref = yaml.safe_load(open(DROPIN_YAML))
+    gpu = json.load(open(DROPIN_RUN))["gpu_side"]
+    d, p, chunk = gpu["d"], gpu["p"], gpu["chunk_size"]
+    data = gen_bytes(gpu["seed"], gpu["length"])
+    assert ref["length"] == gpu["length"] and len(ref["parts"]) == gpu["parts"]
+    for k, (L, chunks) in enumerate(fx.parts_of(data, d, p, chunk)):
+        part = ref["parts"][k]
+        assert part["chunksize"] == L
+        hexes = [hashlib.sha256(c.tobytes()).hexdigest() for c in chunks]
+        assert [c["sha256"] for c in part["data"]] == hexes[:d], k
+        assert [c["sha256"] for c in part["parity"]] == hexes[d:], k
+        assert all(c["locations"] == [f"sha256-{c['sha256']}"]
+                   for c in part["data"] + part["parity"])
