@@ -16,6 +16,15 @@ Rank 0 prints ONE JSON line.  `roofline` describes the dominant kernel, timed wi
 on the stream its launches go to; `cpu_baseline` times the CPU restatement of the reference
 crates (oracle/, the same scalar galois_8 table path + SHA-256 with SHA-NI like sha2 0.9.9's
 cpufeatures dispatch) on this host's cores over a bounded sample of the same workload.
+
+The default (c2) line also carries: `north_star` (RS(10,4) encode and 2-erasure reconstruct_data
+on the headline's buffer, fractions of 8 TB/s), `baseline_configs` (BASELINE configs[2] C3 and
+configs[3] C4 per GPU), `end_to_end` (host-produced write stream, read + repair stream with
+damaged fetches retried, the PCIe link alone, the one-process scheduler path), and at N = 1
+`check_vs_oracle` (whole sampled parts of those buffers against the oracle, in the cpu_baseline
+leg).  At N > 1: `ranks` (each rank's own figures) and `node` (configs[3] and C3 at node level).
+`--config c5` / `c5r` run BASELINE configs[4]: a `--stream-gib` (1 TiB) stream fed per batch
+from pageable rings, written, or read back with `--corrupt` of the fetched chunks damaged.
 """
 import argparse
 import json
