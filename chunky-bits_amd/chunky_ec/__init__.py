@@ -14,6 +14,12 @@ like the Rust API the reference calls on its hot path so that tests read like th
   (``FilePart::write_with_encoder`` / ``read_with_context`` / ``resilver`` / ``verify``,
   src/file/file_part.rs:73-390), batched over parts resident in HBM.
 
+Host loops built on these (submodules): :mod:`chunky_ec.readstream` (FileReadBuilder's part
+loop over a ReadPipeline with read_with_context's retry rule), :mod:`chunky_ec.batchwriter` /
+:mod:`chunky_ec.batchreader` (the batched FileWriteBuilder / FileReadBuilder loops over the
+multi-GPU scheduler: twins of the Rust crate's ``batch`` module), :mod:`chunky_ec.sharding`
+(part ranges and the bench's cross-rank helpers).
+
 All computation runs in the HIP library on the GPU; there is no CPU fallback.  If the
 library is missing this module raises on import.
 """
