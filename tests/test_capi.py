@@ -68,6 +68,23 @@ def test_codec_matrix_matches_oracle(d, p):
     assert np.array_equal(np.array(rs.matrix(), dtype=np.uint8), oracle.coding_matrix(d, p))
 
 
+def test_codec_matrix_kat_rows(kats):
+    """The engine's own RS(5,5) matrix (csrc/gf256.cpp, not the oracle) against the published
+    decode-matrix KAT (crate_kats.json matrix_inverse[1]: rows 0, 1, 3, 4, 5) and RS(5,5)'s
+    one-encode parity."""
+    import chunky_ec as ce
+    m = np.array(ce.ReedSolomon(5, 5).matrix(), dtype=np.uint8)
+    assert m[[0, 1, 3, 4, 5]].tolist() == kats["matrix_inverse"][1]["m"]
+    k = kats["rs_one_encode"]
+    data = np.array(k["data"], np.uint8)
+    par = [[0, 0] for _ in range(5)]
+    for r in range(5):
+        for j in range(5):
+            for c in range(2):
+                par[r][c] ^= oracle.gf_mul(int(m[5 + r, j]), int(data[j, c]))
+    assert par == k["parity"]
+
+
 def test_codec_new_errors():
     import chunky_ec as ce
     for (d, p), code in [((0, 1), ce.TOO_FEW_DATA_SHARDS), ((1, 0), ce.TOO_FEW_PARITY_SHARDS),

@@ -2,7 +2,8 @@
 
 - the reference's own SHA-256 KAT (reference tests/hash.rs:7-8) and FIPS 180-2 vectors;
 - hashlib (OpenSSL) on every length class, scalar and SHA-NI paths;
-- the crate's / JavaReedSolomon's published GF and RS(5,5) known answers;
+- the crate's / JavaReedSolomon's / klauspost's published GF, matrix-inverse and RS(5,5) known
+  answers;
 - structural properties of the coding matrix and reconstruct (first-d-present rule);
 - the committed golden vectors (tests/golden/golden_vectors.json) reproduce exactly.
 """
@@ -68,6 +69,37 @@ def test_rs_one_encode_kat(kats):
     st, par = oracle.encode_sep(k["data_shards"], k["parity_shards"], k["data"])
     assert st == 0
     assert [list(map(int, x)) for x in par] == k["parity"]
+
+
+def test_gf_mul_slice_kat(kats):
+    for v in kats["gf_mul_slice"]:
+        assert [oracle.gf_mul(v["c"], x) for x in v["in"]] == v["out"]
+
+
+def _gf_matmul(a, b):
+    out = np.zeros((len(a), len(b[0])), np.uint8)
+    for i, j in itertools.product(range(len(a)), range(len(b[0]))):
+        acc = 0
+        for k in range(len(b)):
+            acc ^= oracle.gf_mul(int(a[i][k]), int(b[k][j]))
+        out[i, j] = acc
+    return out
+
+
+def test_matrix_kats(kats):
+    """The crate's / JavaReedSolomon's matrix tests: the Gauss-Jordan inversion the decode path
+    uses (oracle/cec_oracle.c gf_invert), and GF matrix products."""
+    for v in kats["matrix_inverse"]:
+        m = np.array(v["m"], np.uint8)
+        inv = oracle.gf_invert(m)
+        assert inv.tolist() == v["inv"]
+        assert np.array_equal(_gf_matmul(m, inv), np.eye(len(m), dtype=np.uint8))
+    for v in kats["matrix_multiply"]:
+        assert _gf_matmul(v["a"], v["b"]).tolist() == v["ab"]
+    # the second inverse case is RS(5,5)'s decode matrix for data shard 2 lost: coding-matrix
+    # rows 0, 1, 3, 4 and the first parity row (so it also pins that row of V * inv(V_top))
+    m = np.array(kats["matrix_inverse"][1]["m"], np.uint8)
+    assert np.array_equal(oracle.coding_matrix(5, 5)[[0, 1, 3, 4, 5]], m)
 
 
 @pytest.mark.parametrize("d,p", [(1, 1), (3, 2), (10, 4), (20, 8), (5, 5), (128, 128), (255, 1)])
