@@ -94,6 +94,9 @@ def test_matrix_kats(kats):
         inv = oracle.gf_invert(m)
         assert inv.tolist() == v["inv"]
         assert np.array_equal(_gf_matmul(m, inv), np.eye(len(m), dtype=np.uint8))
+    for m in kats["matrix_singular"]:
+        with pytest.raises(ValueError):
+            oracle.gf_invert(np.array(m, np.uint8))
     for v in kats["matrix_multiply"]:
         assert _gf_matmul(v["a"], v["b"]).tolist() == v["ab"]
     # the second inverse case is RS(5,5)'s decode matrix for data shard 2 lost: coding-matrix
