@@ -508,7 +508,7 @@ def run_stream(args, cfg, codec, world, rank, device, reduce_dev):
             f"threads from a pageable source ring ({ring_parts} distinct parts, "
             f"{size_label(ring.nbytes)}) into the pinned slot, global part number stamped",
             check_digests_vs_source=ok)), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 
@@ -544,7 +544,7 @@ def run_read_stream(args, cfg, codec, world, rank, device, reduce_dev):
             f"region by {threads} host threads into the pinned slot, {args.corrupt:g} of the "
             "fetched chunks damaged (seeded), failed parts retried",
             read_repair=stats, check_vs_stored=ok, checks=checks)), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 
@@ -1143,9 +1143,11 @@ def main():
     # own threads), 8 at most
     e2e_threads = _rank_threads(world)
     # RCCL ("nccl") carries only the barrier and the max-over-ranks all-reduce.
-    # CEC_BENCH_BACKEND=gloo rehearses N > 1 with several ranks on one GPU.
+    # CEC_BENCH_BACKEND=gloo rehearses N > 1 with several ranks on one GPU; CEC_BENCH_PG=1 starts
+    # the process group at world 1 too, so one GPU runs the N > 1 line's RCCL branch (init with
+    # device_id, barriers, the float64 all-reduces, the per-rank rows).
     backend = os.environ.get("CEC_BENCH_BACKEND", "nccl")
-    if world > 1:
+    if world > 1 or os.environ.get("CEC_BENCH_PG") == "1":
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=device)
         else:
@@ -1410,7 +1412,7 @@ def main():
     # per-rank figures for the N > 1 line (a straggler or a cross-NUMA placement must be
     # visible from the line alone)
     ranks = node = None
-    if world > 1:
+    if dist.is_initialized():
         e2e_v, link_v = (e2e or {}).get("_local") or (0.0, 0.0)
         rr_v = ((e2e or {}).get("read_repair") or {}).get("_local") or 0.0
         # each rank's own north_star / C3 / C4 figures (the blocks run on every rank, on its
@@ -1496,7 +1498,7 @@ def main():
                                                 quota)
         print(json.dumps(line), flush=True)
 
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -17,9 +17,19 @@ def part_range(n_parts: int, rank: int, world: int) -> Tuple[int, int]:
     return n_parts * rank // world, n_parts * (rank + 1) // world
 
 
+def collective(world: int) -> bool:
+    """Whether the rank helpers below go through torch.distributed: world > 1, or a process group
+    was initialised at world 1 (bench.py's CEC_BENCH_PG=1 rehearsal of the RCCL branch on one
+    GPU)."""
+    if world > 1:
+        return True
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized()
+
+
 def max_over_ranks(x: float, world: int, device=None) -> float:
     """Max of a per-rank float over all ranks (the step time the bench reports)."""
-    if world == 1:
+    if not collective(world):
         return x
     import torch
     import torch.distributed as dist
@@ -32,7 +42,7 @@ def gather_rows(row, world: int, device=None):
     """Every rank's `row` (a list of floats of the same length on every rank), in rank order, on
     every rank (a collective: every rank must call it).  A SUM all-reduce of a [world][k] zero
     tensor with each rank's own row filled in, so it works on gloo and on RCCL alike."""
-    if world == 1:
+    if not collective(world):
         return [list(map(float, row))]
     import torch
     import torch.distributed as dist
@@ -50,7 +60,7 @@ def all_ranks_ok(ok: bool, world: int, device=None) -> bool:
 
 
 def barrier(world: int) -> None:
-    if world > 1:
+    if collective(world):
         import torch.distributed as dist
         dist.barrier()
 

@@ -105,3 +105,34 @@ def test_gloo_sharding_matches_single_process(world):
             assert not (set(merged) & set(part_map))  # disjoint ownership
             merged.update(part_map)
         assert merged == single
+
+
+def _single_pg_worker(port, out_q):
+    import torch.distributed as dist
+    from chunky_ec import sharding
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    before = sharding.collective(1)
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    calls = []
+    real = dist.all_reduce
+    dist.all_reduce = lambda *a, **k: (calls.append(1), real(*a, **k))[1]
+    try:
+        out_q.put((before, sharding.collective(1), sharding.max_over_ranks(2.5, 1),
+                   sharding.gather_rows([1, 2], 1), sharding.all_ranks_ok(True, 1), len(calls)))
+        sharding.barrier(1)
+    finally:
+        dist.all_reduce = real
+        dist.destroy_process_group()
+
+
+def test_world1_process_group_takes_collective_path():
+    """bench.py's CEC_BENCH_PG=1 rehearsal: with a process group at world 1 the rank helpers go
+    through torch.distributed (3 all-reduces), with the same results as without one."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    pr = ctx.Process(target=_single_pg_worker, args=(_free_port(), q))
+    pr.start()
+    res = q.get(timeout=120)
+    pr.join(60)
+    assert pr.exitcode == 0
+    assert res == (False, True, 2.5, [[1.0, 2.0]], True, 3)
