@@ -21,8 +21,8 @@ The default (c2) line also carries: `north_star` (RS(10,4) encode and 2-erasure 
 on the headline's buffer, fractions of 8 TB/s), `baseline_configs` (BASELINE configs[2] C3 and
 configs[3] C4 per GPU), `end_to_end` (host-produced write stream, read + repair stream with
 damaged fetches retried, the PCIe link alone, the one-process scheduler path), and at N = 1
-`check_vs_oracle` (whole sampled parts of those buffers against the oracle, in the cpu_baseline
-leg).  At N > 1: `ranks` (each rank's own figures) and `node` (configs[3] and C3 at node level).
+`check_vs_oracle` (whole sampled parts of those buffers against the oracle, and every headline
+part's d+p digests against the oracle's encode + SHA-256 of its data, in the cpu_baseline leg).  At N > 1: `ranks` (each rank's own figures) and `node` (configs[3] and C3 at node level).
 `--config c5` / `c5r` run BASELINE configs[4]: a `--stream-gib` (1 TiB) stream fed per batch
 from pageable rings, written, or read back with `--corrupt` of the fetched chunks damaged.
 """
@@ -734,7 +734,17 @@ def snapshot_parts(buf, digests, parts):
             for k in parts]
 
 
-def check_vs_oracle(snap, d, p):
+def snapshot_data(buf, d, slab=256):
+    """Host copy of the d data chunks of every part of a device batch ([n][d][L], pageable), slab
+    by slab: the input of the cpu_baseline leg's whole-batch digest check."""
+    n, _, L = buf.shape
+    host = torch.empty((n, d, L), dtype=torch.uint8)
+    for k in range(0, n, slab):
+        host[k:k + slab].copy_(buf[k:k + slab, :d])
+    return host.numpy()
+
+
+def check_vs_oracle(snap, d, p, threads=16):
     """cpu_baseline leg: the sampled parts of the default line's own buffers against the CPU
     restatement of the reference crates (oracle.encode_sep, the galois_8 table path) and
     hashlib SHA-256:
@@ -742,7 +752,11 @@ def check_vs_oracle(snap, d, p):
       north_star      -- the parity the north_star encode (bit-sliced kernel) rewrote;
       c3_reconstruct  -- every chunk after C3's 1-4 erasures were rebuilt (data + parity);
       c4_encode_hash  -- RS(20,8) parity + 28 digests of the fused kernel (C4's buffer);
-      c4_round_trip   -- the same C4 parts after 8 erasures and reconstruct."""
+      c4_round_trip   -- the same C4 parts after 8 erasures and reconstruct;
+      headline_all_parts -- every part of the headline batch: the fused kernel's d+p digests
+                         against oracle.encode_hash_parts (encode_sep + SHA-256 on `threads` CPU
+                         workers) of the data chunks copied down after the timed launches, so
+                         the parity of all parts is pinned through its digests."""
     import hashlib
 
     import numpy as np
@@ -776,7 +790,15 @@ def check_vs_oracle(snap, d, p):
         if "c4_round_trip" in snap:
             res["c4_round_trip"] = all(np.array_equal(part, first[k])
                                        for k, part, _ in snap["c4_round_trip"])
-    return {"ok": all(res.values()), "checks": res, "parts": list(snap["parts"]),
+    extra = {}
+    if "headline_data" in snap:
+        want = oracle.encode_hash_parts(d, p, snap["headline_data"], threads)
+        got = snap["headline_digests"]
+        bad = np.nonzero((want != got).any(axis=(1, 2)))[0]
+        res["headline_all_parts"] = bad.size == 0
+        extra = {"all_parts_digests_compared": int(want.shape[0] * want.shape[1]),
+                 "all_parts_mismatched": [int(k) for k in bad[:8]]}
+    return {"ok": all(res.values()), "checks": res, "parts": list(snap["parts"]), **extra,
             "erased_in_c3": {str(k): v for k, v in snap.get("c3_erased", {}).items()},
             "basis": "whole parts (all chunks) copied from the buffers that produced value, "
                      "north_star and baseline_configs, compared with oracle.encode_sep (CPU "
@@ -1089,6 +1111,9 @@ def main():
     ap.add_argument("--parts", type=int, default=None, help="override parts per GPU")
     ap.add_argument("--shape", default=None, help="d,p override for the encode-only configs")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-full-check", action="store_true",
+                    help="c2: check only the sampled parts against the oracle, not every part's "
+                         "digests")
     ap.add_argument("--e2e-gib", type=float, default=64.0,
                     help="c2: GiB per GPU of the PCIe-bound end-to-end figure (0 = skip)")
     ap.add_argument("--check", action="store_true", help="verify a sampled part vs the oracle")
@@ -1391,6 +1416,9 @@ def main():
     if (args.config == "c2" and fused and world == 1 and not args.no_cpu_baseline):
         snap = {"parts": (0, n_parts // 2, n_parts - 1)}
         snap["headline"] = snapshot_parts(buf, digests, snap["parts"])
+        if not args.no_full_check:
+            snap["headline_digests"] = digests.cpu().numpy()
+            snap["headline_data"] = snapshot_data(buf, d)
     # north_star's two >= 60 % targets on the same buffer (C2 only)
     nstar = None
     if args.config == "c2" and not args.separate and not args.no_north_star:
@@ -1486,14 +1514,17 @@ def main():
         if world == 1 and not args.no_cpu_baseline and cfg["op"] in ("encode_hash", "encode"):
             # the cpu_baseline leg (after every timed region), the one place the bench runs the
             # oracle: first the sampled full-size parts of this run's buffers against it
-            if snap is not None:
-                detail = check_vs_oracle(snap, d, p)
-                line["check_vs_oracle"] = detail["ok"]
-                line["check_vs_oracle_detail"] = detail
             # the process's full CPU set (the main thread was bound to GPU0's NUMA node above)
             os.sched_setaffinity(0, full_affinity)
             avail, quota = len(full_affinity), cpu_quota()[1]
             threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, avail)
+            if snap is not None:
+                t0 = time.perf_counter()
+                detail = check_vs_oracle(snap, d, p, threads)
+                detail["seconds"] = round(time.perf_counter() - t0, 2)
+                snap.pop("headline_data", None)
+                line["check_vs_oracle"] = detail["ok"]
+                line["check_vs_oracle_detail"] = detail
             line["cpu_baseline"] = cpu_baseline(cfg, threads, os.cpu_count() or avail, avail,
                                                 quota)
         print(json.dumps(line), flush=True)

@@ -73,6 +73,10 @@ def lib() -> ctypes.CDLL:
             ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t,
             ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
         ]
+        L.or_encode_hash_parts.argtypes = [
+            ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, u8p,
+            ctypes.c_size_t, u8p, ctypes.c_int,
+        ]
         _lib = L
     return _lib
 
@@ -194,6 +198,19 @@ def part_encode(d: int, p: int, data_buf: np.ndarray, length: int):
     if st:
         raise ValueError(st)
     return cs.value, par[: p * L].reshape(p, L), dig.reshape(d + p, 32)
+
+
+def encode_hash_parts(d: int, p: int, data: np.ndarray, threads: int) -> np.ndarray:
+    """Digests [n][d+p][32] of the full parts in `data` ([n][d][L] uint8, C-contiguous):
+    encode_sep then SHA-256 of every chunk, as part_encode does, over `threads` workers."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    n, dd, L = data.shape
+    assert dd == d
+    out = np.zeros((n, d + p, 32), dtype=np.uint8)
+    st = lib().or_encode_hash_parts(d, p, L, n, _u8p(data), d * L, _u8p(out), threads)
+    if st:
+        raise ValueError(st)
+    return out
 
 
 def baseline_encode_sha(d: int, p: int, L: int, total_parts: int, pool: int, threads: int,

@@ -603,3 +603,69 @@ int or_baseline_encode_sha(size_t d, size_t p, size_t L, size_t total_parts, siz
     pthread_mutex_destroy(&c.mu);
     return OR_OK;
 }
+
+/* ------------------------------------------------------------------------------------------ */
+/* Checker: FilePart::write_with_encoder's digests for a whole batch of full parts            */
+/* ------------------------------------------------------------------------------------------ */
+
+typedef struct {
+    size_t d, p, L, n_parts, part_stride;
+    const uint8_t* data;
+    uint8_t* digests;
+    int shani;
+    volatile size_t next;
+    pthread_mutex_t mu;
+} digest_ctx;
+
+static void* digest_worker(void* a_) {
+    digest_ctx* c = (digest_ctx*)a_;
+    size_t d = c->d, p = c->p, L = c->L;
+    const uint8_t* rows[256];
+    uint8_t* m = (uint8_t*)malloc((d + p) * d);
+    uint8_t* par = (uint8_t*)malloc(p * L);
+    or_rs_matrix(d, p, m);
+    for (size_t i = 0; i < p; i++) rows[i] = m + (d + i) * d;
+    for (;;) {
+        pthread_mutex_lock(&c->mu);
+        size_t part = c->next++;
+        pthread_mutex_unlock(&c->mu);
+        if (part >= c->n_parts) break;
+        const uint8_t* base = c->data + part * c->part_stride;
+        const uint8_t* in[256];
+        uint8_t* out[256];
+        for (size_t j = 0; j < d; j++) in[j] = base + j * L;
+        for (size_t i = 0; i < p; i++) out[i] = par + i * L;
+        code_some_slices(rows, d, in, p, out, L);
+        uint8_t* dig = c->digests + part * (d + p) * 32;
+        for (size_t j = 0; j < d; j++) sha256_impl(in[j], L, dig + 32 * j, c->shani);
+        for (size_t i = 0; i < p; i++) sha256_impl(out[i], L, dig + 32 * (d + i), c->shani);
+    }
+    free(par);
+    free(m);
+    return NULL;
+}
+
+/*
+ * digests[n_parts][d+p][32] of n_parts full parts whose d data chunks (L bytes each, back to
+ * back) start `part_stride` bytes apart in `data`: encode_sep (file_part.rs:161-165) then
+ * Sha256Hash::from_buf of each chunk in order (:185), over n_threads workers.  The bench's
+ * cpu_baseline leg checks a whole device batch's digests with it.
+ */
+int or_encode_hash_parts(size_t d, size_t p, size_t L, size_t n_parts, const uint8_t* data,
+                         size_t part_stride, uint8_t* digests, int n_threads) {
+    gf_ready();
+    if (d == 0 || p == 0 || d + p > 256 || L == 0 || n_threads <= 0 || part_stride < d * L)
+        return OR_INVALID_ARGUMENT;
+    digest_ctx c;
+    memset(&c, 0, sizeof c);
+    c.d = d; c.p = p; c.L = L; c.n_parts = n_parts; c.part_stride = part_stride;
+    c.data = data; c.digests = digests;
+    c.shani = or_cpu_has_shani();
+    pthread_mutex_init(&c.mu, NULL);
+    pthread_t* th = (pthread_t*)calloc((size_t)n_threads, sizeof(pthread_t));
+    for (int t = 0; t < n_threads; t++) pthread_create(&th[t], NULL, digest_worker, &c);
+    for (int t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
+    free(th);
+    pthread_mutex_destroy(&c.mu);
+    return OR_OK;
+}

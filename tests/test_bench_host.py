@@ -187,3 +187,33 @@ def test_node_figures_from_rank_rows():
     rows[1][12] = 0
     assert "c4_encode_hash" not in bench.node_figures(
         [bench.rank_row(r, row) for r, row in enumerate(rows)])
+
+
+def test_check_vs_oracle_whole_batch_digests():
+    """The cpu_baseline leg's whole-batch check: every part's digests against the oracle's
+    encode + SHA-256 of its data; a single wrong digest is reported with its part."""
+    import torch
+
+    import oracle
+    d, p, L, n = 3, 2, 512, 6
+    t = d + p
+    rng = np.random.default_rng(5)
+    data = rng.integers(0, 256, (n, d, L), dtype=np.uint8)
+    dig = oracle.encode_hash_parts(d, p, data, 2)
+    full = np.zeros((n, t, L), np.uint8)
+    full[:, :d] = data
+    for k in range(n):
+        st, par = oracle.encode_sep(d, p, list(data[k]))
+        full[k, d:] = np.stack(par)
+    buf = torch.from_numpy(full)
+    snap = {"parts": (0, n - 1)}
+    snap["headline"] = bench.snapshot_parts(buf, torch.from_numpy(dig), snap["parts"])
+    snap["headline_digests"] = dig.copy()
+    snap["headline_data"] = bench.snapshot_data(buf, d, slab=4)
+    assert np.array_equal(snap["headline_data"], data)
+    det = bench.check_vs_oracle(snap, d, p, 2)
+    assert det["ok"] and det["checks"]["headline_all_parts"]
+    assert det["all_parts_digests_compared"] == n * t and det["all_parts_mismatched"] == []
+    snap["headline_digests"][4, t - 1, 7] ^= 1  # one parity digest of part 4
+    det = bench.check_vs_oracle(snap, d, p, 2)
+    assert not det["ok"] and det["all_parts_mismatched"] == [4]

@@ -66,6 +66,10 @@ def test_default_line_checks_vs_oracle_small():
     assert line["check_vs_oracle"] is True
     det = line["check_vs_oracle_detail"]["checks"]
     assert det["headline"] is True and det["north_star_encode"] is True
+    # every part's 14 digests against the oracle's encode + SHA-256 of its data
+    assert det["headline_all_parts"] is True
+    assert line["check_vs_oracle_detail"]["all_parts_digests_compared"] == 64 * 14
+    assert line["check_vs_oracle_detail"]["all_parts_mismatched"] == []
 
 
 def test_end_to_end_read_repair_small():

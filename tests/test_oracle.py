@@ -281,3 +281,18 @@ def test_coding_matrix_by_lagrange_interpolation():
     assert lagrange_row(3, 3) == [1, 1, 1] and lagrange_row(3, 4) == [15, 8, 6]
     assert lagrange_row(10, 10) == [129, 150, 175, 184, 210, 196, 254, 232, 3, 2]
     assert lagrange_row(10, 12) == [191, 214, 98, 10, 6, 111, 223, 183, 5, 4]
+
+
+@pytest.mark.parametrize("d,p,L", [(10, 4, 4096), (3, 2, 683), (20, 8, 1000), (1, 1, 64)])
+def test_encode_hash_parts_matches_part_encode(d, p, L):
+    """The bench's whole-batch digest checker equals part_encode + hashlib, part by part."""
+    n = 9
+    data = gen_bytes(d * 7 + p + L, n * d * L).reshape(n, d, L)
+    for threads in (1, 3):
+        dg = oracle.encode_hash_parts(d, p, data, threads)
+        for k in range(n):
+            cs, par, dig = oracle.part_encode(d, p, data[k].reshape(-1), d * L)
+            assert cs == L and np.array_equal(dg[k], dig)
+            chunks = list(data[k]) + list(par)
+            assert [hashlib.sha256(c.tobytes()).digest() for c in chunks] == \
+                [dg[k, i].tobytes() for i in range(d + p)]
