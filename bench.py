@@ -756,7 +756,8 @@ def check_vs_oracle(snap, d, p, threads=16):
       headline_all_parts -- every part of the headline batch: the fused kernel's d+p digests
                          against oracle.encode_hash_parts (encode_sep + SHA-256 on `threads` CPU
                          workers) of the data chunks copied down after the timed launches, so
-                         the parity of all parts is pinned through its digests."""
+                         the parity of all parts is pinned through its digests;
+      c4_all_parts    -- the same for every part of C4's RS(20,8) batch."""
     import hashlib
 
     import numpy as np
@@ -798,6 +799,13 @@ def check_vs_oracle(snap, d, p, threads=16):
         res["headline_all_parts"] = bad.size == 0
         extra = {"all_parts_digests_compared": int(want.shape[0] * want.shape[1]),
                  "all_parts_mismatched": [int(k) for k in bad[:8]]}
+    if "c4_data" in snap:
+        c4 = CONFIGS["c4"]
+        want = oracle.encode_hash_parts(c4["d"], c4["p"], snap["c4_data"], threads)
+        bad = np.nonzero((want != snap["c4_digests"]).any(axis=(1, 2)))[0]
+        res["c4_all_parts"] = bad.size == 0
+        extra["c4_all_parts_digests_compared"] = int(want.shape[0] * want.shape[1])
+        extra["c4_all_parts_mismatched"] = [int(k) for k in bad[:8]]
     return {"ok": all(res.values()), "checks": res, "parts": list(snap["parts"]), **extra,
             "erased_in_c3": {str(k): v for k, v in snap.get("c3_erased", {}).items()},
             "basis": "whole parts (all chunks) copied from the buffers that produced value, "
@@ -963,6 +971,9 @@ def baseline_configs_block(codec, batch, buf, digests, stream, device, rank, d, 
     ms = timed(lambda: ce.encode_hash_batch(codec4, b4, dig4.data_ptr(), stream))
     if snap is not None:  # RS(20,8) parity + all 28 digests of the fused kernel
         snap["c4_encode_hash"] = snapshot_parts(buf4, dig4, (0, n4 - 1))
+        if "headline_data" in snap:  # and every part's digests (the whole-batch check)
+            snap["c4_digests"] = dig4.cpu().numpy()
+            snap["c4_data"] = snapshot_data(buf4, d4)
     data_gbs = n4 * d4 * L4 / (ms / 1e3) / 1e9
     hbm = n4 * t4 * (L4 + 32) / (ms / 1e3) / 1e9
     g = torch.Generator().manual_seed(2828 + rank)
@@ -1523,6 +1534,7 @@ def main():
                 detail = check_vs_oracle(snap, d, p, threads)
                 detail["seconds"] = round(time.perf_counter() - t0, 2)
                 snap.pop("headline_data", None)
+                snap.pop("c4_data", None)
                 line["check_vs_oracle"] = detail["ok"]
                 line["check_vs_oracle_detail"] = detail
             line["cpu_baseline"] = cpu_baseline(cfg, threads, os.cpu_count() or avail, avail,

@@ -217,3 +217,16 @@ def test_check_vs_oracle_whole_batch_digests():
     snap["headline_digests"][4, t - 1, 7] ^= 1  # one parity digest of part 4
     det = bench.check_vs_oracle(snap, d, p, 2)
     assert not det["ok"] and det["all_parts_mismatched"] == [4]
+    snap["headline_digests"][4, t - 1, 7] ^= 1
+    # C4's batch (the config's RS(20,8) shape), 3 small parts
+    c4 = bench.CONFIGS["c4"]
+    d4, p4 = c4["d"], c4["p"]
+    c4_data = rng.integers(0, 256, (3, d4, 256), dtype=np.uint8)
+    snap["c4_data"] = c4_data
+    snap["c4_digests"] = oracle.encode_hash_parts(d4, p4, c4_data, 2)
+    det = bench.check_vs_oracle(snap, d, p, 2)
+    assert det["ok"] and det["checks"]["c4_all_parts"]
+    assert det["c4_all_parts_digests_compared"] == 3 * (d4 + p4)
+    snap["c4_digests"][1, 0, 0] ^= 0x80  # a data digest of part 1
+    det = bench.check_vs_oracle(snap, d, p, 2)
+    assert not det["ok"] and det["c4_all_parts_mismatched"] == [1]

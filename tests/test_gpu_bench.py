@@ -60,8 +60,8 @@ def test_reconstruct_config_line_small():
 
 
 def test_default_line_checks_vs_oracle_small():
-    """The default line's oracle leg on its own buffers (headline fused kernel + north_star's
-    bit-sliced re-encode at this size; C3 / C4 parts join at full size)."""
+    """The default line's oracle leg on its own buffers (headline fused kernel, north_star's
+    bit-sliced re-encode, C3 and C4 scaled to --parts) and the whole-batch digest checks."""
     line = _run("--parts", "64", "--steps", "1", "--warmup", "1", "--e2e-gib", "0")
     assert line["check_vs_oracle"] is True
     det = line["check_vs_oracle_detail"]["checks"]
@@ -70,6 +70,9 @@ def test_default_line_checks_vs_oracle_small():
     assert det["headline_all_parts"] is True
     assert line["check_vs_oracle_detail"]["all_parts_digests_compared"] == 64 * 14
     assert line["check_vs_oracle_detail"]["all_parts_mismatched"] == []
+    # C4's RS(20,8) batch (scaled with --parts: 64 parts) likewise, all 28 digests per part
+    assert det["c4_all_parts"] is True
+    assert line["check_vs_oracle_detail"]["c4_all_parts_digests_compared"] == 64 * 28
 
 
 def test_end_to_end_read_repair_small():
