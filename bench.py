@@ -734,14 +734,24 @@ def snapshot_parts(buf, digests, parts):
             for k in parts]
 
 
-def snapshot_data(buf, d, slab=256):
-    """Host copy of the d data chunks of every part of a device batch ([n][d][L], pageable), slab
-    by slab: the input of the cpu_baseline leg's whole-batch digest check."""
-    n, _, L = buf.shape
-    host = torch.empty((n, d, L), dtype=torch.uint8)
-    for k in range(0, n, slab):
-        host[k:k + slab].copy_(buf[k:k + slab, :d])
+def snapshot_all(buf, slab=256):
+    """Host copy of every chunk of every part of a device batch ([n][t][L], pageable), slab by
+    slab: the input of the cpu_baseline leg's whole-batch check."""
+    host = torch.empty(buf.shape, dtype=torch.uint8)
+    for k in range(0, buf.shape[0], slab):
+        host[k:k + slab].copy_(buf[k:k + slab])
     return host.numpy()
+
+
+def mismatched_parts(buf, host, slab=256):
+    """Parts of a device batch whose bytes differ from a host copy ([n][t][L]), slab by slab."""
+    import numpy as np
+    bad = []
+    for k in range(0, buf.shape[0], slab):
+        got = buf[k:k + slab].cpu().numpy()
+        diff = (got != host[k:k + slab]).reshape(got.shape[0], -1).any(axis=1)
+        bad.extend(int(k + i) for i in np.nonzero(diff)[0])
+    return bad
 
 
 def check_vs_oracle(snap, d, p, threads=16):
@@ -753,11 +763,13 @@ def check_vs_oracle(snap, d, p, threads=16):
       c3_reconstruct  -- every chunk after C3's 1-4 erasures were rebuilt (data + parity);
       c4_encode_hash  -- RS(20,8) parity + 28 digests of the fused kernel (C4's buffer);
       c4_round_trip   -- the same C4 parts after 8 erasures and reconstruct;
-      headline_all_parts -- every part of the headline batch: the fused kernel's d+p digests
-                         against oracle.encode_hash_parts (encode_sep + SHA-256 on `threads` CPU
-                         workers) of the data chunks copied down after the timed launches, so
-                         the parity of all parts is pinned through its digests;
-      c4_all_parts    -- the same for every part of C4's RS(20,8) batch."""
+      headline_all_parts -- every part of the headline batch, copied down after the timed
+                         launches: the fused kernel's d+p digests and parity against
+                         oracle.encode_hash_parts (encode_sep + SHA-256 of the data chunks on
+                         `threads` CPU workers);
+      c3_all_parts    -- every part after C3's 1-4 erasures and rebuild, byte for byte against
+                         that (oracle-checked) copy;
+      c4_all_parts    -- the headline_all_parts check for every part of C4's RS(20,8) batch."""
     import hashlib
 
     import numpy as np
@@ -792,20 +804,24 @@ def check_vs_oracle(snap, d, p, threads=16):
             res["c4_round_trip"] = all(np.array_equal(part, first[k])
                                        for k, part, _ in snap["c4_round_trip"])
     extra = {}
-    if "headline_data" in snap:
-        want = oracle.encode_hash_parts(d, p, snap["headline_data"], threads)
-        got = snap["headline_digests"]
-        bad = np.nonzero((want != got).any(axis=(1, 2)))[0]
-        res["headline_all_parts"] = bad.size == 0
-        extra = {"all_parts_digests_compared": int(want.shape[0] * want.shape[1]),
-                 "all_parts_mismatched": [int(k) for k in bad[:8]]}
-    if "c4_data" in snap:
+
+    def whole_batch(key, dd, pp, parts, digests):
+        want, par_ok = oracle.encode_hash_parts(dd, pp, parts, threads, check_parity=True)
+        bad = np.nonzero((want != digests).any(axis=(1, 2)) | ~par_ok)[0]
+        res[f"{key}_all_parts"] = bad.size == 0
+        extra[f"{key}_all_parts_checked"] = {"parts": int(want.shape[0]),
+                                             "digests": int(want.shape[0] * want.shape[1])}
+        extra[f"{key}_all_parts_mismatched"] = [int(k) for k in bad[:8]]
+
+    if "headline_all" in snap:
+        whole_batch("headline", d, p, snap["headline_all"], snap["headline_digests"])
+    if "c3_all_parts_mismatched" in snap:
+        bad = snap["c3_all_parts_mismatched"]
+        res["c3_all_parts"] = not bad
+        extra["c3_all_parts_mismatched"] = bad[:8]
+    if "c4_all" in snap:
         c4 = CONFIGS["c4"]
-        want = oracle.encode_hash_parts(c4["d"], c4["p"], snap["c4_data"], threads)
-        bad = np.nonzero((want != snap["c4_digests"]).any(axis=(1, 2)))[0]
-        res["c4_all_parts"] = bad.size == 0
-        extra["c4_all_parts_digests_compared"] = int(want.shape[0] * want.shape[1])
-        extra["c4_all_parts_mismatched"] = [int(k) for k in bad[:8]]
+        whole_batch("c4", c4["d"], c4["p"], snap["c4_all"], snap["c4_digests"])
     return {"ok": all(res.values()), "checks": res, "parts": list(snap["parts"]), **extra,
             "erased_in_c3": {str(k): v for k, v in snap.get("c3_erased", {}).items()},
             "basis": "whole parts (all chunks) copied from the buffers that produced value, "
@@ -942,6 +958,8 @@ def baseline_configs_block(codec, batch, buf, digests, stream, device, rank, d, 
     ms = timed(lambda: ce.reconstruct_batch(codec, batch, present, False, stream))
     if snap is not None:  # every chunk after the rebuild (each sampled part lost 1-4 of them)
         snap["c3_reconstruct"] = snapshot_parts(buf, None, snap["parts"])
+        if "headline_all" in snap:  # every part against the headline's bytes
+            snap["c3_all_parts_mismatched"] = mismatched_parts(buf, snap["headline_all"])
         snap["c3_erased"] = {k: [int(i) for i in (pres[k] == 0).nonzero().flatten()]
                              for k in snap["parts"]}
     touched = int((pres.sum(1) < t).sum().item())
@@ -971,9 +989,9 @@ def baseline_configs_block(codec, batch, buf, digests, stream, device, rank, d, 
     ms = timed(lambda: ce.encode_hash_batch(codec4, b4, dig4.data_ptr(), stream))
     if snap is not None:  # RS(20,8) parity + all 28 digests of the fused kernel
         snap["c4_encode_hash"] = snapshot_parts(buf4, dig4, (0, n4 - 1))
-        if "headline_data" in snap:  # and every part's digests (the whole-batch check)
+        if "headline_all" in snap:  # and every part (the whole-batch check)
             snap["c4_digests"] = dig4.cpu().numpy()
-            snap["c4_data"] = snapshot_data(buf4, d4)
+            snap["c4_all"] = snapshot_all(buf4)
     data_gbs = n4 * d4 * L4 / (ms / 1e3) / 1e9
     hbm = n4 * t4 * (L4 + 32) / (ms / 1e3) / 1e9
     g = torch.Generator().manual_seed(2828 + rank)
@@ -1429,7 +1447,7 @@ def main():
         snap["headline"] = snapshot_parts(buf, digests, snap["parts"])
         if not args.no_full_check:
             snap["headline_digests"] = digests.cpu().numpy()
-            snap["headline_data"] = snapshot_data(buf, d)
+            snap["headline_all"] = snapshot_all(buf)
     # north_star's two >= 60 % targets on the same buffer (C2 only)
     nstar = None
     if args.config == "c2" and not args.separate and not args.no_north_star:
@@ -1533,8 +1551,8 @@ def main():
                 t0 = time.perf_counter()
                 detail = check_vs_oracle(snap, d, p, threads)
                 detail["seconds"] = round(time.perf_counter() - t0, 2)
-                snap.pop("headline_data", None)
-                snap.pop("c4_data", None)
+                snap.pop("headline_all", None)
+                snap.pop("c4_all", None)
                 line["check_vs_oracle"] = detail["ok"]
                 line["check_vs_oracle_detail"] = detail
             line["cpu_baseline"] = cpu_baseline(cfg, threads, os.cpu_count() or avail, avail,

@@ -75,7 +75,7 @@ def lib() -> ctypes.CDLL:
         ]
         L.or_encode_hash_parts.argtypes = [
             ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, u8p,
-            ctypes.c_size_t, u8p, ctypes.c_int,
+            ctypes.c_size_t, u8p, ctypes.c_void_p, ctypes.c_int,
         ]
         _lib = L
     return _lib
@@ -200,17 +200,22 @@ def part_encode(d: int, p: int, data_buf: np.ndarray, length: int):
     return cs.value, par[: p * L].reshape(p, L), dig.reshape(d + p, 32)
 
 
-def encode_hash_parts(d: int, p: int, data: np.ndarray, threads: int) -> np.ndarray:
-    """Digests [n][d+p][32] of the full parts in `data` ([n][d][L] uint8, C-contiguous):
-    encode_sep then SHA-256 of every chunk, as part_encode does, over `threads` workers."""
-    data = np.ascontiguousarray(data, dtype=np.uint8)
-    n, dd, L = data.shape
-    assert dd == d
+def encode_hash_parts(d: int, p: int, parts: np.ndarray, threads: int,
+                      check_parity: bool = False):
+    """Digests [n][d+p][32] of the full parts in `parts` ([n][c][L] uint8, C-contiguous, c >= d:
+    the first d chunks of each part are its data): encode_sep then SHA-256 of every chunk, as
+    part_encode does, over `threads` workers.  With check_parity (c >= d+p) also returns
+    parity_ok [n] (bool): chunks d..d+p-1 of the part equal the computed parity."""
+    parts = np.ascontiguousarray(parts, dtype=np.uint8)
+    n, c, L = parts.shape
+    assert c >= d and (not check_parity or c >= d + p)
     out = np.zeros((n, d + p, 32), dtype=np.uint8)
-    st = lib().or_encode_hash_parts(d, p, L, n, _u8p(data), d * L, _u8p(out), threads)
+    match = np.zeros(n, dtype=np.uint8) if check_parity else None
+    st = lib().or_encode_hash_parts(d, p, L, n, _u8p(parts), c * L, _u8p(out),
+                                    None if match is None else match.ctypes.data, threads)
     if st:
         raise ValueError(st)
-    return out
+    return (out, match.astype(bool)) if check_parity else out
 
 
 def baseline_encode_sha(d: int, p: int, L: int, total_parts: int, pool: int, threads: int,

@@ -612,6 +612,7 @@ typedef struct {
     size_t d, p, L, n_parts, part_stride;
     const uint8_t* data;
     uint8_t* digests;
+    uint8_t* parity_match;
     int shani;
     volatile size_t next;
     pthread_mutex_t mu;
@@ -636,6 +637,8 @@ static void* digest_worker(void* a_) {
         for (size_t j = 0; j < d; j++) in[j] = base + j * L;
         for (size_t i = 0; i < p; i++) out[i] = par + i * L;
         code_some_slices(rows, d, in, p, out, L);
+        if (c->parity_match)
+            c->parity_match[part] = memcmp(par, base + d * L, p * L) == 0;
         uint8_t* dig = c->digests + part * (d + p) * 32;
         for (size_t j = 0; j < d; j++) sha256_impl(in[j], L, dig + 32 * j, c->shani);
         for (size_t i = 0; i < p; i++) sha256_impl(out[i], L, dig + 32 * (d + i), c->shani);
@@ -648,18 +651,22 @@ static void* digest_worker(void* a_) {
 /*
  * digests[n_parts][d+p][32] of n_parts full parts whose d data chunks (L bytes each, back to
  * back) start `part_stride` bytes apart in `data`: encode_sep (file_part.rs:161-165) then
- * Sha256Hash::from_buf of each chunk in order (:185), over n_threads workers.  The bench's
- * cpu_baseline leg checks a whole device batch's digests with it.
+ * Sha256Hash::from_buf of each chunk in order (:185), over n_threads workers.  With
+ * parity_match != NULL the p chunks that follow the data chunks in `data` (part_stride >=
+ * (d+p)*L) are compared with the computed parity: parity_match[part] = 1 if equal.  The bench's
+ * cpu_baseline leg checks a whole device batch with it.
  */
 int or_encode_hash_parts(size_t d, size_t p, size_t L, size_t n_parts, const uint8_t* data,
-                         size_t part_stride, uint8_t* digests, int n_threads) {
+                         size_t part_stride, uint8_t* digests, uint8_t* parity_match,
+                         int n_threads) {
     gf_ready();
-    if (d == 0 || p == 0 || d + p > 256 || L == 0 || n_threads <= 0 || part_stride < d * L)
+    if (d == 0 || p == 0 || d + p > 256 || L == 0 || n_threads <= 0 || part_stride < d * L ||
+        (parity_match && part_stride < (d + p) * L))
         return OR_INVALID_ARGUMENT;
     digest_ctx c;
     memset(&c, 0, sizeof c);
     c.d = d; c.p = p; c.L = L; c.n_parts = n_parts; c.part_stride = part_stride;
-    c.data = data; c.digests = digests;
+    c.data = data; c.digests = digests; c.parity_match = parity_match;
     c.shani = or_cpu_has_shani();
     pthread_mutex_init(&c.mu, NULL);
     pthread_t* th = (pthread_t*)calloc((size_t)n_threads, sizeof(pthread_t));

@@ -189,44 +189,56 @@ def test_node_figures_from_rank_rows():
         [bench.rank_row(r, row) for r, row in enumerate(rows)])
 
 
-def test_check_vs_oracle_whole_batch_digests():
-    """The cpu_baseline leg's whole-batch check: every part's digests against the oracle's
-    encode + SHA-256 of its data; a single wrong digest is reported with its part."""
+def test_check_vs_oracle_whole_batch():
+    """The cpu_baseline leg's whole-batch check: every part's digests and parity against the
+    oracle's encode + SHA-256 of its data, and C3's rebuilt batch byte for byte against that copy;
+    a single wrong digest, parity byte or rebuilt byte is reported with its part."""
     import torch
 
     import oracle
+
+    def batch(rng, d, p, L, n):
+        data = rng.integers(0, 256, (n, d, L), dtype=np.uint8)
+        full = np.zeros((n, d + p, L), np.uint8)
+        full[:, :d] = data
+        for k in range(n):
+            st, par = oracle.encode_sep(d, p, list(data[k]))
+            full[k, d:] = np.stack(par)
+        return full, oracle.encode_hash_parts(d, p, data, 2)
+
     d, p, L, n = 3, 2, 512, 6
     t = d + p
     rng = np.random.default_rng(5)
-    data = rng.integers(0, 256, (n, d, L), dtype=np.uint8)
-    dig = oracle.encode_hash_parts(d, p, data, 2)
-    full = np.zeros((n, t, L), np.uint8)
-    full[:, :d] = data
-    for k in range(n):
-        st, par = oracle.encode_sep(d, p, list(data[k]))
-        full[k, d:] = np.stack(par)
-    buf = torch.from_numpy(full)
+    full, dig = batch(rng, d, p, L, n)
+    buf = torch.from_numpy(full.copy())
     snap = {"parts": (0, n - 1)}
     snap["headline"] = bench.snapshot_parts(buf, torch.from_numpy(dig), snap["parts"])
     snap["headline_digests"] = dig.copy()
-    snap["headline_data"] = bench.snapshot_data(buf, d, slab=4)
-    assert np.array_equal(snap["headline_data"], data)
+    snap["headline_all"] = bench.snapshot_all(buf, slab=4)
+    assert np.array_equal(snap["headline_all"], full)
+    snap["c3_all_parts_mismatched"] = bench.mismatched_parts(buf, snap["headline_all"], slab=4)
     det = bench.check_vs_oracle(snap, d, p, 2)
-    assert det["ok"] and det["checks"]["headline_all_parts"]
-    assert det["all_parts_digests_compared"] == n * t and det["all_parts_mismatched"] == []
+    assert det["ok"] and det["checks"]["headline_all_parts"] and det["checks"]["c3_all_parts"]
+    assert det["headline_all_parts_checked"] == {"parts": n, "digests": n * t}
+    assert det["headline_all_parts_mismatched"] == []
     snap["headline_digests"][4, t - 1, 7] ^= 1  # one parity digest of part 4
     det = bench.check_vs_oracle(snap, d, p, 2)
-    assert not det["ok"] and det["all_parts_mismatched"] == [4]
+    assert not det["ok"] and det["headline_all_parts_mismatched"] == [4]
     snap["headline_digests"][4, t - 1, 7] ^= 1
+    snap["headline_all"][2, d, 100] ^= 1  # a parity byte of part 2 (its digest unchanged)
+    det = bench.check_vs_oracle(snap, d, p, 2)
+    assert not det["ok"] and det["headline_all_parts_mismatched"] == [2]
+    snap["headline_all"][2, d, 100] ^= 1
+    buf[5, 1, 9] ^= 0x40  # a rebuilt byte of part 5
+    assert bench.mismatched_parts(buf, snap["headline_all"], slab=4) == [5]
+    buf[5, 1, 9] ^= 0x40  # (a CPU tensor: the sampled snapshot of part 5 shares its memory)
     # C4's batch (the config's RS(20,8) shape), 3 small parts
     c4 = bench.CONFIGS["c4"]
     d4, p4 = c4["d"], c4["p"]
-    c4_data = rng.integers(0, 256, (3, d4, 256), dtype=np.uint8)
-    snap["c4_data"] = c4_data
-    snap["c4_digests"] = oracle.encode_hash_parts(d4, p4, c4_data, 2)
+    snap["c4_all"], snap["c4_digests"] = batch(rng, d4, p4, 256, 3)
     det = bench.check_vs_oracle(snap, d, p, 2)
     assert det["ok"] and det["checks"]["c4_all_parts"]
-    assert det["c4_all_parts_digests_compared"] == 3 * (d4 + p4)
+    assert det["c4_all_parts_checked"] == {"parts": 3, "digests": 3 * (d4 + p4)}
     snap["c4_digests"][1, 0, 0] ^= 0x80  # a data digest of part 1
     det = bench.check_vs_oracle(snap, d, p, 2)
     assert not det["ok"] and det["c4_all_parts_mismatched"] == [1]

@@ -296,3 +296,19 @@ def test_encode_hash_parts_matches_part_encode(d, p, L):
             chunks = list(data[k]) + list(par)
             assert [hashlib.sha256(c.tobytes()).digest() for c in chunks] == \
                 [dg[k, i].tobytes() for i in range(d + p)]
+
+
+def test_encode_hash_parts_parity_check():
+    """With check_parity the checker compares the parts' own parity chunks with the computed
+    ones: one flipped parity byte fails exactly that part, and the digests do not depend on it."""
+    d, p, L, n = 10, 4, 1000, 5
+    data = gen_bytes(77, n * d * L).reshape(n, d, L)
+    full = np.zeros((n, d + p, L), np.uint8)
+    full[:, :d] = data
+    for k in range(n):
+        full[k, d:] = np.stack(oracle.encode_sep(d, p, list(data[k]))[1])
+    dg, ok = oracle.encode_hash_parts(d, p, full, 2, check_parity=True)
+    assert ok.all() and np.array_equal(dg, oracle.encode_hash_parts(d, p, data, 2))
+    full[3, d + 2, 999] ^= 0x10
+    dg2, ok = oracle.encode_hash_parts(d, p, full, 2, check_parity=True)
+    assert ok.tolist() == [True, True, True, False, True] and np.array_equal(dg, dg2)
