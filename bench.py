@@ -326,11 +326,13 @@ def ring_part_digests(ring, part: int):
     return [hashlib.sha256(c.tobytes()).digest() for c in src]
 
 
-def timed_write(pl, fill, first: int, n_parts: int, world: int):
+def timed_write(pl, fill, first: int, n_parts: int, world: int, collect=None):
     """FileWriteBuilder::write's part loop through `pl` (cec_pipeline): parts [first, first +
     n_parts) produced by fill() into each acquired slot, then H2D, encode + SHA-256, D2H.  One
-    untimed warmup batch per slot, barrier, the timed stream, drain, barrier.  Returns (local
-    seconds, the slot of the last batch, its part count)."""
+    untimed warmup batch per slot, barrier, the timed stream, drain, barrier.  With `collect`
+    ([n_parts][d+p][32]) every batch's digests are copied out of its slot when the slot comes
+    round again (as the reference's writer takes each part's digests for its FileReference).
+    Returns (local seconds, the slot of the last batch, its part count)."""
     P, depth = pl.parts, pl.depth
     for _ in range(depth):
         slot, data = pl.acquire()
@@ -338,18 +340,46 @@ def timed_write(pl, fill, first: int, n_parts: int, world: int):
         pl.submit(slot, P)
     pl.drain()
     barrier(world)
+    held = {}
+
+    def take(slot):
+        if collect is not None and slot in held:
+            k, m = held.pop(slot)
+            collect[k - first:k - first + m] = pl.wait(slot)[1]
+
     t0 = time.perf_counter()
     part, end, last = first, first + n_parts, (0, 0)
     while part < end:
         slot, data = pl.acquire()
+        take(slot)
         n = min(P, end - part)
         fill(data, part, n)
         pl.submit(slot, n)
+        held[slot] = (part, n)
         part += n
         last = (slot, n)
     pl.drain()
+    for slot in list(held):
+        take(slot)
     barrier(world)
     return (time.perf_counter() - t0,) + last
+
+
+def stream_check(ring, digests, d, p, threads):
+    """cpu_baseline leg: every part of a ring-fed write stream that started at part 0 (part k =
+    ring part k mod R with its first 8 bytes set to k, ring_reader) against the oracle's encode +
+    SHA-256, lap by lap over the ring, stamped in place (the stream is over).  Returns the
+    mismatched parts."""
+    import numpy as np
+    import oracle
+    R, n = len(ring), len(digests)
+    bad = []
+    for k in range(0, n, R):
+        m = min(R, n - k)
+        ring[:m, 0, :8] = part_stamps(k, m)
+        want = oracle.encode_hash_parts(d, p, ring[:m], threads)
+        bad.extend(int(k + i) for i in np.nonzero((want != digests[k:k + m]).any(axis=(1, 2)))[0])
+    return bad
 
 
 def write_check(pl, ring, slot: int, n: int, last_part: int):
@@ -549,7 +579,7 @@ def run_read_stream(args, cfg, codec, world, rank, device, reduce_dev):
 
 
 def end_to_end(codec, d, p, L, gib, world, rank, reduce_dev, host_threads, device_ordinal,
-               device, corrupt):
+               device, corrupt, full_check=False):
     """North-star's PCIe-bound end-to-end figures beside the device-resident headline: the same
     RS(10,4) encode + SHA-256 with the parts produced in host memory, parity + digests landing
     back in it, `gib` GiB per rank (weak scaling like the headline), max over ranks.  Not
@@ -593,7 +623,9 @@ def end_to_end(codec, d, p, L, gib, world, rank, reduce_dev, host_threads, devic
     def stamp_only(data, part, n):
         data[:n, 0, :8] = part_stamps(part, n)
 
-    loc_ring, slot, n = timed_write(pl, ring_reader(ring, copier), 0, n_parts, world)
+    import numpy as np
+    collect = np.empty((n_parts, d + p, 32), np.uint8) if full_check else None
+    loc_ring, slot, n = timed_write(pl, ring_reader(ring, copier), 0, n_parts, world, collect)
     el_ring = max_over_ranks(loc_ring, world, reduce_dev)
     # the ring-fed batches are checked for the property that holds at any size: the digests of
     # the data chunks equal SHA-256 of the bytes the reader produced (sampled)
@@ -627,6 +659,8 @@ def end_to_end(codec, d, p, L, gib, world, rank, reduce_dev, host_threads, devic
     # the scheduler's pageable path (what `cp` through the C++ FileWriteBuilder batch takes)
     res["scheduler_pageable"] = scheduler_pageable(codec, d, p, L, ring, n_parts, world,
                                                    reduce_dev, device_ordinal)
+    if collect is not None:  # every part's digests, checked in the cpu_baseline leg
+        res["_stream"] = (ring, collect)
     del ring
     res["read_repair"] = read_repair_form(codec, d, p, L, n_parts, world, rank, reduce_dev,
                                           copier, device, corrupt)
@@ -1461,10 +1495,11 @@ def main():
     torch.cuda.empty_cache()
 
     # every rank streams its own share (barriers inside): the PCIe-inclusive figure
-    e2e = None
+    e2e = stream = None
     if args.config == "c2" and args.e2e_gib > 0 and not args.separate:
         e2e = end_to_end(codec, d, p, L, args.e2e_gib, world, rank, reduce_dev, e2e_threads,
-                         ordinal, device, args.corrupt)
+                         ordinal, device, args.corrupt,
+                         full_check=snap is not None and "headline_all" in snap)
 
     # per-rank figures for the N > 1 line (a straggler or a cross-NUMA placement must be
     # visible from the line alone)
@@ -1528,6 +1563,7 @@ def main():
             line["baseline_configs"] = others
         if e2e is not None:
             e2e.pop("_local", None)
+            stream = e2e.pop("_stream", None)
             (e2e.get("read_repair") or {}).pop("_local", None)
             line["end_to_end"] = e2e
         if ranks is not None:
@@ -1550,6 +1586,14 @@ def main():
             if snap is not None:
                 t0 = time.perf_counter()
                 detail = check_vs_oracle(snap, d, p, threads)
+                if stream is not None:  # every part of end_to_end's write stream
+                    bad = stream_check(stream[0], stream[1], d, p, threads)
+                    detail["checks"]["end_to_end_all_parts"] = not bad
+                    detail["end_to_end_all_parts_checked"] = {
+                        "parts": len(stream[1]), "digests": int(stream[1].size // 32)}
+                    detail["end_to_end_all_parts_mismatched"] = bad[:8]
+                    detail["ok"] = detail["ok"] and not bad
+                    stream = None
                 detail["seconds"] = round(time.perf_counter() - t0, 2)
                 snap.pop("headline_all", None)
                 snap.pop("c4_all", None)

@@ -242,3 +242,36 @@ def test_check_vs_oracle_whole_batch():
     snap["c4_digests"][1, 0, 0] ^= 0x80  # a data digest of part 1
     det = bench.check_vs_oracle(snap, d, p, 2)
     assert not det["ok"] and det["c4_all_parts_mismatched"] == [1]
+
+
+class _OracleWritePipeline(_FakeWritePipeline):
+    """The same slot contract, with the d + p digests of the oracle's encode + SHA-256."""
+
+    def __init__(self, d, p, L, parts, depth):
+        super().__init__(d, L, parts, depth)
+        self.p = p
+
+    def submit(self, slot, n):
+        import oracle
+        data = self.slots[slot][:n]
+        self.seen.append(data[:, 0, :8].copy().view(np.uint64).ravel().tolist())
+        self.dig[slot] = oracle.encode_hash_parts(self.d, self.p, data, 1)
+
+
+def test_write_stream_collects_every_digest_and_checks_them():
+    """end_to_end's full check: timed_write copies each batch's digests out when its slot comes
+    round again (and after the drain), and stream_check re-derives every part (ring part k mod R,
+    stamped with k) with the oracle; one wrong digest is reported with its part."""
+    c = bench.HostCopier(2)
+    try:
+        d, p, L, P, depth, n = 3, 2, 256, 4, 3, 23
+        ring = bench.source_ring(5, d, L, 11, c)  # 23 stream parts wrap the 5-part ring
+        pl = _OracleWritePipeline(d, p, L, P, depth)
+        got = np.full((n, d + p, 32), 0xEE, np.uint8)
+        bench.timed_write(pl, bench.ring_reader(ring, c), 0, n, 1, got)
+        assert not (got == 0xEE).all(axis=(1, 2)).any()  # every part's digests were collected
+        assert bench.stream_check(ring.copy(), got, d, p, 2) == []
+        got[17, d + 1, 3] ^= 1
+        assert bench.stream_check(ring.copy(), got, d, p, 2) == [17]
+    finally:
+        c.close()

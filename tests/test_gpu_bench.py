@@ -91,6 +91,20 @@ def test_end_to_end_read_repair_small():
     assert any(c["attempts"] > 1 for c in rr["checks"])
 
 
+def test_end_to_end_write_stream_checked_whole():
+    """With the cpu_baseline leg on, every part of end_to_end's ring-fed write stream is checked
+    against the oracle (3 GiB asked; the stream is at least 4 batches: 1 024 parts; the ring's
+    wrap-around is covered on the CPU, tests/test_bench_host.py)."""
+    line = _run("--parts", "64", "--steps", "1", "--warmup", "1", "--e2e-gib", "3",
+                "--no-north-star")
+    det = line["check_vs_oracle_detail"]
+    n = (3 << 30) // (10 << 20)
+    assert det["checks"]["end_to_end_all_parts"] is True and line["check_vs_oracle"] is True
+    assert det["end_to_end_all_parts_checked"] == {"parts": max(n, 4 * 256), "digests":
+                                                   max(n, 4 * 256) * 14}
+    assert det["end_to_end_all_parts_mismatched"] == []
+
+
 def test_stream_configs_small():
     """C5 and its verify/repair side at 4 GiB, fed from the pageable rings inside the timed
     region."""
