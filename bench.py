@@ -1578,8 +1578,8 @@ def main():
         line["host"] = host_report
         if world == 1 and not args.no_cpu_baseline and cfg["op"] in ("encode_hash", "encode"):
             # the cpu_baseline leg (after every timed region), the one place the bench runs the
-            # oracle: first the sampled full-size parts of this run's buffers against it
-            # the process's full CPU set (the main thread was bound to GPU0's NUMA node above)
+            # oracle: first this run's own buffers against it, then the timed CPU baseline; both
+            # on the process's full CPU set (the main thread was bound to GPU0's NUMA node above)
             os.sched_setaffinity(0, full_affinity)
             avail, quota = len(full_affinity), cpu_quota()[1]
             threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, avail)
@@ -1601,6 +1601,11 @@ def main():
                 line["check_vs_oracle_detail"] = detail
             line["cpu_baseline"] = cpu_baseline(cfg, threads, os.cpu_count() or avail, avail,
                                                 quota)
+        # the process's peak resident host memory (page-locked slots, rings, the full-check
+        # copies): what the run asks of the box
+        import resource
+        host_report["peak_rss_gib"] = round(
+            resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / (1 << 20), 1)
         print(json.dumps(line), flush=True)
 
     if dist.is_initialized():
