@@ -768,22 +768,18 @@ def snapshot_parts(buf, digests, parts):
             for k in parts]
 
 
-def snapshot_all(buf, slab=256):
-    """Host copy of every chunk of every part of a device batch ([n][t][L], pageable), slab by
-    slab: the input of the cpu_baseline leg's whole-batch check."""
-    host = torch.empty(buf.shape, dtype=torch.uint8)
-    for k in range(0, buf.shape[0], slab):
-        host[k:k + slab].copy_(buf[k:k + slab])
-    return host.numpy()
-
-
-def mismatched_parts(buf, host, slab=256):
-    """Parts of a device batch whose bytes differ from a host copy ([n][t][L]), slab by slab."""
+def batch_vs_oracle(dev, digests, d, p, threads, slab=256):
+    """cpu_baseline leg: every part of a device batch ([n][d+p][L], torch tensor; copied down
+    slab by slab) against the oracle: encode_sep of its data chunks must equal its parity chunks,
+    and SHA-256 of all d+p chunks must equal `digests` ([n][d+p][32], host).  Returns the
+    mismatched parts."""
     import numpy as np
+    import oracle
     bad = []
-    for k in range(0, buf.shape[0], slab):
-        got = buf[k:k + slab].cpu().numpy()
-        diff = (got != host[k:k + slab]).reshape(got.shape[0], -1).any(axis=1)
+    for k in range(0, dev.shape[0], slab):
+        host = dev[k:k + slab].cpu().numpy()
+        want, par_ok = oracle.encode_hash_parts(d, p, host, threads, check_parity=True)
+        diff = (want != digests[k:k + slab]).any(axis=(1, 2)) | ~par_ok
         bad.extend(int(k + i) for i in np.nonzero(diff)[0])
     return bad
 
@@ -797,13 +793,14 @@ def check_vs_oracle(snap, d, p, threads=16):
       c3_reconstruct  -- every chunk after C3's 1-4 erasures were rebuilt (data + parity);
       c4_encode_hash  -- RS(20,8) parity + 28 digests of the fused kernel (C4's buffer);
       c4_round_trip   -- the same C4 parts after 8 erasures and reconstruct;
-      headline_all_parts -- every part of the headline batch, copied down after the timed
-                         launches: the fused kernel's d+p digests and parity against
-                         oracle.encode_hash_parts (encode_sep + SHA-256 of the data chunks on
-                         `threads` CPU workers);
-      c3_all_parts    -- every part after C3's 1-4 erasures and rebuild, byte for byte against
-                         that (oracle-checked) copy;
-      c4_all_parts    -- the headline_all_parts check for every part of C4's RS(20,8) batch."""
+      c2_all_parts    -- every part of the C2 buffer as the device-resident blocks left it
+                         (the fused encode, north_star's re-encode and 2-erasure rebuild, C3's
+                         re-encode and 1-4-erasure rebuild of data + parity): its parity equals
+                         the oracle's encode_sep of its data, and SHA-256 of its 14 chunks the
+                         digests the fused kernel produced (oracle.encode_hash_parts, `threads`
+                         CPU workers, streamed down slab by slab: batch_vs_oracle);
+      c4_all_parts    -- the same for C4's RS(20,8) buffer after its fused encode and 8-erasure
+                         round trip."""
     import hashlib
 
     import numpy as np
@@ -839,23 +836,18 @@ def check_vs_oracle(snap, d, p, threads=16):
                                        for k, part, _ in snap["c4_round_trip"])
     extra = {}
 
-    def whole_batch(key, dd, pp, parts, digests):
-        want, par_ok = oracle.encode_hash_parts(dd, pp, parts, threads, check_parity=True)
-        bad = np.nonzero((want != digests).any(axis=(1, 2)) | ~par_ok)[0]
-        res[f"{key}_all_parts"] = bad.size == 0
-        extra[f"{key}_all_parts_checked"] = {"parts": int(want.shape[0]),
-                                             "digests": int(want.shape[0] * want.shape[1])}
-        extra[f"{key}_all_parts_mismatched"] = [int(k) for k in bad[:8]]
+    def whole_batch(key, dd, pp, dev, digests):
+        bad = batch_vs_oracle(dev, digests, dd, pp, threads)
+        res[f"{key}_all_parts"] = not bad
+        extra[f"{key}_all_parts_checked"] = {"parts": int(digests.shape[0]),
+                                             "digests": int(digests.shape[0] * digests.shape[1])}
+        extra[f"{key}_all_parts_mismatched"] = bad[:8]
 
-    if "headline_all" in snap:
-        whole_batch("headline", d, p, snap["headline_all"], snap["headline_digests"])
-    if "c3_all_parts_mismatched" in snap:
-        bad = snap["c3_all_parts_mismatched"]
-        res["c3_all_parts"] = not bad
-        extra["c3_all_parts_mismatched"] = bad[:8]
-    if "c4_all" in snap:
+    if "c2_dev" in snap:
+        whole_batch("c2", d, p, snap["c2_dev"], snap["c2_digests"])
+    if "c4_dev" in snap:
         c4 = CONFIGS["c4"]
-        whole_batch("c4", c4["d"], c4["p"], snap["c4_all"], snap["c4_digests"])
+        whole_batch("c4", c4["d"], c4["p"], snap["c4_dev"], snap["c4_digests"])
     return {"ok": all(res.values()), "checks": res, "parts": list(snap["parts"]), **extra,
             "erased_in_c3": {str(k): v for k, v in snap.get("c3_erased", {}).items()},
             "basis": "whole parts (all chunks) copied from the buffers that produced value, "
@@ -992,8 +984,6 @@ def baseline_configs_block(codec, batch, buf, digests, stream, device, rank, d, 
     ms = timed(lambda: ce.reconstruct_batch(codec, batch, present, False, stream))
     if snap is not None:  # every chunk after the rebuild (each sampled part lost 1-4 of them)
         snap["c3_reconstruct"] = snapshot_parts(buf, None, snap["parts"])
-        if "headline_all" in snap:  # every part against the headline's bytes
-            snap["c3_all_parts_mismatched"] = mismatched_parts(buf, snap["headline_all"])
         snap["c3_erased"] = {k: [int(i) for i in (pres[k] == 0).nonzero().flatten()]
                              for k in snap["parts"]}
     touched = int((pres.sum(1) < t).sum().item())
@@ -1023,9 +1013,9 @@ def baseline_configs_block(codec, batch, buf, digests, stream, device, rank, d, 
     ms = timed(lambda: ce.encode_hash_batch(codec4, b4, dig4.data_ptr(), stream))
     if snap is not None:  # RS(20,8) parity + all 28 digests of the fused kernel
         snap["c4_encode_hash"] = snapshot_parts(buf4, dig4, (0, n4 - 1))
-        if "headline_all" in snap:  # and every part (the whole-batch check)
+        if "c2_dev" in snap:  # and every part: the buffer stays for the cpu_baseline leg
             snap["c4_digests"] = dig4.cpu().numpy()
-            snap["c4_all"] = snapshot_all(buf4)
+            snap["c4_dev"] = buf4
     data_gbs = n4 * d4 * L4 / (ms / 1e3) / 1e9
     hbm = n4 * t4 * (L4 + 32) / (ms / 1e3) / 1e9
     g = torch.Generator().manual_seed(2828 + rank)
@@ -1480,8 +1470,8 @@ def main():
         snap = {"parts": (0, n_parts // 2, n_parts - 1)}
         snap["headline"] = snapshot_parts(buf, digests, snap["parts"])
         if not args.no_full_check:
-            snap["headline_digests"] = digests.cpu().numpy()
-            snap["headline_all"] = snapshot_all(buf)
+            snap["c2_digests"] = digests.cpu().numpy()
+            snap["c2_dev"] = buf  # checked whole in the cpu_baseline leg (batch_vs_oracle)
     # north_star's two >= 60 % targets on the same buffer (C2 only)
     nstar = None
     if args.config == "c2" and not args.separate and not args.no_north_star:
@@ -1491,7 +1481,9 @@ def main():
     if args.config == "c2" and not args.separate and not args.no_north_star:
         others = baseline_configs_block(codec, batch, buf, digests, stream, device, rank, d, p,
                                         L, args.steps, snap)
-    del buf, digests  # the end-to-end forms below use their own buffers
+    # the end-to-end forms below use their own buffers (with the whole-batch check on, `snap`
+    # keeps the C2 and C4 device buffers, ~84 GiB of HBM, for the cpu_baseline leg)
+    del buf, digests
     torch.cuda.empty_cache()
 
     # every rank streams its own share (barriers inside): the PCIe-inclusive figure
@@ -1499,7 +1491,7 @@ def main():
     if args.config == "c2" and args.e2e_gib > 0 and not args.separate:
         e2e = end_to_end(codec, d, p, L, args.e2e_gib, world, rank, reduce_dev, e2e_threads,
                          ordinal, device, args.corrupt,
-                         full_check=snap is not None and "headline_all" in snap)
+                         full_check=snap is not None and "c2_dev" in snap)
 
     # per-rank figures for the N > 1 line (a straggler or a cross-NUMA placement must be
     # visible from the line alone)
@@ -1595,8 +1587,8 @@ def main():
                     detail["ok"] = detail["ok"] and not bad
                     stream = None
                 detail["seconds"] = round(time.perf_counter() - t0, 2)
-                snap.pop("headline_all", None)
-                snap.pop("c4_all", None)
+                snap.pop("c2_dev", None)
+                snap.pop("c4_dev", None)
                 line["check_vs_oracle"] = detail["ok"]
                 line["check_vs_oracle_detail"] = detail
             line["cpu_baseline"] = cpu_baseline(cfg, threads, os.cpu_count() or avail, avail,

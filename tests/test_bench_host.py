@@ -190,9 +190,9 @@ def test_node_figures_from_rank_rows():
 
 
 def test_check_vs_oracle_whole_batch():
-    """The cpu_baseline leg's whole-batch check: every part's digests and parity against the
-    oracle's encode + SHA-256 of its data, and C3's rebuilt batch byte for byte against that copy;
-    a single wrong digest, parity byte or rebuilt byte is reported with its part."""
+    """The cpu_baseline leg's whole-batch check (batch_vs_oracle, slab by slab): every part's
+    parity against the oracle's encode_sep of its data and its digests against SHA-256 of its
+    chunks; a single wrong digest or parity byte is reported with its part."""
     import torch
 
     import oracle
@@ -204,38 +204,33 @@ def test_check_vs_oracle_whole_batch():
         for k in range(n):
             st, par = oracle.encode_sep(d, p, list(data[k]))
             full[k, d:] = np.stack(par)
-        return full, oracle.encode_hash_parts(d, p, data, 2)
+        return torch.from_numpy(full), oracle.encode_hash_parts(d, p, data, 2)
 
     d, p, L, n = 3, 2, 512, 6
     t = d + p
     rng = np.random.default_rng(5)
-    full, dig = batch(rng, d, p, L, n)
-    buf = torch.from_numpy(full.copy())
+    buf, dig = batch(rng, d, p, L, n)
     snap = {"parts": (0, n - 1)}
-    snap["headline"] = bench.snapshot_parts(buf, torch.from_numpy(dig), snap["parts"])
-    snap["headline_digests"] = dig.copy()
-    snap["headline_all"] = bench.snapshot_all(buf, slab=4)
-    assert np.array_equal(snap["headline_all"], full)
-    snap["c3_all_parts_mismatched"] = bench.mismatched_parts(buf, snap["headline_all"], slab=4)
+    snap["headline"] = [(k, buf[k].numpy().copy(), dig[k]) for k in snap["parts"]]
+    snap["c2_digests"], snap["c2_dev"] = dig.copy(), buf
     det = bench.check_vs_oracle(snap, d, p, 2)
-    assert det["ok"] and det["checks"]["headline_all_parts"] and det["checks"]["c3_all_parts"]
-    assert det["headline_all_parts_checked"] == {"parts": n, "digests": n * t}
-    assert det["headline_all_parts_mismatched"] == []
-    snap["headline_digests"][4, t - 1, 7] ^= 1  # one parity digest of part 4
+    assert det["ok"] and det["checks"]["c2_all_parts"]
+    assert det["c2_all_parts_checked"] == {"parts": n, "digests": n * t}
+    assert det["c2_all_parts_mismatched"] == []
+    assert bench.batch_vs_oracle(buf, dig, d, p, 2, slab=4) == []
+    snap["c2_digests"][4, t - 1, 7] ^= 1  # one parity digest of part 4
     det = bench.check_vs_oracle(snap, d, p, 2)
-    assert not det["ok"] and det["headline_all_parts_mismatched"] == [4]
-    snap["headline_digests"][4, t - 1, 7] ^= 1
-    snap["headline_all"][2, d, 100] ^= 1  # a parity byte of part 2 (its digest unchanged)
-    det = bench.check_vs_oracle(snap, d, p, 2)
-    assert not det["ok"] and det["headline_all_parts_mismatched"] == [2]
-    snap["headline_all"][2, d, 100] ^= 1
-    buf[5, 1, 9] ^= 0x40  # a rebuilt byte of part 5
-    assert bench.mismatched_parts(buf, snap["headline_all"], slab=4) == [5]
-    buf[5, 1, 9] ^= 0x40  # (a CPU tensor: the sampled snapshot of part 5 shares its memory)
-    # C4's batch (the config's RS(20,8) shape), 3 small parts
+    assert not det["ok"] and det["c2_all_parts_mismatched"] == [4]
+    snap["c2_digests"][4, t - 1, 7] ^= 1
+    buf[2, d, 100] ^= 1  # a parity byte of part 2 (its digest is the oracle's, so it differs)
+    buf[5, 0, 0] ^= 1  # a data byte of part 5 (parity and digest both differ)
+    assert bench.batch_vs_oracle(buf, dig, d, p, 2, slab=4) == [2, 5]
+    buf[2, d, 100] ^= 1
+    buf[5, 0, 0] ^= 1
+    # C4's buffer (the config's RS(20,8) shape), 3 small parts
     c4 = bench.CONFIGS["c4"]
     d4, p4 = c4["d"], c4["p"]
-    snap["c4_all"], snap["c4_digests"] = batch(rng, d4, p4, 256, 3)
+    snap["c4_dev"], snap["c4_digests"] = batch(rng, d4, p4, 256, 3)
     det = bench.check_vs_oracle(snap, d, p, 2)
     assert det["ok"] and det["checks"]["c4_all_parts"]
     assert det["c4_all_parts_checked"] == {"parts": 3, "digests": 3 * (d4 + p4)}

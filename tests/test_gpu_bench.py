@@ -66,15 +66,14 @@ def test_default_line_checks_vs_oracle_small():
     assert line["check_vs_oracle"] is True
     det = line["check_vs_oracle_detail"]["checks"]
     assert det["headline"] is True and det["north_star_encode"] is True
-    # every part's 14 digests and 4 parity chunks against the oracle's encode + SHA-256 of its
-    # data, every part after C3's rebuild against those bytes, and C4's batch (scaled with
-    # --parts: 64 parts) like the headline's
+    # every part of the C2 buffer (after north_star's and C3's rebuilds) and of C4's (after its
+    # round trip): parity vs the oracle's encode of the data, 14 / 28 digests vs the fused
+    # kernel's (C4 scaled with --parts: 64 parts)
     det_all = line["check_vs_oracle_detail"]
-    assert det["headline_all_parts"] is True and det["c3_all_parts"] is True
-    assert det["c4_all_parts"] is True
-    assert det_all["headline_all_parts_checked"] == {"parts": 64, "digests": 64 * 14}
+    assert det["c2_all_parts"] is True and det["c4_all_parts"] is True
+    assert det_all["c2_all_parts_checked"] == {"parts": 64, "digests": 64 * 14}
     assert det_all["c4_all_parts_checked"] == {"parts": 64, "digests": 64 * 28}
-    assert det_all["headline_all_parts_mismatched"] == det_all["c3_all_parts_mismatched"] == []
+    assert det_all["c2_all_parts_mismatched"] == det_all["c4_all_parts_mismatched"] == []
 
 
 def test_end_to_end_read_repair_small():
