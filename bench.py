@@ -522,12 +522,24 @@ def run_stream(args, cfg, codec, world, rank, device, reduce_dev):
     ring_parts = 2 * depth * P if world == 1 else 2 * P
     ring = source_ring(ring_parts, d, L, 0xC5 + rank, copier)
     pl = ce.Pipeline(codec, L, P, depth)
-    loc, slot, n = timed_write(pl, ring_reader(ring, copier), lo, hi - lo, world)
+    # --check at N = 1: every part's digests kept (47 MB per TiB) and, after the timed region,
+    # every part re-derived from the ring through the oracle (stream_check; ~100 s per TiB on 16
+    # CPU workers)
+    import numpy as np
+    collect = np.empty((hi - lo, d + p, 32), np.uint8) if args.check and world == 1 else None
+    loc, slot, n = timed_write(pl, ring_reader(ring, copier), lo, hi - lo, world, collect)
     ok = write_check(pl, ring, slot, n, hi - 1) if hi > lo else True
     ok = all_ranks_ok(ok, world, reduce_dev)
     el = max_over_ranks(loc, world, reduce_dev)
     del pl
     copier.close()
+    whole = None
+    if collect is not None:
+        t0 = time.perf_counter()
+        bad = stream_check(ring, collect, d, p, min(16, len(os.sched_getaffinity(0))))
+        whole = {"parts": len(collect), "digests": int(collect.size // 32),
+                 "mismatched": bad[:8], "ok": not bad,
+                 "seconds": round(time.perf_counter() - t0, 1)}
     if rank == 0:
         total = total_parts * d * L
         print(json.dumps(_stream_line(
@@ -537,7 +549,9 @@ def run_stream(args, cfg, codec, world, rank, device, reduce_dev):
             f"synthetic host stream: every part copied inside the timed region by {threads} host "
             f"threads from a pageable source ring ({ring_parts} distinct parts, "
             f"{size_label(ring.nbytes)}) into the pinned slot, global part number stamped",
-            check_digests_vs_source=ok)), flush=True)
+            check_digests_vs_source=ok,
+            **({"check_all_parts_vs_oracle": whole} if whole is not None else {}))),
+            flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
 

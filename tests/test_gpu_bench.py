@@ -107,8 +107,11 @@ def test_end_to_end_write_stream_checked_whole():
 def test_stream_configs_small():
     """C5 and its verify/repair side at 4 GiB, fed from the pageable rings inside the timed
     region."""
-    line = _run("--config", "c5", "--stream-gib", "4")
+    line = _run("--config", "c5", "--stream-gib", "4", "--check")
     assert line["check_digests_vs_source"] is True and line["value"] > 0
+    # --check: every part of the stream re-derived through the oracle
+    whole = line["check_all_parts_vs_oracle"]
+    assert whole["ok"] is True and whole["parts"] == (4 << 30) // (10 << 20)
     assert line["config"]["stream_bytes"] == (4 << 30) // (10 << 20) * (10 << 20)
     line = _run("--config", "c5r", "--stream-gib", "4", "--corrupt", "0.02")
     rr = line["read_repair"]
