@@ -83,6 +83,10 @@ def test_codec_matrix_kat_rows(kats):
             for c in range(2):
                 par[r][c] ^= oracle.gf_mul(int(m[5 + r, j]), int(data[j, c]))
     assert par == k["parity"]
+    for v in kats["coding_matrix_published"]:  # the engine's own matrix at RS(4,2)
+        d, p = v["data_shards"], v["parity_shards"]
+        m = np.array(ce.ReedSolomon(d, p).matrix(), dtype=np.uint8)
+        assert m[d:].tolist() == v["parity_rows"]
 
 
 def test_codec_new_errors():

@@ -312,3 +312,11 @@ def test_encode_hash_parts_parity_check():
     full[3, d + 2, 999] ^= 0x10
     dg2, ok = oracle.encode_hash_parts(d, p, full, 2, check_parity=True)
     assert ok.tolist() == [True, True, True, False, True] and np.array_equal(dg, dg2)
+
+
+def test_published_coding_matrix(kats):
+    """A coding matrix printed by the JavaReedSolomon authors (RS(4,2)): the oracle's
+    construction (V * inv(V_top), exp(0, 0) = 1) reproduces it at a second shape."""
+    for v in kats["coding_matrix_published"]:
+        d, p = v["data_shards"], v["parity_shards"]
+        assert oracle.coding_matrix(d, p)[d:].tolist() == v["parity_rows"]
