@@ -21,10 +21,16 @@ The default (c2) line also carries: `north_star` (RS(10,4) encode and 2-erasure 
 on the headline's buffer, fractions of 8 TB/s), `baseline_configs` (BASELINE configs[2] C3 and
 configs[3] C4 per GPU), `end_to_end` (host-produced write stream, read + repair stream with
 damaged fetches retried, the PCIe link alone, the one-process scheduler path), and at N = 1
-`check_vs_oracle` (whole sampled parts of those buffers against the oracle, and every headline
-part's d+p digests against the oracle's encode + SHA-256 of its data, in the cpu_baseline leg).  At N > 1: `ranks` (each rank's own figures) and `node` (configs[3] and C3 at node level).
-`--config c5` / `c5r` run BASELINE configs[4]: a `--stream-gib` (1 TiB) stream fed per batch
-from pageable rings, written, or read back with `--corrupt` of the fetched chunks damaged.
+`check_vs_oracle` (every part of the C2 and C4 buffers and of the end-to-end write stream
+against the oracle, plus whole sampled parts of each block).  At N > 1: `ranks` (each rank's own
+figures) and `node` (configs[3] and C3 at node level).  `--config c5` / `c5r` run BASELINE
+configs[4]: a `--stream-gib` (1 TiB) stream fed per batch from pageable rings, written, or read
+back with `--corrupt` of the fetched chunks damaged.
+
+The oracle (oracle/) is only the checker and the CPU baseline: it is imported only in the
+host-side leg that runs after every timed region (the `cpu_baseline` leg: `check_vs_oracle`, the
+`--check` comparisons of any config, and the timed CPU baseline), never inside a timed region
+and never on the product path.
 """
 import argparse
 import json
