@@ -614,6 +614,7 @@ typedef struct {
     uint8_t* digests;
     uint8_t* parity_match;
     int shani;
+    int failed; /* a worker could not allocate its scratch */
     volatile size_t next;
     pthread_mutex_t mu;
 } digest_ctx;
@@ -624,6 +625,14 @@ static void* digest_worker(void* a_) {
     const uint8_t* rows[256];
     uint8_t* m = (uint8_t*)malloc((d + p) * d);
     uint8_t* par = (uint8_t*)malloc(p * L);
+    if (!m || !par) {
+        free(par);
+        free(m);
+        pthread_mutex_lock(&c->mu);
+        c->failed = 1;
+        pthread_mutex_unlock(&c->mu);
+        return NULL;
+    }
     or_rs_matrix(d, p, m);
     for (size_t i = 0; i < p; i++) rows[i] = m + (d + i) * d;
     for (;;) {
@@ -670,9 +679,14 @@ int or_encode_hash_parts(size_t d, size_t p, size_t L, size_t n_parts, const uin
     c.shani = or_cpu_has_shani();
     pthread_mutex_init(&c.mu, NULL);
     pthread_t* th = (pthread_t*)calloc((size_t)n_threads, sizeof(pthread_t));
-    for (int t = 0; t < n_threads; t++) pthread_create(&th[t], NULL, digest_worker, &c);
-    for (int t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
+    if (!th) return OR_INVALID_ARGUMENT;
+    int started = 0;
+    for (int t = 0; t < n_threads; t++)
+        if (pthread_create(&th[t], NULL, digest_worker, &c) == 0) started++;
+        else break;
+    for (int t = 0; t < started; t++) pthread_join(th[t], NULL);
     free(th);
     pthread_mutex_destroy(&c.mu);
-    return OR_OK;
+    /* every part was claimed by a worker that ran to completion, or the call fails */
+    return (started == 0 || c.failed || c.next < n_parts) ? OR_INVALID_ARGUMENT : OR_OK;
 }
