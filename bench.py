@@ -51,8 +51,8 @@ from chunky_ec.sharding import (all_ranks_ok, barrier, dist_env, gather_rows,  #
                                 max_over_ranks, part_range, rank_seed)
 
 METRIC = "RS(10,4) encode+sha256 GB/s per node at 1/2/4/8 GPUs; % of HBM roofline"
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md); 5.79 TB/s measured
-# streaming ceiling of the 10-read/4-write RS(10,4) pattern (tools/ubench_stream.hip)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md).  The encode kernel streams
+# 6.37 TB/s (0.796 of it), at the guide's measured 6.29 TB/s copy ceiling
 MiB = 1 << 20
 
 # VALU roofline of SHA-256 (the bound of every hashed config).  Per 64-byte block one lane issues
@@ -213,7 +213,10 @@ def host_info():
         pass
     aff, quota = cpu_quota()
     return {"cpu": model, "logical_cpus": os.cpu_count(), "affinity_cpus": aff,
-            "cgroup_cpu_quota": quota, "numa_nodes": len(nodes), "mem_gib": mem}
+            "cgroup_cpu_quota": quota, "numa_nodes": len(nodes), "mem_gib": mem,
+            # provenance: the loaded library's source hash and whether it equals the hash of the
+            # sources shipped with this tree (chunky_ec refuses a mismatch on import)
+            "build_id": ce.BUILD_ID, "build_matches_source": ce.BUILD_MATCHES_SOURCE}
 
 
 def cpu_baseline(cfg, threads: int, cores_total: int, cores_avail: int, quota):

@@ -76,6 +76,35 @@ ABI_VERSION = 2
 if _lib.cec_abi_version() != ABI_VERSION:
     raise ImportError(f"chunky_ec: {LIB_PATH} has ABI {_lib.cec_abi_version()}, this binding "
                       f"needs {ABI_VERSION}; rebuild with `make -C chunky-bits_amd/csrc`")
+if not hasattr(_lib, "cec_build_id"):
+    raise ImportError(f"chunky_ec: {LIB_PATH} predates cec_build_id; rebuild with "
+                      "`make -C chunky-bits_amd/csrc`")
+_sig("cec_build_id", [], ctypes.c_char_p)
+
+
+def _shipped_source_hash() -> Optional[str]:
+    """Hash of the library sources shipped beside this package (csrc/source_hash.py), or None
+    when they are not (an installed copy)."""
+    csrc = os.path.join(os.path.dirname(_HERE), "csrc")
+    script = os.path.join(csrc, "source_hash.py")
+    if not os.path.exists(script):
+        return None
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("_cec_source_hash", script)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod.source_hash()
+
+
+BUILD_ID = _lib.cec_build_id().decode()
+SOURCE_HASH = _shipped_source_hash()
+# Build provenance: a library built from other sources than the ones shipped with it (a stale
+# build, or objects carried over from another tree) is refused, so what runs on a GPU box is what
+# the tree says.  CEC_ALLOW_STALE_BUILD=1 lets a developer load it anyway.
+BUILD_MATCHES_SOURCE = SOURCE_HASH is None or SOURCE_HASH == BUILD_ID
+if not BUILD_MATCHES_SOURCE and os.environ.get("CEC_ALLOW_STALE_BUILD") != "1":
+    raise ImportError(f"chunky_ec: {LIB_PATH} was built from sources {BUILD_ID}, the shipped "
+                      f"sources hash to {SOURCE_HASH}; rebuild with `make -C chunky-bits_amd/csrc`")
 _sig("cec_status_name", [ctypes.c_int], ctypes.c_char_p)
 _sig("cec_last_error", [], ctypes.c_char_p)
 _sig("cec_device_count", [])

@@ -225,6 +225,7 @@ pub mod sys {
         ) -> c_int;
         pub fn cec_coalesce_stats(calls: *mut u64, launches: *mut u64);
         pub fn cec_build_info() -> *const std::os::raw::c_char;
+        pub fn cec_build_id() -> *const std::os::raw::c_char;
         pub fn cec_current_device(device: *mut c_int) -> c_int;
         pub fn cec_set_device(device: c_int) -> c_int;
         pub fn cec_device_numa_node(device: c_int) -> c_int;
@@ -1115,6 +1116,12 @@ impl Multi {
 /// Visible HIP devices (0 when none; never fails).
 pub fn device_count() -> c_int {
     unsafe { sys::cec_device_count() }
+}
+
+/// Hash of the sources the linked library was built from (`cec_build_id`): a `build.rs` or a
+/// service's startup log can compare it with the engine checkout it expects.
+pub fn build_id() -> String {
+    unsafe { std::ffi::CStr::from_ptr(sys::cec_build_id()) }.to_string_lossy().into_owned()
 }
 
 /// Frees the engine's idle per-call staging on `device` (every device when < 0); returns the

@@ -94,6 +94,10 @@ int cec_device_numa_node(int device);
  * ab_tools=0: the timing-attribution kernels (wrong outputs by design) exist only in the
  * separate A/B build used by tools/ (DESIGN.md §6.1). */
 const char* cec_build_info(void);
+/* Provenance: 16 hex digits, the hash of the sources the library was built from
+ * (chunky-bits_amd/csrc/source_hash.py: every .cpp, .hip and .hpp file of csrc, its Makefile
+ * and this header).  The Python binding refuses a library whose id differs from its shipped sources. */
+const char* cec_build_id(void);
 /* Environment knobs (CEC_APPLY_*, CEC_FUSED*, CEC_SHA_VARIANT, CEC_COALESCE_*, CEC_READ_*, ...;
  * DESIGN.md §4) are read ONCE, on the first call that needs one, into an immutable snapshot;
  * no launch path calls getenv (the reference drives the hot path from tokio worker threads,

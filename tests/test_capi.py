@@ -48,6 +48,22 @@ def test_library_has_gfx950_code_object():
     assert b"amdgcn-amd-amdhsa--gfx950" in data  # offload bundle entry id of the .hip_fatbin
 
 
+def test_library_was_built_from_these_sources():
+    """Build provenance: the library's cec_build_id is the hash of the sources in this tree
+    (csrc/source_hash.py), so the .so a GPU run loads was built from HEAD's sources, and the
+    binding refuses one that was not."""
+    import importlib.util
+    import chunky_ec as ce
+    spec = importlib.util.spec_from_file_location(
+        "sh", os.path.join(ROOT, "chunky-bits_amd", "csrc", "source_hash.py"))
+    sh = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(sh)
+    assert ce.BUILD_ID == sh.source_hash() == ce.SOURCE_HASH
+    assert ce.BUILD_MATCHES_SOURCE
+    assert "include/chunky_ec.h" in sh.source_files()
+    assert any(f.endswith("rs_kernels.hip") for f in sh.source_files())
+
+
 def test_status_codes_match_crate_order():
     import chunky_ec as ce
     names = ["Ok", "TooFewShards", "TooManyShards", "TooFewDataShards", "TooManyDataShards",
