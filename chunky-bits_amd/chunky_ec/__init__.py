@@ -926,14 +926,18 @@ class Multi:
         del keep
         return [p or 0 for p in ptrs[: n_parts * self.t]]
 
-    def verify_sync(self, chunks, present, expected, n_parts: int, verified) -> None:
-        """FilePart::verify's compute: verified[n][d+p] for every loaded chunk."""
+    def verify(self, chunks, present, expected, n_parts: int, verified) -> int:
+        """FilePart::verify's compute: verified[n][d+p] for every loaded chunk; returns the job."""
         job = ctypes.c_uint64(0)
         code = _lib.cec_multi_verify(self._h, _addr(chunks), _addr(present), _addr(expected),
                                      n_parts, _addr(verified), ctypes.byref(job))
         if code != OK:
             raise MultiError(code)
-        self.wait(job.value)
+        self._keep[job.value] = (chunks, present, expected, verified)
+        return job.value
+
+    def verify_sync(self, chunks, present, expected, n_parts: int, verified) -> None:
+        self.wait(self.verify(chunks, present, expected, n_parts, verified))
 
     def wait(self, job: int) -> None:
         code = _lib.cec_multi_wait(self._h, job)

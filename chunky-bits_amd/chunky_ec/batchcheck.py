@@ -1,0 +1,281 @@
+"""FileReference::verify / resilver batched over the multi-GPU scheduler, hashing every location
+of every chunk like the reference: the Python twin of the Rust crate's
+``chunky_ec_sys::batch::BatchChecker`` (chunky-bits_amd/rust/chunky-ec-sys/src/batch.rs) and of
+the C++ ``FileReference::check_run`` (include/chunky_ec.hpp), step for step, tested on the GPU
+(tests/test_gpu_batchcheck.py).
+
+The reference's ``FilePart::verify`` reads every location of every chunk and compares each copy's
+SHA-256 with the metadata (src/file/file_part.rs:228-251).  ``resilver`` does the same, keeps
+each chunk's first copy that verifies (:266-294), rebuilds -- data AND parity, ``reconstruct`` --
+every chunk that has none (:296-308), writes those and APPENDS the new locations to the chunk's
+list (``chunk.locations.extend``, :340-347).  A chunk with a bad copy and a good one is healthy
+and is not rewritten.
+
+``read_all(part, chunk)`` returns one entry per location of the chunk, in the metadata's order:
+the copy's bytes, or None where the location cannot be read (``Location::read``).  Each readable
+copy is one hashing item:
+
+* verify: every copy of a window of parts goes to one ``cec_multi_verify`` job, ``d + p`` items
+  per scheduler row, whatever chunk they belong to (the job hashes and compares items; it does not
+  care which part an item is from);
+* resilver: a window whose chunks have one location each is one ``cec_multi_resilver`` job (hash
+  each copy, rebuild what does not verify).  When some chunk of the window has several locations,
+  those chunks' copies are hashed first (a verify job), and the resilver job then gets their first
+  valid copy flagged ``CEC_PRESENT_VERIFIED`` (used, not hashed again): every copy is still hashed
+  exactly once.
+
+``sink(part, CheckedPart)`` receives each part, in file order, with the per-location results
+(True valid, False invalid, None unreadable: the reference's ``read_results``), and for resilver
+the rebuilt chunks to write back and the part's ``write_error``.  A part that cannot be rebuilt
+reports its error and the other parts go on (file_reference.rs:103-110 collects every report).
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional, Sequence
+
+import numpy as np
+
+from . import OK, PRESENT_VERIFIED, HostBuffer, Multi, ReedSolomon
+
+ReadAll = Callable[[int, int], Sequence[Optional[bytes]]]
+
+
+@dataclass
+class CheckedPart:
+    index: int
+    # [chunk][location]: True (valid), False (invalid), None (unreadable), d data then p parity
+    locations: List[List[Optional[bool]]]
+    # resilver: chunk index -> rebuilt bytes, for every chunk with no valid copy (valid in sink)
+    rebuilt: Dict[int, memoryview] = field(default_factory=dict)
+    # resilver: the part's rebuild failure (ResilverPartReport::write_error), a status code
+    error: Optional[int] = None
+
+    def chunk_valid(self, i: int) -> bool:
+        return any(r is True for r in self.locations[i])
+
+    def healthy_chunks(self) -> int:
+        """Chunks with a valid copy (file_part.rs:545-547), counting rebuilt ones as written."""
+        return sum(1 for i in range(len(self.locations)) if self.chunk_valid(i) or i in self.rebuilt)
+
+    def unavailable_locations(self) -> int:
+        return sum(r is None for locs in self.locations for r in locs)
+
+    def invalid_locations(self) -> int:
+        return sum(r is False for locs in self.locations for r in locs)
+
+
+@dataclass
+class _Window:
+    slot: int
+    job: Optional[int]
+    first: int
+    n: int
+    parts: list  # [q] -> CheckedPart being filled
+    items: list  # verify: [(q, i, j)] per hashed copy, in job order
+    single: list  # resilver: [(q, i)] chunks whose lone copy the resilver job hashes
+    ver: Optional[np.ndarray] = None
+
+
+class BatchChecker:
+    def __init__(self, data: int, parity: int, chunk_size: int, parts_per_batch: int, depth: int,
+                 devices: List[int]):
+        self.codec = ReedSolomon(data, parity)  # file_part.rs:302
+        self.multi = Multi(self.codec, chunk_size, parts_per_batch, depth, devices)
+        self.d, self.p, self.t, self.L = data, parity, data + parity, chunk_size
+        self.window = parts_per_batch * max(len(devices), 1)
+        dev0 = devices[0] if devices else -1
+        W, t, L = self.window, self.t, chunk_size
+        self.chunks = [HostBuffer(W * t * L, dev0) for _ in range(2)]
+        self.rebuilt = [HostBuffer(W * t * L, dev0) for _ in range(2)]
+        self.present = [np.zeros((W, t), np.uint8) for _ in range(2)]
+        self.expected = [np.zeros((W, t, 32), np.uint8) for _ in range(2)]
+        self.verified = [np.zeros((W, t), np.uint8) for _ in range(2)]
+        self.status = [np.zeros(W, np.int32) for _ in range(2)]
+        self.extra_passes = 0  # windows whose multi-location chunks needed a verify job first
+
+    # -- the two operations --------------------------------------------------------------------
+
+    def verify(self, n_parts: int, read_all: ReadAll, digests: Callable[[int], np.ndarray],
+               sink: Callable[[int, CheckedPart], None]) -> None:
+        self._run(n_parts, read_all, digests, sink, resilver=False)
+
+    def resilver(self, n_parts: int, read_all: ReadAll, digests: Callable[[int], np.ndarray],
+                 sink: Callable[[int, CheckedPart], None]) -> None:
+        self._run(n_parts, read_all, digests, sink, resilver=True)
+
+    def _run(self, n_parts, read_all, digests, sink, resilver):
+        at = slot = 0
+        pending: Optional[_Window] = None
+        while True:
+            cur = None
+            if at < n_parts:
+                cnt = min(self.window, n_parts - at)
+                try:
+                    cur = (self._submit_resilver if resilver else self._submit_verify)(
+                        slot, at, cnt, read_all, digests)
+                except BaseException:
+                    self._drain(pending)
+                    raise
+                at += cnt
+            if pending is not None:  # the older window first: file order
+                prev, pending = pending, None
+                try:
+                    (self._collect_resilver if resilver else self._collect_verify)(prev, sink)
+                except BaseException:
+                    self._drain(cur)
+                    raise
+            if cur is None:
+                return
+            pending = cur
+            slot ^= 1
+
+    # -- verify ----------------------------------------------------------------------------------
+
+    def _copies(self, first, cnt, read_all):
+        """Every location's copy of every chunk of the window (None: unreadable), and the parts'
+        result skeletons: None for an unreadable copy, False for one of the wrong size (it cannot
+        hash to the digest), to be filled for the rest."""
+        t, L = self.t, self.L
+        copies = [[list(read_all(first + q, i)) for i in range(t)] for q in range(cnt)]
+        parts = [CheckedPart(first + q, [[None if c is None else (False if len(c) != L else True)
+                                          for c in copies[q][i]] for i in range(t)])
+                 for q in range(cnt)]
+        return copies, parts
+
+    def _hash_items(self, items, copies, digs, buf):
+        """A verify job over `items` [(q, i, j)], d + p of them per scheduler row; returns (job,
+        verified flags in item order)."""
+        t, L = self.t, self.L
+        g = -(-len(items) // t)
+        if buf is None or len(items) > self.window * t:
+            buf = np.zeros(g * t * L, np.uint8)  # more copies than the pinned window holds
+        view = buf.view(-1, t, L) if isinstance(buf, HostBuffer) else buf.reshape(-1, t, L)
+        pres = np.zeros((g, t), np.uint8)
+        exp = np.zeros((g, t, 32), np.uint8)
+        ver = np.zeros((g, t), np.uint8)
+        for x, (q, i, j) in enumerate(items):
+            view[x // t, x % t] = np.frombuffer(copies[q][i][j], np.uint8)
+            pres[x // t, x % t] = 1
+            exp[x // t, x % t] = digs[q][i]
+        return self.multi.verify(buf, pres, exp, g, ver), ver.reshape(-1)
+
+    def _submit_verify(self, slot, first, cnt, read_all, digests) -> _Window:
+        copies, parts = self._copies(first, cnt, read_all)
+        digs = [digests(first + q) for q in range(cnt)]
+        items = [(q, i, j) for q in range(cnt) for i in range(self.t)
+                 for j, r in enumerate(parts[q].locations[i]) if r is True]
+        w = _Window(slot, None, first, cnt, parts, items, [])
+        if items:
+            w.job, w.ver = self._hash_items(items, copies, digs, self.chunks[slot])
+        return w
+
+    def _collect_verify(self, w: _Window, sink) -> None:
+        if w.job is not None:
+            self.multi.wait(w.job)
+        for x, (q, i, j) in enumerate(w.items):
+            w.parts[q].locations[i][j] = bool(w.ver[x])
+        for q in range(w.n):
+            sink(w.first + q, w.parts[q])
+
+    # -- resilver --------------------------------------------------------------------------------
+
+    def _submit_resilver(self, slot, first, cnt, read_all, digests) -> _Window:
+        t, L = self.t, self.L
+        copies, parts = self._copies(first, cnt, read_all)
+        digs = [digests(first + q) for q in range(cnt)]
+        ch = self.chunks[slot].view(self.window, t, L)
+        pres, exp = self.present[slot], self.expected[slot]
+        pres[:cnt] = 0
+        # chunks with several locations: every copy hashed first (file_part.rs:277-289 reads each
+        # location and keeps the first match), in a verify job of their own
+        multi = [(q, i, j) for q in range(cnt) for i in range(t) if len(copies[q][i]) > 1
+                 for j, r in enumerate(parts[q].locations[i]) if r is True]
+        if multi:
+            job, ver = self._hash_items(multi, copies, digs, None)
+            self.multi.wait(job)
+            self.extra_passes += 1
+            for x, (q, i, j) in enumerate(multi):
+                parts[q].locations[i][j] = bool(ver[x])
+        single = []
+        for q in range(cnt):
+            exp[q] = digs[q]
+            for i in range(t):
+                locs = parts[q].locations[i]
+                if len(locs) == 1:
+                    if locs[0] is True:  # the lone copy: hashed by the resilver job itself
+                        ch[q, i] = np.frombuffer(copies[q][i][0], np.uint8)
+                        pres[q, i] = 1
+                        single.append((q, i))
+                elif True in locs:  # its first valid copy, already verified
+                    ch[q, i] = np.frombuffer(copies[q][i][locs.index(True)], np.uint8)
+                    pres[q, i] = PRESENT_VERIFIED
+        job, _ = self.multi.resilver(self.chunks[slot], pres, exp, cnt, self.rebuilt[slot],
+                                     self.verified[slot], self.status[slot])
+        return _Window(slot, job, first, cnt, parts, [], single)
+
+    def _collect_resilver(self, w: _Window, sink) -> None:
+        self.multi.wait(w.job)
+        t, L = self.t, self.L
+        ver, st = self.verified[w.slot], self.status[w.slot]
+        for q, i in w.single:
+            w.parts[q].locations[i][0] = bool(ver[q, i])
+        out = memoryview(self.rebuilt[w.slot].array)
+        for q in range(w.n):
+            part = w.parts[q]
+            missing = [i for i in range(t) if not ver[q, i]]
+            if missing and st[q] != OK:
+                part.error = int(st[q])  # write_error: this part only, the others go on
+            elif missing:
+                part.rebuilt = {i: out[(q * t + i) * L:(q * t + i + 1) * L] for i in missing}
+            sink(w.first + q, part)
+
+    def _drain(self, w: Optional[_Window]) -> None:
+        if w is not None and w.job is not None:
+            try:
+                self.multi.wait(w.job)
+            except Exception:  # noqa: BLE001 (the error being raised is the caller's)
+                pass
+
+
+class FileChecker:
+    """FileReference::verify / resilver over a whole file (file_reference.rs:78-113): consecutive
+    parts of one shape (d, p, chunk size) go through one BatchChecker of that shape -- kept (the
+    ``keep`` most recently used shapes) for the next file, since its windows pin memory -- with
+    the reports in file order; a lone part (the short last part) through a checker of one part per
+    window."""
+
+    def __init__(self, parts_per_batch: int, depth: int, devices: List[int], keep: int = 2):
+        self.ppb, self.depth, self.devices, self.keep = parts_per_batch, depth, list(devices), keep
+        self.checkers: "OrderedDict[tuple, BatchChecker]" = OrderedDict()
+
+    def checker(self, shape: tuple, ppb: int) -> BatchChecker:
+        key = shape + (ppb,)
+        c = self.checkers.pop(key, None)
+        if c is None:
+            while len(self.checkers) >= self.keep:  # free the least recently used first
+                self.checkers.popitem(last=False)
+            d, p, L = shape
+            c = BatchChecker(d, p, L, ppb, self.depth, self.devices)
+        self.checkers[key] = c
+        return c
+
+    def verify(self, shapes, read_all: ReadAll, digests, sink) -> None:
+        self._runs(shapes, read_all, digests, sink, False)
+
+    def resilver(self, shapes, read_all: ReadAll, digests, sink) -> None:
+        self._runs(shapes, read_all, digests, sink, True)
+
+    def _runs(self, shapes, read_all, digests, sink, resilver):
+        k = 0
+        while k < len(shapes):
+            run = 1
+            while k + run < len(shapes) and shapes[k + run] == shapes[k]:
+                run += 1
+            c = self.checker(tuple(shapes[k]), self.ppb if run > 1 else 1)
+            k0 = k
+            (c.resilver if resilver else c.verify)(
+                run, lambda q, i: read_all(k0 + q, i), lambda q: digests(k0 + q),
+                lambda q, part: (setattr(part, "index", k0 + q), sink(k0 + q, part)))
+            k += run

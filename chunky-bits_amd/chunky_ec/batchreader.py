@@ -1,29 +1,71 @@
 """FileReadBuilder's reader batched over the multi-GPU scheduler, with read_with_context's retry
 rule, parts handed out in file order: the Python twin of the Rust crate's
-``chunky_ec_sys::batch::BatchReader`` (chunky-bits_amd/rust/chunky-ec-sys/src/batch.rs) and of
-the C++ ``FileReference::read_run`` / ``retry`` (include/chunky_ec.hpp), step for step, so the
-loop the Rust side would run is executed and tested on the GPU (tests/test_gpu_batchreader.py).
+``chunky_ec_sys::batch::BatchReader`` / ``read_part`` / ``FileReader``
+(chunky-bits_amd/rust/chunky-ec-sys/src/batch.rs) and of the C++ ``FileReference::read_run`` /
+``retry`` (include/chunky_ec.hpp), step for step, so the loop the Rust side would run is executed
+and tested on the GPU (tests/test_gpu_batchreader.py).
 
-The reference reads a part by loading chunks until d of them verify (src/file/file_part.rs:
-86-107), rebuilds the missing data chunks (:123-129) and FileReadBuilder yields the parts in file
-order (src/file/reader.rs:40-75).  :class:`BatchReader` loads a window of
-``parts_per_batch * len(devices)`` parts at a time -- for each part the first d chunks its
-``fetch`` returns (data chunks first, so an intact part needs no rebuild) -- into a page-locked
-buffer and submits the window as one scheduler job (verify every loaded chunk, rebuild the data
-chunks; parts split over the GPUs in contiguous ranges) while it loads the next window.  A part
-whose loaded chunks do not all verify is resubmitted with the chunks that verified flagged
-``CEC_PRESENT_VERIFIED`` (used, not hashed again) and as many untried chunks as it is short of d,
-until it decodes; a part that runs out of chunks fails the read with TooFewShardsPresent, as the
-reference's does.
+The reference reads a part by drawing chunks until d of them verify (src/file/file_part.rs:
+86-107): for each drawn chunk it walks the chunk's locations in order and keeps the first copy
+whose SHA-256 matches the metadata, and only when none does it draws another chunk.  It then
+rebuilds the missing data chunks (:123-129), and FileReadBuilder yields the parts in file order
+(src/file/reader.rs:40-75).
+
+``fetch(part, chunk, start)`` is that walk's step: it reads the chunk's locations from index
+``start`` on and returns ``(location index, bytes)`` of the first one that reads, or None when no
+location is left (``Location::read_with_context`` over ``chunk.locations[start..]``).  A copy
+that fails verification is followed by the same chunk's next location (``start`` = its index + 1)
+before another chunk is drawn, so a chunk listed ``[bad, good]`` -- what resilver leaves behind
+when it appends a rebuilt copy's location (file_part.rs:346) -- reads like in the reference.
+
+:class:`BatchReader` loads a window of ``parts_per_batch * len(devices)`` parts of one shape at a
+time -- for each part the first d chunks that fetch returns a copy of (data chunks first, so an
+intact part needs no rebuild) -- into a page-locked buffer and submits the window as one scheduler
+job (verify every loaded chunk, rebuild the data chunks; parts split over the GPUs in contiguous
+ranges) while it loads the next window.  A part whose loaded chunks do not all verify is
+resubmitted with the chunks that verified flagged ``CEC_PRESENT_VERIFIED`` (used, not hashed
+again), the failed chunks' next copies, then untried chunks, up to d, until it decodes; a part
+that runs out of copies fails the read with TooFewShardsPresent, as the reference's does.
+:func:`read_part` is the same rule for one part through the per-call API, and :class:`FileReader`
+splits a file into runs of one shape (chunk size, d, p: the short last part has its own chunk size,
+file_part.rs:152) and keeps one BatchReader per shape.
 """
 from __future__ import annotations
 
+from collections import OrderedDict
 from dataclasses import dataclass
-from typing import Callable, List, Optional
+from typing import Callable, List, Optional, Sequence, Tuple
 
 import numpy as np
 
-from . import OK, PRESENT_VERIFIED, TOO_FEW_SHARDS_PRESENT, Error, HostBuffer, Multi, ReedSolomon
+from . import (OK, PRESENT_VERIFIED, TOO_FEW_SHARDS_PRESENT, Error, HostBuffer, Multi, ReedSolomon,
+               Sha256Hash)
+
+Fetch = Callable[[int, int, int], Optional[Tuple[int, bytes]]]
+
+
+def next_copy(fetch: Fetch, part: int, chunk: int, start: int, size: int):
+    """The chunk's next copy from location ``start`` on: ``(next start, bytes)``, or None when its
+    locations are exhausted.  A copy that is not ``size`` bytes cannot hash to the metadata digest
+    (the reference hashes it and moves on), so it is passed over here."""
+    while True:
+        got = fetch(part, chunk, start)
+        if got is None:
+            return None
+        loc, b = got
+        start = loc + 1
+        if len(b) == size:
+            return start, b
+
+
+def draw_order(good, tried, exhausted):
+    """Chunk indices to load next for a part that is short of d verified chunks: the chunks whose
+    copy failed verification first (their next location: file_part.rs:100-107 walks a chunk's
+    locations before drawing another chunk), then the untried ones."""
+    t = len(good)
+    again = [i for i in range(t) if tried[i] and not good[i] and not exhausted[i]]
+    fresh = [i for i in range(t) if not tried[i] and not exhausted[i]]
+    return again + fresh
 
 
 @dataclass
@@ -49,12 +91,15 @@ class BatchReader:
         self.expected = [np.zeros((W, t, 32), np.uint8) for _ in range(2)]
         self.verified = [np.zeros((W, t), np.uint8) for _ in range(2)]
         self.status = [np.zeros(W, np.int32) for _ in range(2)]
+        # per chunk of the window: the next location to read, and whether none is left
+        self.cursor = [np.zeros((W, t), np.int64) for _ in range(2)]
+        self.exhausted = [np.zeros((W, t), bool) for _ in range(2)]
         self.retries = 0  # part resubmissions (a part retried twice counts twice)
 
-    def read(self, n_parts: int, fetch: Callable[[int, int], Optional[bytes]],
-             digests: Callable[[int], np.ndarray], sink: Callable[[int, List[memoryview]], None]):
-        """Parts 0..n_parts-1: ``fetch(part, chunk)`` returns the stored chunk's bytes (None if
-        no location has it), ``digests(part)`` its metadata digests [d+p][32]; ``sink(part,
+    def read(self, n_parts: int, fetch: Fetch, digests: Callable[[int], np.ndarray],
+             sink: Callable[[int, List[memoryview]], None]):
+        """Parts 0..n_parts-1 (all of this reader's shape): ``fetch(part, chunk, start)`` as the
+        module describes, ``digests(part)`` the part's metadata digests [d+p][32]; ``sink(part,
         data_chunks)`` gets the d data chunks of every part, in file order."""
         at = slot = 0
         pending: Optional[_Window] = None
@@ -82,21 +127,26 @@ class BatchReader:
             slot ^= 1
 
     def _load(self, slot, first, cnt, fetch, digests):
-        """The first d chunks each part's fetch returns (file_part.rs:86-107 loads d), with
-        every chunk's metadata digest."""
+        """The first d chunks of each part that fetch returns a copy of (file_part.rs:86-107 loads
+        d), with every chunk's metadata digest."""
         d, t, L = self.d, self.t, self.L
         ch = self.chunks[slot].view(self.window, t, L)
         pres, exp = self.present[slot], self.expected[slot]
+        cur, ex = self.cursor[slot], self.exhausted[slot]
         pres[:cnt] = 0
+        cur[:cnt] = 0
+        ex[:cnt] = False
         for q in range(cnt):
             exp[q] = digests(first + q)
             loaded = 0
             for i in range(t):
                 if loaded == d:
                     break
-                b = fetch(first + q, i)
-                if b is None or len(b) != L:
+                c = next_copy(fetch, first + q, i, 0, L)
+                if c is None:
+                    ex[q, i] = True
                     continue
+                cur[q, i], b = c
                 ch[q, i] = np.frombuffer(b, np.uint8)
                 pres[q, i] = 1
                 loaded += 1
@@ -119,14 +169,17 @@ class BatchReader:
 
     def _retry(self, w: _Window, failed, fetch):
         """file_part.rs:92-107: the failed parts go again with the chunks that verified
-        (PRESENT_VERIFIED, taken from the window's buffer: the bytes that verified) plus untried
-        ones up to d, until each decodes or runs out of chunks."""
+        (PRESENT_VERIFIED, taken from the window's buffer: the bytes that verified) plus, up to
+        d, the failed chunks' next copies and then untried chunks, until each decodes or runs out
+        of copies."""
         d, t, L = self.d, self.t, self.L
         ch = self.chunks[w.slot].view(self.window, t, L)
         pres, ver = self.present[w.slot], self.verified[w.slot]
         out = self.out[w.slot].view(self.window, d, L)
         tried = {q: pres[q] != 0 for q in failed}
         good = {q: ver[q] != 0 for q in failed}
+        cursor = {q: self.cursor[w.slot][q].copy() for q in failed}
+        exhausted = {q: self.exhausted[w.slot][q].copy() for q in failed}
         keep = {q: ch[q].copy() for q in failed}  # bytes of every chunk loaded so far
         f = len(failed)
         # pageable (the scheduler stages them): pinning a retry buffer per window would cost more
@@ -141,20 +194,24 @@ class BatchReader:
             for s, q in enumerate(open_):
                 r_exp[s] = self.expected[w.slot][q]
                 have = int(good[q].sum())
-                added = 0
                 for i in range(t):
                     if good[q][i]:
                         rc[s, i] = keep[q][i]
                         r_pres[s, i] = PRESENT_VERIFIED
-                    elif not tried[q][i] and have + added < d:
-                        tried[q][i] = True
-                        b = fetch(w.first + q, i)
-                        if b is None or len(b) != L:
-                            continue
-                        keep[q][i] = np.frombuffer(b, np.uint8)
-                        rc[s, i] = keep[q][i]
-                        r_pres[s, i] = 1
-                        added += 1
+                added = 0
+                for i in draw_order(good[q], tried[q], exhausted[q]):
+                    if not have + added < d:
+                        break
+                    tried[q][i] = True
+                    c = next_copy(fetch, w.first + q, i, int(cursor[q][i]), L)
+                    if c is None:
+                        exhausted[q][i] = True
+                        continue
+                    cursor[q][i], b = c
+                    keep[q][i] = np.frombuffer(b, np.uint8)
+                    rc[s, i] = keep[q][i]
+                    r_pres[s, i] = 1
+                    added += 1
                 if added == 0:
                     raise Error(TOO_FEW_SHARDS_PRESENT)
             job, _ = self.multi.read(rc, r_pres, r_exp, g, ro, r_ver, r_st)
@@ -175,3 +232,90 @@ class BatchReader:
                 self.multi.wait(w.job)
             except Exception:  # noqa: BLE001 (the error being raised is the caller's)
                 pass
+
+
+def read_part(codec: ReedSolomon, chunksize: int, digests: np.ndarray, fetch: Fetch,
+              part: int) -> bytes:
+    """read_with_context (file_part.rs:73-135) for one part through the per-call API, with the
+    batched loop's rule: d chunks drawn (data first), each kept at its first copy that verifies,
+    failed chunks' next copies and then untried chunks until d verify (TooFewShardsPresent when
+    the copies run out), missing data rebuilt.  The path for a part whose shape no BatchReader of
+    the file has (the short last part, chunk size ceil(len / d))."""
+    d = codec.data_shard_count()
+    t = codec.total_shard_count()
+    good, tried, exhausted = [False] * t, [False] * t, [False] * t
+    cursor = [0] * t
+    shards: List[Optional[bytearray]] = [None] * t
+    while sum(good) < d:
+        batch = []
+        for i in draw_order(good, tried, exhausted):
+            if sum(good) + len(batch) >= d:
+                break
+            tried[i] = True
+            c = next_copy(fetch, part, i, cursor[i], chunksize)
+            if c is None:
+                exhausted[i] = True
+                continue
+            cursor[i], b = c
+            batch.append((i, b))
+        if not batch:
+            raise Error(TOO_FEW_SHARDS_PRESENT)
+        hashes = Sha256Hash.from_bufs([b for _, b in batch])  # one launch per round
+        for (i, b), h in zip(batch, hashes):
+            if h.digest == bytes(digests[i]):
+                good[i] = True
+                shards[i] = bytearray(b)
+    if not all(s is not None for s in shards[:d]):
+        codec.reconstruct_data(shards)
+    return b"".join(bytes(s) for s in shards[:d])
+
+
+Shape = Tuple[int, int, int]  # (d, p, chunksize) of a part
+
+
+class FileReader:
+    """FileReadBuilder's reader over a whole file (reader.rs:32-74): consecutive parts of one
+    shape (d, p, chunk size) form a run; a run of two or more parts goes through a BatchReader of
+    that shape -- kept (the ``keep`` most recently used shapes) for the next file, since its
+    windows pin memory (~0.35 s per GiB) -- and a lone part (the short last part) through
+    :func:`read_part`.  Parts reach ``sink(part, data_chunks)`` in file order."""
+
+    def __init__(self, parts_per_batch: int, depth: int, devices: List[int], keep: int = 2):
+        self.ppb, self.depth, self.devices, self.keep = parts_per_batch, depth, list(devices), keep
+        self.readers: "OrderedDict[Shape, BatchReader]" = OrderedDict()
+        self.codecs: "OrderedDict[Tuple[int, int], ReedSolomon]" = OrderedDict()
+
+    def reader(self, shape: Shape) -> BatchReader:
+        r = self.readers.pop(shape, None)
+        if r is None:
+            while len(self.readers) >= self.keep:  # free the least recently used first
+                self.readers.popitem(last=False)
+            d, p, L = shape
+            r = BatchReader(d, p, L, self.ppb, self.depth, self.devices)
+        self.readers[shape] = r
+        return r
+
+    def _codec(self, d: int, p: int) -> ReedSolomon:
+        c = self.codecs.pop((d, p), None) or ReedSolomon(d, p)
+        self.codecs[(d, p)] = c
+        while len(self.codecs) > self.keep:
+            self.codecs.popitem(last=False)
+        return c
+
+    def read(self, shapes: Sequence[Shape], fetch: Fetch, digests: Callable[[int], np.ndarray],
+             sink: Callable[[int, List], None]) -> None:
+        k = 0
+        while k < len(shapes):
+            run = 1
+            while k + run < len(shapes) and shapes[k + run] == shapes[k]:
+                run += 1
+            d, p, L = shapes[k]
+            if run < 2:
+                data = read_part(self._codec(d, p), L, digests(k), fetch, k)
+                sink(k, [memoryview(data)[j * L:(j + 1) * L] for j in range(d)])
+            else:
+                k0 = k
+                self.reader(shapes[k]).read(
+                    run, lambda q, i, s: fetch(k0 + q, i, s), lambda q: digests(k0 + q),
+                    lambda q, data: sink(k0 + q, data))
+            k += run

@@ -8,8 +8,8 @@
 //   reed_solomon_erasure::Error (13 variants)          chunky_ec::Error + ErasureError exception
 //   file::hash::Sha256Hash (sha256.rs:14-47)           chunky_ec::Sha256Hash
 //     from_buf / verify / Display (lower-case hex)        from_buf / verify / to_string
-//   file::Chunk (chunk.rs:10-17)                       chunky_ec::Chunk (hash; locations are
-//                                                        keys of a ChunkStore, below)
+//   file::Chunk (chunk.rs:10-17)                       chunky_ec::Chunk (hash + locations: keys
+//                                                        of a ChunkStore, below)
 //   file::FilePart (file_part.rs:57-390)               chunky_ec::FilePart
 //     write_with_encoder (137-225)                        write_with_encoder
 //     read_with_context (73-135)                          read_with_context
@@ -18,7 +18,7 @@
 //   file::FileReference (file_reference.rs)            chunky_ec::FileReference
 //
 // Storage, placement and networking are out of scope: a ChunkStore stands in
-// for the content-addressed locations (`sha256-<hex>` files, location.rs:612).  Rust's
+// for the locations (location -> bytes; shards written as `sha256-<hex>`, location.rs:612).  Rust's
 // `Result<_, Error>` + `?` becomes a thrown ErasureError carrying the same variant; engine
 // failures (no GPU, HIP errors) throw EngineError and are never disguised as crate errors.
 #ifndef CHUNKY_EC_HPP
@@ -409,8 +409,15 @@ class Sha256Hash {
     std::array<uint8_t, 32> digest_{};
 };
 
-// Content-addressed chunk storage standing in for the reference's locations (a shard is
-// written under its hash, location.rs:612).  Not thread-safe.
+// file::Location (location.rs:61-68): where one copy of a chunk lives.  The reference's are file
+// paths and URLs; here they are keys of a ChunkStore.
+using Location = std::string;
+
+// Chunk storage standing in for the reference's locations: location -> bytes.  A shard written
+// through write_shard lands at "sha256-<hex>" (location.rs:605-616: one destination directory;
+// OnConflict::Overwrite, the default outside clusters, location.rs:505) and that location is
+// returned, as ShardWriter::write_shard returns the locations it wrote.  Reads of different
+// locations may run concurrently; writes need the caller's lock.
 class ChunkStore {
    public:
     ChunkStore() = default;
@@ -421,26 +428,32 @@ class ChunkStore {
         return s;
     }
     bool discards() const { return discard_; }
-    void write_shard(const Sha256Hash& hash, Bytes bytes) {
-        if (!discard_) store_[hash] = std::move(bytes);
+    static Location location_of(const Sha256Hash& hash) { return "sha256-" + hash.to_string(); }
+    Location write_shard(const Sha256Hash& hash, Bytes bytes) {
+        Location loc = location_of(hash);
+        if (!discard_) store_[loc] = std::move(bytes);
+        return loc;
     }
-    void write_shard(const Sha256Hash& hash, const uint8_t* bytes, size_t n) {
-        if (!discard_) store_[hash] = Bytes(bytes, bytes + n);
+    Location write_shard(const Sha256Hash& hash, const uint8_t* bytes, size_t n) {
+        return write_shard(hash, Bytes(bytes, bytes + n));
     }
-    std::optional<Bytes> read(const Sha256Hash& hash) const {
-        auto it = store_.find(hash);
+    // Put bytes at any location (a replica elsewhere, a stale copy in tests).
+    void put(const Location& loc, Bytes bytes) { store_[loc] = std::move(bytes); }
+    std::optional<Bytes> read(const Location& loc) const {
+        auto it = store_.find(loc);
         if (it == store_.end()) return std::nullopt;
         return it->second;
     }
-    // The stored bytes without a copy (nullptr if absent); valid until the shard is erased.
-    const Bytes* find(const Sha256Hash& hash) const {
-        auto it = store_.find(hash);
+    // The stored bytes without a copy (nullptr if the location does not read); valid until that
+    // location is written or erased.
+    const Bytes* find(const Location& loc) const {
+        auto it = store_.find(loc);
         return it == store_.end() ? nullptr : &it->second;
     }
-    bool erase(const Sha256Hash& hash) { return store_.erase(hash) > 0; }
-    // Replace a stored shard's bytes (bit rot / tampering in tests).
-    bool corrupt(const Sha256Hash& hash, size_t offset) {
-        auto it = store_.find(hash);
+    bool erase(const Location& loc) { return store_.erase(loc) > 0; }
+    // Flip a bit of the copy at `loc` (bit rot / tampering in tests).
+    bool corrupt(const Location& loc, size_t offset) {
+        auto it = store_.find(loc);
         if (it == store_.end() || offset >= it->second.size()) return false;
         it->second[offset] ^= 0x01;
         return true;
@@ -448,23 +461,31 @@ class ChunkStore {
     size_t size() const { return store_.size(); }
 
    private:
-    std::map<Sha256Hash, Bytes> store_;
+    std::map<Location, Bytes> store_;
     bool discard_ = false;
 };
 
-// file::Chunk: the hash of one chunk (its locations are the ChunkStore key).
+// file::Chunk (chunk.rs:10-17): the hash of one chunk and the locations of its copies, in order.
 struct Chunk {
     Sha256Hash hash;
+    std::vector<Location> locations;
 };
 
-enum class LocationIntegrity { Valid, Invalid, Unavailable, Resilvered };
+// LocationIntegrity (file_part.rs:397-403), in the reference's order (chunk_integrity keeps the
+// smallest).
+enum class LocationIntegrity { Valid, Resilvered, Invalid, Unavailable };
 
-// VerifyPartReport / ResilverPartReport (file_part.rs:392-520, 671-676), reduced to per-chunk
-// status.  write_error: ResilverPartReport::write_error — the reconstruct failure of this part
-// (TooFewShardsPresent when fewer than d chunks verified, file_part.rs:296-308); the other parts
-// of the file are still resilvered.
+// VerifyPartReport / ResilverPartReport (file_part.rs:570-811).  locations: the result of every
+// location of every chunk (read_results: Valid, Invalid, or Unavailable when it does not read).
+// chunks: each chunk's integrity (chunk_integrity, :599-613: Valid when a location is, else the
+// best of its locations; no location at all is Unavailable), Resilvered for a chunk resilver
+// rebuilt and wrote.  new_locations: resilver's writes, appended to the chunks' location lists
+// (:340-347).  write_error: the reconstruct failure of this part (TooFewShardsPresent when fewer
+// than d chunks have a valid copy, :296-308); the other parts of the file are still resilvered.
 struct PartReport {
-    std::vector<LocationIntegrity> chunks;  // d data then p parity
+    std::vector<std::vector<LocationIntegrity>> locations;  // [chunk][location], d data then p
+    std::vector<LocationIntegrity> chunks;                  // d data then p parity
+    std::vector<Location> new_locations;
     std::optional<Error> write_error;
     bool is_ideal() const {
         if (write_error) return false;
@@ -477,7 +498,52 @@ struct PartReport {
         for (auto c : chunks) n += c == what;
         return n;
     }
+    size_t unavailable_locations() const { return count_locations(LocationIntegrity::Unavailable); }
+    size_t invalid_locations() const { return count_locations(LocationIntegrity::Invalid); }
+    size_t count_locations(LocationIntegrity what) const {
+        size_t n = 0;
+        for (const auto& c : locations)
+            for (auto l : c) n += l == what;
+        return n;
+    }
+    // chunks[] from locations[] (chunk_integrity).
+    void summarize() {
+        chunks.assign(locations.size(), LocationIntegrity::Unavailable);
+        for (size_t i = 0; i < locations.size(); ++i)
+            for (auto l : locations[i]) chunks[i] = std::min(chunks[i], l);
+    }
 };
+
+namespace detail {
+// file_part.rs:100-107's walk over a chunk's locations, one step: the first location from `start`
+// on that reads and holds `size` bytes (a copy of another size cannot hash to the digest; the
+// reference hashes it and moves on); *next = the index after it.  nullptr when none is left.
+inline const Bytes* next_copy(const ChunkStore& src, const Chunk& c, size_t start, size_t size,
+                              size_t* next) {
+    for (size_t j = start; j < c.locations.size(); ++j) {
+        const Bytes* b = src.find(c.locations[j]);
+        if (b && b->size() == size) {
+            *next = j + 1;
+            return b;
+        }
+    }
+    *next = c.locations.size();
+    return nullptr;
+}
+
+// Chunks to load next for a part short of d verified chunks: those whose copy failed first (at
+// their next location: the reference walks a chunk's locations before it draws another chunk),
+// then the untried ones.
+inline std::vector<size_t> draw_order(const uint8_t* good, const uint8_t* tried,
+                                      const uint8_t* exhausted, size_t t) {
+    std::vector<size_t> order;
+    for (size_t i = 0; i < t; ++i)
+        if (tried[i] && !good[i] && !exhausted[i]) order.push_back(i);
+    for (size_t i = 0; i < t; ++i)
+        if (!tried[i] && !exhausted[i]) order.push_back(i);
+    return order;
+}
+}  // namespace detail
 
 // file::FilePart.
 struct FilePart {
@@ -489,7 +555,7 @@ struct FilePart {
 
     // write_with_encoder (file_part.rs:137-225): L = ceil(length/d); data chunk j =
     // data_buf[L*j .. L*(j+1)] (data_buf zero padded to d*L, writer.rs:172); parity from
-    // encode_sep; every chunk hashed, in order, and written to `dest` under its hash.
+    // encode_sep; every chunk hashed, in order, and written to `dest`, its location recorded.
     // dest_mu (optional): held while the chunks go into `dest` (several parts written at once,
     // FileWriteBuilder::concurrency); the GPU work runs outside it.
     static FilePart write_with_encoder(const ReedSolomon& encoder, ChunkStore& dest,
@@ -511,92 +577,144 @@ struct FilePart {
         for (size_t i = 0; i < d + p; ++i) {
             std::array<uint8_t, 32> h{};
             std::memcpy(h.data(), &digests[32 * i], 32);
-            const Chunk c{Sha256Hash(h)};
+            Chunk c{Sha256Hash(h), {}};
             const uint8_t* src = i < d ? &data_buf[i * L] : &parity[(i - d) * L];
-            dest.write_shard(c.hash, src, L);
-            (i < d ? part.data : part.parity).push_back(c);
+            c.locations.push_back(dest.write_shard(c.hash, src, L));
+            (i < d ? part.data : part.parity).push_back(std::move(c));
         }
         return part;
     }
 
-    // read_with_context (file_part.rs:73-135): read the chunks, keep those whose hash
-    // verifies, rebuild missing data with reconstruct_data (TooFewShardsPresent when fewer than
-    // d verify) and return the d data chunks concatenated (len_bytes() bytes).  The reference
-    // samples d random chunks; any d verified chunks decode to the same bytes.
+    // read_with_context (file_part.rs:73-135): chunks drawn until d verify (data chunks first
+    // here, so an intact part needs no rebuild; the reference samples at random, and any d
+    // verified chunks decode to the same bytes), each at its first copy whose hash verifies --
+    // a failed copy is followed by the same chunk's next location before another chunk is drawn
+    // (:100-107) -- one hashing launch per round; missing data rebuilt with reconstruct_data
+    // (TooFewShardsPresent when the copies run out); the d data chunks concatenated.
     Bytes read_with_context(const ChunkStore& src) const {
-        const ReedSolomon r(data.size(), parity.size());
-        Shards all = load_verified(src, nullptr);
+        const size_t d = data.size(), t = d + parity.size();
+        std::vector<uint8_t> good(t), tried(t), exhausted(t);
+        std::vector<size_t> cursor(t);
+        Shards all(t);
+        size_t have = 0;
+        while (have < d) {
+            std::vector<size_t> idx;
+            std::vector<const Bytes*> copies;
+            for (size_t i : detail::draw_order(good.data(), tried.data(), exhausted.data(), t)) {
+                if (have + idx.size() >= d) break;
+                tried[i] = 1;
+                const Bytes* b = detail::next_copy(src, chunk(i), cursor[i], chunksize, &cursor[i]);
+                if (!b) {
+                    exhausted[i] = 1;
+                    continue;
+                }
+                idx.push_back(i);
+                copies.push_back(b);
+            }
+            if (idx.empty()) throw ErasureError(Error::TooFewShardsPresent);
+            const std::vector<Sha256Hash> got = Sha256Hash::from_bufs(copies);  // one launch
+            for (size_t k = 0; k < idx.size(); ++k)
+                if (got[k] == chunk(idx[k]).hash) {
+                    good[idx[k]] = 1;
+                    all[idx[k]] = *copies[k];
+                    ++have;
+                }
+        }
         bool complete = true;
-        for (size_t i = 0; i < data.size(); ++i) complete = complete && all[i].has_value();
-        if (!complete) r.reconstruct_data(all);
+        for (size_t i = 0; i < d; ++i) complete = complete && all[i].has_value();
+        if (!complete) ReedSolomon(d, parity.size()).reconstruct_data(all);
         Bytes out;
         out.reserve(len_bytes());
-        for (size_t i = 0; i < data.size(); ++i) out.insert(out.end(), all[i]->begin(), all[i]->end());
+        for (size_t i = 0; i < d; ++i) out.insert(out.end(), all[i]->begin(), all[i]->end());
         return out;
     }
 
-    // verify (file_part.rs:228-251): every chunk read and checked against its hash.
+    // verify (file_part.rs:228-251): every location of every chunk read and its copy checked
+    // against the chunk's hash (one hashing launch).
     PartReport verify(const ChunkStore& src) const {
         PartReport rep;
-        load_verified(src, &rep);
+        check_locations(src, rep, nullptr, nullptr);
+        rep.summarize();
         return rep;
     }
 
-    // resilver (file_part.rs:253-390): verify, reconstruct every missing/invalid chunk (data
-    // and parity) and write it back under its hash.  Rebuilt chunks report Resilvered.
-    // dest_mu (optional): held while reading from and writing to `dest` (several parts resilvered
-    // at once, FileReference::resilver); the GPU work runs outside it.
-    PartReport resilver(ChunkStore& dest, std::mutex* dest_mu = nullptr) const {
+    // resilver (file_part.rs:253-390): every location of every chunk read and checked; each
+    // chunk's first valid copy kept; if a chunk has none, reconstruct (data AND parity), then
+    // every such chunk written to `dest` and the new location APPENDED to the chunk's list
+    // (chunk.locations.extend, :346).  A chunk with a bad copy and a valid one is not rewritten.
+    // Rebuilt chunks report Resilvered.  dest_mu (optional): held while reading from and writing
+    // to `dest` (several parts resilvered at once, FileReference::resilver); the GPU work runs
+    // outside it.
+    PartReport resilver(ChunkStore& dest, std::mutex* dest_mu = nullptr) {
         PartReport rep;
-        Shards all = load_verified(dest, &rep, dest_mu);
+        const size_t d = data.size(), t = d + parity.size();
+        Shards all(t);
+        check_locations(dest, rep, &all, dest_mu);
+        rep.summarize();
         bool any_missing = false;
         for (const auto& s : all) any_missing = any_missing || !s;
         if (!any_missing) return rep;
-        const ReedSolomon r(data.size(), parity.size());
         try {
-            r.reconstruct(all);
+            ReedSolomon(d, parity.size()).reconstruct(all);
         } catch (const ErasureError& e) {  // recorded in the report, as write_error
             rep.write_error = e.error();
             return rep;
         }
         std::unique_lock<std::mutex> lk;
         if (dest_mu) lk = std::unique_lock<std::mutex>(*dest_mu);
-        for (size_t i = 0; i < all.size(); ++i) {
+        for (size_t i = 0; i < t; ++i) {
             if (rep.chunks[i] == LocationIntegrity::Valid) continue;
-            dest.write_shard(chunk(i).hash, *all[i]);
+            Chunk& c = chunk_mut(i);
+            c.locations.push_back(dest.write_shard(c.hash, *all[i]));
+            rep.new_locations.push_back(c.locations.back());
             rep.chunks[i] = LocationIntegrity::Resilvered;
         }
         return rep;
     }
 
     const Chunk& chunk(size_t i) const { return i < data.size() ? data[i] : parity[i - data.size()]; }
+    Chunk& chunk_mut(size_t i) { return i < data.size() ? data[i] : parity[i - data.size()]; }
 
    private:
-    Shards load_verified(const ChunkStore& src, PartReport* rep,
-                         std::mutex* src_mu = nullptr) const {
+    // Every location's copy of every chunk hashed in one launch: rep.locations filled; with
+    // `first_valid`, each chunk's first valid copy is copied there.  The copies are taken under
+    // `mu` (a resilver elsewhere may be writing the store).
+    void check_locations(const ChunkStore& src, PartReport& rep, Shards* first_valid,
+                         std::mutex* mu) const {
         const size_t t = data.size() + parity.size();
-        Shards all(t);
-        std::vector<const Bytes*> loaded;
-        std::vector<size_t> idx;
+        rep.locations.assign(t, {});
+        std::vector<Bytes> held;  // copies taken under the lock
+        std::vector<const Bytes*> copies;
+        std::vector<std::pair<size_t, size_t>> at;
         {
             std::unique_lock<std::mutex> lk;
-            if (src_mu) lk = std::unique_lock<std::mutex>(*src_mu);
-            for (size_t i = 0; i < t; ++i) all[i] = src.read(chunk(i).hash);
-        }
-        for (size_t i = 0; i < t; ++i) {
-            if (all[i]) {
-                loaded.push_back(&*all[i]);
-                idx.push_back(i);
+            if (mu) lk = std::unique_lock<std::mutex>(*mu);
+            held.reserve(64);
+            for (size_t i = 0; i < t; ++i) {
+                const Chunk& c = chunk(i);
+                rep.locations[i].assign(c.locations.size(), LocationIntegrity::Unavailable);
+                for (size_t j = 0; j < c.locations.size(); ++j) {
+                    const Bytes* b = src.find(c.locations[j]);
+                    if (!b) continue;
+                    if (b->size() != chunksize) {  // cannot hash to the digest
+                        rep.locations[i][j] = LocationIntegrity::Invalid;
+                        continue;
+                    }
+                    at.emplace_back(i, j);
+                    if (mu) held.push_back(*b);
+                    else copies.push_back(b);
+                }
             }
         }
-        if (rep) rep->chunks.assign(t, LocationIntegrity::Unavailable);
-        const std::vector<Sha256Hash> got = Sha256Hash::from_bufs(loaded);  // one launch
-        for (size_t k = 0; k < idx.size(); ++k) {
-            const bool ok = got[k] == chunk(idx[k]).hash;
-            if (rep) rep->chunks[idx[k]] = ok ? LocationIntegrity::Valid : LocationIntegrity::Invalid;
-            if (!ok) all[idx[k]].reset();
+        if (mu)
+            for (const Bytes& b : held) copies.push_back(&b);
+        const std::vector<Sha256Hash> got = Sha256Hash::from_bufs(copies);  // one launch
+        for (size_t k = 0; k < at.size(); ++k) {
+            const auto [i, j] = at[k];
+            const bool ok = got[k] == chunk(i).hash;
+            rep.locations[i][j] = ok ? LocationIntegrity::Valid : LocationIntegrity::Invalid;
+            if (ok && first_valid && !(*first_valid)[i]) (*first_valid)[i] = *copies[k];
         }
-        return all;
     }
 };
 
@@ -616,10 +734,10 @@ struct FileReference {
     // parts_per_batch > 0: runs of parts of one shape go through the multi-GPU scheduler
     // (cec_multi: a whole window of parts verified + rebuilt per launch, sharded over `devices`,
     // default the current device) the way the reference reads (file_part.rs:86-122): d chunks
-    // loaded per part, and for a part whose loaded chunks do not all verify, more chunks loaded
-    // and the part resubmitted (CEC_PRESENT_VERIFIED marks the chunks already verified) until d
-    // verify or none are left (TooFewShardsPresent).  Same bytes and the same failure as the
-    // per-part path.
+    // loaded per part, and for a part whose loaded chunks do not all verify, the failed chunks'
+    // next locations and then more chunks loaded and the part resubmitted (CEC_PRESENT_VERIFIED
+    // marks the chunks already verified) until d verify or the copies run out
+    // (TooFewShardsPresent).  Same bytes and the same failure as the per-part path.
     Bytes read(const ChunkStore& src, size_t parts_per_batch = 0, size_t depth = 4,
                const std::vector<int>& devices = {}) const {
         uint64_t total = 0;
@@ -656,32 +774,25 @@ struct FileReference {
                 [&](size_t, const Bytes& b) { emit(b.data(), b.size()); });
             return;
         }
-        size_t k = 0;
-        while (k < parts.size()) {
-            size_t run = 1;
-            // A run shares one scheduler, so its parts must share the whole shape: the metadata
-            // allows a different d/p per part (file_part.rs:77 builds a codec per part).
-            while (parts_per_batch && k + run < parts.size() &&
-                   parts[k + run].chunksize == parts[k].chunksize &&
-                   parts[k + run].data.size() == parts[k].data.size() &&
-                   parts[k + run].parity.size() == parts[k].parity.size())
-                ++run;
-            if (run < 2) {
-                const Bytes b = parts[k].read_with_context(src);
+        for_runs(parts_per_batch, [&](size_t k0, size_t n) {
+            // a run shares one scheduler, so its parts share the whole shape: the metadata allows
+            // a different d/p per part (file_part.rs:77 builds a codec per part)
+            if (n < 2) {
+                const Bytes b = parts[k0].read_with_context(src);
                 emit(b.data(), b.size());
             } else {
-                read_run(src, k, run, parts_per_batch, depth, devices, emit);
+                read_run(src, k0, n, parts_per_batch, depth, devices, emit);
             }
-            k += run;
-        }
+        });
     }
     // FileReference::verify / resilver (file_reference.rs:78-113 over FilePart::verify /
     // resilver, file_part.rs:228-390).  parts_per_batch > 0: runs of parts of one shape go
     // through the multi-GPU scheduler (cec_multi_verify / cec_multi_resilver over `devices`):
-    // every stored chunk loaded, hashed against its metadata digest, and (resilver) every chunk
-    // that is missing or fails rebuilt and written back.  Same reports as the per-part calls: a
-    // part that cannot be rebuilt gets write_error (TooFewShardsPresent) in its report and the
-    // remaining parts are still resilvered (file_reference.rs:103-110 collects every report).
+    // every location of every chunk hashed against its metadata digest, and (resilver) every
+    // chunk with no valid copy rebuilt, written back and its new location appended.  Same
+    // reports as the per-part calls: a part that cannot be rebuilt gets write_error in its
+    // report and the remaining parts are still resilvered (file_reference.rs:103-110 collects
+    // every report).
     std::vector<PartReport> verify(const ChunkStore& src, size_t parts_per_batch = 0,
                                    size_t depth = 4, const std::vector<int>& devices = {}) const {
         std::vector<PartReport> r(parts.size());
@@ -694,12 +805,12 @@ struct FileReference {
         for_runs(parts_per_batch, [&](size_t k0, size_t n) {
             if (n < 2) r[k0] = parts[k0].verify(src);
             else check_run(const_cast<ChunkStore&>(src), k0, n, parts_per_batch, depth, devices,
-                           false, r);
+                           nullptr, r);  // verify only reads the store
         });
         return r;
     }
     std::vector<PartReport> resilver(ChunkStore& dest, size_t parts_per_batch = 0,
-                                     size_t depth = 4, const std::vector<int>& devices = {}) const {
+                                     size_t depth = 4, const std::vector<int>& devices = {}) {
         std::vector<PartReport> r(parts.size());
         if (!parts_per_batch) {  // buffered(10) (file_reference.rs:103-110)
             std::mutex dest_mu;
@@ -711,7 +822,7 @@ struct FileReference {
         }
         for_runs(parts_per_batch, [&](size_t k0, size_t n) {
             if (n < 2) r[k0] = parts[k0].resilver(dest);
-            else check_run(dest, k0, n, parts_per_batch, depth, devices, true, r);
+            else check_run(dest, k0, n, parts_per_batch, depth, devices, &parts, r);
         });
         return r;
     }
@@ -739,10 +850,14 @@ struct FileReference {
         size_t first = 0, n = 0;
         uint64_t job = 0;
         bool live = false;
-        detail::PinnedBuf chunks;   // [W][t][L] every stored chunk (DMA'd directly)
+        detail::PinnedBuf chunks;   // [W][t][L] the copies (DMA'd directly)
         detail::PinnedBuf rebuilt;  // [W][t][L] resilver: the rebuilt chunks
+        Bytes spill;                // verify: copies beyond the pinned window (many locations)
         std::vector<uint8_t> present, expected, verified;
         std::vector<int> status;
+        // verify: one item per copy hashed, (window part, chunk, location); resilver: the chunks
+        // whose lone copy the resilver job hashes
+        std::vector<std::array<uint32_t, 3>> items;
     };
     static std::array<CheckWindow, 8>& check_windows() {
         thread_local std::array<CheckWindow, 8> win;
@@ -751,11 +866,17 @@ struct FileReference {
 
     // verify / resilver of parts [k0, k0 + n) (one shape) through cec_multi: windows of one
     // pipeline batch per shard (ppb x shards parts), up to `depth` in flight, so loading the next
-    // windows overlaps the GPU work; every stored chunk is loaded, reports (and resilver's
-    // write-backs) are made window by window in file order.
+    // windows overlaps the GPU work; reports (and resilver's write-backs) are made window by
+    // window in file order.  verify: every copy of the window is one item of a cec_multi_verify
+    // job, d + p items per scheduler row whatever chunk they belong to.  resilver: a window whose
+    // chunks have one location each is one cec_multi_resilver job; the copies of chunks with
+    // several locations are hashed first (a verify job) and their first valid copy goes to the
+    // resilver job flagged CEC_PRESENT_VERIFIED: every copy is hashed exactly once.
+    // rebuilt_into: resilver (its parts get the new locations); nullptr: verify.
     void check_run(ChunkStore& store, size_t k0, size_t n, size_t ppb, size_t depth,
-                   const std::vector<int>& devices, bool resilver,
+                   const std::vector<int>& devices, std::vector<FilePart>* rebuilt_into,
                    std::vector<PartReport>& reports) const {
+        const bool resilver = rebuilt_into != nullptr;
         const FilePart& first = parts[k0];
         const size_t d = first.data.size(), t = d + first.parity.size(), L = first.chunksize;
         const std::vector<int> devs = detail::devices_or_current(devices);
@@ -763,58 +884,159 @@ struct FileReference {
         const size_t W = ppb * devs.size();
         std::array<CheckWindow, 8>& win = check_windows();
         const size_t nwin = std::min<size_t>(std::max<size_t>(depth, 2), win.size());
-        auto submit = [&](CheckWindow& w, size_t at, size_t cnt) {
-            uint8_t* chunks = w.chunks.reserve(W * t * L, devs[0]);
-            uint8_t* rebuilt = resilver ? w.rebuilt.reserve(W * t * L, devs[0]) : nullptr;
-            w.present.assign(cnt * t, 0);
-            w.expected.resize(cnt * t * 32);
-            w.verified.assign(cnt * t, 0);
-            w.status.assign(cnt, 0);
-            detail::parallel_for(cnt, [&](size_t q) {
+        // the report skeleton of window part q: Unavailable where a location does not read,
+        // Invalid where its copy has the wrong size, Valid (to be checked) otherwise
+        auto skeleton = [&](size_t at, size_t cnt) {
+            for (size_t q = 0; q < cnt; ++q) {
                 const FilePart& part = parts[k0 + at + q];
+                PartReport& rep = reports[k0 + at + q];
+                rep = PartReport{};
+                rep.locations.assign(t, {});
                 for (size_t i = 0; i < t; ++i) {
-                    std::memcpy(&w.expected[(q * t + i) * 32], part.chunk(i).hash.digest().data(), 32);
-                    const Bytes* bytes = store.find(part.chunk(i).hash);
-                    const bool ok = bytes && bytes->size() == L;
-                    w.present[q * t + i] = ok ? 1 : 0;
-                    if (ok) std::memcpy(chunks + (q * t + i) * L, bytes->data(), L);
+                    const Chunk& c = part.chunk(i);
+                    rep.locations[i].assign(c.locations.size(), LocationIntegrity::Unavailable);
+                    for (size_t j = 0; j < c.locations.size(); ++j) {
+                        const Bytes* b = store.find(c.locations[j]);
+                        if (b) rep.locations[i][j] = b->size() == L ? LocationIntegrity::Valid
+                                                                    : LocationIntegrity::Invalid;
+                    }
                 }
+            }
+        };
+        // a verify job over `items` of window [at, at + cnt): copies into buf (g rows of t),
+        // flags into `verified`; returns the job
+        auto verify_items = [&](const std::vector<std::array<uint32_t, 3>>& items, size_t at,
+                                uint8_t* buf, std::vector<uint8_t>& present,
+                                std::vector<uint8_t>& expected, std::vector<uint8_t>& verified) {
+            const size_t g = (items.size() + t - 1) / t;
+            present.assign(g * t, 0);
+            expected.assign(g * t * 32, 0);
+            verified.assign(g * t, 0);
+            detail::parallel_for(items.size(), [&](size_t x) {
+                const auto& it = items[x];
+                const Chunk& c = parts[k0 + at + it[0]].chunk(it[1]);
+                std::memcpy(buf + x * L, store.find(c.locations[it[2]])->data(), L);
+                std::memcpy(&expected[x * 32], c.hash.digest().data(), 32);
+                present[x] = 1;
             });
-            if (resilver)
-                detail::check_multi(cec_multi_resilver(m, chunks, w.present.data(), w.expected.data(),
-                                                       cnt, rebuilt, w.verified.data(),
-                                                       w.status.data(), nullptr, &w.job));
-            else
-                detail::check_multi(cec_multi_verify(m, chunks, w.present.data(), w.expected.data(),
-                                                     cnt, w.verified.data(), &w.job));
+            uint64_t job = 0;
+            detail::check_multi(cec_multi_verify(m, buf, present.data(), expected.data(), g,
+                                                 verified.data(), &job));
+            return job;
+        };
+        auto submit = [&](CheckWindow& w, size_t at, size_t cnt) {
+            skeleton(at, cnt);
+            uint8_t* chunks = w.chunks.reserve(W * t * L, devs[0]);
+            w.items.clear();
+            if (!resilver) {
+                for (size_t q = 0; q < cnt; ++q)
+                    for (size_t i = 0; i < t; ++i) {
+                        const auto& locs = reports[k0 + at + q].locations[i];
+                        for (size_t j = 0; j < locs.size(); ++j)
+                            if (locs[j] == LocationIntegrity::Valid)
+                                w.items.push_back({uint32_t(q), uint32_t(i), uint32_t(j)});
+                    }
+                uint8_t* buf = chunks;
+                if (w.items.size() > W * t) {  // more copies than the pinned window holds
+                    w.spill.resize(w.items.size() * L);
+                    buf = w.spill.data();
+                }
+                w.job = w.items.empty() ? 0 : verify_items(w.items, at, buf, w.present,
+                                                          w.expected, w.verified);
+            } else {
+                // chunks with several locations: every copy hashed first (file_part.rs:277-289)
+                std::vector<std::array<uint32_t, 3>> multi;
+                for (size_t q = 0; q < cnt; ++q)
+                    for (size_t i = 0; i < t; ++i) {
+                        const auto& locs = reports[k0 + at + q].locations[i];
+                        if (locs.size() < 2) continue;
+                        for (size_t j = 0; j < locs.size(); ++j)
+                            if (locs[j] == LocationIntegrity::Valid)
+                                multi.push_back({uint32_t(q), uint32_t(i), uint32_t(j)});
+                    }
+                if (!multi.empty()) {
+                    Bytes buf(((multi.size() + t - 1) / t) * t * L);
+                    std::vector<uint8_t> pr, ex, ver;
+                    const uint64_t job = verify_items(multi, at, buf.data(), pr, ex, ver);
+                    detail::check_multi(cec_multi_wait(m, job));
+                    for (size_t x = 0; x < multi.size(); ++x)
+                        reports[k0 + at + multi[x][0]].locations[multi[x][1]][multi[x][2]] =
+                            ver[x] ? LocationIntegrity::Valid : LocationIntegrity::Invalid;
+                }
+                uint8_t* rebuilt = w.rebuilt.reserve(W * t * L, devs[0]);
+                w.present.assign(cnt * t, 0);
+                w.expected.resize(cnt * t * 32);
+                w.verified.assign(cnt * t, 0);
+                w.status.assign(cnt, 0);
+                for (size_t q = 0; q < cnt; ++q)
+                    for (size_t i = 0; i < t; ++i) {
+                        const auto& locs = reports[k0 + at + q].locations[i];
+                        if (locs.size() == 1 && locs[0] == LocationIntegrity::Valid)
+                            w.items.push_back({uint32_t(q), uint32_t(i), 0});
+                    }
+                detail::parallel_for(cnt, [&](size_t q) {
+                    const FilePart& part = parts[k0 + at + q];
+                    const auto& rl = reports[k0 + at + q].locations;
+                    for (size_t i = 0; i < t; ++i) {
+                        const Chunk& c = part.chunk(i);
+                        std::memcpy(&w.expected[(q * t + i) * 32], c.hash.digest().data(), 32);
+                        const auto& locs = rl[i];
+                        const auto valid = std::find(locs.begin(), locs.end(),
+                                                     LocationIntegrity::Valid);
+                        if (valid == locs.end()) continue;
+                        const size_t j = size_t(valid - locs.begin());
+                        std::memcpy(chunks + (q * t + i) * L, store.find(c.locations[j])->data(), L);
+                        // a lone copy is hashed by the resilver job; one from a chunk with several
+                        // locations was verified above
+                        w.present[q * t + i] = locs.size() == 1 ? 1 : CEC_PRESENT_VERIFIED;
+                    }
+                });
+                detail::check_multi(cec_multi_resilver(m, chunks, w.present.data(),
+                                                       w.expected.data(), cnt, rebuilt,
+                                                       w.verified.data(), w.status.data(), nullptr,
+                                                       &w.job));
+            }
             w.first = at;
             w.n = cnt;
             w.live = true;
         };
         auto collect = [&](CheckWindow& w) {
             w.live = false;
+            if (!resilver) {
+                if (!w.items.empty()) detail::check_multi(cec_multi_wait(m, w.job));
+                for (size_t x = 0; x < w.items.size(); ++x) {
+                    const auto& it = w.items[x];
+                    reports[k0 + w.first + it[0]].locations[it[1]][it[2]] =
+                        w.verified[x] ? LocationIntegrity::Valid : LocationIntegrity::Invalid;
+                }
+                for (size_t q = 0; q < w.n; ++q) reports[k0 + w.first + q].summarize();
+                return;
+            }
             detail::check_multi(cec_multi_wait(m, w.job));
-            const uint8_t* rebuilt = resilver ? w.rebuilt.reserve(W * t * L, devs[0]) : nullptr;
+            for (const auto& it : w.items)  // the lone copies the resilver job hashed
+                reports[k0 + w.first + it[0]].locations[it[1]][0] =
+                    w.verified[it[0] * t + it[1]] ? LocationIntegrity::Valid
+                                                  : LocationIntegrity::Invalid;
+            const uint8_t* rebuilt = w.rebuilt.reserve(W * t * L, devs[0]);
             for (size_t q = 0; q < w.n; ++q) {
                 PartReport& rep = reports[k0 + w.first + q];
-                rep.chunks.assign(t, LocationIntegrity::Unavailable);
+                rep.summarize();
                 bool missing = false;
-                for (size_t i = 0; i < t; ++i) {
-                    if (w.present[q * t + i])
-                        rep.chunks[i] = w.verified[q * t + i] ? LocationIntegrity::Valid
-                                                              : LocationIntegrity::Invalid;
-                    missing = missing || !w.verified[q * t + i];
-                }
-                if (!resilver || !missing) continue;
-                if (w.status[q] == CEC_TOO_FEW_SHARDS_PRESENT) {  // this part's write_error;
-                    rep.write_error = Error::TooFewShardsPresent;  // the others go on
+                for (size_t i = 0; i < t; ++i) missing = missing || !w.verified[q * t + i];
+                if (!missing) continue;
+                if (w.status[q] != CEC_OK) {  // this part's write_error; the others go on
+                    if (w.status[q] >= CEC_TOO_FEW_SHARDS && w.status[q] <= CEC_INVALID_INDEX)
+                        rep.write_error = static_cast<Error>(w.status[q]);
+                    else
+                        detail::check(w.status[q]);  // an engine failure is the job's
                     continue;
                 }
-                detail::check(w.status[q]);  // any other failure is itself, as per part
-                const FilePart& part = parts[k0 + w.first + q];
+                FilePart& part = (*rebuilt_into)[k0 + w.first + q];
                 for (size_t i = 0; i < t; ++i) {
                     if (w.verified[q * t + i]) continue;
-                    store.write_shard(part.chunk(i).hash, rebuilt + (q * t + i) * L, L);
+                    Chunk& c = part.chunk_mut(i);
+                    c.locations.push_back(store.write_shard(c.hash, rebuilt + (q * t + i) * L, L));
+                    rep.new_locations.push_back(c.locations.back());
                     rep.chunks[i] = LocationIntegrity::Resilvered;
                 }
             }
@@ -835,7 +1057,7 @@ struct FileReference {
         } catch (...) {
             for (auto& w : win)  // no job may still write into the window buffers
                 if (w.live) {
-                    (void)cec_multi_wait(m, w.job);
+                    if (resilver || !w.items.empty()) (void)cec_multi_wait(m, w.job);
                     w.live = false;
                 }
             throw;
@@ -849,7 +1071,8 @@ struct FileReference {
         bool live = false;
         detail::PinnedBuf chunks;  // [W][t][L] loaded chunk bytes (DMA'd directly)
         detail::PinnedBuf out;     // [W][d][L] the parts' data (DMA'd directly)
-        std::vector<uint8_t> present, expected, verified;
+        std::vector<uint8_t> present, expected, verified, exhausted;
+        std::vector<size_t> cursor;  // per chunk: the next location to read
         std::vector<int> status;
     };
     static constexpr size_t kMaxReadWindows = 8;
@@ -880,17 +1103,24 @@ struct FileReference {
             w.present.assign(cnt * t, 0);
             w.expected.resize(cnt * t * 32);
             w.verified.assign(cnt * t, 0);
+            w.exhausted.assign(cnt * t, 0);
+            w.cursor.assign(cnt * t, 0);
             w.status.assign(cnt, 0);
-            // The reference loads d chunks per part (file_part.rs:86-107): the first d stored
-            // ones here (data chunks first: no rebuild when they are all there).
+            // The reference loads d chunks per part (file_part.rs:86-107): the first d that have
+            // a copy here (data chunks first: no rebuild when they are all there), each at its
+            // first location that reads.
             detail::parallel_for(cnt, [&](size_t q) {
                 const FilePart& part = parts[k0 + at + q];
                 size_t loaded = 0;
                 for (size_t i = 0; i < t; ++i) {
                     std::memcpy(&w.expected[(q * t + i) * 32], part.chunk(i).hash.digest().data(), 32);
                     if (loaded == d) continue;
-                    const Bytes* bytes = src.find(part.chunk(i).hash);
-                    if (!bytes || bytes->size() != L) continue;
+                    const Bytes* bytes =
+                        detail::next_copy(src, part.chunk(i), 0, L, &w.cursor[q * t + i]);
+                    if (!bytes) {
+                        w.exhausted[q * t + i] = 1;
+                        continue;
+                    }
                     std::memcpy(ch + (q * t + i) * L, bytes->data(), L);
                     w.present[q * t + i] = 1;
                     ++loaded;
@@ -936,20 +1166,32 @@ struct FileReference {
         }
     }
 
-    // file_part.rs:92-107: a loaded chunk whose hash fails is dropped and another one is read.
-    // The failed parts of a window are resubmitted with the chunks that verified (marked
-    // CEC_PRESENT_VERIFIED: not hashed again) plus as many untried stored chunks as are missing,
-    // until they decode or no chunk is left (TooFewShardsPresent, as the reference's read).
-    // The rebuilt data of window part q goes to out + q*d*L.
+    // file_part.rs:92-107: a copy whose hash fails is dropped and the same chunk's next location
+    // read, and a chunk with no valid copy left is replaced by another chunk.  The failed parts of
+    // a window are resubmitted with the chunks that verified (marked CEC_PRESENT_VERIFIED: not
+    // hashed again) plus, up to d, the failed chunks' next copies and then untried chunks, until
+    // they decode or no copy is left (TooFewShardsPresent, as the reference's read).  The rebuilt
+    // data of window part q goes to out + q*d*L.
     void retry(const ChunkStore& src, cec_multi* m, size_t k0, size_t d, size_t t, size_t L,
                const ReadWindow& w, const std::vector<size_t>& failed, uint8_t* out) const {
         const size_t f = failed.size();
-        std::vector<uint8_t> tried(f * t), good(f * t);
+        std::vector<uint8_t> tried(f * t), good(f * t), exhausted(f * t);
+        std::vector<size_t> cursor(f * t);
+        std::vector<const Bytes*> held(f * t, nullptr);  // the copy each chunk verified with
         for (size_t r = 0; r < f; ++r)
             for (size_t i = 0; i < t; ++i) {
-                tried[r * t + i] = w.present[failed[r] * t + i] != 0;
-                good[r * t + i] = w.verified[failed[r] * t + i] != 0;
+                const size_t x = failed[r] * t + i;
+                tried[r * t + i] = w.present[x] != 0;
+                good[r * t + i] = w.verified[x] != 0;
+                exhausted[r * t + i] = w.exhausted[x];
+                cursor[r * t + i] = w.cursor[x];
             }
+        // the copies that verified in the window's pass: the location before each cursor
+        for (size_t r = 0; r < f; ++r) {
+            const FilePart& part = parts[k0 + w.first + failed[r]];
+            for (size_t i = 0; i < t; ++i)
+                if (good[r * t + i]) held[r * t + i] = src.find(part.chunk(i).locations[cursor[r * t + i] - 1]);
+        }
         Bytes chunks(f * t * L), data(f * d * L);
         std::vector<uint8_t> present(f * t), expected(f * t * 32), verified(f * t);
         std::vector<int> status(f);
@@ -964,19 +1206,26 @@ struct FileReference {
                 const size_t r = open[q];
                 const FilePart& part = parts[k0 + w.first + failed[r]];
                 size_t have = 0, added = 0;
-                for (size_t i = 0; i < t; ++i) have += good[r * t + i];
                 for (size_t i = 0; i < t; ++i) {
                     std::memcpy(&expected[(q * t + i) * 32], part.chunk(i).hash.digest().data(), 32);
-                    const Bytes* bytes = src.find(part.chunk(i).hash);
-                    if (good[r * t + i]) {
-                        std::memcpy(&chunks[(q * t + i) * L], bytes->data(), L);
-                        present[q * t + i] = CEC_PRESENT_VERIFIED;
-                    } else if (!tried[r * t + i] && have + added < d && bytes && bytes->size() == L) {
-                        std::memcpy(&chunks[(q * t + i) * L], bytes->data(), L);
-                        present[q * t + i] = 1;
-                        tried[r * t + i] = 1;
-                        ++added;
+                    if (!good[r * t + i]) continue;
+                    ++have;
+                    std::memcpy(&chunks[(q * t + i) * L], held[r * t + i]->data(), L);
+                    present[q * t + i] = CEC_PRESENT_VERIFIED;
+                }
+                for (size_t i : detail::draw_order(&good[r * t], &tried[r * t], &exhausted[r * t], t)) {
+                    if (!(have + added < d)) break;
+                    tried[r * t + i] = 1;
+                    const Bytes* bytes = detail::next_copy(src, part.chunk(i), cursor[r * t + i], L,
+                                                           &cursor[r * t + i]);
+                    if (!bytes) {
+                        exhausted[r * t + i] = 1;
+                        continue;
                     }
+                    held[r * t + i] = bytes;
+                    std::memcpy(&chunks[(q * t + i) * L], bytes->data(), L);
+                    present[q * t + i] = 1;
+                    ++added;
                 }
                 if (added == 0) throw ErasureError(Error::TooFewShardsPresent);
             }
@@ -1132,11 +1381,11 @@ class FileWriteBuilder {
                 for (size_t i = 0; i < t; ++i) {
                     std::array<uint8_t, 32> h{};
                     std::memcpy(h.data(), dig + (k * t + i) * 32, 32);
-                    const Chunk c{Sha256Hash(h)};
+                    Chunk c{Sha256Hash(h), {}};
                     const uint8_t* src = i < d ? bytes + ((w.first + k) * d + i) * L
                                                : par + (k * p + (i - d)) * L;
-                    dest.write_shard(c.hash, src, L);
-                    (i < d ? part.data : part.parity).push_back(c);
+                    c.locations.push_back(dest.write_shard(c.hash, src, L));
+                    (i < d ? part.data : part.parity).push_back(std::move(c));
                 }
                 file.parts.push_back(std::move(part));
             }

@@ -13,6 +13,8 @@
 //                               chunks: 17 parts, last chunksize 699 051, read back bit-exact
 //   test_batched_paths          FileWriteBuilder::batch / FileReference::read batched through
 //                               the host-staged pipelines == the per-part path, bit-exact
+//   test_locations_bad_then_good  chunks listed [bad copy, good copy]: read walks the locations,
+//                               verify flags exactly the bad ones, resilver appends
 //   test_one_encode             JavaReedSolomon testOneEncode RS(5,5) (crate KAT)
 //   test_matrix_rows            SURVEY.md Appendix A RS(3,2) / RS(10,4) parity rows
 //   test_errors                 reed_solomon_erasure::Error variants of ReedSolomon::new,
@@ -102,36 +104,40 @@ void test_file_write() {
 void test_resilver() {
     ChunkStore store;
     const Bytes input = cluster_reader_bytes();
-    const FileReference file_ref =
+    FileReference file_ref =
         FileWriteBuilder().chunk_size(size_t(1) << 10).data_chunks(3).parity_chunks(2).write(input, store);
     // File should be 100% valid
     for (const auto& r : file_ref.verify(store)) CHECK(r.is_ideal());
     size_t deleted_chunks = 0;
     for (const auto& part : file_ref.parts) {
-        CHECK(store.erase(part.data.front().hash));    // delete 1 / 3 data chunks
-        CHECK(!store.read(part.data.front().hash));
-        CHECK(store.erase(part.parity.front().hash));  // delete 1 / 2 parity chunks
-        CHECK(!store.read(part.parity.front().hash));
+        const Location& d0 = part.data.front().locations.front();  // delete 1 / 3 data chunks
+        CHECK(store.erase(d0));
+        CHECK(!store.read(d0));
+        const Location& p0 = part.parity.front().locations.front();  // delete 1 / 2 parity chunks
+        CHECK(store.erase(p0));
+        CHECK(!store.read(p0));
         deleted_chunks += 2;
     }
     // File should not be 100% valid, but still available
     size_t unavailable = 0;
     for (const auto& r : file_ref.verify(store)) {
         CHECK(!r.is_ideal());
-        unavailable += r.count(LocationIntegrity::Unavailable);
+        unavailable += r.unavailable_locations();  // verify_report.unavailable_locations()
     }
     CHECK(unavailable == deleted_chunks);
     CHECK(file_ref.read(store) == input);  // reads decode around the holes
-    size_t resilvered = 0;
+    size_t new_locations = 0;
     for (const auto& r : file_ref.resilver(store)) {
         CHECK(r.is_ideal());
-        resilvered += r.count(LocationIntegrity::Resilvered);
+        new_locations += r.new_locations.size();  // resilver_report.new_locations()
     }
-    CHECK(resilvered == deleted_chunks);
+    CHECK(new_locations == deleted_chunks);
+    // the new locations are appended (file_part.rs:346): [the deleted one, the rewritten one]
+    for (const auto& part : file_ref.parts) CHECK(part.data.front().locations.size() == 2);
     for (const auto& r : file_ref.verify(store)) CHECK(r.is_ideal());
     CHECK(file_ref.read(store) == input);
     // a corrupted chunk is not trusted: it verifies Invalid and is rebuilt by resilver
-    const Sha256Hash& victim = file_ref.parts[2].data[1].hash;
+    const Location victim = file_ref.parts[2].data[1].locations.front();
     CHECK(store.corrupt(victim, 17));
     CHECK(file_ref.parts[2].verify(store).count(LocationIntegrity::Invalid) == 1);
     CHECK(file_ref.read(store) == input);
@@ -191,8 +197,8 @@ void test_cp_50mib() {
     CHECK(Sha256Hash::from_buf(&input[0], size_t(1) << 20) == f.parts[0].data[0].hash);
     CHECK(Sha256Hash::from_buf(&input[size_t(48) << 20], 699051) == f.parts[16].data[0].hash);
     for (const auto& part : f.parts) {
-        store.erase(part.data[2].hash);
-        store.erase(part.parity[1].hash);
+        store.erase(part.data[2].locations[0]);
+        store.erase(part.parity[1].locations[0]);
     }
     CHECK(f.read(store) == input);
 }
@@ -244,16 +250,17 @@ void test_batched_paths() {
             CHECK(a.parts[k].chunksize == c.parts[k].chunksize);
             for (size_t i = 0; i < d + p; ++i) {
                 CHECK(a.parts[k].chunk(i).hash == c.parts[k].chunk(i).hash);
-                CHECK(batched.read(c.parts[k].chunk(i).hash) == per_part.read(a.parts[k].chunk(i).hash));
+                CHECK(batched.read(c.parts[k].chunk(i).locations[0]) ==
+                      per_part.read(a.parts[k].chunk(i).locations[0]));
             }
         }
         // holes: one data + one parity chunk per part, then (where p leaves room) a corrupted
         // chunk in part 3 that the read must not trust
         for (const auto& part : c.parts) {
-            batched.erase(part.data[1 % d].hash);
-            batched.erase(part.parity[0].hash);
+            batched.erase(part.data[1 % d].locations[0]);
+            batched.erase(part.parity[0].locations[0]);
         }
-        if (p >= 3) CHECK(batched.corrupt(c.parts[3].data[0].hash, 5));
+        if (p >= 3) CHECK(batched.corrupt(c.parts[3].data[0].locations[0], 5));
         CHECK(c.read(batched, 8, 3) == input);
         CHECK(c.read(batched) == input);
         // streamed (reader.rs:40-75): the same bytes in order, piece by piece, the last part cut
@@ -276,8 +283,8 @@ void test_batched_paths() {
             CHECK(pieces >= 2);
         }
         // a part with fewer than d usable chunks fails like the per-part read
-        for (size_t i = 2; i < d + p; ++i) batched.erase(c.parts[5].chunk(i).hash);
-        CHECK(batched.corrupt(c.parts[5].chunk(0).hash, 1));
+        for (size_t i = 2; i < d + p; ++i) batched.erase(c.parts[5].chunk(i).locations[0]);
+        CHECK(batched.corrupt(c.parts[5].chunk(0).locations[0], 1));
         CHECK(throws_erasure([&] { c.read(batched, 8, 3); }, Error::TooFewShardsPresent));
     }
 }
@@ -308,10 +315,10 @@ void test_multi_device_paths() {
         CHECK(c.read(store, 3, 2, devs) == input);
         // data chunk 0 corrupted in every other part: the d-chunk first pass fails its hash,
         // the retry loads the next stored chunk
-        for (size_t k = 0; k < n_parts; k += 2) CHECK(store.corrupt(c.parts[k].data[0].hash, 9));
+        for (size_t k = 0; k < n_parts; k += 2) CHECK(store.corrupt(c.parts[k].data[0].locations[0], 9));
         CHECK(c.read(store, 3, 2, devs) == input);
         // and a part whose usable chunks run out
-        for (size_t i = 1; i < d + p - (d - 2); ++i) store.erase(c.parts[7].chunk(i).hash);
+        for (size_t i = 1; i < d + p - (d - 2); ++i) store.erase(c.parts[7].chunk(i).locations[0]);
         CHECK(throws_erasure([&] { c.read(store, 3, 2, devs); }, Error::TooFewShardsPresent));
     }
 }
@@ -324,13 +331,13 @@ void test_batched_verify_resilver() {
     const size_t d = 3, p = 3, chunk = 1024;  // 2 lost + 1 corrupt leaves exactly d
     const Bytes input = random_bytes(d * chunk * 11 + 500, 99);
     ChunkStore store;
-    const FileReference f =
+    FileReference f =
         FileWriteBuilder().chunk_size(chunk).data_chunks(d).parity_chunks(p).write(input, store);
     for (const auto& devs : std::vector<std::vector<int>>{{}, {0, 0}}) {
         for (size_t k = 0; k < f.parts.size(); ++k) {
-            store.erase(f.parts[k].data[0].hash);
-            store.erase(f.parts[k].parity[0].hash);
-            if (k % 3 == 1) CHECK(store.corrupt(f.parts[k].data[2].hash, 7));
+            store.erase(f.parts[k].data[0].locations[0]);
+            store.erase(f.parts[k].parity[0].locations[0]);
+            if (k % 3 == 1) CHECK(store.corrupt(f.parts[k].data[2].locations[0], 7));
         }
         auto before = f.verify(store, 4, 2, devs);
         CHECK(before.size() == f.parts.size());
@@ -343,7 +350,10 @@ void test_batched_verify_resilver() {
         }
         // the per-part verify reports the same
         const auto per_part = f.verify(store);
-        for (size_t k = 0; k < f.parts.size(); ++k) CHECK(per_part[k].chunks == before[k].chunks);
+        for (size_t k = 0; k < f.parts.size(); ++k) {
+            CHECK(per_part[k].chunks == before[k].chunks);
+            CHECK(per_part[k].locations == before[k].locations);
+        }
         const auto rep = f.resilver(store, 4, 2, devs);
         for (size_t k = 0; k < f.parts.size(); ++k) {
             CHECK(rep[k].chunks[0] == LocationIntegrity::Resilvered);
@@ -370,9 +380,9 @@ void test_batched_verify_resilver() {
     // a part with fewer than d usable chunks: its report carries the reconstruct error
     // (ResilverPartReport::write_error) and the other parts are still resilvered, batched and
     // per part alike
-    for (size_t i = 1; i < d + p; ++i) store.erase(f.parts[4].chunk(i).hash);
+    for (size_t i = 1; i < d + p; ++i) store.erase(f.parts[4].chunk(i).locations[0]);
     for (const size_t ppb : {size_t(4), size_t(0)}) {
-        store.erase(f.parts[7].data[1].hash);  // a repairable hole in another part
+        store.erase(f.parts[7].data[1].locations[0]);  // a repairable hole in another part
         const auto rep = f.resilver(store, ppb, 2);
         CHECK(rep.size() == f.parts.size());
         CHECK(rep[4].write_error && *rep[4].write_error == Error::TooFewShardsPresent);
@@ -380,6 +390,66 @@ void test_batched_verify_resilver() {
         CHECK(!rep[7].write_error && rep[7].chunks[1] == LocationIntegrity::Resilvered);
         for (size_t k = 0; k < f.parts.size(); ++k)
             if (k != 4) CHECK(!rep[k].write_error && rep[k].is_ideal());
+    }
+}
+
+// A store a resilver has touched lists chunks as [bad copy, good copy] (resilver appends the
+// rebuilt copy's location, file_part.rs:346).  p + 1 chunks of every part get a stale copy listed
+// first, so fewer than d first copies verify: the read succeeds only by walking each chunk's
+// locations before drawing another chunk (file_part.rs:100-107), per part and batched over one
+// and two shards; verify flags exactly the stale locations (file_part.rs:236-243); resilver
+// rebuilds nothing (every chunk has a valid copy) -- until a chunk's every copy is bad, when it
+// is rebuilt and its location appended.
+void test_locations_bad_then_good() {
+    for (const auto& shape : std::vector<std::array<size_t, 3>>{{3, 2, 4096}, {10, 4, 2048}}) {
+        const size_t d = shape[0], p = shape[1], chunk = shape[2], t = d + p;
+        const Bytes input = random_bytes(d * chunk * 13 + 211, d * 7 + 1);
+        ChunkStore store;
+        FileReference f =
+            FileWriteBuilder().chunk_size(chunk).data_chunks(d).parity_chunks(p).write(input, store);
+        size_t stale = 0;
+        for (size_t k = 0; k < f.parts.size(); ++k)
+            for (size_t m = 0; m <= p; ++m) {
+                Chunk& c = f.parts[k].chunk_mut((k + 2 * m) % t);
+                Bytes bad = *store.read(c.locations[0]);
+                bad[bad.size() / 2] ^= 0x10;
+                const Location loc = "stale/" + ChunkStore::location_of(c.hash);
+                store.put(loc, bad);
+                c.locations.insert(c.locations.begin(), loc);
+                ++stale;
+            }
+        CHECK(f.read(store) == input);
+        for (const auto& devs : std::vector<std::vector<int>>{{}, {0, 0}}) {
+            CHECK(f.read(store, 3, 2, devs) == input);
+            for (const auto& reps : {f.verify(store), f.verify(store, 3, 2, devs)}) {
+                size_t invalid = 0;
+                for (size_t k = 0; k < reps.size(); ++k) {
+                    CHECK(reps[k].is_ideal());  // every chunk has a valid copy
+                    for (size_t i = 0; i < t; ++i) {
+                        const auto& locs = reps[k].locations[i];
+                        const bool has_stale = f.parts[k].chunk(i).locations.size() == 2;
+                        CHECK(locs.size() == (has_stale ? 2u : 1u));
+                        CHECK(locs.back() == LocationIntegrity::Valid);
+                        if (has_stale) CHECK(locs[0] == LocationIntegrity::Invalid);
+                    }
+                    invalid += reps[k].invalid_locations();
+                }
+                CHECK(invalid == stale);
+            }
+        }
+        // resilver: nothing to rebuild (per part and batched)
+        for (const size_t ppb : {size_t(0), size_t(3)})
+            for (const auto& r : f.resilver(store, ppb, 2)) CHECK(r.new_locations.empty() && r.is_ideal());
+        // part 4: a chunk whose copies are both bad is rebuilt, its location appended
+        Chunk& victim = f.parts[4].chunk_mut(4 % t);
+        CHECK(victim.locations.size() == 2);
+        CHECK(store.corrupt(victim.locations[1], 3));
+        const auto rep = f.resilver(store, 3, 2);
+        CHECK(rep[4].new_locations.size() == 1 && victim.locations.size() == 3);
+        CHECK(rep[4].chunks[4 % t] == LocationIntegrity::Resilvered);
+        CHECK(victim.locations[2] == ChunkStore::location_of(victim.hash));
+        for (const auto& r : f.verify(store, 3, 2)) CHECK(r.is_ideal());
+        CHECK(f.read(store, 3, 2) == input);
     }
 }
 
@@ -462,7 +532,7 @@ void test_errors() {
     ChunkStore store;
     const FileReference f = FileWriteBuilder().chunk_size(1024).data_chunks(3).parity_chunks(2).write(
         Bytes(3000, 7), store);
-    for (size_t i = 0; i < 3; ++i) store.erase(f.parts[0].chunk(i).hash);
+    for (size_t i = 0; i < 3; ++i) store.erase(f.parts[0].chunk(i).locations[0]);
     CHECK(throws_erasure([&] { f.read(store); }, Error::TooFewShardsPresent));
 }
 
@@ -511,6 +581,7 @@ const Test kTests[] = {
     {"test_multi_device_paths", test_multi_device_paths},
     {"test_mixed_shape_read", test_mixed_shape_read},
     {"test_batched_verify_resilver", test_batched_verify_resilver},
+    {"test_locations_bad_then_good", test_locations_bad_then_good},
     {"test_one_encode", test_one_encode},
     {"test_matrix_rows", test_matrix_rows},
     {"test_errors", test_errors},

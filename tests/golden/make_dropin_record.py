@@ -39,9 +39,16 @@ def main():
     summary = json.load(open(os.path.join(src, "summary.json")))
     with tempfile.TemporaryDirectory() as tmp:
         for f in os.listdir(src):
-            shutil.copy(os.path.join(src, f), tmp)
+            if os.path.isfile(os.path.join(src, f)):
+                shutil.copy(os.path.join(src, f), tmp)
+        shutil.copytree(os.path.join(src, "stale"), os.path.join(tmp, "stale"))
         run = subprocess.run([sys.executable, REFERENCE_SCRIPT, "file.yaml"], cwd=tmp,
                              capture_output=True, check=False)
+        # stale.yaml lists p + 1 chunks per part as [stale copy, good copy]; the reference's python
+        # reader checks only each data chunk's first location, so it must name exactly the data
+        # chunks whose first copy is stale (the engine's reader walked on to the good copy)
+        stale_run = subprocess.run([sys.executable, REFERENCE_SCRIPT, "stale.yaml"], cwd=tmp,
+                                   capture_output=True, check=False)
         import yaml
         ref = yaml.safe_load(open(os.path.join(tmp, "file.yaml")))
         bad = os.path.join(tmp, ref["parts"][2]["data"][0]["locations"][0])
@@ -53,6 +60,7 @@ def main():
                                  capture_output=True, check=False)
         shutil.copy(os.path.join(src, "file.yaml"),
                     os.path.join(HERE, "dropin_file_reference.yaml"))
+        stale_ref = yaml.safe_load(open(os.path.join(tmp, "stale.yaml")))
     record = {
         "script": "python/chunky-bits.py (the reference's own reader, run in the build container "
                   "by tests/golden/make_dropin_record.py) on the store tools/dropin_cp_repair.py "
@@ -69,11 +77,22 @@ def main():
             control.stderr.decode(),
             "stdout_sha256_differs": hashlib.sha256(control.stdout).hexdigest() !=
             hashlib.sha256(run.stdout).hexdigest()},
+        "stale_file": {
+            "what": "stale.yaml: p + 1 chunks per part listed [stale copy, good copy]; the "
+                    "reader checks data chunks' first location only",
+            "returncode": stale_run.returncode,
+            "stderr_lines": stale_run.stderr.decode().strip().splitlines(),
+            "stale_data_chunks": [[k, i] for k, i in summary["stale"]["stale_chunks"] if i < 3],
+            "stale_data_hashes": [stale_ref["parts"][k]["data"][i]["sha256"]
+                                  for k, i in summary["stale"]["stale_chunks"] if i < 3]},
     }
     with open(os.path.join(HERE, "dropin_reference_run.json"), "w") as fh:
         json.dump(record, fh, indent=1)
         fh.write("\n")
     print(json.dumps(record, indent=1))
+    st = record["stale_file"]
+    assert sorted(line.split(" != ")[0] for line in st["stderr_lines"]) == \
+        sorted(st["stale_data_hashes"]), "reference reader and the stale copies disagree"
     assert run.returncode == 0 and not run.stderr and \
         record["stdout_sha256"] == summary["input_sha256"], "reference reader disagrees"
 

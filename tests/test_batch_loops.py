@@ -1,11 +1,13 @@
-"""The batched write / read loops (chunky_ec.batchwriter / batchreader: the executed twins of the
-Rust crate's batch::BatchWriter / BatchReader) on the CPU, with the scheduler and the page-locked
-buffers replaced by stand-ins that keep the C-ABI's contract (cec_multi_encode_hash / _read:
-asynchronous jobs, per-part status, CEC_PRESENT_VERIFIED chunks used but not hashed) and compute
-with the oracle and hashlib.  Checks the loop logic itself -- part cut (writer.rs:172-194), file
-order across windows, the short last part, read retries (file_part.rs:92-107), failures, and
-that no job is left in flight -- in the CPU suite; tests/test_gpu_batchwriter.py and
-tests/test_gpu_batchreader.py run the same loops on the real engine."""
+"""The batched write / read / verify / resilver loops (chunky_ec.batchwriter / batchreader /
+batchcheck: the executed twins of the Rust crate's batch::BatchWriter / BatchReader / FileReader /
+BatchChecker) on the CPU, with the scheduler and the page-locked buffers replaced by stand-ins that
+keep the C-ABI's contract (cec_multi_encode_hash / _read / _verify / _resilver: asynchronous jobs,
+per-part status, CEC_PRESENT_VERIFIED chunks used but not hashed) and compute with the oracle and
+hashlib.  Checks the loop logic itself -- part cut (writer.rs:172-194), file order across windows,
+the short last part, read retries that walk a chunk's locations before drawing another chunk
+(file_part.rs:92-107), every location hashed by verify / resilver (:236-243, :277-289), failures,
+and that no job is left in flight -- in the CPU suite; tests/test_gpu_batch*.py run the same loops
+on the real engine."""
 import hashlib
 import io
 import itertools
@@ -15,6 +17,8 @@ import pytest
 
 import oracle
 from chunky_ec import OK, PRESENT_VERIFIED, TOO_FEW_SHARDS_PRESENT, EncodedPart, Sha256Hash
+from _stores import Locations
+import chunky_ec.batchcheck as bc
 import chunky_ec.batchreader as br
 import chunky_ec.batchwriter as bw
 
@@ -90,6 +94,44 @@ class FakeMulti:
             st[k] = OK
         return self._job(), None
 
+    def _verify_flags(self, ch, pres, exp, ver, n):
+        for k in range(n):
+            for i in range(self.t):
+                if pres[k, i] == PRESENT_VERIFIED:
+                    ver[k, i] = 1
+                elif pres[k, i]:
+                    ver[k, i] = hashlib.sha256(ch[k, i].tobytes()).digest() == exp[k, i].tobytes()
+                else:
+                    ver[k, i] = 0
+
+    def verify(self, chunks, present, expected, n, verified):
+        t, L = self.t, self.L
+        self._verify_flags(_arr(chunks)[:n * t * L].reshape(n, t, L),
+                           np.asarray(present).reshape(-1, t), np.asarray(expected).reshape(-1, t, 32),
+                           np.asarray(verified).reshape(-1, t), n)
+        return self._job()
+
+    def resilver(self, chunks, present, expected, n, rebuilt, verified, status):
+        d, t, L = self.d, self.t, self.L
+        ch = _arr(chunks)[:n * t * L].reshape(n, t, L)
+        out = _arr(rebuilt)[:n * t * L].reshape(n, t, L)
+        ver = np.asarray(verified).reshape(-1, t)
+        st = np.asarray(status)
+        self._verify_flags(ch, np.asarray(present).reshape(-1, t),
+                           np.asarray(expected).reshape(-1, t, 32), ver, n)
+        for k in range(n):
+            if ver[k].sum() < d:
+                st[k] = TOO_FEW_SHARDS_PRESENT
+                continue
+            code, rec = oracle.reconstruct(d, self.p, [ch[k, i].copy() if ver[k, i] else None
+                                                       for i in range(t)], data_only=False)
+            assert code == 0
+            for i in range(t):
+                if not ver[k, i]:
+                    out[k, i] = rec[i]
+            st[k] = OK
+        return self._job(), None
+
     def wait(self, job):
         self.live.remove(job)
 
@@ -100,12 +142,51 @@ def _oracle_part_encode(codec, buf, length):
     return EncodedPart(cs, [x.tobytes() for x in par], [Sha256Hash(x.tobytes()) for x in dig])
 
 
+class _HashlibSha:
+    """Sha256Hash.from_bufs on the CPU (read_part's per-call hashing)."""
+
+    def __init__(self, digest):
+        self.digest = digest
+
+    @classmethod
+    def from_bufs(cls, bufs):
+        return [cls(hashlib.sha256(bytes(b)).digest()) for b in bufs]
+
+
+class _OracleCodec:
+    """ReedSolomon's per-call reconstruct_data (read_part) on the CPU."""
+
+    def __init__(self, d, p):
+        self.d, self.p = d, p
+
+    def data_shard_count(self):
+        return self.d
+
+    def total_shard_count(self):
+        return self.d + self.p
+
+    def parity_shard_count(self):
+        return self.p
+
+    def reconstruct_data(self, shards):
+        code, rec = oracle.reconstruct(self.d, self.p, [None if s is None else
+                                                        np.frombuffer(bytes(s), np.uint8)
+                                                        for s in shards], data_only=True)
+        assert code == 0
+        for i in range(self.d):
+            if shards[i] is None:
+                shards[i] = bytearray(rec[i].tobytes())
+
+
 @pytest.fixture
 def fakes(monkeypatch):
-    for mod in (bw, br):
+    for mod in (bw, br, bc):
         monkeypatch.setattr(mod, "Multi", FakeMulti)
         monkeypatch.setattr(mod, "HostBuffer", FakeHostBuffer)
     monkeypatch.setattr(bw, "part_encode", _oracle_part_encode)
+    monkeypatch.setattr(br, "Sha256Hash", _HashlibSha)
+    for mod in (bw, br, bc):
+        monkeypatch.setattr(mod, "ReedSolomon", _OracleCodec)
 
 
 def _expected_part(file_bytes, k):
@@ -163,7 +244,7 @@ def test_batch_writer_sink_error_drains(fakes):
     assert w.multi.live == set()  # the window in flight was waited for
 
 
-def _store(n, seed):
+def _store(n, seed, L=L):
     rng = np.random.default_rng(seed)
     chunks = np.zeros((n, T, L), np.uint8)
     dig = np.zeros((n, T, 32), np.uint8)
@@ -176,42 +257,167 @@ def _store(n, seed):
     return chunks, dig
 
 
-def _fetcher(chunks, missing=(), damaged=()):
-    calls = []
-
-    def fetch(part, i):
-        calls.append((part, i))
-        if (part, i) in missing:
-            return None
-        b = chunks[part, i].copy()
-        if (part, i) in damaged:
-            b[3] ^= 1
-        return b.tobytes()
-    return fetch, calls
-
-
 def test_batch_reader_loop(fakes):
     n = 17
     chunks, dig = _store(n, 3)
+    st = Locations(chunks)
     # part 6: chunk 0 missing; part 9: chunk 1 damaged; part 12: chunks 0 and 2 damaged (two
     # replacements, taken from the parity chunks); part 16 (the last, in a short window): chunk 2
-    fetch, calls = _fetcher(chunks, missing={(6, 0)}, damaged={(9, 1), (12, 0), (12, 2), (16, 2)})
+    st.set(6, 0, "gone")
+    for k, i in ((9, 1), (12, 0), (12, 2), (16, 2)):
+        st.set(k, i, "bad")
     r = br.BatchReader(D, P, L, 2, 2, [0, 0])
     got = []
-    r.read(n, fetch, lambda k: dig[k], lambda k, data: got.append((k, b"".join(map(bytes, data)))))
+    r.read(n, st.fetch, lambda k: dig[k], lambda k, data: got.append((k, b"".join(map(bytes, data)))))
     assert [k for k, _ in got] == list(range(n))
     assert all(b == chunks[k, :D].tobytes() for k, b in got)
     assert r.retries == 3 and r.multi.live == set()
-    assert [c for c in calls if c[0] == 12] == [(12, i) for i in range(T)]
-    assert [c for c in calls if c[0] == 6] == [(6, 0), (6, 1), (6, 2), (6, 3)]
+    # part 12: its damaged chunks have no further location (fetch from 1 finds none), then the
+    # two parity chunks are drawn
+    assert [c for c in st.calls if c[0] == 12] == [(12, i, 0) for i in range(D)] + \
+        [(12, 0, 1), (12, 2, 1), (12, 3, 0), (12, 4, 0)]
+    # part 6: chunk 0 has no readable location: never asked again
+    assert [c for c in st.calls if c[0] == 6] == [(6, 0, 0), (6, 1, 0), (6, 2, 0), (6, 3, 0)]
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0]])
+def test_batch_reader_walks_a_chunks_locations_first(fakes, devices):
+    """p + 1 chunks per part listed [bad, good] (what resilver leaves when it appends a rebuilt
+    copy, file_part.rs:346): too few first copies verify, but each chunk's second location does.
+    The reference reads it (file_part.rs:100-107); so must the batched loop, re-fetching the same
+    chunk's next location before it draws another chunk."""
+    n = 9
+    chunks, dig = _store(n, 8)
+    st = Locations(chunks)
+    for k in range(n):
+        for i in range(P + 1):
+            st.set(k, (k + i) % T, "bad", "good")
+    st.set(4, 3, "gone", "short", "bad", "good")  # unreadable, wrong size, bad, then good
+    r = br.BatchReader(D, P, L, 2, 2, devices)
+    got = []
+    r.read(n, st.fetch, lambda k: dig[k], lambda k, data: got.append((k, b"".join(map(bytes, data)))))
+    assert [k for k, _ in got] == list(range(n))
+    assert all(b == chunks[k, :D].tobytes() for k, b in got)
+    # part 0 (chunks 0, 1, 2 listed [bad, good]): one retry, on the same three chunks' location 1
+    assert [c for c in st.calls if c[0] == 0] == [(0, 0, 0), (0, 1, 0), (0, 2, 0),
+                                                  (0, 0, 1), (0, 1, 1), (0, 2, 1)]
+    assert r.multi.live == set()
 
 
 def test_batch_reader_out_of_chunks(fakes):
     chunks, dig = _store(9, 4)
-    fetch, _ = _fetcher(chunks, damaged={(5, 0), (5, 3), (5, 4)})  # 2 good < d = 3
+    st = Locations(chunks)
+    for i in (0, 3):
+        st.set(5, i, "bad")
+    st.set(5, 4, "bad", "gone", "bad")  # 2 good chunks < d = 3, whatever the locations hold
     r = br.BatchReader(D, P, L, 2, 2, [0])
     got = []
     with pytest.raises(Exception) as e:
-        r.read(9, fetch, lambda k: dig[k], lambda k, data: got.append(k))
+        r.read(9, st.fetch, lambda k: dig[k], lambda k, data: got.append(k))
     assert getattr(e.value, "code", None) == TOO_FEW_SHARDS_PRESENT
     assert got == [0, 1, 2, 3] and r.multi.live == set()
+
+
+def _file(nbytes, seed, d=D, p=P, chunk=L):
+    """A file cut as writer.rs:172-194 / file_part.rs:150-158 does: (shapes, chunks per part,
+    digests per part, the file bytes)."""
+    fb = np.random.default_rng(seed).integers(0, 256, nbytes, dtype=np.uint8).tobytes()
+    cap = d * chunk
+    shapes, parts, digs = [], [], []
+    for off in range(0, nbytes, cap):
+        piece = fb[off:off + cap]
+        Lk = -(-len(piece) // d)
+        buf = np.zeros(d * Lk, np.uint8)
+        buf[:len(piece)] = np.frombuffer(piece, np.uint8)
+        data = [buf[j * Lk:(j + 1) * Lk] for j in range(d)]
+        st, par = oracle.encode_sep(d, p, data)
+        cs = [c.tobytes() for c in data] + [c.tobytes() for c in par]
+        shapes.append((d, p, Lk))
+        parts.append(cs)
+        digs.append(np.array([np.frombuffer(hashlib.sha256(c).digest(), np.uint8) for c in cs]))
+    return shapes, parts, digs, fb
+
+
+@pytest.mark.parametrize("extra", [0, 1, 700])
+def test_file_reader_short_last_part(fakes, extra):
+    """The short last part has chunk size ceil(len / d) (file_part.rs:152): FileReader reads it
+    through read_part instead of the full-size BatchReader (which would drop its chunks as the
+    wrong size and fail the read), with its own damaged chunk walked to its second location."""
+    shapes, parts, digs, fb = _file(7 * D * L + extra, 11)
+    copies = {(k, i): [c] for k, cs in enumerate(parts) for i, c in enumerate(cs)}
+    last = len(parts) - 1
+    if extra:
+        good = parts[last][1]
+        copies[(last, 1)] = [bytes([good[0] ^ 1]) + good[1:], good]  # [bad, good]
+        copies[(last, 0)] = [None]
+    calls = []
+
+    def fetch(k, i, start):
+        calls.append((k, i, start))
+        locs = copies[(k, i)]
+        for j in range(start, len(locs)):
+            if locs[j] is not None:
+                return j, locs[j]
+        return None
+    reader = br.FileReader(2, 2, [0])
+    out = bytearray()
+    seen = []
+    reader.read(shapes, fetch, lambda k: digs[k],
+                lambda k, data: (seen.append(k), out.extend(b"".join(map(bytes, data)))))
+    assert seen == list(range(len(parts)))
+    assert bytes(out[:len(fb)]) == fb  # FileReference::length truncates the padding
+    assert list(reader.readers) == [(D, P, L)]
+    # a second file of the same shape reuses the kept reader (its pinned windows)
+    keep = reader.readers[(D, P, L)]
+    reader.read(shapes, fetch, lambda k: digs[k], lambda k, data: None)
+    assert reader.readers[(D, P, L)] is keep
+
+
+def test_checker_verify_hashes_every_location(fakes):
+    n = 7
+    chunks, dig = _store(n, 12)
+    st = Locations(chunks)
+    st.set(1, 0, "bad", "good")
+    st.set(2, 4, "gone", "good", "bad")
+    st.set(3, 2, "short")
+    st.set(5, 1, "gone")
+    st.set(6, 3)  # no locations at all
+    c = bc.BatchChecker(D, P, L, 2, 2, [0])
+    got = {}
+    c.verify(n, st.read_all, lambda k: dig[k], lambda k, part: got.__setitem__(k, part))
+    assert sorted(got) == list(range(n)) and c.multi.live == set()
+    assert got[0].locations == [[True]] * T
+    assert got[1].locations[0] == [False, True] and got[1].healthy_chunks() == T
+    assert got[2].locations[4] == [None, True, False]
+    assert got[3].locations[2] == [False] and got[3].healthy_chunks() == T - 1
+    assert got[5].locations[1] == [None] and got[5].unavailable_locations() == 1
+    assert got[6].locations[3] == [] and got[6].healthy_chunks() == T - 1
+    assert sum(p.invalid_locations() for p in got.values()) == 3
+
+
+def test_checker_resilver_rebuilds_only_chunks_without_a_valid_copy(fakes):
+    n = 9
+    chunks, dig = _store(n, 13)
+    st = Locations(chunks)
+    st.set(0, 0, "gone")                  # one location, unreadable: rebuilt
+    st.set(0, D, "bad")                   # one location, bad: rebuilt
+    st.set(2, 1, "bad", "good")           # a valid second copy: healthy, not rebuilt
+    st.set(2, 4, "bad", "gone")           # no valid copy among two: rebuilt
+    st.set(4, 2, "short", "bad", "good")
+    for i in range(P + 1):                # too few chunks: write_error, the others go on
+        st.set(7, i, "bad")
+    c = bc.BatchChecker(D, P, L, 2, 2, [0])
+    got = {}
+    c.resilver(n, st.read_all, lambda k: dig[k],
+               lambda k, part: got.__setitem__(k, (part, {i: bytes(b) for i, b in
+                                                          part.rebuilt.items()})))
+    assert sorted(got) == list(range(n)) and c.multi.live == set()
+    assert sorted(got[0][1]) == [0, D] and got[0][0].locations[D] == [False]
+    assert sorted(got[2][1]) == [4] and got[2][0].locations[1] == [False, True]
+    assert got[4][1] == {} and got[4][0].locations[2] == [False, False, True]
+    for k, (part, rebuilt) in got.items():
+        for i, b in rebuilt.items():
+            assert b == chunks[k, i].tobytes(), (k, i)
+    assert got[7][0].error == TOO_FEW_SHARDS_PRESENT and got[7][1] == {}
+    assert all(got[k][0].error is None for k in got if k != 7)
+    assert c.extra_passes == 2  # windows holding parts 2 and 4 (multi-location chunks)

@@ -142,11 +142,37 @@ def test_reference_reader_reads_the_engines_repaired_store():
     data = gen_bytes(gpu["seed"], gpu["length"])
     assert run["stdout_len"] == gpu["length"]
     assert run["stdout_sha256"] == gpu["input_sha256"] == hashlib.sha256(data.tobytes()).hexdigest()
-    assert gpu["cat_equals_input"] is True and gpu["read_retries"] >= 1
+    assert gpu["cat_equals_input"] is True and gpu["cat_after_repair_equals_input"] is True
     assert sorted(map(tuple, gpu["repaired"])) == sorted(map(tuple, gpu["deleted"] +
                                                              [gpu["corrupted"]]))
+    # the engine's verify before the repair: exactly the deleted locations unavailable and the
+    # damaged one invalid; after it, every location of every chunk valid
+    assert sorted(tuple(x[:2]) for x in gpu["verify_before"]["unavailable"]) == \
+        sorted(map(tuple, gpu["deleted"]))
+    assert [x[:2] for x in gpu["verify_before"]["invalid"]] == [gpu["corrupted"]]
+    assert gpu["verify_after"] == {"unavailable": [], "invalid": [], "unhealthy_chunks": 0}
     c = run["corrupted_control"]
     assert c["stderr_lines"] == 1 and c["stderr_names_the_chunk"] and c["stdout_sha256_differs"]
+
+
+def test_engine_reads_chunks_listed_bad_then_good():
+    """stale.yaml: p + 1 chunks of every part listed [stale copy, good copy], so fewer than d first
+    copies verify.  The engine's batched reader walked each chunk's locations like
+    read_with_context (file_part.rs:100-107) and read the file back; its verify flagged exactly the
+    stale copies and resilver rebuilt nothing (each chunk has a valid copy).  The reference's
+    python reader, which checks each data chunk's FIRST location only, confirms those first copies
+    are the bad ones: its mismatch lines name exactly the stale data chunks."""
+    run = json.load(open(DROPIN_RUN))
+    s = run["gpu_side"]["stale"]
+    assert s["cat_equals_input"] is True and s["repaired"] == [] and s["resilver_errors"] == []
+    assert sorted(x[:2] for x in s["verify"]["invalid"]) == sorted(s["stale_chunks"])
+    assert all(x[2] == 0 for x in s["verify"]["invalid"]) and s["verify"]["unhealthy_chunks"] == 0
+    d, p = run["gpu_side"]["d"], run["gpu_side"]["p"]
+    assert len(s["stale_chunks"]) == s["parts"] * (p + 1)
+    ref = run["stale_file"]
+    assert sorted(x.split(" != ")[0] for x in ref["stderr_lines"]) == \
+        sorted(ref["stale_data_hashes"])
+    assert len(ref["stale_data_hashes"]) == sum(1 for k, i in s["stale_chunks"] if i < d)
 
 
 def test_engines_store_equals_the_oracle_file_reference():
@@ -165,5 +191,8 @@ def test_engines_store_equals_the_oracle_file_reference():
         hexes = [hashlib.sha256(c.tobytes()).hexdigest() for c in chunks]
         assert [c["sha256"] for c in part["data"]] == hexes[:d], k
         assert [c["sha256"] for c in part["parity"]] == hexes[d:], k
-        assert all(c["locations"] == [f"sha256-{c['sha256']}"]
-                   for c in part["data"] + part["parity"])
+        # one location per chunk; a repaired chunk lists its rewritten file a second time
+        # (resilver appends the new location, file_part.rs:346)
+        for i, c in enumerate(part["data"] + part["parity"]):
+            n = 2 if [k, i] in gpu["repaired"] else 1
+            assert c["locations"] == [f"sha256-{c['sha256']}"] * n, (k, i)

@@ -1,10 +1,10 @@
-"""chunky_ec.batchreader.BatchReader (the executed twin of the Rust crate's batch::BatchReader and
-the C++ FileReference::read_run / retry) on the GPU: parts come out in file order with their
-stored data chunks, with chunks missing from storage, chunks served damaged (rejected by the
-SHA-256 verification and replaced, file_part.rs:92-107), over one and two scheduler shards; a part
-that runs out of good chunks fails the read with TooFewShardsPresent."""
-import hashlib
-
+"""chunky_ec.batchreader (the executed twin of the Rust crate's batch::BatchReader / read_part /
+FileReader and of the C++ FileReference::read_run / retry) on the GPU: parts come out in file
+order with their stored data chunks, with chunks missing from storage, chunks served damaged
+(rejected by the SHA-256 verification and replaced, file_part.rs:92-107), chunks listed with a bad
+copy before a good one (the next location of the same chunk is read before another chunk is
+drawn, file_part.rs:100-107), a short last part, over one and two scheduler shards; a part that
+runs out of good copies fails the read with TooFewShardsPresent."""
 import numpy as np
 import pytest
 
@@ -16,74 +16,120 @@ if not torch.cuda.is_available():  # pragma: no cover
 
 import chunky_ec as ce  # noqa: E402
 import oracle  # noqa: E402
-from chunky_ec.batchreader import BatchReader  # noqa: E402
+from _stores import Locations, make_parts  # noqa: E402
+from chunky_ec.batchreader import BatchReader, FileReader  # noqa: E402
 
 D, P, L = 4, 2, 4096
 T = D + P
 
 
-def _store(n, seed):
-    rng = np.random.default_rng(seed)
-    chunks = np.zeros((n, T, L), np.uint8)
-    dig = np.zeros((n, T, 32), np.uint8)
-    for k in range(n):
-        data = rng.integers(0, 256, size=(D, L), dtype=np.uint8)
-        st, par = oracle.encode_sep(D, P, list(data))
-        assert st == 0
-        chunks[k, :D], chunks[k, D:] = data, np.stack(par)
-        for i in range(T):
-            dig[k, i] = np.frombuffer(hashlib.sha256(chunks[k, i].tobytes()).digest(), np.uint8)
-    return chunks, dig
-
-
-def _fetcher(chunks, missing=(), damaged=()):
-    calls = []
-
-    def fetch(part, i):
-        calls.append((part, i))
-        if (part, i) in missing:
-            return None
-        b = chunks[part, i].copy()
-        if (part, i) in damaged:
-            b[17] ^= 0x40
-        return b.tobytes()
-    return fetch, calls
-
-
 @pytest.mark.parametrize("devices", [[0], [0, 0]])
 def test_batch_reader_in_order_with_missing_and_damaged_chunks(devices):
     n = 23
-    chunks, dig = _store(n, 5)
-    missing = {(3, 0), (4, 0), (4, 1), (11, 2)}
-    damaged = {(5, 1), (8, 0), (8, 3), (16, 2), (22, 0)}
-    fetch, calls = _fetcher(chunks, missing, damaged)
+    chunks, dig = make_parts(n, D, P, L, 5)
+    st = Locations(chunks)
+    for k, i in ((3, 0), (4, 0), (4, 1), (11, 2)):
+        st.set(k, i, "gone")
+    for k, i in ((5, 1), (8, 0), (8, 3), (16, 2), (22, 0)):
+        st.set(k, i, "bad")
     r = BatchReader(D, P, L, 3, 2, devices)
     got = []
-    r.read(n, fetch, lambda k: dig[k], lambda k, data: got.append((k, b"".join(bytes(x)
-                                                                                  for x in data))))
+    r.read(n, st.fetch, lambda k: dig[k],
+           lambda k, data: got.append((k, b"".join(bytes(x) for x in data))))
     assert [k for k, _ in got] == list(range(n))
     for k, b in got:
         assert b == chunks[k, :D].tobytes(), k
     # every part with a damaged chunk was resubmitted once; an intact part loaded exactly its d
-    # data chunks; part 8 (chunks 0 and 3 damaged) took the two parity chunks on its retry
+    # data chunks; part 8 (chunks 0 and 3 damaged, no second copy) took the two parity chunks on
+    # its retry
     assert r.retries == 4
-    assert [c for c in calls if c[0] == 0] == [(0, i) for i in range(D)]
-    assert [c for c in calls if c[0] == 8] == [(8, i) for i in range(T)]
+    assert [c for c in st.calls if c[0] == 0] == [(0, i, 0) for i in range(D)]
+    assert [c for c in st.calls if c[0] == 8] == [(8, i, 0) for i in range(D)] + \
+        [(8, 0, 1), (8, 3, 1), (8, 4, 0), (8, 5, 0)]
+
+
+@pytest.mark.parametrize("d,p,L", [(3, 2, 65536), (10, 4, 16384)])
+@pytest.mark.parametrize("devices", [[0], [0, 0]])
+def test_batch_reader_reads_chunks_listed_bad_then_good(d, p, L, devices):
+    """RS(3,2) and RS(10,4) stores where p + 1 chunks of every part are listed [bad, good] -- a
+    store a resilver has touched (file_part.rs:346 appends the rebuilt copy's location): fewer
+    than d first copies verify, so only a reader that walks each chunk's locations decodes it.
+    Every part must come back bit-exact with the oracle's data."""
+    n = 11
+    chunks, dig = make_parts(n, d, p, L, 40 + d)
+    st = Locations(chunks)
+    t = d + p
+    for k in range(n):
+        for i in range(p + 1):
+            st.set(k, (k + 3 * i) % t, "bad", "good")
+    st.set(2, 0, "gone", "short", "bad", "good")
+    r = BatchReader(d, p, L, 4, 2, devices)
+    got = []
+    r.read(n, st.fetch, lambda k: dig[k],
+           lambda k, data: got.append((k, b"".join(bytes(x) for x in data))))
+    assert [k for k, _ in got] == list(range(n))
+    for k, b in got:
+        assert b == chunks[k, :d].tobytes(), k
+    for k in range(n):
+        # the bad copies were followed by their chunk's next location
+        bad = {(k + 3 * i) % t for i in range(p + 1)}
+        loaded = [i for (kk, i, s) in st.calls if kk == k and s == 0]
+        for i in bad & set(loaded):
+            assert (k, i, 1) in st.calls or (k == 2 and i == 0), (k, i)
 
 
 def test_batch_reader_part_out_of_chunks_fails_the_read():
     n = 7
-    chunks, dig = _store(n, 6)
-    damaged = {(4, 0), (4, 2), (4, 5)}  # 3 of 6 bad: 3 good < d = 4
-    fetch, _ = _fetcher(chunks, damaged=damaged)
+    chunks, dig = make_parts(n, D, P, L, 6)
+    st = Locations(chunks)
+    st.set(4, 0, "bad", "bad")
+    st.set(4, 2, "gone", "bad")
+    st.set(4, 5, "bad")  # 3 of 6 chunks without a good copy: 3 good < d = 4
     r = BatchReader(D, P, L, 2, 2, [0])
     got = []
     with pytest.raises(ce.Error) as e:
-        r.read(n, fetch, lambda k: dig[k], lambda k, data: got.append(k))
+        r.read(n, st.fetch, lambda k: dig[k], lambda k, data: got.append(k))
     assert e.value.code == ce.TOO_FEW_SHARDS_PRESENT
     assert got == [0, 1, 2, 3]  # the windows before the failing one were handed out, in order
     # the reader is reusable after the failure (no job left in flight on its windows)
-    fetch, _ = _fetcher(chunks)
+    st = Locations(chunks)
     got = []
-    r.read(n, fetch, lambda k: dig[k], lambda k, data: got.append(k))
+    r.read(n, st.fetch, lambda k: dig[k], lambda k, data: got.append(k))
     assert got == list(range(n))
+
+
+def test_file_reader_with_short_last_part():
+    """A file whose last part is short (chunk size ceil(len / d), file_part.rs:152): FileReader
+    reads the full parts through a BatchReader and the last one through read_part (per-call
+    engine calls), its first data chunk listed [bad, good]."""
+    import hashlib
+    d, p, chunk = 3, 2, 8192
+    rng = np.random.default_rng(21)
+    fb = rng.integers(0, 256, 9 * d * chunk + 1001, dtype=np.uint8).tobytes()
+    shapes, copies, digs = [], {}, []
+    for k, off in enumerate(range(0, len(fb), d * chunk)):
+        piece = fb[off:off + d * chunk]
+        Lk = -(-len(piece) // d)
+        buf = np.zeros(d * Lk, np.uint8)
+        buf[:len(piece)] = np.frombuffer(piece, np.uint8)
+        data = [buf[j * Lk:(j + 1) * Lk] for j in range(d)]
+        st, par = oracle.encode_sep(d, p, data)
+        cs = [c.tobytes() for c in data] + [c.tobytes() for c in par]
+        for i, c in enumerate(cs):
+            copies[(k, i)] = [c]
+        shapes.append((d, p, Lk))
+        digs.append(np.array([np.frombuffer(hashlib.sha256(c).digest(), np.uint8) for c in cs]))
+    last = len(shapes) - 1
+    good = copies[(last, 0)][0]
+    copies[(last, 0)] = [bytes([good[0] ^ 0x10]) + good[1:], good]
+
+    def fetch(k, i, start):
+        locs = copies[(k, i)]
+        for j in range(start, len(locs)):
+            if locs[j] is not None:
+                return j, locs[j]
+        return None
+    out = bytearray()
+    FileReader(4, 2, [0]).read(shapes, fetch, lambda k: digs[k],
+                               lambda k, data: out.extend(b"".join(bytes(x) for x in data)))
+    assert bytes(out[:len(fb)]) == fb

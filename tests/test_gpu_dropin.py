@@ -30,7 +30,11 @@ def test_dropin_cp_cat_repair(tmp_path):
                           str(tmp_path)], capture_output=True, text=True, timeout=240)
     assert out.returncode == 0, out.stderr[-2000:]
     s = json.load(open(tmp_path / "summary.json"))
-    assert s["cat_equals_input"] is True and s["read_retries"] >= 1
+    assert s["cat_equals_input"] is True and s["cat_after_repair_equals_input"] is True
+    # the stale file: p + 1 chunks per part listed [bad, good], read / verified / not rebuilt
+    assert s["stale"]["cat_equals_input"] is True and s["stale"]["repaired"] == []
+    assert sorted(x[:2] for x in s["stale"]["verify"]["invalid"]) == \
+        sorted(s["stale"]["stale_chunks"])
     ref = yaml.safe_load(open(tmp_path / "file.yaml"))
     data = gen_bytes(s["seed"], s["length"])
     assert s["input_sha256"] == hashlib.sha256(data.tobytes()).hexdigest()
@@ -40,5 +44,9 @@ def test_dropin_cp_cat_repair(tmp_path):
         for c, entry in zip(chunks, part["data"] + part["parity"]):
             h = hashlib.sha256(c.tobytes()).hexdigest()
             assert entry["sha256"] == h, (k, entry)
-            # every chunk file exists after the repair and holds exactly that chunk
+            # every chunk file exists after the repair and holds exactly that chunk; a repaired
+            # chunk lists its rewritten location a second time (appended, file_part.rs:346)
             assert open(tmp_path / f"sha256-{h}", "rb").read() == c.tobytes(), (k, h)
+            assert set(entry["locations"]) == {f"sha256-{h}"}
+            assert len(entry["locations"]) == (2 if [k, (part["data"] + part["parity"]).index(
+                entry)] in s["repaired"] else 1)

@@ -55,15 +55,15 @@ int main(int argc, char** argv) {
         // write into RAM, lose one data + one parity chunk per part, read back
         ChunkStore store;
         t0 = std::chrono::steady_clock::now();
-        const FileReference f = write(store);
+        FileReference f = write(store);
         const double w_ram = secs(t0);
         if (batched) {  // pins the verify / resilver windows (nothing to rebuild yet)
             (void)f.resilver(store, 128, 4, devices);
             (void)f.verify(store, 128, 4, devices);
         }
         for (const auto& part : f.parts) {
-            store.erase(part.data[3].hash);
-            store.erase(part.parity[1].hash);
+            store.erase(part.data[3].locations[0]);
+            store.erase(part.parity[1].locations[0]);
         }
         if (batched) (void)f.read(store, 128, 4, devices);  // pins the read windows
         t0 = std::chrono::steady_clock::now();
