@@ -47,8 +47,9 @@ import torch.distributed as dist  # noqa: E402
 
 import chunky_ec as ce  # noqa: E402
 from chunky_ec.readstream import ReadRepairStream  # noqa: E402
-from chunky_ec.sharding import (all_ranks_ok, barrier, dist_env, gather_rows,  # noqa: E402
-                                max_over_ranks, part_range, rank_seed)
+from chunky_ec.sharding import (all_ranks_ok, barrier, cpu_quota, dist_env,  # noqa: E402
+                                gather_rows, max_over_ranks, multi_copy_threads, part_range,
+                                quota_share, rank_seed, rank_threads)
 
 METRIC = "RS(10,4) encode+sha256 GB/s per node at 1/2/4/8 GPUs; % of HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md).  The encode kernel streams
@@ -177,19 +178,6 @@ def measured_traffic(config: str, kernel: str, full_size: bool, with_source: boo
         return total
     return total, "committed PMC run (not this run): " + ", ".join(
         sorted({e.get("source", "profiles/traffic.json") for e in entries}))
-
-
-def cpu_quota():
-    """CPUs this process may use: (affinity count, cgroup v2 cpu.max quota in CPUs or None)."""
-    aff = len(os.sched_getaffinity(0))
-    quota = None
-    try:
-        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
-        if q != "max":
-            quota = round(int(q) / int(period), 2)
-    except (OSError, ValueError):
-        pass
-    return aff, quota
 
 
 def host_info():
@@ -508,12 +496,6 @@ def _stream_line(args, cfg, world, n_batches, warm, el, total, extra_config, dat
     return line
 
 
-def _rank_threads(world):
-    """Host threads for a rank's reader: half the CPUs its main thread may use, 8 at most."""
-    return int(os.environ.get("CEC_E2E_THREADS", "0")) or max(
-        1, min(8, len(os.sched_getaffinity(0)) // 2))
-
-
 def run_stream(args, cfg, codec, world, rank, device, reduce_dev):
     """C5 (BASELINE configs[4], write side): a `--stream-gib` object stream, split into
     contiguous part ranges over the ranks (strong scaling), each rank's parts produced inside
@@ -526,7 +508,7 @@ def run_stream(args, cfg, codec, world, rank, device, reduce_dev):
     lo, hi = part_range(total_parts, rank, world)
     if args.devices:
         return run_stream_multi(args, cfg, codec, total_parts)
-    threads = _rank_threads(world)
+    threads = rank_threads(world)
     copier = HostCopier(threads)
     ring_parts = 2 * depth * P if world == 1 else 2 * P
     ring = source_ring(ring_parts, d, L, 0xC5 + rank, copier)
@@ -577,7 +559,7 @@ def run_read_stream(args, cfg, codec, world, rank, device, reduce_dev):
     depth = int(os.environ.get("CEC_STREAM_DEPTH", "4"))  # slots in flight (A/B knob)
     total_parts = int(args.stream_gib * (1 << 30)) // (d * L)
     lo, hi = part_range(total_parts, rank, world)
-    threads = _rank_threads(world)
+    threads = rank_threads(world)
     copier = HostCopier(threads)
     ring, ring_dig = encoded_ring(codec, d, p, L, 2 * P, rank_seed(0xC5C5, rank), device, P)
     loc, stats, checks = timed_read_repair(codec, ring, ring_dig, L, P, depth, lo, hi - lo,
@@ -1086,7 +1068,7 @@ def run_stream_multi(args, cfg, codec, total_parts):
     m = ce.Multi(codec, L, P, depth, devices)
     S = _segments(args, cfg, len(devices))
     J = args.jobs_in_flight
-    copier = HostCopier(_rank_threads(1))
+    copier = HostCopier(rank_threads(1))
     ring = source_ring(S, d, L, 0xC5, copier)
     copier.close()
     outs = [(ce.HostBuffer(S * p * L, devices[0]), ce.HostBuffer(S * t * 32, devices[0]))
@@ -1128,7 +1110,8 @@ def run_stream_multi(args, cfg, codec, total_parts):
 RANK_FIELDS = ("device", "numa_node", "host_threads_numa_bound", "cpus", "step_ms",
                "end_to_end_GBs", "pcie_link_GBs", "north_star_encode_frac",
                "north_star_reconstruct_data_frac", "c3_reconstruct_frac", "c3_algorithmic_bytes",
-               "c3_ms", "c4_ms", "c4_data_bytes", "read_repair_GBs")
+               "c3_ms", "c4_ms", "c4_data_bytes", "read_repair_GBs", "quota_share_cpus",
+               "host_threads", "multi_copy_threads")
 
 
 def rank_row(r: int, row) -> dict:
@@ -1136,7 +1119,8 @@ def rank_row(r: int, row) -> dict:
     a figure the rank did not produce (0) is None."""
     out = {"rank": r}
     for name, v in zip(RANK_FIELDS, row):
-        if name in ("device", "numa_node", "cpus", "c3_algorithmic_bytes", "c4_data_bytes"):
+        if name in ("device", "numa_node", "cpus", "c3_algorithmic_bytes", "c4_data_bytes",
+                    "host_threads", "multi_copy_threads"):
             out[name] = int(v)
         elif name == "host_threads_numa_bound":
             out[name] = bool(v)
@@ -1241,8 +1225,15 @@ def main():
     rank_cpus = len(os.sched_getaffinity(0))
     host_report["rank_cpus_after_numa_bind"] = rank_cpus
     # host threads of this rank's end-to-end reader: half its CPUs (the rest run the engine's
-    # own threads), 8 at most
-    e2e_threads = _rank_threads(world)
+    # own threads), 8 at most, within its share of the job's cgroup CPU quota (all ranks of the
+    # node share one quota); the scheduler's staging threads per shard likewise
+    e2e_threads = rank_threads(world)
+    if "CEC_MULTI_COPY_THREADS" not in os.environ:
+        os.environ["CEC_MULTI_COPY_THREADS"] = str(multi_copy_threads(world))
+        ce.reload_knobs()
+    host_report["quota_share_cpus"] = quota_share(world)
+    host_report["rank_host_threads"] = e2e_threads
+    host_report["multi_copy_threads"] = int(os.environ["CEC_MULTI_COPY_THREADS"])
     # RCCL ("nccl") carries only the barrier and the max-over-ranks all-reduce.
     # CEC_BENCH_BACKEND=gloo rehearses N > 1 with several ranks on one GPU; CEC_BENCH_PG=1 starts
     # the process group at world 1 too, so one GPU runs the N > 1 line's RCCL branch (init with
@@ -1530,7 +1521,8 @@ def main():
         c4 = (others or {}).get("c4_encode_hash", {})
         row = [ordinal, numa_node, 1.0 if numa_bound else 0.0, rank_cpus, local_s * 1e3, e2e_v,
                link_v, ns_enc, ns_rec, c3.get("frac") or 0.0, c3.get("algorithmic_bytes") or 0,
-               c3.get("ms") or 0.0, c4.get("ms") or 0.0, c4.get("data_bytes") or 0, rr_v]
+               c3.get("ms") or 0.0, c4.get("ms") or 0.0, c4.get("data_bytes") or 0, rr_v,
+               quota_share(world) or 0.0, e2e_threads, int(os.environ["CEC_MULTI_COPY_THREADS"])]
         rows = gather_rows(row, world, reduce_dev)
         ranks = [rank_row(r, row) for r, row in enumerate(rows)]
         node = node_figures(ranks)

@@ -68,3 +68,51 @@ def barrier(world: int) -> None:
 def rank_seed(base: int, rank: int) -> int:
     """Synthetic-data seed of a rank's parts (weak scaling: every rank owns distinct parts)."""
     return base + rank
+
+
+def cpu_quota():
+    """CPUs this process may use: (affinity count, cgroup v2 cpu.max quota in CPUs or None)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = round(int(q) / int(period), 2)
+    except (OSError, ValueError):
+        pass
+    return aff, quota
+
+
+def quota_share(world: int):
+    """One rank's share of the cgroup CPU quota, or None without a quota.  The quota covers the
+    whole job -- every rank of the node runs in the same cgroup -- so N ranks split it N ways,
+    whatever each rank's affinity (a NUMA node's 128 CPUs on the 2-socket hosts) says."""
+    _, quota = cpu_quota()
+    return None if quota is None else quota / max(world, 1)
+
+
+def rank_threads(world: int) -> int:
+    """Host copy threads of one rank's reader (the bench's end-to-end and stream legs): half the
+    CPUs its main thread may use, 8 at most, and no more than its quota share less one CPU for the
+    rank's main thread and the engine's own threads.  CEC_E2E_THREADS overrides."""
+    env = int(os.environ.get("CEC_E2E_THREADS", "0"))
+    if env:
+        return env
+    n = max(1, min(8, len(os.sched_getaffinity(0)) // 2))
+    share = quota_share(world)
+    if share is not None:
+        n = max(1, min(n, int(share) - 1))
+    return n
+
+
+def multi_copy_threads(world: int) -> int:
+    """Staging copy threads per cec_multi shard (CEC_MULTI_COPY_THREADS; the engine's default is
+    4): at N > 1 under a quota, half the rank's share, so the ranks' reader and staging threads
+    together stay within the job's CPUs."""
+    env = os.environ.get("CEC_MULTI_COPY_THREADS")
+    if env:
+        return int(env)
+    share = quota_share(world)
+    if share is None or world <= 1:
+        return 4
+    return max(1, min(4, int(share) // 2))

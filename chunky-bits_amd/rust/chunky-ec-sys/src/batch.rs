@@ -296,16 +296,51 @@ struct LiveRead {
     n: usize,
 }
 
+/// The chunk's next copy from location `start` on (`fetch` reads `chunk.locations[start..]` and
+/// returns `(index, bytes)` of the first location that reads): `(next start, bytes)`, or `None`
+/// when the locations are exhausted.  A copy that is not `size` bytes cannot hash to the metadata
+/// digest (the reference hashes it and moves on, file_part.rs:100-107), so it is passed over.
+fn next_copy<F>(fetch: &mut F, part: usize, chunk: usize, start: usize, size: usize) -> Option<(usize, Vec<u8>)>
+where
+    F: FnMut(usize, usize, usize) -> Option<(usize, Vec<u8>)>,
+{
+    let mut start = start;
+    loop {
+        let (loc, bytes) = fetch(part, chunk, start)?;
+        start = loc + 1;
+        if bytes.len() == size {
+            return Some((start, bytes));
+        }
+    }
+}
+
+/// Chunks to load next for a part short of d verified chunks: those whose copy failed
+/// verification first (their next location: file_part.rs:100-107 walks a chunk's locations
+/// before it draws another chunk), then the untried ones.
+fn draw_order(good: &[bool], tried: &[bool], exhausted: &[bool]) -> Vec<usize> {
+    let t = good.len();
+    let again = (0..t).filter(|&i| tried[i] && !good[i] && !exhausted[i]);
+    let fresh = (0..t).filter(|&i| !tried[i] && !exhausted[i]);
+    again.chain(fresh).collect()
+}
+
 /// `FileReadBuilder`'s reader (reader.rs:40-75) batched over the multi-GPU scheduler with
 /// `read_with_context`'s retry rule (file_part.rs:86-129), parts handed out in file order.
 ///
-/// For each part of a window of `parts_per_batch * devices.len()` parts it loads the first d
-/// chunks `fetch` returns (data chunks first, so an intact part needs no rebuild) into a
-/// page-locked buffer, and submits the window as one scheduler job: every loaded chunk verified
+/// `fetch(part, chunk, start)` is one step of the reference's walk over a chunk's locations: it
+/// reads `chunk.locations[start..]` in order and returns `(index, bytes)` of the first location
+/// that reads, or `None` when none is left.  For each part of a window of
+/// `parts_per_batch * devices.len()` parts (all of this reader's shape) the reader loads the first
+/// d chunks that have a copy (data chunks first, so an intact part needs no rebuild) into a
+/// page-locked buffer and submits the window as one scheduler job: every loaded chunk verified
 /// against its metadata digest, the data chunks rebuilt.  It loads the next window while that one
 /// runs.  A part whose loaded chunks do not all verify goes again with the chunks that verified
-/// (`CEC_PRESENT_VERIFIED`: used, not hashed again) and as many untried chunks as it is short of
-/// d, until it decodes or runs out of chunks.  `include/chunky_ec.hpp`'s
+/// (`CEC_PRESENT_VERIFIED`: used, not hashed again), the failed chunks' NEXT copies (the same
+/// chunk's next location is read before another chunk is drawn, file_part.rs:100-107), then
+/// untried chunks, up to d, until it decodes or runs out of copies.  So a chunk listed
+/// `[bad, good]` -- what resilver leaves when it appends a rebuilt copy's location
+/// (file_part.rs:346) -- reads as in the reference.  [`FileReader`] splits a file into runs of one
+/// shape (the short last part has its own chunk size).  `include/chunky_ec.hpp`'s
 /// `FileReference::read_run` / `retry` is the same loop in C++ and
 /// `chunky-bits_amd/chunky_ec/batchreader.py` its Python twin; both are tested on the GPU.
 pub struct BatchReader {
@@ -322,6 +357,9 @@ pub struct BatchReader {
     expected: [Vec<u8>; 2],
     verified: [Vec<u8>; 2],
     status: [Vec<c_int>; 2],
+    // per chunk of a window: the next location to read, and whether none is left
+    cursor: [Vec<usize>; 2],
+    exhausted: [Vec<bool>; 2],
     retries: u64,
 }
 
@@ -348,6 +386,8 @@ impl BatchReader {
             expected: [vec![0u8; window * t * 32], vec![0u8; window * t * 32]],
             verified: [vec![0u8; window * t], vec![0u8; window * t]],
             status: [vec![0; window], vec![0; window]],
+            cursor: [vec![0; window * t], vec![0; window * t]],
+            exhausted: [vec![false; window * t], vec![false; window * t]],
             multi,
             codec,
             d: data,
@@ -368,11 +408,10 @@ impl BatchReader {
         &self.codec
     }
 
-    /// Parts `0..n_parts` of a file: `digests` holds the metadata digests, `n_parts * (d + p)`
-    /// of them, part by part (`FilePart::data` then `parity`); `fetch(part, chunk)` returns the
-    /// stored chunk's bytes, or `None` when no location has it (`Location::read_with_context`
-    /// over the chunk's locations, file_part.rs:100-107); `sink(part, data_chunks)` gets the d
-    /// data chunks of every part in file order, valid during the call.
+    /// Parts `0..n_parts` of a file, all of this reader's shape: `digests` holds the metadata
+    /// digests, `n_parts * (d + p)` of them, part by part (`FilePart::data` then `parity`);
+    /// `fetch(part, chunk, start)` as above; `sink(part, data_chunks)` gets the d data chunks of
+    /// every part in file order, valid during the call.
     pub fn read<F, S, E>(
         &mut self,
         n_parts: usize,
@@ -381,7 +420,7 @@ impl BatchReader {
         mut sink: S,
     ) -> Result<(), BatchReadError<E>>
     where
-        F: FnMut(usize, usize) -> Option<Vec<u8>>,
+        F: FnMut(usize, usize, usize) -> Option<(usize, Vec<u8>)>,
         S: FnMut(usize, &[&[u8]]) -> Result<(), E>,
     {
         if digests.len() < n_parts * self.t {
@@ -419,31 +458,37 @@ impl BatchReader {
         }
     }
 
-    /// The first d chunks `fetch` returns for each part of window `slot` (file_part.rs:86-107
-    /// loads d), and every chunk's metadata digest.
+    /// The first d chunks of each part of window `slot` that have a copy (file_part.rs:86-107
+    /// loads d), each at its first location that reads, and every chunk's metadata digest.
     fn load<F>(&mut self, slot: usize, first: usize, cnt: usize, digests: &[[u8; 32]], fetch: &mut F)
     where
-        F: FnMut(usize, usize) -> Option<Vec<u8>>,
+        F: FnMut(usize, usize, usize) -> Option<(usize, Vec<u8>)>,
     {
         let (d, t, l) = (self.d, self.t, self.chunk_size);
         let ch: &mut [u8] = &mut self.chunks[slot];
         let pres = &mut self.present[slot];
         let exp = &mut self.expected[slot];
+        let cur = &mut self.cursor[slot];
+        let ex = &mut self.exhausted[slot];
         for q in 0..cnt {
             let mut loaded = 0usize;
             for i in 0..t {
                 let x = q * t + i;
                 exp[x * 32..(x + 1) * 32].copy_from_slice(&digests[(first + q) * t + i]);
                 pres[x] = 0;
+                cur[x] = 0;
+                ex[x] = false;
                 if loaded == d {
                     continue;
                 }
-                if let Some(b) = fetch(first + q, i) {
-                    if b.len() == l {
+                match next_copy(fetch, first + q, i, 0, l) {
+                    Some((next, b)) => {
+                        cur[x] = next;
                         ch[x * l..(x + 1) * l].copy_from_slice(&b);
                         pres[x] = 1;
                         loaded += 1;
-                    }
+                    },
+                    None => ex[x] = true,
                 }
             }
         }
@@ -466,7 +511,7 @@ impl BatchReader {
     /// Waits for a window's job, retries its failed parts, then hands its parts to the sink.
     fn collect<F, S, E>(&mut self, w: LiveRead, fetch: &mut F, sink: &mut S) -> Result<(), BatchReadError<E>>
     where
-        F: FnMut(usize, usize) -> Option<Vec<u8>>,
+        F: FnMut(usize, usize, usize) -> Option<(usize, Vec<u8>)>,
         S: FnMut(usize, &[&[u8]]) -> Result<(), E>,
     {
         self.multi.wait(w.job).map_err(BatchReadError::Engine)?;
@@ -484,16 +529,19 @@ impl BatchReader {
     }
 
     /// file_part.rs:92-107: the failed parts go again with the chunks that verified (flagged
-    /// `CEC_PRESENT_VERIFIED`, taken from the window's buffer: the bytes that verified) plus
-    /// untried ones up to d, until each decodes; a part with no untried chunk left fails the read.
+    /// `CEC_PRESENT_VERIFIED`, taken from the window's buffer: the bytes that verified) plus, up
+    /// to d, the failed chunks' next copies and then untried chunks, until each decodes; a part
+    /// with no copy left fails the read.
     fn retry<F>(&mut self, w: &LiveRead, failed: &[usize], fetch: &mut F) -> Result<(), CecError>
     where
-        F: FnMut(usize, usize) -> Option<Vec<u8>>,
+        F: FnMut(usize, usize, usize) -> Option<(usize, Vec<u8>)>,
     {
         let (d, t, l) = (self.d, self.t, self.chunk_size);
         let f = failed.len();
         let mut tried = vec![false; f * t];
         let mut good = vec![false; f * t];
+        let mut exhausted = vec![false; f * t];
+        let mut cursor = vec![0usize; f * t];
         let mut keep = vec![0u8; f * t * l];  // bytes of every chunk loaded so far
         {
             let ch: &[u8] = &self.chunks[w.slot];
@@ -501,6 +549,8 @@ impl BatchReader {
                 for i in 0..t {
                     tried[r * t + i] = self.present[w.slot][q * t + i] != 0;
                     good[r * t + i] = self.verified[w.slot][q * t + i] != 0;
+                    exhausted[r * t + i] = self.exhausted[w.slot][q * t + i];
+                    cursor[r * t + i] = self.cursor[w.slot][q * t + i];
                 }
                 keep[r * t * l..(r + 1) * t * l].copy_from_slice(&ch[q * t * l..(q + 1) * t * l]);
             }
@@ -520,23 +570,32 @@ impl BatchReader {
                 r_exp[s * t * 32..(s + 1) * t * 32]
                     .copy_from_slice(&self.expected[w.slot][q * t * 32..(q + 1) * t * 32]);
                 let have = (0..t).filter(|&i| good[r * t + i]).count();
-                let mut added = 0usize;
                 for i in 0..t {
                     let (x, y) = (r * t + i, s * t + i);
                     r_pres[y] = 0;
                     if good[x] {
                         r_chunks[y * l..(y + 1) * l].copy_from_slice(&keep[x * l..(x + 1) * l]);
                         r_pres[y] = crate::sys::CEC_PRESENT_VERIFIED;
-                    } else if !tried[x] && have + added < d {
-                        tried[x] = true;
-                        if let Some(b) = fetch(w.first + q, i) {
-                            if b.len() == l {
-                                keep[x * l..(x + 1) * l].copy_from_slice(&b);
-                                r_chunks[y * l..(y + 1) * l].copy_from_slice(&b);
-                                r_pres[y] = 1;
-                                added += 1;
-                            }
-                        }
+                    }
+                }
+                let mut added = 0usize;
+                let order = draw_order(&good[r * t..(r + 1) * t], &tried[r * t..(r + 1) * t],
+                                       &exhausted[r * t..(r + 1) * t]);
+                for i in order {
+                    if !(have + added < d) {
+                        break;
+                    }
+                    let (x, y) = (r * t + i, s * t + i);
+                    tried[x] = true;
+                    match next_copy(fetch, w.first + q, i, cursor[x], l) {
+                        Some((next, b)) => {
+                            cursor[x] = next;
+                            keep[x * l..(x + 1) * l].copy_from_slice(&b);
+                            r_chunks[y * l..(y + 1) * l].copy_from_slice(&b);
+                            r_pres[y] = 1;
+                            added += 1;
+                        },
+                        None => exhausted[x] = true,
                     }
                 }
                 if added == 0 {
@@ -568,5 +627,672 @@ impl BatchReader {
         if let Some(w) = w {
             let _ = self.multi.wait(w.job);
         }
+    }
+}
+
+/// `read_with_context` (file_part.rs:73-135) for one part through the per-call API, with the
+/// batched loop's rule: chunks drawn data first, each kept at its first copy that verifies (one
+/// `sha256_many`-style round of GPU digests per draw), the failed chunks' next copies and then
+/// untried chunks until d verify (`TooFewShardsPresent` when the copies run out), missing data
+/// rebuilt with `reconstruct_data`; returns the d data chunks concatenated.  The path for a part
+/// whose shape no batched run has: the short last part (chunk size ceil(len / d)).
+pub fn read_part<F>(
+    codec: &ReedSolomon,
+    chunksize: usize,
+    digests: &[[u8; 32]],
+    part: usize,
+    mut fetch: F,
+) -> Result<Vec<u8>, CecError>
+where
+    F: FnMut(usize, usize, usize) -> Option<(usize, Vec<u8>)>,
+{
+    let (d, t) = (codec.data_shard_count(), codec.total_shard_count());
+    if digests.len() < t {
+        return Err(crate::too_small("digests"));
+    }
+    let (mut good, mut tried, mut exhausted) = (vec![false; t], vec![false; t], vec![false; t]);
+    let mut cursor = vec![0usize; t];
+    let mut shards: Vec<Option<Vec<u8>>> = vec![None; t];
+    let mut have = 0usize;
+    while have < d {
+        let mut round: Vec<(usize, Vec<u8>)> = Vec::new();
+        for i in draw_order(&good, &tried, &exhausted) {
+            if have + round.len() >= d {
+                break;
+            }
+            tried[i] = true;
+            match next_copy(&mut fetch, part, i, cursor[i], chunksize) {
+                Some((next, b)) => {
+                    cursor[i] = next;
+                    round.push((i, b));
+                },
+                None => exhausted[i] = true,
+            }
+        }
+        if round.is_empty() {
+            return Err(CecError::Erasure(crate::Error::TooFewShardsPresent));
+        }
+        let hashes = crate::sha256_many(&round.iter().map(|(_, b)| b.as_slice()).collect::<Vec<_>>())?;
+        for ((i, b), h) in round.into_iter().zip(hashes) {
+            if h == digests[i] {
+                good[i] = true;
+                shards[i] = Some(b);
+                have += 1;
+            }
+        }
+    }
+    if shards[..d].iter().any(Option::is_none) {
+        codec.reconstruct_data(&mut shards)?;
+    }
+    let mut out = Vec::with_capacity(d * chunksize);
+    for s in shards.into_iter().take(d).flatten() {
+        out.extend_from_slice(&s);
+    }
+    Ok(out)
+}
+
+/// A part's shape: (d, p, chunk size).  Consecutive parts of one shape form a batched run.
+pub type Shape = (usize, usize, usize);
+
+/// Keeps the `keep` most recently used values per key (the readers' and checkers' windows pin
+/// host memory, ~0.35 s per GiB, so a service reuses them across files).
+struct ShapeCache<K, V> {
+    keep: usize,
+    entries: Vec<(K, V)>,
+}
+
+impl<K: PartialEq + Copy, V> ShapeCache<K, V> {
+    fn new(keep: usize) -> Self {
+        ShapeCache { keep: keep.max(1), entries: Vec::new() }
+    }
+
+    /// The value for `shape`, made by `make` when absent (evicting the least recently used).
+    fn get<M>(&mut self, shape: K, make: M) -> Result<&mut V, CecError>
+    where
+        M: FnOnce() -> Result<V, CecError>,
+    {
+        if let Some(at) = self.entries.iter().position(|(s, _)| *s == shape) {
+            let e = self.entries.remove(at);
+            self.entries.push(e);
+        } else {
+            while self.entries.len() >= self.keep {
+                self.entries.remove(0);  // dropped: frees its pinned windows
+            }
+            let v = make()?;
+            self.entries.push((shape, v));
+        }
+        match self.entries.last_mut() {
+            Some((_, v)) => Ok(v),
+            None => Err(crate::too_small("shape cache")),
+        }
+    }
+}
+
+/// Runs of consecutive equal shapes: (first part, parts in the run).
+fn shape_runs(shapes: &[Shape]) -> Vec<(usize, usize)> {
+    let mut runs = Vec::new();
+    let mut k = 0;
+    while k < shapes.len() {
+        let mut n = 1;
+        while k + n < shapes.len() && shapes[k + n] == shapes[k] {
+            n += 1;
+        }
+        runs.push((k, n));
+        k += n;
+    }
+    runs
+}
+
+/// `FileReadBuilder`'s reader over a whole file (reader.rs:32-74): consecutive parts of one shape
+/// go through a [`BatchReader`] of that shape, kept for later files (the `keep` most recently
+/// used shapes); a lone part -- the short last part, whose chunk size is ceil(len / d)
+/// (file_part.rs:152) -- through [`read_part`].  One `FileReader` per service thread replaces
+/// the per-file `BatchReader::new` of INTEGRATION.md §3.2.
+pub struct FileReader {
+    parts_per_batch: usize,
+    depth: usize,
+    devices: Vec<c_int>,
+    readers: ShapeCache<Shape, BatchReader>,
+    codecs: ShapeCache<(usize, usize), ReedSolomon>,
+}
+
+impl FileReader {
+    pub fn new(parts_per_batch: usize, depth: usize, devices: &[c_int], keep: usize) -> FileReader {
+        FileReader {
+            parts_per_batch,
+            depth,
+            devices: devices.to_vec(),
+            readers: ShapeCache::new(keep),
+            codecs: ShapeCache::new(keep),
+        }
+    }
+
+    /// Every part of a file, in order: `shapes[k]` is part k's (d, p, chunksize), `digests` its
+    /// d + p metadata digests part by part, `fetch` / `sink` as [`BatchReader::read`] with file
+    /// part numbers.
+    pub fn read<F, S, E>(
+        &mut self,
+        shapes: &[Shape],
+        digests: &[[u8; 32]],
+        mut fetch: F,
+        mut sink: S,
+    ) -> Result<(), BatchReadError<E>>
+    where
+        F: FnMut(usize, usize, usize) -> Option<(usize, Vec<u8>)>,
+        S: FnMut(usize, &[&[u8]]) -> Result<(), E>,
+    {
+        let mut base = 0usize;  // index of part k's first digest
+        let mut offsets = Vec::with_capacity(shapes.len() + 1);
+        for &(d, p, _) in shapes {
+            offsets.push(base);
+            base += d + p;
+        }
+        if digests.len() < base {
+            return Err(BatchReadError::Engine(crate::too_small("digests")));
+        }
+        let (ppb, depth) = (self.parts_per_batch, self.depth);
+        for (k0, n) in shape_runs(shapes) {
+            let (d, p, l) = shapes[k0];
+            let dig = &digests[offsets[k0]..offsets[k0] + n * (d + p)];
+            if n == 1 {
+                let codec = self.codecs.get((d, p), || ReedSolomon::new(d, p))
+                    .map_err(BatchReadError::Engine)?;
+                let data = read_part(codec, l, dig, k0, &mut fetch).map_err(BatchReadError::Engine)?;
+                let chunks: Vec<&[u8]> = data.chunks(l.max(1)).take(d).collect();
+                sink(k0, &chunks).map_err(BatchReadError::Sink)?;
+                continue;
+            }
+            let devices = &self.devices;
+            let reader = self.readers.get((d, p, l), || BatchReader::new(d, p, l, ppb, depth, devices))
+                .map_err(BatchReadError::Engine)?;
+            reader.read(n, dig, |q, i, s| fetch(k0 + q, i, s), |q, data| sink(k0 + q, data))?;
+        }
+        Ok(())
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Verify and resilver
+// ---------------------------------------------------------------------------------------------
+
+/// One location's copy, as the reference reports it (`Result<bool, LocationError>` of
+/// file_part.rs:236-243 / :277-289: `Ok(true)`, `Ok(false)`, `Err(_)`).
+#[derive(Clone, Copy, Debug, PartialEq, Eq)]
+pub enum CopyCheck {
+    Valid,
+    Invalid,
+    Unreadable,
+}
+
+/// One part of a [`BatchChecker`] pass, handed to the sink in file order.
+pub struct CheckedPart<'a> {
+    /// Part number in file order.
+    pub index: usize,
+    /// `[chunk][location]`, d data then p parity chunks, each chunk's locations in the
+    /// metadata's order: the reference's `read_results`.
+    pub locations: Vec<Vec<CopyCheck>>,
+    /// Resilver: every chunk with no valid copy, rebuilt (data and parity), to be written back
+    /// with its new location appended to `chunk.locations` (file_part.rs:331-347).  Valid during
+    /// the sink call.
+    pub rebuilt: Vec<(usize, &'a [u8])>,
+    /// Resilver: this part's rebuild failure (`ResilverPartReport::write_error`,
+    /// file_part.rs:296-308), e.g. `TooFewShardsPresent`; the other parts go on.
+    pub error: Option<CecError>,
+}
+
+impl CheckedPart<'_> {
+    /// Chunks with a valid copy (file_part.rs:545-547's healthy chunks, before any write-back).
+    pub fn valid_chunks(&self) -> usize {
+        self.locations.iter().filter(|l| l.contains(&CopyCheck::Valid)).count()
+    }
+}
+
+/// A verify / resilver window submitted to the scheduler and not yet handed to the sink.  Its
+/// `Vec`s are the job's buffers: their heap storage does not move with the struct and they are
+/// dropped only after the job was waited for.
+struct LiveCheck {
+    slot: usize,
+    job: Option<u64>,
+    first: usize,
+    n: usize,
+    locations: Vec<Vec<Vec<CopyCheck>>>,
+    items: Vec<(usize, usize, usize)>,
+    single: Vec<(usize, usize)>,
+    present: Vec<u8>,
+    expected: Vec<u8>,
+    ver: Vec<u8>,
+    spill: Vec<u8>,
+}
+
+/// `FileReference::verify` / `resilver` (file_reference.rs:78-113 over `FilePart::verify` /
+/// `resilver`, file_part.rs:228-390) batched over the multi-GPU scheduler, hashing every location
+/// of every chunk like the reference.  `read_all(part, chunk)` returns one entry per location of
+/// the chunk, in the metadata's order: the copy's bytes, or `None` where the location does not
+/// read (`Location::read`).  Each readable copy is one hashing item:
+///
+/// * verify: every copy of a window goes to one `cec_multi_verify` job, d + p items per scheduler
+///   row whatever chunk they belong to;
+/// * resilver: a window whose chunks have one location each is one `cec_multi_resilver` job;
+///   when some chunk has several, those chunks' copies are hashed first (a verify job) and the
+///   resilver job gets their first valid copy flagged `CEC_PRESENT_VERIFIED`: every copy is still
+///   hashed exactly once, each chunk keeps its first valid copy (:277-289) and only the chunks
+///   with none are rebuilt (:296-308).
+///
+/// Two windows in flight (the next one loads while the GPU hashes the current one).
+/// `chunky-bits_amd/chunky_ec/batchcheck.py` is its Python twin (tested on the GPU) and
+/// `include/chunky_ec.hpp`'s `FileReference::check_run` the same loop in C++.
+pub struct BatchChecker {
+    // declared (so dropped) first: the scheduler refers to the codec and the windows
+    multi: Multi,
+    codec: ReedSolomon,
+    t: usize,
+    chunk_size: usize,
+    window: usize,
+    chunks: [HostBuffer; 2],
+    rebuilt: [HostBuffer; 2],
+    present: [Vec<u8>; 2],
+    expected: [Vec<u8>; 2],
+    verified: [Vec<u8>; 2],
+    status: [Vec<c_int>; 2],
+}
+
+impl BatchChecker {
+    pub fn new(
+        data: usize,
+        parity: usize,
+        chunk_size: usize,
+        parts_per_batch: usize,
+        depth: usize,
+        devices: &[c_int],
+    ) -> Result<BatchChecker, CecError> {
+        let codec = ReedSolomon::new(data, parity)?;  // file_part.rs:302
+        let multi = Multi::new(&codec, chunk_size, parts_per_batch, depth, devices)?;
+        let window = parts_per_batch * devices.len().max(1);
+        let dev0 = devices.first().copied().unwrap_or(-1);
+        let t = data + parity;
+        let buf = |n: usize| HostBuffer::zeroed(n, dev0);
+        Ok(BatchChecker {
+            chunks: [buf(window * t * chunk_size)?, buf(window * t * chunk_size)?],
+            rebuilt: [buf(window * t * chunk_size)?, buf(window * t * chunk_size)?],
+            present: [vec![0u8; window * t], vec![0u8; window * t]],
+            expected: [vec![0u8; window * t * 32], vec![0u8; window * t * 32]],
+            verified: [vec![0u8; window * t], vec![0u8; window * t]],
+            status: [vec![0; window], vec![0; window]],
+            multi,
+            codec,
+            t,
+            chunk_size,
+            window,
+        })
+    }
+
+    /// The codec of the parts (`FilePart`'s d and p).
+    pub fn codec(&self) -> &ReedSolomon {
+        &self.codec
+    }
+
+    /// `FilePart::verify` of parts `0..n_parts` (this checker's shape), reports in file order.
+    pub fn verify<R, S, E>(&mut self, n_parts: usize, digests: &[[u8; 32]], read_all: R, sink: S)
+        -> Result<(), BatchReadError<E>>
+    where
+        R: FnMut(usize, usize) -> Vec<Option<Vec<u8>>>,
+        S: FnMut(&CheckedPart<'_>) -> Result<(), E>,
+    {
+        self.run(0, n_parts, digests, read_all, sink, false)
+    }
+
+    /// `FilePart::resilver` of parts `0..n_parts`: the sink writes each part's `rebuilt` chunks
+    /// and appends their new locations.
+    pub fn resilver<R, S, E>(&mut self, n_parts: usize, digests: &[[u8; 32]], read_all: R, sink: S)
+        -> Result<(), BatchReadError<E>>
+    where
+        R: FnMut(usize, usize) -> Vec<Option<Vec<u8>>>,
+        S: FnMut(&CheckedPart<'_>) -> Result<(), E>,
+    {
+        self.run(0, n_parts, digests, read_all, sink, true)
+    }
+
+    /// The window loop; `base` is added to the part numbers the sink sees (a run of a file).
+    #[allow(clippy::too_many_arguments)]
+    fn run<R, S, E>(&mut self, base: usize, n_parts: usize, digests: &[[u8; 32]], mut read_all: R,
+                    mut sink: S, resilver: bool) -> Result<(), BatchReadError<E>>
+    where
+        R: FnMut(usize, usize) -> Vec<Option<Vec<u8>>>,
+        S: FnMut(&CheckedPart<'_>) -> Result<(), E>,
+    {
+        if digests.len() < n_parts * self.t {
+            return Err(BatchReadError::Engine(crate::too_small("digests")));
+        }
+        let mut at = 0usize;
+        let mut slot = 0usize;
+        let mut pending: Option<LiveCheck> = None;
+        loop {
+            let mut current = None;
+            if at < n_parts {
+                let cnt = self.window.min(n_parts - at);
+                let submitted = if resilver {
+                    self.submit_resilver(slot, at, cnt, digests, &mut read_all)
+                } else {
+                    self.submit_verify(slot, at, cnt, digests, &mut read_all)
+                };
+                match submitted {
+                    Ok(w) => current = Some(w),
+                    Err(e) => {
+                        self.drain(pending.take());
+                        return Err(BatchReadError::Engine(e));
+                    },
+                }
+                at += cnt;
+            }
+            // the older window's parts go out first: file order
+            if let Some(prev) = pending.take() {
+                let done = if resilver {
+                    self.collect_resilver(prev, base, &mut sink)
+                } else {
+                    self.collect_verify(prev, base, &mut sink)
+                };
+                if let Err(e) = done {
+                    self.drain(current);
+                    return Err(e);
+                }
+            }
+            match current {
+                None => return Ok(()),
+                Some(c) => pending = Some(c),
+            }
+            slot ^= 1;
+        }
+    }
+
+    /// Every location's copy of every chunk of window [first, first + cnt) and the results'
+    /// skeleton: `Unreadable` where a location does not read, `Invalid` where its copy has the
+    /// wrong size (it cannot hash to the digest), `Valid` (still to be checked) otherwise.
+    #[allow(clippy::type_complexity)]
+    fn copies<R>(&self, first: usize, cnt: usize, read_all: &mut R)
+        -> (Vec<Vec<Vec<Option<Vec<u8>>>>>, Vec<Vec<Vec<CopyCheck>>>)
+    where
+        R: FnMut(usize, usize) -> Vec<Option<Vec<u8>>>,
+    {
+        let copies: Vec<Vec<Vec<Option<Vec<u8>>>>> =
+            (0..cnt).map(|q| (0..self.t).map(|i| read_all(first + q, i)).collect()).collect();
+        let l = self.chunk_size;
+        let locations = copies
+            .iter()
+            .map(|part| {
+                part.iter()
+                    .map(|locs| {
+                        locs.iter()
+                            .map(|c| match c {
+                                None => CopyCheck::Unreadable,
+                                Some(b) if b.len() != l => CopyCheck::Invalid,
+                                Some(_) => CopyCheck::Valid,
+                            })
+                            .collect()
+                    })
+                    .collect()
+            })
+            .collect();
+        (copies, locations)
+    }
+
+    /// Fills a verify job's rows for `items` [(part, chunk, location)]: the copies into `buf`, d
+    /// + p per row; returns (rows, present, expected, verified flags).
+    #[allow(clippy::type_complexity)]
+    fn rows(t: usize, l: usize, items: &[(usize, usize, usize)],
+            copies: &[Vec<Vec<Option<Vec<u8>>>>], first: usize, digests: &[[u8; 32]],
+            buf: &mut [u8]) -> (usize, Vec<u8>, Vec<u8>, Vec<u8>) {
+        let g = (items.len() + t - 1) / t;
+        let mut present = vec![0u8; g * t];
+        let mut expected = vec![0u8; g * t * 32];
+        for (x, &(q, i, j)) in items.iter().enumerate() {
+            if let Some(b) = &copies[q][i][j] {
+                buf[x * l..(x + 1) * l].copy_from_slice(b);
+                present[x] = 1;
+                expected[x * 32..(x + 1) * 32].copy_from_slice(&digests[(first + q) * t + i]);
+            }
+        }
+        (g, present, expected, vec![0u8; g * t])
+    }
+
+    fn submit_verify<R>(&mut self, slot: usize, first: usize, cnt: usize, digests: &[[u8; 32]],
+                        read_all: &mut R) -> Result<LiveCheck, CecError>
+    where
+        R: FnMut(usize, usize) -> Vec<Option<Vec<u8>>>,
+    {
+        let (copies, locations) = self.copies(first, cnt, read_all);
+        let mut items = Vec::new();
+        for (q, part) in locations.iter().enumerate() {
+            for (i, locs) in part.iter().enumerate() {
+                for (j, c) in locs.iter().enumerate() {
+                    if *c == CopyCheck::Valid {
+                        items.push((q, i, j));
+                    }
+                }
+            }
+        }
+        let mut w = LiveCheck { slot, job: None, first, n: cnt, locations, items, single: Vec::new(),
+                                present: Vec::new(), expected: Vec::new(), ver: Vec::new(),
+                                spill: Vec::new() };
+        if w.items.is_empty() {
+            return Ok(w);
+        }
+        let (t, l) = (self.t, self.chunk_size);
+        let rows_needed = (w.items.len() + t - 1) / t;
+        // more copies than the pinned window holds (many locations): a pageable buffer, staged
+        let pinned = rows_needed <= self.window;
+        if !pinned {
+            w.spill = vec![0u8; rows_needed * t * l];
+        }
+        let (g, present, expected, ver) = {
+            let buf: &mut [u8] = if pinned { &mut self.chunks[slot] } else { &mut w.spill };
+            Self::rows(t, l, &w.items, &copies, first, digests, buf)
+        };
+        w.present = present;
+        w.expected = expected;
+        w.ver = ver;
+        let buf: *const u8 = if pinned { self.chunks[slot].as_ptr() } else { w.spill.as_ptr() };
+        w.job = Some(unsafe {
+            self.multi.submit_verify(buf, w.present.as_ptr(), w.expected.as_ptr(), g, w.ver.as_mut_ptr())
+        }?);
+        Ok(w)
+    }
+
+    fn collect_verify<S, E>(&mut self, mut w: LiveCheck, base: usize, sink: &mut S)
+        -> Result<(), BatchReadError<E>>
+    where
+        S: FnMut(&CheckedPart<'_>) -> Result<(), E>,
+    {
+        if let Some(job) = w.job {
+            self.multi.wait(job).map_err(BatchReadError::Engine)?;
+        }
+        for (x, &(q, i, j)) in w.items.iter().enumerate() {
+            w.locations[q][i][j] = if w.ver[x] != 0 { CopyCheck::Valid } else { CopyCheck::Invalid };
+        }
+        for (q, locations) in w.locations.into_iter().enumerate() {
+            let part = CheckedPart { index: base + w.first + q, locations, rebuilt: Vec::new(), error: None };
+            sink(&part).map_err(BatchReadError::Sink)?;
+        }
+        Ok(())
+    }
+
+    fn submit_resilver<R>(&mut self, slot: usize, first: usize, cnt: usize, digests: &[[u8; 32]],
+                          read_all: &mut R) -> Result<LiveCheck, CecError>
+    where
+        R: FnMut(usize, usize) -> Vec<Option<Vec<u8>>>,
+    {
+        let (t, l) = (self.t, self.chunk_size);
+        let (copies, mut locations) = self.copies(first, cnt, read_all);
+        // chunks with several locations: every copy hashed first (file_part.rs:277-289)
+        let mut multi = Vec::new();
+        for (q, part) in locations.iter().enumerate() {
+            for (i, locs) in part.iter().enumerate() {
+                if locs.len() > 1 {
+                    for (j, c) in locs.iter().enumerate() {
+                        if *c == CopyCheck::Valid {
+                            multi.push((q, i, j));
+                        }
+                    }
+                }
+            }
+        }
+        if !multi.is_empty() {
+            let mut buf = vec![0u8; ((multi.len() + t - 1) / t) * t * l];
+            let (g, present, expected, mut ver) = Self::rows(t, l, &multi, &copies, first, digests, &mut buf);
+            self.multi.verify(&buf, &present, &expected, g, &mut ver)?;
+            for (x, &(q, i, j)) in multi.iter().enumerate() {
+                locations[q][i][j] = if ver[x] != 0 { CopyCheck::Valid } else { CopyCheck::Invalid };
+            }
+        }
+        let mut single = Vec::new();
+        {
+            let ch: &mut [u8] = &mut self.chunks[slot];
+            let pres = &mut self.present[slot];
+            let exp = &mut self.expected[slot];
+            for q in 0..cnt {
+                for i in 0..t {
+                    let x = q * t + i;
+                    exp[x * 32..(x + 1) * 32].copy_from_slice(&digests[(first + q) * t + i]);
+                    pres[x] = 0;
+                    let locs = &locations[q][i];
+                    // a lone copy is hashed by the resilver job; a chunk with several locations
+                    // brings its first valid copy, already verified
+                    let pick = match locs.iter().position(|c| *c == CopyCheck::Valid) {
+                        Some(j) if locs.len() == 1 => Some((j, 1u8)),
+                        Some(j) => Some((j, crate::sys::CEC_PRESENT_VERIFIED)),
+                        None => None,
+                    };
+                    if let Some((j, flag)) = pick {
+                        if let Some(b) = &copies[q][i][j] {
+                            ch[x * l..(x + 1) * l].copy_from_slice(b);
+                            pres[x] = flag;
+                            if flag == 1 {
+                                single.push((q, i));
+                            }
+                        }
+                    }
+                }
+            }
+        }
+        let job = unsafe {
+            self.multi.submit_resilver(
+                self.chunks[slot].as_ptr(),
+                self.present[slot].as_ptr(),
+                self.expected[slot].as_ptr(),
+                cnt,
+                self.rebuilt[slot].as_mut_ptr(),
+                self.verified[slot].as_mut_ptr(),
+                self.status[slot].as_mut_ptr(),
+            )
+        }?;
+        Ok(LiveCheck { slot, job: Some(job), first, n: cnt, locations, items: Vec::new(), single,
+                       present: Vec::new(), expected: Vec::new(), ver: Vec::new(), spill: Vec::new() })
+    }
+
+    fn collect_resilver<S, E>(&mut self, mut w: LiveCheck, base: usize, sink: &mut S)
+        -> Result<(), BatchReadError<E>>
+    where
+        S: FnMut(&CheckedPart<'_>) -> Result<(), E>,
+    {
+        if let Some(job) = w.job {
+            self.multi.wait(job).map_err(BatchReadError::Engine)?;
+        }
+        let (t, l) = (self.t, self.chunk_size);
+        let ver = &self.verified[w.slot];
+        for &(q, i) in &w.single {
+            w.locations[q][i][0] = if ver[q * t + i] != 0 { CopyCheck::Valid } else { CopyCheck::Invalid };
+        }
+        let rebuilt: &[u8] = &self.rebuilt[w.slot];
+        for (q, locations) in w.locations.into_iter().enumerate() {
+            let missing: Vec<usize> = (0..t).filter(|&i| ver[q * t + i] == 0).collect();
+            let mut part = CheckedPart { index: base + w.first + q, locations, rebuilt: Vec::new(), error: None };
+            if !missing.is_empty() {
+                match crate::check(self.status[w.slot][q]) {
+                    // this part's write_error; the other parts go on (file_reference.rs:103-110)
+                    Err(e @ CecError::Erasure(_)) => part.error = Some(e),
+                    Err(e) => return Err(BatchReadError::Engine(e)),
+                    Ok(()) => {
+                        part.rebuilt = missing
+                            .into_iter()
+                            .map(|i| (i, &rebuilt[(q * t + i) * l..(q * t + i + 1) * l]))
+                            .collect();
+                    },
+                }
+            }
+            sink(&part).map_err(BatchReadError::Sink)?;
+        }
+        Ok(())
+    }
+
+    /// Waits for a window's job without handing out its parts (error paths).
+    fn drain(&self, w: Option<LiveCheck>) {
+        if let Some(LiveCheck { job: Some(job), .. }) = w {
+            let _ = self.multi.wait(job);
+        }
+    }
+}
+
+/// `FileReference::verify` / `resilver` over a whole file: consecutive parts of one shape through
+/// a [`BatchChecker`] of that shape (kept for later files, the `keep` most recently used), a lone
+/// part (the short last part) through a checker of one part per window.  Reports reach the sink
+/// in file order with file part numbers.
+pub struct FileChecker {
+    parts_per_batch: usize,
+    depth: usize,
+    devices: Vec<c_int>,
+    checkers: ShapeCache<(Shape, usize), BatchChecker>,
+}
+
+impl FileChecker {
+    pub fn new(parts_per_batch: usize, depth: usize, devices: &[c_int], keep: usize) -> FileChecker {
+        FileChecker { parts_per_batch, depth, devices: devices.to_vec(), checkers: ShapeCache::new(keep) }
+    }
+
+    pub fn verify<R, S, E>(&mut self, shapes: &[Shape], digests: &[[u8; 32]], read_all: R, sink: S)
+        -> Result<(), BatchReadError<E>>
+    where
+        R: FnMut(usize, usize) -> Vec<Option<Vec<u8>>>,
+        S: FnMut(&CheckedPart<'_>) -> Result<(), E>,
+    {
+        self.runs(shapes, digests, read_all, sink, false)
+    }
+
+    pub fn resilver<R, S, E>(&mut self, shapes: &[Shape], digests: &[[u8; 32]], read_all: R, sink: S)
+        -> Result<(), BatchReadError<E>>
+    where
+        R: FnMut(usize, usize) -> Vec<Option<Vec<u8>>>,
+        S: FnMut(&CheckedPart<'_>) -> Result<(), E>,
+    {
+        self.runs(shapes, digests, read_all, sink, true)
+    }
+
+    fn runs<R, S, E>(&mut self, shapes: &[Shape], digests: &[[u8; 32]], mut read_all: R, mut sink: S,
+                     resilver: bool) -> Result<(), BatchReadError<E>>
+    where
+        R: FnMut(usize, usize) -> Vec<Option<Vec<u8>>>,
+        S: FnMut(&CheckedPart<'_>) -> Result<(), E>,
+    {
+        let mut offsets = Vec::with_capacity(shapes.len());
+        let mut base = 0usize;
+        for &(d, p, _) in shapes {
+            offsets.push(base);
+            base += d + p;
+        }
+        if digests.len() < base {
+            return Err(BatchReadError::Engine(crate::too_small("digests")));
+        }
+        let depth = self.depth;
+        for (k0, n) in shape_runs(shapes) {
+            let (d, p, l) = shapes[k0];
+            let ppb = if n > 1 { self.parts_per_batch } else { 1 };
+            let devices = &self.devices;
+            // a lone part's checker has one-part windows: the window size is part of the key
+            let checker = self.checkers.get(((d, p, l), ppb), || {
+                BatchChecker::new(d, p, l, ppb, depth, devices)
+            }).map_err(BatchReadError::Engine)?;
+            let dig = &digests[offsets[k0]..offsets[k0] + n * (d + p)];
+            let read = |q: usize, i: usize| read_all(k0 + q, i);
+            checker.run(k0, n, dig, read, &mut sink, resilver)?;
+        }
+        Ok(())
     }
 }

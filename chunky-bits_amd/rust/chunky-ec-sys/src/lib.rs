@@ -562,6 +562,26 @@ pub fn sha256(buf: &[u8]) -> Result<[u8; 32], CecError> {
     Ok(out)
 }
 
+/// Many `Sha256::digest` calls in one launch (`cec_sha256_many`): the digest of every buffer, in
+/// order.  Concurrent callers are coalesced like [`sha256`]'s.
+pub fn sha256_many(bufs: &[&[u8]]) -> Result<Vec<[u8; 32]>, CecError> {
+    if bufs.is_empty() {
+        return Ok(Vec::new());
+    }
+    let ptrs: Vec<*const u8> = bufs.iter().map(|b| b.as_ptr()).collect();
+    let lens: Vec<usize> = bufs.iter().map(|b| b.len()).collect();
+    let mut out = vec![0u8; 32 * bufs.len()];
+    check(unsafe { sys::cec_sha256_many(ptrs.as_ptr(), lens.as_ptr(), bufs.len(), out.as_mut_ptr()) })?;
+    Ok(out
+        .chunks(32)
+        .map(|c| {
+            let mut a = [0u8; 32];
+            a.copy_from_slice(c);
+            a
+        })
+        .collect())
+}
+
 /// `FilePart::write_with_encoder`'s compute for one part: (chunksize, parity chunks, d+p digests).
 pub fn part_encode(
     codec: &ReedSolomon,
@@ -1107,7 +1127,91 @@ impl Multi {
         Ok(job)
     }
 
-    /// Waits for a job queued with [`Multi::submit_encode_hash`] or [`Multi::submit_read`].
+    /// `FilePart::verify`'s compute (file_part.rs:228-251) for `n_parts` rows of d + p items:
+    /// `verified[x] = 1` iff item x (`present[x] != 0`) hashes to `expected[x]`.  The rows need
+    /// not be parts: any d + p copies per row, whatever chunk each belongs to (one item per
+    /// location, [`crate::batch::BatchChecker`]).
+    pub fn verify(
+        &self,
+        chunks: &[u8],
+        present: &[u8],
+        expected: &[u8],
+        n_parts: usize,
+        verified: &mut [u8],
+    ) -> Result<(), CecError> {
+        let (t, l) = (self.t, self.chunk_len);
+        if chunks.len() < n_parts * t * l {
+            return Err(too_small("chunks"));
+        }
+        if present.len() < n_parts * t || verified.len() < n_parts * t {
+            return Err(too_small("present / verified"));
+        }
+        if expected.len() < n_parts * t * 32 {
+            return Err(too_small("expected"));
+        }
+        let job = unsafe {
+            self.submit_verify(chunks.as_ptr(), present.as_ptr(), expected.as_ptr(), n_parts,
+                               verified.as_mut_ptr())
+        }?;
+        self.wait(job)
+    }
+
+    /// Asynchronous [`Multi::verify`].
+    ///
+    /// # Safety
+    /// `chunks` (`n_parts * (d + p) * L` bytes), `present` / `verified` (`n_parts * (d + p)`)
+    /// and `expected` (`n_parts * (d + p) * 32`) must stay valid, and the inputs unmodified, until
+    /// the job has been waited for.
+    pub unsafe fn submit_verify(
+        &self,
+        chunks: *const u8,
+        present: *const u8,
+        expected: *const u8,
+        n_parts: usize,
+        verified: *mut u8,
+    ) -> Result<u64, CecError> {
+        let mut job = 0u64;
+        check_multi(sys::cec_multi_verify(self.raw, chunks, present, expected, n_parts, verified,
+                                          &mut job))?;
+        Ok(job)
+    }
+
+    /// `FilePart::resilver`'s compute (file_part.rs:266-308), asynchronous: every chunk of the
+    /// `n_parts` parts whose `present` flag is 0, or whose copy does not verify, rebuilt (data
+    /// and parity) into `rebuilt` `[n][d+p][L]`; `verified` and `status` as [`Multi::read`].
+    ///
+    /// # Safety
+    /// `chunks` / `rebuilt` (`n_parts * (d + p) * L` bytes), `present` / `verified`
+    /// (`n_parts * (d + p)`), `expected` (`n_parts * (d + p) * 32`) and `status` (`n_parts`) must
+    /// stay valid, and the inputs unmodified, until the job has been waited for.
+    #[allow(clippy::too_many_arguments)]
+    pub unsafe fn submit_resilver(
+        &self,
+        chunks: *const u8,
+        present: *const u8,
+        expected: *const u8,
+        n_parts: usize,
+        rebuilt: *mut u8,
+        verified: *mut u8,
+        status: *mut c_int,
+    ) -> Result<u64, CecError> {
+        let mut job = 0u64;
+        check_multi(sys::cec_multi_resilver(
+            self.raw,
+            chunks,
+            present,
+            expected,
+            n_parts,
+            rebuilt,
+            verified,
+            status,
+            std::ptr::null_mut(),
+            &mut job,
+        ))?;
+        Ok(job)
+    }
+
+    /// Waits for a job queued with one of the `submit_*` calls.
     pub fn wait(&self, job: u64) -> Result<(), CecError> {
         check_multi(unsafe { sys::cec_multi_wait(self.raw, job) })
     }

@@ -270,3 +270,22 @@ def test_write_stream_collects_every_digest_and_checks_them():
         assert bench.stream_check(ring.copy(), got, d, p, 2) == [17]
     finally:
         c.close()
+
+
+def test_rank_threads_respect_the_quota_share(monkeypatch):
+    """N ranks share one cgroup CPU quota: each rank's reader threads stay within its share (less
+    one CPU for its main thread), the scheduler's staging threads take half of it; without a quota
+    the affinity rule (half the CPUs, 8 at most) applies."""
+    from chunky_ec import sharding
+    monkeypatch.delenv("CEC_E2E_THREADS", raising=False)
+    monkeypatch.delenv("CEC_MULTI_COPY_THREADS", raising=False)
+    monkeypatch.setattr(sharding.os, "sched_getaffinity", lambda pid: set(range(128)))
+    monkeypatch.setattr(sharding, "cpu_quota", lambda: (128, 16.0))
+    assert [sharding.rank_threads(w) for w in (1, 2, 4, 8)] == [8, 7, 3, 1]
+    assert [sharding.multi_copy_threads(w) for w in (1, 2, 4, 8)] == [4, 4, 2, 1]
+    assert sharding.quota_share(8) == 2.0
+    monkeypatch.setattr(sharding, "cpu_quota", lambda: (128, None))
+    assert [sharding.rank_threads(w) for w in (1, 8)] == [8, 8]
+    assert sharding.multi_copy_threads(8) == 4 and sharding.quota_share(8) is None
+    monkeypatch.setenv("CEC_E2E_THREADS", "3")
+    assert sharding.rank_threads(8) == 3

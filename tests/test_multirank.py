@@ -51,10 +51,13 @@ def _worker(rank, world, port, n_parts, out_q):
         # bench.py's N > 1 line: each rank's C3 / C4 figures in the RANK_FIELDS row, the node's
         # configs[2] / configs[3] figures computed from the gathered rows on every rank
         import bench
+        from chunky_ec.sharding import multi_copy_threads, quota_share, rank_threads
         row = [rank, 0, 1, 8, 40.0, 50.0, 55.0, 0.8, 0.74, 0.7 + 0.01 * rank, 1e9 * (rank + 1),
-               5.0 + rank, 10.0 + rank, (rank + 1) * 1e9, 30.0]
-        node = bench.node_figures([bench.rank_row(r, x) for r, x in
-                                   enumerate(gather_rows(row, world))])
+               5.0 + rank, 10.0 + rank, (rank + 1) * 1e9, 30.0,
+               quota_share(world) or 0.0, rank_threads(world), multi_copy_threads(world)]
+        ranks = [bench.rank_row(r, x) for r, x in enumerate(gather_rows(row, world))]
+        node = bench.node_figures(ranks)
+        node["rank_rows"] = ranks
         gathered = [None] * world
         dist.all_gather_object(gathered, res)
         out_q.put((rank, t, gathered, ok_all, ok_one_fails, rows, node))
@@ -95,6 +98,14 @@ def test_gloo_sharding_matches_single_process(world):
         assert c4["max_ms"] == 10.0 + world - 1
         assert c4["value"] == round(c4["data_bytes"] / ((10.0 + world - 1) / 1e3) / 1e9, 2)
         assert node["c3_reconstruct"]["min_frac"] == 0.7 and node["ranks"] == world
+        # every rank reports the host threads it used and its share of the job's CPU quota
+        from chunky_ec.sharding import cpu_quota
+        quota = cpu_quota()[1]
+        for row in node["rank_rows"]:
+            assert row["host_threads"] >= 1 and row["multi_copy_threads"] >= 1
+            if quota:
+                assert row["quota_share_cpus"] == pytest.approx(quota / world, rel=1e-3)
+                assert row["host_threads"] <= max(1, int(quota / world) - 1)
         assert t == pytest.approx(0.5 * world)  # max over ranks of (rank+1)*0.5
         assert ok_all and not ok_one_fails
         assert rows == [[float(r), 10.0 * r + 0.5,

@@ -186,3 +186,34 @@ def test_batch_reader_mirrors_the_cpp_and_python_loops():
     for s in ("def _load", "def _submit", "def _collect", "def _retry", "have + added < d",
               "PRESENT_VERIFIED", "TOO_FEW_SHARDS_PRESENT"):
         assert s in py, s
+
+
+def test_location_walk_is_the_same_rule_in_rust_python_and_cpp():
+    """The read loops walk a chunk's locations before drawing another chunk (file_part.rs:100-107)
+    and verify / resilver hash every location (:236-243, :277-289), resilver appending the
+    rebuilt copy's location (:346): the same helpers and steps in the Rust crate, its Python twins
+    (run on the GPU) and the C++ host layer (run on the GPU by the mirror test)."""
+    batch = _crate_sources()["batch.rs"]
+    for s in ("fn next_copy<", "fn draw_order(", "FnMut(usize, usize, usize) -> Option<(usize, Vec<u8>)>",
+              "pub fn read_part<", "pub struct FileReader", "pub struct BatchChecker",
+              "pub struct FileChecker", "CEC_PRESENT_VERIFIED", "submit_verify(", "submit_resilver(",
+              "pub enum CopyCheck"):
+        assert s in batch, s
+    retry = batch[batch.index("    fn retry<"):batch.index("    fn drain(&self, w: Option<LiveRead>)")]
+    assert "draw_order(" in retry and "next_copy(" in retry and "cursor[x]" in retry
+    lib = open(RUST).read()
+    for s in ("pub fn sha256_many(", "pub unsafe fn submit_verify(", "pub unsafe fn submit_resilver(",
+              "pub fn build_id("):
+        assert s in lib, s
+    py_reader = open(os.path.join(ROOT, "chunky-bits_amd", "chunky_ec", "batchreader.py")).read()
+    for s in ("def next_copy", "def draw_order", "def read_part", "class FileReader"):
+        assert s in py_reader, s
+    py_check = open(os.path.join(ROOT, "chunky-bits_amd", "chunky_ec", "batchcheck.py")).read()
+    for s in ("class BatchChecker", "class FileChecker", "PRESENT_VERIFIED", "def _submit_resilver",
+              "def _submit_verify"):
+        assert s in py_check, s
+    hpp = open(os.path.join(ROOT, "include", "chunky_ec.hpp")).read()
+    for s in ("inline const Bytes* next_copy(", "inline std::vector<size_t> draw_order(",
+              "std::vector<Location> locations;", "c.locations.push_back(dest.write_shard(",
+              "CEC_PRESENT_VERIFIED"):
+        assert s in hpp, s
