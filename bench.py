@@ -207,6 +207,25 @@ def host_info():
             "build_id": ce.BUILD_ID, "build_matches_source": ce.BUILD_MATCHES_SOURCE}
 
 
+def measured_valu(config: str, kernel: str, full_size: bool):
+    """VALU issue of `kernel` from the committed SQ counter runs (profiles/valu.json, written by
+    profiles/summarize_shapes.py): SIMD-cycles per VALU wave-instruction and the busy fraction
+    (4 x SQ_INSTS_VALU / SIMD-cycles, 4 cycles = one VALU issue of a lone wave), or None when this
+    workload was not profiled."""
+    path = os.path.join(ROOT, "profiles", "valu.json")
+    if not full_size or not os.path.exists(path):
+        return None
+    e = json.load(open(path)).get(config, {}).get(KERNEL_SYMBOL.get(kernel, kernel)
+                                                  if isinstance(KERNEL_SYMBOL.get(kernel, kernel), str)
+                                                  else kernel)
+    if not e:
+        return None
+    return {"simd_cycles_per_valu": e["simd_cycles_per_valu"], "valu_busy": e["valu_busy"],
+            "unit": "SIMD-cycles per wave64 VALU instruction; busy = 4 x SQ_INSTS_VALU / "
+                    "((GRBM_GUI_ACTIVE / 8) x 1024)",
+            "source": "committed rocprofv3 SQ pass (not this run): " + e["source"]}
+
+
 def cpu_baseline(cfg, threads: int, cores_total: int, cores_avail: int, quota):
     """Oracle restatement of the crate path timed on this host (rank 0, N=1 only), with the
     process's full CPU affinity (the caller restores it: the bench binds its main thread to
@@ -1452,6 +1471,12 @@ def main():
                 "ms": round(floor_ms, 2), "frac": round(floor_ms / sha_ms, 4),
                 "basis": f"{blocks} blocks per chunk x {SHA_VALU_PER_BLOCK} VALU x 4 cycles per "
                          f"instruction of one wave alone, {MI355X_CLOCK_GHZ} GHz"}
+        # the same kernel's VALU issue measured by rocprofv3 SQ counters (committed run of this
+        # command, not this run): SQ_INSTS_VALU over (GRBM_GUI_ACTIVE / 8 XCDs) x 1024 SIMDs
+        counters = measured_valu(args.config, sha_kernel,
+                                 n_parts == CONFIGS[args.config]["parts"] and not args.shape)
+        if counters:
+            valu["counters"] = counters
 
     ok = None
     if args.check and rank == 0 and cfg["op"] == "read":

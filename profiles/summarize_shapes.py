@@ -5,7 +5,9 @@ one row per (kernel, grid size), and merge the full-size launch of each kernel (
 into profiles/traffic.json under --config (read by bench.py).
 
     python profiles/summarize_shapes.py <tag> [--config c2] [--fetch-mult 2]
-                                        [--grid encode_hash_kernel=131072,...]
+                                        [--grid encode_hash_kernel=131072,...] [--committed]
+
+--committed re-reads the CSVs already copied to profiles/<tag>/ (no GPU run needed).
 
 --grid names the launch shape to merge for a kernel when its largest grid is not the config's
 (the default line also runs BASELINE's C3 / C4 configurations: C4's fused kernel and C3's
@@ -15,6 +17,15 @@ Durations come from the kernel trace (run_kernel_trace.csv, every dispatch); cou
 separate --pmc passes, matched to the same (kernel, grid).  HBM traffic per launch, as
 profiles/summarize.py: 2 x FETCH_SIZE x 1024 + WRITE_SIZE x 1024 (gfx950 FETCH_SIZE reports half
 the bytes of these streaming reads, tools/ubench_fetch.hip).
+
+VALU utilisation per launch, from the SQ pass (units stated in the table): GRBM_GUI_ACTIVE counts
+cycles summed over the 8 XCDs, so the launch lasts GRBM_GUI_ACTIVE / 8 cycles and offers
+(GRBM_GUI_ACTIVE / 8) x 1024 SIMD-cycles (256 CUs x 4 SIMDs); SQ_INSTS_VALU counts wave64 VALU
+instructions.  SIMD-cycles per VALU instruction = that ratio; a SIMD issues at most one VALU
+wave-instruction per 4 cycles to one wave (the lone-wave issue floor, MI355X_MICROARCH.md), so
+"VALU busy" = 4 x SQ_INSTS_VALU / SIMD-cycles.  SQ_ACTIVE_INST_VALU equals SQ_INSTS_VALU on gfx950
+(one count per instruction), so it adds no separate figure.  The full-size launch of each kernel
+goes into profiles/valu.json under --config (read by bench.py's valu_roofline).
 """
 import collections
 import csv
@@ -70,11 +81,16 @@ def main():
         for kv in sys.argv[sys.argv.index("--grid") + 1].split(","):
             k, g = kv.split("=")
             pick[k] = int(g)
-    src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
-    tr = trace_groups(os.path.join(src, "trace", "run_kernel_trace.csv"))
-    sq, sq_dur = pmc_groups(os.path.join(src, "pmc_sq", "run_counter_collection.csv"))
-    fetch, _ = pmc_groups(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"))
-    write, _ = pmc_groups(os.path.join(src, "pmc_write", "run_counter_collection.csv"))
+    committed = "--committed" in sys.argv
+    src = os.path.join(ROOT, "profiles", tag) if committed else \
+        os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+
+    def csv_path(sub, fn):  # gpurun_out/prof_<tag>/<sub>/<fn>, or its committed copy
+        return os.path.join(src, f"{sub}_{fn}") if committed else os.path.join(src, sub, fn)
+    tr = trace_groups(csv_path("trace", "run_kernel_trace.csv"))
+    sq, sq_dur = pmc_groups(csv_path("pmc_sq", "run_counter_collection.csv"))
+    fetch, _ = pmc_groups(csv_path("pmc_fetch", "run_counter_collection.csv"))
+    write, _ = pmc_groups(csv_path("pmc_write", "run_counter_collection.csv"))
     cmd = open(os.path.join(src, "command.txt")).read().strip() \
         if os.path.exists(os.path.join(src, "command.txt")) else "bench.py"
     lines = [f"# rocprofv3 summary `{tag}` ({config})", "",
@@ -91,8 +107,15 @@ def main():
     lines += ["", "## Counters (separate `--pmc` passes; per-launch means over the launches of "
               "that shape)", "",
               "| kernel | grid | clock GHz (GRBM_GUI_ACTIVE/8/dur) | SQ_WAVES | VALU insts/wave | "
+              "SIMD-cycles per VALU inst ((GRBM_GUI_ACTIVE/8)x1024/SQ_INSTS_VALU) | "
+              "VALU busy (4xSQ_INSTS_VALU/SIMD-cycles) | "
               f"FETCH_SIZE KiB | WRITE_SIZE KiB | HBM traffic GB ({fmult:g}xFETCH+WRITE) |",
-              "|---|---|---|---|---|---|---|---|"]
+              "|---|---|---|---|---|---|---|---|---|---|"]
+    valu_table = {}
+    vpath = os.path.join(ROOT, "profiles", "valu.json")
+    if os.path.exists(vpath):
+        valu_table = json.load(open(vpath))
+    valu_big = {}
     traffic = {}
     tpath = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tpath):
@@ -107,11 +130,20 @@ def main():
         ghz = mean(c["GRBM_GUI_ACTIVE"]) / 8 / (d_ms / 1e3) / 1e9 if d_ms else float("nan")
         waves = mean(c["SQ_WAVES"])
         vpw = mean(c["SQ_INSTS_VALU"]) / waves if waves else float("nan")
+        simd_cycles = mean(c["GRBM_GUI_ACTIVE"]) / 8 * 1024
+        insts = mean(c["SQ_INSTS_VALU"])
+        cpi = simd_cycles / insts if insts else float("nan")
+        busy = 4 * insts / simd_cycles if simd_cycles else float("nan")
         f = mean(fetch[key].get("FETCH_SIZE", []))
         w = mean(write[key].get("WRITE_SIZE", []))
         tb = (fmult * f + w) * 1024 if f == f and w == w else None
-        lines.append(f"| {k} | {grid} | {ghz:.2f} | {waves:.0f} | {vpw:.0f} | {f:.0f} | {w:.0f} | "
-                     f"{tb / 1e9 if tb else float('nan'):.2f} |")
+        lines.append(f"| {k} | {grid} | {ghz:.2f} | {waves:.0f} | {vpw:.0f} | {cpi:.2f} | "
+                     f"{busy:.3f} | {f:.0f} | {w:.0f} | {tb / 1e9 if tb else float('nan'):.2f} |")
+        vchosen = grid == pick[k] if k in pick else grid > valu_big.get(k, (0, None))[0]
+        if insts and k in TRAFFIC_KERNELS and vchosen:
+            valu_big[k] = (grid, {"simd_cycles_per_valu": round(cpi, 3), "valu_busy": round(busy, 4),
+                                  "valu_insts": insts, "simd_cycles": simd_cycles, "grid": grid,
+                                  "source": f"profiles/{tag}_summary.md"})
         chosen = grid == pick[k] if k in pick else grid > biggest.get(k, (0, None))[0]
         if tb and k in TRAFFIC_KERNELS and chosen:
             biggest[k] = (grid, {"bytes_per_launch": int(tb), "fetch_kib": f, "write_kib": w,
@@ -119,11 +151,18 @@ def main():
                                  "source": f"profiles/{tag}_summary.md"})
     for k, (_, entry) in biggest.items():
         traffic.setdefault(config, {})[k] = entry
+    for k, (_, entry) in valu_big.items():
+        valu_table.setdefault(config, {})[k] = entry
+    with open(vpath, "w") as fh:
+        json.dump(valu_table, fh, indent=1)
     with open(os.path.join(ROOT, "profiles", f"{tag}_summary.md"), "w") as fh:
         fh.write("\n".join(lines) + "\n")
     with open(tpath, "w") as fh:
         json.dump(traffic, fh, indent=1)
     dst = os.path.join(ROOT, "profiles", tag)
+    if committed:  # the CSVs are already there
+        print("\n".join(lines))
+        return
     os.makedirs(dst, exist_ok=True)
     for sub in ("trace", "pmc_sq", "pmc_fetch", "pmc_write"):
         for fn in ("run_kernel_stats.csv", "run_counter_collection.csv", "run_kernel_trace.csv"):

@@ -289,3 +289,14 @@ def test_rank_threads_respect_the_quota_share(monkeypatch):
     assert sharding.multi_copy_threads(8) == 4 and sharding.quota_share(8) is None
     monkeypatch.setenv("CEC_E2E_THREADS", "3")
     assert sharding.rank_threads(8) == 3
+
+
+def test_measured_valu_names_its_source():
+    """valu_roofline.counters: the headline kernel's VALU issue from the committed SQ counters
+    (profiles/valu.json, profiles/summarize_shapes.py): about one VALU per 4.15 SIMD-cycles, i.e.
+    ~0.96 of a lone wave's one-per-4-cycles issue floor; None for unprofiled shapes."""
+    v = bench.measured_valu("c2", "encode_hash_kernel", True)
+    assert v and 4.0 < v["simd_cycles_per_valu"] < 4.4 and 0.9 < v["valu_busy"] <= 1.0
+    assert "not this run" in v["source"] and "r4e_c2_summary.md" in v["source"]
+    assert bench.measured_valu("c2", "encode_hash_kernel", False) is None
+    assert bench.measured_valu("c4", "encode_hash_kernel", True) is None
