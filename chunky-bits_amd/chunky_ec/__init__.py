@@ -180,6 +180,10 @@ _sig("cec_pipeline_new_ex", [_vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_siz
 _sig("cec_pipeline_submit_from", [_vp, ctypes.c_size_t, _vp, ctypes.c_size_t, _vp, _vp])
 _sig("cec_read_pipeline_submit_from", [_vp, ctypes.c_size_t, _vp, _vp, _vp, ctypes.c_size_t, _vp])
 _sig("cec_read_pipeline_submit_packed", [_vp, ctypes.c_size_t, _vp, _vp, _vp, ctypes.c_size_t, _vp])
+_sig("cec_read_pipeline_carry_ids", [_vp, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int32)])
+_sig("cec_read_pipeline_submit_carried", [_vp, ctypes.c_size_t, ctypes.c_size_t,
+                                          ctypes.POINTER(ctypes.c_int32)])
+_sig("cec_read_pipeline_carry_release", [_vp, ctypes.c_int32])
 _sig("cec_multi_new", [_vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t,
                        ctypes.POINTER(ctypes.c_int), ctypes.c_size_t, ctypes.POINTER(_vp)])
 _sig("cec_multi_free", [_vp], None)
@@ -665,6 +669,7 @@ class ReadPipeline:
     """
 
     REBUILT_ONLY = 1  # CEC_READ_REBUILT_ONLY
+    CARRY = 16  # CEC_READ_CARRY: retries' verified chunks kept on the device
 
     def __init__(self, codec: ReedSolomon, chunk_len: int, parts_per_batch: int, depth: int = 4,
                  flags: int = 0):
@@ -680,6 +685,7 @@ class ReadPipeline:
         self.L = chunk_len
         self.parts = parts_per_batch
         self.depth = depth
+        self.carry = bool(flags & self.CARRY)
 
     def __del__(self, _free=_lib.cec_read_pipeline_free):
         h = getattr(self, "_h", None)
@@ -702,6 +708,28 @@ class ReadPipeline:
 
     def submit(self, slot: int, n_parts: int) -> None:
         _check(_lib.cec_read_pipeline_submit(self._h, slot, n_parts))
+
+    def carry_ids(self, slot: int, n_parts: int):
+        """[n_parts] int32: each part's carry entry after wait (-1: none; CARRY pipelines)."""
+        import numpy as np
+        ids = np.full(max(n_parts, 1), -1, np.int32)
+        _check(_lib.cec_read_pipeline_carry_ids(
+            self._h, slot, ids.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
+        return ids[:n_parts]
+
+    def submit_carried(self, slot: int, n_parts: int, carry_ids) -> None:
+        """submit, with carry_ids[n_parts] (-1 = none): those parts' CEC_PRESENT_VERIFIED chunks
+        come from the carry pool (the slot need not hold them)."""
+        import numpy as np
+        ids = np.ascontiguousarray(carry_ids, dtype=np.int32)
+        assert len(ids) >= n_parts
+        code = _lib.cec_read_pipeline_submit_carried(
+            self._h, slot, n_parts, ids.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+        if code != OK:
+            raise Error(code)
+
+    def carry_release(self, carry_id: int) -> None:
+        _check(_lib.cec_read_pipeline_carry_release(self._h, int(carry_id)))
 
     def submit_from(self, slot: int, chunks, present, expected, n_parts: int, data=None) -> None:
         """Batch from the caller's buffers (page-locked ones are DMA'd directly)."""
@@ -835,6 +863,7 @@ PIPE_EXTERNAL = 2  # CEC_PIPE_EXTERNAL
 PRESENT_VERIFIED = 0x80  # CEC_PRESENT_VERIFIED: read-retry flag (loaded, verified by an earlier pass)
 READ_RESILVER = 4  # CEC_READ_RESILVER: read-pipeline flag, FilePart::resilver's compute
 READ_VERIFY_ONLY = 8  # CEC_READ_VERIFY_ONLY: read-pipeline flag, FilePart::verify's compute
+READ_CARRY = 16  # CEC_READ_CARRY: read-pipeline flag, retries' verified chunks kept on the device
 
 
 class MultiError(Error):

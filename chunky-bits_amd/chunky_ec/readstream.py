@@ -15,7 +15,10 @@ slots, `depth` batches in flight):
   ``CEC_PRESENT_VERIFIED`` (used, not hashed again) plus as many untried chunks, drawn at random,
   as it is short of d; the next batch carries the queued retries ahead of its new parts;
 * a part with fewer than d chunks left to try is undecodable (the reference's read fails with
-  ``TooFewShardsPresent`` there; the stream counts it and goes on).
+  ``TooFewShardsPresent`` there; the stream counts it and goes on);
+* on a pipeline made with ``ReadPipeline.CARRY`` the verified chunks of a part to retry stay on
+  the device (the reference keeps them in memory, file_part.rs:102-104): its retry takes them
+  from the carry pool, so only the new chunks are fetched and uploaded.
 
 The caller supplies the storage side: ``fetch(chunks, rows)`` copies the chunk bytes into the
 slot's pinned [parts][d+p][L] array for every (row, part id, flags) in ``rows``, for each chunk
@@ -42,6 +45,7 @@ class _Part:
     tried: np.ndarray         # [t] bool: chunks loaded by any pass so far
     good: np.ndarray          # [t] bool: chunks that verified
     attempts: int = 1         # submissions of this part so far
+    carry: int = -1           # CARRY pipelines: the carry entry holding its verified chunks
 
 
 @dataclass
@@ -54,6 +58,7 @@ class ReadRepairStats:
     rejected_chunks: int = 0    # loaded chunks whose sha256 did not match the metadata
     undecodable_parts: int = 0  # parts left with fewer than d chunks to try
     chunks_loaded: int = 0      # chunk loads (first loads, retry loads and re-sent verified ones)
+    carried_chunks: int = 0     # verified chunks a retry took from the device carry pool
     undecodable: List[int] = field(default_factory=list)  # their part ids (first 64)
 
     def as_dict(self) -> dict:
@@ -78,6 +83,7 @@ class ReadRepairStream:
         self.on_part = on_part
         self.P, self.d, self.t = rp.parts, rp.d, rp.t
         self.depth = rp.depth
+        self.carry = bool(getattr(rp, "carry", False))
         self.stats = ReadRepairStats()
         self._retry: Deque[_Part] = deque()
         self._inflight: Deque[Tuple[int, List[_Part], np.ndarray]] = deque()
@@ -108,6 +114,9 @@ class ReadRepairStream:
                 self.stats.undecodable_parts += 1
                 if len(self.stats.undecodable) < 64:
                     self.stats.undecodable.append(e.part)
+                if e.carry >= 0:  # its kept chunks will not be used
+                    self.rp.carry_release(e.carry)
+                    e.carry = -1
                 continue
             new = self.rng.choice(untried, need, replace=False)
             row = np.where(e.good, PRESENT_VERIFIED, 0).astype(np.uint8)
@@ -124,10 +133,20 @@ class ReadRepairStream:
         pres[:n] = present
         ids = np.fromiter((e.part for e in parts), dtype=np.int64, count=n)
         expected[:n] = self.digests(ids)
-        self.fetch(chunks, [(k, int(ids[k]), present[k]) for k in range(n)])
-        self.rp.submit(slot, n)
+        carry = np.fromiter((e.carry for e in parts), dtype=np.int32, count=n)
+        # a carried part's verified chunks are on the device already: fetch only its new ones
+        fetch_rows = present.copy()
+        fetch_rows[(carry >= 0)[:, None] & (present == PRESENT_VERIFIED)] = 0
+        self.fetch(chunks, [(k, int(ids[k]), fetch_rows[k]) for k in range(n)])
+        if (carry >= 0).any():
+            self.rp.submit_carried(slot, n, carry)
+            for e in parts:
+                e.carry = -1  # an entry is used once
+        else:
+            self.rp.submit(slot, n)
         self.stats.batches += 1
-        self.stats.chunks_loaded += int(np.count_nonzero(present))
+        self.stats.chunks_loaded += int(np.count_nonzero(fetch_rows))
+        self.stats.carried_chunks += int(np.count_nonzero(present) - np.count_nonzero(fetch_rows))
         self._inflight.append((slot, parts, present))
 
     # -- results --------------------------------------------------------------------------------
@@ -136,6 +155,7 @@ class ReadRepairStream:
         slot, parts, present = self._inflight.popleft()
         _, ver, status = self.rp.wait(slot)
         n = len(parts)
+        carry = self.rp.carry_ids(slot, n) if self.carry else None
         for k in range(n):
             st = int(status[k])
             e = parts[k]
@@ -150,6 +170,7 @@ class ReadRepairStream:
             ok = ver[k] != 0
             self.stats.rejected_chunks += int(np.count_nonzero(loaded & ~ok))
             e.good = ok.copy()
+            e.carry = int(carry[k]) if carry is not None else -1
             e.attempts += 1
             self.stats.retried_parts += 1
             self._retry.append(e)

@@ -122,6 +122,8 @@ struct MoveParams {
     const uint32_t* ids;
     uint32_t n;
     uint32_t to_batch;
+    // nullable: chunk j of the packed side is at packed + packed_ids[j] * len (else j * len)
+    const uint32_t* packed_ids = nullptr;
 };
 hipError_t launch_move_chunks(const MoveParams& a, hipStream_t s);
 

@@ -1,8 +1,9 @@
 // Environment knobs of the engine, read ONCE per process.
 //
 // Every A/B and test knob (CEC_APPLY_*, CEC_FUSED*, CEC_SHA_VARIANT, CEC_COALESCE_*,
-// CEC_READ_*, CEC_SPEC_LDS_KIB, CEC_VERIFY_COMPACT, CEC_MULTI_COPY_THREADS) is parsed into one
-// immutable snapshot on first use; the launch paths read the snapshot, never the environment.
+// CEC_READ_*, CEC_SPEC_LDS_KIB, CEC_VERIFY_COMPACT, CEC_MULTI_COPY_THREADS, CEC_SLOT_QUEUES)
+// is parsed into one immutable snapshot on first use; the launch paths read the snapshot, never
+// the environment.
 // The reference calls the hot path from tokio worker threads (writer.rs:200-210 spawns a task
 // per part; file_part.rs:161 runs the encode inside block_in_place), and getenv racing a setenv
 // elsewhere in the host process is undefined behaviour; a snapshot read is a plain load.
@@ -52,6 +53,7 @@ struct Knobs {
     bool read_side = false;              // CEC_READ_SIDE
     bool read_upstream = false;          // CEC_READ_UPSTREAM
     unsigned multi_copy_threads = 4;     // CEC_MULTI_COPY_THREADS (1..32)
+    bool slot_queues = true;             // CEC_SLOT_QUEUES: a hardware queue per pipeline slot
 };
 
 // The current snapshot (parsed on first call).

@@ -6,7 +6,9 @@
 // command per batch instead of one per run of consecutive loaded chunks (~900 per 256-part
 // RS(10,4) batch at ~11 us each: 47 vs 57 GB/s, tools/h2d_bench.hip).  This kernel then places
 // chunk j of the packed buffer at its batch position ids[j] = k*t + i: an HBM-to-HBM copy of the
-// loaded bytes (~1 ms per 2.5 GiB batch), far below the PCIe time it saves.
+// loaded bytes (~1 ms per 2.5 GiB batch), far below the PCIe time it saves.  With packed_ids the
+// packed side is itself indexed (chunk j at packed_ids[j]): the read pipeline's carry pool moves
+// a batch's kept chunks in and out with one launch each (CEC_READ_CARRY).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -32,7 +34,8 @@ __global__ void __launch_bounds__(kMoveThreads) move_chunks_kernel(MoveParams a,
         const uint64_t n = (a.len - off < kMoveSlice) ? a.len - off : kMoveSlice;
         const uint32_t id = a.ids[j];
         uint8_t* b = a.batch + uint64_t(id / a.t) * a.part_stride + uint64_t(id % a.t) * a.chunk_stride + off;
-        uint8_t* p = a.packed + j * a.len + off;
+        const uint64_t pj = a.packed_ids ? a.packed_ids[j] : j;
+        uint8_t* p = a.packed + pj * a.len + off;
         const uint8_t* src = a.to_batch ? p : b;
         uint8_t* dst = a.to_batch ? b : p;
         if (vec16) {

@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <deque>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -60,6 +61,23 @@ class DeviceGuard {
     bool switched_ = false;
     hipError_t err_ = hipSuccess;
 };
+
+// A slot's stream.  HIP maps streams onto GPU_MAX_HW_QUEUES (4 by default) hardware queues per
+// process, the null stream included, so `depth` slot streams made with hipStreamCreate can land
+// two slots on one queue: the later slot's next batch then waits in that queue behind the whole
+// of the other's batch (measured: the first 4-deep read pipeline of a process had slots 2 and 3
+// on one queue and ran 24% slower than the second).  A CU-masked stream gets a hardware queue of
+// its own; the mask names every CU, so the kernels see the whole GPU (CEC_SLOT_QUEUES=0: plain
+// streams).
+hipError_t slot_stream(hipStream_t* stream, int device) {
+    if (!cec::knobs().slot_queues) return hipStreamCreateWithFlags(stream, hipStreamNonBlocking);
+    int cus = 0;
+    hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+    if (e != hipSuccess) return e;
+    std::vector<uint32_t> mask((size_t(cus) + 31) / 32, ~0u);
+    if (cus % 32) mask.back() = (1u << (cus % 32)) - 1;
+    return hipExtStreamCreateWithCUMask(stream, uint32_t(mask.size()), mask.data());
+}
 
 struct Slot {
     uint8_t* h_data = nullptr;    // pinned [parts][d][L] (null with CEC_PIPE_EXTERNAL)
@@ -182,7 +200,7 @@ int cec_pipeline_new_ex(const cec_codec* codec, size_t chunk_len, size_t parts_p
         host(&s.h_dig, pl->parts * pl->t * 32);
         if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_buf), pl->parts * pl->t * pl->cs);
         if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_dig), pl->parts * pl->t * 32);
-        if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
+        if (e == hipSuccess) e = slot_stream(&s.stream, pl->device);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
         if (e != hipSuccess) {
             delete pl;
@@ -320,6 +338,17 @@ struct ReadSlot {
     std::vector<uint8_t> decode_mask;  // present mask the speculative decode used
     std::vector<const uint8_t*> data_ptrs;  // [parts][d]: where each data chunk is (after wait)
     std::vector<size_t> src_off;  // [parts][t]: byte offset of a loaded chunk in src_chunks
+    // CEC_READ_CARRY: per part of this batch, the carry entry its verified chunks were kept in
+    // at wait (-1: none), and whether its CEC_PRESENT_VERIFIED chunks came from the carry pool at
+    // submit (not from the caller's buffer: they are copied back like rebuilt ones)
+    std::vector<int32_t> carry_ids;
+    std::vector<uint8_t> carried;
+    hipEvent_t stashed = nullptr;  // after the last stash out of d_buf
+    bool stash_pending = false;    // the next upload into d_buf must wait for `stashed`
+    // the move kernel's index lists: [0, 2*parts*t) the stash's (batch positions, then pool
+    // positions), [2*parts*t, 4*parts*t) the consume's; pinned, then uploaded
+    uint32_t* h_cids = nullptr;
+    uint32_t* d_cids = nullptr;
 };
 
 }  // namespace
@@ -347,6 +376,18 @@ struct cec_read_pipeline {
     hipStream_t up = nullptr;
     std::vector<ReadSlot> slots;
     size_t next = 0;
+    // CEC_READ_CARRY: device pool of `carry_cap` entries of [t][cs] bytes (made with the
+    // pipeline: a fresh multi-GiB allocation is cleared by the driver in the background, which
+    // would compete with the uploads if it were made mid-stream) holding the verified chunks of
+    // parts reported CEC_TOO_FEW_SHARDS_PRESENT until their retry takes them (or the caller
+    // releases them); per entry an event after its last stash or consumption, so reusing an entry
+    // waits for its previous copies.
+    bool carry = false;
+    size_t carry_cap = 0;
+    uint8_t* d_carry = nullptr;
+    std::vector<hipEvent_t> carry_ready;
+    std::vector<uint8_t> carry_used;
+    std::deque<int32_t> carry_free;
 
     ~cec_read_pipeline() {
         int cur = 0;
@@ -356,21 +397,97 @@ struct cec_read_pipeline {
         for (ReadSlot& s : slots) {
             if (s.stream) (void)hipStreamSynchronize(s.stream);
             if (s.side) (void)hipStreamSynchronize(s.side);
-            for (hipEvent_t ev : {s.done, s.fork, s.join, s.uploaded})
+            for (hipEvent_t ev : {s.done, s.fork, s.join, s.uploaded, s.stashed})
                 if (ev) (void)hipEventDestroy(ev);
             if (s.stream) (void)hipStreamDestroy(s.stream);
             if (s.side) (void)hipStreamDestroy(s.side);
             for (void* dptr : {static_cast<void*>(s.d_buf), static_cast<void*>(s.d_expected),
                                static_cast<void*>(s.d_flags), static_cast<void*>(s.d_pack),
-                               static_cast<void*>(s.d_ids)})
+                               static_cast<void*>(s.d_ids), static_cast<void*>(s.d_cids)})
                 if (dptr) (void)hipFree(dptr);
             if (s.h_ids) (void)hipHostFree(s.h_ids);
+            if (s.h_cids) (void)hipHostFree(s.h_cids);
             for (uint8_t* hptr : {s.h_chunks, s.h_present, s.h_expected, s.h_data, s.h_ok, s.h_hash})
                 if (hptr) (void)hipHostFree(hptr);
             delete[] s.h_status;
         }
         if (up) (void)hipStreamDestroy(up);
+        for (hipEvent_t ev : carry_ready)
+            if (ev) (void)hipEventDestroy(ev);
+        if (d_carry) (void)hipFree(d_carry);
         (void)hipSetDevice(cur);
+    }
+
+    // The carry pool and its events (at creation).
+    hipError_t make_carry_pool() {
+        hipError_t e = hipMalloc(reinterpret_cast<void**>(&d_carry), carry_cap * t * cs);
+        if (e != hipSuccess) {
+            d_carry = nullptr;
+            return e;
+        }
+        // touched once here, not by the first stashes mid-stream
+        e = hipMemset(d_carry, 0, carry_cap * t * cs);
+        if (e != hipSuccess) return e;
+        carry_ready.assign(carry_cap, nullptr);
+        for (auto& ev : carry_ready) {
+            e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+            if (e != hipSuccess) return e;
+        }
+        carry_used.assign(carry_cap, 0);
+        carry_free.clear();
+        for (size_t i = 0; i < carry_cap; ++i) carry_free.push_back(int32_t(i));
+        return hipSuccess;
+    }
+
+    // A free carry entry (-1 when the pool is full).
+    int32_t carry_take() {
+        while (!carry_free.empty()) {  // the entry freed longest ago first (FIFO)
+            const int32_t id = carry_free.front();
+            carry_free.pop_front();
+            carry_used[size_t(id)] = 1;
+            return id;
+        }
+        return -1;
+    }
+    void carry_give_back(int32_t id) {
+        carry_used[size_t(id)] = 0;
+        carry_free.push_back(id);
+    }
+    bool carry_valid(int32_t id) const {
+        return id >= 0 && size_t(id) < carry_used.size() && carry_used[size_t(id)];
+    }
+    // The slot's carry index lists (made on first use).
+    int ensure_carry_ids(ReadSlot& s) const {
+        const size_t n = 4 * parts * t;
+        hipError_t e = hipSuccess;
+        if (!s.d_cids) e = hipMalloc(reinterpret_cast<void**>(&s.d_cids), n * sizeof(uint32_t));
+        if (e == hipSuccess && !s.h_cids)
+            e = cec::host_malloc_near(reinterpret_cast<void**>(&s.h_cids), n * sizeof(uint32_t),
+                                      hipHostMallocDefault, device);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            return pipe_fail(e, "read pipeline carry index lists");
+        }
+        return CEC_OK;
+    }
+    // Moves chunks between d_buf and the pool with one kernel: pairs[j] = (batch position, pool
+    // position), written into the slot's index list at `region` (0: stash, 1: consume), uploaded
+    // on `stream`, then moved (to_batch: pool -> d_buf).
+    int carry_move(ReadSlot& s, const std::vector<std::pair<uint32_t, uint32_t>>& pairs,
+                   size_t region, bool to_batch, hipStream_t stream) const {
+        const size_t m = pairs.size();
+        if (!m) return CEC_OK;
+        uint32_t* h = s.h_cids + region * 2 * parts * t;
+        uint32_t* dv = s.d_cids + region * 2 * parts * t;
+        for (size_t j = 0; j < m; ++j) {
+            h[j] = pairs[j].first;
+            h[m + j] = pairs[j].second;
+        }
+        PIPE_TRY(hipMemcpyAsync(dv, h, 2 * m * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
+        cec::MoveParams mv{s.d_buf, t * cs, cs, uint32_t(t), d_carry, cs, dv, uint32_t(m),
+                           to_batch ? 1u : 0u, dv + m};
+        PIPE_TRY(cec::launch_move_chunks(mv, stream));
+        return CEC_OK;
     }
 
     cec_part_batch batch(ReadSlot& s, size_t n) const {
@@ -381,13 +498,16 @@ struct cec_read_pipeline {
     // them) into their data slots: one copy per run of consecutive missing data chunks.
     int copy_rebuilt_back(ReadSlot& s, size_t k, hipStream_t stream) const {
         const uint8_t* pr = s.h_present + k * t;
+        const bool carried = !s.carried.empty() && s.carried[k];
+        // in the caller's buffer: loaded chunks, except those a carried part took from the pool
+        auto held = [&](size_t j) { return pr[j] && !(carried && pr[j] == CEC_PRESENT_VERIFIED); };
         for (size_t j = 0; j < d;) {
-            if (pr[j]) {
+            if (held(j)) {
                 ++j;
                 continue;
             }
             size_t e = j;
-            while (e < d && !pr[e]) ++e;
+            while (e < d && !held(e)) ++e;
             uint8_t* dst = s.dst_data + (k * d + j) * L;
             const uint8_t* src = s.d_buf + (k * t + j) * cs;
             if (cs == L)
@@ -486,8 +606,11 @@ struct cec_read_pipeline {
     // packed: `chunks` holds the loaded chunks back to back (part by part, ascending chunk
     // index), uploaded with ONE copy and placed by the move kernel; else chunk (k, i) is at
     // chunks + (k*t + i)*L and goes up with one copy per run of consecutive loaded chunks.
+    // carry_ids (CEC_READ_CARRY, nullable): per part, a carry entry whose chunks replace the
+    // part's CEC_PRESENT_VERIFIED chunks (copied on the device; the caller's buffer need not hold
+    // them), or -1.
     int submit(ReadSlot& s, const uint8_t* chunks, size_t n_parts, uint8_t* data_out,
-               bool packed = false) {
+               bool packed = false, const int32_t* carry_ids = nullptr) {
         DeviceGuard guard(device);
         PIPE_TRY(guard.status());
         if (s.in_flight) {  // the slot's pinned arrays may still be read by its last batch
@@ -495,12 +618,62 @@ struct cec_read_pipeline {
             s.in_flight = false;
         }
         const size_t n = n_parts * t;
+        s.carried.assign(carry_ids ? n_parts : 0, 0);
+        if (carry_ids) {
+            if (!carry || packed) {
+                g_pipe_error = "carry ids need CEC_READ_CARRY and an unpacked submit";
+                return CEC_ERR_INVALID_ARGUMENT;
+            }
+            for (size_t k = 0; k < n_parts; ++k) {
+                if (carry_ids[k] < 0) continue;
+                if (!carry_valid(carry_ids[k])) {
+                    g_pipe_error = "carry id not held (already used or released)";
+                    return CEC_ERR_INVALID_ARGUMENT;
+                }
+                for (size_t q = 0; q < k; ++q)
+                    if (carry_ids[q] == carry_ids[k]) {
+                        g_pipe_error = "carry id given twice";
+                        return CEC_ERR_INVALID_ARGUMENT;
+                    }
+                s.carried[k] = 1;
+            }
+        }
         s.src_chunks = chunks;
         s.dst_data = data_out;
         s.src_off.resize(n);
         const int sst = ensure_streams(s);
         if (sst != CEC_OK) return sst;
         const hipStream_t us = upload_stream(s);
+        if (s.stash_pending) {  // the last batch's carried chunks leave d_buf before it is refilled
+            if (us != s.stream) PIPE_TRY(hipStreamWaitEvent(us, s.stashed, 0));
+            s.stash_pending = false;
+        }
+        // carried parts: their verified chunks from the pool, one move launch on the compute
+        // stream (after each entry's stash), queued BEFORE the uploads (it writes only the
+        // positions they do not, and the slot's last batch is done): an entry is free again as
+        // soon as this move has run, not once the PCIe uploads ahead of it in the stream have
+        if (!s.carried.empty()) {
+            std::vector<std::pair<uint32_t, uint32_t>> pairs;
+            std::vector<int32_t> used;
+            for (size_t k = 0; k < n_parts; ++k) {
+                if (!s.carried[k]) continue;
+                const int32_t id = carry_ids[k];
+                PIPE_TRY(hipStreamWaitEvent(s.stream, carry_ready[size_t(id)], 0));
+                const uint8_t* pr = s.h_present + k * t;
+                for (size_t i = 0; i < t; ++i)
+                    if (pr[i] == CEC_PRESENT_VERIFIED)
+                        pairs.emplace_back(uint32_t(k * t + i), uint32_t(size_t(id) * t + i));
+                used.push_back(id);
+            }
+            const int cst = ensure_carry_ids(s);
+            if (cst != CEC_OK) return cst;
+            const int mst = carry_move(s, pairs, 1, true, s.stream);
+            if (mst != CEC_OK) return mst;
+            for (int32_t id : used) {
+                PIPE_TRY(hipEventRecord(carry_ready[size_t(id)], s.stream));
+                carry_give_back(id);
+            }
+        }
         if (packed) {
             const int est = ensure_packed(s);
             if (est != CEC_OK) return est;
@@ -524,16 +697,19 @@ struct cec_read_pipeline {
             return submit_compute(s, n_parts);
         }
         for (size_t x = 0; x < n; ++x) s.src_off[x] = x * L;
-        // loaded chunks up: one copy per run of consecutive loaded chunks of a part
+        // loaded chunks up: one copy per run of consecutive loaded chunks of a part (a carried
+        // part's verified chunks come from the carry pool instead, below)
         for (size_t k = 0; k < n_parts; ++k) {
             const uint8_t* pr = s.h_present + k * t;
+            const bool carried = !s.carried.empty() && s.carried[k];
+            auto up = [&](size_t i) { return pr[i] && !(carried && pr[i] == CEC_PRESENT_VERIFIED); };
             for (size_t i = 0; i < t;) {
-                if (!pr[i]) {
+                if (!up(i)) {
                     ++i;
                     continue;
                 }
                 size_t j = i;
-                while (j < t && pr[j]) ++j;
+                while (j < t && up(j)) ++j;
                 const uint8_t* src = chunks + (k * t + i) * L;
                 uint8_t* dst = s.d_buf + (k * t + i) * cs;
                 if (cs == L)
@@ -632,8 +808,9 @@ int cec_read_pipeline_new_ex(const cec_codec* codec, size_t chunk_len, size_t pa
                              size_t depth, unsigned flags, cec_read_pipeline** out) {
     if (!codec || !out || chunk_len == 0 || parts_per_batch == 0 || depth == 0 || depth > 16 ||
         (flags & ~unsigned(CEC_READ_REBUILT_ONLY | CEC_PIPE_EXTERNAL | CEC_READ_RESILVER |
-                           CEC_READ_VERIFY_ONLY)) ||
-        ((flags & CEC_READ_RESILVER) && (flags & CEC_READ_VERIFY_ONLY)))
+                           CEC_READ_VERIFY_ONLY | CEC_READ_CARRY)) ||
+        ((flags & CEC_READ_RESILVER) && (flags & CEC_READ_VERIFY_ONLY)) ||
+        ((flags & CEC_READ_CARRY) && (flags & (CEC_READ_RESILVER | CEC_READ_VERIFY_ONLY))))
         return CEC_ERR_INVALID_ARGUMENT;
     *out = nullptr;
     if (cec_device_count() <= 0) return CEC_ERR_NO_DEVICE;
@@ -650,6 +827,8 @@ int cec_read_pipeline_new_ex(const cec_codec* codec, size_t chunk_len, size_t pa
     pl->external = (flags & CEC_PIPE_EXTERNAL) != 0;
     pl->resilver = (flags & CEC_READ_RESILVER) != 0;
     pl->verify_only = (flags & CEC_READ_VERIFY_ONLY) != 0;
+    pl->carry = (flags & CEC_READ_CARRY) != 0;
+    pl->carry_cap = pl->carry ? parts_per_batch : 0;  // a batch's worth of parts to retry
     pl->side_decode = cec::knobs().read_side;
     pl->shared_upload = cec::knobs().read_upstream;
     pl->slots.resize(depth);
@@ -675,7 +854,7 @@ int cec_read_pipeline_new_ex(const cec_codec* codec, size_t chunk_len, size_t pa
         dev(&s.d_buf, P * t * pl->cs);
         dev(&s.d_expected, P * t * 32);
         dev(&s.d_flags, 2 * P * t);
-        if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
+        if (e == hipSuccess) e = slot_stream(&s.stream, pl->device);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
         s.h_status = new int[P];
         if (e != hipSuccess) {
@@ -683,6 +862,14 @@ int cec_read_pipeline_new_ex(const cec_codec* codec, size_t chunk_len, size_t pa
             return pipe_fail(e, "cec_read_pipeline_new allocation");
         }
         std::memset(s.h_present, 0, P * t);
+    }
+    if (pl->carry) {
+        const hipError_t e = pl->make_carry_pool();
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            delete pl;
+            return pipe_fail(e, "cec_read_pipeline_new carry pool");
+        }
     }
     *out = pl;
     return CEC_OK;
@@ -808,10 +995,44 @@ int cec_read_pipeline_wait(cec_read_pipeline* pl, size_t slot, const uint8_t** d
             }
             PIPE_TRY(hipStreamSynchronize(s.stream));
         }
+        // CEC_READ_CARRY: keep the verified chunks of every part that still lacks d of them in
+        // the carry pool, so its retry need not upload them again
+        if (pl->carry) {
+            DeviceGuard guard(pl->device);
+            PIPE_TRY(guard.status());
+            s.carry_ids.assign(n, -1);
+            std::vector<std::pair<uint32_t, uint32_t>> pairs;
+            std::vector<int32_t> used;
+            for (size_t k = 0; k < n; ++k) {
+                if (s.h_status[k] != CEC_TOO_FEW_SHARDS_PRESENT) continue;
+                const uint8_t* ok = s.h_ok + k * t;
+                if (std::none_of(ok, ok + t, [](uint8_t f) { return f != 0; })) continue;
+                const int32_t id = pl->carry_take();
+                if (id < 0) continue;  // pool full: the caller sends the chunks again
+                PIPE_TRY(hipStreamWaitEvent(s.stream, pl->carry_ready[size_t(id)], 0));
+                for (size_t i = 0; i < t; ++i)
+                    if (ok[i]) pairs.emplace_back(uint32_t(k * t + i), uint32_t(size_t(id) * t + i));
+                s.carry_ids[k] = id;
+                used.push_back(id);
+            }
+            const bool any = !used.empty();
+            if (any) {
+                const int cst = pl->ensure_carry_ids(s);
+                if (cst != CEC_OK) return cst;
+                const int mst = pl->carry_move(s, pairs, 0, false, s.stream);
+                if (mst != CEC_OK) return mst;
+                for (int32_t id : used) PIPE_TRY(hipEventRecord(pl->carry_ready[size_t(id)], s.stream));
+                if (!s.stashed)
+                    PIPE_TRY(hipEventCreateWithFlags(&s.stashed, hipEventDisableTiming));
+                PIPE_TRY(hipEventRecord(s.stashed, s.stream));
+                s.stash_pending = true;
+            }
+        }
         // Where each data chunk is: re-decoded parts and (without REBUILT_ONLY) every part in the
         // data output; otherwise a loaded chunk stays in the chunk buffer it was read from (it
         // verified: parts with a failed chunk were re-decoded) and a rebuilt one came back into
-        // the data output.
+        // the data output -- as did a carried part's verified data chunks (the caller's buffer
+        // does not hold them).
         std::vector<uint8_t> redone(n, 0);
         for (size_t k : redo) redone[k] = 1;
         if (pl->resilver) {  // [parts][t]: verified chunks where they were read, others rebuilt
@@ -825,7 +1046,10 @@ int cec_read_pipeline_wait(cec_read_pipeline* pl, size_t slot, const uint8_t** d
             s.data_ptrs.resize(n * d);
             for (size_t k = 0; k < n; ++k)
                 for (size_t j = 0; j < d; ++j) {
-                    const bool in_place = pl->rebuilt_only && !redone[k] && s.h_present[k * t + j];
+                    const uint8_t f = s.h_present[k * t + j];
+                    const bool from_pool = !s.carried.empty() && s.carried[k] &&
+                                           f == CEC_PRESENT_VERIFIED;
+                    const bool in_place = pl->rebuilt_only && !redone[k] && f && !from_pool;
                     s.data_ptrs[k * d + j] = in_place ? s.src_chunks + s.src_off[k * t + j]
                                                       : s.dst_data + (k * d + j) * pl->L;
                 }
@@ -847,6 +1071,32 @@ int cec_read_pipeline_data_chunks(cec_read_pipeline* pl, size_t slot, const uint
         if (st != CEC_OK) return st;
     }
     std::copy(s.data_ptrs.begin(), s.data_ptrs.end(), ptrs);
+    return CEC_OK;
+}
+
+int cec_read_pipeline_carry_ids(cec_read_pipeline* pl, size_t slot, int32_t* ids) {
+    if (!pl || slot >= pl->slots.size() || !ids || !pl->carry) return CEC_ERR_INVALID_ARGUMENT;
+    ReadSlot& s = pl->slots[slot];
+    if (s.in_flight || !s.checked) {
+        const int st = cec_read_pipeline_wait(pl, slot, nullptr, nullptr, nullptr, nullptr);
+        if (st != CEC_OK) return st;
+    }
+    for (size_t k = 0; k < s.n_parts; ++k) ids[k] = k < s.carry_ids.size() ? s.carry_ids[k] : -1;
+    return CEC_OK;
+}
+
+int cec_read_pipeline_submit_carried(cec_read_pipeline* pl, size_t slot, size_t n_parts,
+                                     const int32_t* carry_ids) {
+    if (!pl || slot >= pl->slots.size() || n_parts == 0 || n_parts > pl->parts || pl->external ||
+        !carry_ids)
+        return CEC_ERR_INVALID_ARGUMENT;
+    ReadSlot& s = pl->slots[slot];
+    return pl->submit(s, s.h_chunks, n_parts, s.h_data, false, carry_ids);
+}
+
+int cec_read_pipeline_carry_release(cec_read_pipeline* pl, int32_t id) {
+    if (!pl || !pl->carry_valid(id)) return CEC_ERR_INVALID_ARGUMENT;
+    pl->carry_give_back(id);
     return CEC_OK;
 }
 

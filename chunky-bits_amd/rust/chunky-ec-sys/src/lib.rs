@@ -44,6 +44,8 @@ pub mod sys {
     pub const CEC_PIPE_EXTERNAL: std::os::raw::c_uint = 2;
     /// Present-flag value of a read retry: loaded and already verified (not hashed again).
     pub const CEC_PRESENT_VERIFIED: u8 = 0x80;
+    /// Read-pipeline flag: keep retries' verified chunks on the device (carry pool).
+    pub const CEC_READ_CARRY: std::os::raw::c_uint = 16;
 
     #[repr(C)]
     #[derive(Clone, Copy, Debug)]
@@ -271,6 +273,18 @@ pub mod sys {
             data_out: *mut u8,
         ) -> c_int;
         pub fn cec_read_pipeline_query(pipeline: *mut cec_read_pipeline, slot: usize) -> c_int;
+        pub fn cec_read_pipeline_carry_ids(
+            pipeline: *mut cec_read_pipeline,
+            slot: usize,
+            ids: *mut i32,
+        ) -> c_int;
+        pub fn cec_read_pipeline_submit_carried(
+            pipeline: *mut cec_read_pipeline,
+            slot: usize,
+            n_parts: usize,
+            carry_ids: *const i32,
+        ) -> c_int;
+        pub fn cec_read_pipeline_carry_release(pipeline: *mut cec_read_pipeline, id: i32) -> c_int;
         pub fn cec_multi_new(
             codec: *const cec_codec,
             chunk_len: usize,

@@ -345,6 +345,27 @@ int cec_read_pipeline_new_ex(const cec_codec* codec, size_t chunk_len, size_t pa
  * hashed and compared with its metadata digest; nothing is decoded or copied back (wait gives
  * the verified flags; part_status is CEC_OK; data_out may be NULL). */
 #define CEC_READ_VERIFY_ONLY 8u
+/* Read-pipeline flag (read mode only): keep retries' verified chunks on the device.  The
+ * reference keeps a chunk that verified in memory while it draws another for the one that failed
+ * (file_part.rs:92-107); without this flag the retry of a part sends its verified chunks up
+ * again (CEC_PRESENT_VERIFIED).  With it, wait copies the verified chunks of every part it
+ * reports CEC_TOO_FEW_SHARDS_PRESENT into a device carry pool (parts_per_batch entries of
+ * (d+p) chunks, made with the pipeline);
+ * cec_read_pipeline_carry_ids gives each such part its entry (-1: none kept, pool full).  The
+ * retry passes the ids to cec_read_pipeline_submit_carried: a part with an id takes its
+ * CEC_PRESENT_VERIFIED chunks from the pool (the caller need not fill them in the slot) and its
+ * data chunks among them come back like rebuilt ones (REBUILT_ONLY data_chunks point at the
+ * data output for them).  An id is used once; one the caller will not use (an undecodable part)
+ * goes back with cec_read_pipeline_carry_release. */
+#define CEC_READ_CARRY 16u
+/* After wait: ids[k] = the carry entry of part k of the slot's batch, or -1. */
+int cec_read_pipeline_carry_ids(cec_read_pipeline* pipeline, size_t slot, int32_t* ids);
+/* As cec_read_pipeline_submit, with carry_ids[n_parts] (-1 = none) for the parts whose verified
+ * chunks come from the carry pool. */
+int cec_read_pipeline_submit_carried(cec_read_pipeline* pipeline, size_t slot, size_t n_parts,
+                                     const int32_t* carry_ids);
+/* Hands an unused carry entry back. */
+int cec_read_pipeline_carry_release(cec_read_pipeline* pipeline, int32_t id);
 /* After (or instead of) wait: ptrs[k*d + j] = the chunk_len bytes of data chunk j of part k —
  * in the slot's chunk buffer (loaded and verified, REBUILT_ONLY) or in its data buffer
  * (rebuilt, re-decoded, or without REBUILT_ONLY).  Valid until the slot is acquired again;

@@ -138,11 +138,13 @@ def test_argument_errors_precede_device_use():
 
 
 def test_read_pipeline_argument_checks_precede_device_use():
-    """cec_read_pipeline_new_ex rejects unknown flags and bad shapes before any HIP call; without
-    a device a valid request reports NoDevice (no host-side fallback pipeline)."""
+    """cec_read_pipeline_new_ex rejects unknown flags, exclusive modes (RESILVER with
+    VERIFY_ONLY; CARRY with either) and bad shapes before any HIP call; without a device a valid
+    request reports NoDevice (no host-side fallback pipeline)."""
     import chunky_ec as ce
     rs = ce.ReedSolomon(10, 4)
-    for args in [(1 << 20, 4, 2, 16), (1 << 20, 4, 2, 12), (0, 4, 2, 0), (1 << 20, 0, 2, 0),
+    for args in [(1 << 20, 4, 2, 32), (1 << 20, 4, 2, 12), (1 << 20, 4, 2, 16 | 4),
+                 (1 << 20, 4, 2, 16 | 8), (0, 4, 2, 0), (1 << 20, 0, 2, 0),
                  (1 << 20, 4, 0, 0),
                  (1 << 20, 4, 17, 0)]:
         with pytest.raises(ce.Error) as e:
@@ -151,6 +153,9 @@ def test_read_pipeline_argument_checks_precede_device_use():
     if ce.device_count() == 0:
         with pytest.raises(ce.Error) as e:
             ce.ReadPipeline(rs, 1 << 20, 4, 2, ce.ReadPipeline.REBUILT_ONLY)
+        assert e.value.code == ce.ERR_NO_DEVICE
+        with pytest.raises(ce.Error) as e:
+            ce.ReadPipeline(rs, 1 << 20, 4, 2, ce.ReadPipeline.REBUILT_ONLY | ce.ReadPipeline.CARRY)
         assert e.value.code == ce.ERR_NO_DEVICE
 
 

@@ -37,18 +37,25 @@ def _store(n, d, p, L, seed):
     return chunks, dig
 
 
+@pytest.mark.parametrize("carry", [False, True])
 @pytest.mark.parametrize("d,p,L,corrupt", [(10, 4, 4096, 0.05), (3, 2, 1000, 0.2),
                                            (20, 8, 777, 0.03)])
-def test_read_repair_stream_on_the_pipeline(d, p, L, corrupt):
+def test_read_repair_stream_on_the_pipeline(d, p, L, corrupt, carry):
+    """carry: CEC_READ_CARRY -- a retried part's verified chunks come from the device carry pool
+    (the slot's bytes for them are overwritten with garbage here, so a path that uploaded them
+    anyway, or read them back from the slot, would decode wrong), its data chunks among them
+    come back like rebuilt ones; odd L (1000, 777) takes the pitched copies."""
     n, P, depth = 61, 8, 3
     chunks, dig = _store(n, d, p, L, d * 100 + p)
     codec = ce.ReedSolomon(d, p)
-    rp = ce.ReadPipeline(codec, L, P, depth, ce.ReadPipeline.REBUILT_ONLY)
+    flags_ = ce.ReadPipeline.REBUILT_ONLY | (ce.ReadPipeline.CARRY if carry else 0)
+    rp = ce.ReadPipeline(codec, L, P, depth, flags_)
     rng = np.random.default_rng(5)
     damaged = [0]
 
     def fetch(slot_chunks, rows):
         for k, part, flags in rows:
+            slot_chunks[k] = 0x3C  # nothing the reader did not fetch may be trusted
             for j in np.flatnonzero(flags):
                 slot_chunks[k, j] = chunks[part, j]
                 if flags[j] == 1 and rng.random() < corrupt:
@@ -63,16 +70,19 @@ def test_read_repair_stream_on_the_pipeline(d, p, L, corrupt):
     s = ReadRepairStream(rp, fetch, lambda ids: dig[ids], seed=1, on_part=on_part).run(0, n)
     assert s.parts + s.undecodable_parts == n
     assert s.rejected_chunks == damaged[0] > 0 and s.retried_parts > 0
+    assert (s.carried_chunks > 0) == carry
     for part, (out, _) in got.items():
         assert out == chunks[part, :d].tobytes(), part
     assert any(a > 1 for _, a in got.values())
     assert set(got) | set(s.undecodable) == set(range(n))
 
 
-def test_read_repair_stream_runs_out_of_chunks_on_the_pipeline():
+@pytest.mark.parametrize("carry", [False, True])
+def test_read_repair_stream_runs_out_of_chunks_on_the_pipeline(carry):
     d, p, L, n = 3, 2, 512, 10
     chunks, dig = _store(n, d, p, L, 4)
-    rp = ce.ReadPipeline(ce.ReedSolomon(d, p), L, 4, 2, ce.ReadPipeline.REBUILT_ONLY)
+    rp = ce.ReadPipeline(ce.ReedSolomon(d, p), L, 4, 2, ce.ReadPipeline.REBUILT_ONLY |
+                         (ce.ReadPipeline.CARRY if carry else 0))
 
     def fetch(slot_chunks, rows):
         for k, part, flags in rows:
@@ -85,6 +95,44 @@ def test_read_repair_stream_runs_out_of_chunks_on_the_pipeline():
 
     s = ReadRepairStream(rp, fetch, lambda ids: dig[ids], seed=0).run(0, n)
     assert s.undecodable == [3] and s.parts == n - 1
+
+
+def test_carry_ids_contract():
+    """CEC_READ_CARRY's API: ids only for parts reported TooFewShardsPresent with a verified chunk;
+    an id is used once (a second use or a released id is refused before anything is queued)."""
+    d, p, L = 3, 2, 256
+    chunks, dig = _store(2, d, p, L, 8)
+    rp = ce.ReadPipeline(ce.ReedSolomon(d, p), L, 2, 2, ce.ReadPipeline.REBUILT_ONLY |
+                         ce.ReadPipeline.CARRY)
+    slot, ch, pres, exp = rp.acquire()
+    pres[:2] = 0
+    pres[0, :3] = 1          # part 0: chunks 0-2, chunk 2 damaged -> TooFew, 2 verified kept
+    pres[1, [0, 1, 3]] = 1   # part 1: decodes
+    ch[:2] = chunks[:2]
+    ch[0, 2, 5] ^= 1
+    exp[:2] = dig[:2]
+    rp.submit(slot, 2)
+    _, ver, st = rp.wait(slot)
+    assert list(st) == [ce.TOO_FEW_SHARDS_PRESENT, ce.OK]
+    ids = rp.carry_ids(slot, 2)
+    assert ids[0] >= 0 and ids[1] == -1
+    # the retry: chunks 0-1 from the pool (slot bytes garbage), chunk 3 fetched
+    slot, ch, pres, exp = rp.acquire()
+    pres[:1] = 0
+    pres[0, :2] = ce.PRESENT_VERIFIED
+    pres[0, 3] = 1
+    ch[0] = 0x77
+    ch[0, 3] = chunks[0, 3]
+    exp[:1] = dig[:1]
+    rp.submit_carried(slot, 1, ids[:1])
+    _, ver, st = rp.wait(slot)
+    assert list(st) == [ce.OK] and list(ver[0]) == [1, 1, 0, 1, 0]
+    assert rp.part_bytes(slot, 1, 0) == chunks[0, :d].tobytes()
+    slot, ch, pres, exp = rp.acquire()
+    with pytest.raises(ce.Error):  # used once
+        rp.submit_carried(slot, 1, ids[:1])
+    with pytest.raises(ce.Error):
+        rp.carry_release(int(ids[0]))
 
 
 def test_bench_timed_read_repair_small():

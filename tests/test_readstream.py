@@ -169,3 +169,93 @@ def test_read_repair_stream_status_other_than_too_few_raises():
     with pytest.raises(chunky_ec.Error):
         ReadRepairStream(fp, fetch, lambda ids: dig[ids]).run(0, 3)
     assert OK == 0
+
+
+class FakeCarryPipeline(FakeReadPipeline):
+    """cec_read_pipeline with CEC_READ_CARRY: wait keeps the verified chunks of every part it
+    reports TooFewShardsPresent in a pool of 2 x parts entries (-1 when full); submit_carried takes
+    a carried part's CEC_PRESENT_VERIFIED chunks from the pool, whatever the slot holds there."""
+    carry = True
+
+    def __init__(self, *a, cap=None):
+        super().__init__(*a)
+        self.cap = 2 * self.parts if cap is None else cap
+        self.pool = {}       # id -> [t][L] chunks
+        self.free = list(range(self.cap))
+        self.ids = {}        # slot -> ids of its last batch
+        self.released = []
+
+    def submit(self, slot, n):
+        self._carried = None
+        super().submit(slot, n)
+        self._keep(slot, n)
+
+    def submit_carried(self, slot, n, ids):
+        s = self.slots[slot]
+        for k in range(n):
+            if ids[k] >= 0:
+                assert ids[k] in self.pool, "carry id not held"
+                vpos = s["present"][k] == PRESENT_VERIFIED
+                s["chunks"][k, vpos] = 0xEE  # whatever the caller left there is not used...
+                s["chunks"][k, vpos] = self.pool.pop(int(ids[k]))[vpos]  # ...the pool's bytes are
+                self.free.append(int(ids[k]))
+        super().submit(slot, n)
+        self._keep(slot, n)
+
+    def _keep(self, slot, n):
+        s = self.slots[slot]
+        _, ver, st = s["res"]
+        ids = np.full(n, -1, np.int32)
+        for k in range(n):
+            if st[k] == TOO_FEW_SHARDS_PRESENT and ver[k].any() and self.free:
+                e = self.free.pop()
+                self.pool[e] = np.where(ver[k][:, None] != 0, s["chunks"][k], 0)
+                ids[k] = e
+        self.ids[slot] = ids
+
+    def carry_ids(self, slot, n):
+        return self.ids[slot][:n]
+
+    def carry_release(self, e):
+        self.released.append(e)
+        self.pool.pop(e)
+        self.free.append(e)
+
+
+@pytest.mark.parametrize("cap", [None, 1])
+def test_read_repair_stream_carries_verified_chunks(cap):
+    """CARRY: a retried part's verified chunks come from the device pool, so the reader fetches
+    only the new chunks; the parts decode exactly as without carry, and an undecodable part's
+    entry is released.  cap=1: the pool fills, and parts without an entry are re-sent as before."""
+    d, p, L, P, depth, n = 4, 3, 96, 5, 3, 41
+    chunks, dig = _store(n, d, p, L, 9)
+    rng = np.random.default_rng(5)
+    fetched = []
+
+    def fetch(slot_chunks, rows):
+        for k, part, flags in rows:
+            fetched.append((part, flags.copy()))
+            for j in np.flatnonzero(flags):
+                slot_chunks[k, j] = chunks[part, j]
+                if flags[j] == 1 and (rng.random() < 0.2 or part == 7):  # part 7: never decodes
+                    slot_chunks[k, j, rng.integers(L)] ^= 0x5A
+
+    fp = FakeCarryPipeline(d, p, L, P, depth, cap=cap)
+    got = {}
+    s = ReadRepairStream(fp, fetch, lambda ids: dig[ids], seed=4,
+                         on_part=lambda slot, nb, k, part, tries: got.__setitem__(
+                             part, fp.slots[slot]["res"][0][k].copy())).run(0, n)
+    assert s.parts + s.undecodable_parts == n and 7 in s.undecodable
+    for part, out in got.items():
+        assert np.array_equal(out, chunks[part, :d]), part
+    assert s.carried_chunks > 0
+    if cap is None:
+        # nothing verified is fetched twice: every fetch of a part is of chunks not fetched before
+        seen = {}
+        for part, flags in fetched:
+            new = set(np.flatnonzero(flags))
+            assert not new & seen.get(part, set()), part
+            assert PRESENT_VERIFIED not in flags
+            seen.setdefault(part, set()).update(new)
+    assert not fp.pool or fp.released  # entries are used or released, never left behind
+    assert sorted(fp.free) == list(range(fp.cap))

@@ -15,7 +15,7 @@ RUST = os.path.join(ROOT, "chunky-bits_amd", "rust", "chunky-ec-sys", "src", "li
 
 # C base type -> canonical name shared with Rust
 C_BASE = {"size_t": "usize", "int": "c_int", "unsigned": "c_uint", "unsigned int": "c_uint",
-          "uint64_t": "u64", "uint8_t": "u8", "char": "c_char", "void": "c_void",
+          "uint64_t": "u64", "uint8_t": "u8", "int32_t": "i32", "char": "c_char", "void": "c_void",
           "cec_codec": "cec_codec", "cec_pipeline": "cec_pipeline",
           "cec_read_pipeline": "cec_read_pipeline", "cec_multi": "cec_multi",
           "cec_part_batch": "cec_part_batch"}
@@ -113,7 +113,8 @@ def test_part_batch_layout_and_constants_match():
           for f in rfields.split(",") if ":" in f]
     assert [(t, n) for t, n in cf] == [(t, n) for t, n in rf]
     for const in ("CEC_ABI_VERSION", "CEC_READ_REBUILT_ONLY", "CEC_PIPE_EXTERNAL",
-                  "CEC_PRESENT_VERIFIED", "CEC_READ_RESILVER", "CEC_READ_VERIFY_ONLY"):
+                  "CEC_PRESENT_VERIFIED", "CEC_READ_RESILVER", "CEC_READ_VERIFY_ONLY",
+                  "CEC_READ_CARRY"):
         cv = re.search(rf"#define {const}\s+(0x[0-9a-fA-F]+|\d+)u?", hsrc).group(1)
         rv = re.search(rf"pub const {const}:[^=]+=\s*(0x[0-9a-fA-F]+|\d+);", rsrc).group(1)
         assert int(cv, 0) == int(rv, 0), const
