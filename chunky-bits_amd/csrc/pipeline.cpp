@@ -68,7 +68,9 @@ class DeviceGuard {
 // of the other's batch (measured: the first 4-deep read pipeline of a process had slots 2 and 3
 // on one queue and ran 24% slower than the second).  A CU-masked stream gets a hardware queue of
 // its own; the mask names every CU, so the kernels see the whole GPU (CEC_SLOT_QUEUES=0: plain
-// streams).
+// streams).  HIP makes such a stream without flags, i.e. blocking: work the process puts on the
+// null stream (a synchronous hipMemcpy, torch's default stream) orders against the slots'
+// in-flight batches, which costs time while both run but never changes a result.
 hipError_t slot_stream(hipStream_t* stream, int device) {
     if (!cec::knobs().slot_queues) return hipStreamCreateWithFlags(stream, hipStreamNonBlocking);
     int cus = 0;
