@@ -127,6 +127,29 @@ struct MoveParams {
 };
 hipError_t launch_move_chunks(const MoveParams& a, hipStream_t s);
 
+// CEC_READ_CARRY's stash, queued in the batch's own stream after the verification: every part
+// with 0 < verified chunks < d (the parts wait() will report CEC_TOO_FEW_SHARDS_PRESENT) gets the
+// next of the `n_reserved` pool entries the host reserved for this batch, in part order, and its
+// verified chunks (present == CEC_PRESENT_VERIFIED, or loaded and ok) are copied to
+// pool + (entry * t + i) * len.  map[k] = the entry of part k, or -1 (none needed, or the
+// reservation ran out).
+struct CarryStashParams {
+    const uint8_t* batch;
+    uint64_t part_stride;
+    uint64_t chunk_stride;
+    uint32_t t;
+    uint32_t d;
+    uint32_t n_parts;
+    uint8_t* pool;
+    uint64_t len;             // bytes per chunk copied (the pool's chunk stride)
+    const uint8_t* present;   // device [n_parts][t]: the caller's loaded flags
+    const uint8_t* ok;        // device [n_parts][t]: verification of the freshly loaded chunks
+    const uint32_t* reserved;
+    uint32_t n_reserved;
+    int32_t* map;             // device [n_parts]
+};
+hipError_t launch_carry_stash(const CarryStashParams& a, hipStream_t s);
+
 // Host mirror of the device generator (cec_synth_byte).
 uint8_t synth_byte(uint64_t seed, uint64_t part, uint64_t chunk, uint64_t offset);
 

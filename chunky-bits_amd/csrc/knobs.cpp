@@ -73,7 +73,7 @@ Knobs* parse() {
     k->read_upstream = on("CEC_READ_UPSTREAM");
     k->multi_copy_threads = unsigned(
         std::min<unsigned long long>(std::max(number("CEC_MULTI_COPY_THREADS", 4), 1ull), 32ull));
-    k->slot_queues = flag("CEC_SLOT_QUEUES", true);
+    k->slot_queues = on("CEC_SLOT_QUEUES");
     return k;
 }
 

@@ -53,7 +53,7 @@ struct Knobs {
     bool read_side = false;              // CEC_READ_SIDE
     bool read_upstream = false;          // CEC_READ_UPSTREAM
     unsigned multi_copy_threads = 4;     // CEC_MULTI_COPY_THREADS (1..32)
-    bool slot_queues = true;             // CEC_SLOT_QUEUES: a hardware queue per pipeline slot
+    bool slot_queues = false;            // CEC_SLOT_QUEUES: a hardware queue per pipeline slot
 };
 
 // The current snapshot (parsed on first call).

@@ -66,11 +66,13 @@ class DeviceGuard {
 // process, the null stream included, so `depth` slot streams made with hipStreamCreate can land
 // two slots on one queue: the later slot's next batch then waits in that queue behind the whole
 // of the other's batch (measured: the first 4-deep read pipeline of a process had slots 2 and 3
-// on one queue and ran 24% slower than the second).  A CU-masked stream gets a hardware queue of
-// its own; the mask names every CU, so the kernels see the whole GPU (CEC_SLOT_QUEUES=0: plain
-// streams).  HIP makes such a stream without flags, i.e. blocking: work the process puts on the
-// null stream (a synchronous hipMemcpy, torch's default stream) orders against the slots'
-// in-flight batches, which costs time while both run but never changes a result.
+// on one queue; with CEC_READ_CARRY that pipeline ran 24% slower than the second).  A CU-masked
+// stream gets a hardware queue of its own (the mask names every CU, so the kernels see the whole
+// GPU), but making one while other queues of the process are busy deadlocked inside the HIP
+// runtime (a scheduler worker blocked in hipExtStreamCreateWithCUMask on a lock the runtime's
+// event thread held, profiles/r5_queues/), so plain streams stay the default and CU-masked ones
+// are the CEC_SLOT_QUEUES=1 A/B only.  HIP makes them blocking (no flags argument): null-stream
+// work would order against the slots' batches.
 hipError_t slot_stream(hipStream_t* stream, int device) {
     if (!cec::knobs().slot_queues) return hipStreamCreateWithFlags(stream, hipStreamNonBlocking);
     int cus = 0;
@@ -341,16 +343,20 @@ struct ReadSlot {
     std::vector<const uint8_t*> data_ptrs;  // [parts][d]: where each data chunk is (after wait)
     std::vector<size_t> src_off;  // [parts][t]: byte offset of a loaded chunk in src_chunks
     // CEC_READ_CARRY: per part of this batch, the carry entry its verified chunks were kept in
-    // at wait (-1: none), and whether its CEC_PRESENT_VERIFIED chunks came from the carry pool at
-    // submit (not from the caller's buffer: they are copied back like rebuilt ones)
+    // (-1: none), and whether its CEC_PRESENT_VERIFIED chunks came from the carry pool at submit
+    // (not from the caller's buffer: they are copied back like rebuilt ones)
     std::vector<int32_t> carry_ids;
     std::vector<uint8_t> carried;
-    hipEvent_t stashed = nullptr;  // after the last stash out of d_buf
-    bool stash_pending = false;    // the next upload into d_buf must wait for `stashed`
-    // the move kernel's index lists: [0, 2*parts*t) the stash's (batch positions, then pool
-    // positions), [2*parts*t, 4*parts*t) the consume's; pinned, then uploaded
+    std::vector<int32_t> reserved;  // pool entries this batch's stash may fill
+    // made with the pipeline: the consume's index lists ([0, parts*t) batch positions, then
+    // pool positions), the reserved entries, the stash's part -> entry map, the loaded flags
     uint32_t* h_cids = nullptr;
     uint32_t* d_cids = nullptr;
+    uint32_t* h_res = nullptr;
+    uint32_t* d_res = nullptr;
+    int32_t* h_map = nullptr;
+    int32_t* d_map = nullptr;
+    uint8_t* d_present = nullptr;
 };
 
 }  // namespace
@@ -382,9 +388,16 @@ struct cec_read_pipeline {
     // pipeline: a fresh multi-GiB allocation is cleared by the driver in the background, which
     // would compete with the uploads if it were made mid-stream) holding the verified chunks of
     // parts reported CEC_TOO_FEW_SHARDS_PRESENT until their retry takes them (or the caller
-    // releases them); per entry an event after its last stash or consumption, so reusing an entry
-    // waits for its previous copies.
+    // releases them).  Each batch reserves up to `carry_batch` free entries at submit and its
+    // stash kernels fill them in the batch's own stream, right after the verification: the stash
+    // needs no host round trip, and nothing the next uploads depend on is queued behind another
+    // slot's batch (slot streams can share a hardware queue, where a kernel waits for every
+    // packet queued before it).  Per entry an event after its last stash or consumption, so
+    // reusing an entry waits for its previous copies.  carry_used: kFree, kHeld (a carry id the
+    // caller has), kReserved (by an in-flight batch).
+    static constexpr uint8_t kFree = 0, kHeld = 1, kReserved = 2;
     bool carry = false;
+    size_t carry_batch = 0;
     size_t carry_cap = 0;
     uint8_t* d_carry = nullptr;
     std::vector<hipEvent_t> carry_ready;
@@ -399,16 +412,19 @@ struct cec_read_pipeline {
         for (ReadSlot& s : slots) {
             if (s.stream) (void)hipStreamSynchronize(s.stream);
             if (s.side) (void)hipStreamSynchronize(s.side);
-            for (hipEvent_t ev : {s.done, s.fork, s.join, s.uploaded, s.stashed})
+            for (hipEvent_t ev : {s.done, s.fork, s.join, s.uploaded})
                 if (ev) (void)hipEventDestroy(ev);
             if (s.stream) (void)hipStreamDestroy(s.stream);
             if (s.side) (void)hipStreamDestroy(s.side);
             for (void* dptr : {static_cast<void*>(s.d_buf), static_cast<void*>(s.d_expected),
                                static_cast<void*>(s.d_flags), static_cast<void*>(s.d_pack),
-                               static_cast<void*>(s.d_ids), static_cast<void*>(s.d_cids)})
+                               static_cast<void*>(s.d_ids), static_cast<void*>(s.d_cids),
+                               static_cast<void*>(s.d_res), static_cast<void*>(s.d_map),
+                               static_cast<void*>(s.d_present)})
                 if (dptr) (void)hipFree(dptr);
-            if (s.h_ids) (void)hipHostFree(s.h_ids);
-            if (s.h_cids) (void)hipHostFree(s.h_cids);
+            for (void* hptr : {static_cast<void*>(s.h_ids), static_cast<void*>(s.h_cids),
+                               static_cast<void*>(s.h_res), static_cast<void*>(s.h_map)})
+                if (hptr) (void)hipHostFree(hptr);
             for (uint8_t* hptr : {s.h_chunks, s.h_present, s.h_expected, s.h_data, s.h_ok, s.h_hash})
                 if (hptr) (void)hipHostFree(hptr);
             delete[] s.h_status;
@@ -420,7 +436,7 @@ struct cec_read_pipeline {
         (void)hipSetDevice(cur);
     }
 
-    // The carry pool and its events (at creation).
+    // The carry pool, its events and every slot's carry buffers (at creation).
     hipError_t make_carry_pool() {
         hipError_t e = hipMalloc(reinterpret_cast<void**>(&d_carry), carry_cap * t * cs);
         if (e != hipSuccess) {
@@ -435,60 +451,85 @@ struct cec_read_pipeline {
             e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
             if (e != hipSuccess) return e;
         }
-        carry_used.assign(carry_cap, 0);
+        carry_used.assign(carry_cap, kFree);
         carry_free.clear();
         for (size_t i = 0; i < carry_cap; ++i) carry_free.push_back(int32_t(i));
-        return hipSuccess;
+        for (ReadSlot& s : slots) {
+            auto dev = [&](void** ptr, size_t bytes) {
+                if (e == hipSuccess) e = hipMalloc(ptr, bytes);
+            };
+            auto host = [&](void** ptr, size_t bytes) {
+                if (e == hipSuccess) e = cec::host_malloc_near(ptr, bytes, hipHostMallocDefault, device);
+            };
+            dev(reinterpret_cast<void**>(&s.d_cids), 2 * parts * t * sizeof(uint32_t));
+            host(reinterpret_cast<void**>(&s.h_cids), 2 * parts * t * sizeof(uint32_t));
+            dev(reinterpret_cast<void**>(&s.d_res), carry_batch * sizeof(uint32_t));
+            host(reinterpret_cast<void**>(&s.h_res), carry_batch * sizeof(uint32_t));
+            dev(reinterpret_cast<void**>(&s.d_map), parts * sizeof(int32_t));
+            host(reinterpret_cast<void**>(&s.h_map), parts * sizeof(int32_t));
+            dev(reinterpret_cast<void**>(&s.d_present), parts * t);
+        }
+        return e;
     }
 
-    // A free carry entry (-1 when the pool is full).
-    int32_t carry_take() {
-        while (!carry_free.empty()) {  // the entry freed longest ago first (FIFO)
-            const int32_t id = carry_free.front();
-            carry_free.pop_front();
-            carry_used[size_t(id)] = 1;
-            return id;
-        }
-        return -1;
+    // Entries of a slot's batch that its stash did not fill (or that were never mapped because
+    // the slot was not waited for) go back to the free list.
+    void carry_unreserve(ReadSlot& s) {
+        for (int32_t id : s.reserved)
+            if (carry_used[size_t(id)] == kReserved) carry_give_back(id);
+        s.reserved.clear();
     }
     void carry_give_back(int32_t id) {
-        carry_used[size_t(id)] = 0;
+        carry_used[size_t(id)] = kFree;
         carry_free.push_back(id);
     }
-    bool carry_valid(int32_t id) const {
-        return id >= 0 && size_t(id) < carry_used.size() && carry_used[size_t(id)];
+    bool carry_valid(int32_t id) const {  // a carry id the caller holds
+        return id >= 0 && size_t(id) < carry_used.size() && carry_used[size_t(id)] == kHeld;
     }
-    // The slot's carry index lists (made on first use).
-    int ensure_carry_ids(ReadSlot& s) const {
-        const size_t n = 4 * parts * t;
-        hipError_t e = hipSuccess;
-        if (!s.d_cids) e = hipMalloc(reinterpret_cast<void**>(&s.d_cids), n * sizeof(uint32_t));
-        if (e == hipSuccess && !s.h_cids)
-            e = cec::host_malloc_near(reinterpret_cast<void**>(&s.h_cids), n * sizeof(uint32_t),
-                                      hipHostMallocDefault, device);
-        if (e != hipSuccess) {
-            (void)hipGetLastError();
-            return pipe_fail(e, "read pipeline carry index lists");
-        }
-        return CEC_OK;
-    }
-    // Moves chunks between d_buf and the pool with one kernel: pairs[j] = (batch position, pool
-    // position), written into the slot's index list at `region` (0: stash, 1: consume), uploaded
-    // on `stream`, then moved (to_batch: pool -> d_buf).
-    int carry_move(ReadSlot& s, const std::vector<std::pair<uint32_t, uint32_t>>& pairs,
-                   size_t region, bool to_batch, hipStream_t stream) const {
+
+    // The retry's consume: pairs[j] = (batch position, pool position), one move kernel launch
+    // (pool -> d_buf) after the index lists go up, on the slot's stream.
+    int carry_consume(ReadSlot& s, const std::vector<std::pair<uint32_t, uint32_t>>& pairs) const {
         const size_t m = pairs.size();
         if (!m) return CEC_OK;
-        uint32_t* h = s.h_cids + region * 2 * parts * t;
-        uint32_t* dv = s.d_cids + region * 2 * parts * t;
         for (size_t j = 0; j < m; ++j) {
-            h[j] = pairs[j].first;
-            h[m + j] = pairs[j].second;
+            s.h_cids[j] = pairs[j].first;
+            s.h_cids[m + j] = pairs[j].second;
         }
-        PIPE_TRY(hipMemcpyAsync(dv, h, 2 * m * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
-        cec::MoveParams mv{s.d_buf, t * cs, cs, uint32_t(t), d_carry, cs, dv, uint32_t(m),
-                           to_batch ? 1u : 0u, dv + m};
-        PIPE_TRY(cec::launch_move_chunks(mv, stream));
+        PIPE_TRY(hipMemcpyAsync(s.d_cids, s.h_cids, 2 * m * sizeof(uint32_t), hipMemcpyHostToDevice,
+                                s.stream));
+        cec::MoveParams mv{s.d_buf, t * cs, cs, uint32_t(t), d_carry, cs, s.d_cids, uint32_t(m), 1u,
+                           s.d_cids + m};
+        PIPE_TRY(cec::launch_move_chunks(mv, s.stream));
+        return CEC_OK;
+    }
+
+    // The batch's stash (CEC_READ_CARRY), queued after its verification: reserve up to
+    // carry_batch free entries (each waits for its last copies), let the stash kernels fill them
+    // with the verified chunks of the parts that will come back TooFewShardsPresent, and bring
+    // the part -> entry map back with the batch.
+    int carry_stash(ReadSlot& s, size_t n_parts) {
+        carry_unreserve(s);
+        while (s.reserved.size() < carry_batch && !carry_free.empty()) {
+            const int32_t id = carry_free.front();  // the entry freed longest ago first (FIFO)
+            carry_free.pop_front();
+            carry_used[size_t(id)] = kReserved;
+            s.h_res[s.reserved.size()] = uint32_t(id);
+            s.reserved.push_back(id);
+            PIPE_TRY(hipStreamWaitEvent(s.stream, carry_ready[size_t(id)], 0));
+        }
+        const size_t n = n_parts * t;
+        PIPE_TRY(hipMemcpyAsync(s.d_present, s.h_present, n, hipMemcpyHostToDevice, s.stream));
+        if (!s.reserved.empty())
+            PIPE_TRY(hipMemcpyAsync(s.d_res, s.h_res, s.reserved.size() * sizeof(uint32_t),
+                                    hipMemcpyHostToDevice, s.stream));
+        cec::CarryStashParams cp{s.d_buf, t * cs, cs, uint32_t(t), uint32_t(d), uint32_t(n_parts),
+                                 d_carry, cs, s.d_present, s.d_flags + n, s.d_res,
+                                 uint32_t(s.reserved.size()), s.d_map};
+        PIPE_TRY(cec::launch_carry_stash(cp, s.stream));
+        for (int32_t id : s.reserved) PIPE_TRY(hipEventRecord(carry_ready[size_t(id)], s.stream));
+        PIPE_TRY(hipMemcpyAsync(s.h_map, s.d_map, n_parts * sizeof(int32_t), hipMemcpyDeviceToHost,
+                                s.stream));
         return CEC_OK;
     }
 
@@ -646,36 +687,6 @@ struct cec_read_pipeline {
         const int sst = ensure_streams(s);
         if (sst != CEC_OK) return sst;
         const hipStream_t us = upload_stream(s);
-        if (s.stash_pending) {  // the last batch's carried chunks leave d_buf before it is refilled
-            if (us != s.stream) PIPE_TRY(hipStreamWaitEvent(us, s.stashed, 0));
-            s.stash_pending = false;
-        }
-        // carried parts: their verified chunks from the pool, one move launch on the compute
-        // stream (after each entry's stash), queued BEFORE the uploads (it writes only the
-        // positions they do not, and the slot's last batch is done): an entry is free again as
-        // soon as this move has run, not once the PCIe uploads ahead of it in the stream have
-        if (!s.carried.empty()) {
-            std::vector<std::pair<uint32_t, uint32_t>> pairs;
-            std::vector<int32_t> used;
-            for (size_t k = 0; k < n_parts; ++k) {
-                if (!s.carried[k]) continue;
-                const int32_t id = carry_ids[k];
-                PIPE_TRY(hipStreamWaitEvent(s.stream, carry_ready[size_t(id)], 0));
-                const uint8_t* pr = s.h_present + k * t;
-                for (size_t i = 0; i < t; ++i)
-                    if (pr[i] == CEC_PRESENT_VERIFIED)
-                        pairs.emplace_back(uint32_t(k * t + i), uint32_t(size_t(id) * t + i));
-                used.push_back(id);
-            }
-            const int cst = ensure_carry_ids(s);
-            if (cst != CEC_OK) return cst;
-            const int mst = carry_move(s, pairs, 1, true, s.stream);
-            if (mst != CEC_OK) return mst;
-            for (int32_t id : used) {
-                PIPE_TRY(hipEventRecord(carry_ready[size_t(id)], s.stream));
-                carry_give_back(id);
-            }
-        }
         if (packed) {
             const int est = ensure_packed(s);
             if (est != CEC_OK) return est;
@@ -720,6 +731,28 @@ struct cec_read_pipeline {
                     PIPE_TRY(hipMemcpy2DAsync(dst, cs, src, L, L, j - i, hipMemcpyHostToDevice, us));
                 i = j;
             }
+        }
+        // carried parts: their verified chunks come from the pool, one move launch queued after
+        // the uploads (it writes only positions they do not); each entry waits for its stash and
+        // is free again once this move has run
+        if (!s.carried.empty()) {
+            std::vector<std::pair<uint32_t, uint32_t>> pairs;
+            for (size_t k = 0; k < n_parts; ++k) {
+                if (!s.carried[k]) continue;
+                const int32_t id = carry_ids[k];
+                PIPE_TRY(hipStreamWaitEvent(s.stream, carry_ready[size_t(id)], 0));
+                const uint8_t* pr = s.h_present + k * t;
+                for (size_t i = 0; i < t; ++i)
+                    if (pr[i] == CEC_PRESENT_VERIFIED)
+                        pairs.emplace_back(uint32_t(k * t + i), uint32_t(size_t(id) * t + i));
+            }
+            const int mst = carry_consume(s, pairs);
+            if (mst != CEC_OK) return mst;
+            for (size_t k = 0; k < n_parts; ++k)
+                if (s.carried[k]) {
+                    PIPE_TRY(hipEventRecord(carry_ready[size_t(carry_ids[k])], s.stream));
+                    carry_give_back(carry_ids[k]);
+                }
         }
         const int ust = uploads_done(s);
         if (ust != CEC_OK) return ust;
@@ -790,6 +823,10 @@ struct cec_read_pipeline {
             PIPE_TRY(hipEventRecord(s.join, s.side));
             PIPE_TRY(hipStreamWaitEvent(s.stream, s.join, 0));
         }
+        if (carry) {
+            const int cst = carry_stash(s, n_parts);
+            if (cst != CEC_OK) return cst;
+        }
         PIPE_TRY(hipMemcpyAsync(s.h_ok, s.d_flags + n, n, hipMemcpyDeviceToHost, s.stream));
         PIPE_TRY(hipEventRecord(s.done, s.stream));
         s.in_flight = true;
@@ -830,7 +867,10 @@ int cec_read_pipeline_new_ex(const cec_codec* codec, size_t chunk_len, size_t pa
     pl->resilver = (flags & CEC_READ_RESILVER) != 0;
     pl->verify_only = (flags & CEC_READ_VERIFY_ONLY) != 0;
     pl->carry = (flags & CEC_READ_CARRY) != 0;
-    pl->carry_cap = pl->carry ? parts_per_batch : 0;  // a batch's worth of parts to retry
+    // a quarter of a batch's parts per batch (a 1 % damaged-fetch rate fails ~10 % of RS(10,4)
+    // parts): entries for every batch in flight plus one batch's retries
+    pl->carry_batch = pl->carry ? std::min<size_t>(parts_per_batch, std::max<size_t>(8, parts_per_batch / 4)) : 0;
+    pl->carry_cap = pl->carry_batch * (depth + 1);
     pl->side_decode = cec::knobs().read_side;
     pl->shared_upload = cec::knobs().read_upstream;
     pl->slots.resize(depth);
@@ -997,38 +1037,22 @@ int cec_read_pipeline_wait(cec_read_pipeline* pl, size_t slot, const uint8_t** d
             }
             PIPE_TRY(hipStreamSynchronize(s.stream));
         }
-        // CEC_READ_CARRY: keep the verified chunks of every part that still lacks d of them in
-        // the carry pool, so its retry need not upload them again
+        // CEC_READ_CARRY: the stash kept the verified chunks of every part with fewer than d of
+        // them (exactly the parts reported TooFewShardsPresent) in a reserved entry, while
+        // reservations lasted; those become the caller's carry ids, the rest go back
         if (pl->carry) {
-            DeviceGuard guard(pl->device);
-            PIPE_TRY(guard.status());
             s.carry_ids.assign(n, -1);
-            std::vector<std::pair<uint32_t, uint32_t>> pairs;
-            std::vector<int32_t> used;
             for (size_t k = 0; k < n; ++k) {
-                if (s.h_status[k] != CEC_TOO_FEW_SHARDS_PRESENT) continue;
-                const uint8_t* ok = s.h_ok + k * t;
-                if (std::none_of(ok, ok + t, [](uint8_t f) { return f != 0; })) continue;
-                const int32_t id = pl->carry_take();
-                if (id < 0) continue;  // pool full: the caller sends the chunks again
-                PIPE_TRY(hipStreamWaitEvent(s.stream, pl->carry_ready[size_t(id)], 0));
-                for (size_t i = 0; i < t; ++i)
-                    if (ok[i]) pairs.emplace_back(uint32_t(k * t + i), uint32_t(size_t(id) * t + i));
+                const int32_t id = s.h_map[k];
+                if (id < 0 || s.h_status[k] != CEC_TOO_FEW_SHARDS_PRESENT) continue;
+                if (size_t(id) >= pl->carry_cap || pl->carry_used[size_t(id)] != pl->kReserved) {
+                    g_pipe_error = "carry stash returned an entry the batch did not reserve";
+                    return CEC_ERR_HIP;
+                }
+                pl->carry_used[size_t(id)] = pl->kHeld;
                 s.carry_ids[k] = id;
-                used.push_back(id);
             }
-            const bool any = !used.empty();
-            if (any) {
-                const int cst = pl->ensure_carry_ids(s);
-                if (cst != CEC_OK) return cst;
-                const int mst = pl->carry_move(s, pairs, 0, false, s.stream);
-                if (mst != CEC_OK) return mst;
-                for (int32_t id : used) PIPE_TRY(hipEventRecord(pl->carry_ready[size_t(id)], s.stream));
-                if (!s.stashed)
-                    PIPE_TRY(hipEventCreateWithFlags(&s.stashed, hipEventDisableTiming));
-                PIPE_TRY(hipEventRecord(s.stashed, s.stream));
-                s.stash_pending = true;
-            }
+            pl->carry_unreserve(s);
         }
         // Where each data chunk is: re-decoded parts and (without REBUILT_ONLY) every part in the
         // data output; otherwise a loaded chunk stays in the chunk buffer it was read from (it

@@ -348,10 +348,11 @@ int cec_read_pipeline_new_ex(const cec_codec* codec, size_t chunk_len, size_t pa
 /* Read-pipeline flag (read mode only): keep retries' verified chunks on the device.  The
  * reference keeps a chunk that verified in memory while it draws another for the one that failed
  * (file_part.rs:92-107); without this flag the retry of a part sends its verified chunks up
- * again (CEC_PRESENT_VERIFIED).  With it, wait copies the verified chunks of every part it
- * reports CEC_TOO_FEW_SHARDS_PRESENT into a device carry pool (parts_per_batch entries of
- * (d+p) chunks, made with the pipeline);
- * cec_read_pipeline_carry_ids gives each such part its entry (-1: none kept, pool full).  The
+ * again (CEC_PRESENT_VERIFIED).  With it, each batch keeps the verified chunks of every part it
+ * will report CEC_TOO_FEW_SHARDS_PRESENT in a device carry pool, on the device right after the
+ * verification (up to max(8, parts_per_batch/4) parts per batch, in part order; the pool holds
+ * depth+1 times that many entries of (d+p) chunks and is made with the pipeline);
+ * after wait, cec_read_pipeline_carry_ids gives each such part its entry (-1: none kept).  The
  * retry passes the ids to cec_read_pipeline_submit_carried: a part with an id takes its
  * CEC_PRESENT_VERIFIED chunks from the pool (the caller need not fill them in the slot) and its
  * data chunks among them come back like rebuilt ones (REBUILT_ONLY data_chunks point at the

@@ -135,6 +135,47 @@ def test_carry_ids_contract():
         rp.carry_release(int(ids[0]))
 
 
+def test_carry_reservation_runs_out():
+    """A batch reserves max(8, parts/4) pool entries for its stash: with 40 parts
+    all failing, the first 10 in part order get carry ids and the rest -1; the retry mixes
+    carried parts (slot bytes of their verified chunks garbage) with parts that send their
+    verified chunks again, and every part decodes to the stored bytes."""
+    d, p, L, n = 4, 2, 1024, 40
+    chunks, dig = _store(n, d, p, L, 12)
+    rp = ce.ReadPipeline(ce.ReedSolomon(d, p), L, n, 2, ce.ReadPipeline.REBUILT_ONLY |
+                         ce.ReadPipeline.CARRY)
+    slot, ch, pres, exp = rp.acquire()
+    pres[:] = 0
+    pres[:, :d] = 1
+    ch[:] = chunks
+    ch[:, 1, 7] ^= 0x40       # chunk 1 of every part damaged: 3 verified of 4 -> TooFew
+    ch[5, 2, 0] ^= 1          # part 5: chunks 1 and 2 damaged, 2 verified
+    exp[:] = dig
+    rp.submit(slot, n)
+    _, ver, st = rp.wait(slot)
+    assert all(s == ce.TOO_FEW_SHARDS_PRESENT for s in st)
+    good = ver.astype(bool).copy()
+    ids = rp.carry_ids(slot, n)
+    assert list(ids[:10] >= 0) == [True] * 10 and list(ids[10:]) == [-1] * (n - 10)
+    assert len(set(ids[:10].tolist())) == 10
+    slot, ch, pres, exp = rp.acquire()
+    pres[:] = np.where(good, ce.PRESENT_VERIFIED, 0)
+    ch[:] = 0x5A
+    for k in range(n):
+        if ids[k] < 0:  # no entry: its verified chunks go up again from the slot
+            for j in np.flatnonzero(good[k]):
+                ch[k, j] = chunks[k, j]
+        for j in [4, 5] if k == 5 else [4]:  # the parity chunk(s) still needed
+            pres[k, j] = 1
+            ch[k, j] = chunks[k, j]
+    exp[:] = dig
+    rp.submit_carried(slot, n, ids)
+    _, ver, st = rp.wait(slot)
+    assert list(st) == [ce.OK] * n
+    for k in range(n):
+        assert rp.part_bytes(slot, n, k) == chunks[k, :d].tobytes(), k
+
+
 def test_bench_timed_read_repair_small():
     sys.path.insert(0, ROOT)
     import bench
