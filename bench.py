@@ -440,19 +440,18 @@ def timed_read_repair(codec, ring, ring_dig, L, P, depth, first, n_parts, world,
     fraction of the fresh loads comes back with a flipped byte (the location served bad bytes);
     the GPU verifies every fresh chunk against the metadata digest, decodes the missing data
     chunks, and a part whose load failed verification is retried with one more chunk
-    (file_part.rs:92-107) with its verified chunks sent again flagged CEC_PRESENT_VERIFIED
-    (CEC_BENCH_CARRY=1: kept on the device instead, CEC_READ_CARRY).  One untimed warmup pass of
-    `depth` batches, then the timed stream.
+    (file_part.rs:92-107), its verified chunks kept on the device (CEC_READ_CARRY: only the new
+    chunk is fetched and uploaded; CEC_BENCH_CARRY=0 sends them again flagged
+    CEC_PRESENT_VERIFIED).  One untimed warmup pass of `depth` batches, then the timed stream.
     Returns (local seconds, stats dict, sampled output checks)."""
     import numpy as np
     d = codec.data_shard_count()
     R = len(ring)
     if rp is None:
-        # CEC_BENCH_CARRY=1: CEC_READ_CARRY, a retried part's verified chunks kept on the device
-        # (not fetched or uploaded again).  Off by default: it pays only when no two slots share
-        # a hardware queue, which plain HIP streams do not guarantee (DESIGN §4.5b)
+        # CEC_READ_CARRY: a retried part's verified chunks stay on the device (not fetched or
+        # uploaded again); CEC_BENCH_CARRY=0 turns it off for A/B runs (DESIGN §4.5b)
         flags = ce.ReadPipeline.REBUILT_ONLY
-        if os.environ.get("CEC_BENCH_CARRY", "0") == "1":
+        if os.environ.get("CEC_BENCH_CARRY", "1") != "0":
             flags |= ce.ReadPipeline.CARRY
         rp = ce.ReadPipeline(codec, L, P, depth, flags)
     crng = np.random.default_rng(seed)
@@ -606,7 +605,7 @@ def run_read_stream(args, cfg, codec, world, rank, device, reduce_dev):
             f"region by {threads} host threads into the pinned slot, {args.corrupt:g} of the "
             "fetched chunks damaged (seeded), failed parts retried"
             + (" (their verified chunks kept on the device, CEC_READ_CARRY)"
-               if os.environ.get("CEC_BENCH_CARRY", "0") == "1" else ""),
+               if os.environ.get("CEC_BENCH_CARRY", "1") != "0" else ""),
             read_repair=stats, check_vs_stored=ok, checks=checks)), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
