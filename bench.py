@@ -431,6 +431,17 @@ def encoded_ring(codec, d, p, L, n_parts, seed, device, P=256):
     return ring, dig
 
 
+def bench_carry():
+    """CEC_READ_CARRY in the read-repair streams: a retried part's verified chunks stay on the
+    device (not fetched or uploaded again); CEC_BENCH_CARRY=0 turns it off for A/B runs
+    (DESIGN §4.5b)."""
+    return os.environ.get("CEC_BENCH_CARRY", "1") != "0"
+
+
+def read_repair_flags():
+    return ce.ReadPipeline.REBUILT_ONLY | (ce.ReadPipeline.CARRY if bench_carry() else 0)
+
+
 def timed_read_repair(codec, ring, ring_dig, L, P, depth, first, n_parts, world, corrupt,
                       copier, seed, n_samples=3, rp=None):
     """FileReadBuilder over parts [first, first + n_parts) with read_with_context's retries
@@ -448,12 +459,7 @@ def timed_read_repair(codec, ring, ring_dig, L, P, depth, first, n_parts, world,
     d = codec.data_shard_count()
     R = len(ring)
     if rp is None:
-        # CEC_READ_CARRY: a retried part's verified chunks stay on the device (not fetched or
-        # uploaded again); CEC_BENCH_CARRY=0 turns it off for A/B runs
-        flags = ce.ReadPipeline.REBUILT_ONLY
-        if os.environ.get("CEC_BENCH_CARRY", "1") != "0":
-            flags |= ce.ReadPipeline.CARRY
-        rp = ce.ReadPipeline(codec, L, P, depth, flags)
+        rp = ce.ReadPipeline(codec, L, P, depth, read_repair_flags())
     crng = np.random.default_rng(seed)
     damaged = [0]
 
@@ -605,7 +611,7 @@ def run_read_stream(args, cfg, codec, world, rank, device, reduce_dev):
             f"region by {threads} host threads into the pinned slot, {args.corrupt:g} of the "
             "fetched chunks damaged (seeded), failed parts retried"
             + (" (their verified chunks kept on the device, CEC_READ_CARRY)"
-               if os.environ.get("CEC_BENCH_CARRY", "1") != "0" else ""),
+               if bench_carry() else ""),
             read_repair=stats, check_vs_stored=ok, checks=checks)), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
@@ -709,7 +715,7 @@ def read_repair_form(codec, d, p, L, n_parts, world, rank, reduce_dev, copier, d
     # cannot get them every rank skips the form together, before any barrier of the stream
     try:
         ring, ring_dig = encoded_ring(codec, d, p, L, 2 * P, rank_seed(0xE2ED, rank), device, P)
-        rp, err = ce.ReadPipeline(codec, L, P, depth, ce.ReadPipeline.REBUILT_ONLY), None
+        rp, err = ce.ReadPipeline(codec, L, P, depth, read_repair_flags()), None
     except Exception as e:  # noqa: BLE001 (reported in the line)
         ring, rp, err = None, None, f"{type(e).__name__}: {e}"
     if not all_ranks_ok(err is None, world, reduce_dev):
@@ -735,8 +741,10 @@ def read_repair_form(codec, d, p, L, n_parts, world, rank, reduce_dev, copier, d
                     "page-locked slot, a seeded fraction of them damaged -> H2D -> SHA-256 "
                     "verify + reconstruct_data -> D2H of the rebuilt data chunks; parts with a "
                     "rejected chunk resubmitted in the next batch, ahead of its new parts, with "
-                    "their verified chunks (CEC_PRESENT_VERIFIED) and one more "
-                    f"(cec_read_pipeline, {P}-part batches, {depth} slots)"}
+                    + ("their verified chunks kept on the device (CEC_READ_CARRY) "
+                       if bench_carry() else "their verified chunks (CEC_PRESENT_VERIFIED) ")
+                    + f"and one more (cec_read_pipeline, {P}-part batches, {depth} slots)",
+            "carried_chunks": stats["carried_chunks"]}
 
 
 def scheduler_pageable(codec, d, p, L, ring, n_parts, world, reduce_dev, device_ordinal):
