@@ -172,9 +172,10 @@ def test_read_repair_stream_status_other_than_too_few_raises():
 
 
 class FakeCarryPipeline(FakeReadPipeline):
-    """cec_read_pipeline with CEC_READ_CARRY: wait keeps the verified chunks of every part it
-    reports TooFewShardsPresent in a pool of 2 x parts entries (-1 when full); submit_carried takes
-    a carried part's CEC_PRESENT_VERIFIED chunks from the pool, whatever the slot holds there."""
+    """cec_read_pipeline with CEC_READ_CARRY: each batch keeps the verified chunks of every part
+    it reports TooFewShardsPresent in a pool of 2 x parts entries (-1 when none is free; the real
+    pipeline's stash kernels do this on the device); submit_carried takes a carried part's
+    CEC_PRESENT_VERIFIED chunks from the pool, whatever the slot holds there."""
     carry = True
 
     def __init__(self, *a, cap=None):
