@@ -889,6 +889,66 @@ impl ReadPipeline {
             })
             .collect())
     }
+
+    /// As [`ReadPipeline::new_rebuilt_only`] with `CEC_READ_CARRY`: the verified chunks of a
+    /// part that comes back `TooFewShardsPresent` stay on the device for its retry
+    /// ([`ReadPipeline::carry_ids`], [`ReadPipeline::submit_carried`]), so the loader fetches and
+    /// uploads only the retry's new chunks -- the reference keeps them in memory the same way
+    /// while it draws another chunk (file_part.rs:92-107).
+    pub fn new_carry(
+        codec: &ReedSolomon,
+        chunk_len: usize,
+        parts_per_batch: usize,
+        depth: usize,
+    ) -> Result<ReadPipeline, CecError> {
+        let mut raw = std::ptr::null_mut();
+        check_pipe(unsafe {
+            sys::cec_read_pipeline_new_ex(
+                codec.raw,
+                chunk_len,
+                parts_per_batch,
+                depth,
+                sys::CEC_READ_REBUILT_ONLY | sys::CEC_READ_CARRY,
+                &mut raw,
+            )
+        })?;
+        Ok(ReadPipeline {
+            raw,
+            d: codec.data_shard_count(),
+            t: codec.total_shard_count(),
+            chunk_len,
+            parts: parts_per_batch,
+        })
+    }
+
+    /// After [`ReadPipeline::wait`]: each of the slot's `n_parts` parts' carry entry (`None`: its
+    /// verified chunks were not kept; it resends them flagged `CEC_PRESENT_VERIFIED`).
+    pub fn carry_ids(&mut self, slot: usize, n_parts: usize) -> Result<Vec<Option<i32>>, CecError> {
+        let mut ids = vec![-1i32; n_parts.max(1)];
+        check_pipe(unsafe { sys::cec_read_pipeline_carry_ids(self.raw, slot, ids.as_mut_ptr()) })?;
+        Ok(ids.into_iter().take(n_parts).map(|id| if id >= 0 { Some(id) } else { None }).collect())
+    }
+
+    /// [`ReadPipeline::submit`] where the parts with `Some(id)` take their
+    /// `CEC_PRESENT_VERIFIED` chunks from that carry entry (the slot need not hold them).  An
+    /// entry is used once.
+    pub fn submit_carried(
+        &mut self,
+        slot: usize,
+        n_parts: usize,
+        carry: &[Option<i32>],
+    ) -> Result<(), CecError> {
+        if carry.len() < n_parts {
+            return Err(too_small("submit_carried"));
+        }
+        let ids: Vec<i32> = carry.iter().take(n_parts).map(|c| c.unwrap_or(-1)).collect();
+        check_pipe(unsafe { sys::cec_read_pipeline_submit_carried(self.raw, slot, n_parts, ids.as_ptr()) })
+    }
+
+    /// Hands back the entry of a part the caller gives up on (undecodable: no chunk left).
+    pub fn carry_release(&mut self, id: i32) -> Result<(), CecError> {
+        check_pipe(unsafe { sys::cec_read_pipeline_carry_release(self.raw, id) })
+    }
 }
 
 /// Page-locked host memory (`cec_host_alloc`) placed on `device`'s NUMA node: use it for the
