@@ -120,3 +120,58 @@ def test_fuzz_read_batch(seed):
         assert status[k] == ce.OK, (seed, k)
         for j in range(d):
             assert got[k, j, :L].tobytes() == ref[k, j, :L].tobytes(), (seed, k, j)
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_fuzz_read_stream_carry(seed):
+    """The read-repair loop (file_part.rs:92-107) on the pipeline with and without
+    CEC_READ_CARRY, same seeded store and damage: the same parts decode, to the stored bytes,
+    the same parts are undecodable, and with carry the retries take their verified chunks from
+    the device (slot bytes for them are garbage) instead of fetching them again."""
+    from chunky_ec.readstream import ReadRepairStream
+    rng = np.random.default_rng(9000 + seed)
+    d = int(rng.integers(1, 13))
+    p = int(rng.integers(1, 7))
+    t = d + p
+    L = int(rng.choice([int(rng.integers(1, 300)), 64 * int(rng.integers(1, 40))]))
+    n = int(rng.integers(5, 60))
+    P = int(rng.integers(1, 12))
+    depth = int(rng.integers(1, 5))
+    corrupt = float(rng.choice([0.05, 0.15, 0.3]))
+    stored = rng.integers(0, 256, (n, t, L), dtype=np.uint8)
+    dig = np.zeros((n, t, 32), np.uint8)
+    for k in range(n):
+        st, par = oracle.encode_sep(d, p, [stored[k, j] for j in range(d)])
+        assert st == 0
+        stored[k, d:] = np.stack(par)
+        for i in range(t):
+            dig[k, i] = np.frombuffer(hashlib.sha256(stored[k, i].tobytes()).digest(), np.uint8)
+    damage = rng.random((n, t)) < corrupt  # per (part, chunk): a chunk is fetched fresh once
+    runs = {}
+    for carry in (False, True):
+        rp = ce.ReadPipeline(ce.ReedSolomon(d, p), L, P, depth, ce.ReadPipeline.REBUILT_ONLY |
+                             (ce.ReadPipeline.CARRY if carry else 0))
+        def fetch(slot_chunks, rows):
+            for k, part, flags in rows:
+                slot_chunks[k] = 0xA5
+                for j in np.flatnonzero(flags):
+                    slot_chunks[k, j] = stored[part, j]
+                    if flags[j] == 1 and damage[part, j]:
+                        slot_chunks[k, j, (part * 31 + j) % L] ^= 0x24
+
+        got = {}
+
+        def on_part(slot, nb, k, part, attempts, rp=rp, got=got):
+            got[part] = rp.part_bytes(slot, nb, k)
+
+        s = ReadRepairStream(rp, fetch, lambda ids: dig[ids], seed=seed, on_part=on_part).run(0, n)
+        for part, out in got.items():
+            assert out == stored[part, :d].tobytes(), (seed, carry, part)
+        assert set(got) | set(s.undecodable) == set(range(n))
+        runs[carry] = (set(got), s)
+        del rp
+    assert runs[False][0] == runs[True][0], seed
+    s0, s1 = runs[False][1], runs[True][1]
+    assert s1.retried_parts == s0.retried_parts and s1.rejected_chunks == s0.rejected_chunks
+    # the same batches: every chunk the carry run did not fetch came from the pool
+    assert s1.chunks_loaded + s1.carried_chunks == s0.chunks_loaded and s0.carried_chunks == 0
