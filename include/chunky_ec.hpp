@@ -435,6 +435,7 @@ class ChunkStore {
         return loc;
     }
     Location write_shard(const Sha256Hash& hash, const uint8_t* bytes, size_t n) {
+        if (discard_) return location_of(hash);  // no copy of bytes nobody keeps
         return write_shard(hash, Bytes(bytes, bytes + n));
     }
     // Put bytes at any location (a replica elsewhere, a stale copy in tests).
@@ -850,9 +851,11 @@ struct FileReference {
         size_t first = 0, n = 0;
         uint64_t job = 0;
         bool live = false;
-        detail::PinnedBuf chunks;   // [W][t][L] the copies (DMA'd directly)
+        // [W][t][L] the copies (DMA'd directly); verify grows it when a window has more copies
+        // than chunks (chunks with several locations), and keeps it for the next windows
+        detail::PinnedBuf chunks;
         detail::PinnedBuf rebuilt;  // [W][t][L] resilver: the rebuilt chunks
-        Bytes spill;                // verify: copies beyond the pinned window (many locations)
+        detail::PinnedBuf prepass;  // resilver: the copies of chunks with several locations
         std::vector<uint8_t> present, expected, verified;
         std::vector<int> status;
         // verify: one item per copy hashed, (window part, chunk, location); resilver: the chunks
@@ -936,11 +939,10 @@ struct FileReference {
                             if (locs[j] == LocationIntegrity::Valid)
                                 w.items.push_back({uint32_t(q), uint32_t(i), uint32_t(j)});
                     }
-                uint8_t* buf = chunks;
-                if (w.items.size() > W * t) {  // more copies than the pinned window holds
-                    w.spill.resize(w.items.size() * L);
-                    buf = w.spill.data();
-                }
+                // page-locked whatever the count: a pageable spill would go through the
+                // scheduler's staging copies, into memory touched for the first time
+                uint8_t* buf = w.items.size() > W * t ? w.chunks.reserve(w.items.size() * L, devs[0])
+                                                      : chunks;
                 w.job = w.items.empty() ? 0 : verify_items(w.items, at, buf, w.present,
                                                           w.expected, w.verified);
             } else {
@@ -955,9 +957,9 @@ struct FileReference {
                                 multi.push_back({uint32_t(q), uint32_t(i), uint32_t(j)});
                     }
                 if (!multi.empty()) {
-                    Bytes buf(((multi.size() + t - 1) / t) * t * L);
+                    uint8_t* buf = w.prepass.reserve(((multi.size() + t - 1) / t) * t * L, devs[0]);
                     std::vector<uint8_t> pr, ex, ver;
-                    const uint64_t job = verify_items(multi, at, buf.data(), pr, ex, ver);
+                    const uint64_t job = verify_items(multi, at, buf, pr, ex, ver);
                     detail::check_multi(cec_multi_wait(m, job));
                     for (size_t x = 0; x < multi.size(); ++x)
                         reports[k0 + at + multi[x][0]].locations[multi[x][1]][multi[x][2]] =
@@ -1436,6 +1438,7 @@ inline void release_thread_buffers() {
     for (auto& w : FileReference::check_windows()) {
         w.chunks.release();
         w.rebuilt.release();
+        w.prepass.release();
     }
     detail::cached_multi_entry() = detail::CachedMulti{};
 }
