@@ -86,8 +86,10 @@ class BatchChecker:
         self.d, self.p, self.t, self.L = data, parity, data + parity, chunk_size
         self.window = parts_per_batch * max(len(devices), 1)
         dev0 = devices[0] if devices else -1
+        self.dev0 = dev0
         W, t, L = self.window, self.t, chunk_size
         self.chunks = [HostBuffer(W * t * L, dev0) for _ in range(2)]
+        self.prepass = [None, None]  # resilver: copies of multi-location chunks (grown, kept)
         self.rebuilt = [HostBuffer(W * t * L, dev0) for _ in range(2)]
         self.present = [np.zeros((W, t), np.uint8) for _ in range(2)]
         self.expected = [np.zeros((W, t, 32), np.uint8) for _ in range(2)]
@@ -144,14 +146,19 @@ class BatchChecker:
                  for q in range(cnt)]
         return copies, parts
 
+    def _pinned(self, bufs, slot, n):
+        """bufs[slot], grown to n bytes if smaller: page-locked whatever the count (a pageable
+        overflow would go through the scheduler's staging copies), and kept for later windows."""
+        if bufs[slot] is None or bufs[slot].nbytes < n:
+            bufs[slot] = HostBuffer(n, self.dev0)
+        return bufs[slot]
+
     def _hash_items(self, items, copies, digs, buf):
-        """A verify job over `items` [(q, i, j)], d + p of them per scheduler row; returns (job,
-        verified flags in item order)."""
+        """A verify job over `items` [(q, i, j)], d + p of them per scheduler row, copies in the
+        page-locked `buf`; returns (job, verified flags in item order)."""
         t, L = self.t, self.L
         g = -(-len(items) // t)
-        if buf is None or len(items) > self.window * t:
-            buf = np.zeros(g * t * L, np.uint8)  # more copies than the pinned window holds
-        view = buf.view(-1, t, L) if isinstance(buf, HostBuffer) else buf.reshape(-1, t, L)
+        view = buf.view(-1, t, L)
         pres = np.zeros((g, t), np.uint8)
         exp = np.zeros((g, t, 32), np.uint8)
         ver = np.zeros((g, t), np.uint8)
@@ -168,7 +175,9 @@ class BatchChecker:
                  for j, r in enumerate(parts[q].locations[i]) if r is True]
         w = _Window(slot, None, first, cnt, parts, items, [])
         if items:
-            w.job, w.ver = self._hash_items(items, copies, digs, self.chunks[slot])
+            g = -(-len(items) // self.t)
+            buf = self._pinned(self.chunks, slot, g * self.t * self.L)  # chunks with 2+ copies
+            w.job, w.ver = self._hash_items(items, copies, digs, buf)
         return w
 
     def _collect_verify(self, w: _Window, sink) -> None:
@@ -185,7 +194,7 @@ class BatchChecker:
         t, L = self.t, self.L
         copies, parts = self._copies(first, cnt, read_all)
         digs = [digests(first + q) for q in range(cnt)]
-        ch = self.chunks[slot].view(self.window, t, L)
+        ch = self.chunks[slot].array[: self.window * t * L].reshape(self.window, t, L)
         pres, exp = self.present[slot], self.expected[slot]
         pres[:cnt] = 0
         # chunks with several locations: every copy hashed first (file_part.rs:277-289 reads each
@@ -193,7 +202,9 @@ class BatchChecker:
         multi = [(q, i, j) for q in range(cnt) for i in range(t) if len(copies[q][i]) > 1
                  for j, r in enumerate(parts[q].locations[i]) if r is True]
         if multi:
-            job, ver = self._hash_items(multi, copies, digs, None)
+            g = -(-len(multi) // t)
+            job, ver = self._hash_items(multi, copies, digs,
+                                        self._pinned(self.prepass, slot, g * t * L))
             self.multi.wait(job)
             self.extra_passes += 1
             for x, (q, i, j) in enumerate(multi):

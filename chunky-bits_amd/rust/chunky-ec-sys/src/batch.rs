@@ -861,7 +861,6 @@ struct LiveCheck {
     present: Vec<u8>,
     expected: Vec<u8>,
     ver: Vec<u8>,
-    spill: Vec<u8>,
 }
 
 /// `FileReference::verify` / `resilver` (file_reference.rs:78-113 over `FilePart::verify` /
@@ -888,8 +887,12 @@ pub struct BatchChecker {
     t: usize,
     chunk_size: usize,
     window: usize,
+    dev0: c_int,
+    // [window][t][chunk_size] the copies, DMA'd directly; verify grows a slot's buffer when a
+    // window has more copies than chunks (chunks with several locations) and keeps it
     chunks: [HostBuffer; 2],
     rebuilt: [HostBuffer; 2],
+    prepass: [Option<HostBuffer>; 2],  // resilver: the copies of multi-location chunks
     present: [Vec<u8>; 2],
     expected: [Vec<u8>; 2],
     verified: [Vec<u8>; 2],
@@ -914,6 +917,7 @@ impl BatchChecker {
         Ok(BatchChecker {
             chunks: [buf(window * t * chunk_size)?, buf(window * t * chunk_size)?],
             rebuilt: [buf(window * t * chunk_size)?, buf(window * t * chunk_size)?],
+            prepass: [None, None],
             present: [vec![0u8; window * t], vec![0u8; window * t]],
             expected: [vec![0u8; window * t * 32], vec![0u8; window * t * 32]],
             verified: [vec![0u8; window * t], vec![0u8; window * t]],
@@ -923,6 +927,7 @@ impl BatchChecker {
             t,
             chunk_size,
             window,
+            dev0,
         })
     }
 
@@ -1071,26 +1076,23 @@ impl BatchChecker {
             }
         }
         let mut w = LiveCheck { slot, job: None, first, n: cnt, locations, items, single: Vec::new(),
-                                present: Vec::new(), expected: Vec::new(), ver: Vec::new(),
-                                spill: Vec::new() };
+                                present: Vec::new(), expected: Vec::new(), ver: Vec::new() };
         if w.items.is_empty() {
             return Ok(w);
         }
         let (t, l) = (self.t, self.chunk_size);
         let rows_needed = (w.items.len() + t - 1) / t;
-        // more copies than the pinned window holds (many locations): a pageable buffer, staged
-        let pinned = rows_needed <= self.window;
-        if !pinned {
-            w.spill = vec![0u8; rows_needed * t * l];
+        // more copies than the window holds (chunks with several locations): the slot's buffer
+        // grows, page-locked (a pageable one would go through the scheduler's staging copies)
+        if rows_needed * t * l > self.chunks[slot].len() {
+            self.chunks[slot] = HostBuffer::zeroed(rows_needed * t * l, self.dev0)?;
         }
-        let (g, present, expected, ver) = {
-            let buf: &mut [u8] = if pinned { &mut self.chunks[slot] } else { &mut w.spill };
-            Self::rows(t, l, &w.items, &copies, first, digests, buf)
-        };
+        let (g, present, expected, ver) =
+            Self::rows(t, l, &w.items, &copies, first, digests, &mut self.chunks[slot]);
         w.present = present;
         w.expected = expected;
         w.ver = ver;
-        let buf: *const u8 = if pinned { self.chunks[slot].as_ptr() } else { w.spill.as_ptr() };
+        let buf: *const u8 = self.chunks[slot].as_ptr();
         w.job = Some(unsafe {
             self.multi.submit_verify(buf, w.present.as_ptr(), w.expected.as_ptr(), g, w.ver.as_mut_ptr())
         }?);
@@ -1136,11 +1138,16 @@ impl BatchChecker {
             }
         }
         if !multi.is_empty() {
-            let mut buf = vec![0u8; ((multi.len() + t - 1) / t) * t * l];
-            let (g, present, expected, mut ver) = Self::rows(t, l, &multi, &copies, first, digests, &mut buf);
-            self.multi.verify(&buf, &present, &expected, g, &mut ver)?;
-            for (x, &(q, i, j)) in multi.iter().enumerate() {
-                locations[q][i][j] = if ver[x] != 0 { CopyCheck::Valid } else { CopyCheck::Invalid };
+            let need = ((multi.len() + t - 1) / t) * t * l;
+            if self.prepass[slot].as_ref().map_or(true, |b| b.len() < need) {
+                self.prepass[slot] = Some(HostBuffer::zeroed(need, self.dev0)?);
+            }
+            if let Some(buf) = self.prepass[slot].as_mut() {
+                let (g, present, expected, mut ver) = Self::rows(t, l, &multi, &copies, first, digests, buf);
+                self.multi.verify(buf, &present, &expected, g, &mut ver)?;
+                for (x, &(q, i, j)) in multi.iter().enumerate() {
+                    locations[q][i][j] = if ver[x] != 0 { CopyCheck::Valid } else { CopyCheck::Invalid };
+                }
             }
         }
         let mut single = Vec::new();
@@ -1185,7 +1192,7 @@ impl BatchChecker {
             )
         }?;
         Ok(LiveCheck { slot, job: Some(job), first, n: cnt, locations, items: Vec::new(), single,
-                       present: Vec::new(), expected: Vec::new(), ver: Vec::new(), spill: Vec::new() })
+                       present: Vec::new(), expected: Vec::new(), ver: Vec::new() })
     }
 
     fn collect_resilver<S, E>(&mut self, mut w: LiveCheck, base: usize, sink: &mut S)
