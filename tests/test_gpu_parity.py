@@ -171,6 +171,75 @@ def test_reconstruct_every_pattern(d, p, L):
                     assert shards[i] is None
 
 
+@pytest.mark.parametrize("d,p,L", [(128, 128, 1000), (1, 255, 4097), (255, 1, 513),
+                                   (100, 156, 64)])
+def test_max_shard_counts_vs_oracle(d, p, L):
+    """The largest codes the crate allows (d + p = 256, galois_8's field size): encode, then the
+    most erasures a part survives (p of them, drawn at random, data and parity mixed), through
+    reconstruct and reconstruct_data, against the oracle."""
+    full = _encoded(d, p, L, d * 7 + p)
+    rs = ce.ReedSolomon(d, p)
+    par = [bytearray(L) for _ in range(p)]
+    rs.encode_sep(full[:d], par)
+    assert [bytes(x) for x in par] == full[d:]
+    t = d + p
+    rng = np.random.default_rng(d * 1000 + p)
+    for _ in range(3):
+        miss = set(rng.choice(t, p, replace=False).tolist())
+        shards = [None if i in miss else bytearray(full[i]) for i in range(t)]
+        rs.reconstruct(shards)
+        assert [bytes(s) for s in shards] == full, sorted(miss)[:8]
+        shards = [None if i in miss else bytearray(full[i]) for i in range(t)]
+        rs.reconstruct_data(shards)
+        st, ref = oracle.reconstruct(d, p, [None if i in miss else full[i] for i in range(t)],
+                                     data_only=True)
+        assert st == 0
+        for i in range(t):
+            if i < d:
+                assert bytes(shards[i]) == full[i] == bytes(ref[i]), i
+            elif i in miss:
+                assert shards[i] is None and ref[i] is None
+
+
+@pytest.mark.parametrize("d,p,L", [(128, 128, 4096), (200, 56, 1000), (1, 255, 777),
+                                   (255, 1, 4096)])
+def test_max_shard_counts_device_batch(d, p, L):
+    """The device-batch kernels at d + p = 256: fused encode + SHA-256 of every chunk, then
+    reconstruct_batch with p erasures per part (a different random set per part, so the
+    mixed-pattern kernel runs with up to p output rows), against the oracle and hashlib."""
+    n, t = 3, d + p
+    buf, batch = _device_parts(n, t, L, None, seed=d + 3 * p)
+    rs = ce.ReedSolomon(d, p)
+    dig = torch.zeros((n, t, 32), dtype=torch.uint8, device=DEV)
+    ce.encode_hash_batch(rs, batch, dig.data_ptr())
+    torch.cuda.synchronize()
+    full, hd = buf.cpu().numpy().copy(), dig.cpu().numpy()
+    for k in range(n):
+        st, par = oracle.encode_sep(d, p, [full[k, j] for j in range(d)])
+        assert st == 0
+        for i in range(p):
+            assert np.array_equal(full[k, d + i], par[i]), (k, i)
+        for i in range(t):
+            assert hd[k, i].tobytes() == hashlib.sha256(full[k, i].tobytes()).digest(), (k, i)
+    rng = np.random.default_rng(t * 7 + L)
+    for data_only in (False, True):
+        present = np.ones((n, t), np.uint8)
+        for k in range(n):
+            present[k, rng.choice(t, p, replace=False)] = 0
+        dev = torch.from_numpy(full).to(DEV)
+        dev[torch.from_numpy(present == 0).to(DEV)] = 0
+        buf.copy_(dev)
+        ce.reconstruct_batch(rs, batch, present.tobytes(), data_only)
+        torch.cuda.synchronize()
+        got = buf.cpu().numpy()
+        for k in range(n):
+            for i in range(t):
+                if present[k, i] or i < d or not data_only:
+                    assert np.array_equal(got[k, i], full[k, i]), (data_only, k, i)
+                else:
+                    assert not got[k, i].any(), (data_only, k, i)  # parity left missing
+
+
 def test_reconstruct_first_d_present_rule():
     """A corrupt shard beyond the first d present ones is never read (crate behaviour)."""
     d, p, L = 3, 3, 40
