@@ -135,6 +135,39 @@ def test_carry_ids_contract():
         rp.carry_release(int(ids[0]))
 
 
+def test_carry_from_a_packed_batch():
+    """The stash runs in every batch of a CARRY pipeline, packed ones included: a part whose
+    packed load fails verification gets a carry id, and its unpacked retry takes the verified
+    chunks from the pool (the slot's copy of them is garbage)."""
+    d, p, L = 4, 2, 2048
+    chunks, dig = _store(3, d, p, L, 21)
+    rp = ce.ReadPipeline(ce.ReedSolomon(d, p), L, 3, 2, ce.ReadPipeline.REBUILT_ONLY |
+                         ce.ReadPipeline.CARRY)
+    present = np.zeros((3, d + p), np.uint8)
+    present[:, :d] = 1
+    packed = np.concatenate([chunks[k, :d] for k in range(3)]).copy()
+    packed[1 * d + 2, 9] ^= 0x10  # part 1, chunk 2 damaged
+    slot, _, _, _ = rp.acquire()
+    rp.submit_packed(slot, packed, present, dig.copy(), 3)
+    _, ver, st = rp.wait(slot)
+    assert list(st) == [ce.OK, ce.TOO_FEW_SHARDS_PRESENT, ce.OK]
+    ids = rp.carry_ids(slot, 3)
+    assert ids[0] == -1 and ids[1] >= 0 and ids[2] == -1
+    for k in (0, 2):
+        assert rp.part_bytes(slot, 3, k) == chunks[k, :d].tobytes()
+    slot, ch, pres, exp = rp.acquire()
+    pres[:1] = 0
+    pres[0, [0, 1, 3]] = ce.PRESENT_VERIFIED
+    pres[0, 4] = 1
+    ch[0] = 0x6B
+    ch[0, 4] = chunks[1, 4]
+    exp[:1] = dig[1:2]
+    rp.submit_carried(slot, 1, ids[1:2])
+    _, ver, st = rp.wait(slot)
+    assert list(st) == [ce.OK]
+    assert rp.part_bytes(slot, 1, 0) == chunks[1, :d].tobytes()
+
+
 def test_carry_reservation_runs_out():
     """A batch reserves max(8, parts/4) pool entries for its stash: with 40 parts
     all failing, the first 10 in part order get carry ids and the rest -1; the retry mixes
