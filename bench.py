@@ -8,9 +8,12 @@ reference src/file/file_part.rs:150-185), over BASELINE.json configs[1]'s shape:
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4]
 
-For N > 1 the driver launches one rank per GPU with torch.distributed.run; each rank owns its
+For N > 1 one rank runs per GPU under torch.distributed.run: the driver's launcher, or, when
+`--gpus N` is given with no WORLD_SIZE in the environment, this script starts it itself as a child
+process (launch_ranks; a world size other than --gpus is an error, exit 2).  Each rank owns its
 own 4096 parts (parts are independent: weak scaling, no collective on the data path); the
-process group is used only for the barrier and the max-over-ranks step time.
+process group carries only the barrier, the max-over-ranks step time and the per-rank rows, whose
+`check_vs_oracle` (each rank's own sampled parts vs the oracle) is ANDed into the line's.
 
 Rank 0 prints ONE JSON line.  `roofline` describes the dominant kernel, timed with HIP events
 on the stream its launches go to; `cpu_baseline` times the CPU restatement of the reference
@@ -1147,7 +1150,44 @@ RANK_FIELDS = ("device", "numa_node", "host_threads_numa_bound", "cpus", "step_m
                "end_to_end_GBs", "pcie_link_GBs", "north_star_encode_frac",
                "north_star_reconstruct_data_frac", "c3_reconstruct_frac", "c3_algorithmic_bytes",
                "c3_ms", "c4_ms", "c4_data_bytes", "read_repair_GBs", "quota_share_cpus",
-               "host_threads", "multi_copy_threads")
+               "host_threads", "multi_copy_threads", "check_vs_oracle")
+
+
+def free_port() -> int:
+    """A TCP port free on 127.0.0.1 now (the rendezvous port of the ranks launch_ranks starts)."""
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_launch_cmd(n: int, argv, port: int):
+    """The command that runs this bench as n ranks on one node (the driver's own form:
+    torch.distributed.run, one process per GPU, rendezvous on 127.0.0.1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port),
+            os.path.abspath(__file__), *argv]
+
+
+def launch_ranks(n: int, argv) -> int:
+    """`bench.py --gpus N` started without a launcher (no WORLD_SIZE): run the N ranks as a CHILD
+    process (never exec: a process that may have touched the GPU must not replace itself) and
+    return its exit status.  The ranks inherit stdout, so rank 0's JSON line is this run's line."""
+    import subprocess
+    cmd = rank_launch_cmd(n, argv, free_port())
+    print(f"bench: --gpus {n} without WORLD_SIZE: starting {n} ranks: {' '.join(cmd)}",
+          file=sys.stderr, flush=True)
+    return subprocess.run(cmd, env=dict(os.environ)).returncode
+
+
+def world_mismatch(world: int, gpus: int):
+    """The error text when this rank's world size is not what --gpus asked for, else None (a line
+    measured on another number of ranks than it claims must not be printed)."""
+    if world == gpus:
+        return None
+    return (f"bench: WORLD_SIZE={world} but --gpus={gpus}: the line would misstate the GPU count; "
+            "run `bench.py --gpus N` alone (it starts the ranks) or under torch.distributed.run "
+            "with --nproc-per-node equal to --gpus")
 
 
 def rank_row(r: int, row) -> dict:
@@ -1160,6 +1200,8 @@ def rank_row(r: int, row) -> dict:
             out[name] = int(v)
         elif name == "host_threads_numa_bound":
             out[name] = bool(v)
+        elif name == "check_vs_oracle":  # 1 passed, 0 failed, -1 not run
+            out[name] = None if v < 0 else bool(v)
         elif name == "step_ms":
             out[name] = round(v, 3)
         elif name.endswith("_frac"):
@@ -1243,9 +1285,15 @@ def main():
         cfg["workload"] = cfg["workload"].replace(
             "RS(10,4)", f"RS({cfg['d']},{cfg['p']})").replace(
             "RS(3,2)", f"RS({cfg['d']},{cfg['p']})").replace("RS(20,8)", f"RS({cfg['d']},{cfg['p']})")
+    # --gpus N > 1 with no launcher around this process: start the N ranks as a child (before
+    # anything here touches the GPU) and exit with its status
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world, rank, local = dist_env()
-    if world != args.gpus and rank == 0:
-        print(f"note: WORLD_SIZE={world} but --gpus={args.gpus}", file=sys.stderr)
+    err = world_mismatch(world, args.gpus)
+    if err:
+        print(err, file=sys.stderr, flush=True)
+        sys.exit(2)
     # one rank per GPU; more ranks than GPUs (gloo rehearsal) share them round-robin
     ordinal = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(ordinal)
@@ -1495,8 +1543,10 @@ def main():
         if counters:
             valu["counters"] = counters
 
+    # --check: a sampled part of this rank's own buffer against the oracle, on EVERY rank (ANDed
+    # over the ranks below)
     ok = None
-    if args.check and rank == 0 and cfg["op"] == "read":
+    if args.check and cfg["op"] == "read":
         import numpy as np
         import oracle
         k = n_parts // 2
@@ -1506,7 +1556,7 @@ def main():
                                      data_only=True)
         ok = (st == 0 and not any(read_status) and
               all(np.array_equal(out[i], host[i]) for i in range(d)))
-    elif args.check and rank == 0 and cfg["op"] != "reconstruct":
+    elif args.check and cfg["op"] != "reconstruct":
         import hashlib
         import numpy as np
         import oracle
@@ -1520,12 +1570,13 @@ def main():
                             for j in range(t))
 
     # sampled whole parts of the buffers behind value / north_star / baseline_configs, checked
-    # against the oracle in the cpu_baseline leg (N = 1, after every timed region)
+    # against the oracle after every timed region: at N = 1 in the cpu_baseline leg (with every
+    # part of the C2 / C4 buffers), at N > 1 on every rank, its own buffers, ANDed over the ranks
     snap = None
-    if (args.config == "c2" and fused and world == 1 and not args.no_cpu_baseline):
+    if args.config == "c2" and fused and (world > 1 or not args.no_cpu_baseline):
         snap = {"parts": (0, n_parts // 2, n_parts - 1)}
         snap["headline"] = snapshot_parts(buf, digests, snap["parts"])
-        if not args.no_full_check:
+        if world == 1 and not args.no_full_check:
             snap["c2_digests"] = digests.cpu().numpy()
             snap["c2_dev"] = buf  # checked whole in the cpu_baseline leg (batch_vs_oracle)
     # north_star's two >= 60 % targets on the same buffer (C2 only)
@@ -1549,6 +1600,16 @@ def main():
                          ordinal, device, args.corrupt,
                          full_check=snap is not None and "c2_dev" in snap)
 
+    # N > 1: every rank checks the sampled whole parts of ITS OWN buffers (headline, north_star,
+    # C3, C4: the snapshots above) against the oracle, after every timed region; the line's
+    # check_vs_oracle is the AND over the ranks (the rows below carry each rank's result)
+    rank_ok, rank_detail = ok, None
+    if snap is not None and world > 1:
+        t0 = time.perf_counter()
+        rank_detail = check_vs_oracle(snap, d, p, max(1, e2e_threads))
+        rank_detail["seconds"] = round(time.perf_counter() - t0, 2)
+        rank_ok = rank_detail["ok"] and (ok is None or ok)
+
     # per-rank figures for the N > 1 line (a straggler or a cross-NUMA placement must be
     # visible from the line alone)
     ranks = node = None
@@ -1564,10 +1625,15 @@ def main():
         row = [ordinal, numa_node, 1.0 if numa_bound else 0.0, rank_cpus, local_s * 1e3, e2e_v,
                link_v, ns_enc, ns_rec, c3.get("frac") or 0.0, c3.get("algorithmic_bytes") or 0,
                c3.get("ms") or 0.0, c4.get("ms") or 0.0, c4.get("data_bytes") or 0, rr_v,
-               quota_share(world) or 0.0, e2e_threads, int(os.environ["CEC_MULTI_COPY_THREADS"])]
+               quota_share(world) or 0.0, e2e_threads, int(os.environ["CEC_MULTI_COPY_THREADS"]),
+               -1.0 if rank_ok is None else float(bool(rank_ok))]
         rows = gather_rows(row, world, reduce_dev)
         ranks = [rank_row(r, row) for r, row in enumerate(rows)]
         node = node_figures(ranks)
+        if world > 1:
+            checks = [r["check_vs_oracle"] for r in ranks]
+            # every rank ran its check (or none did: --no-north-star etc. with no --check)
+            ok = None if all(c is None for c in checks) else all(c is True for c in checks)
 
     if rank == 0:
         total_data = data_bytes * world
@@ -1624,6 +1690,15 @@ def main():
                                           "min": round(min(steps_ms), 3)}
         if ok is not None:
             line["check_vs_oracle"] = bool(ok)
+        if world > 1 and ok is not None:
+            line["check_vs_oracle_detail"] = {
+                "all_ranks_ok": bool(ok),
+                "ranks_ok": [r["check_vs_oracle"] for r in ranks],
+                "rank0": rank_detail,
+                "basis": "each rank's own sampled whole parts (headline C2 buffer, north_star's "
+                         "re-encode, C3's rebuild, C4's fused encode and round trip; plus --check's "
+                         "part) vs oracle.encode_sep and hashlib SHA-256, after every timed region; "
+                         "ANDed over the ranks (every part of the buffers: N = 1 only)"}
         line["host"] = host_report
         if world == 1 and not args.no_cpu_baseline and cfg["op"] in ("encode_hash", "encode"):
             # the cpu_baseline leg (after every timed region), the one place the bench runs the

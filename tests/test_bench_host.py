@@ -300,3 +300,50 @@ def test_measured_valu_names_its_source():
     assert "not this run" in v["source"] and "r4e_c2_summary.md" in v["source"]
     assert bench.measured_valu("c2", "encode_hash_kernel", False) is None
     assert bench.measured_valu("c4", "encode_hash_kernel", True) is None
+
+
+def test_gpus_n_without_launcher_starts_the_ranks_as_a_child(monkeypatch):
+    """`bench.py --gpus 8` with no WORLD_SIZE: the script starts torch.distributed.run with 8
+    ranks on 127.0.0.1 as a CHILD (subprocess, never exec), passes its own arguments through, and
+    exits with the child's status; nothing touches the GPU first."""
+    import subprocess
+    seen = {}
+
+    def fake_run(cmd, env=None, **kw):
+        seen["cmd"], seen["env"] = cmd, env
+        return subprocess.CompletedProcess(cmd, 3)
+
+    monkeypatch.setattr(subprocess, "run", fake_run)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8", "--steps", "5", "--warmup", "2"])
+    with pytest.raises(SystemExit) as ex:
+        bench.main()
+    assert ex.value.code == 3
+    cmd = seen["cmd"]
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in cmd and "--nnodes=1" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert int(cmd[cmd.index("--master-port") + 1]) > 0
+    assert cmd[-7:] == [os.path.join(ROOT, "bench.py"), "--gpus", "8", "--steps", "5",
+                        "--warmup", "2"]
+    assert bench.rank_launch_cmd(2, ["--gpus", "2"], 29500)[4] == "--nproc-per-node=2"
+
+
+def test_world_size_other_than_gpus_exits_nonzero():
+    """Under a launcher whose world size differs from --gpus the bench refuses to print a line
+    (exit 2) instead of reporting the wrong n_gpus; run as the driver would, in a subprocess."""
+    import subprocess
+    assert bench.world_mismatch(4, 4) is None and "WORLD_SIZE=2" in bench.world_mismatch(2, 8)
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1"],
+                         env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 2, out.stderr[-2000:]
+    assert "WORLD_SIZE=2 but --gpus=1" in out.stderr and not out.stdout.strip()
+
+
+def test_rank_rows_carry_each_ranks_oracle_check():
+    """The N > 1 line's per-rank rows: check_vs_oracle 1 / 0 / -1 -> True / False / None."""
+    base = [0, 0, 1, 64, 40.0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 4, 4]
+    assert bench.rank_row(0, base + [1.0])["check_vs_oracle"] is True
+    assert bench.rank_row(1, base + [0.0])["check_vs_oracle"] is False
+    assert bench.rank_row(2, base + [-1.0])["check_vs_oracle"] is None
