@@ -58,6 +58,8 @@ METRIC = "RS(10,4) encode+sha256 GB/s per node at 1/2/4/8 GPUs; % of HBM rooflin
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md).  The encode kernel streams
 # 6.37 TB/s (0.796 of it), at the guide's measured 6.29 TB/s copy ceiling
 MiB = 1 << 20
+# slots in flight of the stream configs' pipelines (4 measured best of 2-8)
+STREAM_DEPTH = 4
 
 # VALU roofline of SHA-256 (the bound of every hashed config).  Per 64-byte block one lane issues
 # 1406 VALU instructions (gfx950 ISA of the SHA loop: 576 v_alignbit, 241 v_add3, 16 v_perm
@@ -538,7 +540,7 @@ def run_stream(args, cfg, codec, world, rank, device, reduce_dev):
     (ring_reader), then H2D -> fused encode + SHA-256 -> D2H of parity + digests (cec_pipeline,
     `depth` slots).  Time = first submit to last result, max over ranks."""
     d, p, L, P = cfg["d"], cfg["p"], cfg["chunk"], cfg["parts"]
-    depth = int(os.environ.get("CEC_STREAM_DEPTH", "4"))  # slots in flight (A/B knob)
+    depth = STREAM_DEPTH
     total_parts = int(args.stream_gib * (1 << 30)) // (d * L)
     lo, hi = part_range(total_parts, rank, world)
     if args.devices:
@@ -591,7 +593,7 @@ def run_read_stream(args, cfg, codec, world, rank, device, reduce_dev):
     ranges over the ranks (strong scaling); value = part data bytes delivered / s, max over
     ranks."""
     d, p, L, P = cfg["d"], cfg["p"], cfg["chunk"], cfg["parts"]
-    depth = int(os.environ.get("CEC_STREAM_DEPTH", "4"))  # slots in flight (A/B knob)
+    depth = STREAM_DEPTH
     total_parts = int(args.stream_gib * (1 << 30)) // (d * L)
     lo, hi = part_range(total_parts, rank, world)
     threads = rank_threads(world)
@@ -761,7 +763,7 @@ def scheduler_pageable(codec, d, p, L, ring, n_parts, world, reduce_dev, device_
     # every rank must reach the barriers below, or none: a rank that cannot build its scheduler
     # makes every rank skip this form together
     try:
-        m, err = ce.Multi(codec, L, P, depth, [device_ordinal]), None
+        m, err = ce.Multi(codec, L, P, depth, [device_ordinal], kinds=ce.Multi.WRITE), None
         outs = [(ce.HostBuffer(S * p * L, device_ordinal),
                  ce.HostBuffer(S * t * 32, device_ordinal)) for _ in range(J)]
     except Exception as e:  # noqa: BLE001 (reported in the line)
@@ -1103,8 +1105,8 @@ def run_stream_multi(args, cfg, codec, total_parts):
     d, p, L, P = cfg["d"], cfg["p"], cfg["chunk"], cfg["parts"]
     t = d + p
     devices = args.devices
-    depth = int(os.environ.get("CEC_STREAM_DEPTH", "4"))  # slots in flight (A/B knob)
-    m = ce.Multi(codec, L, P, depth, devices)
+    depth = STREAM_DEPTH
+    m = ce.Multi(codec, L, P, depth, devices, kinds=ce.Multi.WRITE)
     S = _segments(args, cfg, len(devices))
     J = args.jobs_in_flight
     copier = HostCopier(rank_threads(1))

@@ -72,7 +72,7 @@ def _sig(name, argtypes, restype=ctypes.c_int):
 
 _sig("cec_abi_version", [])
 # the include/chunky_ec.h this binding mirrors (2: CEC_PRESENT_VERIFIED = 0x80)
-ABI_VERSION = 2
+ABI_VERSION = 3
 if _lib.cec_abi_version() != ABI_VERSION:
     raise ImportError(f"chunky_ec: {LIB_PATH} has ABI {_lib.cec_abi_version()}, this binding "
                       f"needs {ABI_VERSION}; rebuild with `make -C chunky-bits_amd/csrc`")
@@ -164,7 +164,8 @@ _sig("cec_read_pipeline_wait", [_vp, ctypes.c_size_t, ctypes.POINTER(_u8p), ctyp
 _sig("cec_read_pipeline_drain", [_vp])
 _sig("cec_read_pipeline_new_ex", [_vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t,
                                   ctypes.c_uint, ctypes.POINTER(_vp)])
-_sig("cec_read_pipeline_data_chunks", [_vp, ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)])
+_sig("cec_read_pipeline_data_chunks", [_vp, ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p),
+                                       ctypes.c_size_t])
 _sig("cec_synth_byte", [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64],
      ctypes.c_uint8)
 _sig("cec_current_device", [ctypes.POINTER(ctypes.c_int)])
@@ -180,10 +181,41 @@ _sig("cec_pipeline_new_ex", [_vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_siz
 _sig("cec_pipeline_submit_from", [_vp, ctypes.c_size_t, _vp, ctypes.c_size_t, _vp, _vp])
 _sig("cec_read_pipeline_submit_from", [_vp, ctypes.c_size_t, _vp, _vp, _vp, ctypes.c_size_t, _vp])
 _sig("cec_read_pipeline_submit_packed", [_vp, ctypes.c_size_t, _vp, _vp, _vp, ctypes.c_size_t, _vp])
-_sig("cec_read_pipeline_carry_ids", [_vp, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int32)])
+_sig("cec_read_pipeline_carry_ids", [_vp, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int32),
+                                     ctypes.c_size_t])
 _sig("cec_read_pipeline_submit_carried", [_vp, ctypes.c_size_t, ctypes.c_size_t,
                                           ctypes.POINTER(ctypes.c_int32)])
 _sig("cec_read_pipeline_carry_release", [_vp, ctypes.c_int32])
+_sig("cec_read_pipeline_carry_held", [_vp], ctypes.c_size_t)
+
+
+class ReadSubmitStruct(ctypes.Structure):
+    """cec_read_submit (include/chunky_ec.h)."""
+    _fields_ = [("chunks", ctypes.c_void_p), ("present", ctypes.c_void_p),
+                ("expected", ctypes.c_void_p), ("n_parts", ctypes.c_size_t),
+                ("data_out", ctypes.c_void_p), ("carry_ids", ctypes.c_void_p),
+                ("flags", ctypes.c_uint)]
+
+
+class MultiStatsStruct(ctypes.Structure):
+    """cec_multi_stats (include/chunky_ec.h)."""
+    _fields_ = [("device", ctypes.c_int), ("numa_node", ctypes.c_int),
+                ("parts", ctypes.c_uint64), ("pipelines_made", ctypes.c_uint64),
+                ("chunks_uploaded", ctypes.c_uint64), ("chunks_carried", ctypes.c_uint64),
+                ("carry_held", ctypes.c_uint64)]
+
+
+_sig("cec_read_pipeline_submit_ex", [_vp, ctypes.c_size_t, ctypes.POINTER(ReadSubmitStruct)])
+_sig("cec_pipelines_made", [], ctypes.c_uint64)
+_sig("cec_multi_new_ex", [_vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t,
+                          ctypes.POINTER(ctypes.c_int), ctypes.c_size_t, ctypes.c_uint,
+                          ctypes.POINTER(_vp)])
+_sig("cec_multi_read_carry", [_vp, _vp, _vp, _vp, ctypes.c_size_t, _vp, _vp,
+                              ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_void_p),
+                              ctypes.c_uint, ctypes.POINTER(ctypes.c_int32),
+                              ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_uint64)])
+_sig("cec_multi_carry_release", [_vp, ctypes.c_int32])
+_sig("cec_multi_shard_stats", [_vp, ctypes.c_size_t, ctypes.POINTER(MultiStatsStruct)])
 _sig("cec_multi_new", [_vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t,
                        ctypes.POINTER(ctypes.c_int), ctypes.c_size_t, ctypes.POINTER(_vp)])
 _sig("cec_multi_free", [_vp], None)
@@ -670,6 +702,7 @@ class ReadPipeline:
 
     REBUILT_ONLY = 1  # CEC_READ_REBUILT_ONLY
     CARRY = 16  # CEC_READ_CARRY: retries' verified chunks kept on the device
+    SUBMIT_PACKED = 32  # CEC_SUBMIT_PACKED (submit_ex)
 
     def __init__(self, codec: ReedSolomon, chunk_len: int, parts_per_batch: int, depth: int = 4,
                  flags: int = 0):
@@ -710,12 +743,38 @@ class ReadPipeline:
         _check(_lib.cec_read_pipeline_submit(self._h, slot, n_parts))
 
     def carry_ids(self, slot: int, n_parts: int):
-        """[n_parts] int32: each part's carry entry after wait (-1: none; CARRY pipelines)."""
+        """[n_parts] int32: each part's carry entry after wait (-1: none; CARRY pipelines); the
+        caller now holds the entries (submit them with a retry, or carry_release them)."""
         import numpy as np
-        ids = np.full(max(n_parts, 1), -1, np.int32)
+        ids = np.full(self.parts, -1, np.int32)  # room for the largest batch a slot can hold
         _check(_lib.cec_read_pipeline_carry_ids(
-            self._h, slot, ids.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
+            self._h, slot, ids.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), len(ids)))
         return ids[:n_parts]
+
+    def carry_held(self) -> int:
+        """Carry entries the caller holds (taken with carry_ids, not yet used or released)."""
+        return _lib.cec_read_pipeline_carry_held(self._h)
+
+    def submit_ex(self, slot: int, n_parts: int, chunks=None, present=None, expected=None,
+                  data=None, carry_ids=None, mode: int = 0, packed: bool = False) -> None:
+        """cec_read_pipeline_submit_ex: any mode (0 read, REBUILT_ONLY, READ_RESILVER,
+        READ_VERIFY_ONLY) on this pipeline, the caller's or the slot's buffers (None), carry ids
+        (CARRY pipelines) and a packed upload."""
+        import numpy as np
+        ids = None
+        if carry_ids is not None:
+            ids = np.ascontiguousarray(carry_ids, dtype=np.int32)
+            assert len(ids) >= n_parts
+        a = ReadSubmitStruct(
+            _addr(chunks) if chunks is not None else None,
+            _addr(present) if present is not None else None,
+            _addr(expected) if expected is not None else None, n_parts,
+            _addr(data) if data is not None else None,
+            ids.ctypes.data if ids is not None else None,
+            mode | (self.SUBMIT_PACKED if packed else 0))
+        code = _lib.cec_read_pipeline_submit_ex(self._h, slot, ctypes.byref(a))
+        if code != OK:
+            raise Error(code)
 
     def submit_carried(self, slot: int, n_parts: int, carry_ids) -> None:
         """submit, with carry_ids[n_parts] (-1 = none): those parts' CEC_PRESENT_VERIFIED chunks
@@ -753,18 +812,22 @@ class ReadPipeline:
         _check(_lib.cec_read_pipeline_wait(self._h, slot, ctypes.byref(data), ctypes.byref(ok),
                                            ctypes.byref(status), ctypes.byref(n)))
         k, t, d, L = n.value, self.t, self.d, self.L
-        out = np.ctypeslib.as_array(data, shape=(max(k * d * L, 1),))[: k * d * L].reshape(k, d, L)
+        out = None  # a verify batch of a pipeline without its own output has none
+        if data:
+            out = np.ctypeslib.as_array(data, shape=(max(k * d * L, 1),))[: k * d * L].reshape(k, d, L)
         ver = np.ctypeslib.as_array(ok, shape=(max(k * t, 1),))[: k * t].reshape(k, t)
         st = np.ctypeslib.as_array(status, shape=(max(k, 1),))[:k]
         return out, ver, st
 
-    def data_chunks(self, slot: int, n_parts: int):
-        """[n_parts][d] addresses of the data chunks (cec_read_pipeline_data_chunks)."""
+    def data_chunks(self, slot: int, n_parts: int, out_chunks: Optional[int] = None):
+        """[n_parts][out] addresses of the output chunks (cec_read_pipeline_data_chunks; out = d,
+        or d+p after a resilver batch)."""
         import numpy as np
-        ptrs = (ctypes.c_void_p * max(n_parts * self.d, 1))()
-        _check(_lib.cec_read_pipeline_data_chunks(self._h, slot, ptrs))
-        return np.array([p or 0 for p in ptrs[: n_parts * self.d]],
-                        dtype=np.uint64).reshape(n_parts, self.d)
+        w = out_chunks or self.d
+        ptrs = (ctypes.c_void_p * (self.parts * self.t))()  # room for any batch of the slot
+        _check(_lib.cec_read_pipeline_data_chunks(self._h, slot, ptrs, len(ptrs)))
+        return np.array([p or 0 for p in ptrs[: n_parts * w]],
+                        dtype=np.uint64).reshape(n_parts, w)
 
     def part_bytes(self, slot: int, n_parts: int, k: int) -> bytes:
         """Part k's d data chunks concatenated (read_with_context's output), via data_chunks."""
@@ -882,14 +945,18 @@ class Multi:
     directly) and return a job id for ``wait``; the blocking forms ``encode_hash_sync`` /
     ``read_sync`` do both.  Shard g owns parts [g*n/G, (g+1)*n/G) of every job."""
 
+    WRITE = 1  # CEC_MULTI_WRITE
+    READ = 2  # CEC_MULTI_READ
+
     def __init__(self, codec: ReedSolomon, chunk_len: int, parts_per_batch: int, depth: int,
-                 devices: Sequence[int]):
+                 devices: Sequence[int], kinds: int = WRITE | READ):
+        """``kinds``: the job kinds (WRITE, READ) whose pipelines every shard makes here, once."""
         h = _vp()
         devs = (ctypes.c_int * max(len(devices), 1))(*devices)
-        code = _lib.cec_multi_new(codec.handle, chunk_len, parts_per_batch, depth, devs,
-                                  len(devices), ctypes.byref(h))
+        code = _lib.cec_multi_new_ex(codec.handle, chunk_len, parts_per_batch, depth, devs,
+                                     len(devices), kinds, ctypes.byref(h))
         if code != OK:
-            raise Error(code)
+            raise MultiError(code)
         self._h = h
         self.codec = codec
         self.d, self.p = codec.data_shard_count(), codec.parity_shard_count()
@@ -912,6 +979,18 @@ class Multi:
                                          ctypes.byref(parts)))
         return dev.value, numa.value, parts.value
 
+    def stats(self, g: int) -> dict:
+        """Shard g's counters (cec_multi_shard_stats)."""
+        st = MultiStatsStruct()
+        _check(_lib.cec_multi_shard_stats(self._h, g, ctypes.byref(st)))
+        return {name: getattr(st, name) for name, _ in MultiStatsStruct._fields_}
+
+    def carry_release(self, carry_id: int) -> None:
+        """Gives back a carry id this caller will not use (cec_multi_carry_release)."""
+        code = _lib.cec_multi_carry_release(self._h, int(carry_id))
+        if code != OK:
+            raise MultiError(code)
+
     def encode_hash(self, data, n_parts: int, parity, digests) -> int:
         job = ctypes.c_uint64(0)
         code = _lib.cec_multi_encode_hash(self._h, _addr(data), n_parts, _addr(parity),
@@ -922,17 +1001,32 @@ class Multi:
         return job.value
 
     def read(self, chunks, present, expected, n_parts: int, data, verified, status,
-             rebuilt_only: bool = False):
-        """Returns (job, data_ptrs) where data_ptrs ([n*d] c_void_p) is filled at wait()."""
+             rebuilt_only: bool = False, carry_in=None, carry_out=None):
+        """Returns (job, data_ptrs) where data_ptrs ([n*d] c_void_p) is filled at wait().
+        carry_out ([n] int32 numpy, nullable) receives, at wait(), a carry id for each part
+        reported TOO_FEW_SHARDS_PRESENT whose verified chunks stay on its GPU (-1: none);
+        carry_in ([n] int32, nullable) hands such ids to a retry: those parts' PRESENT_VERIFIED
+        chunks are taken from the GPU, not from `chunks` (cec_multi_read_carry)."""
+        import numpy as np
         job = ctypes.c_uint64(0)
         ptrs = (ctypes.c_void_p * max(n_parts * self.d, 1))()
-        code = _lib.cec_multi_read(self._h, _addr(chunks), _addr(present), _addr(expected),
-                                   n_parts, _addr(data), _addr(verified),
-                                   ctypes.cast(_addr(status), ctypes.POINTER(ctypes.c_int)),
-                                   ptrs, 1 if rebuilt_only else 0, ctypes.byref(job))
+        i32 = ctypes.POINTER(ctypes.c_int32)
+        cin = None
+        if carry_in is not None:
+            cin = np.ascontiguousarray(carry_in, dtype=np.int32)
+            assert len(cin) >= n_parts
+        if carry_out is not None:
+            assert carry_out.dtype == np.int32 and carry_out.flags.c_contiguous
+            assert len(carry_out) >= n_parts
+        code = _lib.cec_multi_read_carry(
+            self._h, _addr(chunks), _addr(present), _addr(expected), n_parts, _addr(data),
+            _addr(verified), ctypes.cast(_addr(status), ctypes.POINTER(ctypes.c_int)), ptrs,
+            1 if rebuilt_only else 0, cin.ctypes.data_as(i32) if cin is not None else None,
+            carry_out.ctypes.data_as(i32) if carry_out is not None else None, ctypes.byref(job))
         if code != OK:
             raise MultiError(code)
-        self._keep[job.value] = (chunks, present, expected, data, verified, status, ptrs)
+        self._keep[job.value] = (chunks, present, expected, data, verified, status, ptrs, cin,
+                                 carry_out)
         return job.value, ptrs
 
     def resilver(self, chunks, present, expected, n_parts: int, rebuilt, verified, status):

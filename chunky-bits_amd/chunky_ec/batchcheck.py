@@ -82,7 +82,8 @@ class BatchChecker:
     def __init__(self, data: int, parity: int, chunk_size: int, parts_per_batch: int, depth: int,
                  devices: List[int]):
         self.codec = ReedSolomon(data, parity)  # file_part.rs:302
-        self.multi = Multi(self.codec, chunk_size, parts_per_batch, depth, devices)
+        self.multi = Multi(self.codec, chunk_size, parts_per_batch, depth, devices,
+                           kinds=Multi.READ)
         self.d, self.p, self.t, self.L = data, parity, data + parity, chunk_size
         self.window = parts_per_batch * max(len(devices), 1)
         dev0 = devices[0] if devices else -1

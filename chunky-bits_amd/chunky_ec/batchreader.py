@@ -78,9 +78,13 @@ class _Window:
 
 class BatchReader:
     def __init__(self, data: int, parity: int, chunk_size: int, parts_per_batch: int, depth: int,
-                 devices: List[int]):
+                 devices: List[int], carry: bool = True):
+        """carry=False: retries send their verified chunks again instead of leaving them on the
+        GPU (the comparison tests/test_gpu_batchreader.py makes)."""
         self.codec = ReedSolomon(data, parity)  # file_part.rs:77
-        self.multi = Multi(self.codec, chunk_size, parts_per_batch, depth, devices)
+        self.multi = Multi(self.codec, chunk_size, parts_per_batch, depth, devices,
+                           kinds=Multi.READ)
+        self.use_carry = carry
         self.d, self.p, self.t, self.L = data, parity, data + parity, chunk_size
         self.window = parts_per_batch * max(len(devices), 1)
         dev0 = devices[0] if devices else -1
@@ -94,7 +98,10 @@ class BatchReader:
         # per chunk of the window: the next location to read, and whether none is left
         self.cursor = [np.zeros((W, t), np.int64) for _ in range(2)]
         self.exhausted = [np.zeros((W, t), bool) for _ in range(2)]
+        # per part of the window: the scheduler's carry id of its verified chunks (-1: none)
+        self.carry = [np.full(W, -1, np.int32) for _ in range(2)]
         self.retries = 0  # part resubmissions (a part retried twice counts twice)
+        self.carried_parts = 0  # retried parts whose verified chunks stayed on the GPU
 
     def read(self, n_parts: int, fetch: Fetch, digests: Callable[[int], np.ndarray],
              sink: Callable[[int, List[memoryview]], None]):
@@ -153,7 +160,8 @@ class BatchReader:
 
     def _submit(self, slot, cnt) -> int:
         job, _ = self.multi.read(self.chunks[slot], self.present[slot], self.expected[slot], cnt,
-                                 self.out[slot], self.verified[slot], self.status[slot])
+                                 self.out[slot], self.verified[slot], self.status[slot],
+                                 carry_out=self.carry[slot] if self.use_carry else None)
         return job
 
     def _collect(self, w: _Window, fetch, sink):
@@ -169,9 +177,10 @@ class BatchReader:
 
     def _retry(self, w: _Window, failed, fetch):
         """file_part.rs:92-107: the failed parts go again with the chunks that verified
-        (PRESENT_VERIFIED, taken from the window's buffer: the bytes that verified) plus, up to
-        d, the failed chunks' next copies and then untried chunks, until each decodes or runs out
-        of copies."""
+        (PRESENT_VERIFIED) plus, up to d, the failed chunks' next copies and then untried chunks,
+        until each decodes or runs out of copies.  The verified chunks stay on the GPU where the
+        scheduler kept them (the part's carry id: only the new chunks are sent), or, when it kept
+        none, are sent again from the window's buffer (the bytes that verified)."""
         d, t, L = self.d, self.t, self.L
         ch = self.chunks[w.slot].view(self.window, t, L)
         pres, ver = self.present[w.slot], self.verified[w.slot]
@@ -187,16 +196,32 @@ class BatchReader:
         rc, ro = np.zeros((f, t, L), np.uint8), np.zeros((f, d, L), np.uint8)
         r_pres, r_exp = np.zeros((f, t), np.uint8), np.zeros((f, t, 32), np.uint8)
         r_ver, r_st = np.zeros((f, t), np.uint8), np.zeros(f, np.int32)
+        r_cin, r_cout = np.full(f, -1, np.int32), np.full(f, -1, np.int32)
+        cid = {q: int(self.carry[w.slot][q]) if self.use_carry else -1 for q in failed}
         open_ = list(failed)
+        try:
+            self._retry_rounds(w, open_, fetch, tried, good, cursor, exhausted, keep, cid, rc, ro,
+                               r_pres, r_exp, r_ver, r_st, r_cin, r_cout, out)
+        except BaseException:
+            for q in open_:  # ids the failed read will not use go back to their GPUs
+                if cid[q] >= 0:
+                    self.multi.carry_release(cid[q])
+            raise
+
+    def _retry_rounds(self, w, open_, fetch, tried, good, cursor, exhausted, keep, cid, rc, ro,
+                      r_pres, r_exp, r_ver, r_st, r_cin, r_cout, out):
+        d, t, L = self.d, self.t, self.L
         while open_:
             g = len(open_)
             r_pres[:g] = 0
             for s, q in enumerate(open_):
                 r_exp[s] = self.expected[w.slot][q]
+                r_cin[s] = cid[q]
                 have = int(good[q].sum())
                 for i in range(t):
                     if good[q][i]:
-                        rc[s, i] = keep[q][i]
+                        if cid[q] < 0:  # not kept on the GPU: send the bytes that verified
+                            rc[s, i] = keep[q][i]
                         r_pres[s, i] = PRESENT_VERIFIED
                 added = 0
                 for i in draw_order(good[q], tried[q], exhausted[q]):
@@ -214,7 +239,11 @@ class BatchReader:
                     added += 1
                 if added == 0:
                     raise Error(TOO_FEW_SHARDS_PRESENT)
-            job, _ = self.multi.read(rc, r_pres, r_exp, g, ro, r_ver, r_st)
+            job, _ = self.multi.read(rc, r_pres, r_exp, g, ro, r_ver, r_st, carry_in=r_cin,
+                                     carry_out=r_cout if self.use_carry else None)
+            for s, q in enumerate(open_):  # submitted: the ids are the job's now
+                self.carried_parts += 1 if cid[q] >= 0 else 0
+                cid[q] = -1
             self.multi.wait(job)
             self.retries += g
             still = []
@@ -223,8 +252,9 @@ class BatchReader:
                 if r_st[s] == OK:
                     out[q] = ro[s]
                 else:
+                    cid[q] = int(r_cout[s])
                     still.append(q)
-            open_ = still
+            open_[:] = still
 
     def _drain(self, w: Optional[_Window]) -> None:
         if w is not None:

@@ -43,7 +43,8 @@ class BatchWriter:
     def __init__(self, data: int, parity: int, chunk_size: int, parts_per_batch: int, depth: int,
                  devices: List[int]):
         self.codec = ReedSolomon(data, parity)  # writer.rs:131
-        self.multi = Multi(self.codec, chunk_size, parts_per_batch, depth, devices)
+        self.multi = Multi(self.codec, chunk_size, parts_per_batch, depth, devices,
+                           kinds=Multi.WRITE)
         self.d, self.p, self.L = data, parity, chunk_size
         self.window = parts_per_batch * depth * max(len(devices), 1)
         dev0 = devices[0] if devices else -1

@@ -1,9 +1,11 @@
 // Environment knobs of the engine, read ONCE per process.
 //
-// Every A/B and test knob (CEC_APPLY_*, CEC_FUSED*, CEC_SHA_VARIANT, CEC_COALESCE_*,
-// CEC_READ_*, CEC_SPEC_LDS_KIB, CEC_VERIFY_COMPACT, CEC_MULTI_COPY_THREADS, CEC_SLOT_QUEUES)
-// is parsed into one immutable snapshot on first use; the launch paths read the snapshot, never
-// the environment.
+// Every knob is parsed into one immutable snapshot on first use; the launch paths read the
+// snapshot, never the environment.  The product library reads only capacity / diagnostic knobs
+// and the test knobs that force one of its own paths (CEC_APPLY_BS, CEC_APPLY_MAX_BLOCKS,
+// CEC_SHA_VARIANT 1/2, CEC_FUSED_MODE 3, CEC_FUSED, CEC_COALESCE_US / _MAX_MIB / _INFLIGHT /
+// _TRACE, CEC_IDLE_STAGING_MIB, CEC_MULTI_COPY_THREADS); the losing arms of finished A/B
+// experiments (the other fields below) are read only by the A/B build (-DCEC_AB_TOOLS).
 // The reference calls the hot path from tokio worker threads (writer.rs:200-210 spawns a task
 // per part; file_part.rs:161 runs the encode inside block_in_place), and getenv racing a setenv
 // elsewhere in the host process is undefined behaviour; a snapshot read is a plain load.
@@ -49,11 +51,8 @@ struct Knobs {
     bool read_speculate = true;          // CEC_READ_SPECULATE
     bool verify_compact = true;          // CEC_VERIFY_COMPACT
     size_t idle_staging_bytes = size_t(1) << 30;  // CEC_IDLE_STAGING_MIB (per device)
-    // pipeline.cpp / multi.cpp (read when a pipeline / scheduler is made)
-    bool read_side = false;              // CEC_READ_SIDE
-    bool read_upstream = false;          // CEC_READ_UPSTREAM
+    // multi.cpp
     unsigned multi_copy_threads = 4;     // CEC_MULTI_COPY_THREADS (1..32)
-    bool slot_queues = false;            // CEC_SLOT_QUEUES: a hardware queue per pipeline slot
 };
 
 // The current snapshot (parsed on first call).

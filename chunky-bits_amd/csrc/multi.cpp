@@ -9,13 +9,22 @@
 // part's own position, so results come back in file order without any reordering.
 //
 // One worker thread per shard (a device may carry several shards).  Each worker binds itself to
-// its device's NUMA node (hostmem.cpp) before allocating anything, owns a write and a read
-// pipeline of `depth` slots (pipeline.cpp, CEC_PIPE_EXTERNAL), and streams its range batch by
-// batch: caller buffers that are page-locked (cec_host_alloc) are DMA'd directly; pageable ones
-// go through the worker's own NUMA-local pinned staging.  Jobs are queued and run in submission
-// order; a worker keeps its batches in flight across job boundaries: with its queue empty it
-// completes batches as their events fire while watching the queue, so the next job of a stream
-// is queued behind the batches still running instead of after a drain (no bubble).
+// its device's NUMA node (hostmem.cpp), then makes its write and read pipelines of `depth` slots
+// (pipeline.cpp, CEC_PIPE_EXTERNAL) ONCE, before cec_multi_new returns: nothing creates streams
+// or device buffers while another shard's batches run (the round-5 deadlock, profiles/HISTORY.md).
+// Read, resilver and verify jobs use the same read pipeline, the mode picked per submit.  A worker
+// streams its share batch by batch: caller buffers that are page-locked (cec_host_alloc) are
+// DMA'd directly; pageable ones go through the worker's own NUMA-local pinned staging.  Jobs are
+// queued and run in submission order; a worker keeps its batches in flight across job
+// boundaries: with its queue empty it completes batches as their events fire while watching the
+// queue, so the next job of a stream is queued behind the batches still running instead of after
+// a drain (no bubble).
+//
+// Read retries keep their verified chunks on the device (file_part.rs:92-107 keeps them in
+// memory): the read pipeline's carry pool stashes the verified chunks of every part reported
+// TooFewShardsPresent; a job given carry_out gets an id per such part (shard << 20 | entry), and a
+// retry job given those ids as carry_in sends each carried part to the shard holding its chunks
+// and uploads only its new chunks.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -40,13 +49,17 @@ namespace {
 
 thread_local std::string g_multi_error;
 
+// scheduler carry id = shard << kCarryShift | the shard read pipeline's entry
+constexpr int kCarryShift = 20;
+constexpr int32_t kCarryEntryMask = (int32_t(1) << kCarryShift) - 1;
+
 enum class Kind { Write, Read };
 
 struct Job {
     uint64_t id = 0;
     Kind kind = Kind::Write;
     size_t n = 0;
-    unsigned flags = 0;
+    unsigned mode = 0;  // read: the read pipeline's mode bits for this job's submits
     // write
     const uint8_t* data = nullptr;
     uint8_t* parity = nullptr;
@@ -59,18 +72,25 @@ struct Job {
     uint8_t* verified = nullptr;
     int* status = nullptr;
     const uint8_t** data_ptrs = nullptr;
-    bool resilver = false;  // FilePart::resilver's compute: output [n][t][L], t pointers a part
-    bool verify_only = false;  // FilePart::verify's compute: verified flags only
+    const int32_t* carry_in = nullptr;  // [n] scheduler carry ids (-1 none), nullable
+    int32_t* carry_out = nullptr;       // [n] out, nullable
+    // per shard, the parts it runs (a job with carry_in: a carried part goes to the shard holding
+    // its chunks); empty: the contiguous ranges
+    std::vector<std::vector<uint32_t>> share;
     // completion
     size_t remaining = 0;  // parts not yet finished (guarded by cec_multi::mu)
     int result = CEC_OK;
     std::string error;
 };
 
+size_t out_chunks(unsigned mode, size_t d, size_t t) {
+    return (mode & CEC_READ_VERIFY_ONLY) ? 0 : (mode & CEC_READ_RESILVER) ? t : d;
+}
+
 // Pinned staging of one slot (pageable caller buffers only), NUMA-local to the worker.
 struct Staging {
-    uint8_t* in = nullptr;   // write: [P][d][L]; read: [P][t][L]
-    uint8_t* out = nullptr;  // write: [P][p][L]; read: [P][d][L]
+    uint8_t* in = nullptr;   // write: [P][d][L]; read: the packed uploaded chunks
+    uint8_t* out = nullptr;  // write: [P][p][L]; read: [P][d or d+p][L]
     size_t in_cap = 0, out_cap = 0;
     void release() {
         if (in) (void)hipHostFree(in);
@@ -136,9 +156,11 @@ void parallel_copy(uint8_t* dst, const uint8_t* src, size_t n) {
 // A batch in flight on one slot of a shard's pipeline.
 struct InFlight {
     Job* job = nullptr;
-    size_t first = 0, n = 0;  // parts [first, first + n) of the job
+    size_t first = 0, n = 0;        // parts [first, first + n) of the job (idx == nullptr)
+    const uint32_t* idx = nullptr;  // else: the job's parts idx[0..n)
     bool staged_in = false, staged_out = false;
     bool direct_dig = false;  // write: digests DMA'd straight into the job's buffer
+    size_t pos(size_t k) const { return idx ? idx[k] : first + k; }
 };
 
 }  // namespace
@@ -154,17 +176,25 @@ struct Shard {
     int numa = -1;
     bool bound = false;
     std::thread th;
-    std::deque<Job*> queue;  // guarded by cec_multi::mu
+    std::deque<Job*> queue;         // guarded by cec_multi::mu
+    std::vector<int32_t> releases;  // carry entries to give back (guarded by cec_multi::mu)
     std::atomic<uint64_t> parts{0};
+    std::atomic<uint64_t> pipelines_made{0};
+    std::atomic<uint64_t> chunks_uploaded{0};
+    std::atomic<uint64_t> chunks_carried{0};
+    std::atomic<uint64_t> carry_held{0};
     // worker-thread state
     cec_pipeline* wp = nullptr;
     cec_read_pipeline* rp = nullptr;
-    unsigned rp_flags = 0;
     Kind active = Kind::Write;
     std::vector<InFlight> wslots, rslots;
     std::deque<size_t> worder, rorder;  // slots in flight, oldest first
     std::vector<Staging> wstage, rstage;
-    std::vector<const uint8_t*> ptrs;  // read: data chunk locations of one batch
+    std::vector<const uint8_t*> ptrs;  // read: output chunk locations of one batch
+    std::vector<int32_t> ids;          // read: carry ids of one batch
+    // gathered per-batch arrays of a non-contiguous batch (copied in at submit)
+    std::vector<uint8_t> g_present, g_expected;
+    std::vector<int32_t> g_carry;
 };
 
 }  // namespace
@@ -172,10 +202,14 @@ struct Shard {
 struct cec_multi {
     const cec_codec* codec = nullptr;
     size_t d = 0, p = 0, t = 0, L = 0, P = 0, depth = 0;
+    unsigned kinds = 0;  // CEC_MULTI_WRITE | CEC_MULTI_READ
     std::vector<std::unique_ptr<Shard>> shards;
     std::mutex mu;
-    std::condition_variable work_cv, done_cv;
+    std::condition_variable work_cv, done_cv, ready_cv;
     bool stop = false;
+    size_t ready = 0;  // workers done making their pipelines (guarded by mu)
+    int init_status = CEC_OK;
+    std::string init_error;
     uint64_t next_id = 1;
     std::map<uint64_t, std::unique_ptr<Job>> jobs;  // submitted, not yet waited for
 
@@ -190,34 +224,33 @@ struct cec_multi {
         if (job->remaining == 0) done_cv.notify_all();
     }
 
-    // ---- per-shard work ----
-    int ensure_write_pipe(Shard& s) {
-        if (s.wp) return CEC_OK;
-        int st = cec_pipeline_new_ex(codec, L, P, depth, CEC_PIPE_EXTERNAL, &s.wp);
-        if (st != CEC_OK) g_multi_error = cec_pipeline_last_error();
-        s.wslots.assign(depth, InFlight{});
-        s.wstage.resize(depth);
-        return st;
-    }
-
-    int ensure_read_pipe(Shard& s, unsigned flags, bool resilver, bool verify_only) {
-        const unsigned want = (flags & CEC_READ_REBUILT_ONLY) | CEC_PIPE_EXTERNAL |
-                              (resilver ? CEC_READ_RESILVER : 0u) |
-                              (verify_only ? CEC_READ_VERIFY_ONLY : 0u);
-        if (s.rp && s.rp_flags == want) return CEC_OK;
-        if (s.rp) {
-            drain_read(s);
-            cec_read_pipeline_free(s.rp);
-            s.rp = nullptr;
+    // ---- the shard's pipelines, made once when the worker starts ----
+    int make_pipelines(Shard& s, std::string& err) {
+        if (kinds & CEC_MULTI_WRITE) {
+            const int st = cec_pipeline_new_ex(codec, L, P, depth, CEC_PIPE_EXTERNAL, &s.wp);
+            if (st != CEC_OK) {
+                err = std::string("write pipeline: ") + cec_pipeline_last_error();
+                return st;
+            }
+            s.pipelines_made.fetch_add(1);
+            s.wslots.assign(depth, InFlight{});
+            s.wstage.resize(depth);
         }
-        int st = cec_read_pipeline_new_ex(codec, L, P, depth, want, &s.rp);
-        if (st != CEC_OK) g_multi_error = cec_pipeline_last_error();
-        s.rp_flags = want;
-        s.rslots.assign(depth, InFlight{});
-        s.rstage.resize(depth);
-        return st;
+        if (kinds & CEC_MULTI_READ) {
+            const int st = cec_read_pipeline_new_ex(codec, L, P, depth,
+                                                    CEC_PIPE_EXTERNAL | CEC_READ_CARRY, &s.rp);
+            if (st != CEC_OK) {
+                err = std::string("read pipeline: ") + cec_pipeline_last_error();
+                return st;
+            }
+            s.pipelines_made.fetch_add(1);
+            s.rslots.assign(depth, InFlight{});
+            s.rstage.resize(depth);
+        }
+        return CEC_OK;
     }
 
+    // ---- per-shard work ----
     void finish_write(Shard& s, size_t slot) {
         InFlight& f = s.wslots[slot];
         if (!f.job) return;
@@ -247,24 +280,33 @@ struct cec_multi {
         const int* status = nullptr;
         size_t got = 0;
         Job* job = f.job;
-        // chunks per part in the output / pointer table: d (read) or t (resilver)
-        const size_t W = (s.rp_flags & CEC_READ_RESILVER) ? t : d;
-        const bool verify_only = (s.rp_flags & CEC_READ_VERIFY_ONLY) != 0;
+        const size_t W = out_chunks(job->mode, d, t);  // output chunks per part
         int st = cec_read_pipeline_wait(s.rp, slot, &data, &ver, &status, &got);
-        if (st == CEC_OK && !verify_only) {
+        if (st == CEC_OK && W) {
             s.ptrs.resize(f.n * W);
-            st = cec_read_pipeline_data_chunks(s.rp, slot, s.ptrs.data());
+            st = cec_read_pipeline_data_chunks(s.rp, slot, s.ptrs.data(), s.ptrs.size());
+        }
+        // a read job given carry_out takes its parts' carry entries (the others go back when the
+        // slot is submitted again)
+        if (st == CEC_OK && job->carry_out) {
+            s.ids.assign(f.n, -1);
+            st = cec_read_pipeline_carry_ids(s.rp, slot, s.ids.data(), s.ids.size());
+            for (size_t k = 0; st == CEC_OK && k < f.n; ++k)
+                job->carry_out[f.pos(k)] =
+                    s.ids[k] < 0 ? -1 : int32_t(s.index << kCarryShift) | s.ids[k];
         }
         std::string err = st == CEC_OK ? std::string() : cec_pipeline_last_error();
-        if (st == CEC_OK && verify_only) {
-            std::memcpy(job->verified + f.first * t, ver, f.n * t);
-        } else if (st == CEC_OK) {
-            std::memcpy(job->verified + f.first * t, ver, f.n * t);
-            std::memcpy(job->status + f.first, status, f.n * sizeof(int));
+        if (st == CEC_OK) {
+            for (size_t k = 0; k < f.n; ++k) {
+                std::memcpy(job->verified + f.pos(k) * t, ver + k * t, t);
+                if (job->status) job->status[f.pos(k)] = status[k];
+            }
+        }
+        if (st == CEC_OK && W) {
             const bool staged = f.staged_in || f.staged_out;
             parallel_for(f.n, staged ? f.n * W * L : 0, [&](size_t k) {
                 for (size_t j = 0; j < W; ++j) {
-                    const size_t q = (f.first + k) * W + j;
+                    const size_t q = f.pos(k) * W + j;
                     const uint8_t* src = s.ptrs[k * W + j];
                     uint8_t* dst = job->out_data + q * L;
                     if (staged) {
@@ -277,6 +319,7 @@ struct cec_multi {
                 }
             });
         }
+        s.carry_held.store(cec_read_pipeline_carry_held(s.rp), std::memory_order_relaxed);
         s.parts.fetch_add(f.n, std::memory_order_relaxed);
         const size_t n = f.n;
         f = InFlight{};
@@ -297,6 +340,19 @@ struct cec_multi {
     }
     bool in_flight(const Shard& s) const { return !s.worder.empty() || !s.rorder.empty(); }
 
+    // Carry entries the caller gave back (cec_multi_carry_release), applied on the worker: the
+    // pipeline is the worker's alone.
+    void apply_releases(Shard& s) {
+        std::vector<int32_t> ids;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            ids.swap(s.releases);
+        }
+        if (ids.empty() || !s.rp) return;
+        for (int32_t id : ids) (void)cec_read_pipeline_carry_release(s.rp, id);
+        s.carry_held.store(cec_read_pipeline_carry_held(s.rp), std::memory_order_relaxed);
+    }
+
     // Finish the oldest batch in flight if it is complete; never blocks.  False when it is still
     // running (or nothing is in flight).
     bool finish_oldest_if_done(Shard& s) {
@@ -316,8 +372,6 @@ struct cec_multi {
     }
 
     void run_write(Shard& s, Job* job, size_t lo, size_t hi) {
-        int st = ensure_write_pipe(s);
-        if (st != CEC_OK) return finish_parts(job, hi - lo, st, g_multi_error);
         if (s.active != Kind::Write) drain_read(s);
         s.active = Kind::Write;
         const size_t dw = d * L, pw = p * L;
@@ -325,7 +379,7 @@ struct cec_multi {
             const size_t n = std::min(P, hi - first);
             size_t slot = 0;
             uint8_t* unused = nullptr;
-            st = cec_pipeline_acquire(s.wp, &slot, &unused);
+            int st = cec_pipeline_acquire(s.wp, &slot, &unused);
             if (st != CEC_OK) {
                 finish_parts(job, hi - first, st, cec_pipeline_last_error());
                 return;
@@ -371,30 +425,67 @@ struct cec_multi {
         }
     }
 
+    // The shard's parts of a read job: the list of a carried job, else [lo, hi).
     void run_read(Shard& s, Job* job, size_t lo, size_t hi) {
-        int st = ensure_read_pipe(s, job->flags, job->resilver, job->verify_only);
-        if (st != CEC_OK) return finish_parts(job, hi - lo, st, g_multi_error);
+        apply_releases(s);
         if (s.active != Kind::Read) drain_write(s);
         s.active = Kind::Read;
-        const size_t cw = t * L, dw = (job->resilver ? t : d) * L;  // output per part
-        for (size_t first = lo; first < hi; first += P) {
-            const size_t n = std::min(P, hi - first);
+        const std::vector<uint32_t>* list = job->share.empty() ? nullptr : &job->share[s.index];
+        const size_t count = list ? list->size() : hi - lo;
+        const size_t W = out_chunks(job->mode, d, t);
+        const size_t cw = t * L, dw = W * L;  // input / output bytes per part
+        for (size_t at = 0; at < count; at += P) {
+            const size_t n = std::min(P, count - at);
             size_t slot = 0;
             uint8_t *c = nullptr, *pr = nullptr, *ex = nullptr;
-            st = cec_read_pipeline_acquire(s.rp, &slot, &c, &pr, &ex);
+            int st = cec_read_pipeline_acquire(s.rp, &slot, &c, &pr, &ex);
             if (st != CEC_OK) {
-                finish_parts(job, hi - first, st, cec_pipeline_last_error());
+                finish_parts(job, count - at, st, cec_pipeline_last_error());
                 return;
             }
             finish_read(s, slot);
             InFlight f;
             f.job = job;
-            f.first = first;
             f.n = n;
-            const uint8_t* src = job->chunks + first * cw;
-            uint8_t* dst = job->verify_only ? nullptr : job->out_data + first * dw;
-            f.staged_in = !cec::pinned_range(src, n * cw);
-            f.staged_out = !job->verify_only && !cec::pinned_range(dst, n * dw);
+            const uint32_t* ix = list ? list->data() + at : nullptr;
+            const bool contiguous = !ix || size_t(ix[n - 1] - ix[0]) == n - 1;
+            f.first = ix ? ix[0] : lo + at;
+            f.idx = contiguous ? nullptr : ix;
+            // the batch's flags and digests: the job's own rows, or gathered for a list batch
+            const uint8_t* prs = job->present + f.first * t;
+            const uint8_t* exs = job->expected + f.first * t * 32;
+            if (!contiguous) {
+                s.g_present.resize(n * t);
+                s.g_expected.resize(n * t * 32);
+                for (size_t k = 0; k < n; ++k) {
+                    std::memcpy(s.g_present.data() + k * t, job->present + f.pos(k) * t, t);
+                    std::memcpy(s.g_expected.data() + k * t * 32,
+                                job->expected + f.pos(k) * t * 32, t * 32);
+                }
+                prs = s.g_present.data();
+                exs = s.g_expected.data();
+            }
+            // carry ids of this shard's entries (routing sent every carried part here)
+            const int32_t* cin = nullptr;
+            if (job->carry_in) {
+                s.g_carry.assign(n, -1);
+                for (size_t k = 0; k < n; ++k) {
+                    const int32_t id = job->carry_in[f.pos(k)];
+                    if (id >= 0) {
+                        s.g_carry[k] = id & kCarryEntryMask;
+                        cin = s.g_carry.data();
+                    }
+                }
+            }
+            auto carried = [&](size_t k) { return cin && cin[k] >= 0; };
+            auto uploaded = [&](size_t k, size_t i) {
+                const uint8_t fl = prs[k * t + i];
+                return fl && !(carried(k) && fl == CEC_PRESENT_VERIFIED);
+            };
+            const uint8_t* src = job->chunks + f.first * cw;
+            uint8_t* dst = W ? job->out_data + f.first * dw : nullptr;
+            f.staged_in = !contiguous || !cec::pinned_range(src, n * cw);
+            f.staged_out = W && (!contiguous || !cec::pinned_range(dst, n * dw));
             Staging& sg = s.rstage[slot];
             if (f.staged_in || f.staged_out) {
                 hipError_t e = hipSuccess;  // every slot at once (see run_write)
@@ -403,38 +494,45 @@ struct cec_multi {
                         e = each.reserve(f.staged_in ? P * cw : 0, f.staged_out ? P * dw : 0,
                                          s.device);
                 if (e != hipSuccess) {
-                    finish_parts(job, hi - first, CEC_ERR_OUT_OF_MEMORY,
+                    finish_parts(job, count - at, CEC_ERR_OUT_OF_MEMORY,
                                  std::string("multi staging: ") + hipGetErrorString(e));
                     return;
                 }
             }
+            size_t up = 0, kept = 0;
+            for (size_t k = 0; k < n; ++k)
+                for (size_t i = 0; i < t; ++i) {
+                    up += uploaded(k, i) ? 1 : 0;
+                    kept += carried(k) && prs[k * t + i] == CEC_PRESENT_VERIFIED ? 1 : 0;
+                }
+            cec_read_submit a{src, prs, exs, n, f.staged_out ? sg.out : dst, cin, job->mode};
             if (f.staged_in) {
-                // only the loaded chunks are staged, packed back to back (part by part, index
-                // ascending): the batch then goes up as one copy (submit_packed)
-                const uint8_t* prs = job->present + first * t;
-                std::vector<size_t> at(n + 1, 0);
-                for (size_t k = 0; k < n; ++k)
-                    at[k + 1] = at[k] + size_t(std::count_if(prs + k * t, prs + (k + 1) * t,
-                                                             [](uint8_t x) { return x != 0; }));
-                const uint8_t* from = src;
+                // only the uploaded chunks are staged, packed back to back (part by part, index
+                // ascending): the batch then goes up as one copy (CEC_SUBMIT_PACKED)
+                std::vector<size_t> at_k(n + 1, 0);
+                for (size_t k = 0; k < n; ++k) {
+                    size_t m = 0;
+                    for (size_t i = 0; i < t; ++i) m += uploaded(k, i) ? 1 : 0;
+                    at_k[k + 1] = at_k[k] + m;
+                }
                 uint8_t* to = sg.in;
                 parallel_for(n, n * cw, [&](size_t k) {
-                    size_t pos = at[k];
-                    for (size_t i = k * t; i < (k + 1) * t; ++i)
-                        if (prs[i]) std::memcpy(to + (pos++) * L, from + i * L, L);
+                    size_t q = at_k[k];
+                    const uint8_t* from = job->chunks + f.pos(k) * cw;
+                    for (size_t i = 0; i < t; ++i)
+                        if (uploaded(k, i)) std::memcpy(to + (q++) * L, from + i * L, L);
                 });
-                st = cec_read_pipeline_submit_packed(s.rp, slot, sg.in, prs,
-                                                     job->expected + first * t * 32, n,
-                                                     f.staged_out ? sg.out : dst);
-            } else {
-                st = cec_read_pipeline_submit_from(s.rp, slot, src, job->present + first * t,
-                                                   job->expected + first * t * 32, n,
-                                                   f.staged_out ? sg.out : dst);
+                a.chunks = sg.in;
+                a.flags |= CEC_SUBMIT_PACKED;
             }
+            st = cec_read_pipeline_submit_ex(s.rp, slot, &a);
             if (st != CEC_OK) {
-                finish_parts(job, hi - first, st, cec_pipeline_last_error());
+                finish_parts(job, count - at, st, cec_pipeline_last_error());
                 return;
             }
+            s.chunks_uploaded.fetch_add(up, std::memory_order_relaxed);
+            s.chunks_carried.fetch_add(kept, std::memory_order_relaxed);
+            s.carry_held.store(cec_read_pipeline_carry_held(s.rp), std::memory_order_relaxed);
             s.rslots[slot] = f;
             s.rorder.push_back(slot);
         }
@@ -442,9 +540,22 @@ struct cec_multi {
 
     void worker(Shard& s) {
         s.bound = cec::bind_thread_to_device_node(s.device);
-        if (hipSetDevice(s.device) != hipSuccess) (void)hipGetLastError();
+        std::string err;
+        int st = hipSetDevice(s.device) == hipSuccess ? CEC_OK : CEC_ERR_HIP;
+        if (st != CEC_OK) err = "hipSetDevice failed";
+        if (st == CEC_OK) st = make_pipelines(s, err);
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            ++ready;
+            if (st != CEC_OK && init_status == CEC_OK) {
+                init_status = st;
+                init_error = err;
+            }
+        }
+        ready_cv.notify_all();
         const size_t G = shards.size();
         for (;;) {
+            if (st != CEC_OK) break;  // cec_multi_new fails and frees the scheduler
             Job* job = nullptr;
             {
                 std::unique_lock<std::mutex> lk(mu);
@@ -466,10 +577,8 @@ struct cec_multi {
                 s.queue.pop_front();
             }
             const size_t lo = job->n * s.index / G, hi = job->n * (s.index + 1) / G;
-            if (hi > lo) {
-                if (job->kind == Kind::Write) run_write(s, job, lo, hi);
-                else run_read(s, job, lo, hi);
-            }
+            if (job->kind == Kind::Write) run_write(s, job, lo, hi);
+            else run_read(s, job, lo, hi);
         }
         drain(s);
         if (s.wp) cec_pipeline_free(s.wp);
@@ -480,7 +589,30 @@ struct cec_multi {
         s.rp = nullptr;
     }
 
+    // The shard of part k under the contiguous split of an n-part job.
+    size_t range_shard(size_t k, size_t n) const {
+        const size_t G = shards.size();
+        size_t g = k * G / n;
+        while (g + 1 < G && n * (g + 1) / G <= k) ++g;
+        while (g > 0 && n * g / G > k) --g;
+        return g;
+    }
+
     int submit(std::unique_ptr<Job> job, uint64_t* id) {
+        const size_t G = shards.size();
+        if (job->carry_in && job->n) {
+            // a carried part runs on the shard whose pool holds its chunks; the others as usual
+            job->share.assign(G, {});
+            for (size_t k = 0; k < job->n; ++k) {
+                const int32_t c = job->carry_in[k];
+                const size_t g = c >= 0 ? size_t(c >> kCarryShift) : range_shard(k, job->n);
+                if (g >= G) {
+                    g_multi_error = "carry id of no shard of this scheduler";
+                    return CEC_ERR_INVALID_ARGUMENT;
+                }
+                job->share[g].push_back(uint32_t(k));
+            }
+        }
         std::lock_guard<std::mutex> lk(mu);
         job->id = next_id++;
         job->remaining = job->n;
@@ -488,11 +620,13 @@ struct cec_multi {
         Job* raw = job.get();
         jobs.emplace(raw->id, std::move(job));
         if (raw->n == 0) return CEC_OK;
-        // Only shards with a non-empty range get the job: once the others have finished, the
-        // caller may free it, and a shard popping it later would read freed memory.
-        const size_t G = shards.size();
-        for (size_t g = 0; g < G; ++g)
-            if (raw->n * (g + 1) / G > raw->n * g / G) shards[g]->queue.push_back(raw);
+        // Only shards with parts get the job: once the others have finished, the caller may free
+        // it, and a shard popping it later would read freed memory.
+        for (size_t g = 0; g < G; ++g) {
+            const bool any = raw->share.empty() ? raw->n * (g + 1) / G > raw->n * g / G
+                                                : !raw->share[g].empty();
+            if (any) shards[g]->queue.push_back(raw);
+        }
         work_cv.notify_all();
         return CEC_OK;
     }
@@ -512,10 +646,12 @@ extern "C" {
 
 const char* cec_multi_last_error(void) { return g_multi_error.c_str(); }
 
-int cec_multi_new(const cec_codec* codec, size_t chunk_len, size_t parts_per_batch, size_t depth,
-                  const int* devices, size_t n_devices, cec_multi** out) {
+int cec_multi_new_ex(const cec_codec* codec, size_t chunk_len, size_t parts_per_batch,
+                     size_t depth, const int* devices, size_t n_devices, unsigned flags,
+                     cec_multi** out) {
     if (!codec || !out || chunk_len == 0 || parts_per_batch == 0 || depth == 0 || depth > 16 ||
-        !devices || n_devices == 0 || n_devices > 64)
+        !devices || n_devices == 0 || n_devices > 64 || flags == 0 ||
+        (flags & ~unsigned(CEC_MULTI_WRITE | CEC_MULTI_READ)))
         return CEC_ERR_INVALID_ARGUMENT;
     *out = nullptr;
     const int count = cec_device_count();
@@ -530,6 +666,7 @@ int cec_multi_new(const cec_codec* codec, size_t chunk_len, size_t parts_per_bat
     m->L = chunk_len;
     m->P = parts_per_batch;
     m->depth = depth;
+    m->kinds = flags;
     for (size_t g = 0; g < n_devices; ++g) {
         auto s = std::make_unique<Shard>();
         s->owner = m.get();
@@ -543,8 +680,23 @@ int cec_multi_new(const cec_codec* codec, size_t chunk_len, size_t parts_per_bat
         cec_multi* mp = m.get();
         sp->th = std::thread([mp, sp] { mp->worker(*sp); });
     }
+    // every worker has made its pipelines (or failed) before the scheduler is handed out
+    int st = CEC_OK;
+    {
+        std::unique_lock<std::mutex> lk(m->mu);
+        m->ready_cv.wait(lk, [&] { return m->ready == m->shards.size(); });
+        st = m->init_status;
+        if (st != CEC_OK) g_multi_error = m->init_error;
+    }
+    if (st != CEC_OK) return st;  // m's destructor stops and joins the workers
     *out = m.release();
     return CEC_OK;
+}
+
+int cec_multi_new(const cec_codec* codec, size_t chunk_len, size_t parts_per_batch, size_t depth,
+                  const int* devices, size_t n_devices, cec_multi** out) {
+    return cec_multi_new_ex(codec, chunk_len, parts_per_batch, depth, devices, n_devices,
+                            CEC_MULTI_WRITE | CEC_MULTI_READ, out);
 }
 
 void cec_multi_free(cec_multi* m) { delete m; }
@@ -560,9 +712,26 @@ int cec_multi_shard_info(cec_multi* m, size_t g, int* device, int* numa_node, ui
     return CEC_OK;
 }
 
+int cec_multi_shard_stats(cec_multi* m, size_t g, cec_multi_stats* out) {
+    if (!m || !out || g >= m->shards.size()) return CEC_ERR_INVALID_ARGUMENT;
+    const Shard& s = *m->shards[g];
+    out->device = s.device;
+    out->numa_node = s.numa;
+    out->parts = s.parts.load();
+    out->pipelines_made = s.pipelines_made.load();
+    out->chunks_uploaded = s.chunks_uploaded.load();
+    out->chunks_carried = s.chunks_carried.load();
+    out->carry_held = s.carry_held.load();
+    return CEC_OK;
+}
+
 int cec_multi_encode_hash(cec_multi* m, const uint8_t* data, size_t n_parts, uint8_t* parity,
                           uint8_t* digests, uint64_t* job) {
     if (!m || !job || (n_parts && (!data || !parity || !digests))) return CEC_ERR_INVALID_ARGUMENT;
+    if (!(m->kinds & CEC_MULTI_WRITE)) {
+        g_multi_error = "scheduler made without CEC_MULTI_WRITE";
+        return CEC_ERR_INVALID_ARGUMENT;
+    }
     auto j = std::make_unique<Job>();
     j->kind = Kind::Write;
     j->n = n_parts;
@@ -572,17 +741,22 @@ int cec_multi_encode_hash(cec_multi* m, const uint8_t* data, size_t n_parts, uin
     return m->submit(std::move(j), job);
 }
 
-int cec_multi_read(cec_multi* m, const uint8_t* chunks, const uint8_t* present,
-                   const uint8_t* expected, size_t n_parts, uint8_t* data, uint8_t* verified,
-                   int* part_status, const uint8_t** data_ptrs, unsigned flags, uint64_t* job) {
+int cec_multi_read_carry(cec_multi* m, const uint8_t* chunks, const uint8_t* present,
+                         const uint8_t* expected, size_t n_parts, uint8_t* data, uint8_t* verified,
+                         int* part_status, const uint8_t** data_ptrs, unsigned flags,
+                         const int32_t* carry_in, int32_t* carry_out, uint64_t* job) {
     if (!m || !job || (flags & ~unsigned(CEC_READ_REBUILT_ONLY))) return CEC_ERR_INVALID_ARGUMENT;
     if (n_parts && (!chunks || !present || !expected || !data || !verified || !part_status))
         return CEC_ERR_INVALID_ARGUMENT;
     if ((flags & CEC_READ_REBUILT_ONLY) && !data_ptrs) return CEC_ERR_INVALID_ARGUMENT;
+    if (!(m->kinds & CEC_MULTI_READ)) {
+        g_multi_error = "scheduler made without CEC_MULTI_READ";
+        return CEC_ERR_INVALID_ARGUMENT;
+    }
     auto j = std::make_unique<Job>();
     j->kind = Kind::Read;
     j->n = n_parts;
-    j->flags = flags;
+    j->mode = flags & CEC_READ_REBUILT_ONLY;
     j->chunks = chunks;
     j->present = present;
     j->expected = expected;
@@ -590,7 +764,29 @@ int cec_multi_read(cec_multi* m, const uint8_t* chunks, const uint8_t* present,
     j->verified = verified;
     j->status = part_status;
     j->data_ptrs = data_ptrs;
+    j->carry_in = carry_in;
+    j->carry_out = carry_out;
+    if (carry_out)
+        for (size_t k = 0; k < n_parts; ++k) carry_out[k] = -1;
     return m->submit(std::move(j), job);
+}
+
+int cec_multi_read(cec_multi* m, const uint8_t* chunks, const uint8_t* present,
+                   const uint8_t* expected, size_t n_parts, uint8_t* data, uint8_t* verified,
+                   int* part_status, const uint8_t** data_ptrs, unsigned flags, uint64_t* job) {
+    return cec_multi_read_carry(m, chunks, present, expected, n_parts, data, verified, part_status,
+                                data_ptrs, flags, nullptr, nullptr, job);
+}
+
+int cec_multi_carry_release(cec_multi* m, int32_t id) {
+    if (!m || id < 0 || size_t(id >> kCarryShift) >= m->shards.size())
+        return CEC_ERR_INVALID_ARGUMENT;
+    {
+        std::lock_guard<std::mutex> lk(m->mu);
+        m->shards[size_t(id >> kCarryShift)]->releases.push_back(id & kCarryEntryMask);
+    }
+    m->work_cv.notify_all();
+    return CEC_OK;
 }
 
 int cec_multi_resilver(cec_multi* m, const uint8_t* chunks, const uint8_t* present,
@@ -600,9 +796,13 @@ int cec_multi_resilver(cec_multi* m, const uint8_t* chunks, const uint8_t* prese
     if (!m || !job) return CEC_ERR_INVALID_ARGUMENT;
     if (n_parts && (!chunks || !present || !expected || !rebuilt || !verified || !part_status))
         return CEC_ERR_INVALID_ARGUMENT;
+    if (!(m->kinds & CEC_MULTI_READ)) {
+        g_multi_error = "scheduler made without CEC_MULTI_READ";
+        return CEC_ERR_INVALID_ARGUMENT;
+    }
     auto j = std::make_unique<Job>();
     j->kind = Kind::Read;
-    j->resilver = true;
+    j->mode = CEC_READ_RESILVER;
     j->n = n_parts;
     j->chunks = chunks;
     j->present = present;
@@ -618,9 +818,13 @@ int cec_multi_verify(cec_multi* m, const uint8_t* chunks, const uint8_t* present
                      const uint8_t* expected, size_t n_parts, uint8_t* verified, uint64_t* job) {
     if (!m || !job) return CEC_ERR_INVALID_ARGUMENT;
     if (n_parts && (!chunks || !present || !expected || !verified)) return CEC_ERR_INVALID_ARGUMENT;
+    if (!(m->kinds & CEC_MULTI_READ)) {
+        g_multi_error = "scheduler made without CEC_MULTI_READ";
+        return CEC_ERR_INVALID_ARGUMENT;
+    }
     auto j = std::make_unique<Job>();
     j->kind = Kind::Read;
-    j->verify_only = true;
+    j->mode = CEC_READ_VERIFY_ONLY;
     j->n = n_parts;
     j->chunks = chunks;
     j->present = present;

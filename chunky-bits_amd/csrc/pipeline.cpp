@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <deque>
 #include <cstring>
@@ -23,7 +24,6 @@
 #include "chunky_ec.h"
 #include "hostmem.hpp"
 #include "kernels.hpp"
-#include "knobs.hpp"
 
 namespace {
 
@@ -62,26 +62,19 @@ class DeviceGuard {
     hipError_t err_ = hipSuccess;
 };
 
-// A slot's stream.  HIP maps streams onto GPU_MAX_HW_QUEUES (4 by default) hardware queues per
-// process, the null stream included, so `depth` slot streams made with hipStreamCreate can land
-// two slots on one queue: the later slot's next batch then waits in that queue behind the whole
-// of the other's batch (measured: the first 4-deep read pipeline of a process had slots 2 and 3
-// on one queue; with CEC_READ_CARRY that pipeline ran 24% slower than the second).  A CU-masked
-// stream gets a hardware queue of its own (the mask names every CU, so the kernels see the whole
-// GPU), but making one while other queues of the process are busy deadlocked inside the HIP
-// runtime (a scheduler worker blocked in hipExtStreamCreateWithCUMask on a lock the runtime's
-// event thread held, profiles/r5_queues/), so plain streams stay the default and CU-masked ones
-// are the CEC_SLOT_QUEUES=1 A/B only.  HIP makes them blocking (no flags argument): null-stream
-// work would order against the slots' batches.
-hipError_t slot_stream(hipStream_t* stream, int device) {
-    if (!cec::knobs().slot_queues) return hipStreamCreateWithFlags(stream, hipStreamNonBlocking);
-    int cus = 0;
-    hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-    if (e != hipSuccess) return e;
-    std::vector<uint32_t> mask((size_t(cus) + 31) / 32, ~0u);
-    if (cus % 32) mask.back() = (1u << (cus % 32)) - 1;
-    return hipExtStreamCreateWithCUMask(stream, uint32_t(mask.size()), mask.data());
+// A slot's stream: a plain non-blocking stream.  HIP maps streams onto GPU_MAX_HW_QUEUES (4 by
+// default) hardware queues per process, so two slots can share a queue; the carry stash is queued
+// in the batch's own stream for that reason (see cec_read_pipeline::carry_stash).  Streams are
+// made only when a pipeline is made, and a cec_multi makes its pipelines before any job runs
+// (multi.cpp): making streams while other queues of the process were busy is what deadlocked the
+// round-5 scheduler (profiles/HISTORY.md, "slot queues").
+hipError_t slot_stream(hipStream_t* stream) {
+    return hipStreamCreateWithFlags(stream, hipStreamNonBlocking);
 }
+
+// Pipelines made by this process (both kinds): tests check that a scheduler makes its pipelines
+// once, up front (cec_pipelines_made).
+std::atomic<uint64_t> g_pipelines_made{0};
 
 struct Slot {
     uint8_t* h_data = nullptr;    // pinned [parts][d][L] (null with CEC_PIPE_EXTERNAL)
@@ -204,16 +197,19 @@ int cec_pipeline_new_ex(const cec_codec* codec, size_t chunk_len, size_t parts_p
         host(&s.h_dig, pl->parts * pl->t * 32);
         if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_buf), pl->parts * pl->t * pl->cs);
         if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_dig), pl->parts * pl->t * 32);
-        if (e == hipSuccess) e = slot_stream(&s.stream, pl->device);
+        if (e == hipSuccess) e = slot_stream(&s.stream);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
         if (e != hipSuccess) {
             delete pl;
             return pipe_fail(e, "cec_pipeline_new allocation");
         }
     }
+    g_pipelines_made.fetch_add(1, std::memory_order_relaxed);
     *out = pl;
     return CEC_OK;
 }
+
+uint64_t cec_pipelines_made(void) { return g_pipelines_made.load(std::memory_order_relaxed); }
 
 void cec_pipeline_free(cec_pipeline* pl) { delete pl; }
 
@@ -295,6 +291,7 @@ int cec_pipeline_drain(cec_pipeline* pl) {
 
 }  // extern "C"
 
+
 // ------------------------------------------------------------------------------------------
 // Read pipeline (cec_read_pipeline_*): the batched form of FileReadBuilder's part loop
 // (reference src/file/reader.rs:40-75, buffered(5) reads of FilePart::read_with_context,
@@ -302,22 +299,29 @@ int cec_pipeline_drain(cec_pipeline* pl) {
 // metadata digests, and the d data chunks rebuilt from the verified ones.
 //
 // Per slot, asynchronously on the slot's stream: the loaded chunks go up (one copy per run of
-// consecutive loaded chunks), the SHA-256 kernel verifies every loaded chunk against its
-// expected digest, and the missing data chunks are rebuilt SPECULATIVELY from the first d
-// loaded chunks (the pattern is known at submit time, so no host round trip sits between
-// verification and decode); the d data chunks and the verification flags come back.  wait()
-// checks the flags: a part whose loaded chunks all verified is done (the common case); a part
-// with a chunk that failed is decoded again from its verified chunks only (or reported
-// TooFewShardsPresent when fewer than d verify) before wait() returns.
+// consecutive loaded chunks, or one copy of a packed batch), the SHA-256 kernel verifies every
+// loaded chunk against its expected digest, and the missing data chunks are rebuilt
+// SPECULATIVELY from the first d loaded chunks (the pattern is known at submit time, so no host
+// round trip sits between verification and decode); the d data chunks and the verification flags
+// come back.  wait() checks the flags: a part whose loaded chunks all verified is done (the
+// common case); a part with a chunk that failed is decoded again from its verified chunks only
+// (or reported TooFewShardsPresent when fewer than d verify) before wait() returns.
+//
+// The mode (read, REBUILT_ONLY, RESILVER, VERIFY_ONLY) is a property of each SUBMIT (the
+// pipeline's creation flags are only the default of the older entry points): the device buffers
+// are the same for every mode, so one pipeline serves FilePart's verify, resilver and read in
+// turn without being rebuilt (file_part.rs:228-390 runs them on the same parts).
 // ------------------------------------------------------------------------------------------
 
 namespace {
+
+constexpr unsigned kModeBits = CEC_READ_REBUILT_ONLY | CEC_READ_RESILVER | CEC_READ_VERIFY_ONLY;
 
 struct ReadSlot {
     uint8_t* h_chunks = nullptr;    // pinned [parts][t][L]   (caller: loaded chunk bytes)
     uint8_t* h_present = nullptr;   // pinned [parts][t]      (caller: nonzero = loaded)
     uint8_t* h_expected = nullptr;  // pinned [parts][t][32]  (caller: metadata digests)
-    uint8_t* h_data = nullptr;      // pinned [parts][d][L]   (result: data chunks)
+    uint8_t* h_data = nullptr;      // pinned [parts][out][L] (result: data / rebuilt chunks)
     uint8_t* h_ok = nullptr;        // pinned [parts][t]      (result: verified flags)
     uint8_t* h_hash = nullptr;      // pinned [parts][t]      chunks to hash (loaded, not
                                     //                        CEC_PRESENT_VERIFIED)
@@ -330,24 +334,25 @@ struct ReadSlot {
     uint32_t* d_ids = nullptr;      // device [parts*t]
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
-    // side stream (decode + rebuilt D2H beside the verification) and its fork / join events;
-    // uploaded: the shared upload stream's event this slot's compute waits for (made lazily)
-    hipStream_t side = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr, uploaded = nullptr;
     bool in_flight = false;
     bool checked = false;
+    unsigned mode = 0;     // this batch's mode bits (kModeBits)
+    bool stashed = false;  // this batch queued a carry stash
     size_t n_parts = 0;
     const uint8_t* src_chunks = nullptr;  // this batch's chunk bytes (h_chunks or the caller's)
     uint8_t* dst_data = nullptr;          // this batch's data output (h_data or the caller's)
     std::vector<uint8_t> decode_mask;  // present mask the speculative decode used
-    std::vector<const uint8_t*> data_ptrs;  // [parts][d]: where each data chunk is (after wait)
+    std::vector<const uint8_t*> data_ptrs;  // [parts][out]: where each output chunk is
     std::vector<size_t> src_off;  // [parts][t]: byte offset of a loaded chunk in src_chunks
     // CEC_READ_CARRY: per part of this batch, the carry entry its verified chunks were kept in
     // (-1: none), and whether its CEC_PRESENT_VERIFIED chunks came from the carry pool at submit
     // (not from the caller's buffer: they are copied back like rebuilt ones)
     std::vector<int32_t> carry_ids;
     std::vector<uint8_t> carried;
-    std::vector<int32_t> reserved;  // pool entries this batch's stash may fill
+    // pool entries this batch's stash may fill (kReserved); after wait, the entries of its
+    // TooFewShardsPresent parts until the caller claims them (cec_read_pipeline_carry_ids) or
+    // the slot's next submit gives them back
+    std::vector<int32_t> reserved;
     // made with the pipeline: the consume's index lists ([0, parts*t) batch positions, then
     // pool positions), the reserved entries, the stash's part -> entry map, the loaded flags
     uint32_t* h_cids = nullptr;
@@ -365,23 +370,17 @@ struct cec_read_pipeline {
     const cec_codec* codec = nullptr;
     int device = 0;
     size_t d = 0, p = 0, t = 0, L = 0, cs = 0, parts = 0;
-    bool rebuilt_only = false;  // CEC_READ_REBUILT_ONLY: D2H only the data chunks rebuilt
-    // CEC_READ_RESILVER: FilePart::resilver's compute (file_part.rs:253-308): every chunk that
-    // did not verify (data AND parity) is rebuilt and comes back, in a [parts][t][L] output;
-    // the verified ones stay where they were read.
-    bool resilver = false;
-    // CEC_READ_VERIFY_ONLY: FilePart::verify's compute (file_part.rs:228-251): the loaded chunks
-    // are hashed and compared, nothing is decoded or copied back.
-    bool verify_only = false;
-    size_t out_chunks() const { return resilver ? t : d; }  // output chunks per part
-    bool external = false;      // CEC_PIPE_EXTERNAL: no pinned chunk / data slot buffers
-    // A/B knobs (read once at creation): CEC_READ_SIDE=1 runs the speculative decode and the
-    // rebuilt chunks' D2H on a per-slot side stream beside the verification; CEC_READ_UPSTREAM=1
-    // queues every slot's uploads on one pipeline-wide stream (batches go up one after another
-    // in submission order instead of sharing the link).
-    bool side_decode = false;
-    bool shared_upload = false;
-    hipStream_t up = nullptr;
+    // The creation flags' mode: what cec_read_pipeline_submit / submit_from / submit_packed /
+    // submit_carried use.  Mode bits (per submit, cec_read_pipeline_submit_ex):
+    //  CEC_READ_REBUILT_ONLY -- D2H only the data chunks rebuilt;
+    //  CEC_READ_RESILVER     -- FilePart::resilver's compute (file_part.rs:253-308): every chunk
+    //                           that did not verify (data AND parity) is rebuilt and comes back,
+    //                           in a [parts][t][L] output; the verified ones stay where read;
+    //  CEC_READ_VERIFY_ONLY  -- FilePart::verify's compute (file_part.rs:228-251): the loaded
+    //                           chunks are hashed and compared, nothing is decoded or copied back.
+    unsigned default_mode = 0;
+    size_t h_out_chunks = 0;  // output chunks per part the slots' own h_data holds (0: none)
+    bool external = false;    // CEC_PIPE_EXTERNAL: no pinned chunk / data slot buffers
     std::vector<ReadSlot> slots;
     size_t next = 0;
     // CEC_READ_CARRY: device pool of `carry_cap` entries of [t][cs] bytes (made with the
@@ -394,7 +393,9 @@ struct cec_read_pipeline {
     // slot's batch (slot streams can share a hardware queue, where a kernel waits for every
     // packet queued before it).  Per entry an event after its last stash or consumption, so
     // reusing an entry waits for its previous copies.  carry_used: kFree, kHeld (a carry id the
-    // caller has), kReserved (by an in-flight batch).
+    // caller has), kReserved (by a batch: in flight, or waited for and not yet claimed).  Per
+    // entry, the chunks its stash kept (carry_mask [cap][t]) and the part's metadata digests
+    // (carry_exp [cap][t][32]): a retry may take an entry only for the part it was kept for.
     static constexpr uint8_t kFree = 0, kHeld = 1, kReserved = 2;
     bool carry = false;
     size_t carry_batch = 0;
@@ -402,20 +403,22 @@ struct cec_read_pipeline {
     uint8_t* d_carry = nullptr;
     std::vector<hipEvent_t> carry_ready;
     std::vector<uint8_t> carry_used;
+    std::vector<uint8_t> carry_mask;
+    std::vector<uint8_t> carry_exp;
     std::deque<int32_t> carry_free;
+
+    static size_t out_chunks(unsigned mode, size_t d, size_t t) {
+        return (mode & CEC_READ_VERIFY_ONLY) ? 0 : (mode & CEC_READ_RESILVER) ? t : d;
+    }
 
     ~cec_read_pipeline() {
         int cur = 0;
         if (hipGetDevice(&cur) != hipSuccess) return;
         (void)hipSetDevice(device);
-        if (up) (void)hipStreamSynchronize(up);
         for (ReadSlot& s : slots) {
             if (s.stream) (void)hipStreamSynchronize(s.stream);
-            if (s.side) (void)hipStreamSynchronize(s.side);
-            for (hipEvent_t ev : {s.done, s.fork, s.join, s.uploaded})
-                if (ev) (void)hipEventDestroy(ev);
+            if (s.done) (void)hipEventDestroy(s.done);
             if (s.stream) (void)hipStreamDestroy(s.stream);
-            if (s.side) (void)hipStreamDestroy(s.side);
             for (void* dptr : {static_cast<void*>(s.d_buf), static_cast<void*>(s.d_expected),
                                static_cast<void*>(s.d_flags), static_cast<void*>(s.d_pack),
                                static_cast<void*>(s.d_ids), static_cast<void*>(s.d_cids),
@@ -429,7 +432,6 @@ struct cec_read_pipeline {
                 if (hptr) (void)hipHostFree(hptr);
             delete[] s.h_status;
         }
-        if (up) (void)hipStreamDestroy(up);
         for (hipEvent_t ev : carry_ready)
             if (ev) (void)hipEventDestroy(ev);
         if (d_carry) (void)hipFree(d_carry);
@@ -452,6 +454,8 @@ struct cec_read_pipeline {
             if (e != hipSuccess) return e;
         }
         carry_used.assign(carry_cap, kFree);
+        carry_mask.assign(carry_cap * t, 0);
+        carry_exp.assign(carry_cap * t * 32, 0);
         carry_free.clear();
         for (size_t i = 0; i < carry_cap; ++i) carry_free.push_back(int32_t(i));
         for (ReadSlot& s : slots) {
@@ -472,8 +476,8 @@ struct cec_read_pipeline {
         return e;
     }
 
-    // Entries of a slot's batch that its stash did not fill (or that were never mapped because
-    // the slot was not waited for) go back to the free list.
+    // Entries the slot still reserves (its stash did not fill them, or the caller did not claim
+    // them after wait) go back to the free list.
     void carry_unreserve(ReadSlot& s) {
         for (int32_t id : s.reserved)
             if (carry_used[size_t(id)] == kReserved) carry_give_back(id);
@@ -485,6 +489,22 @@ struct cec_read_pipeline {
     }
     bool carry_valid(int32_t id) const {  // a carry id the caller holds
         return id >= 0 && size_t(id) < carry_used.size() && carry_used[size_t(id)] == kHeld;
+    }
+    size_t held_entries() const {
+        return size_t(std::count(carry_used.begin(), carry_used.end(), kHeld));
+    }
+
+    // Whether carry entry `id` was kept for part k of slot s as the slot's present / expected
+    // arrays now describe it: the part's metadata digests are the ones stashed with the entry,
+    // and every chunk it flags CEC_PRESENT_VERIFIED is one the stash kept.  Anything else would
+    // decode stale bytes that are never hashed again.
+    bool carry_matches(const ReadSlot& s, size_t k, int32_t id) const {
+        const uint8_t* pr = s.h_present + k * t;
+        const uint8_t* mask = carry_mask.data() + size_t(id) * t;
+        for (size_t i = 0; i < t; ++i)
+            if (pr[i] == CEC_PRESENT_VERIFIED && !mask[i]) return false;
+        return std::memcmp(s.h_expected + k * t * 32, carry_exp.data() + size_t(id) * t * 32,
+                           t * 32) == 0;
     }
 
     // The retry's consume: pairs[j] = (batch position, pool position), one move kernel launch
@@ -504,10 +524,10 @@ struct cec_read_pipeline {
         return CEC_OK;
     }
 
-    // The batch's stash (CEC_READ_CARRY), queued after its verification: reserve up to
-    // carry_batch free entries (each waits for its last copies), let the stash kernels fill them
-    // with the verified chunks of the parts that will come back TooFewShardsPresent, and bring
-    // the part -> entry map back with the batch.
+    // The batch's stash (CEC_READ_CARRY, read modes), queued after its verification: reserve up
+    // to carry_batch free entries (each waits for its last copies), let the stash kernels fill
+    // them with the verified chunks of the parts that will come back TooFewShardsPresent, and
+    // bring the part -> entry map back with the batch.
     int carry_stash(ReadSlot& s, size_t n_parts) {
         carry_unreserve(s);
         while (s.reserved.size() < carry_batch && !carry_free.empty()) {
@@ -530,6 +550,7 @@ struct cec_read_pipeline {
         for (int32_t id : s.reserved) PIPE_TRY(hipEventRecord(carry_ready[size_t(id)], s.stream));
         PIPE_TRY(hipMemcpyAsync(s.h_map, s.d_map, n_parts * sizeof(int32_t), hipMemcpyDeviceToHost,
                                 s.stream));
+        s.stashed = true;
         return CEC_OK;
     }
 
@@ -539,7 +560,7 @@ struct cec_read_pipeline {
 
     // D2H of the data chunks of part k that were not loaded (the speculative decode rebuilt
     // them) into their data slots: one copy per run of consecutive missing data chunks.
-    int copy_rebuilt_back(ReadSlot& s, size_t k, hipStream_t stream) const {
+    int copy_rebuilt_back(ReadSlot& s, size_t k) const {
         const uint8_t* pr = s.h_present + k * t;
         const bool carried = !s.carried.empty() && s.carried[k];
         // in the caller's buffer: loaded chunks, except those a carried part took from the pool
@@ -554,10 +575,10 @@ struct cec_read_pipeline {
             uint8_t* dst = s.dst_data + (k * d + j) * L;
             const uint8_t* src = s.d_buf + (k * t + j) * cs;
             if (cs == L)
-                PIPE_TRY(hipMemcpyAsync(dst, src, (e - j) * L, hipMemcpyDeviceToHost, stream));
+                PIPE_TRY(hipMemcpyAsync(dst, src, (e - j) * L, hipMemcpyDeviceToHost, s.stream));
             else
                 PIPE_TRY(hipMemcpy2DAsync(dst, L, src, cs, L, e - j, hipMemcpyDeviceToHost,
-                                          stream));
+                                          s.stream));
             j = e;
         }
         return CEC_OK;
@@ -565,7 +586,7 @@ struct cec_read_pipeline {
 
     // Resilver: D2H of the chunks of part k whose flag in `have` is 0 (rebuilt) into their
     // [t] output slots, one copy per run.
-    int copy_missing_back(ReadSlot& s, size_t k, const uint8_t* have, hipStream_t stream) const {
+    int copy_missing_back(ReadSlot& s, size_t k, const uint8_t* have) const {
         for (size_t i = 0; i < t;) {
             if (have[i]) {
                 ++i;
@@ -576,31 +597,30 @@ struct cec_read_pipeline {
             uint8_t* dst = s.dst_data + (k * t + i) * L;
             const uint8_t* src = s.d_buf + (k * t + i) * cs;
             if (cs == L)
-                PIPE_TRY(hipMemcpyAsync(dst, src, (e - i) * L, hipMemcpyDeviceToHost, stream));
+                PIPE_TRY(hipMemcpyAsync(dst, src, (e - i) * L, hipMemcpyDeviceToHost, s.stream));
             else
                 PIPE_TRY(hipMemcpy2DAsync(dst, L, src, cs, L, e - i, hipMemcpyDeviceToHost,
-                                          stream));
+                                          s.stream));
             i = e;
         }
         return CEC_OK;
     }
 
     // D2H of the d data chunks of parts [k0, k0 + n) into the data output.
-    int copy_data_back(ReadSlot& s, size_t k0, size_t n, hipStream_t stream) const {
+    int copy_data_back(ReadSlot& s, size_t k0, size_t n) const {
         const size_t pitch = t * cs, dw = d * L;
         if (cs == L) {
             PIPE_TRY(hipMemcpy2DAsync(s.dst_data + k0 * dw, dw, s.d_buf + k0 * pitch, pitch, dw, n,
-                                      hipMemcpyDeviceToHost, stream));
+                                      hipMemcpyDeviceToHost, s.stream));
         } else {
             for (size_t j = 0; j < d; ++j)
                 PIPE_TRY(hipMemcpy2DAsync(s.dst_data + k0 * dw + j * L, dw,
                                           s.d_buf + k0 * pitch + j * cs, pitch, L, n,
-                                          hipMemcpyDeviceToHost, stream));
+                                          hipMemcpyDeviceToHost, s.stream));
         }
         return CEC_OK;
     }
 
-    // Queue one batch whose present flags / expected digests are in the slot's pinned arrays.
     // Device / pinned buffers of the packed upload, made on a slot's first packed batch.
     int ensure_packed(ReadSlot& s) const {
         const size_t n = parts * t;
@@ -617,54 +637,45 @@ struct cec_read_pipeline {
         return CEC_OK;
     }
 
-    // The shared upload stream, the slot's side stream and the events that order them (A/B
-    // knobs; made on first use).
-    int ensure_streams(ReadSlot& s) {
-        hipError_t e = hipSuccess;
-        if (shared_upload && !up) e = hipStreamCreateWithFlags(&up, hipStreamNonBlocking);
-        if (e == hipSuccess && shared_upload && !s.uploaded)
-            e = hipEventCreateWithFlags(&s.uploaded, hipEventDisableTiming);
-        if (e == hipSuccess && side_decode && !s.side)
-            e = hipStreamCreateWithFlags(&s.side, hipStreamNonBlocking);
-        if (e == hipSuccess && side_decode && !s.fork)
-            e = hipEventCreateWithFlags(&s.fork, hipEventDisableTiming);
-        if (e == hipSuccess && side_decode && !s.join)
-            e = hipEventCreateWithFlags(&s.join, hipEventDisableTiming);
-        if (e != hipSuccess) {
-            (void)hipGetLastError();
-            return pipe_fail(e, "read pipeline streams");
-        }
-        return CEC_OK;
-    }
-
-    // Stream the uploads of slot s go on, and the hand-over to its compute stream.
-    hipStream_t upload_stream(ReadSlot& s) const { return shared_upload ? up : s.stream; }
-    int uploads_done(ReadSlot& s) const {
-        if (!shared_upload) return CEC_OK;
-        PIPE_TRY(hipEventRecord(s.uploaded, up));
-        PIPE_TRY(hipStreamWaitEvent(s.stream, s.uploaded, 0));
-        return CEC_OK;
-    }
-
-    // packed: `chunks` holds the loaded chunks back to back (part by part, ascending chunk
+    // Queue one batch whose present flags / expected digests are in the slot's pinned arrays.
+    // packed: `chunks` holds the uploaded chunks back to back (part by part, ascending chunk
     // index), uploaded with ONE copy and placed by the move kernel; else chunk (k, i) is at
-    // chunks + (k*t + i)*L and goes up with one copy per run of consecutive loaded chunks.
+    // chunks + (k*t + i)*L and goes up with one copy per run of consecutive uploaded chunks.
     // carry_ids (CEC_READ_CARRY, nullable): per part, a carry entry whose chunks replace the
     // part's CEC_PRESENT_VERIFIED chunks (copied on the device; the caller's buffer need not hold
-    // them), or -1.
+    // them, and a packed buffer leaves them out), or -1.
     int submit(ReadSlot& s, const uint8_t* chunks, size_t n_parts, uint8_t* data_out,
-               bool packed = false, const int32_t* carry_ids = nullptr) {
+               unsigned mode, bool packed, const int32_t* carry_ids) {
         DeviceGuard guard(device);
         PIPE_TRY(guard.status());
         if (s.in_flight) {  // the slot's pinned arrays may still be read by its last batch
             PIPE_TRY(hipEventSynchronize(s.done));
             s.in_flight = false;
         }
+        // a new batch on the slot: entries of its last one the caller did not claim go back
+        if (carry) carry_unreserve(s);
+        s.stashed = false;
+        s.n_parts = 0;  // nothing valid on the slot until this batch is queued
+        if ((mode & ~kModeBits) || ((mode & CEC_READ_RESILVER) && (mode & CEC_READ_VERIFY_ONLY))) {
+            g_pipe_error = "invalid read mode";
+            return CEC_ERR_INVALID_ARGUMENT;
+        }
+        const size_t out = out_chunks(mode, d, t);
+        if (out && !data_out) {
+            g_pipe_error = "no output buffer for this mode";
+            return CEC_ERR_INVALID_ARGUMENT;
+        }
+        if (out && data_out == s.h_data && out > h_out_chunks) {
+            g_pipe_error = "the slot's own output holds fewer chunks per part than this mode "
+                           "writes: pass data_out";
+            return CEC_ERR_INVALID_ARGUMENT;
+        }
+        const bool read_mode = !(mode & (CEC_READ_RESILVER | CEC_READ_VERIFY_ONLY));
         const size_t n = n_parts * t;
         s.carried.assign(carry_ids ? n_parts : 0, 0);
         if (carry_ids) {
-            if (!carry || packed) {
-                g_pipe_error = "carry ids need CEC_READ_CARRY and an unpacked submit";
+            if (!carry || !read_mode) {
+                g_pipe_error = "carry ids need CEC_READ_CARRY and a read mode";
                 return CEC_ERR_INVALID_ARGUMENT;
             }
             for (size_t k = 0; k < n_parts; ++k) {
@@ -678,58 +689,63 @@ struct cec_read_pipeline {
                         g_pipe_error = "carry id given twice";
                         return CEC_ERR_INVALID_ARGUMENT;
                     }
+                if (!carry_matches(s, k, carry_ids[k])) {
+                    g_pipe_error = "carry id was kept for another part (digests or verified "
+                                   "chunks differ)";
+                    return CEC_ERR_INVALID_ARGUMENT;
+                }
                 s.carried[k] = 1;
             }
         }
+        s.mode = mode;
         s.src_chunks = chunks;
         s.dst_data = data_out;
-        s.src_off.resize(n);
-        const int sst = ensure_streams(s);
-        if (sst != CEC_OK) return sst;
-        const hipStream_t us = upload_stream(s);
+        s.src_off.assign(n, 0);
+        // chunks that come from the caller's buffer: loaded ones, except the verified chunks of
+        // a carried part (those come from the carry pool, below)
+        auto uploaded = [&](size_t x) {
+            const uint8_t f = s.h_present[x];
+            return f && !(!s.carried.empty() && s.carried[x / t] && f == CEC_PRESENT_VERIFIED);
+        };
         if (packed) {
             const int est = ensure_packed(s);
             if (est != CEC_OK) return est;
             size_t m = 0;
             for (size_t x = 0; x < n; ++x)
-                if (s.h_present[x]) {
+                if (uploaded(x)) {
                     s.h_ids[m] = uint32_t(x);
                     s.src_off[x] = m * L;
                     ++m;
                 }
             if (m) {
-                PIPE_TRY(hipMemcpyAsync(s.d_pack, chunks, m * L, hipMemcpyHostToDevice, us));
+                PIPE_TRY(hipMemcpyAsync(s.d_pack, chunks, m * L, hipMemcpyHostToDevice, s.stream));
                 PIPE_TRY(hipMemcpyAsync(s.d_ids, s.h_ids, m * sizeof(uint32_t),
-                                        hipMemcpyHostToDevice, us));
-                const int ust = uploads_done(s);
-                if (ust != CEC_OK) return ust;
+                                        hipMemcpyHostToDevice, s.stream));
                 cec::MoveParams mv{s.d_buf, t * cs, cs, uint32_t(t), s.d_pack, L, s.d_ids,
                                    uint32_t(m), 1u};
                 PIPE_TRY(cec::launch_move_chunks(mv, s.stream));
             }
-            return submit_compute(s, n_parts);
-        }
-        for (size_t x = 0; x < n; ++x) s.src_off[x] = x * L;
-        // loaded chunks up: one copy per run of consecutive loaded chunks of a part (a carried
-        // part's verified chunks come from the carry pool instead, below)
-        for (size_t k = 0; k < n_parts; ++k) {
-            const uint8_t* pr = s.h_present + k * t;
-            const bool carried = !s.carried.empty() && s.carried[k];
-            auto up = [&](size_t i) { return pr[i] && !(carried && pr[i] == CEC_PRESENT_VERIFIED); };
-            for (size_t i = 0; i < t;) {
-                if (!up(i)) {
-                    ++i;
-                    continue;
+        } else {
+            for (size_t x = 0; x < n; ++x) s.src_off[x] = x * L;
+            // one copy per run of consecutive uploaded chunks of a part
+            for (size_t k = 0; k < n_parts; ++k) {
+                for (size_t i = 0; i < t;) {
+                    if (!uploaded(k * t + i)) {
+                        ++i;
+                        continue;
+                    }
+                    size_t j = i;
+                    while (j < t && uploaded(k * t + j)) ++j;
+                    const uint8_t* src = chunks + (k * t + i) * L;
+                    uint8_t* dst = s.d_buf + (k * t + i) * cs;
+                    if (cs == L)
+                        PIPE_TRY(hipMemcpyAsync(dst, src, (j - i) * L, hipMemcpyHostToDevice,
+                                                s.stream));
+                    else
+                        PIPE_TRY(hipMemcpy2DAsync(dst, cs, src, L, L, j - i, hipMemcpyHostToDevice,
+                                                  s.stream));
+                    i = j;
                 }
-                size_t j = i;
-                while (j < t && up(j)) ++j;
-                const uint8_t* src = chunks + (k * t + i) * L;
-                uint8_t* dst = s.d_buf + (k * t + i) * cs;
-                if (cs == L)
-                    PIPE_TRY(hipMemcpyAsync(dst, src, (j - i) * L, hipMemcpyHostToDevice, us));
-                else
-                    PIPE_TRY(hipMemcpy2DAsync(dst, cs, src, L, L, j - i, hipMemcpyHostToDevice, us));
-                i = j;
             }
         }
         // carried parts: their verified chunks come from the pool, one move launch queued after
@@ -754,27 +770,19 @@ struct cec_read_pipeline {
                     carry_give_back(carry_ids[k]);
                 }
         }
-        const int ust = uploads_done(s);
-        if (ust != CEC_OK) return ust;
         return submit_compute(s, n_parts);
     }
 
     int submit_compute(ReadSlot& s, size_t n_parts) {
         const size_t n = n_parts * t;
+        const bool verify_only = (s.mode & CEC_READ_VERIFY_ONLY) != 0;
+        const bool resilver = (s.mode & CEC_READ_RESILVER) != 0;
         // hash every loaded chunk except those an earlier pass verified (read retries)
         for (size_t i = 0; i < n; ++i)
             s.h_hash[i] = s.h_present[i] != 0 && s.h_present[i] != CEC_PRESENT_VERIFIED;
         PIPE_TRY(hipMemcpyAsync(s.d_expected, s.h_expected, n * 32, hipMemcpyHostToDevice, s.stream));
         PIPE_TRY(hipMemcpyAsync(s.d_flags, s.h_hash, n, hipMemcpyHostToDevice, s.stream));
         cec_part_batch b = batch(s, n_parts);
-        // decode (and its D2H) on the side stream when enabled: it reads only loaded chunks and
-        // writes only chunks that were not loaded, as the verification beside it reads
-        const bool fork = side_decode && !verify_only;
-        const hipStream_t dstream = fork ? s.side : s.stream;
-        if (fork) {
-            PIPE_TRY(hipEventRecord(s.fork, s.stream));
-            PIPE_TRY(hipStreamWaitEvent(s.side, s.fork, 0));
-        }
         int st = cec_verify_batch(&b, 0, t, s.d_flags, s.d_expected, s.d_flags + n, s.stream);
         if (verify_only) {
             if (st != CEC_OK) {
@@ -802,28 +810,22 @@ struct cec_read_pipeline {
                           uint8_t(1));
         }
         if (st == CEC_OK)
-            st = cec_reconstruct_batch(codec, &b, s.decode_mask.data(), resilver ? 0 : 1,
-                                       dstream);
+            st = cec_reconstruct_batch(codec, &b, s.decode_mask.data(), resilver ? 0 : 1, s.stream);
         if (st != CEC_OK) {
             g_pipe_error = cec_last_error();
             return st;
         }
         if (resilver) {
             for (size_t k = 0; k < n_parts && st == CEC_OK; ++k)
-                if (s.h_status[k] == CEC_OK)
-                    st = copy_missing_back(s, k, s.h_present + k * t, dstream);
-        } else if (rebuilt_only) {
+                if (s.h_status[k] == CEC_OK) st = copy_missing_back(s, k, s.h_present + k * t);
+        } else if (s.mode & CEC_READ_REBUILT_ONLY) {
             for (size_t k = 0; k < n_parts && st == CEC_OK; ++k)
-                if (s.h_status[k] == CEC_OK) st = copy_rebuilt_back(s, k, dstream);
+                if (s.h_status[k] == CEC_OK) st = copy_rebuilt_back(s, k);
         } else {
-            st = copy_data_back(s, 0, n_parts, dstream);
+            st = copy_data_back(s, 0, n_parts);
         }
         if (st != CEC_OK) return st;
-        if (fork) {
-            PIPE_TRY(hipEventRecord(s.join, s.side));
-            PIPE_TRY(hipStreamWaitEvent(s.stream, s.join, 0));
-        }
-        if (carry) {
+        if (carry && !resilver) {
             const int cst = carry_stash(s, n_parts);
             if (cst != CEC_OK) return cst;
         }
@@ -832,6 +834,118 @@ struct cec_read_pipeline {
         s.in_flight = true;
         s.checked = false;
         s.n_parts = n_parts;
+        return CEC_OK;
+    }
+
+    // wait's host side for a completed batch (run once per batch).
+    int check(ReadSlot& s) {
+        const size_t n = s.n_parts;
+        for (size_t i = 0; i < n * t; ++i)  // verified by an earlier pass: trusted
+            if (s.h_present[i] == CEC_PRESENT_VERIFIED) s.h_ok[i] = 1;
+        if (s.mode & CEC_READ_VERIFY_ONLY) {
+            s.data_ptrs.clear();
+            s.carry_ids.assign(n, -1);
+            s.checked = true;
+            return CEC_OK;
+        }
+        const bool resilver = (s.mode & CEC_READ_RESILVER) != 0;
+        // parts whose loaded chunks did not all verify: decode again from the verified ones
+        std::vector<uint8_t> mask(n * t, 1);
+        std::vector<size_t> redo;
+        for (size_t k = 0; k < n; ++k) {
+            if (s.h_status[k] != CEC_OK) continue;
+            bool bad = false;
+            size_t good = 0;
+            for (size_t i = 0; i < t; ++i) {
+                bad |= s.h_present[k * t + i] && !s.h_ok[k * t + i];
+                good += s.h_ok[k * t + i] ? 1 : 0;
+            }
+            if (!bad) continue;
+            if (good < d) {
+                s.h_status[k] = CEC_TOO_FEW_SHARDS_PRESENT;
+                continue;
+            }
+            std::copy(s.h_ok + k * t, s.h_ok + (k + 1) * t, mask.begin() + k * t);
+            redo.push_back(k);
+        }
+        if (!redo.empty()) {
+            DeviceGuard guard(device);
+            PIPE_TRY(guard.status());
+            cec_part_batch b = batch(s, n);
+            int st = cec_reconstruct_batch(codec, &b, mask.data(), resilver ? 0 : 1, s.stream);
+            if (st != CEC_OK) {
+                g_pipe_error = cec_last_error();
+                return st;
+            }
+            for (size_t k : redo) {
+                st = resilver ? copy_missing_back(s, k, s.h_ok + k * t) : copy_data_back(s, k, 1);
+                if (st != CEC_OK) return st;
+            }
+            PIPE_TRY(hipStreamSynchronize(s.stream));
+        }
+        // CEC_READ_CARRY: the stash kept the verified chunks of every part with fewer than d of
+        // them (exactly the parts reported TooFewShardsPresent) in a reserved entry, while
+        // reservations lasted.  Those entries stay reserved for the caller to claim
+        // (cec_read_pipeline_carry_ids); the rest go back now.  Each records what it holds.
+        s.carry_ids.assign(n, -1);
+        if (s.stashed) {
+            std::vector<int32_t> keep;
+            for (size_t k = 0; k < n; ++k) {
+                const int32_t id = s.h_map[k];
+                if (id < 0 || s.h_status[k] != CEC_TOO_FEW_SHARDS_PRESENT) continue;
+                if (size_t(id) >= carry_cap || carry_used[size_t(id)] != kReserved) {
+                    g_pipe_error = "carry stash returned an entry the batch did not reserve";
+                    return CEC_ERR_HIP;
+                }
+                s.carry_ids[k] = id;
+                keep.push_back(id);
+                for (size_t i = 0; i < t; ++i)
+                    carry_mask[size_t(id) * t + i] = s.h_present[k * t + i] && s.h_ok[k * t + i];
+                std::memcpy(carry_exp.data() + size_t(id) * t * 32, s.h_expected + k * t * 32,
+                            t * 32);
+            }
+            for (int32_t id : s.reserved)
+                if (std::find(keep.begin(), keep.end(), id) == keep.end() &&
+                    carry_used[size_t(id)] == kReserved)
+                    carry_give_back(id);
+            s.reserved = keep;
+        }
+        // Where each output chunk is: re-decoded parts and (without REBUILT_ONLY) every part in
+        // the data output; otherwise a loaded chunk stays in the chunk buffer it was read from (it
+        // verified: parts with a failed chunk were re-decoded) and a rebuilt one came back into
+        // the data output -- as did a carried part's verified data chunks (the caller's buffer
+        // does not hold them).
+        std::vector<uint8_t> redone(n, 0);
+        for (size_t k : redo) redone[k] = 1;
+        if (resilver) {  // [parts][t]: verified chunks where they were read, others rebuilt
+            s.data_ptrs.resize(n * t);
+            for (size_t k = 0; k < n; ++k)
+                for (size_t i = 0; i < t; ++i)
+                    s.data_ptrs[k * t + i] = s.h_ok[k * t + i] ? s.src_chunks + s.src_off[k * t + i]
+                                                               : s.dst_data + (k * t + i) * L;
+        } else {
+            const bool rebuilt_only = (s.mode & CEC_READ_REBUILT_ONLY) != 0;
+            s.data_ptrs.resize(n * d);
+            for (size_t k = 0; k < n; ++k)
+                for (size_t j = 0; j < d; ++j) {
+                    const uint8_t f = s.h_present[k * t + j];
+                    const bool from_pool = !s.carried.empty() && s.carried[k] &&
+                                           f == CEC_PRESENT_VERIFIED;
+                    const bool in_place = rebuilt_only && !redone[k] && f && !from_pool;
+                    s.data_ptrs[k * d + j] = in_place ? s.src_chunks + s.src_off[k * t + j]
+                                                      : s.dst_data + (k * d + j) * L;
+                }
+        }
+        s.checked = true;
+        return CEC_OK;
+    }
+
+    int finish(ReadSlot& s) {
+        if (s.in_flight) {
+            PIPE_TRY(hipEventSynchronize(s.done));
+            s.in_flight = false;
+        }
+        if (!s.checked && s.n_parts) return check(s);
         return CEC_OK;
     }
 };
@@ -846,10 +960,8 @@ int cec_read_pipeline_new(const cec_codec* codec, size_t chunk_len, size_t parts
 int cec_read_pipeline_new_ex(const cec_codec* codec, size_t chunk_len, size_t parts_per_batch,
                              size_t depth, unsigned flags, cec_read_pipeline** out) {
     if (!codec || !out || chunk_len == 0 || parts_per_batch == 0 || depth == 0 || depth > 16 ||
-        (flags & ~unsigned(CEC_READ_REBUILT_ONLY | CEC_PIPE_EXTERNAL | CEC_READ_RESILVER |
-                           CEC_READ_VERIFY_ONLY | CEC_READ_CARRY)) ||
-        ((flags & CEC_READ_RESILVER) && (flags & CEC_READ_VERIFY_ONLY)) ||
-        ((flags & CEC_READ_CARRY) && (flags & (CEC_READ_RESILVER | CEC_READ_VERIFY_ONLY))))
+        (flags & ~unsigned(kModeBits | CEC_PIPE_EXTERNAL | CEC_READ_CARRY)) ||
+        ((flags & CEC_READ_RESILVER) && (flags & CEC_READ_VERIFY_ONLY)))
         return CEC_ERR_INVALID_ARGUMENT;
     *out = nullptr;
     if (cec_device_count() <= 0) return CEC_ERR_NO_DEVICE;
@@ -862,17 +974,14 @@ int cec_read_pipeline_new_ex(const cec_codec* codec, size_t chunk_len, size_t pa
     pl->L = chunk_len;
     pl->cs = (chunk_len + 255) / 256 * 256;
     pl->parts = parts_per_batch;
-    pl->rebuilt_only = (flags & CEC_READ_REBUILT_ONLY) != 0;
+    pl->default_mode = flags & kModeBits;
     pl->external = (flags & CEC_PIPE_EXTERNAL) != 0;
-    pl->resilver = (flags & CEC_READ_RESILVER) != 0;
-    pl->verify_only = (flags & CEC_READ_VERIFY_ONLY) != 0;
     pl->carry = (flags & CEC_READ_CARRY) != 0;
+    pl->h_out_chunks = pl->external ? 0 : cec_read_pipeline::out_chunks(pl->default_mode, pl->d, pl->t);
     // a quarter of a batch's parts per batch (a 1 % damaged-fetch rate fails ~10 % of RS(10,4)
     // parts): entries for every batch in flight plus one batch's retries
     pl->carry_batch = pl->carry ? std::min<size_t>(parts_per_batch, std::max<size_t>(8, parts_per_batch / 4)) : 0;
     pl->carry_cap = pl->carry_batch * (depth + 1);
-    pl->side_decode = cec::knobs().read_side;
-    pl->shared_upload = cec::knobs().read_upstream;
     pl->slots.resize(depth);
     const size_t P = pl->parts, t = pl->t;
     for (ReadSlot& s : pl->slots) {
@@ -887,7 +996,7 @@ int cec_read_pipeline_new_ex(const cec_codec* codec, size_t chunk_len, size_t pa
         };
         if (!pl->external) {
             host(&s.h_chunks, P * t * pl->L);
-            host(&s.h_data, P * pl->out_chunks() * pl->L);
+            if (pl->h_out_chunks) host(&s.h_data, P * pl->h_out_chunks * pl->L);
         }
         host(&s.h_present, P * t);
         host(&s.h_expected, P * t * 32);
@@ -896,7 +1005,7 @@ int cec_read_pipeline_new_ex(const cec_codec* codec, size_t chunk_len, size_t pa
         dev(&s.d_buf, P * t * pl->cs);
         dev(&s.d_expected, P * t * 32);
         dev(&s.d_flags, 2 * P * t);
-        if (e == hipSuccess) e = slot_stream(&s.stream, pl->device);
+        if (e == hipSuccess) e = slot_stream(&s.stream);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
         s.h_status = new int[P];
         if (e != hipSuccess) {
@@ -913,6 +1022,7 @@ int cec_read_pipeline_new_ex(const cec_codec* codec, size_t chunk_len, size_t pa
             return pipe_fail(e, "cec_read_pipeline_new carry pool");
         }
     }
+    g_pipelines_made.fetch_add(1, std::memory_order_relaxed);
     *out = pl;
     return CEC_OK;
 }
@@ -938,150 +1048,64 @@ int cec_read_pipeline_acquire(cec_read_pipeline* pl, size_t* slot, uint8_t** chu
     return CEC_OK;
 }
 
-int cec_read_pipeline_submit(cec_read_pipeline* pl, size_t slot, size_t n_parts) {
-    if (!pl || slot >= pl->slots.size() || n_parts == 0 || n_parts > pl->parts || pl->external)
+int cec_read_pipeline_submit_ex(cec_read_pipeline* pl, size_t slot, const cec_read_submit* a) {
+    if (!pl || !a || slot >= pl->slots.size() || a->n_parts == 0 || a->n_parts > pl->parts ||
+        (a->flags & ~unsigned(kModeBits | CEC_SUBMIT_PACKED)))
         return CEC_ERR_INVALID_ARGUMENT;
     ReadSlot& s = pl->slots[slot];
-    return pl->submit(s, s.h_chunks, n_parts, s.h_data);
+    const uint8_t* chunks = a->chunks ? a->chunks : s.h_chunks;
+    if (!chunks) return CEC_ERR_INVALID_ARGUMENT;  // CEC_PIPE_EXTERNAL: the caller's chunks
+    if (s.in_flight && (a->present || a->expected)) {
+        // the arrays below are read by the slot's last batch until it completes
+        DeviceGuard guard(pl->device);
+        PIPE_TRY(guard.status());
+        PIPE_TRY(hipEventSynchronize(s.done));
+        s.in_flight = false;
+    }
+    const size_t n = a->n_parts * pl->t;
+    if (a->present) std::memcpy(s.h_present, a->present, n);
+    if (a->expected) std::memcpy(s.h_expected, a->expected, n * 32);
+    const unsigned mode = a->flags & kModeBits;
+    return pl->submit(s, chunks, a->n_parts, a->data_out ? a->data_out : s.h_data, mode,
+                      (a->flags & CEC_SUBMIT_PACKED) != 0, a->carry_ids);
+}
+
+int cec_read_pipeline_submit(cec_read_pipeline* pl, size_t slot, size_t n_parts) {
+    if (!pl || pl->external) return CEC_ERR_INVALID_ARGUMENT;
+    cec_read_submit a{nullptr, nullptr, nullptr, n_parts, nullptr, nullptr, pl->default_mode};
+    return cec_read_pipeline_submit_ex(pl, slot, &a);
 }
 
 int cec_read_pipeline_submit_from(cec_read_pipeline* pl, size_t slot, const uint8_t* chunks,
                                   const uint8_t* present, const uint8_t* expected, size_t n_parts,
                                   uint8_t* data_out) {
-    if (!pl || slot >= pl->slots.size() || !chunks || n_parts == 0 || n_parts > pl->parts)
-        return CEC_ERR_INVALID_ARGUMENT;
-    ReadSlot& s = pl->slots[slot];
-    if (!data_out && !s.h_data && !pl->verify_only) return CEC_ERR_INVALID_ARGUMENT;
-    if (s.in_flight) {  // the flags below are read by the slot's last batch until it completes
-        DeviceGuard guard(pl->device);
-        PIPE_TRY(guard.status());
-        PIPE_TRY(hipEventSynchronize(s.done));
-        s.in_flight = false;
-    }
-    const size_t n = n_parts * pl->t;
-    if (present) std::memcpy(s.h_present, present, n);
-    if (expected) std::memcpy(s.h_expected, expected, n * 32);
-    return pl->submit(s, chunks, n_parts, data_out ? data_out : s.h_data);
+    if (!pl || !chunks) return CEC_ERR_INVALID_ARGUMENT;
+    cec_read_submit a{chunks, present, expected, n_parts, data_out, nullptr, pl->default_mode};
+    return cec_read_pipeline_submit_ex(pl, slot, &a);
 }
 
 int cec_read_pipeline_submit_packed(cec_read_pipeline* pl, size_t slot, const uint8_t* chunks,
                                     const uint8_t* present, const uint8_t* expected,
                                     size_t n_parts, uint8_t* data_out) {
-    if (!pl || slot >= pl->slots.size() || !chunks || n_parts == 0 || n_parts > pl->parts)
-        return CEC_ERR_INVALID_ARGUMENT;
-    ReadSlot& s = pl->slots[slot];
-    if (!data_out && !s.h_data && !pl->verify_only) return CEC_ERR_INVALID_ARGUMENT;
-    if (s.in_flight) {  // the flags below are read by the slot's last batch until it completes
-        DeviceGuard guard(pl->device);
-        PIPE_TRY(guard.status());
-        PIPE_TRY(hipEventSynchronize(s.done));
-        s.in_flight = false;
-    }
-    const size_t n = n_parts * pl->t;
-    if (present) std::memcpy(s.h_present, present, n);
-    if (expected) std::memcpy(s.h_expected, expected, n * 32);
-    return pl->submit(s, chunks, n_parts, data_out ? data_out : s.h_data, true);
+    if (!pl || !chunks) return CEC_ERR_INVALID_ARGUMENT;
+    cec_read_submit a{chunks, present, expected, n_parts, data_out, nullptr,
+                      pl->default_mode | CEC_SUBMIT_PACKED};
+    return cec_read_pipeline_submit_ex(pl, slot, &a);
+}
+
+int cec_read_pipeline_submit_carried(cec_read_pipeline* pl, size_t slot, size_t n_parts,
+                                     const int32_t* carry_ids) {
+    if (!pl || pl->external || !carry_ids) return CEC_ERR_INVALID_ARGUMENT;
+    cec_read_submit a{nullptr, nullptr, nullptr, n_parts, nullptr, carry_ids, pl->default_mode};
+    return cec_read_pipeline_submit_ex(pl, slot, &a);
 }
 
 int cec_read_pipeline_wait(cec_read_pipeline* pl, size_t slot, const uint8_t** data,
                            const uint8_t** verified, const int** part_status, size_t* n_parts) {
     if (!pl || slot >= pl->slots.size()) return CEC_ERR_INVALID_ARGUMENT;
     ReadSlot& s = pl->slots[slot];
-    if (s.in_flight) {
-        PIPE_TRY(hipEventSynchronize(s.done));
-        s.in_flight = false;
-    }
-    if (!s.checked && s.n_parts && pl->verify_only) {
-        for (size_t i = 0; i < s.n_parts * pl->t; ++i)  // verified by an earlier pass: trusted
-            if (s.h_present[i] == CEC_PRESENT_VERIFIED) s.h_ok[i] = 1;
-        s.data_ptrs.clear();
-        s.checked = true;
-    }
-    if (!s.checked && s.n_parts) {
-        const size_t t = pl->t, d = pl->d, n = s.n_parts;
-        for (size_t i = 0; i < n * t; ++i)  // verified by an earlier pass: trusted
-            if (s.h_present[i] == CEC_PRESENT_VERIFIED) s.h_ok[i] = 1;
-        // parts whose loaded chunks did not all verify: decode again from the verified ones
-        std::vector<uint8_t> mask(n * t, 1);
-        std::vector<size_t> redo;
-        for (size_t k = 0; k < n; ++k) {
-            if (s.h_status[k] != CEC_OK) continue;
-            bool bad = false;
-            size_t good = 0;
-            for (size_t i = 0; i < t; ++i) {
-                bad |= s.h_present[k * t + i] && !s.h_ok[k * t + i];
-                good += s.h_ok[k * t + i] ? 1 : 0;
-            }
-            if (!bad) continue;
-            if (good < d) {
-                s.h_status[k] = CEC_TOO_FEW_SHARDS_PRESENT;
-                continue;
-            }
-            std::copy(s.h_ok + k * t, s.h_ok + (k + 1) * t, mask.begin() + k * t);
-            redo.push_back(k);
-        }
-        if (!redo.empty()) {
-            DeviceGuard guard(pl->device);
-            PIPE_TRY(guard.status());
-            cec_part_batch b = pl->batch(s, n);
-            int st = cec_reconstruct_batch(pl->codec, &b, mask.data(), pl->resilver ? 0 : 1,
-                                           s.stream);
-            if (st != CEC_OK) {
-                g_pipe_error = cec_last_error();
-                return st;
-            }
-            for (size_t k : redo) {
-                st = pl->resilver ? pl->copy_missing_back(s, k, s.h_ok + k * t, s.stream)
-                                  : pl->copy_data_back(s, k, 1, s.stream);
-                if (st != CEC_OK) return st;
-            }
-            PIPE_TRY(hipStreamSynchronize(s.stream));
-        }
-        // CEC_READ_CARRY: the stash kept the verified chunks of every part with fewer than d of
-        // them (exactly the parts reported TooFewShardsPresent) in a reserved entry, while
-        // reservations lasted; those become the caller's carry ids, the rest go back
-        if (pl->carry) {
-            s.carry_ids.assign(n, -1);
-            for (size_t k = 0; k < n; ++k) {
-                const int32_t id = s.h_map[k];
-                if (id < 0 || s.h_status[k] != CEC_TOO_FEW_SHARDS_PRESENT) continue;
-                if (size_t(id) >= pl->carry_cap || pl->carry_used[size_t(id)] != pl->kReserved) {
-                    g_pipe_error = "carry stash returned an entry the batch did not reserve";
-                    return CEC_ERR_HIP;
-                }
-                pl->carry_used[size_t(id)] = pl->kHeld;
-                s.carry_ids[k] = id;
-            }
-            pl->carry_unreserve(s);
-        }
-        // Where each data chunk is: re-decoded parts and (without REBUILT_ONLY) every part in the
-        // data output; otherwise a loaded chunk stays in the chunk buffer it was read from (it
-        // verified: parts with a failed chunk were re-decoded) and a rebuilt one came back into
-        // the data output -- as did a carried part's verified data chunks (the caller's buffer
-        // does not hold them).
-        std::vector<uint8_t> redone(n, 0);
-        for (size_t k : redo) redone[k] = 1;
-        if (pl->resilver) {  // [parts][t]: verified chunks where they were read, others rebuilt
-            s.data_ptrs.resize(n * t);
-            for (size_t k = 0; k < n; ++k)
-                for (size_t i = 0; i < t; ++i)
-                    s.data_ptrs[k * t + i] = s.h_ok[k * t + i]
-                                                 ? s.src_chunks + s.src_off[k * t + i]
-                                                 : s.dst_data + (k * t + i) * pl->L;
-        } else {
-            s.data_ptrs.resize(n * d);
-            for (size_t k = 0; k < n; ++k)
-                for (size_t j = 0; j < d; ++j) {
-                    const uint8_t f = s.h_present[k * t + j];
-                    const bool from_pool = !s.carried.empty() && s.carried[k] &&
-                                           f == CEC_PRESENT_VERIFIED;
-                    const bool in_place = pl->rebuilt_only && !redone[k] && f && !from_pool;
-                    s.data_ptrs[k * d + j] = in_place ? s.src_chunks + s.src_off[k * t + j]
-                                                      : s.dst_data + (k * d + j) * pl->L;
-                }
-        }
-        s.checked = true;
-    }
+    const int st = pl->finish(s);
+    if (st != CEC_OK) return st;
     if (data) *data = s.dst_data ? s.dst_data : s.h_data;
     if (verified) *verified = s.h_ok;
     if (part_status) *part_status = s.h_status;
@@ -1089,41 +1113,46 @@ int cec_read_pipeline_wait(cec_read_pipeline* pl, size_t slot, const uint8_t** d
     return CEC_OK;
 }
 
-int cec_read_pipeline_data_chunks(cec_read_pipeline* pl, size_t slot, const uint8_t** ptrs) {
+int cec_read_pipeline_data_chunks(cec_read_pipeline* pl, size_t slot, const uint8_t** ptrs,
+                                  size_t capacity) {
     if (!pl || slot >= pl->slots.size() || !ptrs) return CEC_ERR_INVALID_ARGUMENT;
     ReadSlot& s = pl->slots[slot];
-    if (s.in_flight || !s.checked) {
-        const int st = cec_read_pipeline_wait(pl, slot, nullptr, nullptr, nullptr, nullptr);
-        if (st != CEC_OK) return st;
+    const int st = pl->finish(s);
+    if (st != CEC_OK) return st;
+    if (s.data_ptrs.size() > capacity) {
+        g_pipe_error = "data_chunks: the batch has more chunk pointers than the output holds";
+        return CEC_ERR_INVALID_ARGUMENT;
     }
     std::copy(s.data_ptrs.begin(), s.data_ptrs.end(), ptrs);
     return CEC_OK;
 }
 
-int cec_read_pipeline_carry_ids(cec_read_pipeline* pl, size_t slot, int32_t* ids) {
+int cec_read_pipeline_carry_ids(cec_read_pipeline* pl, size_t slot, int32_t* ids,
+                                size_t capacity) {
     if (!pl || slot >= pl->slots.size() || !ids || !pl->carry) return CEC_ERR_INVALID_ARGUMENT;
     ReadSlot& s = pl->slots[slot];
-    if (s.in_flight || !s.checked) {
-        const int st = cec_read_pipeline_wait(pl, slot, nullptr, nullptr, nullptr, nullptr);
-        if (st != CEC_OK) return st;
+    const int st = pl->finish(s);
+    if (st != CEC_OK) return st;
+    if (s.n_parts > capacity) {
+        g_pipe_error = "carry_ids: the batch has more parts than the output holds";
+        return CEC_ERR_INVALID_ARGUMENT;
     }
+    // the caller now holds these entries (until it submits them or releases them)
+    for (int32_t id : s.reserved)
+        if (pl->carry_used[size_t(id)] == pl->kReserved) pl->carry_used[size_t(id)] = pl->kHeld;
+    s.reserved.clear();
     for (size_t k = 0; k < s.n_parts; ++k) ids[k] = k < s.carry_ids.size() ? s.carry_ids[k] : -1;
     return CEC_OK;
-}
-
-int cec_read_pipeline_submit_carried(cec_read_pipeline* pl, size_t slot, size_t n_parts,
-                                     const int32_t* carry_ids) {
-    if (!pl || slot >= pl->slots.size() || n_parts == 0 || n_parts > pl->parts || pl->external ||
-        !carry_ids)
-        return CEC_ERR_INVALID_ARGUMENT;
-    ReadSlot& s = pl->slots[slot];
-    return pl->submit(s, s.h_chunks, n_parts, s.h_data, false, carry_ids);
 }
 
 int cec_read_pipeline_carry_release(cec_read_pipeline* pl, int32_t id) {
     if (!pl || !pl->carry_valid(id)) return CEC_ERR_INVALID_ARGUMENT;
     pl->carry_give_back(id);
     return CEC_OK;
+}
+
+size_t cec_read_pipeline_carry_held(const cec_read_pipeline* pl) {
+    return pl ? pl->held_entries() : 0;
 }
 
 int cec_read_pipeline_query(cec_read_pipeline* pl, size_t slot) {
@@ -1137,9 +1166,9 @@ int cec_read_pipeline_query(cec_read_pipeline* pl, size_t slot) {
 
 int cec_read_pipeline_drain(cec_read_pipeline* pl) {
     if (!pl) return CEC_ERR_INVALID_ARGUMENT;
-    for (size_t i = 0; i < pl->slots.size(); ++i)
-        if (pl->slots[i].in_flight) {
-            const int st = cec_read_pipeline_wait(pl, i, nullptr, nullptr, nullptr, nullptr);
+    for (ReadSlot& s : pl->slots)
+        if (s.in_flight) {
+            const int st = pl->finish(s);
             if (st != CEC_OK) return st;
         }
     return CEC_OK;

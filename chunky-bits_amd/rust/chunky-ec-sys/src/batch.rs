@@ -91,7 +91,8 @@ impl BatchWriter {
         devices: &[c_int],
     ) -> Result<BatchWriter, CecError> {
         let codec = ReedSolomon::new(data, parity)?;  // writer.rs:131
-        let multi = Multi::new(&codec, chunk_size, parts_per_batch, depth, devices)?;
+        let multi = Multi::with_kinds(&codec, chunk_size, parts_per_batch, depth, devices,
+                                     crate::sys::CEC_MULTI_WRITE)?;
         let window = parts_per_batch * depth * devices.len().max(1);
         // page-locked on the first GPU's NUMA node (the C++ loop's placement)
         let dev0 = devices.first().copied().unwrap_or(-1);
@@ -360,7 +361,10 @@ pub struct BatchReader {
     // per chunk of a window: the next location to read, and whether none is left
     cursor: [Vec<usize>; 2],
     exhausted: [Vec<bool>; 2],
+    // per part of a window: the scheduler's carry id of its verified chunks (-1: none kept)
+    carry: [Vec<i32>; 2],
     retries: u64,
+    carried: u64,
 }
 
 impl BatchReader {
@@ -374,7 +378,8 @@ impl BatchReader {
         devices: &[c_int],
     ) -> Result<BatchReader, CecError> {
         let codec = ReedSolomon::new(data, parity)?;  // file_part.rs:77
-        let multi = Multi::new(&codec, chunk_size, parts_per_batch, depth, devices)?;
+        let multi = Multi::with_kinds(&codec, chunk_size, parts_per_batch, depth, devices,
+                                     crate::sys::CEC_MULTI_READ)?;
         let window = parts_per_batch * devices.len().max(1);
         let dev0 = devices.first().copied().unwrap_or(-1);
         let t = data + parity;
@@ -388,6 +393,7 @@ impl BatchReader {
             status: [vec![0; window], vec![0; window]],
             cursor: [vec![0; window * t], vec![0; window * t]],
             exhausted: [vec![false; window * t], vec![false; window * t]],
+            carry: [vec![-1; window], vec![-1; window]],
             multi,
             codec,
             d: data,
@@ -395,12 +401,18 @@ impl BatchReader {
             chunk_size,
             window,
             retries: 0,
+            carried: 0,
         })
     }
 
     /// Part resubmissions so far (a part retried twice counts twice).
     pub fn retries(&self) -> u64 {
         self.retries
+    }
+
+    /// Resubmissions whose verified chunks stayed on the GPU (only the new chunks were sent).
+    pub fn carried(&self) -> u64 {
+        self.carried
     }
 
     /// The codec the parts were written with (`FilePart`'s d and p).
@@ -505,7 +517,9 @@ impl BatchReader {
         let out = self.out[slot].as_mut_ptr();
         let verified = self.verified[slot].as_mut_ptr();
         let status = self.status[slot].as_mut_ptr();
-        self.multi.submit_read(chunks, present, expected, cnt, out, verified, status)
+        let carry = self.carry[slot].as_mut_ptr();
+        self.multi.submit_read_carry(chunks, present, expected, cnt, out, verified, status,
+                                     std::ptr::null(), carry)
     }
 
     /// Waits for a window's job, retries its failed parts, then hands its parts to the sink.
@@ -529,10 +543,26 @@ impl BatchReader {
     }
 
     /// file_part.rs:92-107: the failed parts go again with the chunks that verified (flagged
-    /// `CEC_PRESENT_VERIFIED`, taken from the window's buffer: the bytes that verified) plus, up
-    /// to d, the failed chunks' next copies and then untried chunks, until each decodes; a part
-    /// with no copy left fails the read.
+    /// `CEC_PRESENT_VERIFIED`: kept on the GPU under the part's carry id, or, when the scheduler
+    /// kept none, sent again from the window's buffer: the bytes that verified) plus, up to d, the
+    /// failed chunks' next copies and then untried chunks, until each decodes; a part with no copy
+    /// left fails the read (its and the other open parts' carry ids go back).
     fn retry<F>(&mut self, w: &LiveRead, failed: &[usize], fetch: &mut F) -> Result<(), CecError>
+    where
+        F: FnMut(usize, usize, usize) -> Option<(usize, Vec<u8>)>,
+    {
+        let mut cid: Vec<i32> = failed.iter().map(|&q| self.carry[w.slot][q]).collect();
+        let res = self.retry_rounds(w, failed, fetch, &mut cid);
+        if res.is_err() {
+            for &id in cid.iter().filter(|&&id| id >= 0) {
+                let _ = self.multi.carry_release(id);
+            }
+        }
+        res
+    }
+
+    fn retry_rounds<F>(&mut self, w: &LiveRead, failed: &[usize], fetch: &mut F,
+                       cid: &mut [i32]) -> Result<(), CecError>
     where
         F: FnMut(usize, usize, usize) -> Option<(usize, Vec<u8>)>,
     {
@@ -562,6 +592,9 @@ impl BatchReader {
         let mut r_pres = vec![0u8; f * t];
         let mut r_exp = vec![0u8; f * t * 32];
         let mut r_ver = vec![0u8; f * t];
+        let mut r_status = vec![0 as c_int; f];
+        let mut r_cin = vec![-1i32; f];
+        let mut r_cout = vec![-1i32; f];
         let mut open: Vec<usize> = (0..f).collect();
         while !open.is_empty() {
             let g = open.len();
@@ -570,11 +603,14 @@ impl BatchReader {
                 r_exp[s * t * 32..(s + 1) * t * 32]
                     .copy_from_slice(&self.expected[w.slot][q * t * 32..(q + 1) * t * 32]);
                 let have = (0..t).filter(|&i| good[r * t + i]).count();
+                r_cin[s] = cid[r];
                 for i in 0..t {
                     let (x, y) = (r * t + i, s * t + i);
                     r_pres[y] = 0;
                     if good[x] {
-                        r_chunks[y * l..(y + 1) * l].copy_from_slice(&keep[x * l..(x + 1) * l]);
+                        if cid[r] < 0 {  // not kept on the GPU: send the bytes that verified
+                            r_chunks[y * l..(y + 1) * l].copy_from_slice(&keep[x * l..(x + 1) * l]);
+                        }
                         r_pres[y] = crate::sys::CEC_PRESENT_VERIFIED;
                     }
                 }
@@ -602,7 +638,19 @@ impl BatchReader {
                     return Err(CecError::Erasure(crate::Error::TooFewShardsPresent));
                 }
             }
-            let status = self.multi.read(&r_chunks, &r_pres, &r_exp, g, &mut r_out, &mut r_ver)?;
+            let job = unsafe {
+                self.multi.submit_read_carry(r_chunks.as_ptr(), r_pres.as_ptr(), r_exp.as_ptr(), g,
+                                             r_out.as_mut_ptr(), r_ver.as_mut_ptr(),
+                                             r_status.as_mut_ptr(), r_cin.as_ptr(),
+                                             r_cout.as_mut_ptr())
+            }?;
+            for &r in open.iter() {  // submitted: the ids are the job's now
+                if cid[r] >= 0 {
+                    self.carried += 1;
+                }
+                cid[r] = -1;
+            }
+            self.multi.wait(job)?;
             self.retries += g as u64;
             let mut still = Vec::new();
             let out: &mut [u8] = &mut self.out[w.slot];
@@ -611,10 +659,13 @@ impl BatchReader {
                 for i in 0..t {
                     good[r * t + i] = r_ver[s * t + i] != 0;
                 }
-                if status[s].is_ok() {
+                if r_status[s] == 0 {
                     out[q * d * l..(q + 1) * d * l].copy_from_slice(&r_out[s * d * l..(s + 1) * d * l]);
-                } else {
+                } else if r_status[s] == crate::sys::CEC_TOO_FEW_SHARDS_PRESENT {
+                    cid[r] = r_cout[s];
                     still.push(r);
+                } else {
+                    return Err(crate::check(r_status[s]).unwrap_err());
                 }
             }
             open = still;
@@ -909,7 +960,8 @@ impl BatchChecker {
         devices: &[c_int],
     ) -> Result<BatchChecker, CecError> {
         let codec = ReedSolomon::new(data, parity)?;  // file_part.rs:302
-        let multi = Multi::new(&codec, chunk_size, parts_per_batch, depth, devices)?;
+        let multi = Multi::with_kinds(&codec, chunk_size, parts_per_batch, depth, devices,
+                                     crate::sys::CEC_MULTI_READ)?;
         let window = parts_per_batch * devices.len().max(1);
         let dev0 = devices.first().copied().unwrap_or(-1);
         let t = data + parity;

@@ -33,7 +33,7 @@ pub mod sys {
         _private: [u8; 0],
     }
 
-    pub const CEC_ABI_VERSION: c_int = 2;
+    pub const CEC_ABI_VERSION: c_int = 3;
     /// cec_read_pipeline_new_ex / cec_multi_read flag: only rebuilt data chunks come back.
     pub const CEC_READ_REBUILT_ONLY: std::os::raw::c_uint = 1;
     /// cec_read_pipeline_new_ex flag: FilePart::resilver's compute (data and parity rebuilt).
@@ -46,6 +46,39 @@ pub mod sys {
     pub const CEC_PRESENT_VERIFIED: u8 = 0x80;
     /// Read-pipeline flag: keep retries' verified chunks on the device (carry pool).
     pub const CEC_READ_CARRY: std::os::raw::c_uint = 16;
+    /// cec_read_submit flag: the chunks are packed back to back (one upload).
+    pub const CEC_SUBMIT_PACKED: std::os::raw::c_uint = 32;
+    /// cec_multi_new_ex job kinds.
+    pub const CEC_MULTI_WRITE: std::os::raw::c_uint = 1;
+    pub const CEC_MULTI_READ: std::os::raw::c_uint = 2;
+    /// Status of a part with fewer than d verified chunks (retry it with more).
+    pub const CEC_TOO_FEW_SHARDS_PRESENT: c_int = 10;
+
+    /// cec_read_pipeline_submit_ex's arguments (include/chunky_ec.h).
+    #[repr(C)]
+    #[derive(Clone, Copy, Debug)]
+    pub struct cec_read_submit {
+        pub chunks: *const u8,
+        pub present: *const u8,
+        pub expected: *const u8,
+        pub n_parts: usize,
+        pub data_out: *mut u8,
+        pub carry_ids: *const i32,
+        pub flags: std::os::raw::c_uint,
+    }
+
+    /// cec_multi_shard_stats's counters (include/chunky_ec.h).
+    #[repr(C)]
+    #[derive(Clone, Copy, Debug, Default)]
+    pub struct cec_multi_stats {
+        pub device: c_int,
+        pub numa_node: c_int,
+        pub parts: u64,
+        pub pipelines_made: u64,
+        pub chunks_uploaded: u64,
+        pub chunks_carried: u64,
+        pub carry_held: u64,
+    }
 
     #[repr(C)]
     #[derive(Clone, Copy, Debug)]
@@ -224,6 +257,7 @@ pub mod sys {
             pipeline: *mut cec_read_pipeline,
             slot: usize,
             ptrs: *mut *const u8,
+            capacity: usize,
         ) -> c_int;
         pub fn cec_coalesce_stats(calls: *mut u64, launches: *mut u64);
         pub fn cec_build_info() -> *const std::os::raw::c_char;
@@ -277,7 +311,42 @@ pub mod sys {
             pipeline: *mut cec_read_pipeline,
             slot: usize,
             ids: *mut i32,
+            capacity: usize,
         ) -> c_int;
+        pub fn cec_read_pipeline_carry_held(pipeline: *const cec_read_pipeline) -> usize;
+        pub fn cec_read_pipeline_submit_ex(
+            pipeline: *mut cec_read_pipeline,
+            slot: usize,
+            submit: *const cec_read_submit,
+        ) -> c_int;
+        pub fn cec_pipelines_made() -> u64;
+        pub fn cec_multi_new_ex(
+            codec: *const cec_codec,
+            chunk_len: usize,
+            parts_per_batch: usize,
+            depth: usize,
+            devices: *const c_int,
+            n_devices: usize,
+            flags: std::os::raw::c_uint,
+            out: *mut *mut cec_multi,
+        ) -> c_int;
+        pub fn cec_multi_read_carry(
+            multi: *mut cec_multi,
+            chunks: *const u8,
+            present: *const u8,
+            expected: *const u8,
+            n_parts: usize,
+            data: *mut u8,
+            verified: *mut u8,
+            part_status: *mut c_int,
+            data_ptrs: *mut *const u8,
+            flags: std::os::raw::c_uint,
+            carry_in: *const i32,
+            carry_out: *mut i32,
+            job: *mut u64,
+        ) -> c_int;
+        pub fn cec_multi_carry_release(multi: *mut cec_multi, id: i32) -> c_int;
+        pub fn cec_multi_shard_stats(multi: *mut cec_multi, g: usize, out: *mut cec_multi_stats) -> c_int;
         pub fn cec_read_pipeline_submit_carried(
             pipeline: *mut cec_read_pipeline,
             slot: usize,
@@ -415,7 +484,7 @@ impl CecError {
     }
 }
 
-fn check(code: c_int) -> Result<(), CecError> {
+pub(crate) fn check(code: c_int) -> Result<(), CecError> {
     Err(CecError::Erasure(match code {
         0 => return Ok(()),
         1 => Error::TooFewShards,
@@ -878,8 +947,13 @@ impl ReadPipeline {
     /// are (the slot's chunk buffer or the rebuilt buffer); valid until the slot is re-acquired.
     /// `read_with_context`'s output is their concatenation (file_part.rs:130-133).
     pub fn data_chunks(&mut self, slot: usize, n_parts: usize) -> Result<Vec<Vec<&[u8]>>, CecError> {
-        let mut ptrs = vec![std::ptr::null::<u8>(); n_parts * self.d];
-        check_pipe(unsafe { sys::cec_read_pipeline_data_chunks(self.raw, slot, ptrs.as_mut_ptr()) })?;
+        // room for the largest batch a slot can hold, whatever n_parts says (the library writes
+        // one pointer per chunk of the slot's batch, and checks the capacity)
+        let mut ptrs = vec![std::ptr::null::<u8>(); self.parts * self.t];
+        check_pipe(unsafe {
+            sys::cec_read_pipeline_data_chunks(self.raw, slot, ptrs.as_mut_ptr(), ptrs.len())
+        })?;
+        ptrs.truncate(n_parts.min(self.parts) * self.d);
         Ok(ptrs
             .chunks(self.d)
             .map(|part| {
@@ -924,8 +998,11 @@ impl ReadPipeline {
     /// After [`ReadPipeline::wait`]: each of the slot's `n_parts` parts' carry entry (`None`: its
     /// verified chunks were not kept; it resends them flagged `CEC_PRESENT_VERIFIED`).
     pub fn carry_ids(&mut self, slot: usize, n_parts: usize) -> Result<Vec<Option<i32>>, CecError> {
-        let mut ids = vec![-1i32; n_parts.max(1)];
-        check_pipe(unsafe { sys::cec_read_pipeline_carry_ids(self.raw, slot, ids.as_mut_ptr()) })?;
+        // room for the largest batch a slot can hold (the library checks the capacity)
+        let mut ids = vec![-1i32; self.parts];
+        check_pipe(unsafe {
+            sys::cec_read_pipeline_carry_ids(self.raw, slot, ids.as_mut_ptr(), ids.len())
+        })?;
         Ok(ids.into_iter().take(n_parts).map(|id| if id >= 0 { Some(id) } else { None }).collect())
     }
 
@@ -1042,6 +1119,7 @@ fn check_multi(code: c_int) -> Result<(), CecError> {
 }
 
 impl Multi {
+    /// A scheduler for both job kinds (write and read / resilver / verify).
     pub fn new(
         codec: &ReedSolomon,
         chunk_len: usize,
@@ -1049,15 +1127,30 @@ impl Multi {
         depth: usize,
         devices: &[c_int],
     ) -> Result<Multi, CecError> {
+        Multi::with_kinds(codec, chunk_len, parts_per_batch, depth, devices,
+                          sys::CEC_MULTI_WRITE | sys::CEC_MULTI_READ)
+    }
+
+    /// A scheduler for the job kinds in `kinds` (`CEC_MULTI_WRITE`, `CEC_MULTI_READ`): every
+    /// shard makes those pipelines here, once (`cec_multi_new_ex`).
+    pub fn with_kinds(
+        codec: &ReedSolomon,
+        chunk_len: usize,
+        parts_per_batch: usize,
+        depth: usize,
+        devices: &[c_int],
+        kinds: std::os::raw::c_uint,
+    ) -> Result<Multi, CecError> {
         let mut raw = std::ptr::null_mut();
         check_multi(unsafe {
-            sys::cec_multi_new(
+            sys::cec_multi_new_ex(
                 codec.raw,
                 chunk_len,
                 parts_per_batch,
                 depth,
                 devices.as_ptr(),
                 devices.len(),
+                kinds,
                 &mut raw,
             )
         })?;
@@ -1199,6 +1292,60 @@ impl Multi {
             &mut job,
         ))?;
         Ok(job)
+    }
+
+    /// Asynchronous [`Multi::read`] that keeps retries' verified chunks on the GPUs
+    /// (`cec_multi_read_carry`): `carry_out[k]` receives, at [`Multi::wait`], an id for each part
+    /// reported `TooFewShardsPresent` whose verified chunks its shard kept (-1: none);
+    /// `carry_in[k]` (-1: none) hands such an id to the part's retry, whose
+    /// `CEC_PRESENT_VERIFIED` chunks then come from that GPU, not from `chunks`.  An id is used
+    /// once; ids that will not be used go back with [`Multi::carry_release`].
+    ///
+    /// # Safety
+    /// As [`Multi::submit_read`]; `carry_in` and `carry_out` (`n_parts` each, either may be
+    /// null) must stay valid until the job has been waited for.
+    #[allow(clippy::too_many_arguments)]
+    pub unsafe fn submit_read_carry(
+        &self,
+        chunks: *const u8,
+        present: *const u8,
+        expected: *const u8,
+        n_parts: usize,
+        data: *mut u8,
+        verified: *mut u8,
+        status: *mut c_int,
+        carry_in: *const i32,
+        carry_out: *mut i32,
+    ) -> Result<u64, CecError> {
+        let mut job = 0u64;
+        check_multi(sys::cec_multi_read_carry(
+            self.raw,
+            chunks,
+            present,
+            expected,
+            n_parts,
+            data,
+            verified,
+            status,
+            std::ptr::null_mut(),
+            0,
+            carry_in,
+            carry_out,
+            &mut job,
+        ))?;
+        Ok(job)
+    }
+
+    /// Gives back a carry id the caller will not use (`cec_multi_carry_release`).
+    pub fn carry_release(&self, id: i32) -> Result<(), CecError> {
+        check_multi(unsafe { sys::cec_multi_carry_release(self.raw, id) })
+    }
+
+    /// Shard `g`'s counters (`cec_multi_shard_stats`).
+    pub fn stats(&self, g: usize) -> Result<sys::cec_multi_stats, CecError> {
+        let mut st = sys::cec_multi_stats::default();
+        check_multi(unsafe { sys::cec_multi_shard_stats(self.raw, g, &mut st) })?;
+        Ok(st)
     }
 
     /// `FilePart::verify`'s compute (file_part.rs:228-251) for `n_parts` rows of d + p items:

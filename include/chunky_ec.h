@@ -48,7 +48,8 @@
 extern "C" {
 #endif
 
-#define CEC_ABI_VERSION 2  /* 2: CEC_PRESENT_VERIFIED moved from 2 to 0x80 */
+#define CEC_ABI_VERSION 3  /* 2: CEC_PRESENT_VERIFIED moved from 2 to 0x80; 3: read-pipeline
+                              * modes per submit, output capacities, scheduler carry */
 
 typedef enum cec_status {
     CEC_OK = 0,
@@ -326,53 +327,66 @@ int cec_read_pipeline_wait(cec_read_pipeline* pipeline, size_t slot, const uint8
                            const uint8_t** verified, const int** part_status, size_t* n_parts);
 int cec_read_pipeline_drain(cec_read_pipeline* pipeline);
 int cec_read_pipeline_query(cec_read_pipeline* pipeline, size_t slot);
-/* As cec_read_pipeline_new with flags.  CEC_READ_REBUILT_ONLY: submit copies back only the data
- * chunks it rebuilt (RS(10,4) with d random chunks loaded: 2.9 of 10 per part), since the
- * loaded ones are already in the caller's pinned chunk buffer; wait's *data then holds only
- * those, and cec_read_pipeline_data_chunks says where each data chunk is. */
+/* As cec_read_pipeline_new with flags: the default MODE of the submits above (mode bits
+ * CEC_READ_REBUILT_ONLY / CEC_READ_RESILVER / CEC_READ_VERIFY_ONLY, below), CEC_PIPE_EXTERNAL and
+ * CEC_READ_CARRY.  The device buffers are the same for every mode, so any submit may pick
+ * another mode (cec_read_pipeline_submit_ex): one pipeline serves verify, resilver and read in
+ * turn (FilePart::verify / resilver / read_with_context on the same parts, file_part.rs:73-390).
+ * Mode CEC_READ_REBUILT_ONLY: submit copies back only the data chunks it rebuilt (RS(10,4) with
+ * d random chunks loaded: 2.9 of 10 per part), since the loaded ones are already in the caller's
+ * pinned chunk buffer; wait's *data then holds only those, and cec_read_pipeline_data_chunks
+ * says where each data chunk is. */
 #define CEC_READ_REBUILT_ONLY 1u
 int cec_read_pipeline_new_ex(const cec_codec* codec, size_t chunk_len, size_t parts_per_batch,
                              size_t depth, unsigned flags, cec_read_pipeline** out);
-/* Read-pipeline flag: FilePart::resilver's compute (file_part.rs:253-308) instead of
- * read_with_context's.  Every chunk that does not verify (data AND parity: missing, or loaded
- * with a bad hash) is rebuilt from the first d verified chunks (reconstruct, not
- * reconstruct_data) and comes back into the slot's / the caller's output, which is then
- * [parts][d+p][chunk_len] (only the rebuilt chunks are written); cec_read_pipeline_data_chunks
- * gives d+p pointers per part (a verified chunk where it was read, a rebuilt one in the output):
- * what resilver writes back to storage is every chunk whose verified flag is 0. */
+/* Mode: FilePart::resilver's compute (file_part.rs:253-308) instead of read_with_context's.
+ * Every chunk that does not verify (data AND parity: missing, or loaded with a bad hash) is
+ * rebuilt from the first d verified chunks (reconstruct, not reconstruct_data) and comes back
+ * into the output, which is then [parts][d+p][chunk_len] (only the rebuilt chunks are written);
+ * cec_read_pipeline_data_chunks gives d+p pointers per part (a verified chunk where it was read,
+ * a rebuilt one in the output): what resilver writes back to storage is every chunk whose
+ * verified flag is 0. */
 #define CEC_READ_RESILVER 4u
-/* Read-pipeline flag: FilePart::verify's compute (file_part.rs:228-251): every loaded chunk is
- * hashed and compared with its metadata digest; nothing is decoded or copied back (wait gives
- * the verified flags; part_status is CEC_OK; data_out may be NULL). */
+/* Mode: FilePart::verify's compute (file_part.rs:228-251): every loaded chunk is hashed and
+ * compared with its metadata digest; nothing is decoded or copied back (wait gives the verified
+ * flags; part_status is CEC_OK; data_out may be NULL). */
 #define CEC_READ_VERIFY_ONLY 8u
-/* Read-pipeline flag (read mode only): keep retries' verified chunks on the device.  The
- * reference keeps a chunk that verified in memory while it draws another for the one that failed
- * (file_part.rs:92-107); without this flag the retry of a part sends its verified chunks up
- * again (CEC_PRESENT_VERIFIED).  With it, each batch keeps the verified chunks of every part it
- * will report CEC_TOO_FEW_SHARDS_PRESENT in a device carry pool, on the device right after the
- * verification (up to max(8, parts_per_batch/4) parts per batch, in part order; the pool holds
- * depth+1 times that many entries of (d+p) chunks and is made with the pipeline);
- * after wait, cec_read_pipeline_carry_ids gives each such part its entry (-1: none kept).  The
- * retry passes the ids to cec_read_pipeline_submit_carried: a part with an id takes its
- * CEC_PRESENT_VERIFIED chunks from the pool (the caller need not fill them in the slot) and its
- * data chunks among them come back like rebuilt ones (REBUILT_ONLY data_chunks point at the
- * data output for them).  An id is used once; one the caller will not use (an undecodable part)
- * goes back with cec_read_pipeline_carry_release. */
+/* Pipeline flag: keep retries' verified chunks on the device (read modes only; a resilver or
+ * verify submit keeps nothing).  The reference keeps a chunk that verified in memory while it
+ * draws another for the one that failed (file_part.rs:92-107); without this flag the retry of a
+ * part sends its verified chunks up again (CEC_PRESENT_VERIFIED).  With it, each batch keeps the
+ * verified chunks of every part it will report CEC_TOO_FEW_SHARDS_PRESENT in a device carry pool,
+ * on the device right after the verification (up to max(8, parts_per_batch/4) parts per batch,
+ * in part order; the pool holds depth+1 times that many entries of (d+p) chunks and is made with
+ * the pipeline).  After wait, cec_read_pipeline_carry_ids gives each such part its entry (-1:
+ * none kept) and hands the entries to the caller; entries of a batch whose ids were not taken go
+ * back when its slot is submitted again.  The retry passes the ids with its submit (carry_ids of
+ * cec_read_submit): a part with an id takes its CEC_PRESENT_VERIFIED chunks from the pool (the
+ * caller need not supply them) and its data chunks among them come back like rebuilt ones
+ * (REBUILT_ONLY data_chunks point at the data output for them).  An id is only accepted for the
+ * part it was kept for (same metadata digests, and every CEC_PRESENT_VERIFIED chunk one the
+ * entry holds): CEC_ERR_INVALID_ARGUMENT otherwise.  An id is used once; one the caller will not
+ * use (an undecodable part) goes back with cec_read_pipeline_carry_release. */
 #define CEC_READ_CARRY 16u
-/* After wait: ids[k] = the carry entry of part k of the slot's batch, or -1. */
-int cec_read_pipeline_carry_ids(cec_read_pipeline* pipeline, size_t slot, int32_t* ids);
+/* After wait: ids[k] = the carry entry of part k of the slot's batch, or -1; capacity = the
+ * entries ids holds (CEC_ERR_INVALID_ARGUMENT when the batch has more parts). */
+int cec_read_pipeline_carry_ids(cec_read_pipeline* pipeline, size_t slot, int32_t* ids,
+                                size_t capacity);
 /* As cec_read_pipeline_submit, with carry_ids[n_parts] (-1 = none) for the parts whose verified
  * chunks come from the carry pool. */
 int cec_read_pipeline_submit_carried(cec_read_pipeline* pipeline, size_t slot, size_t n_parts,
                                      const int32_t* carry_ids);
 /* Hands an unused carry entry back. */
 int cec_read_pipeline_carry_release(cec_read_pipeline* pipeline, int32_t id);
-/* After (or instead of) wait: ptrs[k*d + j] = the chunk_len bytes of data chunk j of part k —
- * in the slot's chunk buffer (loaded and verified, REBUILT_ONLY) or in its data buffer
- * (rebuilt, re-decoded, or without REBUILT_ONLY).  Valid until the slot is acquired again;
- * undefined for parts whose status is not CEC_OK. */
+/* Carry entries the caller holds (taken with carry_ids, not yet submitted or released). */
+size_t cec_read_pipeline_carry_held(const cec_read_pipeline* pipeline);
+/* After (or instead of) wait: ptrs[k*out + j] = the chunk_len bytes of output chunk j of part k
+ * (out = d, or d+p for a resilver batch) -- in the chunk buffer (loaded and verified,
+ * REBUILT_ONLY / resilver) or in the data output (rebuilt, re-decoded, or without REBUILT_ONLY).
+ * capacity = the pointers ptrs holds (CEC_ERR_INVALID_ARGUMENT when the batch has more).  Valid
+ * until the slot is acquired again; undefined for parts whose status is not CEC_OK. */
 int cec_read_pipeline_data_chunks(cec_read_pipeline* pipeline, size_t slot,
-                                  const uint8_t** ptrs);
+                                  const uint8_t** ptrs, size_t capacity);
 /* As cec_read_pipeline_submit, with the loaded chunk bytes read from the caller's chunks
  * [n_parts][d+p][chunk_len] and the data written to data_out [n_parts][d][chunk_len] (NULL: the
  * slot's own buffer); present / expected (NULL: the slot's arrays as filled after acquire) are
@@ -391,6 +405,30 @@ int cec_read_pipeline_submit_from(cec_read_pipeline* pipeline, size_t slot, cons
 int cec_read_pipeline_submit_packed(cec_read_pipeline* pipeline, size_t slot,
                                     const uint8_t* chunks, const uint8_t* present,
                                     const uint8_t* expected, size_t n_parts, uint8_t* data_out);
+/* The general submit: every form above is this with the pipeline's default mode.
+ *   chunks    -- NULL: the slot's pinned chunk buffer (not for CEC_PIPE_EXTERNAL pipelines);
+ *   present, expected -- NULL: the slot's arrays as filled after acquire; else copied in;
+ *   data_out  -- NULL: the slot's own output (CEC_ERR_INVALID_ARGUMENT when it is smaller than
+ *                the mode writes, or absent); [n][d][L], or [n][d+p][L] for CEC_READ_RESILVER;
+ *   carry_ids -- NULL, or [n_parts] carry ids (-1 = none) of a CEC_READ_CARRY pipeline;
+ *   flags     -- the mode bits (0 = read_with_context) | CEC_SUBMIT_PACKED (`chunks` holds
+ *                back to back exactly the chunks that go up: present != 0, except the
+ *                CEC_PRESENT_VERIFIED chunks of parts with a carry id). */
+#define CEC_SUBMIT_PACKED 32u
+typedef struct cec_read_submit {
+    const uint8_t* chunks;
+    const uint8_t* present;
+    const uint8_t* expected;
+    size_t n_parts;
+    uint8_t* data_out;
+    const int32_t* carry_ids;
+    unsigned flags;
+} cec_read_submit;
+int cec_read_pipeline_submit_ex(cec_read_pipeline* pipeline, size_t slot,
+                                const cec_read_submit* submit);
+/* Write and read pipelines made by this process so far (a scheduler makes its own once, in
+ * cec_multi_new: tests check that no job makes another). */
+uint64_t cec_pipelines_made(void);
 
 /* ---------------------------------------------------------------------------------------- */
 /* Multi-GPU part scheduler (one process, several GPUs: SURVEY.md §8e)                       */
@@ -408,6 +446,17 @@ int cec_read_pipeline_submit_packed(cec_read_pipeline* pipeline, size_t slot,
 typedef struct cec_multi cec_multi;
 int cec_multi_new(const cec_codec* codec, size_t chunk_len, size_t parts_per_batch, size_t depth,
                   const int* devices, size_t n_devices, cec_multi** out);
+/* As cec_multi_new for the job kinds in flags: CEC_MULTI_WRITE (cec_multi_encode_hash),
+ * CEC_MULTI_READ (read / resilver / verify); cec_multi_new = both.  Each shard makes its
+ * pipelines for those kinds (one write pipeline; one read pipeline with a carry pool, whose mode
+ * is picked per job) before this returns -- no job ever makes or frees a pipeline, so no stream
+ * or device buffer is created while other shards' batches run -- and an allocation failure is
+ * reported here.  A job of a kind the scheduler was not made for: CEC_ERR_INVALID_ARGUMENT. */
+#define CEC_MULTI_WRITE 1u
+#define CEC_MULTI_READ 2u
+int cec_multi_new_ex(const cec_codec* codec, size_t chunk_len, size_t parts_per_batch,
+                     size_t depth, const int* devices, size_t n_devices, unsigned flags,
+                     cec_multi** out);
 void cec_multi_free(cec_multi* multi);
 size_t cec_multi_shards(const cec_multi* multi);
 /* Shard g's device ordinal, its NUMA node, and the parts it has processed. */
@@ -425,6 +474,36 @@ int cec_multi_encode_hash(cec_multi* multi, const uint8_t* data, size_t n_parts,
 int cec_multi_read(cec_multi* multi, const uint8_t* chunks, const uint8_t* present,
                    const uint8_t* expected, size_t n_parts, uint8_t* data, uint8_t* verified,
                    int* part_status, const uint8_t** data_ptrs, unsigned flags, uint64_t* job);
+/* As cec_multi_read, keeping retries' verified chunks on the devices (file_part.rs:92-107 keeps
+ * them in memory while it draws another chunk).  carry_out[n] (nullable): for each part reported
+ * CEC_TOO_FEW_SHARDS_PRESENT, an id under which its shard keeps the part's verified chunks on its
+ * GPU (-1: none kept, e.g. the shard's carry pool is full; every other part gets -1).
+ * carry_in[n] (nullable): per part, -1 or an id from an earlier job's carry_out.  A part with an
+ * id runs on the shard that holds its chunks (the others split as usual) and takes its
+ * CEC_PRESENT_VERIFIED chunks from there: `chunks` need not hold them and they are not sent
+ * again.  An id is accepted only for the part it was kept for (same expected digests, its
+ * CEC_PRESENT_VERIFIED chunks among the kept ones) and used once; the job fails with
+ * CEC_ERR_INVALID_ARGUMENT otherwise.  Ids the caller will not use go back with
+ * cec_multi_carry_release. */
+int cec_multi_read_carry(cec_multi* multi, const uint8_t* chunks, const uint8_t* present,
+                         const uint8_t* expected, size_t n_parts, uint8_t* data,
+                         uint8_t* verified, int* part_status, const uint8_t** data_ptrs,
+                         unsigned flags, const int32_t* carry_in, int32_t* carry_out,
+                         uint64_t* job);
+int cec_multi_carry_release(cec_multi* multi, int32_t id);
+/* Shard g's counters: device, NUMA node, parts processed, pipelines made (1 per job kind, at
+ * cec_multi_new), chunks sent to the GPU by read jobs, chunks read jobs took from the carry pool
+ * instead, carry entries the caller holds. */
+typedef struct cec_multi_stats {
+    int device;
+    int numa_node;
+    uint64_t parts;
+    uint64_t pipelines_made;
+    uint64_t chunks_uploaded;
+    uint64_t chunks_carried;
+    uint64_t carry_held;
+} cec_multi_stats;
+int cec_multi_shard_stats(cec_multi* multi, size_t g, cec_multi_stats* out);
 /* FilePart::resilver's compute (file_part.rs:253-308) for n_parts parts: as cec_multi_read, but
  * every chunk that does not verify (data AND parity) is rebuilt (reconstruct) into
  * rebuilt [n][d+p][L] (the verified ones are not written there); chunk_ptrs[n*(d+p)] (nullable)

@@ -319,6 +319,13 @@ struct CachedMulti {
     std::shared_ptr<cec_multi> multi;
 };
 
+// Batched read retries leave their verified chunks on the GPU (cec_multi_read_carry) unless this
+// is false (then they are sent again): the with / without figure of tools/cp_bench.
+inline std::atomic<bool>& read_carry() {
+    static std::atomic<bool> on{true};
+    return on;
+}
+
 inline CachedMulti& cached_multi_entry() {
     thread_local CachedMulti e;
     return e;
@@ -333,7 +340,8 @@ inline cec_multi* cached_multi(size_t d, size_t p, size_t L, size_t parts, size_
         e.multi.reset();
         e.codec = std::make_shared<ReedSolomon>(d, p);
         cec_multi* raw = nullptr;
-        check(cec_multi_new(e.codec->raw(), L, parts, depth, devices.data(), devices.size(), &raw));
+        check_multi(cec_multi_new(e.codec->raw(), L, parts, depth, devices.data(), devices.size(),
+                                  &raw));
         e.multi = std::shared_ptr<cec_multi>(raw, cec_multi_free);
         e.key = key;
     }
@@ -1076,6 +1084,7 @@ struct FileReference {
         std::vector<uint8_t> present, expected, verified, exhausted;
         std::vector<size_t> cursor;  // per chunk: the next location to read
         std::vector<int> status;
+        std::vector<int32_t> carry;  // per part: the scheduler's carry id of its verified chunks
     };
     static constexpr size_t kMaxReadWindows = 8;
     // The windows (and their page-locked buffers) of this thread, shared by every read_run
@@ -1108,6 +1117,7 @@ struct FileReference {
             w.exhausted.assign(cnt * t, 0);
             w.cursor.assign(cnt * t, 0);
             w.status.assign(cnt, 0);
+            w.carry.assign(cnt, -1);
             // The reference loads d chunks per part (file_part.rs:86-107): the first d that have
             // a copy here (data chunks first: no rebuild when they are all there), each at its
             // first location that reads.
@@ -1128,9 +1138,11 @@ struct FileReference {
                     ++loaded;
                 }
             });
-            detail::check_multi(cec_multi_read(m, ch, w.present.data(), w.expected.data(), cnt,
-                                               out, w.verified.data(), w.status.data(), nullptr, 0,
-                                               &w.job));
+            detail::check_multi(cec_multi_read_carry(m, ch, w.present.data(), w.expected.data(),
+                                                     cnt, out, w.verified.data(), w.status.data(),
+                                                     nullptr, 0, nullptr,
+                                                     detail::read_carry() ? w.carry.data() : nullptr,
+                                                     &w.job));
             w.first = at;
             w.n = cnt;
             w.live = true;
@@ -1172,10 +1184,27 @@ struct FileReference {
     // read, and a chunk with no valid copy left is replaced by another chunk.  The failed parts of
     // a window are resubmitted with the chunks that verified (marked CEC_PRESENT_VERIFIED: not
     // hashed again) plus, up to d, the failed chunks' next copies and then untried chunks, until
-    // they decode or no copy is left (TooFewShardsPresent, as the reference's read).  The rebuilt
-    // data of window part q goes to out + q*d*L.
+    // they decode or no copy is left (TooFewShardsPresent, as the reference's read).  The
+    // verified chunks of a part the scheduler kept on its GPU (its carry id) are not sent again;
+    // the others are re-sent from their verified copies.  The rebuilt data of window part q goes
+    // to out + q*d*L.
     void retry(const ChunkStore& src, cec_multi* m, size_t k0, size_t d, size_t t, size_t L,
                const ReadWindow& w, const std::vector<size_t>& failed, uint8_t* out) const {
+        const size_t f = failed.size();
+        std::vector<int32_t> cid(f);  // per failed part: its carry id (-1: none held)
+        for (size_t r = 0; r < f; ++r) cid[r] = w.carry[failed[r]];
+        try {
+            retry_rounds(src, m, k0, d, t, L, w, failed, out, cid);
+        } catch (...) {
+            for (int32_t id : cid)  // ids the failed read will not use go back to their GPUs
+                if (id >= 0) (void)cec_multi_carry_release(m, id);
+            throw;
+        }
+    }
+
+    void retry_rounds(const ChunkStore& src, cec_multi* m, size_t k0, size_t d, size_t t,
+                      size_t L, const ReadWindow& w, const std::vector<size_t>& failed,
+                      uint8_t* out, std::vector<int32_t>& cid) const {
         const size_t f = failed.size();
         std::vector<uint8_t> tried(f * t), good(f * t), exhausted(f * t);
         std::vector<size_t> cursor(f * t);
@@ -1197,6 +1226,8 @@ struct FileReference {
         Bytes chunks(f * t * L), data(f * d * L);
         std::vector<uint8_t> present(f * t), expected(f * t * 32), verified(f * t);
         std::vector<int> status(f);
+        std::vector<int32_t> carry_in(f, -1), carry_out(f, -1);
+        const bool carry = detail::read_carry();
         std::vector<size_t> open(f);
         for (size_t r = 0; r < f; ++r) open[r] = r;
         while (!open.empty()) {
@@ -1208,11 +1239,13 @@ struct FileReference {
                 const size_t r = open[q];
                 const FilePart& part = parts[k0 + w.first + failed[r]];
                 size_t have = 0, added = 0;
+                carry_in[q] = cid[r];
                 for (size_t i = 0; i < t; ++i) {
                     std::memcpy(&expected[(q * t + i) * 32], part.chunk(i).hash.digest().data(), 32);
                     if (!good[r * t + i]) continue;
                     ++have;
-                    std::memcpy(&chunks[(q * t + i) * L], held[r * t + i]->data(), L);
+                    if (cid[r] < 0)  // not kept on the GPU: send the copy that verified
+                        std::memcpy(&chunks[(q * t + i) * L], held[r * t + i]->data(), L);
                     present[q * t + i] = CEC_PRESENT_VERIFIED;
                 }
                 for (size_t i : detail::draw_order(&good[r * t], &tried[r * t], &exhausted[r * t], t)) {
@@ -1232,17 +1265,22 @@ struct FileReference {
                 if (added == 0) throw ErasureError(Error::TooFewShardsPresent);
             }
             uint64_t job = 0;
-            detail::check_multi(cec_multi_read(m, chunks.data(), present.data(), expected.data(), g,
-                                               data.data(), verified.data(), status.data(),
-                                               nullptr, 0, &job));
+            detail::check_multi(cec_multi_read_carry(m, chunks.data(), present.data(),
+                                                     expected.data(), g, data.data(),
+                                                     verified.data(), status.data(), nullptr, 0,
+                                                     carry_in.data(),
+                                                     carry ? carry_out.data() : nullptr, &job));
+            for (size_t q = 0; q < g; ++q) cid[open[q]] = -1;  // the job's ids now
             detail::check_multi(cec_multi_wait(m, job));
             for (size_t q = 0; q < g; ++q) {
                 const size_t r = open[q];
                 for (size_t i = 0; i < t; ++i) good[r * t + i] = verified[q * t + i] != 0;
-                if (status[q] == CEC_OK)
+                if (status[q] == CEC_OK) {
                     std::memcpy(out + failed[r] * d * L, &data[q * d * L], d * L);
-                else
+                } else {
+                    cid[r] = carry_out[q];
                     next_open.push_back(r);
+                }
             }
             open.swap(next_open);
         }

@@ -42,13 +42,26 @@ def _arr(b):
 
 
 class FakeMulti:
-    """cec_multi's job contract, computed with the oracle; `live` = jobs not yet waited for."""
+    """cec_multi's job contract, computed with the oracle; `live` = jobs not yet waited for.
+    Carry (cec_multi_read_carry): a part reported TooFewShardsPresent with a verified chunk gets
+    an id whose entry keeps its verified chunks; a retry given the id takes its
+    PRESENT_VERIFIED chunks from the entry (the caller's buffer is not read for them) and is
+    refused unless the id is held and was kept for that part.  `uploaded` counts the chunks a
+    read read from the caller's buffer."""
     ids = itertools.count(1)
+    WRITE, READ = 1, 2
 
-    def __init__(self, codec, chunk_len, parts_per_batch, depth, devices):
+    def __init__(self, codec, chunk_len, parts_per_batch, depth, devices, kinds=3):
         self.d, self.p = codec.data_shard_count(), codec.parity_shard_count()
         self.t, self.L = self.d + self.p, chunk_len
         self.live = set()
+        self.kinds = kinds
+        self.pool = {}  # carry id -> (kept mask, expected digests, chunk bytes)
+        self.next_carry = itertools.count(0)
+        self.uploaded = self.carried = 0
+
+    def carry_release(self, cid):
+        del self.pool[int(cid)]
 
     def _job(self):
         j = next(self.ids)
@@ -68,15 +81,30 @@ class FakeMulti:
                 dig[k, i] = np.frombuffer(hashlib.sha256(c.tobytes()).digest(), np.uint8)
         return self._job()
 
-    def read(self, chunks, present, expected, n, data, verified, status, rebuilt_only=False):
+    def read(self, chunks, present, expected, n, data, verified, status, rebuilt_only=False,
+             carry_in=None, carry_out=None):
+        assert self.kinds & self.READ
         d, t, L = self.d, self.t, self.L
-        ch = _arr(chunks)[:n * t * L].reshape(n, t, L)
+        ch = _arr(chunks)[:n * t * L].reshape(n, t, L).copy()
         pres = np.asarray(present).reshape(-1, t)
         exp = np.asarray(expected).reshape(-1, t, 32)
         out = _arr(data)[:n * d * L].reshape(n, d, L)
         ver = np.asarray(verified).reshape(-1, t)
         st = np.asarray(status)
         for k in range(n):
+            cid = -1 if carry_in is None else int(carry_in[k])
+            if cid >= 0:  # the entry replaces the part's verified chunks
+                mask, want, kept = self.pool.pop(cid)
+                assert np.array_equal(want, exp[k]), "carry id of another part"
+                assert all(mask[i] for i in range(t) if pres[k, i] == PRESENT_VERIFIED)
+                for i in range(t):
+                    if pres[k, i] == PRESENT_VERIFIED:
+                        ch[k, i] = kept[i]
+                        self.carried += 1
+            self.uploaded += sum(1 for i in range(t)
+                                 if pres[k, i] and not (cid >= 0 and pres[k, i] == PRESENT_VERIFIED))
+            if carry_out is not None:
+                carry_out[k] = -1
             for i in range(t):
                 if pres[k, i] == PRESENT_VERIFIED:
                     ver[k, i] = 1
@@ -86,6 +114,10 @@ class FakeMulti:
                     ver[k, i] = 0
             if ver[k].sum() < d:
                 st[k] = TOO_FEW_SHARDS_PRESENT
+                if carry_out is not None and ver[k].any():
+                    c = next(self.next_carry)
+                    self.pool[c] = (ver[k].copy(), exp[k].copy(), ch[k].copy())
+                    carry_out[k] = c
                 continue
             code, rec = oracle.reconstruct(d, self.p, [ch[k, i].copy() if ver[k, i] else None
                                                        for i in range(t)], data_only=True)
@@ -272,6 +304,10 @@ def test_batch_reader_loop(fakes):
     assert [k for k, _ in got] == list(range(n))
     assert all(b == chunks[k, :D].tobytes() for k, b in got)
     assert r.retries == 3 and r.multi.live == set()
+    # every retried part's verified chunks stayed with the scheduler (carry): the retries sent
+    # only their new chunks (9: 1, 12: 2, 16: 1) and no carry entry is left
+    assert r.carried_parts == 3 and r.multi.carried == 2 + 1 + 2 and r.multi.pool == {}
+    assert r.multi.uploaded == n * D + 1 + 2 + 1
     # part 12: its damaged chunks have no further location (fetch from 1 finds none), then the
     # two parity chunks are drawn
     assert [c for c in st.calls if c[0] == 12] == [(12, i, 0) for i in range(D)] + \
@@ -316,6 +352,7 @@ def test_batch_reader_out_of_chunks(fakes):
         r.read(9, st.fetch, lambda k: dig[k], lambda k, data: got.append(k))
     assert getattr(e.value, "code", None) == TOO_FEW_SHARDS_PRESENT
     assert got == [0, 1, 2, 3] and r.multi.live == set()
+    assert r.multi.pool == {}  # the failed part's carry id went back
 
 
 def _file(nbytes, seed, d=D, p=P, chunk=L):

@@ -72,7 +72,7 @@ def test_status_codes_match_crate_order():
              "InvalidShardFlags", "InvalidIndex"]
     for code, name in enumerate(names):
         assert ce.status_name(code) == name
-    assert ce.abi_version() == ce.ABI_VERSION == 2
+    assert ce.abi_version() == ce.ABI_VERSION == 3
 
 
 @pytest.mark.parametrize("d,p", [(1, 1), (3, 2), (10, 4), (20, 8), (5, 5), (17, 3), (128, 128),
@@ -138,13 +138,15 @@ def test_argument_errors_precede_device_use():
 
 
 def test_read_pipeline_argument_checks_precede_device_use():
-    """cec_read_pipeline_new_ex rejects unknown flags, exclusive modes (RESILVER with
-    VERIFY_ONLY; CARRY with either) and bad shapes before any HIP call; without a device a valid
-    request reports NoDevice (no host-side fallback pipeline)."""
+    """cec_read_pipeline_new_ex rejects unknown flags (CEC_SUBMIT_PACKED is a submit flag),
+    exclusive default modes (RESILVER with VERIFY_ONLY) and bad shapes before any HIP call;
+    without a device a valid request reports NoDevice (no host-side fallback pipeline).  CARRY
+    goes with any default mode since ABI 3 (modes are per submit; only read submits keep
+    chunks)."""
     import chunky_ec as ce
     rs = ce.ReedSolomon(10, 4)
-    for args in [(1 << 20, 4, 2, 32), (1 << 20, 4, 2, 12), (1 << 20, 4, 2, 16 | 4),
-                 (1 << 20, 4, 2, 16 | 8), (0, 4, 2, 0), (1 << 20, 0, 2, 0),
+    for args in [(1 << 20, 4, 2, 32), (1 << 20, 4, 2, 64), (1 << 20, 4, 2, 12),
+                 (1 << 20, 4, 2, 16 | 12), (0, 4, 2, 0), (1 << 20, 0, 2, 0),
                  (1 << 20, 4, 0, 0),
                  (1 << 20, 4, 17, 0)]:
         with pytest.raises(ce.Error) as e:
@@ -154,9 +156,11 @@ def test_read_pipeline_argument_checks_precede_device_use():
         with pytest.raises(ce.Error) as e:
             ce.ReadPipeline(rs, 1 << 20, 4, 2, ce.ReadPipeline.REBUILT_ONLY)
         assert e.value.code == ce.ERR_NO_DEVICE
-        with pytest.raises(ce.Error) as e:
-            ce.ReadPipeline(rs, 1 << 20, 4, 2, ce.ReadPipeline.REBUILT_ONLY | ce.ReadPipeline.CARRY)
-        assert e.value.code == ce.ERR_NO_DEVICE
+        for flags in (ce.ReadPipeline.REBUILT_ONLY | ce.ReadPipeline.CARRY,
+                      ce.READ_RESILVER | ce.ReadPipeline.CARRY | ce.PIPE_EXTERNAL):
+            with pytest.raises(ce.Error) as e:
+                ce.ReadPipeline(rs, 1 << 20, 4, 2, flags)
+            assert e.value.code == ce.ERR_NO_DEVICE
 
 
 def test_synth_byte_host_mirror_is_deterministic():
@@ -178,6 +182,10 @@ def test_write_pipeline_and_multi_argument_checks_precede_device_use():
     for devices in ([], list(range(65))):
         with pytest.raises(ce.Error) as e:
             ce.Multi(rs, 1 << 20, 4, 2, devices)
+        assert e.value.code == ce.ERR_INVALID_ARGUMENT
+    for kinds in (0, 4, ce.Multi.WRITE | 8):  # no job kind / an unknown one
+        with pytest.raises(ce.Error) as e:
+            ce.Multi(rs, 1 << 20, 4, 2, [0], kinds=kinds)
         assert e.value.code == ce.ERR_INVALID_ARGUMENT
     if ce.device_count() == 0:
         with pytest.raises(ce.Error) as e:

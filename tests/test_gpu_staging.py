@@ -40,8 +40,8 @@ def test_knob_reload_between_calls_keeps_results(knob_env):
     L = 65536
     data = list(np.random.default_rng(4).integers(0, 256, size=(10, L), dtype=np.uint8))
     base = _encode(rs, data, L)
-    for name, val in (("CEC_APPLY_BS", "0"), ("CEC_APPLY_TUNE", "g8"), ("CEC_APPLY_XCD", "0"),
-                      ("CEC_COALESCE_D2H_WAIT", "device")):
+    for name, val in (("CEC_APPLY_BS", "0"), ("CEC_COALESCE_US", "0"),
+                      ("CEC_COALESCE_INFLIGHT", "1")):
         knob_env.set(name, val)
         assert _encode(rs, data, L) == base, name
     ce.reload_knobs()

@@ -117,7 +117,7 @@ def test_read_pipeline_small_batches_with_redo(flags):
         assert np.array_equal(ver.astype(bool), present.astype(bool) & ~bad), b
         if flags == ce.READ_RESILVER:  # every chunk, verified where read or rebuilt
             ptrs = (ctypes.c_void_p * (P * t))()
-            assert ce._lib.cec_read_pipeline_data_chunks(rp._h, slot, ptrs) == 0
+            assert ce._lib.cec_read_pipeline_data_chunks(rp._h, slot, ptrs, len(ptrs)) == 0
             for q, k in enumerate(idx):
                 for i in range(t):
                     assert ctypes.string_at(ptrs[q * t + i], L) == full[k, i].tobytes(), (b, q, i)

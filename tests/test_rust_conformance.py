@@ -18,7 +18,8 @@ C_BASE = {"size_t": "usize", "int": "c_int", "unsigned": "c_uint", "unsigned int
           "uint64_t": "u64", "uint8_t": "u8", "int32_t": "i32", "char": "c_char", "void": "c_void",
           "cec_codec": "cec_codec", "cec_pipeline": "cec_pipeline",
           "cec_read_pipeline": "cec_read_pipeline", "cec_multi": "cec_multi",
-          "cec_part_batch": "cec_part_batch"}
+          "cec_part_batch": "cec_part_batch", "cec_read_submit": "cec_read_submit",
+          "cec_multi_stats": "cec_multi_stats"}
 
 
 def _strip_c_comments(src):
@@ -105,16 +106,17 @@ def test_rust_declares_every_header_function_with_matching_types():
 def test_part_batch_layout_and_constants_match():
     hsrc = _strip_c_comments(open(HEADER).read())
     rsrc = open(RUST).read()
-    cfields = re.search(r"typedef struct cec_part_batch \{(.*?)\}", hsrc, flags=re.S).group(1)
-    cf = [(c_type(f.strip()), f.strip().split()[-1].lstrip("*")) for f in cfields.split(";")
-          if f.strip()]
-    rfields = re.search(r"pub struct cec_part_batch \{(.*?)\}", rsrc, flags=re.S).group(1)
-    rf = [(rust_type(f.split(":", 1)[1]), f.split(":", 1)[0].replace("pub", "").strip())
-          for f in rfields.split(",") if ":" in f]
-    assert [(t, n) for t, n in cf] == [(t, n) for t, n in rf]
+    for struct in ("cec_part_batch", "cec_read_submit", "cec_multi_stats"):
+        cfields = re.search(rf"typedef struct {struct} \{{(.*?)\}}", hsrc, flags=re.S).group(1)
+        cf = [(c_type(f.strip()), f.strip().split()[-1].lstrip("*")) for f in cfields.split(";")
+              if f.strip()]
+        rfields = re.search(rf"pub struct {struct} \{{(.*?)\}}", rsrc, flags=re.S).group(1)
+        rf = [(rust_type(f.split(":", 1)[1]), f.split(":", 1)[0].replace("pub", "").strip())
+              for f in rfields.split(",") if ":" in f]
+        assert [(t, n) for t, n in cf] == [(t, n) for t, n in rf], struct
     for const in ("CEC_ABI_VERSION", "CEC_READ_REBUILT_ONLY", "CEC_PIPE_EXTERNAL",
                   "CEC_PRESENT_VERIFIED", "CEC_READ_RESILVER", "CEC_READ_VERIFY_ONLY",
-                  "CEC_READ_CARRY"):
+                  "CEC_READ_CARRY", "CEC_SUBMIT_PACKED", "CEC_MULTI_WRITE", "CEC_MULTI_READ"):
         cv = re.search(rf"#define {const}\s+(0x[0-9a-fA-F]+|\d+)u?", hsrc).group(1)
         rv = re.search(rf"pub const {const}:[^=]+=\s*(0x[0-9a-fA-F]+|\d+);", rsrc).group(1)
         assert int(cv, 0) == int(rv, 0), const
@@ -181,7 +183,7 @@ def test_batch_reader_mirrors_the_cpp_and_python_loops():
     assert order == sorted(order) and "slot ^= 1" in body
     retry = batch[batch.index("    fn retry<"):batch.index("    fn drain(&self, w: Option<LiveRead>)")]
     for s in ("CEC_PRESENT_VERIFIED", "have + added < d", "TooFewShardsPresent",
-              "self.multi.read("):
+              "self.multi.submit_read_carry(", "carry_release("):
         assert s in retry, s
     py = open(os.path.join(ROOT, "chunky-bits_amd", "chunky_ec", "batchreader.py")).read()
     for s in ("def _load", "def _submit", "def _collect", "def _retry", "have + added < d",

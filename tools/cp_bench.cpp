@@ -3,7 +3,10 @@
 // losing one data + one parity chunk per part — per-part calls (the reference's shape) vs the
 // batched paths (FileWriteBuilder::batch / read(src, parts_per_batch) through the multi-GPU
 // scheduler, sharded over `devices`: default the current GPU; e.g. 0,0 = two shards on GPU 0).
-//   make -C chunky-bits_amd/csrc cp_bench ; tools/cp_bench [GiB] [devices]
+// Batched only, last: the read with `damage` (default 1 %) of the stored chunk copies flipped,
+// so parts retry (file_part.rs:92-107), with the retries' verified chunks kept on the GPU
+// (carry) and sent again (no carry): time and chunks sent to the GPUs.
+//   make -C chunky-bits_amd/csrc cp_bench ; tools/cp_bench [GiB] [devices] [damage]
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -16,6 +19,7 @@ using namespace chunky_ec;
 
 int main(int argc, char** argv) {
     const double gib = argc > 1 ? std::atof(argv[1]) : 4.0;
+    const double damage = argc > 3 ? std::atof(argv[3]) : 0.01;
     std::vector<int> devices;
     if (argc > 2) {
         std::stringstream ss(argv[2]);
@@ -107,6 +111,43 @@ int main(int argc, char** argv) {
                     double(n) / vs / 1e9, ok ? "yes" : "NO");
         std::fflush(stdout);
         if (!ok) return 1;
+        if (!batched) continue;
+        // the damaged read: a seeded `damage` fraction of the data chunks' copies flipped (a
+        // reader loads the data chunks first, so each flip makes its part retry)
+        uint64_t x = 99;
+        size_t flipped = 0;
+        for (const auto& part : f.parts)
+            for (size_t j = 0; j < d; ++j) {
+                x = x * 6364136223846793005ull + 1442695040888963407ull;
+                if (double(x >> 11) / double(1ull << 53) < damage)
+                    flipped += store.corrupt(part.data[j].locations[0], (x >> 7) % chunk) ? 1 : 0;
+            }
+        cec_multi* m = detail::cached_multi_entry().multi.get();
+        auto uploaded = [&] {
+            uint64_t u = 0;
+            for (size_t g = 0; g < cec_multi_shards(m); ++g) {
+                cec_multi_stats st{};
+                if (cec_multi_shard_stats(m, g, &st) == CEC_OK) u += st.chunks_uploaded;
+            }
+            return u;
+        };
+        for (int carry = 1; carry >= 0; --carry) {
+            detail::read_carry() = carry != 0;
+            (void)f.read(store, 128, 4, devices);  // warm
+            const uint64_t u0 = uploaded();
+            t0 = std::chrono::steady_clock::now();
+            const Bytes dmg = f.read(store, 128, 4, devices);
+            const double rd = secs(t0);
+            const uint64_t up = uploaded() - u0;
+            ok = dmg.size() == n && std::memcmp(dmg.data(), input.data(), n) == 0;
+            std::printf("batched   read with %.2f %% of data copies damaged (%zu flipped) + the "
+                        "lost chunks, %s: %6.2f GB/s, %llu chunks sent to the GPU, bit-exact %s\n",
+                        damage * 100, flipped, carry ? "carry   " : "no carry", double(n) / rd / 1e9,
+                        static_cast<unsigned long long>(up), ok ? "yes" : "NO");
+            std::fflush(stdout);
+            if (!ok) return 1;
+        }
+        detail::read_carry() = true;
     }
     return 0;
 }
