@@ -9,6 +9,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "chunky-bits_amd"))
+# CEC_APPLY_TUNE is read only by the A/B build (make -C chunky-bits_amd/csrc ab)
+os.environ.setdefault("CEC_LIBRARY", os.path.join(ROOT, "tools", "ab", "libchunky_ec.so"))
 import torch  # noqa: E402
 import chunky_ec as ce  # noqa: E402
 

@@ -2,6 +2,8 @@
 # reservation in KiB (L), compacted verify on/off (C); parity tests of the read path first.
 #   CFGS="S L C;..." bash tools/c3r_ab.sh
 set -o pipefail
+# these knobs are read only by the A/B build (make -C chunky-bits_amd/csrc ab)
+export CEC_LIBRARY=${CEC_LIBRARY:-tools/ab/libchunky_ec.so}
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 150 --timeout-method thread -k "read_batch or resilver or reconstruct or verify" > gpurun_out/pt_read.log 2>&1 || { tail -30 gpurun_out/pt_read.log; exit 1; }
 IFS=';' read -ra RUNS <<< "${CFGS:-1 0 1;1 65 1;0 0 1}"
