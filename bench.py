@@ -1182,6 +1182,16 @@ def launch_ranks(n: int, argv) -> int:
     return subprocess.run(cmd, env=dict(os.environ)).returncode
 
 
+def rccl_overcommit(world: int, backend: str, devices: int):
+    """The error text when RCCL ranks would share a GPU (two ranks of one communicator cannot:
+    the run would fail or hang in init), else None.  Only the gloo rehearsal
+    (CEC_BENCH_BACKEND=gloo) puts several ranks on one device."""
+    if backend != "nccl" or world <= 1 or world <= devices:
+        return None
+    return (f"bench: {world} RCCL ranks but {devices} visible GPU(s): one rank per GPU; "
+            "CEC_BENCH_BACKEND=gloo rehearses several ranks on one GPU")
+
+
 def world_mismatch(world: int, gpus: int):
     """The error text when this rank's world size is not what --gpus asked for, else None (a line
     measured on another number of ranks than it claims must not be printed)."""
@@ -1292,7 +1302,9 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world, rank, local = dist_env()
-    err = world_mismatch(world, args.gpus)
+    backend = os.environ.get("CEC_BENCH_BACKEND", "nccl")
+    err = world_mismatch(world, args.gpus) or rccl_overcommit(world, backend,
+                                                              torch.cuda.device_count())
     if err:
         print(err, file=sys.stderr, flush=True)
         sys.exit(2)
@@ -1324,7 +1336,6 @@ def main():
     # CEC_BENCH_BACKEND=gloo rehearses N > 1 with several ranks on one GPU; CEC_BENCH_PG=1 starts
     # the process group at world 1 too, so one GPU runs the N > 1 line's RCCL branch (init with
     # device_id, barriers, the float64 all-reduces, the per-rank rows).
-    backend = os.environ.get("CEC_BENCH_BACKEND", "nccl")
     if world > 1 or os.environ.get("CEC_BENCH_PG") == "1":
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=device)

@@ -347,3 +347,12 @@ def test_rank_rows_carry_each_ranks_oracle_check():
     assert bench.rank_row(0, base + [1.0])["check_vs_oracle"] is True
     assert bench.rank_row(1, base + [0.0])["check_vs_oracle"] is False
     assert bench.rank_row(2, base + [-1.0])["check_vs_oracle"] is None
+
+
+def test_rccl_ranks_never_share_a_gpu():
+    """More RCCL ranks than visible GPUs would fail or hang in the communicator's init: the bench
+    exits 2 first.  The gloo rehearsal may put several ranks on one GPU."""
+    assert bench.rccl_overcommit(8, "nccl", 8) is None
+    assert bench.rccl_overcommit(1, "nccl", 0) is None
+    assert "2 RCCL ranks but 1 visible GPU" in bench.rccl_overcommit(2, "nccl", 1)
+    assert bench.rccl_overcommit(4, "gloo", 1) is None
