@@ -102,6 +102,9 @@ class BatchReader:
         self.carry = [np.full(W, -1, np.int32) for _ in range(2)]
         self.retries = 0  # part resubmissions (a part retried twice counts twice)
         self.carried_parts = 0  # retried parts whose verified chunks stayed on the GPU
+        self.dev0 = dev0
+        self._scr_parts = 0  # retry buffers: page-locked chunks / data, kept copies (grown only)
+        self._scr = None
 
     def read(self, n_parts: int, fetch: Fetch, digests: Callable[[int], np.ndarray],
              sink: Callable[[int, List[memoryview]], None]):
@@ -189,11 +192,15 @@ class BatchReader:
         good = {q: ver[q] != 0 for q in failed}
         cursor = {q: self.cursor[w.slot][q].copy() for q in failed}
         exhausted = {q: self.exhausted[w.slot][q].copy() for q in failed}
-        keep = {q: ch[q].copy() for q in failed}  # bytes of every chunk loaded so far
         f = len(failed)
-        # pageable (the scheduler stages them): pinning a retry buffer per window would cost more
-        # than the few parts it carries (~0.35 s per GiB)
-        rc, ro = np.zeros((f, t, L), np.uint8), np.zeros((f, d, L), np.uint8)
+        # the reader's retry buffers, kept between retries (fresh zeroed ones cost ~200 ms of
+        # page faults per retry of a dozen RS(10,4) 1 MiB parts); rc / ro page-locked, so a
+        # single-shard retry goes up without staging
+        rc, ro, kbuf = self._retry_buffers(f)
+        keep = {}  # bytes of every chunk loaded so far
+        for r, q in enumerate(failed):
+            kbuf[r] = ch[q]
+            keep[q] = kbuf[r]
         r_pres, r_exp = np.zeros((f, t), np.uint8), np.zeros((f, t, 32), np.uint8)
         r_ver, r_st = np.zeros((f, t), np.uint8), np.zeros(f, np.int32)
         r_cin, r_cout = np.full(f, -1, np.int32), np.full(f, -1, np.int32)
@@ -207,6 +214,18 @@ class BatchReader:
                 if cid[q] >= 0:
                     self.multi.carry_release(cid[q])
             raise
+
+    def _retry_buffers(self, f):
+        d, t, L = self.d, self.t, self.L
+        if self._scr_parts < f:
+            self._scr = None  # the old buffers go before the new ones are pinned
+            n = max(f, 2 * self._scr_parts)
+            self._scr = (HostBuffer(n * t * L, self.dev0), HostBuffer(n * d * L, self.dev0),
+                         np.empty((n, t, L), np.uint8))
+            self._scr_parts = n
+        rc_b, ro_b, kbuf = self._scr
+        return (rc_b.array[:f * t * L].reshape(f, t, L), ro_b.array[:f * d * L].reshape(f, d, L),
+                kbuf[:f])
 
     def _retry_rounds(self, w, open_, fetch, tried, good, cursor, exhausted, keep, cid, rc, ro,
                       r_pres, r_exp, r_ver, r_st, r_cin, r_cout, out):

@@ -365,6 +365,29 @@ pub struct BatchReader {
     carry: [Vec<i32>; 2],
     retries: u64,
     carried: u64,
+    dev0: c_int,
+    // retry buffers, kept between retries (grown only): fresh zeroed ones cost ~200 ms of page
+    // faults per retry of a dozen RS(10,4) 1 MiB parts, and page-locked ones go up unstaged
+    retry_bufs: RetryBuffers,
+}
+
+#[derive(Default)]
+struct RetryBuffers {
+    chunks: Option<HostBuffer>,
+    out: Option<HostBuffer>,
+    keep: Vec<u8>,
+}
+
+/// `buf` grown to at least `n` bytes (page-locked on `dev`'s node), its first `n` bytes.
+fn grown(buf: &mut Option<HostBuffer>, n: usize, dev: c_int) -> Result<&mut [u8], CecError> {
+    if buf.as_ref().map_or(true, |b| b.len() < n) {
+        *buf = None;  // the old buffer goes before the new one is pinned
+        *buf = Some(HostBuffer::zeroed(n, dev)?);
+    }
+    match buf.as_mut() {
+        Some(b) => Ok(&mut b[..n]),
+        None => Err(crate::too_small("retry buffer")),
+    }
 }
 
 impl BatchReader {
@@ -402,6 +425,8 @@ impl BatchReader {
             window,
             retries: 0,
             carried: 0,
+            dev0,
+            retry_bufs: RetryBuffers::default(),
         })
     }
 
@@ -552,7 +577,9 @@ impl BatchReader {
         F: FnMut(usize, usize, usize) -> Option<(usize, Vec<u8>)>,
     {
         let mut cid: Vec<i32> = failed.iter().map(|&q| self.carry[w.slot][q]).collect();
-        let res = self.retry_rounds(w, failed, fetch, &mut cid);
+        let mut bufs = std::mem::take(&mut self.retry_bufs);
+        let res = self.retry_rounds(w, failed, fetch, &mut cid, &mut bufs);
+        self.retry_bufs = bufs;
         if res.is_err() {
             for &id in cid.iter().filter(|&&id| id >= 0) {
                 let _ = self.multi.carry_release(id);
@@ -562,7 +589,7 @@ impl BatchReader {
     }
 
     fn retry_rounds<F>(&mut self, w: &LiveRead, failed: &[usize], fetch: &mut F,
-                       cid: &mut [i32]) -> Result<(), CecError>
+                       cid: &mut [i32], bufs: &mut RetryBuffers) -> Result<(), CecError>
     where
         F: FnMut(usize, usize, usize) -> Option<(usize, Vec<u8>)>,
     {
@@ -572,7 +599,10 @@ impl BatchReader {
         let mut good = vec![false; f * t];
         let mut exhausted = vec![false; f * t];
         let mut cursor = vec![0usize; f * t];
-        let mut keep = vec![0u8; f * t * l];  // bytes of every chunk loaded so far
+        if bufs.keep.len() < f * t * l {
+            bufs.keep.resize(f * t * l, 0);
+        }
+        let keep = &mut bufs.keep[..f * t * l];  // bytes of every chunk loaded so far
         {
             let ch: &[u8] = &self.chunks[w.slot];
             for (r, &q) in failed.iter().enumerate() {
@@ -585,10 +615,8 @@ impl BatchReader {
                 keep[r * t * l..(r + 1) * t * l].copy_from_slice(&ch[q * t * l..(q + 1) * t * l]);
             }
         }
-        // pageable (the scheduler stages them): pinning a retry buffer per window would cost more
-        // than the few parts it carries (~0.35 s per GiB)
-        let mut r_chunks = vec![0u8; f * t * l];
-        let mut r_out = vec![0u8; f * d * l];
+        let r_chunks = grown(&mut bufs.chunks, f * t * l, self.dev0)?;
+        let r_out = grown(&mut bufs.out, f * d * l, self.dev0)?;
         let mut r_pres = vec![0u8; f * t];
         let mut r_exp = vec![0u8; f * t * 32];
         let mut r_ver = vec![0u8; f * t];

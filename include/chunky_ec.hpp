@@ -1093,6 +1093,14 @@ struct FileReference {
         thread_local std::array<ReadWindow, kMaxReadWindows> win;
         return win;
     }
+    // Page-locked chunk / data buffers of this thread's read retries (grown, never shrunk).
+    struct RetryBuffers {
+        detail::PinnedBuf chunks, data;
+    };
+    static RetryBuffers& retry_buffers() {
+        thread_local RetryBuffers b;
+        return b;
+    }
 
     // Parts [k0, k0 + n) (one shape) through cec_multi in windows of one pipeline batch per
     // shard (ppb x shards parts), up to `depth` windows in flight, so loading the next windows
@@ -1223,7 +1231,12 @@ struct FileReference {
             for (size_t i = 0; i < t; ++i)
                 if (good[r * t + i]) held[r * t + i] = src.find(part.chunk(i).locations[cursor[r * t + i] - 1]);
         }
-        Bytes chunks(f * t * L), data(f * d * L);
+        // the thread's retry buffers, kept page-locked between retries: fresh zeroed vectors cost
+        // ~200 ms of page faults per retry of a dozen RS(10,4) 1 MiB parts
+        // (profiles/r6final/cp_bench_*.log), and page-locked ones go up without staging
+        RetryBuffers& rb = retry_buffers();
+        uint8_t* chunks = rb.chunks.reserve(f * t * L, -1);
+        uint8_t* data = rb.data.reserve(f * d * L, -1);
         std::vector<uint8_t> present(f * t), expected(f * t * 32), verified(f * t);
         std::vector<int> status(f);
         std::vector<int32_t> carry_in(f, -1), carry_out(f, -1);
@@ -1265,8 +1278,8 @@ struct FileReference {
                 if (added == 0) throw ErasureError(Error::TooFewShardsPresent);
             }
             uint64_t job = 0;
-            detail::check_multi(cec_multi_read_carry(m, chunks.data(), present.data(),
-                                                     expected.data(), g, data.data(),
+            detail::check_multi(cec_multi_read_carry(m, chunks, present.data(),
+                                                     expected.data(), g, data,
                                                      verified.data(), status.data(), nullptr, 0,
                                                      carry_in.data(),
                                                      carry ? carry_out.data() : nullptr, &job));
@@ -1473,6 +1486,8 @@ inline void release_thread_buffers() {
         w.chunks.release();
         w.out.release();
     }
+    FileReference::retry_buffers().chunks.release();
+    FileReference::retry_buffers().data.release();
     for (auto& w : FileReference::check_windows()) {
         w.chunks.release();
         w.rebuilt.release();
