@@ -159,6 +159,8 @@ _sig("cec_read_pipeline_depth", [_vp], ctypes.c_size_t)
 _sig("cec_read_pipeline_acquire", [_vp, _szp, ctypes.POINTER(_u8p), ctypes.POINTER(_u8p),
                                    ctypes.POINTER(_u8p)])
 _sig("cec_read_pipeline_submit", [_vp, ctypes.c_size_t, ctypes.c_size_t])
+_sig("cec_read_pipeline_acquire_idle", [_vp, _szp, ctypes.POINTER(_u8p), ctypes.POINTER(_u8p),
+                                        ctypes.POINTER(_u8p)])
 _sig("cec_read_pipeline_wait", [_vp, ctypes.c_size_t, ctypes.POINTER(_u8p), ctypes.POINTER(_u8p),
                                 ctypes.POINTER(ctypes.POINTER(ctypes.c_int)), _szp])
 _sig("cec_read_pipeline_drain", [_vp])

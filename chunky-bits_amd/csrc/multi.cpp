@@ -438,7 +438,9 @@ struct cec_multi {
             const size_t n = std::min(P, count - at);
             size_t slot = 0;
             uint8_t *c = nullptr, *pr = nullptr, *ex = nullptr;
-            int st = cec_read_pipeline_acquire(s.rp, &slot, &c, &pr, &ex);
+            // a slot whose batch is done if there is one: a retry job (a few parts, submitted
+            // while the reader's other windows run) need not wait for the oldest of them
+            int st = cec_read_pipeline_acquire_idle(s.rp, &slot, &c, &pr, &ex);
             if (st != CEC_OK) {
                 finish_parts(job, count - at, st, cec_pipeline_last_error());
                 return;
@@ -571,7 +573,12 @@ struct cec_multi {
                     if (!s.queue.empty() || !in_flight(s)) break;
                     work_cv.wait_for(lk, std::chrono::microseconds(100));
                 }
-                work_cv.wait(lk, [&] { return stop || !s.queue.empty(); });
+                work_cv.wait(lk, [&] { return stop || !s.queue.empty() || !s.releases.empty(); });
+                if (s.queue.empty() && !stop) {  // carry ids given back while idle
+                    lk.unlock();
+                    apply_releases(s);
+                    continue;
+                }
                 if (s.queue.empty()) break;  // stop requested and nothing left
                 job = s.queue.front();
                 s.queue.pop_front();

@@ -1031,11 +1031,11 @@ void cec_read_pipeline_free(cec_read_pipeline* pl) { delete pl; }
 
 size_t cec_read_pipeline_depth(const cec_read_pipeline* pl) { return pl ? pl->slots.size() : 0; }
 
-int cec_read_pipeline_acquire(cec_read_pipeline* pl, size_t* slot, uint8_t** chunks,
-                              uint8_t** present, uint8_t** expected) {
-    if (!pl || !slot || !chunks || !present || !expected) return CEC_ERR_INVALID_ARGUMENT;
-    const size_t i = pl->next;
-    pl->next = (pl->next + 1) % pl->slots.size();
+namespace {
+
+int read_acquire(cec_read_pipeline* pl, size_t i, size_t* slot, uint8_t** chunks,
+                 uint8_t** present, uint8_t** expected) {
+    pl->next = (i + 1) % pl->slots.size();
     ReadSlot& s = pl->slots[i];
     if (s.in_flight) {
         PIPE_TRY(hipEventSynchronize(s.done));
@@ -1046,6 +1046,28 @@ int cec_read_pipeline_acquire(cec_read_pipeline* pl, size_t* slot, uint8_t** chu
     *present = s.h_present;
     *expected = s.h_expected;
     return CEC_OK;
+}
+
+}  // namespace
+
+int cec_read_pipeline_acquire(cec_read_pipeline* pl, size_t* slot, uint8_t** chunks,
+                              uint8_t** present, uint8_t** expected) {
+    if (!pl || !slot || !chunks || !present || !expected) return CEC_ERR_INVALID_ARGUMENT;
+    return read_acquire(pl, pl->next, slot, chunks, present, expected);
+}
+
+int cec_read_pipeline_acquire_idle(cec_read_pipeline* pl, size_t* slot, uint8_t** chunks,
+                                   uint8_t** present, uint8_t** expected) {
+    if (!pl || !slot || !chunks || !present || !expected) return CEC_ERR_INVALID_ARGUMENT;
+    // the first slot from the round-robin position on whose batch is done (or that has none);
+    // all busy: the round-robin slot, waited for
+    const size_t n = pl->slots.size();
+    for (size_t k = 0; k < n; ++k) {
+        const size_t i = (pl->next + k) % n;
+        if (cec_read_pipeline_query(pl, i) == 1)
+            return read_acquire(pl, i, slot, chunks, present, expected);
+    }
+    return read_acquire(pl, pl->next, slot, chunks, present, expected);
 }
 
 int cec_read_pipeline_submit_ex(cec_read_pipeline* pl, size_t slot, const cec_read_submit* a) {

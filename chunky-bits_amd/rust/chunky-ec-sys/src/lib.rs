@@ -236,6 +236,13 @@ pub mod sys {
             slot: usize,
             n_parts: usize,
         ) -> c_int;
+        pub fn cec_read_pipeline_acquire_idle(
+            pipeline: *mut cec_read_pipeline,
+            slot: *mut usize,
+            chunks: *mut *mut u8,
+            present: *mut *mut u8,
+            expected: *mut *mut u8,
+        ) -> c_int;
         pub fn cec_read_pipeline_wait(
             pipeline: *mut cec_read_pipeline,
             slot: usize,

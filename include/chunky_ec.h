@@ -323,6 +323,12 @@ size_t cec_read_pipeline_depth(const cec_read_pipeline* pipeline);
 int cec_read_pipeline_acquire(cec_read_pipeline* pipeline, size_t* slot, uint8_t** chunks,
                               uint8_t** present, uint8_t** expected);
 int cec_read_pipeline_submit(cec_read_pipeline* pipeline, size_t slot, size_t n_parts);
+/* As cec_read_pipeline_acquire, but takes the first slot (from the round-robin position on)
+ * whose batch has completed or that has none, and waits only when every slot is busy: a small
+ * retry batch submitted while the other slots run starts at once.  The slot's previous results
+ * are no longer valid. */
+int cec_read_pipeline_acquire_idle(cec_read_pipeline* pipeline, size_t* slot, uint8_t** chunks,
+                                   uint8_t** present, uint8_t** expected);
 int cec_read_pipeline_wait(cec_read_pipeline* pipeline, size_t slot, const uint8_t** data,
                            const uint8_t** verified, const int** part_status, size_t* n_parts);
 int cec_read_pipeline_drain(cec_read_pipeline* pipeline);

@@ -348,3 +348,32 @@ def test_one_pipeline_serves_every_mode_per_submit(packed):
         rp.submit_ex(slot, P, chunks=chunks, present=np.ones((P, t), np.uint8), expected=dig,
                      mode=ce.READ_RESILVER)
     assert _made() - made == 1
+
+
+def test_scheduler_releases_carry_ids_while_idle():
+    """cec_multi_carry_release hands the ids to their shard's worker, which gives them back even
+    when no read job follows (the worker wakes for them): the held count drops to 0."""
+    import time
+    d, p, L, n = 4, 2, 4096, 6
+    t = d + p
+    chunks, dig = make_parts(n, d, p, L, 97)
+    m = ce.Multi(ce.ReedSolomon(d, p), L, 8, 2, [0, 0], kinds=ce.Multi.READ)
+    ch = chunks.copy()
+    ch[:, 0, 0] ^= 1  # every part: chunk 0 bad -> TooFewShardsPresent, 3 chunks kept
+    pres = np.zeros((n, t), np.uint8)
+    pres[:, :d] = 1
+    out, ver = np.zeros((n, d, L), np.uint8), np.zeros((n, t), np.uint8)
+    st, cout = np.zeros(n, np.int32), np.full(n, -1, np.int32)
+    job, _ = m.read(ch, pres, dig, n, out, ver, st, carry_out=cout)
+    m.wait(job)
+    assert (st == ce.TOO_FEW_SHARDS_PRESENT).all() and (cout >= 0).all()
+    assert {int(c) >> 20 for c in cout} == {0, 1}  # both shards kept some
+    assert sum(m.stats(g)["carry_held"] for g in range(2)) == n
+    for c in cout:
+        m.carry_release(int(c))
+    deadline = time.time() + 5
+    while sum(m.stats(g)["carry_held"] for g in range(2)) and time.time() < deadline:
+        time.sleep(0.01)
+    assert sum(m.stats(g)["carry_held"] for g in range(2)) == 0
+    with pytest.raises(ce.Error):
+        m.carry_release(7 << 20)  # no shard 7
