@@ -2,7 +2,7 @@
 rule, parts handed out in file order: the Python twin of the Rust crate's
 ``chunky_ec_sys::batch::BatchReader`` / ``read_part`` / ``FileReader``
 (chunky-bits_amd/rust/chunky-ec-sys/src/batch.rs) and of the C++ ``FileReference::read_run`` /
-``retry`` (include/chunky_ec.hpp), step for step, so the loop the Rust side would run is executed
+``retry_start`` / ``retry_finish`` (include/chunky_ec.hpp), step for step, so the loop the Rust side would run is executed
 and tested on the GPU (tests/test_gpu_batchreader.py).
 
 The reference reads a part by drawing chunks until d of them verify (src/file/file_part.rs:
@@ -24,8 +24,11 @@ intact part needs no rebuild) -- into a page-locked buffer and submits the windo
 job (verify every loaded chunk, rebuild the data chunks; parts split over the GPUs in contiguous
 ranges) while it loads the next window.  A part whose loaded chunks do not all verify is
 resubmitted with the chunks that verified flagged ``CEC_PRESENT_VERIFIED`` (used, not hashed
-again), the failed chunks' next copies, then untried chunks, up to d, until it decodes; a part
-that runs out of copies fails the read with TooFewShardsPresent, as the reference's does.
+again; kept on the GPU under the part's carry id), the failed chunks' next copies, then untried
+chunks, up to d, until it decodes; a part that runs out of copies fails the read with
+TooFewShardsPresent, as the reference's does.  Three window buffers: a window is checked (its job
+waited for, its failed parts' first retry round queued) one step before it is emitted, so the
+retry runs on the GPUs while the next window loads.
 :func:`read_part` is the same rule for one part through the per-call API, and :class:`FileReader`
 splits a file into runs of one shape (chunk size, d, p: the short last part has its own chunk size,
 file_part.rs:152) and keeps one BatchReader per shape.
@@ -69,14 +72,33 @@ def draw_order(good, tried, exhausted):
 
 
 @dataclass
+class _Retry:
+    """The retry of a window's failed parts (file_part.rs:92-107), one round in flight at a time."""
+    failed: List[int]                     # window rows of the failed parts
+    tried: dict
+    good: dict
+    cursor: dict
+    exhausted: dict
+    keep: dict                            # bytes of every chunk loaded so far
+    cid: dict                             # carry id of the part's verified chunks (-1: none)
+    open_: List[int]
+    job: int = 0
+    in_flight: bool = False
+
+
+@dataclass
 class _Window:
     slot: int
     job: int
     first: int
     n: int
+    checked: bool = False                 # its read job waited for (and its retry started)
+    retry: Optional[_Retry] = None
 
 
 class BatchReader:
+    R = 3  # window buffers: two windows' read jobs in flight, one being emitted
+
     def __init__(self, data: int, parity: int, chunk_size: int, parts_per_batch: int, depth: int,
                  devices: List[int], carry: bool = True):
         """carry=False: retries send their verified chunks again instead of leaving them on the
@@ -88,53 +110,57 @@ class BatchReader:
         self.d, self.p, self.t, self.L = data, parity, data + parity, chunk_size
         self.window = parts_per_batch * max(len(devices), 1)
         dev0 = devices[0] if devices else -1
-        W, t, L = self.window, self.t, chunk_size
-        self.chunks = [HostBuffer(W * t * L, dev0) for _ in range(2)]
-        self.out = [HostBuffer(W * data * L, dev0) for _ in range(2)]
-        self.present = [np.zeros((W, t), np.uint8) for _ in range(2)]
-        self.expected = [np.zeros((W, t, 32), np.uint8) for _ in range(2)]
-        self.verified = [np.zeros((W, t), np.uint8) for _ in range(2)]
-        self.status = [np.zeros(W, np.int32) for _ in range(2)]
+        W, t, L, R = self.window, self.t, chunk_size, self.R
+        self.chunks = [HostBuffer(W * t * L, dev0) for _ in range(R)]
+        self.out = [HostBuffer(W * data * L, dev0) for _ in range(R)]
+        self.present = [np.zeros((W, t), np.uint8) for _ in range(R)]
+        self.expected = [np.zeros((W, t, 32), np.uint8) for _ in range(R)]
+        self.verified = [np.zeros((W, t), np.uint8) for _ in range(R)]
+        self.status = [np.zeros(W, np.int32) for _ in range(R)]
         # per chunk of the window: the next location to read, and whether none is left
-        self.cursor = [np.zeros((W, t), np.int64) for _ in range(2)]
-        self.exhausted = [np.zeros((W, t), bool) for _ in range(2)]
+        self.cursor = [np.zeros((W, t), np.int64) for _ in range(R)]
+        self.exhausted = [np.zeros((W, t), bool) for _ in range(R)]
         # per part of the window: the scheduler's carry id of its verified chunks (-1: none)
-        self.carry = [np.full(W, -1, np.int32) for _ in range(2)]
+        self.carry = [np.full(W, -1, np.int32) for _ in range(R)]
         self.retries = 0  # part resubmissions (a part retried twice counts twice)
         self.carried_parts = 0  # retried parts whose verified chunks stayed on the GPU
         self.dev0 = dev0
-        self._scr_parts = 0  # retry buffers: page-locked chunks / data, kept copies (grown only)
-        self._scr = None
+        # per window: retry buffers (page-locked chunks / data, kept copies; grown only)
+        self._scr_parts = [0] * R
+        self._scr = [None] * R
 
     def read(self, n_parts: int, fetch: Fetch, digests: Callable[[int], np.ndarray],
              sink: Callable[[int, List[memoryview]], None]):
         """Parts 0..n_parts-1 (all of this reader's shape): ``fetch(part, chunk, start)`` as the
         module describes, ``digests(part)`` the part's metadata digests [d+p][32]; ``sink(part,
-        data_chunks)`` gets the d data chunks of every part, in file order."""
-        at = slot = 0
-        pending: Optional[_Window] = None
-        while True:
-            cur = None
-            if at < n_parts:
-                cnt = min(self.window, n_parts - at)
-                try:
-                    self._load(slot, at, cnt, fetch, digests)
-                    cur = _Window(slot, self._submit(slot, cnt), at, cnt)
-                except BaseException:
-                    self._drain(pending)
-                    raise
-                at += cnt
-            if pending is not None:  # the older window first: file order
-                prev, pending = pending, None
-                try:
-                    self._collect(prev, fetch, sink)
-                except BaseException:
-                    self._drain(cur)
-                    raise
-            if cur is None:
-                return
-            pending = cur
-            slot ^= 1
+        data_chunks)`` gets the d data chunks of every part, in file order.  A window is checked
+        (its job waited for, the first round of its failed parts' retry queued) one step before it
+        is emitted, so that retry runs beside the loading of the next window."""
+        R = self.R
+        live: List[Optional[_Window]] = [None] * R
+        at = i = 0
+        try:
+            while True:
+                # windows are emitted in submission order: live[i % R] went out R steps ago; the
+                # one after it is checked first, so its retry overlaps this step's work
+                nxt = live[(i + 1) % R]
+                if nxt is not None and not nxt.checked:
+                    self._check(nxt, fetch)
+                s = i % R
+                if live[s] is not None:
+                    self._finish(live[s], fetch, sink)
+                    live[s] = None
+                if at < n_parts:
+                    cnt = min(self.window, n_parts - at)
+                    self._load(s, at, cnt, fetch, digests)
+                    live[s] = _Window(s, self._submit(s, cnt), at, cnt)
+                    at += cnt
+                elif all(x is None for x in live):
+                    return
+                i += 1
+        except BaseException:
+            self._drain(live)
+            raise
 
     def _load(self, slot, first, cnt, fetch, digests):
         """The first d chunks of each part that fetch returns a copy of (file_part.rs:86-107 loads
@@ -146,6 +172,7 @@ class BatchReader:
         pres[:cnt] = 0
         cur[:cnt] = 0
         ex[:cnt] = False
+        self.carry[slot][:cnt] = -1
         for q in range(cnt):
             exp[q] = digests(first + q)
             loaded = 0
@@ -167,120 +194,156 @@ class BatchReader:
                                  carry_out=self.carry[slot] if self.use_carry else None)
         return job
 
-    def _collect(self, w: _Window, fetch, sink):
+    def _check(self, w: _Window, fetch):
+        """Waits for the window's read job; its failed parts' first retry round goes out."""
+        w.checked = True
         self.multi.wait(w.job)
         st = self.status[w.slot]
         failed = [q for q in range(w.n) if st[q] != OK]
         if failed:
-            self._retry(w, failed, fetch)
+            self._retry_start(w, failed, fetch)
+
+    def _finish(self, w: _Window, fetch, sink):
+        if not w.checked:
+            self._check(w, fetch)
+        if w.retry is not None:
+            self._retry_finish(w, fetch)
         d, L = self.d, self.L
         out = memoryview(self.out[w.slot].array)
         for q in range(w.n):
             sink(w.first + q, [out[(q * d + j) * L:(q * d + j + 1) * L] for j in range(d)])
 
-    def _retry(self, w: _Window, failed, fetch):
+    def _retry_start(self, w: _Window, failed, fetch):
         """file_part.rs:92-107: the failed parts go again with the chunks that verified
         (PRESENT_VERIFIED) plus, up to d, the failed chunks' next copies and then untried chunks,
         until each decodes or runs out of copies.  The verified chunks stay on the GPU where the
         scheduler kept them (the part's carry id: only the new chunks are sent), or, when it kept
-        none, are sent again from the window's buffer (the bytes that verified)."""
-        d, t, L = self.d, self.t, self.L
+        none, are sent again from the window's buffer (the bytes that verified).  This queues the
+        first round; _retry_finish waits for it and runs any further rounds."""
+        t, L = self.t, self.L
         ch = self.chunks[w.slot].view(self.window, t, L)
         pres, ver = self.present[w.slot], self.verified[w.slot]
-        out = self.out[w.slot].view(self.window, d, L)
-        tried = {q: pres[q] != 0 for q in failed}
-        good = {q: ver[q] != 0 for q in failed}
-        cursor = {q: self.cursor[w.slot][q].copy() for q in failed}
-        exhausted = {q: self.exhausted[w.slot][q].copy() for q in failed}
-        f = len(failed)
-        # the reader's retry buffers, kept between retries (fresh zeroed ones cost ~200 ms of
-        # page faults per retry of a dozen RS(10,4) 1 MiB parts); rc / ro page-locked, so a
-        # single-shard retry goes up without staging
-        rc, ro, kbuf = self._retry_buffers(f)
-        keep = {}  # bytes of every chunk loaded so far
+        _, _, kbuf = self._retry_buffers(w.slot, len(failed))
+        keep = {}
         for r, q in enumerate(failed):
             kbuf[r] = ch[q]
             keep[q] = kbuf[r]
-        r_pres, r_exp = np.zeros((f, t), np.uint8), np.zeros((f, t, 32), np.uint8)
-        r_ver, r_st = np.zeros((f, t), np.uint8), np.zeros(f, np.int32)
-        r_cin, r_cout = np.full(f, -1, np.int32), np.full(f, -1, np.int32)
-        cid = {q: int(self.carry[w.slot][q]) if self.use_carry else -1 for q in failed}
-        open_ = list(failed)
-        try:
-            self._retry_rounds(w, open_, fetch, tried, good, cursor, exhausted, keep, cid, rc, ro,
-                               r_pres, r_exp, r_ver, r_st, r_cin, r_cout, out)
-        except BaseException:
-            for q in open_:  # ids the failed read will not use go back to their GPUs
-                if cid[q] >= 0:
-                    self.multi.carry_release(cid[q])
-            raise
+        cid = {}
+        for q in failed:  # the retry holds the ids now
+            cid[q] = int(self.carry[w.slot][q]) if self.use_carry else -1
+            self.carry[w.slot][q] = -1
+        w.retry = _Retry(failed, {q: pres[q] != 0 for q in failed}, {q: ver[q] != 0 for q in failed},
+                         {q: self.cursor[w.slot][q].copy() for q in failed},
+                         {q: self.exhausted[w.slot][q].copy() for q in failed}, keep, cid,
+                         list(failed))
+        self._retry_round(w, fetch)
 
-    def _retry_buffers(self, f):
+    def _retry_buffers(self, slot, f):
+        """The window's retry buffers, kept between retries (fresh zeroed ones cost ~200 ms of page
+        faults per retry of a dozen RS(10,4) 1 MiB parts); rc / ro page-locked, so a single-shard
+        retry goes up without staging.  Returns rc [f][t][L], ro [f][d][L], kept copies."""
         d, t, L = self.d, self.t, self.L
-        if self._scr_parts < f:
-            self._scr = None  # the old buffers go before the new ones are pinned
-            n = max(f, 2 * self._scr_parts)
-            self._scr = (HostBuffer(n * t * L, self.dev0), HostBuffer(n * d * L, self.dev0),
-                         np.empty((n, t, L), np.uint8))
-            self._scr_parts = n
-        rc_b, ro_b, kbuf = self._scr
+        if self._scr_parts[slot] < f:
+            self._scr[slot] = None  # the old buffers go before the new ones are pinned
+            n = max(f, 2 * self._scr_parts[slot])
+            self._scr[slot] = (HostBuffer(n * t * L, self.dev0), HostBuffer(n * d * L, self.dev0),
+                               np.empty((n, t, L), np.uint8))
+            self._scr_parts[slot] = n
+        rc_b, ro_b, kbuf = self._scr[slot]
         return (rc_b.array[:f * t * L].reshape(f, t, L), ro_b.array[:f * d * L].reshape(f, d, L),
                 kbuf[:f])
 
-    def _retry_rounds(self, w, open_, fetch, tried, good, cursor, exhausted, keep, cid, rc, ro,
-                      r_pres, r_exp, r_ver, r_st, r_cin, r_cout, out):
+    def _retry_round(self, w: _Window, fetch):
+        """Builds and queues one round over the still-open failed parts."""
         d, t, L = self.d, self.t, self.L
-        while open_:
-            g = len(open_)
-            r_pres[:g] = 0
-            for s, q in enumerate(open_):
-                r_exp[s] = self.expected[w.slot][q]
-                r_cin[s] = cid[q]
-                have = int(good[q].sum())
-                for i in range(t):
-                    if good[q][i]:
-                        if cid[q] < 0:  # not kept on the GPU: send the bytes that verified
-                            rc[s, i] = keep[q][i]
-                        r_pres[s, i] = PRESENT_VERIFIED
-                added = 0
-                for i in draw_order(good[q], tried[q], exhausted[q]):
-                    if not have + added < d:
-                        break
-                    tried[q][i] = True
-                    c = next_copy(fetch, w.first + q, i, int(cursor[q][i]), L)
-                    if c is None:
-                        exhausted[q][i] = True
-                        continue
-                    cursor[q][i], b = c
-                    keep[q][i] = np.frombuffer(b, np.uint8)
-                    rc[s, i] = keep[q][i]
-                    r_pres[s, i] = 1
-                    added += 1
-                if added == 0:
-                    raise Error(TOO_FEW_SHARDS_PRESENT)
-            job, _ = self.multi.read(rc, r_pres, r_exp, g, ro, r_ver, r_st, carry_in=r_cin,
-                                     carry_out=r_cout if self.use_carry else None)
-            for s, q in enumerate(open_):  # submitted: the ids are the job's now
-                self.carried_parts += 1 if cid[q] >= 0 else 0
-                cid[q] = -1
-            self.multi.wait(job)
-            self.retries += g
+        rt = w.retry
+        f = len(rt.failed)
+        rc, ro, _ = self._retry_buffers(w.slot, f)
+        g = len(rt.open_)
+        rt.r_pres = np.zeros((g, t), np.uint8)
+        rt.r_exp = np.zeros((g, t, 32), np.uint8)
+        rt.r_ver = np.zeros((g, t), np.uint8)
+        rt.r_st = np.zeros(g, np.int32)
+        rt.r_cin = np.full(g, -1, np.int32)
+        rt.r_cout = np.full(g, -1, np.int32)
+        for s, q in enumerate(rt.open_):
+            rt.r_exp[s] = self.expected[w.slot][q]
+            rt.r_cin[s] = rt.cid[q]
+            have = int(rt.good[q].sum())
+            for i in range(t):
+                if rt.good[q][i]:
+                    if rt.cid[q] < 0:  # not kept on the GPU: send the bytes that verified
+                        rc[s, i] = rt.keep[q][i]
+                    rt.r_pres[s, i] = PRESENT_VERIFIED
+            added = 0
+            for i in draw_order(rt.good[q], rt.tried[q], rt.exhausted[q]):
+                if not have + added < d:
+                    break
+                rt.tried[q][i] = True
+                c = next_copy(fetch, w.first + q, i, int(rt.cursor[q][i]), L)
+                if c is None:
+                    rt.exhausted[q][i] = True
+                    continue
+                rt.cursor[q][i], b = c
+                rt.keep[q][i] = np.frombuffer(b, np.uint8)
+                rc[s, i] = rt.keep[q][i]
+                rt.r_pres[s, i] = 1
+                added += 1
+            if added == 0:
+                raise Error(TOO_FEW_SHARDS_PRESENT)
+        rt.job, _ = self.multi.read(rc[:g], rt.r_pres, rt.r_exp, g, ro[:g], rt.r_ver, rt.r_st,
+                                    carry_in=rt.r_cin,
+                                    carry_out=rt.r_cout if self.use_carry else None)
+        for q in rt.open_:  # submitted: the ids are the job's now
+            self.carried_parts += 1 if rt.cid[q] >= 0 else 0
+            rt.cid[q] = -1
+        rt.in_flight = True
+
+    def _retry_finish(self, w: _Window, fetch):
+        """Waits for the round in flight; the parts that decoded go to the window's output, the
+        others go again (one round at a time) until every part decodes or runs out of copies."""
+        d = self.d
+        rt = w.retry
+        out = self.out[w.slot].view(self.window, d, self.L)
+        _, ro, _ = self._retry_buffers(w.slot, len(rt.failed))
+        while rt.in_flight:
+            rt.in_flight = False
+            self.multi.wait(rt.job)
+            self.retries += len(rt.open_)
             still = []
-            for s, q in enumerate(open_):
-                good[q] = r_ver[s] != 0
-                if r_st[s] == OK:
+            for s, q in enumerate(rt.open_):
+                rt.good[q] = rt.r_ver[s] != 0
+                if rt.r_st[s] == OK:
                     out[q] = ro[s]
                 else:
-                    cid[q] = int(r_cout[s])
+                    rt.cid[q] = int(rt.r_cout[s])
                     still.append(q)
-            open_[:] = still
+            rt.open_ = still
+            if still:
+                self._retry_round(w, fetch)
+        w.retry = None
 
-    def _drain(self, w: Optional[_Window]) -> None:
-        if w is not None:
+    def _drain(self, live) -> None:
+        """Error path: no job may still write into the windows; carry ids nobody will use go back
+        to their GPUs."""
+        for w in live:
+            if w is None:
+                continue
             try:
-                self.multi.wait(w.job)
+                if not w.checked:
+                    self.multi.wait(w.job)
+                if w.retry is not None and w.retry.in_flight:
+                    self.multi.wait(w.retry.job)
             except Exception:  # noqa: BLE001 (the error being raised is the caller's)
                 pass
+            ids = [int(c) for c in self.carry[w.slot][:w.n] if c >= 0]
+            if w.retry is not None:
+                ids += [c for c in w.retry.cid.values() if c >= 0]
+            for c in ids:
+                try:
+                    self.multi.carry_release(c)
+                except Exception:  # noqa: BLE001
+                    pass
 
 
 def read_part(codec: ReedSolomon, chunksize: int, digests: np.ndarray, fetch: Fetch,

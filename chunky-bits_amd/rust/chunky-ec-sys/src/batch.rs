@@ -289,12 +289,38 @@ pub enum BatchReadError<E> {
     Sink(E),
 }
 
+/// Window buffers of a [`BatchReader`]: two windows' read jobs in flight, one being emitted.
+const WINDOWS: usize = 3;
+
 /// A read window submitted to the scheduler and not yet handed to the sink.
 struct LiveRead {
     slot: usize,
     job: u64,
     first: usize,
     n: usize,
+    checked: bool,         // its read job waited for (and its retry started)
+    retry: Option<Retry>,  // its failed parts, while they are being read again
+}
+
+/// The retry of a window's failed parts (file_part.rs:92-107), one round in flight at a time.
+struct Retry {
+    failed: Vec<usize>,  // window rows of the failed parts
+    open: Vec<usize>,    // indices into `failed` of the parts not yet decoded
+    tried: Vec<bool>,    // [f][t]
+    good: Vec<bool>,
+    exhausted: Vec<bool>,
+    cursor: Vec<usize>,
+    cid: Vec<i32>,  // [f] carry id of the part's verified chunks (-1: none)
+    // the round in flight
+    g: usize,
+    job: u64,
+    in_flight: bool,
+    r_pres: Vec<u8>,
+    r_exp: Vec<u8>,
+    r_ver: Vec<u8>,
+    r_status: Vec<c_int>,
+    r_cin: Vec<i32>,
+    r_cout: Vec<i32>,
 }
 
 /// The chunk's next copy from location `start` on (`fetch` reads `chunk.locations[start..]` and
@@ -336,14 +362,17 @@ fn draw_order(good: &[bool], tried: &[bool], exhausted: &[bool]) -> Vec<usize> {
 /// page-locked buffer and submits the window as one scheduler job: every loaded chunk verified
 /// against its metadata digest, the data chunks rebuilt.  It loads the next window while that one
 /// runs.  A part whose loaded chunks do not all verify goes again with the chunks that verified
-/// (`CEC_PRESENT_VERIFIED`: used, not hashed again), the failed chunks' NEXT copies (the same
-/// chunk's next location is read before another chunk is drawn, file_part.rs:100-107), then
-/// untried chunks, up to d, until it decodes or runs out of copies.  So a chunk listed
-/// `[bad, good]` -- what resilver leaves when it appends a rebuilt copy's location
-/// (file_part.rs:346) -- reads as in the reference.  [`FileReader`] splits a file into runs of one
-/// shape (the short last part has its own chunk size).  `include/chunky_ec.hpp`'s
-/// `FileReference::read_run` / `retry` is the same loop in C++ and
-/// `chunky-bits_amd/chunky_ec/batchreader.py` its Python twin; both are tested on the GPU.
+/// (`CEC_PRESENT_VERIFIED`: used, not hashed again; kept on the GPU under the part's carry id), the
+/// failed chunks' NEXT copies (the same chunk's next location is read before another chunk is
+/// drawn, file_part.rs:100-107), then untried chunks, up to d, until it decodes or runs out of
+/// copies.  A window is checked (its job waited for, the first round of its failed parts' retry
+/// queued) one step before it is emitted, so that retry runs beside the loading of the next
+/// window.  So a chunk listed `[bad, good]` -- what resilver leaves when it appends a rebuilt
+/// copy's location (file_part.rs:346) -- reads as in the reference.  [`FileReader`] splits a file
+/// into runs of one shape (the short last part has its own chunk size).
+/// `include/chunky_ec.hpp`'s `FileReference::read_run` / `retry_start` / `retry_finish` is the
+/// same loop in C++ and `chunky-bits_amd/chunky_ec/batchreader.py` its Python twin; both are
+/// tested on the GPU.
 pub struct BatchReader {
     // declared (so dropped) first: the scheduler refers to the codec and the windows
     multi: Multi,
@@ -352,23 +381,24 @@ pub struct BatchReader {
     t: usize,
     chunk_size: usize,
     window: usize,
-    chunks: [HostBuffer; 2],
-    out: [HostBuffer; 2],
-    present: [Vec<u8>; 2],
-    expected: [Vec<u8>; 2],
-    verified: [Vec<u8>; 2],
-    status: [Vec<c_int>; 2],
+    chunks: Vec<HostBuffer>,
+    out: Vec<HostBuffer>,
+    present: Vec<Vec<u8>>,
+    expected: Vec<Vec<u8>>,
+    verified: Vec<Vec<u8>>,
+    status: Vec<Vec<c_int>>,
     // per chunk of a window: the next location to read, and whether none is left
-    cursor: [Vec<usize>; 2],
-    exhausted: [Vec<bool>; 2],
+    cursor: Vec<Vec<usize>>,
+    exhausted: Vec<Vec<bool>>,
     // per part of a window: the scheduler's carry id of its verified chunks (-1: none kept)
-    carry: [Vec<i32>; 2],
+    carry: Vec<Vec<i32>>,
     retries: u64,
     carried: u64,
     dev0: c_int,
-    // retry buffers, kept between retries (grown only): fresh zeroed ones cost ~200 ms of page
-    // faults per retry of a dozen RS(10,4) 1 MiB parts, and page-locked ones go up unstaged
-    retry_bufs: RetryBuffers,
+    // per window: retry buffers, kept between retries (grown only): fresh zeroed ones cost
+    // ~200 ms of page faults per retry of a dozen RS(10,4) 1 MiB parts, and page-locked ones go
+    // up unstaged
+    retry_bufs: Vec<RetryBuffers>,
 }
 
 #[derive(Default)]
@@ -406,17 +436,19 @@ impl BatchReader {
         let window = parts_per_batch * devices.len().max(1);
         let dev0 = devices.first().copied().unwrap_or(-1);
         let t = data + parity;
-        let buf = |n: usize| HostBuffer::zeroed(n, dev0);
+        let bufs = |n: usize| -> Result<Vec<HostBuffer>, CecError> {
+            (0..WINDOWS).map(|_| HostBuffer::zeroed(n, dev0)).collect()
+        };
         Ok(BatchReader {
-            chunks: [buf(window * t * chunk_size)?, buf(window * t * chunk_size)?],
-            out: [buf(window * data * chunk_size)?, buf(window * data * chunk_size)?],
-            present: [vec![0u8; window * t], vec![0u8; window * t]],
-            expected: [vec![0u8; window * t * 32], vec![0u8; window * t * 32]],
-            verified: [vec![0u8; window * t], vec![0u8; window * t]],
-            status: [vec![0; window], vec![0; window]],
-            cursor: [vec![0; window * t], vec![0; window * t]],
-            exhausted: [vec![false; window * t], vec![false; window * t]],
-            carry: [vec![-1; window], vec![-1; window]],
+            chunks: bufs(window * t * chunk_size)?,
+            out: bufs(window * data * chunk_size)?,
+            present: vec![vec![0u8; window * t]; WINDOWS],
+            expected: vec![vec![0u8; window * t * 32]; WINDOWS],
+            verified: vec![vec![0u8; window * t]; WINDOWS],
+            status: vec![vec![0; window]; WINDOWS],
+            cursor: vec![vec![0; window * t]; WINDOWS],
+            exhausted: vec![vec![false; window * t]; WINDOWS],
+            carry: vec![vec![-1; window]; WINDOWS],
             multi,
             codec,
             d: data,
@@ -426,7 +458,7 @@ impl BatchReader {
             retries: 0,
             carried: 0,
             dev0,
-            retry_bufs: RetryBuffers::default(),
+            retry_bufs: (0..WINDOWS).map(|_| RetryBuffers::default()).collect(),
         })
     }
 
@@ -463,35 +495,46 @@ impl BatchReader {
         if digests.len() < n_parts * self.t {
             return Err(BatchReadError::Engine(crate::too_small("digests")));
         }
+        let mut live: Vec<Option<LiveRead>> = (0..WINDOWS).map(|_| None).collect();
+        let res = self.read_windows(n_parts, digests, &mut fetch, &mut sink, &mut live);
+        if res.is_err() {
+            self.drain(&live);
+        }
+        res
+    }
+
+    fn read_windows<F, S, E>(&mut self, n_parts: usize, digests: &[[u8; 32]], fetch: &mut F,
+                             sink: &mut S, live: &mut [Option<LiveRead>])
+                             -> Result<(), BatchReadError<E>>
+    where
+        F: FnMut(usize, usize, usize) -> Option<(usize, Vec<u8>)>,
+        S: FnMut(usize, &[&[u8]]) -> Result<(), E>,
+    {
         let mut at = 0usize;
-        let mut slot = 0usize;
-        let mut pending: Option<LiveRead> = None;
+        let mut i = 0usize;
         loop {
-            let mut current = None;
+            // windows are emitted in submission order: live[i % WINDOWS] went out WINDOWS steps
+            // ago; the one after it is checked first, so its retry overlaps this step's work
+            if let Some(next) = live[(i + 1) % WINDOWS].as_mut() {
+                if !next.checked {
+                    self.check(next, fetch).map_err(BatchReadError::Engine)?;
+                }
+            }
+            let s = i % WINDOWS;
+            if let Some(w) = live[s].as_mut() {
+                self.finish(w, fetch, sink)?;
+            }
+            live[s] = None;
             if at < n_parts {
                 let cnt = self.window.min(n_parts - at);
-                self.load(slot, at, cnt, digests, &mut fetch);
-                match unsafe { self.submit(slot, cnt) } {
-                    Ok(job) => current = Some(LiveRead { slot, job, first: at, n: cnt }),
-                    Err(e) => {
-                        self.drain(pending.take());
-                        return Err(BatchReadError::Engine(e));
-                    },
-                }
+                self.load(s, at, cnt, digests, fetch);
+                let job = unsafe { self.submit(s, cnt) }.map_err(BatchReadError::Engine)?;
+                live[s] = Some(LiveRead { slot: s, job, first: at, n: cnt, checked: false, retry: None });
                 at += cnt;
+            } else if live.iter().all(|w| w.is_none()) {
+                return Ok(());
             }
-            // the older window's parts go out first: file order
-            if let Some(prev) = pending.take() {
-                if let Err(e) = self.collect(prev, &mut fetch, &mut sink) {
-                    self.drain(current);
-                    return Err(e);
-                }
-            }
-            match current {
-                None => return Ok(()),
-                Some(c) => pending = Some(c),
-            }
-            slot ^= 1;
+            i += 1;
         }
     }
 
@@ -507,6 +550,9 @@ impl BatchReader {
         let exp = &mut self.expected[slot];
         let cur = &mut self.cursor[slot];
         let ex = &mut self.exhausted[slot];
+        for c in self.carry[slot].iter_mut().take(cnt) {
+            *c = -1;
+        }
         for q in 0..cnt {
             let mut loaded = 0usize;
             for i in 0..t {
@@ -547,16 +593,31 @@ impl BatchReader {
                                      std::ptr::null(), carry)
     }
 
-    /// Waits for a window's job, retries its failed parts, then hands its parts to the sink.
-    fn collect<F, S, E>(&mut self, w: LiveRead, fetch: &mut F, sink: &mut S) -> Result<(), BatchReadError<E>>
+    /// Waits for a window's read job; its failed parts' first retry round goes out.
+    fn check<F>(&mut self, w: &mut LiveRead, fetch: &mut F) -> Result<(), CecError>
+    where
+        F: FnMut(usize, usize, usize) -> Option<(usize, Vec<u8>)>,
+    {
+        w.checked = true;
+        self.multi.wait(w.job)?;
+        let failed: Vec<usize> = (0..w.n).filter(|&q| self.status[w.slot][q] != 0).collect();
+        if !failed.is_empty() {
+            self.retry_start(w, failed, fetch)?;
+        }
+        Ok(())
+    }
+
+    /// Finishes a window's retry (if any), then hands its parts to the sink.
+    fn finish<F, S, E>(&mut self, w: &mut LiveRead, fetch: &mut F, sink: &mut S) -> Result<(), BatchReadError<E>>
     where
         F: FnMut(usize, usize, usize) -> Option<(usize, Vec<u8>)>,
         S: FnMut(usize, &[&[u8]]) -> Result<(), E>,
     {
-        self.multi.wait(w.job).map_err(BatchReadError::Engine)?;
-        let failed: Vec<usize> = (0..w.n).filter(|&q| self.status[w.slot][q] != 0).collect();
-        if !failed.is_empty() {
-            self.retry(&w, &failed, fetch).map_err(BatchReadError::Engine)?;
+        if !w.checked {
+            self.check(w, fetch).map_err(BatchReadError::Engine)?;
+        }
+        if w.retry.is_some() {
+            self.retry_finish(w, fetch).map_err(BatchReadError::Engine)?;
         }
         let (d, l) = (self.d, self.chunk_size);
         let out: &[u8] = &self.out[w.slot];
@@ -571,140 +632,201 @@ impl BatchReader {
     /// `CEC_PRESENT_VERIFIED`: kept on the GPU under the part's carry id, or, when the scheduler
     /// kept none, sent again from the window's buffer: the bytes that verified) plus, up to d, the
     /// failed chunks' next copies and then untried chunks, until each decodes; a part with no copy
-    /// left fails the read (its and the other open parts' carry ids go back).
-    fn retry<F>(&mut self, w: &LiveRead, failed: &[usize], fetch: &mut F) -> Result<(), CecError>
+    /// left fails the read (its and the other open parts' carry ids go back, `drain`).  This
+    /// queues the first round; `retry_finish` waits for it and runs any further rounds.
+    fn retry_start<F>(&mut self, w: &mut LiveRead, failed: Vec<usize>, fetch: &mut F) -> Result<(), CecError>
     where
         F: FnMut(usize, usize, usize) -> Option<(usize, Vec<u8>)>,
     {
-        let mut cid: Vec<i32> = failed.iter().map(|&q| self.carry[w.slot][q]).collect();
-        let mut bufs = std::mem::take(&mut self.retry_bufs);
-        let res = self.retry_rounds(w, failed, fetch, &mut cid, &mut bufs);
-        self.retry_bufs = bufs;
-        if res.is_err() {
-            for &id in cid.iter().filter(|&&id| id >= 0) {
-                let _ = self.multi.carry_release(id);
+        let (t, l) = (self.t, self.chunk_size);
+        let f = failed.len();
+        let mut rt = Retry {
+            open: (0..f).collect(),
+            tried: vec![false; f * t],
+            good: vec![false; f * t],
+            exhausted: vec![false; f * t],
+            cursor: vec![0usize; f * t],
+            cid: vec![-1; f],
+            g: 0,
+            job: 0,
+            in_flight: false,
+            r_pres: Vec::new(),
+            r_exp: Vec::new(),
+            r_ver: Vec::new(),
+            r_status: Vec::new(),
+            r_cin: Vec::new(),
+            r_cout: Vec::new(),
+            failed,
+        };
+        for (r, &q) in rt.failed.iter().enumerate() {
+            rt.cid[r] = self.carry[w.slot][q];  // the retry holds the id now
+            self.carry[w.slot][q] = -1;
+            for i in 0..t {
+                rt.tried[r * t + i] = self.present[w.slot][q * t + i] != 0;
+                rt.good[r * t + i] = self.verified[w.slot][q * t + i] != 0;
+                rt.exhausted[r * t + i] = self.exhausted[w.slot][q * t + i];
+                rt.cursor[r * t + i] = self.cursor[w.slot][q * t + i];
             }
         }
-        res
+        // bytes of every chunk loaded so far, in the window's retry buffers
+        let bufs = &mut self.retry_bufs[w.slot];
+        if bufs.keep.len() < f * t * l {
+            bufs.keep.resize(f * t * l, 0);
+        }
+        let ch: &[u8] = &self.chunks[w.slot];
+        for (r, &q) in rt.failed.iter().enumerate() {
+            bufs.keep[r * t * l..(r + 1) * t * l].copy_from_slice(&ch[q * t * l..(q + 1) * t * l]);
+        }
+        w.retry = Some(rt);
+        self.retry_round(w, fetch)
     }
 
-    fn retry_rounds<F>(&mut self, w: &LiveRead, failed: &[usize], fetch: &mut F,
-                       cid: &mut [i32], bufs: &mut RetryBuffers) -> Result<(), CecError>
+    /// Builds and queues one round over the window's still-open failed parts.
+    fn retry_round<F>(&mut self, w: &mut LiveRead, fetch: &mut F) -> Result<(), CecError>
     where
         F: FnMut(usize, usize, usize) -> Option<(usize, Vec<u8>)>,
     {
         let (d, t, l) = (self.d, self.t, self.chunk_size);
-        let f = failed.len();
-        let mut tried = vec![false; f * t];
-        let mut good = vec![false; f * t];
-        let mut exhausted = vec![false; f * t];
-        let mut cursor = vec![0usize; f * t];
-        if bufs.keep.len() < f * t * l {
-            bufs.keep.resize(f * t * l, 0);
-        }
-        let keep = &mut bufs.keep[..f * t * l];  // bytes of every chunk loaded so far
-        {
-            let ch: &[u8] = &self.chunks[w.slot];
-            for (r, &q) in failed.iter().enumerate() {
-                for i in 0..t {
-                    tried[r * t + i] = self.present[w.slot][q * t + i] != 0;
-                    good[r * t + i] = self.verified[w.slot][q * t + i] != 0;
-                    exhausted[r * t + i] = self.exhausted[w.slot][q * t + i];
-                    cursor[r * t + i] = self.cursor[w.slot][q * t + i];
-                }
-                keep[r * t * l..(r + 1) * t * l].copy_from_slice(&ch[q * t * l..(q + 1) * t * l]);
-            }
-        }
+        let rt = match w.retry.as_mut() {
+            Some(rt) => rt,
+            None => return Ok(()),
+        };
+        let f = rt.failed.len();
+        let g = rt.open.len();
+        let bufs = &mut self.retry_bufs[w.slot];
         let r_chunks = grown(&mut bufs.chunks, f * t * l, self.dev0)?;
         let r_out = grown(&mut bufs.out, f * d * l, self.dev0)?;
-        let mut r_pres = vec![0u8; f * t];
-        let mut r_exp = vec![0u8; f * t * 32];
-        let mut r_ver = vec![0u8; f * t];
-        let mut r_status = vec![0 as c_int; f];
-        let mut r_cin = vec![-1i32; f];
-        let mut r_cout = vec![-1i32; f];
-        let mut open: Vec<usize> = (0..f).collect();
-        while !open.is_empty() {
-            let g = open.len();
-            for (s, &r) in open.iter().enumerate() {
-                let q = failed[r];
-                r_exp[s * t * 32..(s + 1) * t * 32]
-                    .copy_from_slice(&self.expected[w.slot][q * t * 32..(q + 1) * t * 32]);
-                let have = (0..t).filter(|&i| good[r * t + i]).count();
-                r_cin[s] = cid[r];
-                for i in 0..t {
-                    let (x, y) = (r * t + i, s * t + i);
-                    r_pres[y] = 0;
-                    if good[x] {
-                        if cid[r] < 0 {  // not kept on the GPU: send the bytes that verified
-                            r_chunks[y * l..(y + 1) * l].copy_from_slice(&keep[x * l..(x + 1) * l]);
-                        }
-                        r_pres[y] = crate::sys::CEC_PRESENT_VERIFIED;
+        let keep = &mut bufs.keep[..f * t * l];
+        rt.r_pres = vec![0u8; g * t];
+        rt.r_exp = vec![0u8; g * t * 32];
+        rt.r_ver = vec![0u8; g * t];
+        rt.r_status = vec![0 as c_int; g];
+        rt.r_cin = vec![-1i32; g];
+        rt.r_cout = vec![-1i32; g];
+        for s in 0..g {
+            let r = rt.open[s];
+            let q = rt.failed[r];
+            rt.r_exp[s * t * 32..(s + 1) * t * 32]
+                .copy_from_slice(&self.expected[w.slot][q * t * 32..(q + 1) * t * 32]);
+            let have = (0..t).filter(|&i| rt.good[r * t + i]).count();
+            rt.r_cin[s] = rt.cid[r];
+            for i in 0..t {
+                let (x, y) = (r * t + i, s * t + i);
+                if rt.good[x] {
+                    if rt.cid[r] < 0 {  // not kept on the GPU: send the bytes that verified
+                        r_chunks[y * l..(y + 1) * l].copy_from_slice(&keep[x * l..(x + 1) * l]);
                     }
-                }
-                let mut added = 0usize;
-                let order = draw_order(&good[r * t..(r + 1) * t], &tried[r * t..(r + 1) * t],
-                                       &exhausted[r * t..(r + 1) * t]);
-                for i in order {
-                    if !(have + added < d) {
-                        break;
-                    }
-                    let (x, y) = (r * t + i, s * t + i);
-                    tried[x] = true;
-                    match next_copy(fetch, w.first + q, i, cursor[x], l) {
-                        Some((next, b)) => {
-                            cursor[x] = next;
-                            keep[x * l..(x + 1) * l].copy_from_slice(&b);
-                            r_chunks[y * l..(y + 1) * l].copy_from_slice(&b);
-                            r_pres[y] = 1;
-                            added += 1;
-                        },
-                        None => exhausted[x] = true,
-                    }
-                }
-                if added == 0 {
-                    return Err(CecError::Erasure(crate::Error::TooFewShardsPresent));
+                    rt.r_pres[y] = crate::sys::CEC_PRESENT_VERIFIED;
                 }
             }
-            let job = unsafe {
-                self.multi.submit_read_carry(r_chunks.as_ptr(), r_pres.as_ptr(), r_exp.as_ptr(), g,
-                                             r_out.as_mut_ptr(), r_ver.as_mut_ptr(),
-                                             r_status.as_mut_ptr(), r_cin.as_ptr(),
-                                             r_cout.as_mut_ptr())
-            }?;
-            for &r in open.iter() {  // submitted: the ids are the job's now
-                if cid[r] >= 0 {
-                    self.carried += 1;
+            let mut added = 0usize;
+            let order = draw_order(&rt.good[r * t..(r + 1) * t], &rt.tried[r * t..(r + 1) * t],
+                                   &rt.exhausted[r * t..(r + 1) * t]);
+            for i in order {
+                if !(have + added < d) {
+                    break;
                 }
-                cid[r] = -1;
-            }
-            self.multi.wait(job)?;
-            self.retries += g as u64;
-            let mut still = Vec::new();
-            let out: &mut [u8] = &mut self.out[w.slot];
-            for (s, &r) in open.iter().enumerate() {
-                let q = failed[r];
-                for i in 0..t {
-                    good[r * t + i] = r_ver[s * t + i] != 0;
-                }
-                if r_status[s] == 0 {
-                    out[q * d * l..(q + 1) * d * l].copy_from_slice(&r_out[s * d * l..(s + 1) * d * l]);
-                } else if r_status[s] == crate::sys::CEC_TOO_FEW_SHARDS_PRESENT {
-                    cid[r] = r_cout[s];
-                    still.push(r);
-                } else {
-                    return Err(crate::check(r_status[s]).unwrap_err());
+                let (x, y) = (r * t + i, s * t + i);
+                rt.tried[x] = true;
+                match next_copy(fetch, w.first + q, i, rt.cursor[x], l) {
+                    Some((next, b)) => {
+                        rt.cursor[x] = next;
+                        keep[x * l..(x + 1) * l].copy_from_slice(&b);
+                        r_chunks[y * l..(y + 1) * l].copy_from_slice(&b);
+                        rt.r_pres[y] = 1;
+                        added += 1;
+                    },
+                    None => rt.exhausted[x] = true,
                 }
             }
-            open = still;
+            if added == 0 {
+                return Err(CecError::Erasure(crate::Error::TooFewShardsPresent));
+            }
         }
+        let carry_out = rt.r_cout.as_mut_ptr();
+        rt.job = unsafe {
+            self.multi.submit_read_carry(r_chunks.as_ptr(), rt.r_pres.as_ptr(), rt.r_exp.as_ptr(), g,
+                                         r_out.as_mut_ptr(), rt.r_ver.as_mut_ptr(),
+                                         rt.r_status.as_mut_ptr(), rt.r_cin.as_ptr(), carry_out)
+        }?;
+        for s in 0..g {  // submitted: the ids are the job's now
+            let r = rt.open[s];
+            if rt.cid[r] >= 0 {
+                self.carried += 1;
+            }
+            rt.cid[r] = -1;
+        }
+        rt.g = g;
+        rt.in_flight = true;
         Ok(())
     }
 
-    /// Waits for a window's job without handing out its parts (error paths).
-    fn drain(&self, w: Option<LiveRead>) {
-        if let Some(w) = w {
-            let _ = self.multi.wait(w.job);
+    /// Waits for the round in flight; the parts that decoded go to the window's output, the
+    /// others go again (one round at a time) until every part decodes or one runs out of copies.
+    fn retry_finish<F>(&mut self, w: &mut LiveRead, fetch: &mut F) -> Result<(), CecError>
+    where
+        F: FnMut(usize, usize, usize) -> Option<(usize, Vec<u8>)>,
+    {
+        let (d, t, l) = (self.d, self.t, self.chunk_size);
+        loop {
+            let again = {
+                let rt = match w.retry.as_mut() {
+                    Some(rt) if rt.in_flight => rt,
+                    _ => break,
+                };
+                rt.in_flight = false;
+                self.multi.wait(rt.job)?;
+                self.retries += rt.g as u64;
+                let r_out: &[u8] = match self.retry_bufs[w.slot].out.as_ref() {
+                    Some(b) => &b[..],
+                    None => return Err(crate::too_small("retry buffer")),
+                };
+                let out: &mut [u8] = &mut self.out[w.slot];
+                let mut still = Vec::new();
+                for s in 0..rt.g {
+                    let r = rt.open[s];
+                    let q = rt.failed[r];
+                    for i in 0..t {
+                        rt.good[r * t + i] = rt.r_ver[s * t + i] != 0;
+                    }
+                    if rt.r_status[s] == 0 {
+                        out[q * d * l..(q + 1) * d * l].copy_from_slice(&r_out[s * d * l..(s + 1) * d * l]);
+                    } else if rt.r_status[s] == crate::sys::CEC_TOO_FEW_SHARDS_PRESENT {
+                        rt.cid[r] = rt.r_cout[s];
+                        still.push(r);
+                    } else {
+                        return Err(crate::check(rt.r_status[s]).unwrap_err());
+                    }
+                }
+                rt.open = still;
+                !rt.open.is_empty()
+            };
+            if again {
+                self.retry_round(w, fetch)?;
+            }
+        }
+        w.retry = None;
+        Ok(())
+    }
+
+    /// Error paths: no job may still write into the windows, and carry ids nobody will use go
+    /// back to their GPUs.
+    fn drain(&self, live: &[Option<LiveRead>]) {
+        for w in live.iter().flatten() {
+            if !w.checked {
+                let _ = self.multi.wait(w.job);
+            }
+            for &id in self.carry[w.slot].iter().take(w.n).filter(|&&id| id >= 0) {
+                let _ = self.multi.carry_release(id);
+            }
+            if let Some(rt) = w.retry.as_ref() {
+                if rt.in_flight {
+                    let _ = self.multi.wait(rt.job);
+                }
+                for &id in rt.cid.iter().filter(|&&id| id >= 0) {
+                    let _ = self.multi.carry_release(id);
+                }
+            }
         }
     }
 }

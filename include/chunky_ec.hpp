@@ -1074,17 +1074,39 @@ struct FileReference {
         }
     }
 
+    // The retry of a window's failed parts (file_part.rs:92-107), kept with the window so its
+    // first round runs on the GPU while the reader loads and submits the next window.
+    struct ReadRetry {
+        bool active = false;     // the window has failed parts to finish
+        bool in_flight = false;  // a round's job is queued
+        uint64_t job = 0;
+        size_t f = 0, g = 0;  // failed parts; parts in the round in flight
+        std::vector<size_t> failed, open;
+        std::vector<uint8_t> tried, good, exhausted;  // [f][t]
+        std::vector<size_t> cursor;                   // [f][t]
+        std::vector<const Bytes*> held;  // [f][t] the copy each chunk verified with
+        std::vector<int32_t> cid;        // [f] carry id of the part's verified chunks (-1 none)
+        // the round's job: [g][t] chunks (page-locked: they go up without staging), flags,
+        // digests, results, carry ids
+        detail::PinnedBuf chunks, data;
+        std::vector<uint8_t> present, expected, verified;
+        std::vector<int> status;
+        std::vector<int32_t> carry_in, carry_out;
+    };
+
     // One window of a run in flight: its parts, loaded chunk buffers and results.
     struct ReadWindow {
         size_t first = 0, n = 0;
         uint64_t job = 0;
-        bool live = false;
+        bool live = false;     // its read job was submitted and its parts not yet emitted
+        bool checked = false;  // its read job was waited for (and its retry started)
         detail::PinnedBuf chunks;  // [W][t][L] loaded chunk bytes (DMA'd directly)
         detail::PinnedBuf out;     // [W][d][L] the parts' data (DMA'd directly)
         std::vector<uint8_t> present, expected, verified, exhausted;
         std::vector<size_t> cursor;  // per chunk: the next location to read
         std::vector<int> status;
         std::vector<int32_t> carry;  // per part: the scheduler's carry id of its verified chunks
+        ReadRetry retry;
     };
     static constexpr size_t kMaxReadWindows = 8;
     // The windows (and their page-locked buffers) of this thread, shared by every read_run
@@ -1093,19 +1115,13 @@ struct FileReference {
         thread_local std::array<ReadWindow, kMaxReadWindows> win;
         return win;
     }
-    // Page-locked chunk / data buffers of this thread's read retries (grown, never shrunk).
-    struct RetryBuffers {
-        detail::PinnedBuf chunks, data;
-    };
-    static RetryBuffers& retry_buffers() {
-        thread_local RetryBuffers b;
-        return b;
-    }
 
     // Parts [k0, k0 + n) (one shape) through cec_multi in windows of one pipeline batch per
-    // shard (ppb x shards parts), up to `depth` windows in flight, so loading the next windows
-    // overlaps the GPU work and the output of the earlier ones; each window's data goes to
-    // emit() in file order.
+    // shard (ppb x shards parts), up to `depth` windows' read jobs in flight, so loading the next
+    // windows overlaps the GPU work and the output of the earlier ones; each window's data goes to
+    // emit() in file order.  A window is checked (its job waited for, the first round of its
+    // failed parts' retry queued) one step before it is emitted, so that retry runs beside the
+    // loading of the next window instead of stalling the loop: depth + 1 window buffers.
     template <typename Emit>
     void read_run(const ChunkStore& src, size_t k0, size_t n, size_t ppb, size_t depth,
                   const std::vector<int>& devices, Emit& emit) const {
@@ -1114,7 +1130,8 @@ struct FileReference {
         const std::vector<int> devs = detail::devices_or_current(devices);
         cec_multi* m = detail::cached_multi(d, t - d, L, ppb, depth, devs);
         const size_t W = ppb * devs.size();
-        const size_t nwin = std::min(std::max<size_t>(depth, 2), kMaxReadWindows);
+        const size_t nwin = std::min(std::max<size_t>(depth, 2), kMaxReadWindows - 1);
+        const size_t R = nwin + 1;
         std::array<ReadWindow, kMaxReadWindows>& win = read_windows();
         auto submit = [&](ReadWindow& w, size_t at, size_t cnt) {
             uint8_t* ch = w.chunks.reserve(W * t * L, devs[0]);
@@ -1154,36 +1171,55 @@ struct FileReference {
             w.first = at;
             w.n = cnt;
             w.live = true;
+            w.checked = false;
+            w.retry.active = w.retry.in_flight = false;
         };
-        auto collect = [&](ReadWindow& w) {
-            w.live = false;
+        auto check = [&](ReadWindow& w) {
+            w.checked = true;
             detail::check_multi(cec_multi_wait(m, w.job));
             std::vector<size_t> failed;
             for (size_t q = 0; q < w.n; ++q)
                 if (w.status[q] != CEC_OK) failed.push_back(q);
+            if (!failed.empty()) retry_start(src, m, k0, d, t, L, w, std::move(failed));
+        };
+        auto finish = [&](ReadWindow& w) {
+            if (!w.checked) check(w);
             uint8_t* out = w.out.reserve(W * d * L, devs[0]);
-            if (!failed.empty()) retry(src, m, k0, d, t, L, w, failed, out);
+            if (w.retry.active) retry_finish(src, m, k0, d, t, L, w, out);
+            w.live = false;
             emit(out, w.n * d * L);
         };
         try {
             size_t at = 0;
-            for (size_t i = 0; at < n || std::any_of(win.begin(), win.begin() + nwin,
-                                                     [](const ReadWindow& w) { return w.live; });
-                 ++i) {
-                ReadWindow& w = win[i % nwin];  // windows are collected in submission order
-                if (w.live) collect(w);
+            for (size_t i = 0;; ++i) {
+                // windows are emitted in submission order: win[i % R] was submitted R steps ago;
+                // the one after it is checked first, so its retry overlaps this step's work
+                ReadWindow& next = win[(i + 1) % R];
+                if (next.live && !next.checked) check(next);
+                ReadWindow& w = win[i % R];
+                if (w.live) finish(w);
                 if (at < n) {
                     const size_t cnt = std::min(W, n - at);
                     submit(w, at, cnt);
                     at += cnt;
+                } else if (std::none_of(win.begin(), win.begin() + R,
+                                        [](const ReadWindow& x) { return x.live; })) {
+                    break;
                 }
             }
         } catch (...) {
-            for (auto& w : win)  // no job may still write into the window buffers
-                if (w.live) {
-                    (void)cec_multi_wait(m, w.job);
-                    w.live = false;
-                }
+            for (size_t x = 0; x < R; ++x) {  // no job may still write into the window buffers
+                ReadWindow& w = win[x];
+                if (w.live && !w.checked) (void)cec_multi_wait(m, w.job);
+                if (w.retry.in_flight) (void)cec_multi_wait(m, w.retry.job);
+                if (w.live)  // carry ids the failed read will not use go back to their GPUs
+                    for (int32_t id : w.carry)
+                        if (id >= 0) (void)cec_multi_carry_release(m, id);
+                if (w.retry.active)
+                    for (int32_t id : w.retry.cid)
+                        if (id >= 0) (void)cec_multi_carry_release(m, id);
+                w.live = w.retry.active = w.retry.in_flight = false;
+            }
             throw;
         }
     }
@@ -1194,109 +1230,123 @@ struct FileReference {
     // hashed again) plus, up to d, the failed chunks' next copies and then untried chunks, until
     // they decode or no copy is left (TooFewShardsPresent, as the reference's read).  The
     // verified chunks of a part the scheduler kept on its GPU (its carry id) are not sent again;
-    // the others are re-sent from their verified copies.  The rebuilt data of window part q goes
-    // to out + q*d*L.
-    void retry(const ChunkStore& src, cec_multi* m, size_t k0, size_t d, size_t t, size_t L,
-               const ReadWindow& w, const std::vector<size_t>& failed, uint8_t* out) const {
+    // the others are re-sent from their verified copies.  retry_start queues the first round;
+    // retry_finish waits for it and runs any further rounds, the rebuilt data of window part q
+    // going to out + q*d*L.
+    void retry_start(const ChunkStore& src, cec_multi* m, size_t k0, size_t d, size_t t,
+                     size_t L, ReadWindow& w, std::vector<size_t> failed) const {
+        ReadRetry& r = w.retry;
         const size_t f = failed.size();
-        std::vector<int32_t> cid(f);  // per failed part: its carry id (-1: none held)
-        for (size_t r = 0; r < f; ++r) cid[r] = w.carry[failed[r]];
-        try {
-            retry_rounds(src, m, k0, d, t, L, w, failed, out, cid);
-        } catch (...) {
-            for (int32_t id : cid)  // ids the failed read will not use go back to their GPUs
-                if (id >= 0) (void)cec_multi_carry_release(m, id);
-            throw;
+        r.f = f;
+        r.failed = std::move(failed);
+        r.tried.assign(f * t, 0);
+        r.good.assign(f * t, 0);
+        r.exhausted.assign(f * t, 0);
+        r.cursor.assign(f * t, 0);
+        r.held.assign(f * t, nullptr);
+        r.cid.assign(f, -1);
+        for (size_t j = 0; j < f; ++j) {
+            const size_t q = r.failed[j];
+            r.cid[j] = w.carry[q];  // the retry holds the id now
+            w.carry[q] = -1;
+            for (size_t i = 0; i < t; ++i) {
+                const size_t x = q * t + i;
+                r.tried[j * t + i] = w.present[x] != 0;
+                r.good[j * t + i] = w.verified[x] != 0;
+                r.exhausted[j * t + i] = w.exhausted[x];
+                r.cursor[j * t + i] = w.cursor[x];
+            }
         }
+        // the copies that verified in the window's pass: the location before each cursor
+        for (size_t j = 0; j < f; ++j) {
+            const FilePart& part = parts[k0 + w.first + r.failed[j]];
+            for (size_t i = 0; i < t; ++i)
+                if (r.good[j * t + i])
+                    r.held[j * t + i] = src.find(part.chunk(i).locations[r.cursor[j * t + i] - 1]);
+        }
+        r.open.resize(f);
+        for (size_t j = 0; j < f; ++j) r.open[j] = j;
+        r.active = true;
+        retry_round(src, m, k0, d, t, L, w);
     }
 
-    void retry_rounds(const ChunkStore& src, cec_multi* m, size_t k0, size_t d, size_t t,
-                      size_t L, const ReadWindow& w, const std::vector<size_t>& failed,
-                      uint8_t* out, std::vector<int32_t>& cid) const {
-        const size_t f = failed.size();
-        std::vector<uint8_t> tried(f * t), good(f * t), exhausted(f * t);
-        std::vector<size_t> cursor(f * t);
-        std::vector<const Bytes*> held(f * t, nullptr);  // the copy each chunk verified with
-        for (size_t r = 0; r < f; ++r)
+    // Builds and queues one round over the window's still-open failed parts.
+    void retry_round(const ChunkStore& src, cec_multi* m, size_t k0, size_t d, size_t t,
+                     size_t L, ReadWindow& w) const {
+        ReadRetry& r = w.retry;
+        const size_t g = r.open.size();
+        // kept page-locked between retries: fresh zeroed buffers cost ~200 ms of page faults
+        // per retry of a dozen RS(10,4) 1 MiB parts (profiles/r6/cp_bench_*.log)
+        uint8_t* chunks = r.chunks.reserve(r.f * t * L, -1);
+        r.data.reserve(r.f * d * L, -1);
+        r.present.assign(g * t, 0);
+        r.expected.resize(g * t * 32);
+        r.verified.assign(g * t, 0);
+        r.status.assign(g, 0);
+        r.carry_in.assign(g, -1);
+        r.carry_out.assign(g, -1);
+        for (size_t q = 0; q < g; ++q) {
+            const size_t j = r.open[q];
+            const FilePart& part = parts[k0 + w.first + r.failed[j]];
+            size_t have = 0, added = 0;
+            r.carry_in[q] = r.cid[j];
             for (size_t i = 0; i < t; ++i) {
-                const size_t x = failed[r] * t + i;
-                tried[r * t + i] = w.present[x] != 0;
-                good[r * t + i] = w.verified[x] != 0;
-                exhausted[r * t + i] = w.exhausted[x];
-                cursor[r * t + i] = w.cursor[x];
+                std::memcpy(&r.expected[(q * t + i) * 32], part.chunk(i).hash.digest().data(), 32);
+                if (!r.good[j * t + i]) continue;
+                ++have;
+                if (r.cid[j] < 0)  // not kept on the GPU: send the copy that verified
+                    std::memcpy(&chunks[(q * t + i) * L], r.held[j * t + i]->data(), L);
+                r.present[q * t + i] = CEC_PRESENT_VERIFIED;
             }
-        // the copies that verified in the window's pass: the location before each cursor
-        for (size_t r = 0; r < f; ++r) {
-            const FilePart& part = parts[k0 + w.first + failed[r]];
-            for (size_t i = 0; i < t; ++i)
-                if (good[r * t + i]) held[r * t + i] = src.find(part.chunk(i).locations[cursor[r * t + i] - 1]);
+            for (size_t i : detail::draw_order(&r.good[j * t], &r.tried[j * t], &r.exhausted[j * t], t)) {
+                if (!(have + added < d)) break;
+                r.tried[j * t + i] = 1;
+                const Bytes* bytes = detail::next_copy(src, part.chunk(i), r.cursor[j * t + i], L,
+                                                       &r.cursor[j * t + i]);
+                if (!bytes) {
+                    r.exhausted[j * t + i] = 1;
+                    continue;
+                }
+                r.held[j * t + i] = bytes;
+                std::memcpy(&chunks[(q * t + i) * L], bytes->data(), L);
+                r.present[q * t + i] = 1;
+                ++added;
+            }
+            if (added == 0) throw ErasureError(Error::TooFewShardsPresent);
         }
-        // the thread's retry buffers, kept page-locked between retries: fresh zeroed vectors cost
-        // ~200 ms of page faults per retry of a dozen RS(10,4) 1 MiB parts
-        // (profiles/r6final/cp_bench_*.log), and page-locked ones go up without staging
-        RetryBuffers& rb = retry_buffers();
-        uint8_t* chunks = rb.chunks.reserve(f * t * L, -1);
-        uint8_t* data = rb.data.reserve(f * d * L, -1);
-        std::vector<uint8_t> present(f * t), expected(f * t * 32), verified(f * t);
-        std::vector<int> status(f);
-        std::vector<int32_t> carry_in(f, -1), carry_out(f, -1);
-        const bool carry = detail::read_carry();
-        std::vector<size_t> open(f);
-        for (size_t r = 0; r < f; ++r) open[r] = r;
-        while (!open.empty()) {
-            // build the resubmission of the still-open parts
-            std::vector<size_t> next_open;
-            const size_t g = open.size();
-            std::fill(present.begin(), present.begin() + g * t, uint8_t(0));
-            for (size_t q = 0; q < g; ++q) {
-                const size_t r = open[q];
-                const FilePart& part = parts[k0 + w.first + failed[r]];
-                size_t have = 0, added = 0;
-                carry_in[q] = cid[r];
-                for (size_t i = 0; i < t; ++i) {
-                    std::memcpy(&expected[(q * t + i) * 32], part.chunk(i).hash.digest().data(), 32);
-                    if (!good[r * t + i]) continue;
-                    ++have;
-                    if (cid[r] < 0)  // not kept on the GPU: send the copy that verified
-                        std::memcpy(&chunks[(q * t + i) * L], held[r * t + i]->data(), L);
-                    present[q * t + i] = CEC_PRESENT_VERIFIED;
-                }
-                for (size_t i : detail::draw_order(&good[r * t], &tried[r * t], &exhausted[r * t], t)) {
-                    if (!(have + added < d)) break;
-                    tried[r * t + i] = 1;
-                    const Bytes* bytes = detail::next_copy(src, part.chunk(i), cursor[r * t + i], L,
-                                                           &cursor[r * t + i]);
-                    if (!bytes) {
-                        exhausted[r * t + i] = 1;
-                        continue;
-                    }
-                    held[r * t + i] = bytes;
-                    std::memcpy(&chunks[(q * t + i) * L], bytes->data(), L);
-                    present[q * t + i] = 1;
-                    ++added;
-                }
-                if (added == 0) throw ErasureError(Error::TooFewShardsPresent);
-            }
-            uint64_t job = 0;
-            detail::check_multi(cec_multi_read_carry(m, chunks, present.data(),
-                                                     expected.data(), g, data,
-                                                     verified.data(), status.data(), nullptr, 0,
-                                                     carry_in.data(),
-                                                     carry ? carry_out.data() : nullptr, &job));
-            for (size_t q = 0; q < g; ++q) cid[open[q]] = -1;  // the job's ids now
-            detail::check_multi(cec_multi_wait(m, job));
-            for (size_t q = 0; q < g; ++q) {
-                const size_t r = open[q];
-                for (size_t i = 0; i < t; ++i) good[r * t + i] = verified[q * t + i] != 0;
-                if (status[q] == CEC_OK) {
-                    std::memcpy(out + failed[r] * d * L, &data[q * d * L], d * L);
+        detail::check_multi(cec_multi_read_carry(
+            m, chunks, r.present.data(), r.expected.data(), g, r.data.reserve(r.f * d * L, -1),
+            r.verified.data(), r.status.data(), nullptr, 0, r.carry_in.data(),
+            detail::read_carry() ? r.carry_out.data() : nullptr, &r.job));
+        for (size_t q = 0; q < g; ++q) r.cid[r.open[q]] = -1;  // the job's ids now
+        r.g = g;
+        r.in_flight = true;
+    }
+
+    // Waits for the round in flight; the parts that decoded go to out, the others go again
+    // (one round at a time) until every part decodes or one runs out of copies.
+    void retry_finish(const ChunkStore& src, cec_multi* m, size_t k0, size_t d, size_t t,
+                      size_t L, ReadWindow& w, uint8_t* out) const {
+        ReadRetry& r = w.retry;
+        while (r.in_flight) {
+            r.in_flight = false;
+            detail::check_multi(cec_multi_wait(m, r.job));
+            const uint8_t* data = r.data.reserve(r.f * d * L, -1);
+            std::vector<size_t> still;
+            for (size_t q = 0; q < r.g; ++q) {
+                const size_t j = r.open[q];
+                for (size_t i = 0; i < t; ++i) r.good[j * t + i] = r.verified[q * t + i] != 0;
+                if (r.status[q] == CEC_OK) {
+                    std::memcpy(out + r.failed[j] * d * L, data + q * d * L, d * L);
                 } else {
-                    cid[r] = carry_out[q];
-                    next_open.push_back(r);
+                    r.cid[j] = r.carry_out[q];
+                    still.push_back(j);
                 }
             }
-            open.swap(next_open);
+            r.open.swap(still);
+            if (!r.open.empty()) retry_round(src, m, k0, d, t, L, w);
         }
+        r.active = false;
     }
 };
 
@@ -1485,9 +1535,9 @@ inline void release_thread_buffers() {
     for (auto& w : FileReference::read_windows()) {
         w.chunks.release();
         w.out.release();
+        w.retry.chunks.release();
+        w.retry.data.release();
     }
-    FileReference::retry_buffers().chunks.release();
-    FileReference::retry_buffers().data.release();
     for (auto& w : FileReference::check_windows()) {
         w.chunks.release();
         w.rebuilt.release();

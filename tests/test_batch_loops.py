@@ -59,6 +59,7 @@ class FakeMulti:
         self.pool = {}  # carry id -> (kept mask, expected digests, chunk bytes)
         self.next_carry = itertools.count(0)
         self.uploaded = self.carried = 0
+        self.events = []  # ("read", n, retry?) per read job, in submission order
 
     def carry_release(self, cid):
         del self.pool[int(cid)]
@@ -84,6 +85,7 @@ class FakeMulti:
     def read(self, chunks, present, expected, n, data, verified, status, rebuilt_only=False,
              carry_in=None, carry_out=None):
         assert self.kinds & self.READ
+        self.events.append(("read", n, carry_in is not None))
         d, t, L = self.d, self.t, self.L
         ch = _arr(chunks)[:n * t * L].reshape(n, t, L).copy()
         pres = np.asarray(present).reshape(-1, t)
@@ -458,3 +460,23 @@ def test_checker_resilver_rebuilds_only_chunks_without_a_valid_copy(fakes):
     assert got[7][0].error == TOO_FEW_SHARDS_PRESENT and got[7][1] == {}
     assert all(got[k][0].error is None for k in got if k != 7)
     assert c.extra_passes == 2  # windows holding parts 2 and 4 (multi-location chunks)
+
+
+def test_batch_reader_retry_overlaps_the_next_window(fakes):
+    """A window's failed parts go out again (their first retry round) when the window is
+    checked, one step before it is emitted: after the window behind it was submitted and before
+    the next window is loaded, so the retry runs beside that loading instead of stalling the
+    loop; the parts still reach the sink in file order."""
+    n = 4 * 3
+    chunks, dig = _store(n, 12)
+    st = Locations(chunks)
+    st.set(1, 0, "bad")  # window 0 (parts 0-3): part 1 retries
+    r = br.BatchReader(D, P, L, 4, 2, [0])
+    order = []
+    r.read(n, st.fetch, lambda k: dig[k], lambda k, data: order.append(("emit", k)))
+    assert [k for _, k in order] == list(range(n))
+    ev = r.multi.events
+    # windows 0 and 1 submitted, then window 0's retry, then window 2
+    assert ev[:4] == [("read", 4, False), ("read", 4, False), ("read", 1, True),
+                      ("read", 4, False)], ev
+    assert r.retries == 1 and r.carried_parts == 1 and r.multi.pool == {}

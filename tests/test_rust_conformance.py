@@ -173,20 +173,26 @@ def test_batch_writer_mirrors_the_cpp_loop():
 
 
 def test_batch_reader_mirrors_the_cpp_and_python_loops():
-    """BatchReader::read is the C++ read_run / retry loop (and chunky_ec/batchreader.py, its
-    GPU-tested Python twin): load a window (first d fetched chunks per part), submit it, hand
-    the older window out first; failed parts retried with PRESENT_VERIFIED chunks plus untried
-    ones until they decode, TooFewShardsPresent when none is left."""
+    """BatchReader::read is the C++ read_run / retry_start / retry_finish loop (and
+    chunky_ec/batchreader.py, its GPU-tested Python twin): per step the window after the oldest
+    is checked (its failed parts' first retry round queued), the oldest finished and handed out,
+    then the next window loaded and submitted into its buffers; failed parts retried with
+    PRESENT_VERIFIED chunks plus untried ones until they decode, TooFewShardsPresent when none
+    is left."""
     batch = _crate_sources()["batch.rs"]
     body = batch[batch.index("pub fn read<"):batch.index("    fn load<")]
-    order = [body.index(s) for s in ("self.load(", "self.submit(", "self.collect(prev")]
-    assert order == sorted(order) and "slot ^= 1" in body
-    retry = batch[batch.index("    fn retry<"):batch.index("    fn drain(&self, w: Option<LiveRead>)")]
+    order = [body.index(s) for s in ("self.check(next", "self.finish(w", "self.load(", "self.submit(")]
+    assert order == sorted(order) and "(i + 1) % WINDOWS" in body and "self.drain(&live)" in body
+    retry = batch[batch.index("    fn retry_start<"):batch.index("    fn drain(&self, live: &[Option<LiveRead>])")]
     for s in ("CEC_PRESENT_VERIFIED", "have + added < d", "TooFewShardsPresent",
-              "self.multi.submit_read_carry(", "carry_release("):
+              "self.multi.submit_read_carry(", "self.multi.wait(rt.job)"):
         assert s in retry, s
+    drain = batch[batch.index("    fn drain(&self, live: &[Option<LiveRead>])"):]
+    drain = drain[:drain.index("\n    }\n")]
+    assert "carry_release(" in drain and "rt.cid" in drain and "self.multi.wait(rt.job)" in drain
     py = open(os.path.join(ROOT, "chunky-bits_amd", "chunky_ec", "batchreader.py")).read()
-    for s in ("def _load", "def _submit", "def _collect", "def _retry", "have + added < d",
+    for s in ("def _load", "def _submit", "def _check", "def _finish", "def _retry_start",
+              "def _retry_round", "def _retry_finish", "have + added < d",
               "PRESENT_VERIFIED", "TOO_FEW_SHARDS_PRESENT"):
         assert s in py, s
 
@@ -202,7 +208,7 @@ def test_location_walk_is_the_same_rule_in_rust_python_and_cpp():
               "pub struct FileChecker", "CEC_PRESENT_VERIFIED", "submit_verify(", "submit_resilver(",
               "pub enum CopyCheck"):
         assert s in batch, s
-    retry = batch[batch.index("    fn retry<"):batch.index("    fn drain(&self, w: Option<LiveRead>)")]
+    retry = batch[batch.index("    fn retry_start<"):batch.index("    fn drain(&self, live: &[Option<LiveRead>])")]
     assert "draw_order(" in retry and "next_copy(" in retry and "cursor[x]" in retry
     lib = open(RUST).read()
     for s in ("pub fn sha256_many(", "pub unsafe fn submit_verify(", "pub unsafe fn submit_resilver(",
