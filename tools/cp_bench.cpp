@@ -131,26 +131,34 @@ int main(int argc, char** argv) {
             }
             return u;
         };
-        for (int carry = 1; carry >= 0; --carry) {
+        for (int carry = 1; carry >= 0; --carry) {  // checked (and warms the windows)
             detail::read_carry() = carry != 0;
-            const Bytes dmg = f.read(store, 128, 4, devices);  // checked (and warms the windows)
-            ok = dmg.size() == n && std::memcmp(dmg.data(), input.data(), n) == 0;
-            // timed: streamed to a sink that discards the bytes, as read_to above
-            const uint64_t u0 = uploaded();
-            size_t got = 0;
-            t0 = std::chrono::steady_clock::now();
-            f.read_to(store, [&](const uint8_t*, size_t m) { got += m; }, 128, 4, devices);
-            const double rd = secs(t0);
-            const uint64_t up = uploaded() - u0;
-            ok = ok && got == n;
-            std::printf("batched   read with %.2f %% of data copies damaged (%zu flipped) + the "
-                        "lost chunks, %s: %6.2f GB/s streamed to a sink, %llu chunks sent to the "
-                        "GPU, bit-exact %s\n",
-                        damage * 100, flipped, carry ? "carry   " : "no carry", double(n) / rd / 1e9,
-                        static_cast<unsigned long long>(up), ok ? "yes" : "NO");
-            std::fflush(stdout);
-            if (!ok) return 1;
+            const Bytes dmg = f.read(store, 128, 4, devices);
+            ok = ok && dmg.size() == n && std::memcmp(dmg.data(), input.data(), n) == 0;
         }
+        // timed: streamed to a sink that discards the bytes, as read_to above; the two modes
+        // alternate, 3 runs each, best of each kept (one run is ~1 s: box noise is ±15 %)
+        double best[2] = {0, 0};
+        uint64_t sent[2] = {0, 0};
+        for (int rep = 0; rep < 3; ++rep)
+            for (int carry = 1; carry >= 0; --carry) {
+                detail::read_carry() = carry != 0;
+                const uint64_t u0 = uploaded();
+                size_t got = 0;
+                t0 = std::chrono::steady_clock::now();
+                f.read_to(store, [&](const uint8_t*, size_t m) { got += m; }, 128, 4, devices);
+                best[carry] = std::max(best[carry], double(n) / secs(t0) / 1e9);
+                sent[carry] = uploaded() - u0;
+                ok = ok && got == n;
+            }
+        for (int carry = 1; carry >= 0; --carry)
+            std::printf("batched   read with %.2f %% of data copies damaged (%zu flipped) + the "
+                        "lost chunks, %s: %6.2f GB/s streamed to a sink (best of 3), %llu chunks "
+                        "sent to the GPU, bit-exact %s\n",
+                        damage * 100, flipped, carry ? "carry   " : "no carry", best[carry],
+                        static_cast<unsigned long long>(sent[carry]), ok ? "yes" : "NO");
+        std::fflush(stdout);
+        if (!ok) return 1;
         detail::read_carry() = true;
     }
     return 0;
