@@ -926,6 +926,7 @@ def set_device(device: int) -> None:
 
 PIPE_EXTERNAL = 2  # CEC_PIPE_EXTERNAL
 PRESENT_VERIFIED = 0x80  # CEC_PRESENT_VERIFIED: read-retry flag (loaded, verified by an earlier pass)
+MULTI_AHEAD = 64  # CEC_MULTI_AHEAD: a read job queued ahead of the jobs not yet started
 READ_RESILVER = 4  # CEC_READ_RESILVER: read-pipeline flag, FilePart::resilver's compute
 READ_VERIFY_ONLY = 8  # CEC_READ_VERIFY_ONLY: read-pipeline flag, FilePart::verify's compute
 READ_CARRY = 16  # CEC_READ_CARRY: read-pipeline flag, retries' verified chunks kept on the device
@@ -1003,12 +1004,14 @@ class Multi:
         return job.value
 
     def read(self, chunks, present, expected, n_parts: int, data, verified, status,
-             rebuilt_only: bool = False, carry_in=None, carry_out=None):
+             rebuilt_only: bool = False, carry_in=None, carry_out=None, ahead: bool = False):
         """Returns (job, data_ptrs) where data_ptrs ([n*d] c_void_p) is filled at wait().
         carry_out ([n] int32 numpy, nullable) receives, at wait(), a carry id for each part
         reported TOO_FEW_SHARDS_PRESENT whose verified chunks stay on its GPU (-1: none);
         carry_in ([n] int32, nullable) hands such ids to a retry: those parts' PRESENT_VERIFIED
-        chunks are taken from the GPU, not from `chunks` (cec_multi_read_carry)."""
+        chunks are taken from the GPU, not from `chunks` (cec_multi_read_carry).  ahead
+        (CEC_MULTI_AHEAD): the job goes ahead of the queued jobs not yet started (a reader's retry
+        round, which the window being emitted waits for)."""
         import numpy as np
         job = ctypes.c_uint64(0)
         ptrs = (ctypes.c_void_p * max(n_parts * self.d, 1))()
@@ -1023,7 +1026,8 @@ class Multi:
         code = _lib.cec_multi_read_carry(
             self._h, _addr(chunks), _addr(present), _addr(expected), n_parts, _addr(data),
             _addr(verified), ctypes.cast(_addr(status), ctypes.POINTER(ctypes.c_int)), ptrs,
-            1 if rebuilt_only else 0, cin.ctypes.data_as(i32) if cin is not None else None,
+            (1 if rebuilt_only else 0) | (MULTI_AHEAD if ahead else 0),
+            cin.ctypes.data_as(i32) if cin is not None else None,
             carry_out.ctypes.data_as(i32) if carry_out is not None else None, ctypes.byref(job))
         if code != OK:
             raise MultiError(code)

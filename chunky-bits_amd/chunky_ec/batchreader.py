@@ -26,9 +26,10 @@ ranges) while it loads the next window.  A part whose loaded chunks do not all v
 resubmitted with the chunks that verified flagged ``CEC_PRESENT_VERIFIED`` (used, not hashed
 again; kept on the GPU under the part's carry id), the failed chunks' next copies, then untried
 chunks, up to d, until it decodes; a part that runs out of copies fails the read with
-TooFewShardsPresent, as the reference's does.  Three window buffers: a window is checked (its job
-waited for, its failed parts' first retry round queued) one step before it is emitted, so the
-retry runs on the GPUs while the next window loads.
+TooFewShardsPresent, as the reference's does.  depth + 1 window buffers (at most 8): a window is
+checked (its job waited for, its failed parts' first retry round queued, ahead of the windows
+queued after it: CEC_MULTI_AHEAD) a step or more before it is emitted, so the retry runs on the
+GPUs while the next windows load.
 :func:`read_part` is the same rule for one part through the per-call API, and :class:`FileReader`
 splits a file into runs of one shape (chunk size, d, p: the short last part has its own chunk size,
 file_part.rs:152) and keeps one BatchReader per shape.
@@ -97,7 +98,6 @@ class _Window:
 
 
 class BatchReader:
-    R = 3  # window buffers: two windows' read jobs in flight, one being emitted
 
     def __init__(self, data: int, parity: int, chunk_size: int, parts_per_batch: int, depth: int,
                  devices: List[int], carry: bool = True):
@@ -110,7 +110,11 @@ class BatchReader:
         self.d, self.p, self.t, self.L = data, parity, data + parity, chunk_size
         self.window = parts_per_batch * max(len(devices), 1)
         dev0 = devices[0] if devices else -1
-        W, t, L, R = self.window, self.t, chunk_size, self.R
+        # window buffers: up to depth windows' read jobs in flight, one being emitted; per step
+        # the windows submitted 3 or more steps ago are checked (at least the next one)
+        self.R = R = min(max(depth, 2), 7) + 1
+        self.ahead = R - 3 if R > 4 else 1
+        W, t, L = self.window, self.t, chunk_size
         self.chunks = [HostBuffer(W * t * L, dev0) for _ in range(R)]
         self.out = [HostBuffer(W * data * L, dev0) for _ in range(R)]
         self.present = [np.zeros((W, t), np.uint8) for _ in range(R)]
@@ -134,18 +138,20 @@ class BatchReader:
         """Parts 0..n_parts-1 (all of this reader's shape): ``fetch(part, chunk, start)`` as the
         module describes, ``digests(part)`` the part's metadata digests [d+p][32]; ``sink(part,
         data_chunks)`` gets the d data chunks of every part, in file order.  A window is checked
-        (its job waited for, the first round of its failed parts' retry queued) one step before it
-        is emitted, so that retry runs beside the loading of the next window."""
+        (its job waited for, the first round of its failed parts' retry queued) a step or more
+        before it is emitted, so that retry runs beside the loading of the next windows (a retry
+        round costs one SHA-256 chain, ~33 ms for 1 MiB chunks, whatever its size)."""
         R = self.R
         live: List[Optional[_Window]] = [None] * R
         at = i = 0
         try:
             while True:
                 # windows are emitted in submission order: live[i % R] went out R steps ago; the
-                # one after it is checked first, so its retry overlaps this step's work
-                nxt = live[(i + 1) % R]
-                if nxt is not None and not nxt.checked:
-                    self._check(nxt, fetch)
+                # next ones are checked first, so their retries overlap this step's work
+                for a in range(1, self.ahead + 1):
+                    nxt = live[(i + a) % R]
+                    if nxt is not None and not nxt.checked:
+                        self._check(nxt, fetch)
                 s = i % R
                 if live[s] is not None:
                     self._finish(live[s], fetch, sink)
@@ -293,7 +299,7 @@ class BatchReader:
                 raise Error(TOO_FEW_SHARDS_PRESENT)
         rt.job, _ = self.multi.read(rc[:g], rt.r_pres, rt.r_exp, g, ro[:g], rt.r_ver, rt.r_st,
                                     carry_in=rt.r_cin,
-                                    carry_out=rt.r_cout if self.use_carry else None)
+                                    carry_out=rt.r_cout if self.use_carry else None, ahead=True)
         for q in rt.open_:  # submitted: the ids are the job's now
             self.carried_parts += 1 if rt.cid[q] >= 0 else 0
             rt.cid[q] = -1

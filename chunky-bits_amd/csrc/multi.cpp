@@ -15,7 +15,9 @@
 // Read, resilver and verify jobs use the same read pipeline, the mode picked per submit.  A worker
 // streams its share batch by batch: caller buffers that are page-locked (cec_host_alloc) are
 // DMA'd directly; pageable ones go through the worker's own NUMA-local pinned staging.  Jobs are
-// queued and run in submission order; a worker keeps its batches in flight across job
+// queued and run in submission order, except that a read job flagged CEC_MULTI_AHEAD (a reader's
+// retry round: a few parts whose window waits for them) goes ahead of the queued jobs that have
+// not started, behind earlier such jobs; a worker keeps its batches in flight across job
 // boundaries: with its queue empty it completes batches as their events fire while watching the
 // queue, so the next job of a stream is queued behind the batches still running instead of after
 // a drain (no bubble).
@@ -60,6 +62,7 @@ struct Job {
     Kind kind = Kind::Write;
     size_t n = 0;
     unsigned mode = 0;  // read: the read pipeline's mode bits for this job's submits
+    bool ahead = false;  // CEC_MULTI_AHEAD: queued ahead of the jobs not yet started
     // write
     const uint8_t* data = nullptr;
     uint8_t* parity = nullptr;
@@ -632,7 +635,12 @@ struct cec_multi {
         for (size_t g = 0; g < G; ++g) {
             const bool any = raw->share.empty() ? raw->n * (g + 1) / G > raw->n * g / G
                                                 : !raw->share[g].empty();
-            if (any) shards[g]->queue.push_back(raw);
+            if (!any) continue;
+            std::deque<Job*>& q = shards[g]->queue;
+            auto at = q.end();
+            if (raw->ahead)  // behind the AHEAD jobs already queued, ahead of the others
+                at = std::find_if(q.begin(), q.end(), [](const Job* x) { return !x->ahead; });
+            q.insert(at, raw);
         }
         work_cv.notify_all();
         return CEC_OK;
@@ -752,7 +760,8 @@ int cec_multi_read_carry(cec_multi* m, const uint8_t* chunks, const uint8_t* pre
                          const uint8_t* expected, size_t n_parts, uint8_t* data, uint8_t* verified,
                          int* part_status, const uint8_t** data_ptrs, unsigned flags,
                          const int32_t* carry_in, int32_t* carry_out, uint64_t* job) {
-    if (!m || !job || (flags & ~unsigned(CEC_READ_REBUILT_ONLY))) return CEC_ERR_INVALID_ARGUMENT;
+    if (!m || !job || (flags & ~unsigned(CEC_READ_REBUILT_ONLY | CEC_MULTI_AHEAD)))
+        return CEC_ERR_INVALID_ARGUMENT;
     if (n_parts && (!chunks || !present || !expected || !data || !verified || !part_status))
         return CEC_ERR_INVALID_ARGUMENT;
     if ((flags & CEC_READ_REBUILT_ONLY) && !data_ptrs) return CEC_ERR_INVALID_ARGUMENT;
@@ -764,6 +773,7 @@ int cec_multi_read_carry(cec_multi* m, const uint8_t* chunks, const uint8_t* pre
     j->kind = Kind::Read;
     j->n = n_parts;
     j->mode = flags & CEC_READ_REBUILT_ONLY;
+    j->ahead = (flags & CEC_MULTI_AHEAD) != 0;
     j->chunks = chunks;
     j->present = present;
     j->expected = expected;

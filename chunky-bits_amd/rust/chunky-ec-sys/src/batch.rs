@@ -289,8 +289,17 @@ pub enum BatchReadError<E> {
     Sink(E),
 }
 
-/// Window buffers of a [`BatchReader`]: two windows' read jobs in flight, one being emitted.
-const WINDOWS: usize = 3;
+/// Window buffers of a [`BatchReader`] of scheduler depth `depth`: up to `depth` windows' read
+/// jobs in flight (at most 7) and one being emitted.
+fn read_windows_for(depth: usize) -> usize {
+    depth.clamp(2, 7) + 1
+}
+
+/// Windows checked per step beyond the one emitted: those submitted 3 or more steps ago (their
+/// jobs are done or nearly: upload, a SHA-256 chain, download), at least the next one.
+fn checked_ahead(windows: usize) -> usize {
+    if windows > 4 { windows - 3 } else { 1 }
+}
 
 /// A read window submitted to the scheduler and not yet handed to the sink.
 struct LiveRead {
@@ -360,14 +369,15 @@ fn draw_order(good: &[bool], tried: &[bool], exhausted: &[bool]) -> Vec<usize> {
 /// `parts_per_batch * devices.len()` parts (all of this reader's shape) the reader loads the first
 /// d chunks that have a copy (data chunks first, so an intact part needs no rebuild) into a
 /// page-locked buffer and submits the window as one scheduler job: every loaded chunk verified
-/// against its metadata digest, the data chunks rebuilt.  It loads the next window while that one
-/// runs.  A part whose loaded chunks do not all verify goes again with the chunks that verified
-/// (`CEC_PRESENT_VERIFIED`: used, not hashed again; kept on the GPU under the part's carry id), the
-/// failed chunks' NEXT copies (the same chunk's next location is read before another chunk is
-/// drawn, file_part.rs:100-107), then untried chunks, up to d, until it decodes or runs out of
-/// copies.  A window is checked (its job waited for, the first round of its failed parts' retry
-/// queued) one step before it is emitted, so that retry runs beside the loading of the next
-/// window.  So a chunk listed `[bad, good]` -- what resilver leaves when it appends a rebuilt
+/// against its metadata digest, the data chunks rebuilt.  It loads the next windows while the
+/// earlier ones run (up to `depth` read jobs in flight).  A part whose loaded chunks do not all
+/// verify goes again with the chunks that verified (`CEC_PRESENT_VERIFIED`: used, not hashed
+/// again; kept on the GPU under the part's carry id), the failed chunks' NEXT copies (the same
+/// chunk's next location is read before another chunk is drawn, file_part.rs:100-107), then
+/// untried chunks, up to d, until it decodes or runs out of copies.  A window is checked (its job
+/// waited for, the first round of its failed parts' retry queued ahead of the windows queued after
+/// it, `CEC_MULTI_AHEAD`) a step or more before it is emitted, so that retry runs beside the
+/// loading of the next windows.  So a chunk listed `[bad, good]` -- what resilver leaves when it appends a rebuilt
 /// copy's location (file_part.rs:346) -- reads as in the reference.  [`FileReader`] splits a file
 /// into runs of one shape (the short last part has its own chunk size).
 /// `include/chunky_ec.hpp`'s `FileReference::read_run` / `retry_start` / `retry_finish` is the
@@ -381,6 +391,7 @@ pub struct BatchReader {
     t: usize,
     chunk_size: usize,
     window: usize,
+    windows: usize,  // window buffers (read_windows_for(depth))
     chunks: Vec<HostBuffer>,
     out: Vec<HostBuffer>,
     present: Vec<Vec<u8>>,
@@ -436,19 +447,21 @@ impl BatchReader {
         let window = parts_per_batch * devices.len().max(1);
         let dev0 = devices.first().copied().unwrap_or(-1);
         let t = data + parity;
+        let r = read_windows_for(depth);
         let bufs = |n: usize| -> Result<Vec<HostBuffer>, CecError> {
-            (0..WINDOWS).map(|_| HostBuffer::zeroed(n, dev0)).collect()
+            (0..r).map(|_| HostBuffer::zeroed(n, dev0)).collect()
         };
         Ok(BatchReader {
             chunks: bufs(window * t * chunk_size)?,
             out: bufs(window * data * chunk_size)?,
-            present: vec![vec![0u8; window * t]; WINDOWS],
-            expected: vec![vec![0u8; window * t * 32]; WINDOWS],
-            verified: vec![vec![0u8; window * t]; WINDOWS],
-            status: vec![vec![0; window]; WINDOWS],
-            cursor: vec![vec![0; window * t]; WINDOWS],
-            exhausted: vec![vec![false; window * t]; WINDOWS],
-            carry: vec![vec![-1; window]; WINDOWS],
+            present: vec![vec![0u8; window * t]; r],
+            expected: vec![vec![0u8; window * t * 32]; r],
+            verified: vec![vec![0u8; window * t]; r],
+            status: vec![vec![0; window]; r],
+            cursor: vec![vec![0; window * t]; r],
+            exhausted: vec![vec![false; window * t]; r],
+            carry: vec![vec![-1; window]; r],
+            windows: r,
             multi,
             codec,
             d: data,
@@ -458,7 +471,7 @@ impl BatchReader {
             retries: 0,
             carried: 0,
             dev0,
-            retry_bufs: (0..WINDOWS).map(|_| RetryBuffers::default()).collect(),
+            retry_bufs: (0..r).map(|_| RetryBuffers::default()).collect(),
         })
     }
 
@@ -495,7 +508,7 @@ impl BatchReader {
         if digests.len() < n_parts * self.t {
             return Err(BatchReadError::Engine(crate::too_small("digests")));
         }
-        let mut live: Vec<Option<LiveRead>> = (0..WINDOWS).map(|_| None).collect();
+        let mut live: Vec<Option<LiveRead>> = (0..self.windows).map(|_| None).collect();
         let res = self.read_windows(n_parts, digests, &mut fetch, &mut sink, &mut live);
         if res.is_err() {
             self.drain(&live);
@@ -510,17 +523,21 @@ impl BatchReader {
         F: FnMut(usize, usize, usize) -> Option<(usize, Vec<u8>)>,
         S: FnMut(usize, &[&[u8]]) -> Result<(), E>,
     {
+        let r = self.windows;
         let mut at = 0usize;
         let mut i = 0usize;
         loop {
-            // windows are emitted in submission order: live[i % WINDOWS] went out WINDOWS steps
-            // ago; the one after it is checked first, so its retry overlaps this step's work
-            if let Some(next) = live[(i + 1) % WINDOWS].as_mut() {
-                if !next.checked {
-                    self.check(next, fetch).map_err(BatchReadError::Engine)?;
+            // windows are emitted in submission order: live[i % r] went out r steps ago; the next
+            // ones are checked first, so their retries run on the GPUs during this step's work
+            // (a retry round costs one SHA-256 chain, ~33 ms for 1 MiB chunks, whatever its size)
+            for a in 1..=checked_ahead(r) {
+                if let Some(next) = live[(i + a) % r].as_mut() {
+                    if !next.checked {
+                        self.check(next, fetch).map_err(BatchReadError::Engine)?;
+                    }
                 }
             }
-            let s = i % WINDOWS;
+            let s = i % r;
             if let Some(w) = live[s].as_mut() {
                 self.finish(w, fetch, sink)?;
             }
@@ -590,7 +607,7 @@ impl BatchReader {
         let status = self.status[slot].as_mut_ptr();
         let carry = self.carry[slot].as_mut_ptr();
         self.multi.submit_read_carry(chunks, present, expected, cnt, out, verified, status,
-                                     std::ptr::null(), carry)
+                                     std::ptr::null(), carry, false)
     }
 
     /// Waits for a window's read job; its failed parts' first retry round goes out.
@@ -747,7 +764,7 @@ impl BatchReader {
         rt.job = unsafe {
             self.multi.submit_read_carry(r_chunks.as_ptr(), rt.r_pres.as_ptr(), rt.r_exp.as_ptr(), g,
                                          r_out.as_mut_ptr(), rt.r_ver.as_mut_ptr(),
-                                         rt.r_status.as_mut_ptr(), rt.r_cin.as_ptr(), carry_out)
+                                         rt.r_status.as_mut_ptr(), rt.r_cin.as_ptr(), carry_out, true)
         }?;
         for s in 0..g {  // submitted: the ids are the job's now
             let r = rt.open[s];

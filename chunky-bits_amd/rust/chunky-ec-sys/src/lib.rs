@@ -51,6 +51,8 @@ pub mod sys {
     /// cec_multi_new_ex job kinds.
     pub const CEC_MULTI_WRITE: std::os::raw::c_uint = 1;
     pub const CEC_MULTI_READ: std::os::raw::c_uint = 2;
+    /// cec_multi_read(_carry) flag: the job goes ahead of the queued jobs not yet started.
+    pub const CEC_MULTI_AHEAD: std::os::raw::c_uint = 64;
     /// Status of a part with fewer than d verified chunks (retry it with more).
     pub const CEC_TOO_FEW_SHARDS_PRESENT: c_int = 10;
 
@@ -1306,7 +1308,9 @@ impl Multi {
     /// reported `TooFewShardsPresent` whose verified chunks its shard kept (-1: none);
     /// `carry_in[k]` (-1: none) hands such an id to the part's retry, whose
     /// `CEC_PRESENT_VERIFIED` chunks then come from that GPU, not from `chunks`.  An id is used
-    /// once; ids that will not be used go back with [`Multi::carry_release`].
+    /// once; ids that will not be used go back with [`Multi::carry_release`].  `ahead`
+    /// (`CEC_MULTI_AHEAD`): the job goes ahead of the queued jobs not yet started -- a reader's
+    /// retry round, which the window being emitted waits for.
     ///
     /// # Safety
     /// As [`Multi::submit_read`]; `carry_in` and `carry_out` (`n_parts` each, either may be
@@ -1323,6 +1327,7 @@ impl Multi {
         status: *mut c_int,
         carry_in: *const i32,
         carry_out: *mut i32,
+        ahead: bool,
     ) -> Result<u64, CecError> {
         let mut job = 0u64;
         check_multi(sys::cec_multi_read_carry(
@@ -1335,7 +1340,7 @@ impl Multi {
             verified,
             status,
             std::ptr::null_mut(),
-            0,
+            if ahead { sys::CEC_MULTI_AHEAD } else { 0 },
             carry_in,
             carry_out,
             &mut job,

@@ -447,8 +447,9 @@ uint64_t cec_pipelines_made(void);
  * slots of parts_per_batch parts.  A job of n parts in file order gives shard g the contiguous
  * range [g*n/G, (g+1)*n/G); every result lands at its part's own position (file order).  Jobs
  * are asynchronous (wait with cec_multi_wait; buffers stay the caller's and must live until
- * then) and run in submission order.  Page-locked caller buffers (cec_host_alloc) are DMA'd
- * directly; others go through the workers' NUMA-local pinned staging. */
+ * then) and run in submission order (CEC_MULTI_AHEAD below excepted).  Page-locked caller
+ * buffers (cec_host_alloc) are DMA'd directly; others go through the workers' NUMA-local pinned
+ * staging. */
 typedef struct cec_multi cec_multi;
 int cec_multi_new(const cec_codec* codec, size_t chunk_len, size_t parts_per_batch, size_t depth,
                   const int* devices, size_t n_devices, cec_multi** out);
@@ -477,6 +478,10 @@ int cec_multi_encode_hash(cec_multi* multi, const uint8_t* data, size_t n_parts,
  * flags = CEC_READ_REBUILT_ONLY: data receives only the rebuilt data chunks and data_ptrs[n*d]
  * (required then; optional otherwise) says where each data chunk of each part is (null for a
  * part that is not CEC_OK when its bytes went through the scheduler's own staging). */
+/* flags |= CEC_MULTI_AHEAD (read and read_carry): the job goes ahead of every queued job that has
+ * not started (behind earlier AHEAD jobs) -- a reader's retry round, a few parts that the window
+ * being emitted waits for, need not wait behind whole windows queued after it. */
+#define CEC_MULTI_AHEAD 64u
 int cec_multi_read(cec_multi* multi, const uint8_t* chunks, const uint8_t* present,
                    const uint8_t* expected, size_t n_parts, uint8_t* data, uint8_t* verified,
                    int* part_status, const uint8_t** data_ptrs, unsigned flags, uint64_t* job);

@@ -27,6 +27,7 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <chrono>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
@@ -325,6 +326,25 @@ inline std::atomic<bool>& read_carry() {
     static std::atomic<bool> on{true};
     return on;
 }
+
+// Where this thread's batched reads spent their time (seconds; tools/cp_bench prints them):
+// loading windows from the store, waiting for read jobs, building and waiting for retry rounds,
+// and in the sink.
+struct ReadTimes {
+    double load = 0, wait_job = 0, retry_build = 0, wait_retry = 0, emit = 0;
+    uint64_t windows = 0, retry_rounds = 0;
+};
+inline ReadTimes& read_times() {
+    thread_local ReadTimes t;
+    return t;
+}
+// Adds the seconds from construction to destruction to `acc`.
+struct Timed {
+    double& acc;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    explicit Timed(double& a) : acc(a) {}
+    ~Timed() { acc += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); }
+};
 
 inline CachedMulti& cached_multi_entry() {
     thread_local CachedMulti e;
@@ -1146,6 +1166,9 @@ struct FileReference {
             // The reference loads d chunks per part (file_part.rs:86-107): the first d that have
             // a copy here (data chunks first: no rebuild when they are all there), each at its
             // first location that reads.
+            detail::ReadTimes& times = detail::read_times();
+            ++times.windows;
+            detail::Timed load_time(times.load);
             detail::parallel_for(cnt, [&](size_t q) {
                 const FilePart& part = parts[k0 + at + q];
                 size_t loaded = 0;
@@ -1176,7 +1199,10 @@ struct FileReference {
         };
         auto check = [&](ReadWindow& w) {
             w.checked = true;
-            detail::check_multi(cec_multi_wait(m, w.job));
+            {
+                detail::Timed wait_time(detail::read_times().wait_job);
+                detail::check_multi(cec_multi_wait(m, w.job));
+            }
             std::vector<size_t> failed;
             for (size_t q = 0; q < w.n; ++q)
                 if (w.status[q] != CEC_OK) failed.push_back(q);
@@ -1187,15 +1213,23 @@ struct FileReference {
             uint8_t* out = w.out.reserve(W * d * L, devs[0]);
             if (w.retry.active) retry_finish(src, m, k0, d, t, L, w, out);
             w.live = false;
+            detail::Timed emit_time(detail::read_times().emit);
             emit(out, w.n * d * L);
         };
+        // windows checked per step beyond the one emitted: those submitted 3 or more steps ago
+        // (their jobs are done or nearly: H2D, a SHA-256 chain, D2H), at least the next one
+        const size_t ahead = R > 4 ? R - 3 : 1;
         try {
             size_t at = 0;
             for (size_t i = 0;; ++i) {
                 // windows are emitted in submission order: win[i % R] was submitted R steps ago;
-                // the one after it is checked first, so its retry overlaps this step's work
-                ReadWindow& next = win[(i + 1) % R];
-                if (next.live && !next.checked) check(next);
+                // the next ones are checked first, so their retries run on the GPUs during this
+                // step and the next ones' work (a retry round costs one SHA-256 chain, ~33 ms
+                // for 1 MiB chunks, whatever its size)
+                for (size_t a = 1; a <= ahead; ++a) {
+                    ReadWindow& next = win[(i + a) % R];
+                    if (next.live && !next.checked) check(next);
+                }
                 ReadWindow& w = win[i % R];
                 if (w.live) finish(w);
                 if (at < n) {
@@ -1275,6 +1309,8 @@ struct FileReference {
                      size_t L, ReadWindow& w) const {
         ReadRetry& r = w.retry;
         const size_t g = r.open.size();
+        ++detail::read_times().retry_rounds;
+        detail::Timed build_time(detail::read_times().retry_build);
         // kept page-locked between retries: fresh zeroed buffers cost ~200 ms of page faults
         // per retry of a dozen RS(10,4) 1 MiB parts (profiles/r6/cp_bench_*.log)
         uint8_t* chunks = r.chunks.reserve(r.f * t * L, -1);
@@ -1316,7 +1352,7 @@ struct FileReference {
         }
         detail::check_multi(cec_multi_read_carry(
             m, chunks, r.present.data(), r.expected.data(), g, r.data.reserve(r.f * d * L, -1),
-            r.verified.data(), r.status.data(), nullptr, 0, r.carry_in.data(),
+            r.verified.data(), r.status.data(), nullptr, CEC_MULTI_AHEAD, r.carry_in.data(),
             detail::read_carry() ? r.carry_out.data() : nullptr, &r.job));
         for (size_t q = 0; q < g; ++q) r.cid[r.open[q]] = -1;  // the job's ids now
         r.g = g;
@@ -1330,7 +1366,10 @@ struct FileReference {
         ReadRetry& r = w.retry;
         while (r.in_flight) {
             r.in_flight = false;
-            detail::check_multi(cec_multi_wait(m, r.job));
+            {
+                detail::Timed wait_time(detail::read_times().wait_retry);
+                detail::check_multi(cec_multi_wait(m, r.job));
+            }
             const uint8_t* data = r.data.reserve(r.f * d * L, -1);
             std::vector<size_t> still;
             for (size_t q = 0; q < r.g; ++q) {

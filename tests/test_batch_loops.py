@@ -83,8 +83,9 @@ class FakeMulti:
         return self._job()
 
     def read(self, chunks, present, expected, n, data, verified, status, rebuilt_only=False,
-             carry_in=None, carry_out=None):
+             carry_in=None, carry_out=None, ahead=False):
         assert self.kinds & self.READ
+        assert ahead == (carry_in is not None)  # the readers' retry rounds, and only they
         self.events.append(("read", n, carry_in is not None))
         d, t, L = self.d, self.t, self.L
         ch = _arr(chunks)[:n * t * L].reshape(n, t, L).copy()
@@ -480,3 +481,23 @@ def test_batch_reader_retry_overlaps_the_next_window(fakes):
     assert ev[:4] == [("read", 4, False), ("read", 4, False), ("read", 1, True),
                       ("read", 4, False)], ev
     assert r.retries == 1 and r.carried_parts == 1 and r.multi.pool == {}
+
+
+def test_batch_reader_checks_windows_three_steps_after_submission(fakes):
+    """At depth 4 the reader keeps 5 windows and checks every window submitted 3 or more steps
+    ago: window 0's retry goes out after windows 1 and 2 were submitted and two steps before
+    window 0 is emitted (a retry round costs one SHA-256 chain whatever its size)."""
+    n = 4 * 7
+    chunks, dig = _store(n, 14)
+    st = Locations(chunks)
+    st.set(1, 0, "bad")   # window 0: part 1 retries
+    st.set(13, 2, "bad")  # window 3: part 13 retries
+    r = br.BatchReader(D, P, L, 4, 4, [0])
+    assert (r.R, r.ahead) == (5, 2)
+    order = []
+    r.read(n, st.fetch, lambda k: dig[k], lambda k, data: order.append(k))
+    assert order == list(range(n))
+    ev = r.multi.events
+    assert ev == [("read", 4, False)] * 3 + [("read", 1, True)] + [("read", 4, False)] * 3 \
+        + [("read", 1, True)] + [("read", 4, False)], ev
+    assert r.retries == 2 and r.multi.pool == {}

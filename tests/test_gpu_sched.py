@@ -377,3 +377,46 @@ def test_scheduler_releases_carry_ids_while_idle():
     assert sum(m.stats(g)["carry_held"] for g in range(2)) == 0
     with pytest.raises(ce.Error):
         m.carry_release(7 << 20)  # no shard 7
+
+
+def test_ahead_job_overtakes_queued_jobs():
+    """CEC_MULTI_AHEAD (a reader's retry round): a read job so flagged goes ahead of the queued
+    jobs that have not started, so it is done while most of eight read jobs submitted before it
+    are still to run; every job's parts are still the stored bytes, and an unknown flag bit is
+    refused."""
+    d, p, L, n, P = 4, 2, 1 << 18, 64, 16
+    t = d + p
+    chunks, dig = make_parts(n, d, p, L, 96)
+    m = ce.Multi(ce.ReedSolomon(d, p), L, P, 2, [0], kinds=ce.Multi.READ)
+    host = ce.HostBuffer(n * t * L, 0)  # page-locked: no staging copy in the timing
+    host.view(n, t, L)[:] = chunks
+    pres = np.zeros((n, t), np.uint8)
+    pres[:, :d] = 1
+    jobs, outs = [], []
+    for _ in range(8):
+        out = np.zeros((n, d, L), np.uint8)
+        ver = np.zeros((n, t), np.uint8)
+        st = np.zeros(n, np.int32)
+        outs.append((out, ver, st))
+        jobs.append(m.read(host.array, pres, dig, n, out, ver, st)[0])
+    a_out = np.zeros((1, d, L), np.uint8)
+    a_ver = np.zeros((1, t), np.uint8)
+    a_st = np.zeros(1, np.int32)
+    aj, _ = m.read(host.array[: t * L], pres[:1], dig[:1], 1, a_out, a_ver, a_st, ahead=True)
+    m.wait(aj)
+    done_then = m.stats(0)["parts"]
+    for j in jobs:
+        m.wait(j)
+    assert done_then < 8 * n - n, done_then  # at least one whole earlier job still to run
+    assert a_st[0] == ce.OK and np.array_equal(a_out[0], chunks[0, :d])
+    for out, ver, st in outs:
+        assert (st == ce.OK).all() and np.array_equal(out, chunks[:, :d])
+    with pytest.raises(ce.MultiError):
+        job = ctypes.c_uint64(0)
+        code = ce._lib.cec_multi_read_carry(m._h, host.array.ctypes.data, pres.ctypes.data,
+                                            dig.ctypes.data, 1, a_out.ctypes.data,
+                                            a_ver.ctypes.data, a_st.ctypes.data_as(
+                                                ctypes.POINTER(ctypes.c_int)), None, 128,
+                                            None, None, ctypes.byref(job))
+        if code != ce.OK:
+            raise ce.MultiError(code)

@@ -116,7 +116,8 @@ def test_part_batch_layout_and_constants_match():
         assert [(t, n) for t, n in cf] == [(t, n) for t, n in rf], struct
     for const in ("CEC_ABI_VERSION", "CEC_READ_REBUILT_ONLY", "CEC_PIPE_EXTERNAL",
                   "CEC_PRESENT_VERIFIED", "CEC_READ_RESILVER", "CEC_READ_VERIFY_ONLY",
-                  "CEC_READ_CARRY", "CEC_SUBMIT_PACKED", "CEC_MULTI_WRITE", "CEC_MULTI_READ"):
+                  "CEC_READ_CARRY", "CEC_SUBMIT_PACKED", "CEC_MULTI_WRITE", "CEC_MULTI_READ",
+                  "CEC_MULTI_AHEAD"):
         cv = re.search(rf"#define {const}\s+(0x[0-9a-fA-F]+|\d+)u?", hsrc).group(1)
         rv = re.search(rf"pub const {const}:[^=]+=\s*(0x[0-9a-fA-F]+|\d+);", rsrc).group(1)
         assert int(cv, 0) == int(rv, 0), const
@@ -182,7 +183,8 @@ def test_batch_reader_mirrors_the_cpp_and_python_loops():
     batch = _crate_sources()["batch.rs"]
     body = batch[batch.index("pub fn read<"):batch.index("    fn load<")]
     order = [body.index(s) for s in ("self.check(next", "self.finish(w", "self.load(", "self.submit(")]
-    assert order == sorted(order) and "(i + 1) % WINDOWS" in body and "self.drain(&live)" in body
+    assert order == sorted(order) and "(i + a) % r" in body and "self.drain(&live)" in body
+    assert "checked_ahead(r)" in body and "read_windows_for(depth)" in batch
     retry = batch[batch.index("    fn retry_start<"):batch.index("    fn drain(&self, live: &[Option<LiveRead>])")]
     for s in ("CEC_PRESENT_VERIFIED", "have + added < d", "TooFewShardsPresent",
               "self.multi.submit_read_carry(", "self.multi.wait(rt.job)"):

@@ -41,6 +41,19 @@ int main(int argc, char** argv) {
     auto secs = [](auto t0) {
         return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     };
+    // where the batched read loop's time went since the last call (detail::read_times)
+    auto times = [] {
+        detail::ReadTimes& t = detail::read_times();
+        char buf[256];
+        std::snprintf(buf, sizeof buf,
+                      "[%llu windows: load %.3f s, wait job %.3f s, %llu retry rounds: build %.3f s, "
+                      "wait %.3f s; sink %.3f s]",
+                      static_cast<unsigned long long>(t.windows), t.load, t.wait_job,
+                      static_cast<unsigned long long>(t.retry_rounds), t.retry_build,
+                      t.wait_retry, t.emit);
+        t = detail::ReadTimes{};
+        return std::string(buf);
+    };
     const auto builder = FileWriteBuilder().chunk_size(chunk).data_chunks(d).parity_chunks(p);
     for (int batched = 1; batched >= 0; --batched) {
         const size_t n = batched ? length : std::min(length, size_t(64) * d * chunk);
@@ -77,12 +90,14 @@ int main(int argc, char** argv) {
         // the same read streamed to a sink (FileReadBuilder's reader, reader.rs:40-75) that
         // discards the bytes, as if written to /dev/null (read() above checked them)
         size_t at = 0;
+        (void)times();
         t0 = std::chrono::steady_clock::now();
         if (batched)
             f.read_to(store, [&](const uint8_t*, size_t m) { at += m; }, 128, 4, devices);
         else
             f.read_to(store, [&](const uint8_t*, size_t m) { at += m; });
         const double r_sink = secs(t0);
+        const std::string r_times = times();
         ok = ok && at == n;
         // resilver (rebuild the two lost chunks of every part and write them back), then verify
         // (every stored chunk hashed)
@@ -109,6 +124,7 @@ int main(int argc, char** argv) {
                     double(n) / w / 1e9, double(n) / w_ram / 1e9,
                     double(n) / r / 1e9, double(n) / r_sink / 1e9, double(n) / rs / 1e9,
                     double(n) / vs / 1e9, ok ? "yes" : "NO");
+        if (batched) std::printf("          read to a sink: %s\n", r_times.c_str());
         std::fflush(stdout);
         if (!ok) return 1;
         if (!batched) continue;
@@ -140,14 +156,18 @@ int main(int argc, char** argv) {
         // alternate, 3 runs each, best of each kept (one run is ~1 s: box noise is ±15 %)
         double best[2] = {0, 0};
         uint64_t sent[2] = {0, 0};
+        std::string best_times[2];
         for (int rep = 0; rep < 3; ++rep)
             for (int carry = 1; carry >= 0; --carry) {
                 detail::read_carry() = carry != 0;
                 const uint64_t u0 = uploaded();
                 size_t got = 0;
+                (void)times();
                 t0 = std::chrono::steady_clock::now();
                 f.read_to(store, [&](const uint8_t*, size_t m) { got += m; }, 128, 4, devices);
-                best[carry] = std::max(best[carry], double(n) / secs(t0) / 1e9);
+                const double rate = double(n) / secs(t0) / 1e9;
+                if (rate > best[carry]) best_times[carry] = times();
+                best[carry] = std::max(best[carry], rate);
                 sent[carry] = uploaded() - u0;
                 ok = ok && got == n;
             }
@@ -157,6 +177,8 @@ int main(int argc, char** argv) {
                         "sent to the GPU, bit-exact %s\n",
                         damage * 100, flipped, carry ? "carry   " : "no carry", best[carry],
                         static_cast<unsigned long long>(sent[carry]), ok ? "yes" : "NO");
+        for (int carry = 1; carry >= 0; --carry)
+            std::printf("          %s: %s\n", carry ? "carry   " : "no carry", best_times[carry].c_str());
         std::fflush(stdout);
         if (!ok) return 1;
         detail::read_carry() = true;
