@@ -147,8 +147,9 @@ class BatchReader:
         try:
             while True:
                 # windows are emitted in submission order: live[i % R] went out R steps ago; the
-                # next ones are checked first, so their retries overlap this step's work
-                for a in range(1, self.ahead + 1):
+                # next ones are checked first, so their retries overlap this step's work; with
+                # nothing left to load, every live window is (the last retries run together)
+                for a in range(1, (self.ahead if at < n_parts else R - 1) + 1):
                     nxt = live[(i + a) % R]
                     if nxt is not None and not nxt.checked:
                         self._check(nxt, fetch)

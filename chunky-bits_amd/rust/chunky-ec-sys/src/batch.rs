@@ -529,8 +529,10 @@ impl BatchReader {
         loop {
             // windows are emitted in submission order: live[i % r] went out r steps ago; the next
             // ones are checked first, so their retries run on the GPUs during this step's work
-            // (a retry round costs one SHA-256 chain, ~33 ms for 1 MiB chunks, whatever its size)
-            for a in 1..=checked_ahead(r) {
+            // (a retry round costs one SHA-256 chain, ~33 ms for 1 MiB chunks, whatever its size);
+            // with nothing left to load, every live window is (the last retries run together)
+            let look = if at < n_parts { checked_ahead(r) } else { r - 1 };
+            for a in 1..=look {
                 if let Some(next) = live[(i + a) % r].as_mut() {
                     if !next.checked {
                         self.check(next, fetch).map_err(BatchReadError::Engine)?;

@@ -1225,8 +1225,9 @@ struct FileReference {
                 // windows are emitted in submission order: win[i % R] was submitted R steps ago;
                 // the next ones are checked first, so their retries run on the GPUs during this
                 // step and the next ones' work (a retry round costs one SHA-256 chain, ~33 ms
-                // for 1 MiB chunks, whatever its size)
-                for (size_t a = 1; a <= ahead; ++a) {
+                // for 1 MiB chunks, whatever its size); with nothing left to load, every live
+                // window is checked, so the last windows' retries run together
+                for (size_t a = 1; a <= (at < n ? ahead : R - 1); ++a) {
                     ReadWindow& next = win[(i + a) % R];
                     if (next.live && !next.checked) check(next);
                 }

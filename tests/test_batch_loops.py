@@ -501,3 +501,20 @@ def test_batch_reader_checks_windows_three_steps_after_submission(fakes):
     assert ev == [("read", 4, False)] * 3 + [("read", 1, True)] + [("read", 4, False)] * 3 \
         + [("read", 1, True)] + [("read", 4, False)], ev
     assert r.retries == 2 and r.multi.pool == {}
+
+
+def test_batch_reader_checks_every_window_once_nothing_is_left_to_load(fakes):
+    """After the last window is submitted every live window is checked at once, so the retries of
+    the last windows go out together instead of one per emitted window."""
+    n = 4 * 5
+    chunks, dig = _store(n, 15)
+    st = Locations(chunks)
+    for k in (9, 13, 17):  # windows 2, 3 and 4
+        st.set(k, 0, "bad")
+    r = br.BatchReader(D, P, L, 4, 4, [0])
+    order = []
+    r.read(n, st.fetch, lambda k: dig[k], lambda k, data: order.append(k))
+    assert order == list(range(n))
+    # windows 0-4 submitted (5 windows, 5 buffers), then at the next step windows 2, 3 and 4
+    # are checked before window 0 is emitted: their three retries back to back
+    assert r.multi.events == [("read", 4, False)] * 5 + [("read", 1, True)] * 3, r.multi.events

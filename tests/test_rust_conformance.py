@@ -184,7 +184,7 @@ def test_batch_reader_mirrors_the_cpp_and_python_loops():
     body = batch[batch.index("pub fn read<"):batch.index("    fn load<")]
     order = [body.index(s) for s in ("self.check(next", "self.finish(w", "self.load(", "self.submit(")]
     assert order == sorted(order) and "(i + a) % r" in body and "self.drain(&live)" in body
-    assert "checked_ahead(r)" in body and "read_windows_for(depth)" in batch
+    assert "checked_ahead(r)" in body and "read_windows_for(depth)" in batch and "r - 1" in body
     retry = batch[batch.index("    fn retry_start<"):batch.index("    fn drain(&self, live: &[Option<LiveRead>])")]
     for s in ("CEC_PRESENT_VERIFIED", "have + added < d", "TooFewShardsPresent",
               "self.multi.submit_read_carry(", "self.multi.wait(rt.job)"):
