@@ -46,6 +46,7 @@
 #include "chunky_ec.h"
 #include "hostmem.hpp"
 #include "knobs.hpp"
+#include "pipeline_internal.hpp"
 
 namespace {
 
@@ -192,6 +193,7 @@ struct Shard {
     Kind active = Kind::Write;
     std::vector<InFlight> wslots, rslots;
     std::deque<size_t> worder, rorder;  // slots in flight, oldest first
+    size_t rnext = 0;                   // read: where the search for a free slot starts
     std::vector<Staging> wstage, rstage;
     std::vector<const uint8_t*> ptrs;  // read: output chunk locations of one batch
     std::vector<int32_t> ids;          // read: carry ids of one batch
@@ -240,15 +242,25 @@ struct cec_multi {
             s.wstage.resize(depth);
         }
         if (kinds & CEC_MULTI_READ) {
-            const int st = cec_read_pipeline_new_ex(codec, L, P, depth,
+            // one slot more than depth (pipelines hold at most 16) kept for CEC_MULTI_AHEAD
+            // batches: a retry round need not wait for a window's batch to free a slot
+            const size_t rd = read_slots();
+            const int st = cec_read_pipeline_new_ex(codec, L, P, rd,
                                                     CEC_PIPE_EXTERNAL | CEC_READ_CARRY, &s.rp);
             if (st != CEC_OK) {
                 err = std::string("read pipeline: ") + cec_pipeline_last_error();
                 return st;
             }
             s.pipelines_made.fetch_add(1);
-            s.rslots.assign(depth, InFlight{});
-            s.rstage.resize(depth);
+            if (rd > depth) {
+                const int pst = cec::read_pipeline_priority_slot(s.rp, depth);
+                if (pst != CEC_OK) {
+                    err = std::string("read pipeline AHEAD slot: ") + cec_pipeline_last_error();
+                    return pst;
+                }
+            }
+            s.rslots.assign(rd, InFlight{});
+            s.rstage.resize(rd);
         }
         return CEC_OK;
     }
@@ -356,22 +368,44 @@ struct cec_multi {
         s.carry_held.store(cec_read_pipeline_carry_held(s.rp), std::memory_order_relaxed);
     }
 
-    // Finish the oldest batch in flight if it is complete; never blocks.  False when it is still
-    // running (or nothing is in flight).
-    bool finish_oldest_if_done(Shard& s) {
-        if (!s.worder.empty()) {
-            const size_t slot = s.worder.front();
-            if (cec_pipeline_query(s.wp, slot) != 1) return false;
-            finish_write(s, slot);
-            return true;
+    size_t read_slots() const { return depth < 16 ? depth + 1 : depth; }
+
+    // Finish every batch in flight that is complete, in any order (a retry round finishes while
+    // older windows' batches still run, and its job completes then); never blocks.
+    void finish_done(Shard& s) {
+        for (size_t i = 0; i < s.worder.size();) {
+            const size_t slot = s.worder[i];
+            if (cec_pipeline_query(s.wp, slot) == 1) finish_write(s, slot);  // erases it
+            else ++i;
         }
-        if (!s.rorder.empty()) {
-            const size_t slot = s.rorder.front();
-            if (cec_read_pipeline_query(s.rp, slot) != 1) return false;
-            finish_read(s, slot);
-            return true;
+        for (size_t i = 0; i < s.rorder.size();) {
+            const size_t slot = s.rorder[i];
+            if (cec_read_pipeline_query(s.rp, slot) == 1) finish_read(s, slot);  // erases it
+            else ++i;
         }
-        return false;
+    }
+
+    // A read slot for the next batch: one with no batch in flight -- the AHEAD slot first for an
+    // AHEAD job, which may also take a depth slot; the others never take the AHEAD slot.  None
+    // free: the complete batches are finished (their jobs complete as soon as their batches
+    // are done, not behind older ones) and the slots polled again 50 us later.
+    int read_slot(Shard& s, bool ahead, size_t* slot, uint8_t** c, uint8_t** pr, uint8_t** ex) {
+        const size_t n = s.rslots.size(), nd = std::min(n, depth);
+        for (;;) {
+            finish_done(s);
+            size_t pick = n;
+            if (ahead && n > nd && !s.rslots[nd].job) pick = nd;
+            for (size_t k = 0; pick == n && k < nd; ++k) {
+                const size_t i = (s.rnext + k) % nd;
+                if (!s.rslots[i].job) pick = i;
+            }
+            if (pick < n) {
+                if (pick < nd) s.rnext = (pick + 1) % nd;
+                *slot = pick;
+                return cec::read_pipeline_acquire_slot(s.rp, pick, c, pr, ex);
+            }
+            std::this_thread::sleep_for(std::chrono::microseconds(50));
+        }
     }
 
     void run_write(Shard& s, Job* job, size_t lo, size_t hi) {
@@ -441,14 +475,11 @@ struct cec_multi {
             const size_t n = std::min(P, count - at);
             size_t slot = 0;
             uint8_t *c = nullptr, *pr = nullptr, *ex = nullptr;
-            // a slot whose batch is done if there is one: a retry job (a few parts, submitted
-            // while the reader's other windows run) need not wait for the oldest of them
-            int st = cec_read_pipeline_acquire_idle(s.rp, &slot, &c, &pr, &ex);
+            int st = read_slot(s, job->ahead, &slot, &c, &pr, &ex);
             if (st != CEC_OK) {
                 finish_parts(job, count - at, st, cec_pipeline_last_error());
                 return;
             }
-            finish_read(s, slot);
             InFlight f;
             f.job = job;
             f.n = n;
@@ -570,8 +601,7 @@ struct cec_multi {
                 // sleep on the queue alone only when nothing is in flight.
                 while (s.queue.empty() && in_flight(s)) {
                     lk.unlock();
-                    while (finish_oldest_if_done(s)) {
-                    }
+                    finish_done(s);
                     lk.lock();
                     if (!s.queue.empty() || !in_flight(s)) break;
                     work_cv.wait_for(lk, std::chrono::microseconds(100));

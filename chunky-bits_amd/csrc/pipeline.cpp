@@ -24,6 +24,7 @@
 #include "chunky_ec.h"
 #include "hostmem.hpp"
 #include "kernels.hpp"
+#include "pipeline_internal.hpp"
 
 namespace {
 
@@ -1031,6 +1032,8 @@ void cec_read_pipeline_free(cec_read_pipeline* pl) { delete pl; }
 
 size_t cec_read_pipeline_depth(const cec_read_pipeline* pl) { return pl ? pl->slots.size() : 0; }
 
+}  // extern "C"
+
 namespace {
 
 int read_acquire(cec_read_pipeline* pl, size_t i, size_t* slot, uint8_t** chunks,
@@ -1049,6 +1052,32 @@ int read_acquire(cec_read_pipeline* pl, size_t i, size_t* slot, uint8_t** chunks
 }
 
 }  // namespace
+
+int cec::read_pipeline_acquire_slot(cec_read_pipeline* pl, size_t slot, uint8_t** chunks,
+                                    uint8_t** present, uint8_t** expected) {
+    if (!pl || slot >= pl->slots.size() || !chunks || !present || !expected)
+        return CEC_ERR_INVALID_ARGUMENT;
+    size_t unused = 0;
+    return read_acquire(pl, slot, &unused, chunks, present, expected);
+}
+
+int cec::read_pipeline_priority_slot(cec_read_pipeline* pl, size_t slot) {
+    if (!pl || slot >= pl->slots.size() || pl->slots[slot].in_flight)
+        return CEC_ERR_INVALID_ARGUMENT;
+    ReadSlot& s = pl->slots[slot];
+    DeviceGuard guard(pl->device);
+    PIPE_TRY(guard.status());
+    int least = 0, greatest = 0;
+    PIPE_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    if (least == greatest) return CEC_OK;
+    hipStream_t high = nullptr;
+    PIPE_TRY(hipStreamCreateWithPriority(&high, hipStreamNonBlocking, greatest));
+    if (s.stream) (void)hipStreamDestroy(s.stream);
+    s.stream = high;
+    return CEC_OK;
+}
+
+extern "C" {
 
 int cec_read_pipeline_acquire(cec_read_pipeline* pl, size_t* slot, uint8_t** chunks,
                               uint8_t** present, uint8_t** expected) {

@@ -1121,7 +1121,8 @@ struct FileReference {
         bool live = false;     // its read job was submitted and its parts not yet emitted
         bool checked = false;  // its read job was waited for (and its retry started)
         detail::PinnedBuf chunks;  // [W][t][L] loaded chunk bytes (DMA'd directly)
-        detail::PinnedBuf out;     // [W][d][L] the parts' data (DMA'd directly)
+        detail::PinnedBuf out;     // [W][d][L] rebuilt data chunks and retried parts' data
+        std::vector<const uint8_t*> ptrs;  // [n][d] where each data chunk of each part is
         std::vector<uint8_t> present, expected, verified, exhausted;
         std::vector<size_t> cursor;  // per chunk: the next location to read
         std::vector<int> status;
@@ -1163,6 +1164,7 @@ struct FileReference {
             w.cursor.assign(cnt * t, 0);
             w.status.assign(cnt, 0);
             w.carry.assign(cnt, -1);
+            w.ptrs.assign(cnt * d, nullptr);
             // The reference loads d chunks per part (file_part.rs:86-107): the first d that have
             // a copy here (data chunks first: no rebuild when they are all there), each at its
             // first location that reads.
@@ -1186,9 +1188,11 @@ struct FileReference {
                     ++loaded;
                 }
             });
+            // REBUILT_ONLY: only the rebuilt data chunks come down; a loaded one is emitted from
+            // the window's chunk buffer it went up from (w.ptrs says which)
             detail::check_multi(cec_multi_read_carry(m, ch, w.present.data(), w.expected.data(),
                                                      cnt, out, w.verified.data(), w.status.data(),
-                                                     nullptr, 0, nullptr,
+                                                     w.ptrs.data(), CEC_READ_REBUILT_ONLY, nullptr,
                                                      detail::read_carry() ? w.carry.data() : nullptr,
                                                      &w.job));
             w.first = at;
@@ -1214,7 +1218,19 @@ struct FileReference {
             if (w.retry.active) retry_finish(src, m, k0, d, t, L, w, out);
             w.live = false;
             detail::Timed emit_time(detail::read_times().emit);
-            emit(out, w.n * d * L);
+            // the parts' data chunks in order, runs of adjacent chunks as one piece
+            const uint8_t* run = nullptr;
+            size_t len = 0;
+            for (const uint8_t* p : w.ptrs) {
+                if (run && p == run + len) {
+                    len += L;
+                    continue;
+                }
+                if (run) emit(run, len);
+                run = p;
+                len = L;
+            }
+            if (run) emit(run, len);
         };
         // windows checked per step beyond the one emitted: those submitted 3 or more steps ago
         // (their jobs are done or nearly: H2D, a SHA-256 chain, D2H), at least the next one
@@ -1377,7 +1393,9 @@ struct FileReference {
                 const size_t j = r.open[q];
                 for (size_t i = 0; i < t; ++i) r.good[j * t + i] = r.verified[q * t + i] != 0;
                 if (r.status[q] == CEC_OK) {
-                    std::memcpy(out + r.failed[j] * d * L, data + q * d * L, d * L);
+                    const size_t part = r.failed[j];
+                    std::memcpy(out + part * d * L, data + q * d * L, d * L);
+                    for (size_t i = 0; i < d; ++i) w.ptrs[part * d + i] = out + (part * d + i) * L;
                 } else {
                     r.cid[j] = r.carry_out[q];
                     still.push_back(j);
