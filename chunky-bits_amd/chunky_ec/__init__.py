@@ -235,6 +235,7 @@ _sig("cec_multi_resilver", [_vp, _vp, _vp, _vp, ctypes.c_size_t, _vp, _vp,
 _sig("cec_multi_verify", [_vp, _vp, _vp, _vp, ctypes.c_size_t, _vp,
                           ctypes.POINTER(ctypes.c_uint64)])
 _sig("cec_multi_wait", [_vp, ctypes.c_uint64])
+_sig("cec_multi_query", [_vp, ctypes.c_uint64])
 _sig("cec_multi_last_error", [], ctypes.c_char_p)
 
 # Status codes (include/chunky_ec.h).
@@ -1073,6 +1074,14 @@ class Multi:
         self._keep.pop(job, None)
         if code != OK:
             raise MultiError(code)
+
+    def query(self, job: int) -> bool:
+        """True when the job is done (wait() then returns at once); never blocks
+        (cec_multi_query)."""
+        code = _lib.cec_multi_query(self._h, job)
+        if code not in (0, 1):
+            raise MultiError(code)
+        return code == 1
 
     def encode_hash_sync(self, data, n_parts: int, parity, digests) -> None:
         self.wait(self.encode_hash(data, n_parts, parity, digests))

@@ -2,7 +2,7 @@
 rule, parts handed out in file order: the Python twin of the Rust crate's
 ``chunky_ec_sys::batch::BatchReader`` / ``read_part`` / ``FileReader``
 (chunky-bits_amd/rust/chunky-ec-sys/src/batch.rs) and of the C++ ``FileReference::read_run`` /
-``retry_start`` / ``retry_finish`` (include/chunky_ec.hpp), step for step, so the loop the Rust side would run is executed
+``retry_start`` / ``retry_collect`` (include/chunky_ec.hpp), step for step, so the loop the Rust side would run is executed
 and tested on the GPU (tests/test_gpu_batchreader.py).
 
 The reference reads a part by drawing chunks until d of them verify (src/file/file_part.rs:
@@ -28,22 +28,25 @@ again; kept on the GPU under the part's carry id), the failed chunks' next copie
 chunks, up to d, until it decodes; a part that runs out of copies fails the read with
 TooFewShardsPresent, as the reference's does.  depth + 1 window buffers (at most 8): a window is
 checked (its job waited for, its failed parts' first retry round queued, ahead of the windows
-queued after it: CEC_MULTI_AHEAD) a step or more before it is emitted, so the retry runs on the
-GPUs while the next windows load.
+queued after it: CEC_MULTI_AHEAD) as soon as its job is done (Multi.query), and each next round
+as soon as the last one is, so retries run on the GPUs while the next windows load.  Only the
+rebuilt data chunks come down (REBUILT_ONLY): a loaded one reaches the sink from the window's
+chunk buffer it went up from.
 :func:`read_part` is the same rule for one part through the per-call API, and :class:`FileReader`
 splits a file into runs of one shape (chunk size, d, p: the short last part has its own chunk size,
 file_part.rs:152) and keeps one BatchReader per shape.
 """
 from __future__ import annotations
 
+import time
 from collections import OrderedDict
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 from typing import Callable, List, Optional, Sequence, Tuple
 
 import numpy as np
 
-from . import (OK, PRESENT_VERIFIED, TOO_FEW_SHARDS_PRESENT, Error, HostBuffer, Multi, ReedSolomon,
-               Sha256Hash)
+from . import (ERR_INVALID_ARGUMENT, OK, PRESENT_VERIFIED, TOO_FEW_SHARDS_PRESENT, Error, HostBuffer,
+               Multi, ReedSolomon, Sha256Hash)
 
 Fetch = Callable[[int, int, int], Optional[Tuple[int, bytes]]]
 
@@ -95,6 +98,8 @@ class _Window:
     n: int
     checked: bool = False                 # its read job waited for (and its retry started)
     retry: Optional[_Retry] = None
+    ptrs: object = None                   # [n*d] where each data chunk is (filled at wait)
+    redone: set = field(default_factory=set)  # parts whose data the retries put in `out`
 
 
 class BatchReader:
@@ -110,10 +115,8 @@ class BatchReader:
         self.d, self.p, self.t, self.L = data, parity, data + parity, chunk_size
         self.window = parts_per_batch * max(len(devices), 1)
         dev0 = devices[0] if devices else -1
-        # window buffers: up to depth windows' read jobs in flight, one being emitted; per step
-        # the windows submitted 3 or more steps ago are checked (at least the next one)
+        # window buffers: up to depth windows' read jobs in flight, one being emitted
         self.R = R = min(max(depth, 2), 7) + 1
-        self.ahead = R - 3 if R > 4 else 1
         W, t, L = self.window, self.t, chunk_size
         self.chunks = [HostBuffer(W * t * L, dev0) for _ in range(R)]
         self.out = [HostBuffer(W * data * L, dev0) for _ in range(R)]
@@ -137,30 +140,28 @@ class BatchReader:
              sink: Callable[[int, List[memoryview]], None]):
         """Parts 0..n_parts-1 (all of this reader's shape): ``fetch(part, chunk, start)`` as the
         module describes, ``digests(part)`` the part's metadata digests [d+p][32]; ``sink(part,
-        data_chunks)`` gets the d data chunks of every part, in file order.  A window is checked
-        (its job waited for, the first round of its failed parts' retry queued) a step or more
-        before it is emitted, so that retry runs beside the loading of the next windows (a retry
-        round costs one SHA-256 chain, ~33 ms for 1 MiB chunks, whatever its size)."""
+        data_chunks)`` gets the d data chunks of every part, in file order.  Every window is
+        checked (its job waited for, the first round of its failed parts' retry queued) as soon as
+        its job is done, and its retry's next round queued as soon as the last one is
+        (Multi.query never blocks), so retries run on the GPUs while windows load and while the
+        loop waits for the window it emits (a retry round costs one SHA-256 chain, ~33 ms for
+        1 MiB chunks, whatever its size)."""
         R = self.R
         live: List[Optional[_Window]] = [None] * R
         at = i = 0
         try:
             while True:
-                # windows are emitted in submission order: live[i % R] went out R steps ago; the
-                # next ones are checked first, so their retries overlap this step's work; with
-                # nothing left to load, every live window is (the last retries run together)
-                for a in range(1, (self.ahead if at < n_parts else R - 1) + 1):
-                    nxt = live[(i + a) % R]
-                    if nxt is not None and not nxt.checked:
-                        self._check(nxt, fetch)
+                # windows are emitted in submission order: live[i % R] went out R steps ago
+                self._poll(live, i + 1, None, at >= n_parts, fetch)
                 s = i % R
                 if live[s] is not None:
-                    self._finish(live[s], fetch, sink)
+                    self._finish(live[s], live, i, at >= n_parts, fetch, sink)
                     live[s] = None
                 if at < n_parts:
                     cnt = min(self.window, n_parts - at)
                     self._load(s, at, cnt, fetch, digests)
-                    live[s] = _Window(s, self._submit(s, cnt), at, cnt)
+                    job, ptrs = self._submit(s, cnt)
+                    live[s] = _Window(s, job, at, cnt, ptrs=ptrs)
                     at += cnt
                 elif all(x is None for x in live):
                     return
@@ -195,11 +196,13 @@ class BatchReader:
                 pres[q, i] = 1
                 loaded += 1
 
-    def _submit(self, slot, cnt) -> int:
-        job, _ = self.multi.read(self.chunks[slot], self.present[slot], self.expected[slot], cnt,
-                                 self.out[slot], self.verified[slot], self.status[slot],
-                                 carry_out=self.carry[slot] if self.use_carry else None)
-        return job
+    def _submit(self, slot, cnt):
+        """REBUILT_ONLY: only the rebuilt data chunks come down; a loaded one is handed to the sink
+        from the window's chunk buffer it went up from.  Returns (job, data pointers)."""
+        return self.multi.read(self.chunks[slot], self.present[slot], self.expected[slot], cnt,
+                               self.out[slot], self.verified[slot], self.status[slot],
+                               rebuilt_only=True,
+                               carry_out=self.carry[slot] if self.use_carry else None)
 
     def _check(self, w: _Window, fetch):
         """Waits for the window's read job; its failed parts' first retry round goes out."""
@@ -210,15 +213,49 @@ class BatchReader:
         if failed:
             self._retry_start(w, failed, fetch)
 
-    def _finish(self, w: _Window, fetch, sink):
-        if not w.checked:
-            self._check(w, fetch)
-        if w.retry is not None:
-            self._retry_finish(w, fetch)
+    def _poll(self, live, first, skip, everything, fetch):
+        """Every live window but `skip`: checked if its job is done, its retry's next round
+        queued if the last one is done; everything: checked whatever its state (nothing is left
+        to load: the last retries run together)."""
+        R = self.R
+        for a in range(R):
+            x = live[(first + a) % R]
+            if x is None or x is skip:
+                continue
+            if not x.checked:
+                if everything or self.multi.query(x.job):
+                    self._check(x, fetch)
+            elif x.retry is not None and x.retry.in_flight and self.multi.query(x.retry.job):
+                self._retry_collect(x, fetch)
+
+    def _finish(self, w: _Window, live, i, everything, fetch, sink):
+        """w's job, then its retry rounds (polling the other windows meanwhile), then its parts
+        to the sink."""
+        while True:
+            if not w.checked and self.multi.query(w.job):
+                self._check(w, fetch)
+            rt = w.retry
+            if w.checked and rt is not None and rt.in_flight and self.multi.query(rt.job):
+                self._retry_collect(w, fetch)
+            if w.checked and (w.retry is None or not w.retry.in_flight):
+                break
+            self._poll(live, i + 1, w, everything, fetch)
+            time.sleep(100e-6)
+        w.retry = None
         d, L = self.d, self.L
-        out = memoryview(self.out[w.slot].array)
+        chb, outb = self.chunks[w.slot], self.out[w.slot]
+        ch, out = memoryview(chb.array), memoryview(outb.array)
+
+        def chunk(q, j):
+            if q in w.redone:
+                return out[(q * d + j) * L:(q * d + j + 1) * L]
+            p = w.ptrs[q * d + j] or 0
+            for base, n, view in ((chb.ptr, chb.nbytes, ch), (outb.ptr, outb.nbytes, out)):
+                if base <= p and p + L <= base + n:
+                    return view[p - base:p - base + L]
+            raise Error(ERR_INVALID_ARGUMENT)  # a data pointer outside the window's buffers
         for q in range(w.n):
-            sink(w.first + q, [out[(q * d + j) * L:(q * d + j + 1) * L] for j in range(d)])
+            sink(w.first + q, [chunk(q, j) for j in range(d)])
 
     def _retry_start(self, w: _Window, failed, fetch):
         """file_part.rs:92-107: the failed parts go again with the chunks that verified
@@ -226,7 +263,7 @@ class BatchReader:
         until each decodes or runs out of copies.  The verified chunks stay on the GPU where the
         scheduler kept them (the part's carry id: only the new chunks are sent), or, when it kept
         none, are sent again from the window's buffer (the bytes that verified).  This queues the
-        first round; _retry_finish waits for it and runs any further rounds."""
+        first round; _retry_collect takes each round's results and queues the next round."""
         t, L = self.t, self.L
         ch = self.chunks[w.slot].view(self.window, t, L)
         pres, ver = self.present[w.slot], self.verified[w.slot]
@@ -306,14 +343,15 @@ class BatchReader:
             rt.cid[q] = -1
         rt.in_flight = True
 
-    def _retry_finish(self, w: _Window, fetch):
-        """Waits for the round in flight; the parts that decoded go to the window's output, the
-        others go again (one round at a time) until every part decodes or runs out of copies."""
+    def _retry_collect(self, w: _Window, fetch):
+        """Waits for the round in flight: the parts that decoded go to the window's output, the
+        others go again in the next round, queued here (until every part decodes or one runs out
+        of copies)."""
         d = self.d
         rt = w.retry
         out = self.out[w.slot].view(self.window, d, self.L)
         _, ro, _ = self._retry_buffers(w.slot, len(rt.failed))
-        while rt.in_flight:
+        if rt.in_flight:
             rt.in_flight = False
             self.multi.wait(rt.job)
             self.retries += len(rt.open_)
@@ -322,13 +360,13 @@ class BatchReader:
                 rt.good[q] = rt.r_ver[s] != 0
                 if rt.r_st[s] == OK:
                     out[q] = ro[s]
+                    w.redone.add(q)
                 else:
                     rt.cid[q] = int(rt.r_cout[s])
                     still.append(q)
             rt.open_ = still
             if still:
                 self._retry_round(w, fetch)
-        w.retry = None
 
     def _drain(self, live) -> None:
         """Error path: no job may still write into the windows; carry ids nobody will use go back

@@ -242,8 +242,9 @@ struct cec_multi {
             s.wstage.resize(depth);
         }
         if (kinds & CEC_MULTI_READ) {
-            // one slot more than depth (pipelines hold at most 16) kept for CEC_MULTI_AHEAD
-            // batches: a retry round need not wait for a window's batch to free a slot
+            // up to 3 slots more than depth (pipelines hold at most 16) kept for CEC_MULTI_AHEAD
+            // batches: a retry round need not wait for a window's batch to free a slot, and the
+            // rounds of several windows run together (each is one SHA-256 chain long)
             const size_t rd = read_slots();
             const int st = cec_read_pipeline_new_ex(codec, L, P, rd,
                                                     CEC_PIPE_EXTERNAL | CEC_READ_CARRY, &s.rp);
@@ -252,8 +253,8 @@ struct cec_multi {
                 return st;
             }
             s.pipelines_made.fetch_add(1);
-            if (rd > depth) {
-                const int pst = cec::read_pipeline_priority_slot(s.rp, depth);
+            for (size_t a = depth; a < rd; ++a) {
+                const int pst = cec::read_pipeline_priority_slot(s.rp, a);
                 if (pst != CEC_OK) {
                     err = std::string("read pipeline AHEAD slot: ") + cec_pipeline_last_error();
                     return pst;
@@ -368,7 +369,7 @@ struct cec_multi {
         s.carry_held.store(cec_read_pipeline_carry_held(s.rp), std::memory_order_relaxed);
     }
 
-    size_t read_slots() const { return depth < 16 ? depth + 1 : depth; }
+    size_t read_slots() const { return std::min<size_t>(depth + 3, 16); }
 
     // Finish every batch in flight that is complete, in any order (a retry round finishes while
     // older windows' batches still run, and its job completes then); never blocks.
@@ -385,8 +386,8 @@ struct cec_multi {
         }
     }
 
-    // A read slot for the next batch: one with no batch in flight -- the AHEAD slot first for an
-    // AHEAD job, which may also take a depth slot; the others never take the AHEAD slot.  None
+    // A read slot for the next batch: one with no batch in flight -- an AHEAD slot first for an
+    // AHEAD job, which may also take a depth slot; the others never take an AHEAD slot.  None
     // free: the complete batches are finished (their jobs complete as soon as their batches
     // are done, not behind older ones) and the slots polled again 50 us later.
     int read_slot(Shard& s, bool ahead, size_t* slot, uint8_t** c, uint8_t** pr, uint8_t** ex) {
@@ -394,7 +395,8 @@ struct cec_multi {
         for (;;) {
             finish_done(s);
             size_t pick = n;
-            if (ahead && n > nd && !s.rslots[nd].job) pick = nd;
+            for (size_t a = nd; ahead && pick == n && a < n; ++a)
+                if (!s.rslots[a].job) pick = a;
             for (size_t k = 0; pick == n && k < nd; ++k) {
                 const size_t i = (s.rnext + k) % nd;
                 if (!s.rslots[i].job) pick = i;
@@ -891,6 +893,14 @@ int cec_multi_wait(cec_multi* m, uint64_t job) {
     if (st != CEC_OK) g_multi_error = j->error;
     m->jobs.erase(it);
     return st;
+}
+
+int cec_multi_query(cec_multi* m, uint64_t job) {
+    if (!m) return CEC_ERR_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> lk(m->mu);
+    auto it = m->jobs.find(job);
+    if (it == m->jobs.end()) return CEC_ERR_INVALID_ARGUMENT;
+    return it->second->remaining == 0 ? 1 : 0;
 }
 
 }  // extern "C"

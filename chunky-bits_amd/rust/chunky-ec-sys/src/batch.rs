@@ -295,12 +295,6 @@ fn read_windows_for(depth: usize) -> usize {
     depth.clamp(2, 7) + 1
 }
 
-/// Windows checked per step beyond the one emitted: those submitted 3 or more steps ago (their
-/// jobs are done or nearly: upload, a SHA-256 chain, download), at least the next one.
-fn checked_ahead(windows: usize) -> usize {
-    if windows > 4 { windows - 3 } else { 1 }
-}
-
 /// A read window submitted to the scheduler and not yet handed to the sink.
 struct LiveRead {
     slot: usize,
@@ -380,7 +374,7 @@ fn draw_order(good: &[bool], tried: &[bool], exhausted: &[bool]) -> Vec<usize> {
 /// loading of the next windows.  So a chunk listed `[bad, good]` -- what resilver leaves when it appends a rebuilt
 /// copy's location (file_part.rs:346) -- reads as in the reference.  [`FileReader`] splits a file
 /// into runs of one shape (the short last part has its own chunk size).
-/// `include/chunky_ec.hpp`'s `FileReference::read_run` / `retry_start` / `retry_finish` is the
+/// `include/chunky_ec.hpp`'s `FileReference::read_run` / `retry_start` / `retry_collect` is the
 /// same loop in C++ and `chunky-bits_amd/chunky_ec/batchreader.py` its Python twin; both are
 /// tested on the GPU.
 pub struct BatchReader {
@@ -403,6 +397,11 @@ pub struct BatchReader {
     exhausted: Vec<Vec<bool>>,
     // per part of a window: the scheduler's carry id of its verified chunks (-1: none kept)
     carry: Vec<Vec<i32>>,
+    // per data chunk of a window: its address (`CEC_READ_REBUILT_ONLY`: in the window's chunk
+    // buffer where it was loaded, else in its output), and per part whether a retry rebuilt it
+    // into the output
+    ptrs: Vec<Vec<usize>>,
+    redone: Vec<Vec<bool>>,
     retries: u64,
     carried: u64,
     dev0: c_int,
@@ -417,6 +416,12 @@ struct RetryBuffers {
     chunks: Option<HostBuffer>,
     out: Option<HostBuffer>,
     keep: Vec<u8>,
+}
+
+/// The `len` bytes at address `addr` if they lie inside `buf`.
+fn window_slice(buf: &[u8], addr: usize, len: usize) -> Option<&[u8]> {
+    let off = addr.checked_sub(buf.as_ptr() as usize)?;
+    buf.get(off..off.checked_add(len)?)
 }
 
 /// `buf` grown to at least `n` bytes (page-locked on `dev`'s node), its first `n` bytes.
@@ -461,6 +466,8 @@ impl BatchReader {
             cursor: vec![vec![0; window * t]; r],
             exhausted: vec![vec![false; window * t]; r],
             carry: vec![vec![-1; window]; r],
+            ptrs: vec![vec![0usize; window * data]; r],
+            redone: vec![vec![false; window]; r],
             windows: r,
             multi,
             codec,
@@ -527,23 +534,15 @@ impl BatchReader {
         let mut at = 0usize;
         let mut i = 0usize;
         loop {
-            // windows are emitted in submission order: live[i % r] went out r steps ago; the next
-            // ones are checked first, so their retries run on the GPUs during this step's work
-            // (a retry round costs one SHA-256 chain, ~33 ms for 1 MiB chunks, whatever its size);
-            // with nothing left to load, every live window is (the last retries run together)
-            let look = if at < n_parts { checked_ahead(r) } else { r - 1 };
-            for a in 1..=look {
-                if let Some(next) = live[(i + a) % r].as_mut() {
-                    if !next.checked {
-                        self.check(next, fetch).map_err(BatchReadError::Engine)?;
-                    }
+            // windows are emitted in submission order: live[i % r] went out r steps ago
+            self.poll(live, i + 1, at >= n_parts, fetch).map_err(BatchReadError::Engine)?;
+            let s = i % r;
+            if let Some(mut w) = live[s].take() {
+                if let Err(e) = self.finish(&mut w, live, i, at >= n_parts, fetch, sink) {
+                    live[s] = Some(w);  // drained by the caller
+                    return Err(e);
                 }
             }
-            let s = i % r;
-            if let Some(w) = live[s].as_mut() {
-                self.finish(w, fetch, sink)?;
-            }
-            live[s] = None;
             if at < n_parts {
                 let cnt = self.window.min(n_parts - at);
                 self.load(s, at, cnt, digests, fetch);
@@ -569,6 +568,9 @@ impl BatchReader {
         let exp = &mut self.expected[slot];
         let cur = &mut self.cursor[slot];
         let ex = &mut self.exhausted[slot];
+        for x in self.redone[slot].iter_mut().take(cnt) {
+            *x = false;
+        }
         for c in self.carry[slot].iter_mut().take(cnt) {
             *c = -1;
         }
@@ -596,7 +598,9 @@ impl BatchReader {
         }
     }
 
-    /// Queues the verify + rebuild of the first `cnt` parts of window `slot`.
+    /// Queues the verify + rebuild of the first `cnt` parts of window `slot`.  Only the rebuilt
+    /// data chunks come down (`CEC_READ_REBUILT_ONLY`): a loaded one is handed to the sink from
+    /// the window's chunk buffer it went up from, `ptrs` says which.
     ///
     /// # Safety
     /// The window's buffers are not touched again until the job is collected or drained.
@@ -608,8 +612,10 @@ impl BatchReader {
         let verified = self.verified[slot].as_mut_ptr();
         let status = self.status[slot].as_mut_ptr();
         let carry = self.carry[slot].as_mut_ptr();
+        // usize and a data pointer have one size and layout: the C side writes addresses
+        let ptrs = self.ptrs[slot].as_mut_ptr() as *mut *const u8;
         self.multi.submit_read_carry(chunks, present, expected, cnt, out, verified, status,
-                                     std::ptr::null(), carry, false)
+                                     std::ptr::null(), carry, ptrs, false)
     }
 
     /// Waits for a window's read job; its failed parts' first retry round goes out.
@@ -626,22 +632,80 @@ impl BatchReader {
         Ok(())
     }
 
-    /// Finishes a window's retry (if any), then hands its parts to the sink.
-    fn finish<F, S, E>(&mut self, w: &mut LiveRead, fetch: &mut F, sink: &mut S) -> Result<(), BatchReadError<E>>
+    /// Every live window: checked as soon as its job is done and its retry's next round queued
+    /// as soon as the last one is (`Multi::query` never blocks), so retries run on the GPUs while
+    /// windows load and while the loop waits for the window it emits (a retry round costs one
+    /// SHA-256 chain, ~33 ms for 1 MiB chunks, whatever its size).  `everything`: checked
+    /// whatever its state (nothing is left to load: the last retries run together).
+    fn poll<F>(&mut self, live: &mut [Option<LiveRead>], first: usize, everything: bool,
+               fetch: &mut F) -> Result<(), CecError>
+    where
+        F: FnMut(usize, usize, usize) -> Option<(usize, Vec<u8>)>,
+    {
+        let r = live.len();
+        for a in 0..r {
+            if let Some(x) = live[(first + a) % r].as_mut() {
+                if !x.checked {
+                    if everything || self.multi.query(x.job)? {
+                        self.check(x, fetch)?;
+                    }
+                } else if let Some(job) = x.retry.as_ref().filter(|rt| rt.in_flight).map(|rt| rt.job) {
+                    if self.multi.query(job)? {
+                        self.retry_collect(x, fetch)?;
+                    }
+                }
+            }
+        }
+        Ok(())
+    }
+
+    /// Window `w` (taken out of `live`): its job, then its retry rounds, polling the other
+    /// windows meanwhile; then its parts to the sink.
+    #[allow(clippy::too_many_arguments)]
+    fn finish<F, S, E>(&mut self, w: &mut LiveRead, live: &mut [Option<LiveRead>], i: usize,
+                       everything: bool, fetch: &mut F, sink: &mut S) -> Result<(), BatchReadError<E>>
     where
         F: FnMut(usize, usize, usize) -> Option<(usize, Vec<u8>)>,
         S: FnMut(usize, &[&[u8]]) -> Result<(), E>,
     {
-        if !w.checked {
-            self.check(w, fetch).map_err(BatchReadError::Engine)?;
+        loop {
+            if !w.checked && self.multi.query(w.job).map_err(BatchReadError::Engine)? {
+                self.check(w, fetch).map_err(BatchReadError::Engine)?;
+            }
+            if w.checked {
+                if let Some(job) = w.retry.as_ref().filter(|rt| rt.in_flight).map(|rt| rt.job) {
+                    if self.multi.query(job).map_err(BatchReadError::Engine)? {
+                        self.retry_collect(w, fetch).map_err(BatchReadError::Engine)?;
+                    }
+                }
+            }
+            let in_flight = w.retry.as_ref().map_or(false, |rt| rt.in_flight);
+            if w.checked && !in_flight {
+                break;
+            }
+            self.poll(live, i + 1, everything, fetch).map_err(BatchReadError::Engine)?;
+            std::thread::sleep(std::time::Duration::from_micros(100));
         }
-        if w.retry.is_some() {
-            self.retry_finish(w, fetch).map_err(BatchReadError::Engine)?;
-        }
+        w.retry = None;
         let (d, l) = (self.d, self.chunk_size);
         let out: &[u8] = &self.out[w.slot];
+        let ch: &[u8] = &self.chunks[w.slot];
         for q in 0..w.n {
-            let data: Vec<&[u8]> = (0..d).map(|j| &out[(q * d + j) * l..(q * d + j + 1) * l]).collect();
+            let mut data: Vec<&[u8]> = Vec::with_capacity(d);
+            for j in 0..d {
+                // a retried part's data is in the output at its place; otherwise the chunk is
+                // where the job said (an address inside the chunk buffer or the output)
+                let bytes = if self.redone[w.slot][q] {
+                    out.get((q * d + j) * l..(q * d + j + 1) * l)
+                } else {
+                    let p = self.ptrs[w.slot][q * d + j];
+                    window_slice(ch, p, l).or_else(|| window_slice(out, p, l))
+                };
+                match bytes {
+                    Some(b) => data.push(b),
+                    None => return Err(BatchReadError::Engine(crate::too_small("data pointer"))),
+                }
+            }
             sink(w.first + q, &data).map_err(BatchReadError::Sink)?;
         }
         Ok(())
@@ -652,7 +716,7 @@ impl BatchReader {
     /// kept none, sent again from the window's buffer: the bytes that verified) plus, up to d, the
     /// failed chunks' next copies and then untried chunks, until each decodes; a part with no copy
     /// left fails the read (its and the other open parts' carry ids go back, `drain`).  This
-    /// queues the first round; `retry_finish` waits for it and runs any further rounds.
+    /// queues the first round; `retry_collect` takes each round's results and queues the next.
     fn retry_start<F>(&mut self, w: &mut LiveRead, failed: Vec<usize>, fetch: &mut F) -> Result<(), CecError>
     where
         F: FnMut(usize, usize, usize) -> Option<(usize, Vec<u8>)>,
@@ -766,7 +830,8 @@ impl BatchReader {
         rt.job = unsafe {
             self.multi.submit_read_carry(r_chunks.as_ptr(), rt.r_pres.as_ptr(), rt.r_exp.as_ptr(), g,
                                          r_out.as_mut_ptr(), rt.r_ver.as_mut_ptr(),
-                                         rt.r_status.as_mut_ptr(), rt.r_cin.as_ptr(), carry_out, true)
+                                         rt.r_status.as_mut_ptr(), rt.r_cin.as_ptr(), carry_out,
+                                         std::ptr::null_mut(), true)
         }?;
         for s in 0..g {  // submitted: the ids are the job's now
             let r = rt.open[s];
@@ -780,18 +845,19 @@ impl BatchReader {
         Ok(())
     }
 
-    /// Waits for the round in flight; the parts that decoded go to the window's output, the
-    /// others go again (one round at a time) until every part decodes or one runs out of copies.
-    fn retry_finish<F>(&mut self, w: &mut LiveRead, fetch: &mut F) -> Result<(), CecError>
+    /// Waits for the round in flight: the parts that decoded go to the window's output, the
+    /// others go again in the next round, queued here (until every part decodes or one runs out
+    /// of copies).
+    fn retry_collect<F>(&mut self, w: &mut LiveRead, fetch: &mut F) -> Result<(), CecError>
     where
         F: FnMut(usize, usize, usize) -> Option<(usize, Vec<u8>)>,
     {
         let (d, t, l) = (self.d, self.t, self.chunk_size);
-        loop {
+        {
             let again = {
                 let rt = match w.retry.as_mut() {
                     Some(rt) if rt.in_flight => rt,
-                    _ => break,
+                    _ => return Ok(()),
                 };
                 rt.in_flight = false;
                 self.multi.wait(rt.job)?;
@@ -810,6 +876,7 @@ impl BatchReader {
                     }
                     if rt.r_status[s] == 0 {
                         out[q * d * l..(q + 1) * d * l].copy_from_slice(&r_out[s * d * l..(s + 1) * d * l]);
+                        self.redone[w.slot][q] = true;
                     } else if rt.r_status[s] == crate::sys::CEC_TOO_FEW_SHARDS_PRESENT {
                         rt.cid[r] = rt.r_cout[s];
                         still.push(r);
@@ -824,7 +891,6 @@ impl BatchReader {
                 self.retry_round(w, fetch)?;
             }
         }
-        w.retry = None;
         Ok(())
     }
 

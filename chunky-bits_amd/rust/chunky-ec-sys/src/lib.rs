@@ -424,6 +424,7 @@ pub mod sys {
             job: *mut u64,
         ) -> c_int;
         pub fn cec_multi_wait(multi: *mut cec_multi, job: u64) -> c_int;
+        pub fn cec_multi_query(multi: *mut cec_multi, job: u64) -> c_int;
         pub fn cec_multi_last_error() -> *const std::os::raw::c_char;
         pub fn cec_fill_synthetic(
             batch: *const cec_part_batch,
@@ -1308,13 +1309,16 @@ impl Multi {
     /// reported `TooFewShardsPresent` whose verified chunks its shard kept (-1: none);
     /// `carry_in[k]` (-1: none) hands such an id to the part's retry, whose
     /// `CEC_PRESENT_VERIFIED` chunks then come from that GPU, not from `chunks`.  An id is used
-    /// once; ids that will not be used go back with [`Multi::carry_release`].  `ahead`
+    /// once; ids that will not be used go back with [`Multi::carry_release`].  `data_ptrs`
+    /// (`n_parts * d` entries, nullable): `CEC_READ_REBUILT_ONLY` -- only the rebuilt data chunks
+    /// come back into `data`, and `data_ptrs[k * d + j]` receives, at [`Multi::wait`], where data
+    /// chunk j of part k is (in `chunks` where it was loaded, else in `data`).  `ahead`
     /// (`CEC_MULTI_AHEAD`): the job goes ahead of the queued jobs not yet started -- a reader's
     /// retry round, which the window being emitted waits for.
     ///
     /// # Safety
-    /// As [`Multi::submit_read`]; `carry_in` and `carry_out` (`n_parts` each, either may be
-    /// null) must stay valid until the job has been waited for.
+    /// As [`Multi::submit_read`]; `carry_in`, `carry_out` (`n_parts` each) and `data_ptrs`, any of
+    /// them null, must stay valid until the job has been waited for.
     #[allow(clippy::too_many_arguments)]
     pub unsafe fn submit_read_carry(
         &self,
@@ -1327,9 +1331,11 @@ impl Multi {
         status: *mut c_int,
         carry_in: *const i32,
         carry_out: *mut i32,
+        data_ptrs: *mut *const u8,
         ahead: bool,
     ) -> Result<u64, CecError> {
         let mut job = 0u64;
+        let rebuilt_only = if data_ptrs.is_null() { 0 } else { sys::CEC_READ_REBUILT_ONLY };
         check_multi(sys::cec_multi_read_carry(
             self.raw,
             chunks,
@@ -1339,8 +1345,8 @@ impl Multi {
             data,
             verified,
             status,
-            std::ptr::null_mut(),
-            if ahead { sys::CEC_MULTI_AHEAD } else { 0 },
+            data_ptrs,
+            rebuilt_only | if ahead { sys::CEC_MULTI_AHEAD } else { 0 },
             carry_in,
             carry_out,
             &mut job,
@@ -1447,6 +1453,16 @@ impl Multi {
     /// Waits for a job queued with one of the `submit_*` calls.
     pub fn wait(&self, job: u64) -> Result<(), CecError> {
         check_multi(unsafe { sys::cec_multi_wait(self.raw, job) })
+    }
+
+    /// Whether a job is done ([`Multi::wait`] then returns at once); never blocks
+    /// (`cec_multi_query`).
+    pub fn query(&self, job: u64) -> Result<bool, CecError> {
+        match unsafe { sys::cec_multi_query(self.raw, job) } {
+            0 => Ok(false),
+            1 => Ok(true),
+            code => Err(check_multi(code).err().unwrap_or_else(|| crate::too_small("query"))),
+        }
     }
 }
 

@@ -530,6 +530,10 @@ int cec_multi_verify(cec_multi* multi, const uint8_t* chunks, const uint8_t* pre
                      const uint8_t* expected, size_t n_parts, uint8_t* verified, uint64_t* job);
 /* Blocks until the job is done; returns its first error (message: cec_multi_last_error). */
 int cec_multi_wait(cec_multi* multi, uint64_t job);
+/* Never blocks: 1 when the job is done (cec_multi_wait then returns at once), 0 while it runs;
+ * CEC_ERR_INVALID_ARGUMENT for a job not submitted or already waited for.  A reader polls its
+ * windows' jobs with it, so a window's retry starts as soon as its job is done. */
+int cec_multi_query(cec_multi* multi, uint64_t job);
 const char* cec_multi_last_error(void);
 
 /* ---------------------------------------------------------------------------------------- */

@@ -332,7 +332,7 @@ inline std::atomic<bool>& read_carry() {
 // and in the sink.
 struct ReadTimes {
     double load = 0, wait_job = 0, retry_build = 0, wait_retry = 0, emit = 0;
-    uint64_t windows = 0, retry_rounds = 0;
+    uint64_t windows = 0, retry_rounds = 0, retry_parts = 0, later_rounds = 0;
 };
 inline ReadTimes& read_times() {
     thread_local ReadTimes t;
@@ -1203,19 +1203,43 @@ struct FileReference {
         };
         auto check = [&](ReadWindow& w) {
             w.checked = true;
-            {
-                detail::Timed wait_time(detail::read_times().wait_job);
-                detail::check_multi(cec_multi_wait(m, w.job));
-            }
+            detail::check_multi(cec_multi_wait(m, w.job));
             std::vector<size_t> failed;
             for (size_t q = 0; q < w.n; ++q)
                 if (w.status[q] != CEC_OK) failed.push_back(q);
             if (!failed.empty()) retry_start(src, m, k0, d, t, L, w, std::move(failed));
         };
-        auto finish = [&](ReadWindow& w) {
-            if (!w.checked) check(w);
+        // Every live window but `skip`: checked as soon as its job is done and its retry's next
+        // round queued as soon as the last one is (cec_multi_query never blocks), so retries run
+        // on the GPUs while windows load and while the loop waits for another window (a round
+        // costs one SHA-256 chain, ~33 ms for 1 MiB chunks, whatever its size).  all: check every
+        // window whatever its state (nothing is left to load: the last retries run together).
+        size_t at = 0;
+        auto poll = [&](size_t first, const ReadWindow* skip, bool all) {
+            for (size_t a = 0; a < R; ++a) {
+                ReadWindow& x = win[(first + a) % R];
+                if (!x.live || &x == skip) continue;
+                if (!x.checked) {
+                    if (all || cec_multi_query(m, x.job) == 1) check(x);
+                } else if (x.retry.in_flight && cec_multi_query(m, x.retry.job) == 1) {
+                    retry_collect(src, m, k0, d, t, L, x, x.out.reserve(W * d * L, devs[0]));
+                }
+            }
+        };
+        auto finish = [&](ReadWindow& w, size_t i) {
             uint8_t* out = w.out.reserve(W * d * L, devs[0]);
-            if (w.retry.active) retry_finish(src, m, k0, d, t, L, w, out);
+            // w's job, then its retry rounds, polling the other windows meanwhile
+            detail::ReadTimes& times = detail::read_times();
+            for (;;) {
+                if (!w.checked && cec_multi_query(m, w.job) == 1) check(w);
+                if (w.checked && w.retry.in_flight && cec_multi_query(m, w.retry.job) == 1)
+                    retry_collect(src, m, k0, d, t, L, w, out);
+                if (w.checked && !w.retry.in_flight) break;
+                detail::Timed waited(w.checked ? times.wait_retry : times.wait_job);
+                poll(i + 1, &w, at >= n);
+                std::this_thread::sleep_for(std::chrono::microseconds(100));
+            }
+            w.retry.active = false;
             w.live = false;
             detail::Timed emit_time(detail::read_times().emit);
             // the parts' data chunks in order, runs of adjacent chunks as one piece
@@ -1232,23 +1256,12 @@ struct FileReference {
             }
             if (run) emit(run, len);
         };
-        // windows checked per step beyond the one emitted: those submitted 3 or more steps ago
-        // (their jobs are done or nearly: H2D, a SHA-256 chain, D2H), at least the next one
-        const size_t ahead = R > 4 ? R - 3 : 1;
         try {
-            size_t at = 0;
             for (size_t i = 0;; ++i) {
-                // windows are emitted in submission order: win[i % R] was submitted R steps ago;
-                // the next ones are checked first, so their retries run on the GPUs during this
-                // step and the next ones' work (a retry round costs one SHA-256 chain, ~33 ms
-                // for 1 MiB chunks, whatever its size); with nothing left to load, every live
-                // window is checked, so the last windows' retries run together
-                for (size_t a = 1; a <= (at < n ? ahead : R - 1); ++a) {
-                    ReadWindow& next = win[(i + a) % R];
-                    if (next.live && !next.checked) check(next);
-                }
+                // windows are emitted in submission order: win[i % R] was submitted R steps ago
+                poll(i + 1, nullptr, at >= n);
                 ReadWindow& w = win[i % R];
-                if (w.live) finish(w);
+                if (w.live) finish(w, i);
                 if (at < n) {
                     const size_t cnt = std::min(W, n - at);
                     submit(w, at, cnt);
@@ -1282,13 +1295,14 @@ struct FileReference {
     // they decode or no copy is left (TooFewShardsPresent, as the reference's read).  The
     // verified chunks of a part the scheduler kept on its GPU (its carry id) are not sent again;
     // the others are re-sent from their verified copies.  retry_start queues the first round;
-    // retry_finish waits for it and runs any further rounds, the rebuilt data of window part q
-    // going to out + q*d*L.
+    // retry_collect takes a round's results (the rebuilt data of window part q going to
+    // out + q*d*L) and queues the next round for the parts still short of d.
     void retry_start(const ChunkStore& src, cec_multi* m, size_t k0, size_t d, size_t t,
                      size_t L, ReadWindow& w, std::vector<size_t> failed) const {
         ReadRetry& r = w.retry;
         const size_t f = failed.size();
         r.f = f;
+        r.g = 0;  // no round yet
         r.failed = std::move(failed);
         r.tried.assign(f * t, 0);
         r.good.assign(f * t, 0);
@@ -1327,6 +1341,8 @@ struct FileReference {
         ReadRetry& r = w.retry;
         const size_t g = r.open.size();
         ++detail::read_times().retry_rounds;
+        detail::read_times().retry_parts += g;
+        if (g && r.g) ++detail::read_times().later_rounds;  // a round after the first
         detail::Timed build_time(detail::read_times().retry_build);
         // kept page-locked between retries: fresh zeroed buffers cost ~200 ms of page faults
         // per retry of a dozen RS(10,4) 1 MiB parts (profiles/r6/cp_bench_*.log)
@@ -1376,17 +1392,14 @@ struct FileReference {
         r.in_flight = true;
     }
 
-    // Waits for the round in flight; the parts that decoded go to out, the others go again
-    // (one round at a time) until every part decodes or one runs out of copies.
-    void retry_finish(const ChunkStore& src, cec_multi* m, size_t k0, size_t d, size_t t,
-                      size_t L, ReadWindow& w, uint8_t* out) const {
+    // Waits for the round in flight: the parts that decoded go to out, the others go again in
+    // the next round, queued here.
+    void retry_collect(const ChunkStore& src, cec_multi* m, size_t k0, size_t d, size_t t,
+                       size_t L, ReadWindow& w, uint8_t* out) const {
         ReadRetry& r = w.retry;
-        while (r.in_flight) {
+        {
             r.in_flight = false;
-            {
-                detail::Timed wait_time(detail::read_times().wait_retry);
-                detail::check_multi(cec_multi_wait(m, r.job));
-            }
+            detail::check_multi(cec_multi_wait(m, r.job));
             const uint8_t* data = r.data.reserve(r.f * d * L, -1);
             std::vector<size_t> still;
             for (size_t q = 0; q < r.g; ++q) {
@@ -1403,8 +1416,8 @@ struct FileReference {
             }
             r.open.swap(still);
             if (!r.open.empty()) retry_round(src, m, k0, d, t, L, w);
+            else r.active = false;
         }
-        r.active = false;
     }
 };
 

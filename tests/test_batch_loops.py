@@ -64,6 +64,10 @@ class FakeMulti:
     def carry_release(self, cid):
         del self.pool[int(cid)]
 
+    def query(self, job):
+        assert job in self.live  # a job not submitted or already waited for is refused
+        return True  # the oracle computed it at submission
+
     def _job(self):
         j = next(self.ids)
         self.live.add(j)
@@ -94,6 +98,10 @@ class FakeMulti:
         out = _arr(data)[:n * d * L].reshape(n, d, L)
         ver = np.asarray(verified).reshape(-1, t)
         st = np.asarray(status)
+        # REBUILT_ONLY: only rebuilt data chunks land in `data`; ptrs[k*d + j] says where each
+        # data chunk is (a loaded one where the caller's buffer holds it)
+        ptrs = [None] * (n * d) if rebuilt_only else None
+        base_ch, base_out = _arr(chunks).ctypes.data, _arr(data).ctypes.data
         for k in range(n):
             cid = -1 if carry_in is None else int(carry_in[k])
             if cid >= 0:  # the entry replaces the part's verified chunks
@@ -125,9 +133,18 @@ class FakeMulti:
             code, rec = oracle.reconstruct(d, self.p, [ch[k, i].copy() if ver[k, i] else None
                                                        for i in range(t)], data_only=True)
             assert code == 0
-            out[k] = np.stack(rec[:d])
+            redone = any(pres[k, i] and not ver[k, i] for i in range(t))
+            for j in range(d):
+                in_place = (rebuilt_only and not redone and pres[k, j]
+                            and not (cid >= 0 and pres[k, j] == PRESENT_VERIFIED))
+                if in_place:
+                    ptrs[k * d + j] = base_ch + (k * t + j) * L
+                else:
+                    out[k, j] = rec[j]
+                    if rebuilt_only:
+                        ptrs[k * d + j] = base_out + (k * d + j) * L
             st[k] = OK
-        return self._job(), None
+        return self._job(), ptrs
 
     def _verify_flags(self, ch, pres, exp, ver, n):
         for k in range(n):
@@ -464,10 +481,10 @@ def test_checker_resilver_rebuilds_only_chunks_without_a_valid_copy(fakes):
 
 
 def test_batch_reader_retry_overlaps_the_next_window(fakes):
-    """A window's failed parts go out again (their first retry round) when the window is
-    checked, one step before it is emitted: after the window behind it was submitted and before
-    the next window is loaded, so the retry runs beside that loading instead of stalling the
-    loop; the parts still reach the sink in file order."""
+    """A window's failed parts go out again (their first retry round) as soon as its job is
+    done (Multi.query; the fake's jobs are done at once): before the next window is loaded, so
+    the retry runs beside that loading instead of stalling the loop; the parts still reach the
+    sink in file order."""
     n = 4 * 3
     chunks, dig = _store(n, 12)
     st = Locations(chunks)
@@ -477,35 +494,35 @@ def test_batch_reader_retry_overlaps_the_next_window(fakes):
     r.read(n, st.fetch, lambda k: dig[k], lambda k, data: order.append(("emit", k)))
     assert [k for _, k in order] == list(range(n))
     ev = r.multi.events
-    # windows 0 and 1 submitted, then window 0's retry, then window 2
-    assert ev[:4] == [("read", 4, False), ("read", 4, False), ("read", 1, True),
+    # window 0, its retry, then windows 1 and 2
+    assert ev[:4] == [("read", 4, False), ("read", 1, True), ("read", 4, False),
                       ("read", 4, False)], ev
     assert r.retries == 1 and r.carried_parts == 1 and r.multi.pool == {}
 
 
-def test_batch_reader_checks_windows_three_steps_after_submission(fakes):
-    """At depth 4 the reader keeps 5 windows and checks every window submitted 3 or more steps
-    ago: window 0's retry goes out after windows 1 and 2 were submitted and two steps before
-    window 0 is emitted (a retry round costs one SHA-256 chain whatever its size)."""
+def test_batch_reader_checks_windows_as_soon_as_their_jobs_are_done(fakes):
+    """At depth 4 the reader keeps 5 windows and checks each as soon as its job is done: window
+    0's retry goes out before window 1 is loaded, four steps before window 0 is emitted (a retry
+    round costs one SHA-256 chain whatever its size)."""
     n = 4 * 7
     chunks, dig = _store(n, 14)
     st = Locations(chunks)
     st.set(1, 0, "bad")   # window 0: part 1 retries
     st.set(13, 2, "bad")  # window 3: part 13 retries
     r = br.BatchReader(D, P, L, 4, 4, [0])
-    assert (r.R, r.ahead) == (5, 2)
+    assert r.R == 5
     order = []
     r.read(n, st.fetch, lambda k: dig[k], lambda k, data: order.append(k))
     assert order == list(range(n))
     ev = r.multi.events
-    assert ev == [("read", 4, False)] * 3 + [("read", 1, True)] + [("read", 4, False)] * 3 \
-        + [("read", 1, True)] + [("read", 4, False)], ev
+    assert ev == [("read", 4, False), ("read", 1, True)] + [("read", 4, False)] * 3 \
+        + [("read", 1, True)] + [("read", 4, False)] * 3, ev
     assert r.retries == 2 and r.multi.pool == {}
 
 
-def test_batch_reader_checks_every_window_once_nothing_is_left_to_load(fakes):
-    """After the last window is submitted every live window is checked at once, so the retries of
-    the last windows go out together instead of one per emitted window."""
+def test_batch_reader_retries_of_the_last_windows_go_out_before_any_is_emitted(fakes):
+    """Each window's retry goes out as soon as its job is done, so those of the last windows are
+    all in flight before the first of them is emitted (not one per emitted window)."""
     n = 4 * 5
     chunks, dig = _store(n, 15)
     st = Locations(chunks)
@@ -515,6 +532,7 @@ def test_batch_reader_checks_every_window_once_nothing_is_left_to_load(fakes):
     order = []
     r.read(n, st.fetch, lambda k: dig[k], lambda k, data: order.append(k))
     assert order == list(range(n))
-    # windows 0-4 submitted (5 windows, 5 buffers), then at the next step windows 2, 3 and 4
-    # are checked before window 0 is emitted: their three retries back to back
-    assert r.multi.events == [("read", 4, False)] * 5 + [("read", 1, True)] * 3, r.multi.events
+    # each of windows 2-4 is followed by its retry; all five are submitted before window 0 is
+    # emitted (5 window buffers)
+    assert r.multi.events == [("read", 4, False)] * 3 + [("read", 1, True), ("read", 4, False)] * 2 \
+        + [("read", 1, True)], r.multi.events

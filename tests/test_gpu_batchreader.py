@@ -1,5 +1,5 @@
 """chunky_ec.batchreader (the executed twin of the Rust crate's batch::BatchReader / read_part /
-FileReader and of the C++ FileReference::read_run / retry_start / retry_finish) on the GPU: parts come out in file
+FileReader and of the C++ FileReference::read_run / retry_start / retry_collect) on the GPU: parts come out in file
 order with their stored data chunks, with chunks missing from storage, chunks served damaged
 (rejected by the SHA-256 verification and replaced, file_part.rs:92-107), chunks listed with a bad
 copy before a good one (the next location of the same chunk is read before another chunk is

@@ -174,17 +174,20 @@ def test_batch_writer_mirrors_the_cpp_loop():
 
 
 def test_batch_reader_mirrors_the_cpp_and_python_loops():
-    """BatchReader::read is the C++ read_run / retry_start / retry_finish loop (and
-    chunky_ec/batchreader.py, its GPU-tested Python twin): per step the window after the oldest
-    is checked (its failed parts' first retry round queued), the oldest finished and handed out,
-    then the next window loaded and submitted into its buffers; failed parts retried with
-    PRESENT_VERIFIED chunks plus untried ones until they decode, TooFewShardsPresent when none
-    is left."""
+    """BatchReader::read is the C++ read_run / retry_start / retry_collect loop (and
+    chunky_ec/batchreader.py, its GPU-tested Python twin): per step every window is polled
+    (checked once its job is done, its retry's next round queued once the last one is), the
+    oldest finished and handed out (loaded data chunks from the window's chunk buffer,
+    REBUILT_ONLY), then the next window loaded and submitted into its buffers; failed parts
+    retried with PRESENT_VERIFIED chunks plus untried ones until they decode,
+    TooFewShardsPresent when none is left."""
     batch = _crate_sources()["batch.rs"]
     body = batch[batch.index("pub fn read<"):batch.index("    fn load<")]
-    order = [body.index(s) for s in ("self.check(next", "self.finish(w", "self.load(", "self.submit(")]
-    assert order == sorted(order) and "(i + a) % r" in body and "self.drain(&live)" in body
-    assert "checked_ahead(r)" in body and "read_windows_for(depth)" in batch and "r - 1" in body
+    order = [body.index(s) for s in ("self.poll(live, i + 1", "self.finish(&mut w", "self.load(",
+                                      "self.submit(")]
+    assert order == sorted(order) and "self.drain(&live)" in body
+    assert "read_windows_for(depth)" in batch and "self.multi.query(" in batch
+    assert "CEC_READ_REBUILT_ONLY" in open(RUST).read() and "window_slice(ch, p, l)" in batch
     retry = batch[batch.index("    fn retry_start<"):batch.index("    fn drain(&self, live: &[Option<LiveRead>])")]
     for s in ("CEC_PRESENT_VERIFIED", "have + added < d", "TooFewShardsPresent",
               "self.multi.submit_read_carry(", "self.multi.wait(rt.job)"):
@@ -193,8 +196,8 @@ def test_batch_reader_mirrors_the_cpp_and_python_loops():
     drain = drain[:drain.index("\n    }\n")]
     assert "carry_release(" in drain and "rt.cid" in drain and "self.multi.wait(rt.job)" in drain
     py = open(os.path.join(ROOT, "chunky-bits_amd", "chunky_ec", "batchreader.py")).read()
-    for s in ("def _load", "def _submit", "def _check", "def _finish", "def _retry_start",
-              "def _retry_round", "def _retry_finish", "have + added < d",
+    for s in ("def _load", "def _submit", "def _check", "def _poll", "def _finish",
+              "def _retry_start", "def _retry_round", "def _retry_collect", "have + added < d",
               "PRESENT_VERIFIED", "TOO_FEW_SHARDS_PRESENT"):
         assert s in py, s
 

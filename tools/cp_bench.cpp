@@ -46,10 +46,12 @@ int main(int argc, char** argv) {
         detail::ReadTimes& t = detail::read_times();
         char buf[256];
         std::snprintf(buf, sizeof buf,
-                      "[%llu windows: load %.3f s, wait job %.3f s, %llu retry rounds: build %.3f s, "
-                      "wait %.3f s; sink %.3f s]",
+                      "[%llu windows: load %.3f s, wait job %.3f s, %llu retry rounds (%llu after "
+                      "a first, %llu parts): build %.3f s, wait %.3f s; sink %.3f s]",
                       static_cast<unsigned long long>(t.windows), t.load, t.wait_job,
-                      static_cast<unsigned long long>(t.retry_rounds), t.retry_build,
+                      static_cast<unsigned long long>(t.retry_rounds),
+                      static_cast<unsigned long long>(t.later_rounds),
+                      static_cast<unsigned long long>(t.retry_parts), t.retry_build,
                       t.wait_retry, t.emit);
         t = detail::ReadTimes{};
         return std::string(buf);
