@@ -368,12 +368,15 @@ fn draw_order(good: &[bool], tried: &[bool], exhausted: &[bool]) -> Vec<usize> {
 /// verify goes again with the chunks that verified (`CEC_PRESENT_VERIFIED`: used, not hashed
 /// again; kept on the GPU under the part's carry id), the failed chunks' NEXT copies (the same
 /// chunk's next location is read before another chunk is drawn, file_part.rs:100-107), then
-/// untried chunks, up to d, until it decodes or runs out of copies.  A window is checked (its job
-/// waited for, the first round of its failed parts' retry queued ahead of the windows queued after
-/// it, `CEC_MULTI_AHEAD`) a step or more before it is emitted, so that retry runs beside the
-/// loading of the next windows.  So a chunk listed `[bad, good]` -- what resilver leaves when it appends a rebuilt
-/// copy's location (file_part.rs:346) -- reads as in the reference.  [`FileReader`] splits a file
-/// into runs of one shape (the short last part has its own chunk size).
+/// untried chunks, up to d, until it decodes or runs out of copies.  Every window is polled
+/// (`Multi::query`): checked (its job waited for, the first round of its failed parts' retry
+/// queued ahead of the windows queued after it, `CEC_MULTI_AHEAD`) as soon as its job is done,
+/// and each next round queued as soon as the last one is, so retries run beside the loading of
+/// the next windows.  Only the rebuilt data chunks come down (`CEC_READ_REBUILT_ONLY`): a loaded
+/// one reaches the sink from the window's chunk buffer.  So a chunk listed `[bad, good]` -- what
+/// resilver leaves when it appends a rebuilt copy's location (file_part.rs:346) -- reads as in
+/// the reference.  [`FileReader`] splits a file into runs of one shape (the short last part has
+/// its own chunk size).
 /// `include/chunky_ec.hpp`'s `FileReference::read_run` / `retry_start` / `retry_collect` is the
 /// same loop in C++ and `chunky-bits_amd/chunky_ec/batchreader.py` its Python twin; both are
 /// tested on the GPU.

@@ -194,6 +194,9 @@ def test_write_pipeline_and_multi_argument_checks_precede_device_use():
         with pytest.raises(ce.Error) as e:
             ce.HostBuffer(4096)
         assert e.value.code == ce.ERR_NO_DEVICE
+    # no scheduler: the job calls refuse it before anything else
+    assert ce._lib.cec_multi_query(None, 1) == ce.ERR_INVALID_ARGUMENT
+    assert ce._lib.cec_multi_wait(None, 1) == ce.ERR_INVALID_ARGUMENT
 
 
 def test_product_library_has_no_attribution_kernels():
