@@ -332,6 +332,8 @@ inline std::atomic<bool>& read_carry() {
 // and in the sink.
 struct ReadTimes {
     double load = 0, wait_job = 0, retry_build = 0, wait_retry = 0, emit = 0;
+    // submission to the loop seeing the job done, summed: windows' read jobs, retry rounds
+    double job_latency = 0, round_latency = 0;
     uint64_t windows = 0, retry_rounds = 0, retry_parts = 0, later_rounds = 0;
 };
 inline ReadTimes& read_times() {
@@ -1118,6 +1120,7 @@ struct FileReference {
     struct ReadWindow {
         size_t first = 0, n = 0;
         uint64_t job = 0;
+        std::chrono::steady_clock::time_point sent;  // when the job (or the last round) went out
         bool live = false;     // its read job was submitted and its parts not yet emitted
         bool checked = false;  // its read job was waited for (and its retry started)
         detail::PinnedBuf chunks;  // [W][t][L] loaded chunk bytes (DMA'd directly)
@@ -1195,6 +1198,7 @@ struct FileReference {
                                                      w.ptrs.data(), CEC_READ_REBUILT_ONLY, nullptr,
                                                      detail::read_carry() ? w.carry.data() : nullptr,
                                                      &w.job));
+            w.sent = std::chrono::steady_clock::now();
             w.first = at;
             w.n = cnt;
             w.live = true;
@@ -1204,6 +1208,8 @@ struct FileReference {
         auto check = [&](ReadWindow& w) {
             w.checked = true;
             detail::check_multi(cec_multi_wait(m, w.job));
+            detail::read_times().job_latency +=
+                std::chrono::duration<double>(std::chrono::steady_clock::now() - w.sent).count();
             std::vector<size_t> failed;
             for (size_t q = 0; q < w.n; ++q)
                 if (w.status[q] != CEC_OK) failed.push_back(q);
@@ -1388,6 +1394,7 @@ struct FileReference {
             r.verified.data(), r.status.data(), nullptr, CEC_MULTI_AHEAD, r.carry_in.data(),
             detail::read_carry() ? r.carry_out.data() : nullptr, &r.job));
         for (size_t q = 0; q < g; ++q) r.cid[r.open[q]] = -1;  // the job's ids now
+        w.sent = std::chrono::steady_clock::now();
         r.g = g;
         r.in_flight = true;
     }
@@ -1400,6 +1407,8 @@ struct FileReference {
         {
             r.in_flight = false;
             detail::check_multi(cec_multi_wait(m, r.job));
+            detail::read_times().round_latency +=
+                std::chrono::duration<double>(std::chrono::steady_clock::now() - w.sent).count();
             const uint8_t* data = r.data.reserve(r.f * d * L, -1);
             std::vector<size_t> still;
             for (size_t q = 0; q < r.g; ++q) {

@@ -44,14 +44,18 @@ int main(int argc, char** argv) {
     // where the batched read loop's time went since the last call (detail::read_times)
     auto times = [] {
         detail::ReadTimes& t = detail::read_times();
-        char buf[256];
+        char buf[384];
         std::snprintf(buf, sizeof buf,
-                      "[%llu windows: load %.3f s, wait job %.3f s, %llu retry rounds (%llu after "
-                      "a first, %llu parts): build %.3f s, wait %.3f s; sink %.3f s]",
+                      "[%llu windows: load %.3f s, wait job %.3f s (job latency %.1f ms), %llu retry "
+                      "rounds (%llu after a first, %llu parts, latency %.1f ms): build %.3f s, wait "
+                      "%.3f s; sink %.3f s]",
                       static_cast<unsigned long long>(t.windows), t.load, t.wait_job,
+                      t.windows ? t.job_latency / double(t.windows) * 1e3 : 0.0,
                       static_cast<unsigned long long>(t.retry_rounds),
                       static_cast<unsigned long long>(t.later_rounds),
-                      static_cast<unsigned long long>(t.retry_parts), t.retry_build,
+                      static_cast<unsigned long long>(t.retry_parts),
+                      t.retry_rounds ? t.round_latency / double(t.retry_rounds) * 1e3 : 0.0,
+                      t.retry_build,
                       t.wait_retry, t.emit);
         t = detail::ReadTimes{};
         return std::string(buf);
