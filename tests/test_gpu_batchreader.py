@@ -133,3 +133,70 @@ def test_file_reader_with_short_last_part():
     FileReader(4, 2, [0]).read(shapes, fetch, lambda k: digs[k],
                                lambda k, data: out.extend(b"".join(bytes(x) for x in data)))
     assert bytes(out[:len(fb)]) == fb
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0]])
+def test_batch_readers_in_two_threads_with_random_damage(devices):
+    """The polling read loop under load: two BatchReaders (depth 4: five windows each, every
+    window polled, retry rounds as AHEAD jobs on the scheduler's priority slots, windows bringing
+    down only rebuilt chunks) read two stores with random damage at once from two threads.
+    Locations are random mixes of good, bad, unreadable and short copies, some chunks with
+    several; every part must come out as stored, in order, and a part left without d good
+    chunks must fail its reader with TooFewShardsPresent."""
+    import threading
+
+    d, p, Lc, n = 6, 3, 8192, 96
+    t = d + p
+    results, errors = {}, {}
+
+    def store(seed):
+        chunks, dig = make_parts(n, d, p, Lc, seed)
+        rng = np.random.default_rng(seed)
+        st = Locations(chunks)
+        good = {}
+        for k in range(n):
+            good[k] = 0
+            for i in range(t):
+                u = rng.random()
+                if u < 0.75:
+                    spec = ["good"]
+                elif u < 0.85:
+                    spec = ["bad", "good"]
+                elif u < 0.9:
+                    spec = ["gone", "short", "good"]
+                elif u < 0.95:
+                    spec = ["bad"]
+                else:
+                    spec = ["gone"]
+                st.set(k, i, *spec)
+                good[k] += "good" in spec
+        return chunks, dig, st, good
+
+    def run(name, seed):
+        chunks, dig, st, good = store(seed)
+        r = BatchReader(d, p, Lc, 4, 4, devices)
+        got = []
+        try:
+            r.read(n, st.fetch, lambda k: dig[k],
+                   lambda k, data: got.append((k, b"".join(bytes(x) for x in data))))
+            errors[name] = None
+        except ce.Error as e:
+            errors[name] = e.code
+        results[name] = (chunks, good, got, r)
+
+    threads = [threading.Thread(target=run, args=(f"r{s}", 70 + s)) for s in range(2)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=120)
+    for name, (chunks, good, got, r) in results.items():
+        short = [k for k in range(n) if good[k] < d]
+        # file order, stored bytes, up to the first part that cannot be decoded
+        assert [k for k, _ in got] == list(range(len(got)))
+        for k, b in got:
+            assert b == chunks[k, :d].tobytes(), (name, k)
+        if short:
+            assert errors[name] == ce.TOO_FEW_SHARDS_PRESENT and len(got) <= short[0], name
+        else:
+            assert errors[name] is None and len(got) == n, name
+        assert all(r.multi.stats(g)["carry_held"] == 0 for g in range(len(devices))), name
