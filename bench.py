@@ -468,22 +468,19 @@ def timed_read_repair(codec, ring, ring_dig, L, P, depth, first, n_parts, world,
     crng = np.random.default_rng(seed)
     damaged = [0]
 
-    def fetch(dest, rows):  # dest: readstream.PackedChunks (one upload per batch)
-        flat = dest.flat
-
+    def fetch(chunks, rows):
         def job(a, b):
             for k, part, flags in rows[a:b]:
                 r = part % R
-                js = np.flatnonzero(flags)
-                for q, j in zip(dest.rows(k, js), js):
-                    flat[q] = ring[r, j]
+                for j in np.flatnonzero(flags):
+                    chunks[k, j] = ring[r, j]
         copier.map(job, len(rows))
         if corrupt > 0 and rows:  # fresh reads only: a re-sent verified chunk verified already
             ks = np.fromiter((k for k, _, _ in rows), np.int64, len(rows))
             kk, jj = np.nonzero(np.stack([f for _, _, f in rows]) == 1)
             hit = crng.random(len(kk)) < corrupt
             kk, jj = ks[kk[hit]], jj[hit]
-            flat[dest.rows(kk, jj), crng.integers(L, size=len(kk))] ^= 0xA5
+            chunks[kk, jj, crng.integers(L, size=len(kk))] ^= 0xA5
             damaged[0] += len(kk)
 
     checks = []
@@ -498,13 +495,13 @@ def timed_read_repair(codec, ring, ring_dig, L, P, depth, first, n_parts, world,
             checks.append({"part": int(part), "attempts": int(attempts),
                            "ok": rp.part_bytes(slot, nb, k) == ring[part % R, :d].tobytes()})
 
-    warm = ReadRepairStream(rp, fetch, lambda ids: ring_dig[ids % R], seed=seed + 1, packed=True)
+    warm = ReadRepairStream(rp, fetch, lambda ids: ring_dig[ids % R], seed=seed + 1)
     warm.run(first, min(n_parts, depth * P))
     damaged[0] = 0
     barrier(world)
     t0 = time.perf_counter()
     st = ReadRepairStream(rp, fetch, lambda ids: ring_dig[ids % R], seed=seed + 2,
-                          on_part=on_part, packed=True).run(first, n_parts)
+                          on_part=on_part).run(first, n_parts)
     barrier(world)
     el = time.perf_counter() - t0
     del rp
@@ -746,9 +743,8 @@ def read_repair_form(codec, d, p, L, n_parts, world, rank, reduce_dev, copier, d
             "chunks_loaded": stats["chunks_loaded"],
             "sampled_parts_equal_stored": ok, "checks": checks,
             "path": f"pageable ring of {len(ring)} stored parts ({size_label(ring.nbytes)}) -> "
-                    f"{copier.threads} host threads copy d random chunks per part back to back "
-                    "into a page-locked slot, a seeded fraction of them damaged -> one H2D per "
-                    "batch (CEC_SUBMIT_PACKED) -> SHA-256 "
+                    f"{copier.threads} host threads copy d random chunks per part into a "
+                    "page-locked slot, a seeded fraction of them damaged -> H2D -> SHA-256 "
                     "verify + reconstruct_data -> D2H of the rebuilt data chunks; parts with a "
                     "rejected chunk resubmitted in the next batch, ahead of its new parts, with "
                     + ("their verified chunks kept on the device (CEC_READ_CARRY) "

@@ -722,7 +722,6 @@ class ReadPipeline:
         self.parts = parts_per_batch
         self.depth = depth
         self.carry = bool(flags & self.CARRY)
-        self.mode = flags & (self.REBUILT_ONLY | READ_RESILVER | READ_VERIFY_ONLY)  # per batch
 
     def __del__(self, _free=_lib.cec_read_pipeline_free):
         h = getattr(self, "_h", None)

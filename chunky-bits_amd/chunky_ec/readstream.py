@@ -27,11 +27,6 @@ what the retries are for); one flagged ``CEC_PRESENT_VERIFIED`` must be the byte
 before (the reference keeps a verified chunk in memory, file_part.rs:102-104).
 ``digests(part_ids)`` returns the metadata digests [n][d+p][32].  Host bookkeeping only; all
 hashing and decoding runs in the pipeline's HIP kernels.
-
-``packed=True``: ``fetch`` gets a :class:`PackedChunks` instead of the [parts][d+p][L] array --
-the same ``dest[k, j] = bytes`` / ``dest[k, j, pos]`` indexing, but the chunks land back to back
-in (part, chunk index) order and the batch goes up in one copy (CEC_SUBMIT_PACKED) rather than
-one per run of adjacent loaded chunks (~4 per part when d of d+p are drawn at random).
 """
 from __future__ import annotations
 
@@ -43,44 +38,6 @@ from typing import Callable, Deque, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import OK, PRESENT_VERIFIED, TOO_FEW_SHARDS_PRESENT, Error
-
-
-class PackedChunks:
-    """A slot's chunk buffer filled packed: the chunks flagged in `mask` [n][d+p] back to back in
-    (part, chunk index) order.  ``dest[k, j]`` is chunk j of row k (a writable [L] view),
-    ``dest[k, j, pos]`` one of its bytes, ``dest[k] = v`` fills row k's chunks;
-    ``rows(ks, js)`` gives the packed rows of many (k, j) at once for vectorized access to
-    ``flat`` ([m][L])."""
-
-    def __init__(self, flat: np.ndarray, mask: np.ndarray):
-        self.index = np.full(mask.shape, -1, np.int64)
-        self.index[mask] = np.arange(int(np.count_nonzero(mask)))
-        self.flat = flat
-
-    def rows(self, ks, js) -> np.ndarray:
-        r = self.index[ks, js]
-        if (r < 0).any():
-            raise IndexError("chunk not in the batch's fetch set")
-        return r
-
-    def _row(self, k, j) -> np.ndarray:
-        r = int(self.index[k, j])
-        if r < 0:
-            raise IndexError(f"chunk {j} of row {k} is not in the batch's fetch set")
-        return self.flat[r]
-
-    def __getitem__(self, key):
-        if len(key) == 3:
-            return self._row(key[0], key[1])[key[2]]
-        return self._row(*key)
-
-    def __setitem__(self, key, value):
-        if isinstance(key, (int, np.integer)):
-            self.flat[self.index[key][self.index[key] >= 0]] = value
-        elif len(key) == 3:
-            self._row(key[0], key[1])[key[2]] = value
-        else:
-            self._row(*key)[:] = value
 
 
 @dataclass
@@ -124,10 +81,8 @@ class ReadRepairStream:
 
     def __init__(self, rp, fetch: Callable[[np.ndarray, Sequence[Tuple[int, int, np.ndarray]]], None],
                  digests: Callable[[np.ndarray], np.ndarray], seed: int = 0,
-                 on_part: Optional[Callable[[int, int, int, int, int], None]] = None,
-                 packed: bool = False):
+                 on_part: Optional[Callable[[int, int, int, int, int], None]] = None):
         self.rp = rp
-        self.packed = packed
         self.fetch = fetch
         self.digests = digests
         self.rng = np.random.default_rng(seed)
@@ -190,23 +145,15 @@ class ReadRepairStream:
         # a carried part's verified chunks are on the device already: fetch only its new ones
         fetch_rows = present.copy()
         fetch_rows[(carry >= 0)[:, None] & (present == PRESENT_VERIFIED)] = 0
-        dest = chunks
-        if self.packed:  # one upload per batch instead of one per run of loaded chunks
-            dest = PackedChunks(chunks.reshape(-1, chunks.shape[-1]), fetch_rows[:n] != 0)
         t0 = time.perf_counter()
-        self.fetch(dest, [(k, int(ids[k]), fetch_rows[k]) for k in range(n)])
+        self.fetch(chunks, [(k, int(ids[k]), fetch_rows[k]) for k in range(n)])
         self.stats.fetch_s += time.perf_counter() - t0
-        carried = (carry >= 0).any()
-        if self.packed:
-            self.rp.submit_ex(slot, n, carry_ids=carry if carried else None, mode=self.rp.mode,
-                              packed=True)
-        elif carried:
+        if (carry >= 0).any():
             self.rp.submit_carried(slot, n, carry)
-        else:
-            self.rp.submit(slot, n)
-        if carried:
             for e in parts:
                 e.carry = -1  # an entry is used once
+        else:
+            self.rp.submit(slot, n)
         self.stats.batches += 1
         self.stats.chunks_loaded += int(np.count_nonzero(fetch_rows))
         self.stats.carried_chunks += int(np.count_nonzero(present) - np.count_nonzero(fetch_rows))

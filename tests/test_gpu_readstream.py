@@ -37,16 +37,14 @@ def _store(n, d, p, L, seed):
     return chunks, dig
 
 
-@pytest.mark.parametrize("packed", [False, True])
 @pytest.mark.parametrize("carry", [False, True])
 @pytest.mark.parametrize("d,p,L,corrupt", [(10, 4, 4096, 0.05), (3, 2, 1000, 0.2),
                                            (20, 8, 777, 0.03)])
-def test_read_repair_stream_on_the_pipeline(d, p, L, corrupt, carry, packed):
+def test_read_repair_stream_on_the_pipeline(d, p, L, corrupt, carry):
     """carry: CEC_READ_CARRY -- a retried part's verified chunks come from the device carry pool
     (the slot's bytes for them are overwritten with garbage here, so a path that uploaded them
     anyway, or read them back from the slot, would decode wrong), its data chunks among them
-    come back like rebuilt ones; odd L (1000, 777) takes the pitched copies; packed: the fetched
-    chunks back to back, one upload per batch (the bench's end-to-end read)."""
+    come back like rebuilt ones; odd L (1000, 777) takes the pitched copies."""
     n, P, depth = 61, 8, 3
     chunks, dig = _store(n, d, p, L, d * 100 + p)
     codec = ce.ReedSolomon(d, p)
@@ -69,8 +67,7 @@ def test_read_repair_stream_on_the_pipeline(d, p, L, corrupt, carry, packed):
     def on_part(slot, nb, k, part, attempts):
         got[part] = (rp.part_bytes(slot, nb, k), attempts)
 
-    s = ReadRepairStream(rp, fetch, lambda ids: dig[ids], seed=1, on_part=on_part,
-                         packed=packed).run(0, n)
+    s = ReadRepairStream(rp, fetch, lambda ids: dig[ids], seed=1, on_part=on_part).run(0, n)
     assert s.parts + s.undecodable_parts == n
     assert s.rejected_chunks == damaged[0] > 0 and s.retried_parts > 0
     assert (s.carried_chunks > 0) == carry
@@ -80,9 +77,8 @@ def test_read_repair_stream_on_the_pipeline(d, p, L, corrupt, carry, packed):
     assert set(got) | set(s.undecodable) == set(range(n))
 
 
-@pytest.mark.parametrize("packed", [False, True])
 @pytest.mark.parametrize("carry", [False, True])
-def test_read_repair_stream_runs_out_of_chunks_on_the_pipeline(carry, packed):
+def test_read_repair_stream_runs_out_of_chunks_on_the_pipeline(carry):
     d, p, L, n = 3, 2, 512, 10
     chunks, dig = _store(n, d, p, L, 4)
     rp = ce.ReadPipeline(ce.ReedSolomon(d, p), L, 4, 2, ce.ReadPipeline.REBUILT_ONLY |
@@ -97,7 +93,7 @@ def test_read_repair_stream_runs_out_of_chunks_on_the_pipeline(carry, packed):
                 if flags[j] == 1 and ((part == 7 and j < 2) or (part == 3 and j < 3)):
                     slot_chunks[k, j, 0] ^= 1
 
-    s = ReadRepairStream(rp, fetch, lambda ids: dig[ids], seed=0, packed=packed).run(0, n)
+    s = ReadRepairStream(rp, fetch, lambda ids: dig[ids], seed=0).run(0, n)
     assert s.undecodable == [3] and s.parts == n - 1
 
 

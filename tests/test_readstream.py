@@ -260,26 +260,3 @@ def test_read_repair_stream_carries_verified_chunks(cap):
             seen.setdefault(part, set()).update(new)
     assert not fp.pool or fp.released  # entries are used or released, never left behind
     assert sorted(fp.free) == list(range(fp.cap))
-
-
-def test_packed_chunks_indexing():
-    """PackedChunks (ReadRepairStream(packed=True)): the flagged chunks land back to back in
-    (part, chunk index) order; chunk / byte / whole-row indexing and the vectorized rows()."""
-    from chunky_ec.readstream import PackedChunks
-    L = 8
-    flat = np.zeros((2 * 4, L), np.uint8)
-    mask = np.array([[1, 0, 1, 0], [0, 1, 1, 1]], bool)
-    dest = PackedChunks(flat, mask)
-    dest[0, 0] = np.full(L, 1, np.uint8)
-    dest[0, 2] = np.full(L, 2, np.uint8)
-    dest[1, 3] = np.full(L, 5, np.uint8)
-    dest[1, 1, 0] = 9
-    assert flat[:4, 0].tolist() == [1, 2, 9, 0] and flat[4, 1] == 5
-    assert dest[1, 1, 0] == 9 and bytes(dest[0, 2]) == bytes([2]) * L
-    dest[1] = 7  # row 1's three chunks
-    assert flat[2:5].min() == 7 and flat[:2].max() == 2
-    assert dest.rows(np.array([0, 1]), np.array([2, 3])).tolist() == [1, 4]
-    with pytest.raises(IndexError):
-        dest[0, 1] = np.zeros(L, np.uint8)  # not fetched
-    with pytest.raises(IndexError):
-        dest.rows(np.array([1]), np.array([0]))
