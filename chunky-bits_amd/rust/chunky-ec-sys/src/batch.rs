@@ -856,43 +856,41 @@ impl BatchReader {
         F: FnMut(usize, usize, usize) -> Option<(usize, Vec<u8>)>,
     {
         let (d, t, l) = (self.d, self.t, self.chunk_size);
-        {
-            let again = {
-                let rt = match w.retry.as_mut() {
-                    Some(rt) if rt.in_flight => rt,
-                    _ => return Ok(()),
-                };
-                rt.in_flight = false;
-                self.multi.wait(rt.job)?;
-                self.retries += rt.g as u64;
-                let r_out: &[u8] = match self.retry_bufs[w.slot].out.as_ref() {
-                    Some(b) => &b[..],
-                    None => return Err(crate::too_small("retry buffer")),
-                };
-                let out: &mut [u8] = &mut self.out[w.slot];
-                let mut still = Vec::new();
-                for s in 0..rt.g {
-                    let r = rt.open[s];
-                    let q = rt.failed[r];
-                    for i in 0..t {
-                        rt.good[r * t + i] = rt.r_ver[s * t + i] != 0;
-                    }
-                    if rt.r_status[s] == 0 {
-                        out[q * d * l..(q + 1) * d * l].copy_from_slice(&r_out[s * d * l..(s + 1) * d * l]);
-                        self.redone[w.slot][q] = true;
-                    } else if rt.r_status[s] == crate::sys::CEC_TOO_FEW_SHARDS_PRESENT {
-                        rt.cid[r] = rt.r_cout[s];
-                        still.push(r);
-                    } else {
-                        return Err(crate::check(rt.r_status[s]).unwrap_err());
-                    }
-                }
-                rt.open = still;
-                !rt.open.is_empty()
+        let again = {
+            let rt = match w.retry.as_mut() {
+                Some(rt) if rt.in_flight => rt,
+                _ => return Ok(()),
             };
-            if again {
-                self.retry_round(w, fetch)?;
+            rt.in_flight = false;
+            self.multi.wait(rt.job)?;
+            self.retries += rt.g as u64;
+            let r_out: &[u8] = match self.retry_bufs[w.slot].out.as_ref() {
+                Some(b) => &b[..],
+                None => return Err(crate::too_small("retry buffer")),
+            };
+            let out: &mut [u8] = &mut self.out[w.slot];
+            let mut still = Vec::new();
+            for s in 0..rt.g {
+                let r = rt.open[s];
+                let q = rt.failed[r];
+                for i in 0..t {
+                    rt.good[r * t + i] = rt.r_ver[s * t + i] != 0;
+                }
+                if rt.r_status[s] == 0 {
+                    out[q * d * l..(q + 1) * d * l].copy_from_slice(&r_out[s * d * l..(s + 1) * d * l]);
+                    self.redone[w.slot][q] = true;
+                } else if rt.r_status[s] == crate::sys::CEC_TOO_FEW_SHARDS_PRESENT {
+                    rt.cid[r] = rt.r_cout[s];
+                    still.push(r);
+                } else {
+                    return Err(crate::check(rt.r_status[s]).unwrap_err());
+                }
             }
+            rt.open = still;
+            !rt.open.is_empty()
+        };
+        if again {
+            self.retry_round(w, fetch)?;
         }
         Ok(())
     }
