@@ -6,7 +6,7 @@
 // Batched only, last: the read with `damage` (default 1 %) of the stored chunk copies flipped,
 // so parts retry (file_part.rs:92-107), with the retries' verified chunks kept on the GPU
 // (carry) and sent again (no carry): time and chunks sent to the GPUs.
-//   make -C chunky-bits_amd/csrc cp_bench ; tools/cp_bench [GiB] [devices] [damage]
+//   make -C chunky-bits_amd/csrc cp_bench ; tools/cp_bench [GiB] [devices] [damage] [depth]
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -20,6 +20,7 @@ using namespace chunky_ec;
 int main(int argc, char** argv) {
     const double gib = argc > 1 ? std::atof(argv[1]) : 4.0;
     const double damage = argc > 3 ? std::atof(argv[3]) : 0.01;
+    const size_t depth = argc > 4 ? size_t(std::atoi(argv[4])) : 4;  // scheduler depth (read windows: depth + 1)
     std::vector<int> devices;
     if (argc > 2) {
         std::stringstream ss(argv[2]);
@@ -64,7 +65,7 @@ int main(int argc, char** argv) {
     for (int batched = 1; batched >= 0; --batched) {
         const size_t n = batched ? length : std::min(length, size_t(64) * d * chunk);
         auto write = [&](ChunkStore& store) {
-            return batched ? FileWriteBuilder(builder).batch(128, 4).devices(devices).write(
+            return batched ? FileWriteBuilder(builder).batch(128, depth).devices(devices).write(
                                  input.data(), n, store)
                            : builder.write(input.data(), n, store);
         };
@@ -81,16 +82,16 @@ int main(int argc, char** argv) {
         FileReference f = write(store);
         const double w_ram = secs(t0);
         if (batched) {  // pins the verify / resilver windows (nothing to rebuild yet)
-            (void)f.resilver(store, 128, 4, devices);
-            (void)f.verify(store, 128, 4, devices);
+            (void)f.resilver(store, 128, depth, devices);
+            (void)f.verify(store, 128, depth, devices);
         }
         for (const auto& part : f.parts) {
             store.erase(part.data[3].locations[0]);
             store.erase(part.parity[1].locations[0]);
         }
-        if (batched) (void)f.read(store, 128, 4, devices);  // pins the read windows
+        if (batched) (void)f.read(store, 128, depth, devices);  // pins the read windows
         t0 = std::chrono::steady_clock::now();
-        const Bytes back = batched ? f.read(store, 128, 4, devices) : f.read(store);
+        const Bytes back = batched ? f.read(store, 128, depth, devices) : f.read(store);
         const double r = secs(t0);
         bool ok = back.size() == n && std::memcmp(back.data(), input.data(), n) == 0;
         // the same read streamed to a sink (FileReadBuilder's reader, reader.rs:40-75) that
@@ -99,7 +100,7 @@ int main(int argc, char** argv) {
         (void)times();
         t0 = std::chrono::steady_clock::now();
         if (batched)
-            f.read_to(store, [&](const uint8_t*, size_t m) { at += m; }, 128, 4, devices);
+            f.read_to(store, [&](const uint8_t*, size_t m) { at += m; }, 128, depth, devices);
         else
             f.read_to(store, [&](const uint8_t*, size_t m) { at += m; });
         const double r_sink = secs(t0);
@@ -108,15 +109,15 @@ int main(int argc, char** argv) {
         // resilver (rebuild the two lost chunks of every part and write them back), then verify
         // (every stored chunk hashed)
         t0 = std::chrono::steady_clock::now();
-        const auto rep = batched ? f.resilver(store, 128, 4, devices) : f.resilver(store);
+        const auto rep = batched ? f.resilver(store, 128, depth, devices) : f.resilver(store);
         const double rs = secs(t0);
         // the two repaired chunks of every part now list two locations (the lost one and the new
         // copy, file_part.rs:346; both "sha256-<hex>" here, so both read): 16 copies per part to
         // hash, more than the 14-chunk windows hold, so the first such verify of a thread grows
         // its page-locked windows -- once, like the first call's pinning above
-        if (batched) (void)f.verify(store, 128, 4, devices);
+        if (batched) (void)f.verify(store, 128, depth, devices);
         t0 = std::chrono::steady_clock::now();
-        const auto ver = batched ? f.verify(store, 128, 4, devices) : f.verify(store);
+        const auto ver = batched ? f.verify(store, 128, depth, devices) : f.verify(store);
         const double vs = secs(t0);
         for (const auto& r : ver) ok = ok && r.is_ideal();
         for (const auto& r : rep)
@@ -155,7 +156,7 @@ int main(int argc, char** argv) {
         };
         for (int carry = 1; carry >= 0; --carry) {  // checked (and warms the windows)
             detail::read_carry() = carry != 0;
-            const Bytes dmg = f.read(store, 128, 4, devices);
+            const Bytes dmg = f.read(store, 128, depth, devices);
             ok = ok && dmg.size() == n && std::memcmp(dmg.data(), input.data(), n) == 0;
         }
         // timed: streamed to a sink that discards the bytes, as read_to above; the two modes
@@ -170,7 +171,7 @@ int main(int argc, char** argv) {
                 size_t got = 0;
                 (void)times();
                 t0 = std::chrono::steady_clock::now();
-                f.read_to(store, [&](const uint8_t*, size_t m) { got += m; }, 128, 4, devices);
+                f.read_to(store, [&](const uint8_t*, size_t m) { got += m; }, 128, depth, devices);
                 const double rate = double(n) / secs(t0) / 1e9;
                 if (rate > best[carry]) best_times[carry] = times();
                 best[carry] = std::max(best[carry], rate);
