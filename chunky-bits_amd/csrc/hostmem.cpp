@@ -102,24 +102,6 @@ bool pinned_range(const void* p, size_t n) {
     return a >= s && a + n <= s + size;
 }
 
-void* device_view(const void* p, size_t n) {
-    if (!pinned_range(p, n)) return nullptr;
-    void* start = nullptr;
-    hipDeviceptr_t dp = reinterpret_cast<hipDeviceptr_t>(const_cast<void*>(p));
-    if (hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, dp) != hipSuccess ||
-        !start) {
-        (void)hipGetLastError();
-        return nullptr;
-    }
-    void* dstart = nullptr;
-    if (hipHostGetDevicePointer(&dstart, start, 0) != hipSuccess || !dstart) {
-        (void)hipGetLastError();
-        return nullptr;
-    }
-    return static_cast<uint8_t*>(dstart) +
-           (reinterpret_cast<uintptr_t>(p) - reinterpret_cast<uintptr_t>(start));
-}
-
 int device_numa_node(int device) {
     char bus[64] = {0};
     if (hipDeviceGetPCIBusId(bus, sizeof(bus), device) != hipSuccess) {

@@ -13,11 +13,6 @@ namespace cec {
 // hipHostRegister range HIP reports), so a copy engine can DMA it directly (no staging copy).
 bool pinned_range(const void* p, size_t n);
 
-// The address a kernel uses for [p, p + n) when that range lies in one page-locked allocation the
-// device has mapped (hipHostMalloc / cec_host_alloc: kernels may store to it over PCIe); nullptr
-// otherwise (pageable memory, or registered memory without a device mapping).
-void* device_view(const void* p, size_t n);
-
 // NUMA node of a HIP device's PCIe root (-1 when unknown), from sysfs via its PCI bus id.
 int device_numa_node(int device);
 

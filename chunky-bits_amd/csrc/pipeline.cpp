@@ -333,9 +333,6 @@ struct ReadSlot {
     uint8_t* d_pack = nullptr;      // device [parts*t][L]  packed upload (submit_packed; lazy)
     uint32_t* h_ids = nullptr;      // pinned [parts*t]     batch position of packed chunk j
     uint32_t* d_ids = nullptr;      // device [parts*t]
-    // REBUILT_ONLY down by kernel: batch position and output position of each rebuilt chunk
-    uint32_t* h_down = nullptr;     // pinned [2][parts*d]
-    uint32_t* d_down = nullptr;     // device [2][parts*d]
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
     bool in_flight = false;
@@ -425,13 +422,11 @@ struct cec_read_pipeline {
             if (s.stream) (void)hipStreamDestroy(s.stream);
             for (void* dptr : {static_cast<void*>(s.d_buf), static_cast<void*>(s.d_expected),
                                static_cast<void*>(s.d_flags), static_cast<void*>(s.d_pack),
-                               static_cast<void*>(s.d_ids), static_cast<void*>(s.d_down),
-                               static_cast<void*>(s.d_cids),
+                               static_cast<void*>(s.d_ids), static_cast<void*>(s.d_cids),
                                static_cast<void*>(s.d_res), static_cast<void*>(s.d_map),
                                static_cast<void*>(s.d_present)})
                 if (dptr) (void)hipFree(dptr);
-            for (void* hptr : {static_cast<void*>(s.h_ids), static_cast<void*>(s.h_down),
-                               static_cast<void*>(s.h_cids),
+            for (void* hptr : {static_cast<void*>(s.h_ids), static_cast<void*>(s.h_cids),
                                static_cast<void*>(s.h_res), static_cast<void*>(s.h_map)})
                 if (hptr) (void)hipHostFree(hptr);
             for (uint8_t* hptr : {s.h_chunks, s.h_present, s.h_expected, s.h_data, s.h_ok, s.h_hash})
@@ -587,57 +582,6 @@ struct cec_read_pipeline {
                                           s.stream));
             j = e;
         }
-        return CEC_OK;
-    }
-
-    // REBUILT_ONLY: the rebuilt data chunks of every decoded part go straight into the output
-    // with ONE move launch whose stores cross PCIe, when the output is page-locked memory the
-    // device has mapped (cec_host_alloc / hipHostMalloc: the caller's windows, the scheduler's
-    // staging, the slot's own output).  Copy-engine commands cost ~11 us each whatever their
-    // size, and a 256-part batch of d random chunks per part has ~560 runs of rebuilt chunks:
-    // as separate D2H copies they held the copy engine 30-77 ms per batch, stalling the next
-    // batches' uploads behind them (profiles/HISTORY.md, round 6).  Otherwise one copy per run.
-    int rebuilt_down(ReadSlot& s, size_t n_parts) const {
-        uint8_t* view = static_cast<uint8_t*>(cec::device_view(s.dst_data, n_parts * d * L));
-        if (!view) {
-            for (size_t k = 0; k < n_parts; ++k)
-                if (s.h_status[k] == CEC_OK) {
-                    const int st = copy_rebuilt_back(s, k);
-                    if (st != CEC_OK) return st;
-                }
-            return CEC_OK;
-        }
-        const size_t cap = parts * d;
-        hipError_t e = hipSuccess;  // made on the slot's first such batch
-        if (!s.d_down) e = hipMalloc(reinterpret_cast<void**>(&s.d_down), 2 * cap * sizeof(uint32_t));
-        if (e == hipSuccess && !s.h_down)
-            e = cec::host_malloc_near(reinterpret_cast<void**>(&s.h_down), 2 * cap * sizeof(uint32_t),
-                                      hipHostMallocDefault, device);
-        if (e != hipSuccess) {
-            (void)hipGetLastError();
-            return pipe_fail(e, "read pipeline rebuilt-chunk lists");
-        }
-        uint32_t* at = s.h_down;         // batch position k*t + j
-        uint32_t* to = s.h_down + cap;   // output position k*d + j
-        size_t m = 0;
-        for (size_t k = 0; k < n_parts; ++k) {
-            if (s.h_status[k] != CEC_OK) continue;
-            const uint8_t* pr = s.h_present + k * t;
-            const bool carried = !s.carried.empty() && s.carried[k];
-            for (size_t j = 0; j < d; ++j)
-                if (!(pr[j] && !(carried && pr[j] == CEC_PRESENT_VERIFIED))) {
-                    at[m] = uint32_t(k * t + j);
-                    to[m] = uint32_t(k * d + j);
-                    ++m;
-                }
-        }
-        if (!m) return CEC_OK;
-        PIPE_TRY(hipMemcpyAsync(s.d_down, at, m * sizeof(uint32_t), hipMemcpyHostToDevice, s.stream));
-        PIPE_TRY(hipMemcpyAsync(s.d_down + cap, to, m * sizeof(uint32_t), hipMemcpyHostToDevice,
-                                s.stream));
-        cec::MoveParams mv{s.d_buf, t * cs, cs, uint32_t(t), view, L, s.d_down, uint32_t(m), 0u,
-                           s.d_down + cap};
-        PIPE_TRY(cec::launch_move_chunks(mv, s.stream));
         return CEC_OK;
     }
 
@@ -876,7 +820,8 @@ struct cec_read_pipeline {
             for (size_t k = 0; k < n_parts && st == CEC_OK; ++k)
                 if (s.h_status[k] == CEC_OK) st = copy_missing_back(s, k, s.h_present + k * t);
         } else if (s.mode & CEC_READ_REBUILT_ONLY) {
-            st = rebuilt_down(s, n_parts);
+            for (size_t k = 0; k < n_parts && st == CEC_OK; ++k)
+                if (s.h_status[k] == CEC_OK) st = copy_rebuilt_back(s, k);
         } else {
             st = copy_data_back(s, 0, n_parts);
         }
