@@ -420,3 +420,31 @@ def test_ahead_job_overtakes_queued_jobs():
                                             None, None, ctypes.byref(job))
         if code != ce.OK:
             raise ce.MultiError(code)
+
+
+def test_multi_query_never_blocks_and_tracks_the_job():
+    """cec_multi_query: 0 while a job runs, 1 once it is done (wait then returns at once), and
+    CEC_ERR_INVALID_ARGUMENT for a job already waited for or never submitted."""
+    import time
+    d, p, L, n = 4, 2, 1 << 18, 64
+    t = d + p
+    chunks, dig = make_parts(n, d, p, L, 97)
+    m = ce.Multi(ce.ReedSolomon(d, p), L, 16, 2, [0], kinds=ce.Multi.READ)
+    pres = np.zeros((n, t), np.uint8)
+    pres[:, :d] = 1
+    out = np.zeros((n, d, L), np.uint8)
+    ver = np.zeros((n, t), np.uint8)
+    st = np.zeros(n, np.int32)
+    job, _ = m.read(chunks, pres, dig, n, out, ver, st)
+    seen, t0 = [], time.perf_counter()
+    while not m.query(job):
+        seen.append(0)
+        assert time.perf_counter() - t0 < 60
+        time.sleep(1e-3)
+    assert m.query(job)  # stays done until waited for
+    m.wait(job)
+    assert (st == ce.OK).all() and np.array_equal(out, chunks[:, :d])
+    for bad in (job, job + 1000):
+        with pytest.raises(ce.MultiError) as e:
+            m.query(bad)
+        assert e.value.code == ce.ERR_INVALID_ARGUMENT
