@@ -1143,9 +1143,11 @@ struct FileReference {
     // Parts [k0, k0 + n) (one shape) through cec_multi in windows of one pipeline batch per
     // shard (ppb x shards parts), up to `depth` windows' read jobs in flight, so loading the next
     // windows overlaps the GPU work and the output of the earlier ones; each window's data goes to
-    // emit() in file order.  A window is checked (its job waited for, the first round of its
-    // failed parts' retry queued) one step before it is emitted, so that retry runs beside the
-    // loading of the next window instead of stalling the loop: depth + 1 window buffers.
+    // emit() in file order (the loaded data chunks straight from the window's chunk buffer, the
+    // rebuilt ones from its output: CEC_READ_REBUILT_ONLY).  Every window is polled: checked (its
+    // job waited for, the first round of its failed parts' retry queued as a CEC_MULTI_AHEAD job)
+    // as soon as its job is done, and its next retry round queued as soon as the last one is, so
+    // retries run beside the loading of the next windows: depth + 1 window buffers.
     template <typename Emit>
     void read_run(const ChunkStore& src, size_t k0, size_t n, size_t ppb, size_t depth,
                   const std::vector<int>& devices, Emit& emit) const {
