@@ -526,11 +526,12 @@ struct cec_multi {
             f.staged_out = W && (!contiguous || !cec::pinned_range(dst, n * dw));
             Staging& sg = s.rstage[slot];
             if (f.staged_in || f.staged_out) {
-                hipError_t e = hipSuccess;  // every slot at once (see run_write)
-                for (Staging& each : s.rstage)
-                    if (e == hipSuccess)
-                        e = each.reserve(f.staged_in ? P * cw : 0, f.staged_out ? P * dw : 0,
-                                         s.device);
+                // every depth slot at once (see run_write); an AHEAD slot's when it is used
+                hipError_t e = hipSuccess;
+                for (size_t i = 0; i < s.rstage.size(); ++i)
+                    if (e == hipSuccess && (i < depth || i == slot))
+                        e = s.rstage[i].reserve(f.staged_in ? P * cw : 0,
+                                                f.staged_out ? P * dw : 0, s.device);
                 if (e != hipSuccess) {
                     finish_parts(job, count - at, CEC_ERR_OUT_OF_MEMORY,
                                  std::string("multi staging: ") + hipGetErrorString(e));
