@@ -200,3 +200,29 @@ def test_batch_readers_in_two_threads_with_random_damage(devices):
         else:
             assert errors[name] is None and len(got) == n, name
         assert all(r.multi.stats(g)["carry_held"] == 0 for g in range(len(devices))), name
+
+
+def test_failed_read_leaves_no_job_or_carry_id_behind():
+    """A part that runs out of copies fails the read while other windows' retry rounds are in
+    flight: the reader waits for every job it queued, gives every carry id back (none held), and
+    the same reader then reads another file correctly."""
+    d, p, Lc, n = 4, 2, 8192, 40
+    chunks, dig = make_parts(n, d, p, Lc, 98)
+    st = Locations(chunks)
+    for k in (2, 9, 13, 21, 30):  # retried parts in several windows (4 parts per window)
+        st.set(k, 1, "bad", "good")
+    for i in range(p + 1):  # part 17: p + 1 chunks with no good copy
+        st.set(17, i, "bad")
+    r = BatchReader(d, p, Lc, 4, 4, [0])
+    got = []
+    with pytest.raises(ce.Error) as e:
+        r.read(n, st.fetch, lambda k: dig[k], lambda k, data: got.append(k))
+    assert e.value.code == ce.TOO_FEW_SHARDS_PRESENT
+    assert got == list(range(len(got))) and len(got) <= 17
+    assert r.multi.stats(0)["carry_held"] == 0
+    good = Locations(chunks)
+    out = {}
+    r.read(n, good.fetch, lambda k: dig[k],
+           lambda k, data: out.__setitem__(k, b"".join(bytes(x) for x in data)))
+    assert all(out[k] == chunks[k, :d].tobytes() for k in range(n))
+    assert r.multi.stats(0)["carry_held"] == 0
