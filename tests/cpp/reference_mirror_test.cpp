@@ -320,6 +320,14 @@ void test_multi_device_paths() {
         // and a part whose usable chunks run out
         for (size_t i = 1; i < d + p - (d - 2); ++i) store.erase(c.parts[7].chunk(i).locations[0]);
         CHECK(throws_erasure([&] { c.read(store, 3, 2, devs); }, Error::TooFewShardsPresent));
+        // the failed read (other parts' retry rounds in flight) left the thread's scheduler sound:
+        // no carry entry held, and another file of the shape reads back through it
+        cec_multi* m = detail::cached_multi_entry().multi.get();
+        for (size_t g = 0; m && g < cec_multi_shards(m); ++g) {
+            cec_multi_stats st{};
+            CHECK(cec_multi_shard_stats(m, g, &st) == CEC_OK && st.carry_held == 0);
+        }
+        CHECK(a.read(per_part, 3, 2, devs) == input);
     }
 }
 
