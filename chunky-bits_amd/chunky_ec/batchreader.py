@@ -374,14 +374,18 @@ class BatchReader:
         for w in live:
             if w is None:
                 continue
+            ids = []
             try:
                 if not w.checked:
                     self.multi.wait(w.job)
-                if w.retry is not None and w.retry.in_flight:
-                    self.multi.wait(w.retry.job)
+                rt = w.retry
+                if rt is not None and rt.in_flight:
+                    self.multi.wait(rt.job)
+                    # the round's ids for its parts still short of d: nobody collects them now
+                    ids += [int(c) for c in rt.r_cout[:len(rt.open_)] if c >= 0]
             except Exception:  # noqa: BLE001 (the error being raised is the caller's)
                 pass
-            ids = [int(c) for c in self.carry[w.slot][:w.n] if c >= 0]
+            ids += [int(c) for c in self.carry[w.slot][:w.n] if c >= 0]
             if w.retry is not None:
                 ids += [c for c in w.retry.cid.values() if c >= 0]
             for c in ids:

@@ -906,8 +906,11 @@ impl BatchReader {
                 let _ = self.multi.carry_release(id);
             }
             if let Some(rt) = w.retry.as_ref() {
-                if rt.in_flight {
-                    let _ = self.multi.wait(rt.job);
+                if rt.in_flight && self.multi.wait(rt.job).is_ok() {
+                    // the round's ids for its parts still short of d: nobody collects them now
+                    for &id in rt.r_cout.iter().take(rt.g).filter(|&&id| id >= 0) {
+                        let _ = self.multi.carry_release(id);
+                    }
                 }
                 for &id in rt.cid.iter().filter(|&&id| id >= 0) {
                     let _ = self.multi.carry_release(id);

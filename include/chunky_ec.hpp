@@ -1283,7 +1283,11 @@ struct FileReference {
             for (size_t x = 0; x < R; ++x) {  // no job may still write into the window buffers
                 ReadWindow& w = win[x];
                 if (w.live && !w.checked) (void)cec_multi_wait(m, w.job);
-                if (w.retry.in_flight) (void)cec_multi_wait(m, w.retry.job);
+                if (w.retry.in_flight && cec_multi_wait(m, w.retry.job) == CEC_OK)
+                    // the round's ids for its parts still short of d: nobody collects them now
+                    for (size_t q = 0; q < w.retry.g && q < w.retry.carry_out.size(); ++q)
+                        if (w.retry.carry_out[q] >= 0)
+                            (void)cec_multi_carry_release(m, w.retry.carry_out[q]);
                 if (w.live)  // carry ids the failed read will not use go back to their GPUs
                     for (int32_t id : w.carry)
                         if (id >= 0) (void)cec_multi_carry_release(m, id);

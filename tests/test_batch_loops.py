@@ -16,7 +16,7 @@ import numpy as np
 import pytest
 
 import oracle
-from chunky_ec import OK, PRESENT_VERIFIED, TOO_FEW_SHARDS_PRESENT, EncodedPart, Sha256Hash
+from chunky_ec import OK, PRESENT_VERIFIED, TOO_FEW_SHARDS_PRESENT, EncodedPart, Error, Sha256Hash
 from _stores import Locations
 import chunky_ec.batchcheck as bc
 import chunky_ec.batchreader as br
@@ -536,3 +536,62 @@ def test_batch_reader_retries_of_the_last_windows_go_out_before_any_is_emitted(f
     # emitted (5 window buffers)
     assert r.multi.events == [("read", 4, False)] * 3 + [("read", 1, True), ("read", 4, False)] * 2 \
         + [("read", 1, True)], r.multi.events
+
+
+class _LazyFakeMulti(FakeMulti):
+    """FakeMulti whose jobs report done only after a seeded number of queries (wait always
+    completes them): the polling read loop sees windows and retry rounds finish out of order."""
+    rng = np.random.default_rng(0)
+
+    def __init__(self, *a, **kw):
+        super().__init__(*a, **kw)
+        self.polls = {}
+
+    def query(self, job):
+        assert job in self.live
+        left = self.polls.setdefault(job, int(self.rng.integers(0, 6)))
+        self.polls[job] = left - 1
+        return left <= 0
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_batch_reader_polling_loop_fuzz(fakes, monkeypatch, seed):
+    """Random location mixes (good, bad, unreadable, short copies; several per chunk), random
+    window size and depth, jobs finishing after random numbers of polls: every part comes out in
+    file order as stored, a part with fewer than d good chunks fails the read with
+    TooFewShardsPresent (the parts before it out), and afterwards no job is left unwaited and no
+    carry id held."""
+    monkeypatch.setattr(br, "Multi", _LazyFakeMulti)
+    _LazyFakeMulti.rng = np.random.default_rng(1000 + seed)
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(5, 40))
+    chunks, dig = _store(n, 50 + seed)
+    st = Locations(chunks)
+    good = {}
+    for k in range(n):
+        good[k] = 0
+        for i in range(T):
+            u = rng.random()
+            spec = (["good"] if u < 0.7 else ["bad", "good"] if u < 0.8 else
+                    ["gone", "short", "good"] if u < 0.86 else ["bad", "bad"] if u < 0.93 else
+                    ["gone"])
+            st.set(k, i, *spec)
+            good[k] += "good" in spec
+    ppb, depth = int(rng.integers(1, 5)), int(rng.integers(1, 6))
+    r = br.BatchReader(D, P, L, ppb, depth, [0], carry=bool(rng.integers(0, 2)))
+    got = []
+    short = [k for k in range(n) if good[k] < D]
+    try:
+        r.read(n, st.fetch, lambda k: dig[k],
+               lambda k, data: got.append((k, b"".join(bytes(x) for x in data))))
+        err = None
+    except Error as e:
+        err = e.code
+    assert [k for k, _ in got] == list(range(len(got)))
+    for k, b in got:
+        assert b == chunks[k, :D].tobytes(), (seed, k)
+    if short:
+        assert err == TOO_FEW_SHARDS_PRESENT and len(got) <= short[0], (seed, short, len(got))
+    else:
+        assert err is None and len(got) == n, seed
+    assert r.multi.live == set() and r.multi.pool == {}, seed
