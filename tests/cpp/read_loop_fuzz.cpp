@@ -1,0 +1,387 @@
+// read_loop_fuzz.cpp — the C++ host layer's batched read loop (FileReference::read_to over
+// read_run / retry_start / retry_round / retry_collect, include/chunky_ec.hpp) on the CPU, with
+// the scheduler replaced by a stand-in that keeps the C-ABI's job contract and computes with the
+// oracle (test infrastructure: this binary is built and run only by tests/test_cpp_read_fuzz.py).
+//
+// The stand-in (cec_multi_read_carry / _query / _wait / _carry_release below) computes a job
+// only when it completes: after a seeded number of cec_multi_query calls, or at
+// cec_multi_wait.  So jobs finish out of order, and a loop that touched a job's buffers before
+// the job was done, or read its results early, gets wrong bytes.  Carry ids follow the ABI
+// (include/chunky_ec.h: kept for one part, used once, refused for another part's digests).
+//
+// Each seed writes a store of random location mixes (good; [bad, good]; [gone, short, good];
+// [bad, bad]; gone -- file_part.rs:92-107's location walk), reads it with a random window
+// size, depth, shard list and carry switch, and checks: the bytes out are the file's, in order,
+// up to the first part with fewer than d good chunks, which fails the read with
+// TooFewShardsPresent; afterwards no job is left unwaited, no carry id is held, and no job broke
+// the contract.  Usage: read_loop_fuzz FIRST_SEED N_SEEDS.  Exit status 0 iff every seed passed.
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <random>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "chunky_ec.hpp"
+
+extern "C" {
+// oracle/cec_oracle.c
+void or_sha256(const uint8_t* buf, size_t len, uint8_t out[32]);
+int or_rs_encode_sep(size_t d, size_t p, const uint8_t* const* data, const size_t* data_lens,
+                     size_t n_data, uint8_t* const* parity, const size_t* parity_lens,
+                     size_t n_parity);
+int or_rs_reconstruct(size_t d, size_t p, uint8_t* const* shards, const size_t* lens,
+                      uint8_t* present, size_t n_shards, int data_only);
+}
+
+namespace {
+
+std::mt19937_64 g_poll_rng;  // how many queries a job takes to report done
+int g_violations = 0;        // contract breaches seen by the stand-in
+
+void violation(const char* what) {
+    std::fprintf(stderr, "  contract: %s\n", what);
+    ++g_violations;
+}
+
+}  // namespace
+
+struct cec_codec {
+    size_t d, p;
+};
+
+struct cec_multi {
+    size_t d, p, L, shards;
+    struct Job {
+        const uint8_t *chunks, *present, *expected;
+        size_t n;
+        uint8_t *data, *verified;
+        int* status;
+        const uint8_t** ptrs;
+        unsigned flags;
+        const int32_t* carry_in;
+        int32_t* carry_out;
+        int polls_left;
+        bool done = false;
+        int result = CEC_OK;
+    };
+    struct Entry {
+        std::vector<uint8_t> mask, expected, bytes;  // [t], [t][32], [t][L]
+    };
+    std::map<uint64_t, Job> jobs;  // submitted, not yet waited for
+    std::map<int32_t, Entry> pool;
+    uint64_t next_job = 1;
+    int32_t next_carry = 0;
+    uint64_t uploaded = 0, carried = 0;
+
+    // The job's compute, run at completion (file_part.rs:86-122 per part: verify the loaded
+    // chunks, decode from d verified ones, or TooFewShardsPresent with the verified ones kept).
+    void run(Job& j) {
+        const size_t t = d + p;
+        for (size_t k = 0; k < j.n; ++k) {
+            const uint8_t* pres = j.present + k * t;
+            const uint8_t* exp = j.expected + k * t * 32;
+            std::vector<std::vector<uint8_t>> ch(t);
+            const int32_t cid = j.carry_in ? j.carry_in[k] : -1;
+            const Entry* kept = nullptr;
+            if (cid >= 0) {
+                auto it = pool.find(cid);
+                if (it == pool.end()) {
+                    violation("carry id not held");
+                    j.result = CEC_ERR_INVALID_ARGUMENT;
+                    return;
+                }
+                kept = &it->second;
+                if (std::memcmp(kept->expected.data(), exp, t * 32) != 0) {
+                    violation("carry id of another part");
+                    j.result = CEC_ERR_INVALID_ARGUMENT;
+                    return;
+                }
+                for (size_t i = 0; i < t; ++i)
+                    if (pres[i] == CEC_PRESENT_VERIFIED && !kept->mask[i]) {
+                        violation("verified chunk not in the carry entry");
+                        j.result = CEC_ERR_INVALID_ARGUMENT;
+                        return;
+                    }
+            }
+            uint8_t* ver = j.verified + k * t;
+            size_t good = 0;
+            bool redone = false;
+            for (size_t i = 0; i < t; ++i) {
+                ver[i] = 0;
+                if (!pres[i]) continue;
+                if (kept && pres[i] == CEC_PRESENT_VERIFIED) {
+                    ch[i].assign(kept->bytes.begin() + i * L, kept->bytes.begin() + (i + 1) * L);
+                    ++carried;
+                } else {
+                    ch[i].assign(j.chunks + (k * t + i) * L, j.chunks + (k * t + i + 1) * L);
+                    ++uploaded;
+                }
+                if (pres[i] == CEC_PRESENT_VERIFIED) {
+                    ver[i] = 1;
+                } else {
+                    uint8_t h[32];
+                    or_sha256(ch[i].data(), L, h);
+                    ver[i] = std::memcmp(h, exp + i * 32, 32) == 0;
+                    redone = redone || !ver[i];
+                }
+                good += ver[i];
+            }
+            if (cid >= 0) pool.erase(cid);  // used once
+            if (j.carry_out) j.carry_out[k] = -1;
+            if (j.ptrs)
+                for (size_t i = 0; i < d; ++i) j.ptrs[k * d + i] = nullptr;
+            if (good < d) {
+                j.status[k] = CEC_TOO_FEW_SHARDS_PRESENT;
+                if (j.carry_out && good) {
+                    Entry e;
+                    e.mask.assign(ver, ver + t);
+                    e.expected.assign(exp, exp + t * 32);
+                    e.bytes.assign(t * L, 0);
+                    for (size_t i = 0; i < t; ++i)
+                        if (ver[i]) std::memcpy(&e.bytes[i * L], ch[i].data(), L);
+                    pool[next_carry] = std::move(e);
+                    j.carry_out[k] = next_carry++;
+                }
+                continue;
+            }
+            std::vector<uint8_t> present(t), buf(t * L);
+            std::vector<uint8_t*> ptr(t);
+            std::vector<size_t> lens(t, L);
+            for (size_t i = 0; i < t; ++i) {
+                ptr[i] = &buf[i * L];
+                present[i] = ver[i];
+                if (ver[i]) std::memcpy(ptr[i], ch[i].data(), L);
+            }
+            if (or_rs_reconstruct(d, p, ptr.data(), lens.data(), present.data(), t, 1) != 0) {
+                violation("oracle reconstruct failed");
+                j.result = CEC_ERR_INVALID_ARGUMENT;
+                return;
+            }
+            const bool rebuilt_only = (j.flags & CEC_READ_REBUILT_ONLY) != 0;
+            for (size_t i = 0; i < d; ++i) {
+                // REBUILT_ONLY: a loaded data chunk stays where the caller's buffer holds it
+                const bool in_place = rebuilt_only && !redone && pres[i] &&
+                                      !(kept && pres[i] == CEC_PRESENT_VERIFIED);
+                if (in_place) {
+                    j.ptrs[k * d + i] = j.chunks + (k * t + i) * L;
+                } else {
+                    std::memcpy(j.data + (k * d + i) * L, ptr[i], L);
+                    if (j.ptrs) j.ptrs[k * d + i] = j.data + (k * d + i) * L;
+                }
+            }
+            j.status[k] = CEC_OK;
+        }
+    }
+    void complete(Job& j) {
+        if (!j.done) {
+            j.done = true;
+            run(j);
+        }
+    }
+};
+
+extern "C" {
+
+const char* cec_status_name(int) { return "status"; }
+const char* cec_last_error(void) { return ""; }
+const char* cec_multi_last_error(void) { return "fake scheduler"; }
+int cec_current_device(int* device) {
+    *device = 0;
+    return CEC_OK;
+}
+
+int cec_codec_new(size_t d, size_t p, cec_codec** out) {
+    if (!d || !p || d + p > 256) return CEC_TOO_MANY_SHARDS;
+    *out = new cec_codec{d, p};
+    return CEC_OK;
+}
+void cec_codec_free(cec_codec* c) { delete c; }
+size_t cec_codec_data_shards(const cec_codec* c) { return c->d; }
+size_t cec_codec_parity_shards(const cec_codec* c) { return c->p; }
+size_t cec_codec_total_shards(const cec_codec* c) { return c->d + c->p; }
+
+// The per-part path's calls (a run of one part reads through read_with_context).
+int cec_sha256_many(const uint8_t* const* bufs, const size_t* lens, size_t n, uint8_t* out) {
+    for (size_t i = 0; i < n; ++i) or_sha256(bufs[i], lens[i], out + 32 * i);
+    return CEC_OK;
+}
+static int reconstruct(const cec_codec* c, uint8_t* const* shards, const size_t* lens,
+                       uint8_t* present, size_t n, int data_only) {
+    return or_rs_reconstruct(c->d, c->p, shards, lens, present, n, data_only);
+}
+int cec_reconstruct(const cec_codec* c, uint8_t* const* shards, const size_t* lens,
+                    uint8_t* present, size_t n) {
+    return reconstruct(c, shards, lens, present, n, 0);
+}
+int cec_reconstruct_data(const cec_codec* c, uint8_t* const* shards, const size_t* lens,
+                         uint8_t* present, size_t n) {
+    return reconstruct(c, shards, lens, present, n, 1);
+}
+
+int cec_host_alloc(size_t bytes, int, void** out) {
+    *out = std::malloc(bytes ? bytes : 1);
+    return *out ? CEC_OK : CEC_ERR_INVALID_ARGUMENT;
+}
+void cec_host_free(void* p) { std::free(p); }
+
+int cec_multi_new(const cec_codec* codec, size_t chunk_len, size_t, size_t, const int*,
+                  size_t n_devices, cec_multi** out) {
+    *out = new cec_multi{codec->d, codec->p, chunk_len, n_devices};
+    return CEC_OK;
+}
+void cec_multi_free(cec_multi* m) {
+    if (!m->jobs.empty()) violation("scheduler freed with jobs not waited for");
+    delete m;
+}
+
+int cec_multi_read_carry(cec_multi* m, const uint8_t* chunks, const uint8_t* present,
+                         const uint8_t* expected, size_t n, uint8_t* data, uint8_t* verified,
+                         int* status, const uint8_t** ptrs, unsigned flags,
+                         const int32_t* carry_in, int32_t* carry_out, uint64_t* job) {
+    if ((flags & CEC_READ_REBUILT_ONLY) && !ptrs) return CEC_ERR_INVALID_ARGUMENT;
+    if ((flags & CEC_MULTI_AHEAD) != (carry_in ? CEC_MULTI_AHEAD : 0u))
+        violation("retry rounds (and only they) go AHEAD");
+    cec_multi::Job j{chunks, present, expected, n,     data,      verified, status,
+                     ptrs,   flags,   carry_in, carry_out, int(g_poll_rng() % 6)};
+    *job = m->next_job++;
+    m->jobs.emplace(*job, j);
+    return CEC_OK;
+}
+int cec_multi_query(cec_multi* m, uint64_t job) {
+    auto it = m->jobs.find(job);
+    if (it == m->jobs.end()) return CEC_ERR_INVALID_ARGUMENT;
+    if (it->second.polls_left-- > 0) return 0;
+    m->complete(it->second);
+    return 1;
+}
+int cec_multi_wait(cec_multi* m, uint64_t job) {
+    auto it = m->jobs.find(job);
+    if (it == m->jobs.end()) {
+        violation("wait on a job not submitted or already waited for");
+        return CEC_ERR_INVALID_ARGUMENT;
+    }
+    m->complete(it->second);
+    const int r = it->second.result;
+    m->jobs.erase(it);
+    return r;
+}
+int cec_multi_carry_release(cec_multi* m, int32_t id) {
+    if (!m->pool.erase(id)) {
+        violation("release of an id not held");
+        return CEC_ERR_INVALID_ARGUMENT;
+    }
+    return CEC_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+using namespace chunky_ec;
+
+// One seed: a store, a read, the checks.  Returns true iff it passed.
+bool run_seed(uint64_t seed) {
+    std::mt19937_64 rng(seed);
+    auto uni = [&](size_t lo, size_t hi) { return lo + size_t(rng() % (hi - lo + 1)); };
+    const size_t d = uni(2, 5), p = uni(1, 3), t = d + p, L = 64 * uni(1, 8);
+    const size_t n = uni(5, 40);
+    g_poll_rng.seed(seed * 7919 + 1);
+
+    ChunkStore st;
+    FileReference file;
+    Bytes want;
+    size_t first_short = n;
+    for (size_t k = 0; k < n; ++k) {
+        std::vector<Bytes> c(t, Bytes(L));
+        for (size_t i = 0; i < d; ++i)
+            for (auto& b : c[i]) b = uint8_t(rng());
+        std::vector<const uint8_t*> dp(d);
+        std::vector<uint8_t*> pp(p);
+        std::vector<size_t> dl(d, L), pl(p, L);
+        for (size_t i = 0; i < d; ++i) dp[i] = c[i].data();
+        for (size_t i = 0; i < p; ++i) pp[i] = c[d + i].data();
+        if (or_rs_encode_sep(d, p, dp.data(), dl.data(), d, pp.data(), pl.data(), p) != 0) return false;
+        for (size_t i = 0; i < d; ++i) want.insert(want.end(), c[i].begin(), c[i].end());
+        FilePart part;
+        part.chunksize = L;
+        size_t good = 0;
+        for (size_t i = 0; i < t; ++i) {
+            std::array<uint8_t, 32> h{};
+            or_sha256(c[i].data(), L, h.data());
+            Chunk ch{Sha256Hash(h), {}};
+            const double u = double(rng() % 1000) / 1000.0;
+            const char* spec = u < 0.7 ? "G" : u < 0.8 ? "BG" : u < 0.86 ? "XSG" : u < 0.93 ? "BB" : "X";
+            for (size_t j = 0; spec[j]; ++j) {
+                const Location loc = std::to_string(k) + "/" + std::to_string(i) + "/" + std::to_string(j);
+                ch.locations.push_back(loc);
+                Bytes b = c[i];
+                switch (spec[j]) {
+                    case 'G': st.put(loc, b); ++good; break;
+                    case 'B': b[rng() % L] ^= uint8_t(1 + rng() % 255); st.put(loc, b); break;
+                    case 'S': b.resize(L / 2); st.put(loc, b); break;
+                    default: break;  // 'X': the location does not read
+                }
+            }
+            (i < d ? part.data : part.parity).push_back(std::move(ch));
+        }
+        if (good < d && first_short == n) first_short = k;
+        file.parts.push_back(std::move(part));
+    }
+    file.length = want.size();
+
+    const size_t ppb = uni(1, 4), depth = uni(1, 7);
+    const std::vector<int> devices = rng() % 2 ? std::vector<int>{0} : std::vector<int>{0, 0};
+    detail::read_carry() = rng() % 2 == 0;
+    Bytes got;
+    bool failed = false;
+    try {
+        file.read_to(st, [&](const uint8_t* b, size_t len) { got.insert(got.end(), b, b + len); },
+                     ppb, depth, devices);
+    } catch (const ErasureError& e) {
+        failed = e.error() == Error::TooFewShardsPresent;
+        if (!failed) {
+            std::fprintf(stderr, "seed %llu: unexpected erasure error\n", (unsigned long long)seed);
+            return false;
+        }
+    }
+    const cec_multi* m = detail::cached_multi_entry().multi.get();
+    bool ok = true;
+    auto expect = [&](bool c, const char* what) {
+        if (!c) {
+            std::fprintf(stderr, "seed %llu (d=%zu p=%zu L=%zu n=%zu ppb=%zu depth=%zu shards=%zu): %s\n",
+                         (unsigned long long)seed, d, p, L, n, ppb, depth, devices.size(), what);
+            ok = false;
+        }
+    };
+    expect(got.size() <= want.size() && std::memcmp(got.data(), want.data(), got.size()) == 0,
+           "bytes out differ from the file");
+    expect(got.size() % (d * L) == 0 || got.size() == want.size(), "a part cut short");
+    if (first_short < n) {
+        expect(failed, "a part without d good chunks did not fail the read");
+        expect(got.size() <= first_short * d * L, "parts after the failing one came out");
+    } else {
+        expect(!failed && got.size() == want.size(), "the read did not return the whole file");
+    }
+    expect(m && m->jobs.empty(), "jobs left unwaited");
+    expect(m && m->pool.empty(), "carry ids left held");
+    return ok;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    const uint64_t first = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : 0;
+    const uint64_t count = argc > 2 ? std::strtoull(argv[2], nullptr, 10) : 200;
+    size_t bad = 0;
+    for (uint64_t s = first; s < first + count; ++s) {
+        const int before = g_violations;
+        if (!run_seed(s) || g_violations != before) ++bad;
+    }
+    std::printf("%llu seeds, %zu failed, %d contract violations\n", (unsigned long long)count, bad,
+                g_violations);
+    return bad == 0 ? 0 : 1;
+}

@@ -1,0 +1,37 @@
+"""The C++ host layer's batched read loop (include/chunky_ec.hpp: FileReference::read_to over
+read_run / retry_start / retry_round / retry_collect, the twin of chunky_ec.batchreader and the Rust
+BatchReader) on the CPU: tests/cpp/read_loop_fuzz.cpp links the header against a stand-in
+scheduler that keeps cec_multi's job contract (jobs computed only when they complete, after a
+seeded number of cec_multi_query polls; carry ids kept per part and used once) and computes with
+the oracle.  Random location mixes, window sizes, depths, shard lists and carry switches: every
+part comes out as stored and in order, a part without d good chunks fails the read with
+TooFewShardsPresent (file_part.rs:92-107), and no job or carry id is left behind.  The same fuzz
+found a read that failed with a retry round in flight keeping that round's carry ids."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def fuzz_bin(tmp_path_factory):
+    if not (shutil.which("gcc") and shutil.which("g++")):
+        pytest.skip("no host compiler")
+    d = tmp_path_factory.mktemp("read_fuzz")
+    obj, exe = str(d / "oracle.o"), str(d / "read_loop_fuzz")
+    subprocess.run(["gcc", "-O2", "-c", os.path.join(ROOT, "oracle", "cec_oracle.c"), "-o", obj],
+                   check=True)
+    subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "cpp", "read_loop_fuzz.cpp"), obj, "-lpthread",
+                    "-o", exe], check=True)
+    return exe
+
+
+@pytest.mark.parametrize("first", [0, 1000])
+def test_cpp_read_loop_fuzz(fuzz_bin, first):
+    r = subprocess.run([fuzz_bin, str(first), "500"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr[-4000:]
+    assert "0 failed, 0 contract violations" in r.stdout
