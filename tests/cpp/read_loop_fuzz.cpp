@@ -10,11 +10,13 @@
 // (include/chunky_ec.h: kept for one part, used once, refused for another part's digests).
 //
 // Each seed writes a store of random location mixes (good; [bad, good]; [gone, short, good];
-// [bad, bad]; gone -- file_part.rs:92-107's location walk), reads it with a random window
+// [bad, bad]; bad; gone -- file_part.rs:92-107's location walk), reads it with a random window
 // size, depth, shard list and carry switch, and checks: the bytes out are the file's, in order,
 // up to the first part with fewer than d good chunks, which fails the read with
 // TooFewShardsPresent; afterwards no job is left unwaited, no carry id is held, and no job broke
-// the contract.  Usage: read_loop_fuzz FIRST_SEED N_SEEDS.  Exit status 0 iff every seed passed.
+// the contract.  Then verify and resilver run batched (check_run, cec_multi_verify / _resilver
+// stand-ins) and per part on copies of the file and store: same reports, same write-backs, and
+// the resilvered file reads back whole.  Usage: read_loop_fuzz FIRST_SEED N_SEEDS.  Exit status 0 iff every seed passed.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -67,6 +69,7 @@ struct cec_multi {
         int polls_left;
         bool done = false;
         int result = CEC_OK;
+        enum { READ, VERIFY, RESILVER } kind = READ;
     };
     struct Entry {
         std::vector<uint8_t> mask, expected, bytes;  // [t], [t][32], [t][L]
@@ -81,6 +84,47 @@ struct cec_multi {
     // chunks, decode from d verified ones, or TooFewShardsPresent with the verified ones kept).
     void run(Job& j) {
         const size_t t = d + p;
+        if (j.kind == Job::VERIFY) {  // every loaded row hashed, nothing decoded
+            for (size_t x = 0; x < j.n * t; ++x) {
+                uint8_t h[32];
+                if (j.present[x]) or_sha256(j.chunks + x * L, L, h);
+                j.verified[x] = j.present[x] && std::memcmp(h, j.expected + x * 32, 32) == 0;
+            }
+            return;
+        }
+        if (j.kind == Job::RESILVER) {  // file_part.rs:253-308: every chunk without a valid copy
+            for (size_t k = 0; k < j.n; ++k) {
+                std::vector<uint8_t> buf(t * L), present(t);
+                std::vector<uint8_t*> ptr(t);
+                std::vector<size_t> lens(t, L);
+                size_t good = 0;
+                for (size_t i = 0; i < t; ++i) {
+                    const size_t x = k * t + i;
+                    ptr[i] = &buf[i * L];
+                    uint8_t h[32];
+                    if (j.present[x] && j.present[x] != CEC_PRESENT_VERIFIED)
+                        or_sha256(j.chunks + x * L, L, h);
+                    j.verified[x] = j.present[x] == CEC_PRESENT_VERIFIED ||
+                                    (j.present[x] && std::memcmp(h, j.expected + x * 32, 32) == 0);
+                    if (j.verified[x]) std::memcpy(ptr[i], j.chunks + x * L, L);
+                    present[i] = j.verified[x];
+                    good += present[i];
+                }
+                if (good < d) {
+                    j.status[k] = CEC_TOO_FEW_SHARDS_PRESENT;
+                    continue;
+                }
+                if (or_rs_reconstruct(d, p, ptr.data(), lens.data(), present.data(), t, 0) != 0) {
+                    violation("oracle reconstruct failed");
+                    j.result = CEC_ERR_INVALID_ARGUMENT;
+                    return;
+                }
+                for (size_t i = 0; i < t; ++i)
+                    if (!j.verified[k * t + i]) std::memcpy(j.data + (k * t + i) * L, ptr[i], L);
+                j.status[k] = CEC_OK;
+            }
+            return;
+        }
         for (size_t k = 0; k < j.n; ++k) {
             const uint8_t* pres = j.present + k * t;
             const uint8_t* exp = j.expected + k * t * 32;
@@ -251,6 +295,26 @@ int cec_multi_read_carry(cec_multi* m, const uint8_t* chunks, const uint8_t* pre
     m->jobs.emplace(*job, j);
     return CEC_OK;
 }
+int cec_multi_verify(cec_multi* m, const uint8_t* chunks, const uint8_t* present,
+                     const uint8_t* expected, size_t n, uint8_t* verified, uint64_t* job) {
+    cec_multi::Job j{chunks, present, expected, n, nullptr, verified, nullptr, nullptr, 0u,
+                     nullptr, nullptr, int(g_poll_rng() % 6)};
+    j.kind = cec_multi::Job::VERIFY;
+    *job = m->next_job++;
+    m->jobs.emplace(*job, j);
+    return CEC_OK;
+}
+int cec_multi_resilver(cec_multi* m, const uint8_t* chunks, const uint8_t* present,
+                       const uint8_t* expected, size_t n, uint8_t* rebuilt, uint8_t* verified,
+                       int* status, const uint8_t** chunk_ptrs, uint64_t* job) {
+    if (chunk_ptrs) return CEC_ERR_INVALID_ARGUMENT;  // the loop passes none
+    cec_multi::Job j{chunks, present, expected, n, rebuilt, verified, status, nullptr, 0u,
+                     nullptr, nullptr, int(g_poll_rng() % 6)};
+    j.kind = cec_multi::Job::RESILVER;
+    *job = m->next_job++;
+    m->jobs.emplace(*job, j);
+    return CEC_OK;
+}
 int cec_multi_query(cec_multi* m, uint64_t job) {
     auto it = m->jobs.find(job);
     if (it == m->jobs.end()) return CEC_ERR_INVALID_ARGUMENT;
@@ -314,7 +378,12 @@ bool run_seed(uint64_t seed) {
             or_sha256(c[i].data(), L, h.data());
             Chunk ch{Sha256Hash(h), {}};
             const double u = double(rng() % 1000) / 1000.0;
-            const char* spec = u < 0.7 ? "G" : u < 0.8 ? "BG" : u < 0.86 ? "XSG" : u < 0.93 ? "BB" : "X";
+            const char* spec = u < 0.7    ? "G"
+                               : u < 0.78 ? "BG"
+                               : u < 0.83 ? "XSG"
+                               : u < 0.88 ? "BB"
+                               : u < 0.94 ? "B"
+                                          : "X";
             for (size_t j = 0; spec[j]; ++j) {
                 const Location loc = std::to_string(k) + "/" + std::to_string(i) + "/" + std::to_string(j);
                 ch.locations.push_back(loc);
@@ -368,6 +437,49 @@ bool run_seed(uint64_t seed) {
     }
     expect(m && m->jobs.empty(), "jobs left unwaited");
     expect(m && m->pool.empty(), "carry ids left held");
+
+    // verify and resilver (file_part.rs:228-390): the batched loops' reports and write-backs
+    // equal the per-part calls' on copies of the same file and store
+    FileReference fa = file, fb = file;
+    ChunkStore sa = st, sb = st;
+    auto same = [](const std::vector<PartReport>& a, const std::vector<PartReport>& b) {
+        if (a.size() != b.size()) return false;
+        for (size_t k = 0; k < a.size(); ++k)
+            if (a[k].locations != b[k].locations || a[k].chunks != b[k].chunks ||
+                a[k].new_locations != b[k].new_locations || a[k].write_error != b[k].write_error)
+                return false;
+        return true;
+    };
+    expect(same(fa.verify(sa), fb.verify(sb, ppb, depth, devices)), "batched verify reports differ");
+    const std::vector<PartReport> rb = fb.resilver(sb, ppb, depth, devices);
+    expect(same(fa.resilver(sa), rb), "batched resilver reports differ");
+    bool same_store = true, unrepaired = false;
+    for (size_t k = 0; k < n; ++k) {
+        unrepaired = unrepaired || rb[k].write_error.has_value();
+        for (size_t i = 0; i < t; ++i) {
+            const Chunk &ca = fa.parts[k].chunk(i), &cb = fb.parts[k].chunk(i);
+            same_store = same_store && ca.locations == cb.locations;
+            for (const Location& loc : ca.locations) {
+                const Bytes *x = sa.find(loc), *y = sb.find(loc);
+                same_store = same_store && (x && y ? *x == *y : x == y);
+            }
+        }
+    }
+    expect(same_store, "batched resilver wrote other locations or bytes");
+    expect(unrepaired == (first_short < n), "a part without d good chunks was rebuilt, or one with d was not");
+    // the resilvered file reads back whole, up to a part resilver could not rebuild
+    Bytes back;
+    bool failed_again = false;
+    try {
+        fb.read_to(sb, [&](const uint8_t* b, size_t len) { back.insert(back.end(), b, b + len); },
+                   ppb, depth, devices);
+    } catch (const ErasureError&) {
+        failed_again = true;
+    }
+    expect(failed_again == unrepaired, "read after resilver failed or passed unexpectedly");
+    expect(unrepaired || back == want, "read after resilver differs from the file");
+    m = detail::cached_multi_entry().multi.get();
+    expect(m && m->jobs.empty() && m->pool.empty(), "verify / resilver left a job or carry id");
     return ok;
 }
 

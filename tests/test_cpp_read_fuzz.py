@@ -5,8 +5,11 @@ scheduler that keeps cec_multi's job contract (jobs computed only when they comp
 seeded number of cec_multi_query polls; carry ids kept per part and used once) and computes with
 the oracle.  Random location mixes, window sizes, depths, shard lists and carry switches: every
 part comes out as stored and in order, a part without d good chunks fails the read with
-TooFewShardsPresent (file_part.rs:92-107), and no job or carry id is left behind.  The same fuzz
-found a read that failed with a retry round in flight keeping that round's carry ids."""
+TooFewShardsPresent (file_part.rs:92-107), and no job or carry id is left behind.  Then the
+batched verify / resilver loop (check_run) against the per-part FilePart::verify / resilver on
+copies of the same file and store: same reports, same write-backs, and the resilvered file reads
+back whole (file_part.rs:228-390).  The fuzz found a read that failed with a retry round in flight
+keeping that round's carry ids (fixed)."""
 import os
 import shutil
 import subprocess
