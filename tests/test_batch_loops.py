@@ -595,3 +595,51 @@ def test_batch_reader_polling_loop_fuzz(fakes, monkeypatch, seed):
     else:
         assert err is None and len(got) == n, seed
     assert r.multi.live == set() and r.multi.pool == {}, seed
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_batch_checker_fuzz(fakes, monkeypatch, seed):
+    """BatchChecker verify and resilver over random location mixes (one or several copies per
+    chunk: good, bad, short, unreadable; chunks with no location), random window size, depth and
+    shard list, against a model of file_part.rs:228-390: every location's result (valid /
+    invalid / unavailable), and resilver rebuilding exactly the chunks with no valid copy, with the
+    stored bytes, or TooFewShardsPresent for a part with fewer than d of them; no job left."""
+    monkeypatch.setattr(bc, "Multi", _LazyFakeMulti)
+    _LazyFakeMulti.rng = np.random.default_rng(2000 + seed)
+    rng = np.random.default_rng(100 + seed)
+    n = int(rng.integers(3, 30))
+    chunks, dig = _store(n, 70 + seed)
+    st = Locations(chunks)
+    want = {}
+    kinds = ["good", "bad", "short", "gone"]
+    res = {"good": True, "bad": False, "short": False, "gone": None}
+    for k in range(n):
+        for i in range(T):
+            if rng.random() < 0.6:
+                spec = ["good"]
+            else:
+                spec = [kinds[int(x)] for x in rng.choice(4, int(rng.integers(0, 4)), p=[.35, .3, .1, .25])]
+            st.set(k, i, *spec)
+            want[(k, i)] = [res[s] for s in spec]
+    ppb, depth = int(rng.integers(1, 5)), int(rng.integers(1, 6))
+    devices = [0] if rng.integers(0, 2) else [0, 0]
+    c = bc.BatchChecker(D, P, L, ppb, depth, devices)
+    got = {}
+    c.verify(n, st.read_all, lambda k: dig[k], lambda k, part: got.__setitem__(k, part))
+    assert sorted(got) == list(range(n)) and c.multi.live == set()
+    for k in range(n):
+        assert got[k].locations == [want[(k, i)] for i in range(T)], (seed, k)
+    fixed = {}
+    c.resilver(n, st.read_all, lambda k: dig[k],
+               lambda k, part: fixed.__setitem__(k, (part, {i: bytes(b) for i, b in
+                                                            part.rebuilt.items()})))
+    assert sorted(fixed) == list(range(n)) and c.multi.live == set()
+    for k in range(n):
+        part, rebuilt = fixed[k]
+        assert part.locations == [want[(k, i)] for i in range(T)], (seed, k)
+        lost = [i for i in range(T) if True not in want[(k, i)]]
+        if T - len(lost) < D:
+            assert part.error == TOO_FEW_SHARDS_PRESENT and rebuilt == {}, (seed, k)
+        else:
+            assert part.error is None and sorted(rebuilt) == lost, (seed, k)
+            assert all(rebuilt[i] == chunks[k, i].tobytes() for i in lost), (seed, k)
