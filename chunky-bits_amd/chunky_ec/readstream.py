@@ -194,15 +194,17 @@ class ReadRepairStream:
 
         Every batch takes the queued retries first and fills the rest with new parts, so a retried
         part goes out in the next batch and batches stay full (a batch costs about one SHA-256
-        chain of time whatever its size); only after the last new part do batches of retries
-        alone go out."""
+        chain of time whatever its size).  After the last new part, retries wait until every
+        batch in flight is in and then go out together: one batch (one SHA-256 chain, ~40 ms for
+        1 MiB chunks) for the retries of the last `depth` batches instead of one batch each,
+        which ran one after another (profiles/r6/c5r_sizes: the stream's fixed cost)."""
         nxt, end = first, first + n_parts
         t_run = time.perf_counter()
         while nxt < end or self._retry or self._inflight:
             # a slot is reused round-robin: collect the oldest batch before its slot is acquired
             if len(self._inflight) == self.depth:
                 self._collect()
-            if nxt < end or self._retry:
+            if nxt < end or (self._retry and not self._inflight):
                 parts, present = self._retry_parts()
                 room = self.P - len(parts)
                 if nxt < end and room > 0:

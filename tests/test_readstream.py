@@ -260,3 +260,49 @@ def test_read_repair_stream_carries_verified_chunks(cap):
             seen.setdefault(part, set()).update(new)
     assert not fp.pool or fp.released  # entries are used or released, never left behind
     assert sorted(fp.free) == list(range(fp.cap))
+
+
+def test_read_repair_stream_last_retries_go_out_together():
+    """After the last new part, the retries of the batches still in flight wait for all of them
+    and go out as one batch (each retry round costs one SHA-256 chain whatever its size): every
+    retry-only batch is submitted with nothing else in flight, and the parts still decode."""
+    d, p, L, P, depth, n = 4, 3, 64, 6, 4, 60
+    chunks, dig = _store(n, d, p, L, 21)
+    rng = np.random.default_rng(8)
+
+    class Counting(FakeReadPipeline):
+        def __init__(self, *a):
+            super().__init__(*a)
+            self.out = 0
+            self.log = []  # (rows, batches in flight when submitted)
+
+        def submit(self, slot, n):
+            self.log.append((self.slots[slot]["present"][:n].copy(), self.out))
+            self.out += 1
+            super().submit(slot, n)
+
+        def wait(self, slot):
+            self.out -= 1
+            return super().wait(slot)
+
+    def fetch(slot_chunks, rows):
+        for k, part, flags in rows:
+            for j in np.flatnonzero(flags):
+                slot_chunks[k, j] = chunks[part, j]
+                if flags[j] == 1 and rng.random() < 0.15:
+                    slot_chunks[k, j, rng.integers(L)] ^= 0x5A
+
+    fp = Counting(d, p, L, P, depth)
+    got = {}
+    s = ReadRepairStream(fp, fetch, lambda ids: dig[ids], seed=2,
+                         on_part=lambda slot, nb, k, part, tries: got.__setitem__(
+                             part, fp.slots[slot]["res"][0][k].copy())).run(0, n)
+    assert s.parts + s.undecodable_parts == n
+    assert all(np.array_equal(out, chunks[part, :d]) for part, out in got.items())
+    last_new = max(i for i, (rows, _) in enumerate(fp.log)
+                   if any(not (r == PRESENT_VERIFIED).any() for r in rows))
+    tail = fp.log[last_new + 1:]
+    assert tail and s.retry_batches == len(tail)
+    assert all(busy == 0 for _, busy in tail)
+    # the retries of the last `depth` batches went out together: fewer tail batches than that
+    assert len(tail) < depth
