@@ -1,0 +1,238 @@
+"""Lexical and call-shape checks of the Rust crate (chunky-bits_amd/rust/chunky-ec-sys), which no
+cargo in this image compiles: every source file tokenizes (comments, strings, raw strings, char
+literals vs lifetimes) with balanced brackets, and every call of a method the crate defines --
+`self.f(..)` in an impl block and `self.multi.f(..)` / `self.rp.f(..)` on the crate's own
+wrappers -- names a method that exists with that many arguments.  A renamed method or a call
+left with the old argument list (as an FFI wrapper grows a parameter) fails here."""
+import os
+import re
+
+import pytest
+
+SRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "chunky-bits_amd",
+                   "rust", "chunky-ec-sys", "src")
+FILES = sorted(f for f in os.listdir(SRC) if f.endswith(".rs"))
+
+
+def tokens(src):
+    """(kind, text, line) for Rust source: kinds ident, punct, str, char, num, lifetime."""
+    out, i, line, n = [], 0, 1, len(src)
+    while i < n:
+        c = src[i]
+        if c == "\n":
+            line += 1
+            i += 1
+        elif c.isspace():
+            i += 1
+        elif src.startswith("//", i):
+            j = src.find("\n", i)
+            i = n if j < 0 else j
+        elif src.startswith("/*", i):  # nested block comments
+            depth, j = 1, i + 2
+            while depth and j < n:
+                if src.startswith("/*", j):
+                    depth, j = depth + 1, j + 2
+                elif src.startswith("*/", j):
+                    depth, j = depth - 1, j + 2
+                else:
+                    j += 1
+            assert depth == 0, f"unterminated block comment from line {line}"
+            line += src.count("\n", i, j)
+            i = j
+        elif re.match(r'b?r#*"', src[i:i + 8]):  # raw (byte) string
+            m = re.match(r'(b?r)(#*)"', src[i:])
+            end = '"' + m.group(2)
+            j = src.find(end, i + len(m.group(0)))
+            assert j >= 0, f"unterminated raw string at line {line}"
+            j += len(end)
+            out.append(("str", src[i:j], line))
+            line += src.count("\n", i, j)
+            i = j
+        elif c == '"' or src.startswith('b"', i):
+            j = i + (2 if c == "b" else 1)
+            while j < n and src[j] != '"':
+                j += 2 if src[j] == "\\" else 1
+            assert j < n, f"unterminated string at line {line}"
+            out.append(("str", src[i:j + 1], line))
+            line += src.count("\n", i, j)
+            i = j + 1
+        elif c == "'" or src.startswith("b'", i):
+            k = i + (1 if c == "b" else 0)
+            m = re.match(r"'(\\(?:u\{[0-9a-fA-F]+\}|x[0-9a-fA-F]{2}|.)|[^\\'])'", src[k:])
+            if m:
+                out.append(("char", src[i:k + len(m.group(0))], line))
+                i = k + len(m.group(0))
+            else:
+                m = re.match(r"'[A-Za-z_][A-Za-z0-9_]*", src[i:])
+                assert m, f"stray quote at line {line}"
+                out.append(("lifetime", m.group(0), line))
+                i += len(m.group(0))
+        elif c.isalpha() or c == "_":
+            m = re.match(r"[A-Za-z_][A-Za-z0-9_]*", src[i:])
+            out.append(("ident", m.group(0), line))
+            i += len(m.group(0))
+        elif c.isdigit():
+            m = re.match(r"[0-9][0-9a-zA-Z_]*(\.[0-9][0-9_]*)?([eE][+-]?[0-9]+)?[a-z0-9]*", src[i:])
+            out.append(("num", m.group(0), line))
+            i += len(m.group(0))
+        else:
+            two = src[i:i + 2]
+            if two in ("::", "->", "=>", "==", "!=", "<=", ">=", "&&", "||", "..", "+=", "-=",
+                       "*=", "|=", "&=", "^=", "<<", ">>"):
+                out.append(("punct", two, line))
+                i += 2
+            else:
+                out.append(("punct", c, line))
+                i += 1
+    return out
+
+
+def _read(f):
+    return open(os.path.join(SRC, f)).read()
+
+
+@pytest.mark.parametrize("name", FILES)
+def test_rust_source_tokenizes_with_balanced_brackets(name):
+    stack = []
+    pairs = {")": "(", "]": "[", "}": "{"}
+    for kind, text, line in tokens(_read(name)):
+        if kind != "punct":
+            continue
+        if text in "([{":
+            stack.append((text, line))
+        elif text in ")]}":
+            assert stack, f"{name}:{line}: unmatched {text}"
+            opened, at = stack.pop()
+            assert opened == pairs[text], f"{name}:{line}: {text} closes {opened} of line {at}"
+    assert not stack, f"{name}: unclosed {stack[-1]}"
+
+
+def _group(toks, i):
+    """Index just past the bracket group opening at toks[i]."""
+    depth = 0
+    for j in range(i, len(toks)):
+        t = toks[j][1] if toks[j][0] == "punct" else None
+        if t in ("(", "[", "{"):
+            depth += 1
+        elif t in (")", "]", "}"):
+            depth -= 1
+            if depth == 0:
+                return j + 1
+    raise AssertionError("unbalanced")
+
+
+def _args(toks, i):
+    """Number of top-level arguments of the call whose '(' is toks[i] (closures' |a, b| skipped)."""
+    end = _group(toks, i)
+    inner = toks[i + 1:end - 1]
+    if not inner:
+        return 0
+    count, j, at_start = 1, 0, True
+    while j < len(inner):
+        kind, t, _ = inner[j]
+        if kind == "punct" and t in ("(", "[", "{"):
+            j = i + 1 + j
+            j = _group(toks, j) - (i + 1)
+            at_start = False
+            continue
+        if kind == "punct" and t == "|" and at_start:  # closure parameters
+            j += 1
+            while not (inner[j][0] == "punct" and inner[j][1] == "|"):
+                j += 1
+        elif kind == "punct" and t == "||" and at_start:
+            pass
+        elif kind == "ident" and t == "move" and at_start:
+            j += 1
+            continue
+        elif kind == "punct" and t == ",":
+            if j + 1 < len(inner):
+                count += 1
+            at_start = True
+            j += 1
+            continue
+        at_start = False
+        j += 1
+    return count
+
+
+def _methods(src):
+    """{name: [parameter counts, self excluded]} of every fn with a self receiver, by impl type."""
+    toks = tokens(src)
+    out = {}
+    impl = None
+    depth, impl_depth = 0, None
+    for i, (kind, t, _) in enumerate(toks):
+        if kind == "punct" and t == "{":
+            depth += 1
+        elif kind == "punct" and t == "}":
+            depth -= 1
+            if impl_depth is not None and depth < impl_depth:
+                impl, impl_depth = None, None
+        elif kind == "ident" and t == "impl" and impl is None:
+            j = i + 1
+            if toks[j][1] == "<":  # impl<T>
+                while toks[j][1] != ">":
+                    j += 1
+                j += 1
+            name = toks[j][1]
+            # `impl Trait for Type`
+            k = j
+            while toks[k][1] != "{":
+                if toks[k][1] == "for":
+                    name = toks[k + 1][1]
+                k += 1
+            impl, impl_depth = name, depth + 1
+        elif kind == "ident" and t == "fn" and impl is not None:
+            name = toks[i + 1][1]
+            j = i + 2
+            if toks[j][1] == "<":
+                lvl = 0
+                while True:
+                    lvl += {"<": 1, ">": -1, ">>": -2, "<<": 2}.get(toks[j][1], 0)
+                    j += 1
+                    if lvl <= 0:
+                        break
+            assert toks[j][1] == "(", (name, toks[j])
+            n = _args(toks, j)
+            has_self = any(x[1] == "self" for x in toks[j + 1:_group(toks, j)][:3])
+            if has_self:
+                out.setdefault(impl, {}).setdefault(name, set()).add(n - 1)
+    return out
+
+
+def test_method_calls_name_existing_methods_with_their_arity():
+    defs = {}
+    for f in FILES:
+        for impl, ms in _methods(_read(f)).items():
+            for name, ns in ms.items():
+                defs.setdefault(impl, {}).setdefault(name, set()).update(ns)
+    assert "Multi" in defs and "BatchReader" in defs
+    receivers = {"multi": "Multi", "rp": "ReadPipeline"}
+    checked = 0
+    for f in FILES:
+        toks = tokens(_read(f))
+        # the impl type around each position
+        for i in range(len(toks) - 4):
+            if toks[i][1] != "self" or toks[i + 1][1] != ".":
+                continue
+            if toks[i + 3][1] == "(" and toks[i + 2][0] == "ident":
+                owner, name, paren = None, toks[i + 2][1], i + 3
+                # self.f(..): a method of whichever impl defines it in this crate
+                cands = [t for t, ms in defs.items() if name in ms]
+                if not cands:
+                    continue  # a std trait method (clone, iter, ...)
+                n = _args(toks, paren)
+                assert any(n in defs[t][name] for t in cands), \
+                    f"{f}:{toks[i][2]}: self.{name}() with {n} args; defined {[defs[t][name] for t in cands]}"
+                checked += 1
+            elif (toks[i + 2][1] in receivers and toks[i + 3][1] == "." and toks[i + 5][1] == "("
+                  if i + 5 < len(toks) else False):
+                owner, name = receivers[toks[i + 2][1]], toks[i + 4][1]
+                if owner not in defs:
+                    continue
+                assert name in defs[owner], f"{f}:{toks[i][2]}: {owner} has no method {name}"
+                n = _args(toks, i + 5)
+                assert n in defs[owner][name], \
+                    f"{f}:{toks[i][2]}: self.{toks[i + 2][1]}.{name}() with {n} args, defined {defs[owner][name]}"
+                checked += 1
+    assert checked > 50
