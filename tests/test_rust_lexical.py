@@ -2,8 +2,9 @@
 cargo in this image compiles: every source file tokenizes (comments, strings, raw strings, char
 literals vs lifetimes) with balanced brackets, and every call of a method the crate defines --
 `self.f(..)` in an impl block and `self.multi.f(..)` / `self.rp.f(..)` on the crate's own
-wrappers -- names a method that exists with that many arguments.  A renamed method or a call
-left with the old argument list (as an FFI wrapper grows a parameter) fails here."""
+wrappers -- names a method that exists with that many arguments, and so does every call of the
+crate's free and associated functions.  A renamed method or a call left with the old argument
+list (as an FFI wrapper grows a parameter) fails here."""
 import os
 import re
 
@@ -156,7 +157,8 @@ def _args(toks, i):
 
 
 def _methods(src):
-    """{name: [parameter counts, self excluded]} of every fn with a self receiver, by impl type."""
+    """{impl type: {name: parameter counts}} of every fn with a self receiver (self excluded),
+    {"Type::": ...} of the associated functions and {"": ...} of the free functions."""
     toks = tokens(src)
     out = {}
     impl = None
@@ -197,6 +199,13 @@ def _methods(src):
             has_self = any(x[1] == "self" for x in toks[j + 1:_group(toks, j)][:3])
             if has_self:
                 out.setdefault(impl, {}).setdefault(name, set()).add(n - 1)
+            else:  # an associated function: Type::name(..)
+                out.setdefault(impl + "::", {}).setdefault(name, set()).add(n)
+        elif kind == "ident" and t == "fn" and impl is None and toks[i + 2][1] in ("(", "<"):
+            j = i + 2
+            while toks[j][1] != "(":
+                j += 1
+            out.setdefault("", {}).setdefault(toks[i + 1][1], set()).add(_args(toks, j))
     return out
 
 
@@ -236,3 +245,35 @@ def test_method_calls_name_existing_methods_with_their_arity():
                     f"{f}:{toks[i][2]}: self.{toks[i + 2][1]}.{name}() with {n} args, defined {defs[owner][name]}"
                 checked += 1
     assert checked > 50
+
+
+def test_function_calls_match_the_crates_definitions():
+    """Free functions (`draw_order(..)`) and associated functions (`Multi::new(..)`) of the crate
+    are called with as many arguments as they take."""
+    defs = {}
+    for f in FILES:
+        for impl, ms in _methods(_read(f)).items():
+            for name, ns in ms.items():
+                defs.setdefault(impl, {}).setdefault(name, set()).update(ns)
+    free = defs.get("", {})
+    assert "draw_order" in free or "next_copy" in free or len(free) > 3
+    checked = 0
+    for f in FILES:
+        toks = tokens(_read(f))
+        for i in range(1, len(toks) - 1):
+            kind, name, line = toks[i]
+            if kind != "ident" or toks[i + 1][1] != "(" or toks[i - 1][1] in ("fn", ".", "!"):
+                continue
+            if toks[i - 1][1] == "::":
+                owner = toks[i - 2][1] + "::"
+                if owner == "Self::":
+                    continue  # resolved by the impl in scope; the method check covers self calls
+                if owner in defs and name in defs[owner]:
+                    n = _args(toks, i + 1)
+                    assert n in defs[owner][name], f"{f}:{line}: {owner}{name}() with {n} args"
+                    checked += 1
+            elif name in free:
+                n = _args(toks, i + 1)
+                assert n in free[name], f"{f}:{line}: {name}() with {n} args, defined {free[name]}"
+                checked += 1
+    assert checked > 20
