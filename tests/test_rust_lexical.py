@@ -277,3 +277,68 @@ def test_function_calls_match_the_crates_definitions():
                 assert n in free[name], f"{f}:{line}: {name}() with {n} args, defined {free[name]}"
                 checked += 1
     assert checked > 20
+
+
+def _struct_fields(toks):
+    """{struct name: field names} of the named-field structs."""
+    out = {}
+    for i, (kind, t, _) in enumerate(toks):
+        if kind == "ident" and t == "struct":
+            name = toks[i + 1][1]
+            j = i + 2
+            while toks[j][1] not in ("{", ";", "("):
+                j += 1
+            if toks[j][1] != "{":
+                continue
+            end = _group(toks, j)
+            fields, depth = set(), 0
+            for k in range(j + 1, end - 1):
+                x = toks[k][1]
+                if x in ("(", "[", "{", "<"):
+                    depth += 1
+                elif x in (")", "]", "}", ">"):
+                    depth -= 1
+                elif x == ">>":
+                    depth -= 2
+                elif (depth == 0 and toks[k][0] == "ident" and toks[k + 1][1] == ":"
+                      and toks[k - 1][1] in ("{", ",", "pub", ")")):
+                    fields.add(x)
+            out[name] = fields
+    return out
+
+
+def test_self_fields_exist_in_their_struct():
+    """Inside `impl Type`, every `self.name` that is not a call names a field of struct Type."""
+    fields = {}
+    for f in FILES:
+        fields.update(_struct_fields(tokens(_read(f))))
+    assert "BatchReader" in fields and "windows" in fields["BatchReader"]
+    checked = 0
+    for f in FILES:
+        toks = tokens(_read(f))
+        impl, depth, impl_depth = None, 0, None
+        for i, (kind, t, line) in enumerate(toks):
+            if kind == "punct" and t == "{":
+                depth += 1
+            elif kind == "punct" and t == "}":
+                depth -= 1
+                if impl_depth is not None and depth < impl_depth:
+                    impl, impl_depth = None, None
+            elif kind == "ident" and t == "impl" and impl is None:
+                j = i + 1
+                if toks[j][1] == "<":
+                    while toks[j][1] != ">":
+                        j += 1
+                    j += 1
+                name, k = toks[j][1], j
+                while toks[k][1] != "{":
+                    if toks[k][1] == "for":
+                        name = toks[k + 1][1]
+                    k += 1
+                impl, impl_depth = name, depth + 1
+            elif (impl in fields and kind == "ident" and t == "self" and toks[i + 1][1] == "."
+                  and toks[i + 2][0] == "ident" and toks[i + 3][1] not in ("(", "::")):
+                name = toks[i + 2][1]
+                assert name in fields[impl], f"{f}:{line}: {impl} has no field {name}"
+                checked += 1
+    assert checked > 100
