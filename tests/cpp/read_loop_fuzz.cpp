@@ -16,7 +16,8 @@
 // TooFewShardsPresent; afterwards no job is left unwaited, no carry id is held, and no job broke
 // the contract.  Then verify and resilver run batched (check_run, cec_multi_verify / _resilver
 // stand-ins) and per part on copies of the file and store: same reports, same write-backs, and
-// the resilvered file reads back whole.  Usage: read_loop_fuzz FIRST_SEED N_SEEDS.  Exit status 0 iff every seed passed.
+// the resilvered file reads back whole.  Each seed first writes a file through the batched and
+// the per-part write paths (same parts and stored bytes).  Usage: read_loop_fuzz FIRST_SEED N_SEEDS.  Exit status 0 iff every seed passed.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -51,6 +52,19 @@ void violation(const char* what) {
 
 }  // namespace
 
+// Parity and the d+p digests of one part whose d data chunks are data[0 .. d*L).
+void encode_part(size_t d, size_t p, size_t L, const uint8_t* data, uint8_t* parity,
+                 uint8_t* digests) {
+    std::vector<const uint8_t*> dp(d);
+    std::vector<uint8_t*> pp(p);
+    std::vector<size_t> dl(d, L), pl(p, L);
+    for (size_t i = 0; i < d; ++i) dp[i] = data + i * L;
+    for (size_t i = 0; i < p; ++i) pp[i] = parity + i * L;
+    if (or_rs_encode_sep(d, p, dp.data(), dl.data(), d, pp.data(), pl.data(), p) != 0)
+        violation("oracle encode failed");
+    for (size_t i = 0; i < d + p; ++i) or_sha256(i < d ? dp[i] : pp[i - d], L, digests + 32 * i);
+}
+
 struct cec_codec {
     size_t d, p;
 };
@@ -69,7 +83,7 @@ struct cec_multi {
         int polls_left;
         bool done = false;
         int result = CEC_OK;
-        enum { READ, VERIFY, RESILVER } kind = READ;
+        enum { READ, VERIFY, RESILVER, WRITE } kind = READ;
     };
     struct Entry {
         std::vector<uint8_t> mask, expected, bytes;  // [t], [t][32], [t][L]
@@ -84,6 +98,12 @@ struct cec_multi {
     // chunks, decode from d verified ones, or TooFewShardsPresent with the verified ones kept).
     void run(Job& j) {
         const size_t t = d + p;
+        if (j.kind == Job::WRITE) {  // write_with_encoder's compute: parity + every digest
+            for (size_t k = 0; k < j.n; ++k)
+                encode_part(d, p, L, j.chunks + k * d * L, j.data + k * p * L,
+                            j.verified + k * t * 32);
+            return;
+        }
         if (j.kind == Job::VERIFY) {  // every loaded row hashed, nothing decoded
             for (size_t x = 0; x < j.n * t; ++x) {
                 uint8_t h[32];
@@ -266,6 +286,15 @@ int cec_reconstruct_data(const cec_codec* c, uint8_t* const* shards, const size_
     return reconstruct(c, shards, lens, present, n, 1);
 }
 
+int cec_part_encode(const cec_codec* c, const uint8_t* data_buf, size_t length, uint8_t* parity,
+                    uint8_t* digests, size_t* chunksize) {
+    if (!length) return CEC_EMPTY_SHARD;
+    const size_t L = (length + c->d - 1) / c->d;
+    encode_part(c->d, c->p, L, data_buf, parity, digests);
+    *chunksize = L;
+    return CEC_OK;
+}
+
 int cec_host_alloc(size_t bytes, int, void** out) {
     *out = std::malloc(bytes ? bytes : 1);
     return *out ? CEC_OK : CEC_ERR_INVALID_ARGUMENT;
@@ -291,6 +320,15 @@ int cec_multi_read_carry(cec_multi* m, const uint8_t* chunks, const uint8_t* pre
         violation("retry rounds (and only they) go AHEAD");
     cec_multi::Job j{chunks, present, expected, n,     data,      verified, status,
                      ptrs,   flags,   carry_in, carry_out, int(g_poll_rng() % 6)};
+    *job = m->next_job++;
+    m->jobs.emplace(*job, j);
+    return CEC_OK;
+}
+int cec_multi_encode_hash(cec_multi* m, const uint8_t* data, size_t n, uint8_t* parity,
+                          uint8_t* digests, uint64_t* job) {
+    cec_multi::Job j{data, nullptr, nullptr, n, parity, digests, nullptr, nullptr, 0u,
+                     nullptr, nullptr, int(g_poll_rng() % 6)};
+    j.kind = cec_multi::Job::WRITE;
     *job = m->next_job++;
     m->jobs.emplace(*job, j);
     return CEC_OK;
@@ -354,6 +392,40 @@ bool run_seed(uint64_t seed) {
     const size_t d = uni(2, 5), p = uni(1, 3), t = d + p, L = 64 * uni(1, 8);
     const size_t n = uni(5, 40);
     g_poll_rng.seed(seed * 7919 + 1);
+
+    // write (writer.rs:117-255): the batched path (FileWriteBuilder::batch over cec_multi jobs)
+    // and the per-part path give the same parts, digests, locations and stored bytes, the short
+    // last part included
+    {
+        const size_t cap = d * L, parts = uni(2, 12);
+        Bytes file_bytes(parts * cap - (rng() % 2 ? uni(1, cap - 1) : 0));
+        for (auto& b : file_bytes) b = uint8_t(rng());
+        ChunkStore sa, sb;
+        auto builder = [&] {
+            FileWriteBuilder w;
+            w.chunk_size(L).data_chunks(d).parity_chunks(p).concurrency(uni(2, 10));
+            return w;
+        };
+        const FileReference fa = builder().write(file_bytes, sa);
+        FileWriteBuilder wb = builder();
+        wb.batch(uni(1, 3), uni(1, 4)).devices(rng() % 2 ? std::vector<int>{0} : std::vector<int>{0, 0});
+        const FileReference fb = wb.write(file_bytes, sb);
+        bool same = fa.parts.size() == fb.parts.size() && fa.length == fb.length &&
+                    sa.size() == sb.size();
+        for (size_t k = 0; same && k < fa.parts.size(); ++k)
+            for (size_t i = 0; same && i < t; ++i) {
+                const Chunk &ca = fa.parts[k].chunk(i), &cb = fb.parts[k].chunk(i);
+                same = fa.parts[k].chunksize == fb.parts[k].chunksize && ca.hash == cb.hash &&
+                       ca.locations == cb.locations && *sa.find(ca.locations[0]) == *sb.find(cb.locations[0]);
+            }
+        Bytes back;
+        fb.read_to(sb, [&](const uint8_t* b, size_t len) { back.insert(back.end(), b, b + len); });
+        if (!same || back != file_bytes) {
+            std::fprintf(stderr, "seed %llu: batched write differs from the per-part write\n",
+                         (unsigned long long)seed);
+            return false;
+        }
+    }
 
     ChunkStore st;
     FileReference file;
@@ -491,7 +563,13 @@ int main(int argc, char** argv) {
     size_t bad = 0;
     for (uint64_t s = first; s < first + count; ++s) {
         const int before = g_violations;
-        if (!run_seed(s) || g_violations != before) ++bad;
+        bool ok = false;
+        try {
+            ok = run_seed(s);
+        } catch (const std::exception& e) {
+            std::fprintf(stderr, "seed %llu: uncaught %s\n", (unsigned long long)s, e.what());
+        }
+        if (!ok || g_violations != before) ++bad;
     }
     std::printf("%llu seeds, %zu failed, %d contract violations\n", (unsigned long long)count, bad,
                 g_violations);

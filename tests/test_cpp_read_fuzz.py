@@ -8,7 +8,9 @@ part comes out as stored and in order, a part without d good chunks fails the re
 TooFewShardsPresent (file_part.rs:92-107), and no job or carry id is left behind.  Then the
 batched verify / resilver loop (check_run) against the per-part FilePart::verify / resilver on
 copies of the same file and store: same reports, same write-backs, and the resilvered file reads
-back whole (file_part.rs:228-390).  The fuzz found a read that failed with a retry round in flight
+back whole (file_part.rs:228-390); and each seed first writes a file through the batched write
+(FileWriteBuilder::batch over cec_multi_encode_hash jobs) and the per-part write: same parts,
+digests, locations and stored bytes (writer.rs:117-255).  The fuzz found a read that failed with a retry round in flight
 keeping that round's carry ids (fixed)."""
 import os
 import shutil
