@@ -1,23 +1,24 @@
-// read_loop_fuzz.cpp — the C++ host layer's batched read loop (FileReference::read_to over
-// read_run / retry_start / retry_round / retry_collect, include/chunky_ec.hpp) on the CPU, with
-// the scheduler replaced by a stand-in that keeps the C-ABI's job contract and computes with the
-// oracle (test infrastructure: this binary is built and run only by tests/test_cpp_read_fuzz.py).
+// host_loop_fuzz.cpp — the C++ host layer's batched loops (include/chunky_ec.hpp: the write's
+// write_full_parts, the read's read_run / retry_start / retry_round / retry_collect, verify and
+// resilver's check_run) on the CPU, with the scheduler replaced by a stand-in that keeps the
+// C-ABI's job contract and computes with the oracle (test infrastructure: this binary is built and
+// run only by tests/test_cpp_loop_fuzz.py).
 //
-// The stand-in (cec_multi_read_carry / _query / _wait / _carry_release below) computes a job
-// only when it completes: after a seeded number of cec_multi_query calls, or at
-// cec_multi_wait.  So jobs finish out of order, and a loop that touched a job's buffers before
-// the job was done, or read its results early, gets wrong bytes.  Carry ids follow the ABI
-// (include/chunky_ec.h: kept for one part, used once, refused for another part's digests).
+// The stand-in (cec_multi_* below) computes a job only when it completes: after a seeded number
+// of cec_multi_query calls, or at cec_multi_wait.  So jobs finish out of order, and a loop that
+// touched a job's buffers before the job was done, or read its results early, gets wrong bytes.
+// Carry ids follow the ABI (include/chunky_ec.h: kept for one part, used once, refused for
+// another part's digests).
 //
-// Each seed writes a store of random location mixes (good; [bad, good]; [gone, short, good];
-// [bad, bad]; bad; gone -- file_part.rs:92-107's location walk), reads it with a random window
-// size, depth, shard list and carry switch, and checks: the bytes out are the file's, in order,
-// up to the first part with fewer than d good chunks, which fails the read with
-// TooFewShardsPresent; afterwards no job is left unwaited, no carry id is held, and no job broke
-// the contract.  Then verify and resilver run batched (check_run, cec_multi_verify / _resilver
-// stand-ins) and per part on copies of the file and store: same reports, same write-backs, and
-// the resilvered file reads back whole.  Each seed first writes a file through the batched and
-// the per-part write paths (same parts and stored bytes).  Usage: read_loop_fuzz FIRST_SEED N_SEEDS.  Exit status 0 iff every seed passed.
+// Each seed: (1) writes a file through the batched and the per-part write paths (same parts,
+// digests, locations and stored bytes); (2) builds a store of random location mixes (good;
+// [bad, good]; [gone, short, good]; [bad, bad]; bad; gone -- file_part.rs:92-107's location
+// walk) and reads it with a random window size, depth, shard list and carry switch: the bytes out
+// are the file's, in order, up to the first part with fewer than d good chunks, which fails the
+// read with TooFewShardsPresent, and afterwards no job is left unwaited and no carry id held;
+// (3) runs verify and resilver batched and per part on copies of the file and store: same
+// reports, same write-backs, and the resilvered file reads back whole.  No job may break the
+// contract.  Usage: host_loop_fuzz FIRST_SEED N_SEEDS; exit status 0 iff every seed passed.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>

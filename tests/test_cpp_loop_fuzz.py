@@ -1,6 +1,6 @@
-"""The C++ host layer's batched read loop (include/chunky_ec.hpp: FileReference::read_to over
-read_run / retry_start / retry_round / retry_collect, the twin of chunky_ec.batchreader and the Rust
-BatchReader) on the CPU: tests/cpp/read_loop_fuzz.cpp links the header against a stand-in
+"""The C++ host layer's batched loops (include/chunky_ec.hpp; the read: FileReference::read_to
+over read_run / retry_start / retry_round / retry_collect, the twin of chunky_ec.batchreader and
+the Rust BatchReader) on the CPU: tests/cpp/host_loop_fuzz.cpp links the header against a stand-in
 scheduler that keeps cec_multi's job contract (jobs computed only when they complete, after a
 seeded number of cec_multi_query polls; carry ids kept per part and used once) and computes with
 the oracle.  Random location mixes, window sizes, depths, shard lists and carry switches: every
@@ -26,17 +26,17 @@ def fuzz_bin(tmp_path_factory):
     if not (shutil.which("gcc") and shutil.which("g++")):
         pytest.skip("no host compiler")
     d = tmp_path_factory.mktemp("read_fuzz")
-    obj, exe = str(d / "oracle.o"), str(d / "read_loop_fuzz")
+    obj, exe = str(d / "oracle.o"), str(d / "host_loop_fuzz")
     subprocess.run(["gcc", "-O2", "-c", os.path.join(ROOT, "oracle", "cec_oracle.c"), "-o", obj],
                    check=True)
     subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
-                    os.path.join(ROOT, "tests", "cpp", "read_loop_fuzz.cpp"), obj, "-lpthread",
+                    os.path.join(ROOT, "tests", "cpp", "host_loop_fuzz.cpp"), obj, "-lpthread",
                     "-o", exe], check=True)
     return exe
 
 
 @pytest.mark.parametrize("first", [0, 1000])
-def test_cpp_read_loop_fuzz(fuzz_bin, first):
+def test_cpp_host_loop_fuzz(fuzz_bin, first):
     r = subprocess.run([fuzz_bin, str(first), "500"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr[-4000:]
     assert "0 failed, 0 contract violations" in r.stdout

@@ -196,7 +196,7 @@ def test_batch_reader_mirrors_the_cpp_and_python_loops():
     drain = drain[:drain.index("\n    }\n")]
     assert "carry_release(" in drain and "rt.cid" in drain and "self.multi.wait(rt.job)" in drain
     # a round in flight when the read fails: its ids for parts still short of d go back too
-    # (the leak tests/cpp/read_loop_fuzz.cpp and test_batch_reader_polling_loop_fuzz found)
+    # (the leak tests/cpp/host_loop_fuzz.cpp and test_batch_reader_polling_loop_fuzz found)
     assert "rt.r_cout.iter().take(rt.g)" in drain
     py = open(os.path.join(ROOT, "chunky-bits_amd", "chunky_ec", "batchreader.py")).read()
     for s in ("def _load", "def _submit", "def _check", "def _poll", "def _finish",
