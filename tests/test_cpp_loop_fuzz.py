@@ -37,6 +37,6 @@ def fuzz_bin(tmp_path_factory):
 
 @pytest.mark.parametrize("first", [0, 1000])
 def test_cpp_host_loop_fuzz(fuzz_bin, first):
-    r = subprocess.run([fuzz_bin, str(first), "500"], capture_output=True, text=True, timeout=300)
+    r = subprocess.run([fuzz_bin, str(first), "300"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr[-4000:]
     assert "0 failed, 0 contract violations" in r.stdout
