@@ -643,3 +643,35 @@ def test_batch_checker_fuzz(fakes, monkeypatch, seed):
         else:
             assert part.error is None and sorted(rebuilt) == lost, (seed, k)
             assert all(rebuilt[i] == chunks[k, i].tobytes() for i in lost), (seed, k)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_batch_reader_sink_error_leaves_nothing(fakes, monkeypatch, seed):
+    """A sink that raises part way through a damaged read (jobs finishing out of order): the
+    error reaches the caller, every job is waited for, every carry id given back, and the reader
+    then reads the same store whole."""
+    monkeypatch.setattr(br, "Multi", _LazyFakeMulti)
+    _LazyFakeMulti.rng = np.random.default_rng(3000 + seed)
+    rng = np.random.default_rng(200 + seed)
+    n = int(rng.integers(8, 30))
+    chunks, dig = _store(n, 90 + seed)
+    st = Locations(chunks)
+    for k in range(n):
+        for i in range(T):
+            if rng.random() < 0.15:
+                st.set(k, i, "bad", "good")
+    r = br.BatchReader(D, P, L, int(rng.integers(1, 4)), int(rng.integers(1, 5)), [0])
+    stop = int(rng.integers(0, n))
+
+    def sink(k, data):
+        if k == stop:
+            raise KeyError("sink closed")
+    with pytest.raises(KeyError):
+        r.read(n, st.fetch, lambda k: dig[k], sink)
+    assert r.multi.live == set() and r.multi.pool == {}, seed
+    got = []
+    r.read(n, st.fetch, lambda k: dig[k],
+           lambda k, data: got.append((k, b"".join(bytes(x) for x in data))))
+    assert [k for k, _ in got] == list(range(n))
+    assert all(b == chunks[k, :D].tobytes() for k, b in got)
+    assert r.multi.live == set() and r.multi.pool == {}, seed
