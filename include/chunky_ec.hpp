@@ -792,16 +792,37 @@ struct FileReference {
     template <typename Sink>
     void read_to(const ChunkStore& src, Sink&& sink, size_t parts_per_batch = 0, size_t depth = 4,
                  const std::vector<int>& devices = {}) const {
-        uint64_t left = std::numeric_limits<uint64_t>::max();
-        if (length) left = *length;
+        read_span_to(src, 0, parts.size(), 0, len_bytes(), sink, parts_per_batch, depth, devices);
+    }
+    // FileReference::len_bytes (file_reference.rs:49-56): `length`, else the parts' bytes.
+    uint64_t len_bytes() const {
+        if (length) return *length;
+        uint64_t total = 0;
+        for (const FilePart& part : parts) total += part.len_bytes();
+        return total;
+    }
+    // Parts [k_begin, k_end) read as read_to reads them; of their bytes (d*L per part, the
+    // padding of a short part included) the first `skip` are dropped and at most `limit` go to
+    // the sink -- reader.rs:40-67's read_skip and bytes_remaining (FileReadBuilder below).
+    template <typename Sink>
+    void read_span_to(const ChunkStore& src, size_t k_begin, size_t k_end, uint64_t skip,
+                      uint64_t limit, Sink&& sink, size_t parts_per_batch = 0, size_t depth = 4,
+                      const std::vector<int>& devices = {}) const {
+        k_end = std::min(k_end, parts.size());
+        if (k_begin >= k_end) return;
         auto emit = [&](const uint8_t* p, size_t n) {
-            const size_t m = size_t(std::min<uint64_t>(n, left));
+            const size_t s = size_t(std::min<uint64_t>(n, skip));
+            p += s;
+            n -= s;
+            skip -= s;
+            const size_t m = size_t(std::min<uint64_t>(n, limit));
             if (m) sink(p, m);
-            left -= m;
+            limit -= m;
         };
         if (!parts_per_batch) {  // FileReadBuilder: part reads buffered(5) (reader.rs:63)
             detail::ordered_concurrent(
-                parts.size(), kReadBuffer, [&](size_t k) { return parts[k].read_with_context(src); },
+                k_end - k_begin, kReadBuffer,
+                [&](size_t k) { return parts[k_begin + k].read_with_context(src); },
                 [&](size_t, const Bytes& b) { emit(b.data(), b.size()); });
             return;
         }
@@ -814,7 +835,7 @@ struct FileReference {
             } else {
                 read_run(src, k0, n, parts_per_batch, depth, devices, emit);
             }
-        });
+        }, k_begin, k_end);
     }
     // FileReference::verify / resilver (file_reference.rs:78-113 over FilePart::verify /
     // resilver, file_part.rs:228-390).  parts_per_batch > 0: runs of parts of one shape go
@@ -859,14 +880,16 @@ struct FileReference {
     }
 
    private:
-    // fn(k0, n) over runs of parts of one shape (whole shape: chunk size, d and p); runs of one
-    // part when batching is off.
+    // fn(k0, n) over runs of parts of one shape (whole shape: chunk size, d and p) among parts
+    // [k_begin, k_end); runs of one part when batching is off.
     template <typename Fn>
-    void for_runs(size_t parts_per_batch, Fn fn) const {
-        size_t k = 0;
-        while (k < parts.size()) {
+    void for_runs(size_t parts_per_batch, Fn fn, size_t k_begin = 0,
+                  size_t k_end = std::numeric_limits<size_t>::max()) const {
+        k_end = std::min(k_end, parts.size());
+        size_t k = k_begin;
+        while (k < k_end) {
             size_t run = 1;
-            while (parts_per_batch && k + run < parts.size() &&
+            while (parts_per_batch && k + run < k_end &&
                    parts[k + run].chunksize == parts[k].chunksize &&
                    parts[k + run].data.size() == parts[k].data.size() &&
                    parts[k + run].parity.size() == parts[k].parity.size())
@@ -1439,6 +1462,70 @@ struct FileReference {
 // file::FileWriteBuilder (writer.rs:88-255): the part loop of write().  Parts are
 // d*chunk_size bytes of the input (the last one shorter), each zero padded and handed to
 // FilePart::write_with_encoder with one shared codec.
+// FileReadBuilder (reader.rs:22-173): a file's bytes from `seek` on, `take` of them (0: to the
+// end), read from the parts that hold them -- the HTTP gateway's range reads (http.rs:37-56).
+// Parts wholly before `seek` are not read and the first part's leading bytes are dropped, as the
+// reference does (reader.rs:44-65).  Parts wholly past the range are not read either: the
+// reference still reads every part after it and empties its bytes (the stream's map,
+// reader.rs:67-75), so an undecodable part past the range fails its read and not this one; the
+// range's bytes are the same.  batch() / devices() pick the batched path (FileReference::read_to).
+class FileReadBuilder {
+   public:
+    explicit FileReadBuilder(const FileReference& file) : file_(&file) {}
+    FileReadBuilder& seek(uint64_t s) {
+        seek_ = s;
+        return *this;
+    }
+    FileReadBuilder& take(uint64_t n) {
+        take_ = n;
+        return *this;
+    }
+    FileReadBuilder& batch(size_t parts_per_batch, size_t depth = 4) {
+        batch_ = parts_per_batch;
+        depth_ = depth;
+        return *this;
+    }
+    FileReadBuilder& devices(std::vector<int> devs) {
+        devices_ = std::move(devs);
+        return *this;
+    }
+    uint64_t get_seek() const { return seek_; }
+    const FileReference& file_reference() const { return *file_; }
+    // reader.rs:129-138 (a seek past the end gives 0 here; the reference's u64 subtraction would
+    // underflow there).
+    uint64_t len_bytes() const {
+        const uint64_t length = file_->len_bytes();
+        if (take_ == 0) return length > seek_ ? length - seek_ : 0;
+        if (length > seek_ + take_) return take_;
+        return length > seek_ ? length - seek_ : 0;
+    }
+    template <typename Sink>
+    void read_to(const ChunkStore& src, Sink&& sink) const {
+        const uint64_t want = len_bytes();
+        if (want == 0) return;
+        const std::vector<FilePart>& parts = file_->parts;
+        size_t k = 0;
+        uint64_t skip = seek_;
+        while (k < parts.size() && skip >= parts[k].len_bytes()) skip -= parts[k++].len_bytes();
+        size_t end = k;
+        for (uint64_t covered = 0; end < parts.size() && covered < skip + want; ++end)
+            covered += parts[end].len_bytes();
+        file_->read_span_to(src, k, end, skip, want, sink, batch_, depth_, devices_);
+    }
+    Bytes read(const ChunkStore& src) const {
+        Bytes out;
+        out.reserve(size_t(len_bytes()));
+        read_to(src, [&](const uint8_t* p, size_t n) { out.insert(out.end(), p, p + n); });
+        return out;
+    }
+
+   private:
+    const FileReference* file_;
+    uint64_t seek_ = 0, take_ = 0;
+    size_t batch_ = 0, depth_ = 4;
+    std::vector<int> devices_;
+};
+
 class FileWriteBuilder {
    public:
     FileWriteBuilder& chunk_size(size_t n) {

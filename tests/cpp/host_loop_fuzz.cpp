@@ -434,6 +434,7 @@ bool run_seed(uint64_t seed) {
     FileReference file;
     Bytes want;
     size_t first_short = n;
+    std::vector<size_t> short_parts;
     for (size_t k = 0; k < n; ++k) {
         std::vector<Bytes> c(t, Bytes(L));
         for (size_t i = 0; i < d; ++i)
@@ -473,6 +474,7 @@ bool run_seed(uint64_t seed) {
             (i < d ? part.data : part.parity).push_back(std::move(ch));
         }
         if (good < d && first_short == n) first_short = k;
+        if (good < d) short_parts.push_back(k);
         file.parts.push_back(std::move(part));
     }
     file.length = want.size();
@@ -535,6 +537,39 @@ bool run_seed(uint64_t seed) {
     }
     expect(m && m->jobs.empty(), "jobs left unwaited");
     expect(m && m->pool.empty(), "carry ids left held");
+
+    // range reads (FileReadBuilder::seek / take, reader.rs:22-173; the gateway's Range requests):
+    // the range's bytes, read from the parts that hold them -- a part without d good chunks fails
+    // the read only when the range reaches into it
+    for (int r = 0; r < 3; ++r) {
+        // a third of the seeks on a part boundary (the part before must not be read)
+        const uint64_t seek = rng() % 3 == 0 ? (rng() % (n + 1)) * d * L : rng() % (want.size() + 2);
+        const uint64_t take = rng() % 3 == 0 ? 0 : rng() % (want.size() + 2);
+        FileReadBuilder rb(file);
+        rb.seek(seek).take(take);
+        if (rng() % 2) rb.batch(ppb, depth).devices(devices);
+        const uint64_t len = rb.len_bytes();
+        const uint64_t exp_len = seek >= want.size() ? 0 : take == 0 ? want.size() - seek
+                                                                   : std::min<uint64_t>(take, want.size() - seek);
+        expect(len == exp_len, "len_bytes differs from reader.rs:129-138");
+        const size_t k_lo = size_t(seek / (d * L)), k_hi = size_t((seek + len + d * L - 1) / (d * L));
+        const bool reaches_short = len && std::any_of(short_parts.begin(), short_parts.end(),
+                                                      [&](size_t k) { return k >= k_lo && k < k_hi; });
+        Bytes part_bytes;
+        bool range_failed = false;
+        try {
+            part_bytes = rb.read(st);
+        } catch (const ErasureError&) {
+            range_failed = true;
+        }
+        expect(range_failed == reaches_short, "range read failed or passed unexpectedly");
+        if (!range_failed)
+            expect(part_bytes.size() == len &&
+                   std::equal(part_bytes.begin(), part_bytes.end(), want.begin() + std::ptrdiff_t(std::min<uint64_t>(seek, want.size()))),
+                   "range bytes differ from the file's");
+        m = detail::cached_multi_entry().multi.get();
+        expect(m && m->jobs.empty() && m->pool.empty(), "a range read left a job or carry id");
+    }
 
     // verify and resilver (file_part.rs:228-390): the batched loops' reports and write-backs
     // equal the per-part calls' on copies of the same file and store

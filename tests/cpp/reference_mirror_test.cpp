@@ -11,6 +11,8 @@
 //   test_cluster_digests        golden fixture of the same write (tests/golden, pinned oracle)
 //   test_cp_50mib               BASELINE configs[0]: `cp` of a 50 MiB file, d=3 p=2, 1 MiB
 //                               chunks: 17 parts, last chunksize 699 051, read back bit-exact
+//   test_range_reads            FileReadBuilder::seek / take (reader.rs:22-173) over the same
+//                               file: the gateway's range reads, per part and batched
 //   test_batched_paths          FileWriteBuilder::batch / FileReference::read batched through
 //                               the host-staged pipelines == the per-part path, bit-exact
 //   test_locations_bad_then_good  chunks listed [bad copy, good copy]: read walks the locations,
@@ -201,6 +203,34 @@ void test_cp_50mib() {
         store.erase(part.parity[1].locations[0]);
     }
     CHECK(f.read(store) == input);
+}
+
+// FileReadBuilder::seek / take (reader.rs:22-173), the gateway's Range / Prefix / Suffix reads
+// (http.rs:37-56) of the 50 MiB cp file, holes in every part: the range's bytes, per part and
+// batched; len_bytes as reader.rs:129-138.
+void test_range_reads() {
+    const size_t length = size_t(50) << 20, part = size_t(3) << 20;
+    const Bytes input = random_bytes(length, 51);
+    ChunkStore store;
+    const FileReference f =
+        FileWriteBuilder().chunk_size(size_t(1) << 20).data_chunks(3).parity_chunks(2).write(input, store);
+    for (const auto& pt : f.parts) store.erase(pt.data[1].locations[0]);
+    const uint64_t ranges[][2] = {{0, 0},           {0, 10},          {part - 1, 2},
+                                  {part, part},     {5 * part + 7, 0}, {length - 699051, 0},
+                                  {length - 1, 0},  {length - 100, 1000}, {length, 0},
+                                  {1234567, 20 << 20}};
+    for (const auto& r : ranges) {
+        const uint64_t want = r[0] >= length ? 0 : r[1] == 0 ? length - r[0]
+                                                             : std::min<uint64_t>(r[1], length - r[0]);
+        for (size_t batch : {size_t(0), size_t(4)}) {
+            FileReadBuilder rb(f);
+            rb.seek(r[0]).take(r[1]).batch(batch);
+            CHECK(rb.len_bytes() == want && rb.get_seek() == r[0]);
+            const Bytes got = rb.read(store);
+            CHECK(got.size() == want);
+            CHECK(std::equal(got.begin(), got.end(), input.begin() + std::ptrdiff_t(std::min<uint64_t>(r[0], length))));
+        }
+    }
 }
 
 // FileWriteBuilder::concurrency (writer.rs:106-130): 2 and 64 part tasks at once give the
@@ -584,6 +614,7 @@ const Test kTests[] = {
     {"test_resilver", test_resilver},
     {"test_cluster_digests", test_cluster_digests},
     {"test_cp_50mib", test_cp_50mib},
+    {"test_range_reads", test_range_reads},
     {"test_write_concurrency", test_write_concurrency},
     {"test_batched_paths", test_batched_paths},
     {"test_multi_device_paths", test_multi_device_paths},

@@ -10,6 +10,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(ROOT, "tests", "cpp", "reference_mirror_test")
 NAMES = ["sha256", "test_file_write", "test_resilver", "test_cluster_digests", "test_cp_50mib",
+         "test_range_reads",
          "test_write_concurrency",
          "test_batched_paths", "test_multi_device_paths", "test_mixed_shape_read",
          "test_batched_verify_resilver", "test_locations_bad_then_good", "test_one_encode",
