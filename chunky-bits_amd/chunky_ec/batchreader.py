@@ -464,11 +464,13 @@ class FileReader:
         return c
 
     def read(self, shapes: Sequence[Shape], fetch: Fetch, digests: Callable[[int], np.ndarray],
-             sink: Callable[[int, List], None]) -> None:
-        k = 0
-        while k < len(shapes):
+             sink: Callable[[int, List], None], first: int = 0, end: Optional[int] = None) -> None:
+        """Parts [first, end) (default: every part) to ``sink(part, data_chunks)`` in order."""
+        end = len(shapes) if end is None else min(end, len(shapes))
+        k = first
+        while k < end:
             run = 1
-            while k + run < len(shapes) and shapes[k + run] == shapes[k]:
+            while k + run < end and shapes[k + run] == shapes[k]:
                 run += 1
             d, p, L = shapes[k]
             if run < 2:
@@ -480,3 +482,51 @@ class FileReader:
                     run, lambda q, i, s: fetch(k0 + q, i, s), lambda q: digests(k0 + q),
                     lambda q, data: sink(k0 + q, data))
             k += run
+
+    def read_range(self, shapes: Sequence[Shape], length: int, seek: int, take: int, fetch: Fetch,
+                   digests: Callable[[int], np.ndarray], sink: Callable[[int, List], None]) -> int:
+        """FileReadBuilder::seek / take (reader.rs:22-173): the file's bytes [seek, seek +
+        range_len) -- ``length`` is FileReference::len_bytes -- from the parts that hold them,
+        ``sink(part, pieces)`` getting each part's bytes inside the range as memoryviews.  Parts
+        wholly before the range are not read and the first part's leading bytes are dropped, as
+        the reference does (reader.rs:44-65); parts wholly past it are not read either (the
+        reference reads them and empties their bytes, reader.rs:67-75: an undecodable part past
+        the range fails its read, not this one).  Returns the bytes handed out."""
+        want = range_len(length, seek, take)
+        if want == 0:
+            return 0
+        part_len = [d * L for d, _, L in shapes]
+        k, skip = 0, seek
+        while k < len(shapes) and skip >= part_len[k]:
+            skip -= part_len[k]
+            k += 1
+        end, covered = k, 0
+        while end < len(shapes) and covered < skip + want:
+            covered += part_len[end]
+            end += 1
+        state = {"skip": skip, "left": want}
+
+        def trim(q, data):
+            pieces = []
+            for c in data:
+                c = memoryview(c)
+                s = min(len(c), state["skip"])
+                state["skip"] -= s
+                c = c[s:]
+                m = min(len(c), state["left"])
+                state["left"] -= m
+                if m:
+                    pieces.append(c[:m])
+            sink(q, pieces)
+
+        self.read(shapes, fetch, digests, trim, k, end)
+        return want - state["left"]
+
+
+def range_len(length: int, seek: int, take: int) -> int:
+    """FileReadBuilder::len_bytes (reader.rs:129-138): the bytes a read from ``seek`` taking
+    ``take`` (0: to the end) gives of a ``length``-byte file; 0 for a seek past the end (where the
+    reference's u64 subtraction would underflow)."""
+    if take == 0 or length <= seek + take:
+        return max(length - seek, 0)
+    return take

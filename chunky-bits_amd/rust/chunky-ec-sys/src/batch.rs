@@ -1019,18 +1019,30 @@ impl<K: PartialEq + Copy, V> ShapeCache<K, V> {
 }
 
 /// Runs of consecutive equal shapes: (first part, parts in the run).
-fn shape_runs(shapes: &[Shape]) -> Vec<(usize, usize)> {
+fn shape_runs(shapes: &[Shape], first: usize, end: usize) -> Vec<(usize, usize)> {
     let mut runs = Vec::new();
-    let mut k = 0;
-    while k < shapes.len() {
+    let end = end.min(shapes.len());
+    let mut k = first;
+    while k < end {
         let mut n = 1;
-        while k + n < shapes.len() && shapes[k + n] == shapes[k] {
+        while k + n < end && shapes[k + n] == shapes[k] {
             n += 1;
         }
         runs.push((k, n));
         k += n;
     }
     runs
+}
+
+/// `FileReadBuilder::len_bytes` (reader.rs:129-138): the bytes a read from `seek` taking `take`
+/// (0: to the end) gives of a `length`-byte file; 0 for a seek past the end (where the reference's
+/// u64 subtraction would underflow).
+pub fn range_len(length: u64, seek: u64, take: u64) -> u64 {
+    if take == 0 || length <= seek.saturating_add(take) {
+        length.saturating_sub(seek)
+    } else {
+        take
+    }
 }
 
 /// `FileReadBuilder`'s reader over a whole file (reader.rs:32-74): consecutive parts of one shape
@@ -1064,6 +1076,77 @@ impl FileReader {
         &mut self,
         shapes: &[Shape],
         digests: &[[u8; 32]],
+        fetch: F,
+        sink: S,
+    ) -> Result<(), BatchReadError<E>>
+    where
+        F: FnMut(usize, usize, usize) -> Option<(usize, Vec<u8>)>,
+        S: FnMut(usize, &[&[u8]]) -> Result<(), E>,
+    {
+        self.read_parts(shapes, digests, 0, shapes.len(), fetch, sink)
+    }
+
+    /// `FileReadBuilder::seek` / `take` (reader.rs:22-173; the gateway's Range reads, http.rs:
+    /// 37-56): the file's bytes `[seek, seek + range_len(length, seek, take))` -- `length` is
+    /// `FileReference::len_bytes` -- from the parts that hold them, `sink(part, pieces)` getting
+    /// each part's bytes inside the range.  Parts wholly before the range are not read and the
+    /// first part's leading bytes are dropped, as the reference does (reader.rs:44-65); parts
+    /// wholly past it are not read either (the reference reads them and empties their bytes,
+    /// reader.rs:67-75, so an undecodable part past the range fails its read and not this one).
+    /// Returns the bytes handed out.
+    pub fn read_range<F, S, E>(
+        &mut self,
+        shapes: &[Shape],
+        digests: &[[u8; 32]],
+        length: u64,
+        seek: u64,
+        take: u64,
+        fetch: F,
+        mut sink: S,
+    ) -> Result<u64, BatchReadError<E>>
+    where
+        F: FnMut(usize, usize, usize) -> Option<(usize, Vec<u8>)>,
+        S: FnMut(usize, &[&[u8]]) -> Result<(), E>,
+    {
+        let want = range_len(length, seek, take);
+        if want == 0 {
+            return Ok(0);
+        }
+        let part_len = |k: usize| (shapes[k].0 * shapes[k].2) as u64;
+        let (mut first, mut skip) = (0usize, seek);
+        while first < shapes.len() && skip >= part_len(first) {
+            skip -= part_len(first);
+            first += 1;
+        }
+        let (mut end, mut covered) = (first, 0u64);
+        while end < shapes.len() && covered < skip + want {
+            covered += part_len(end);
+            end += 1;
+        }
+        let mut left = want;
+        self.read_parts(shapes, digests, first, end, fetch, |k, data| {
+            let mut pieces: Vec<&[u8]> = Vec::with_capacity(data.len());
+            for &c in data {
+                let s = (c.len() as u64).min(skip) as usize;
+                skip -= s as u64;
+                let m = ((c.len() - s) as u64).min(left) as usize;
+                left -= m as u64;
+                if m > 0 {
+                    pieces.push(&c[s..s + m]);
+                }
+            }
+            sink(k, &pieces)
+        })?;
+        Ok(want - left)
+    }
+
+    /// Parts `[first, end)` to `sink` in file order (as [`FileReader::read`]).
+    pub fn read_parts<F, S, E>(
+        &mut self,
+        shapes: &[Shape],
+        digests: &[[u8; 32]],
+        first: usize,
+        end: usize,
         mut fetch: F,
         mut sink: S,
     ) -> Result<(), BatchReadError<E>>
@@ -1081,7 +1164,7 @@ impl FileReader {
             return Err(BatchReadError::Engine(crate::too_small("digests")));
         }
         let (ppb, depth) = (self.parts_per_batch, self.depth);
-        for (k0, n) in shape_runs(shapes) {
+        for (k0, n) in shape_runs(shapes, first, end) {
             let (d, p, l) = shapes[k0];
             let dig = &digests[offsets[k0]..offsets[k0] + n * (d + p)];
             if n == 1 {
@@ -1579,7 +1662,7 @@ impl FileChecker {
             return Err(BatchReadError::Engine(crate::too_small("digests")));
         }
         let depth = self.depth;
-        for (k0, n) in shape_runs(shapes) {
+        for (k0, n) in shape_runs(shapes, 0, shapes.len()) {
             let (d, p, l) = shapes[k0];
             let ppb = if n > 1 { self.parts_per_batch } else { 1 };
             let devices = &self.devices;

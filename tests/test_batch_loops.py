@@ -675,3 +675,44 @@ def test_batch_reader_sink_error_leaves_nothing(fakes, monkeypatch, seed):
     assert [k for k, _ in got] == list(range(n))
     assert all(b == chunks[k, :D].tobytes() for k, b in got)
     assert r.multi.live == set() and r.multi.pool == {}, seed
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_file_reader_range_reads(fakes, seed):
+    """FileReader.read_range (FileReadBuilder::seek / take, reader.rs:22-173; the gateway's Range
+    reads): the range's bytes of a file with a short last part and a [bad, good] chunk, read only
+    from the parts that hold the range; range_len as reader.rs:129-138."""
+    rng = np.random.default_rng(seed)
+    shapes, parts, digs, fb = _file(9 * D * L + int(rng.integers(1, D * L)), 30 + seed)
+    copies = {(k, i): [c] for k, cs in enumerate(parts) for i, c in enumerate(cs)}
+    good = parts[3][0]
+    copies[(3, 0)] = [bytes([good[0] ^ 4]) + good[1:], good]
+    calls = []
+
+    def fetch(k, i, start):
+        calls.append(k)
+        locs = copies[(k, i)]
+        for j in range(start, len(locs)):
+            if locs[j] is not None:
+                return j, locs[j]
+        return None
+    reader = br.FileReader(2, 2, [0])
+    starts = np.cumsum([0] + [d * Lk for d, _, Lk in shapes])
+    n = len(fb)
+    for _ in range(8):
+        seek = int(starts[rng.integers(0, len(starts))]) if rng.random() < 0.3 else int(rng.integers(0, n + 3))
+        take = 0 if rng.random() < 0.3 else int(rng.integers(0, n + 3))
+        want = fb[seek:] if take == 0 else fb[seek:seek + take]
+        assert br.range_len(n, seek, take) == len(want)
+        calls.clear()
+        out, seen = bytearray(), []
+        got = reader.read_range(shapes, n, seek, take, fetch, lambda k: digs[k],
+                                lambda k, pieces: (seen.append(k),
+                                                   [out.extend(bytes(x)) for x in pieces]))
+        assert bytes(out) == want and got == len(want), (seek, take)
+        assert seen == sorted(set(seen))
+        # only the parts holding the range were read
+        lo = int(np.searchsorted(starts, seek, side="right")) - 1
+        hi = int(np.searchsorted(starts, seek + len(want), side="left"))
+        assert set(calls) <= set(range(lo, max(hi, lo + 1))), (seek, take, sorted(set(calls)))
+        assert not want or seen[0] == lo

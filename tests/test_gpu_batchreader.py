@@ -226,3 +226,49 @@ def test_failed_read_leaves_no_job_or_carry_id_behind():
            lambda k, data: out.__setitem__(k, b"".join(bytes(x) for x in data)))
     assert all(out[k] == chunks[k, :d].tobytes() for k in range(n))
     assert r.multi.stats(0)["carry_held"] == 0
+
+
+def test_file_reader_range_reads():
+    """FileReader.read_range (FileReadBuilder::seek / take, reader.rs:22-173) on the GPU: the
+    gateway's Range / Prefix / Suffix reads of an RS(3,2) file with a short last part and a lost
+    chunk in every part return the range's bytes, reading only the parts that hold it."""
+    import hashlib
+    d, p, chunk = 3, 2, 8192
+    rng = np.random.default_rng(23)
+    fb = rng.integers(0, 256, 11 * d * chunk + 777, dtype=np.uint8).tobytes()
+    shapes, copies, digs = [], {}, []
+    for k, off in enumerate(range(0, len(fb), d * chunk)):
+        piece = fb[off:off + d * chunk]
+        Lk = -(-len(piece) // d)
+        buf = np.zeros(d * Lk, np.uint8)
+        buf[:len(piece)] = np.frombuffer(piece, np.uint8)
+        data = [buf[j * Lk:(j + 1) * Lk] for j in range(d)]
+        st, par = oracle.encode_sep(d, p, data)
+        cs = [c.tobytes() for c in data] + [c.tobytes() for c in par]
+        for i, c in enumerate(cs):
+            copies[(k, i)] = [None] if i == k % d else [c]
+        shapes.append((d, p, Lk))
+        digs.append(np.array([np.frombuffer(hashlib.sha256(c).digest(), np.uint8) for c in cs]))
+    read = set()
+
+    def fetch(k, i, start):
+        read.add(k)
+        locs = copies[(k, i)]
+        for j in range(start, len(locs)):
+            if locs[j] is not None:
+                return j, locs[j]
+        return None
+    n, part = len(fb), d * chunk
+    reader = FileReader(2, 2, [0])
+    for seek, take in ((0, 0), (0, 10), (part - 1, 2), (part, part), (5 * part + 7, 0),
+                       (n - 777, 0), (n - 1, 0), (n - 100, 1000), (n, 0), (12345, 3 * part)):
+        want = fb[seek:] if take == 0 else fb[seek:seek + take]
+        read.clear()
+        out = bytearray()
+        reader.read_range(shapes, n, seek, take, fetch, lambda k: digs[k],
+                          lambda k, pieces: [out.extend(bytes(x)) for x in pieces])
+        assert bytes(out) == want, (seek, take)
+        if want:
+            assert read == set(range(seek // part, (seek + len(want) - 1) // part + 1)), (seek, take)
+        else:
+            assert not read

@@ -198,6 +198,13 @@ def test_batch_reader_mirrors_the_cpp_and_python_loops():
     # a round in flight when the read fails: its ids for parts still short of d go back too
     # (the leak tests/cpp/host_loop_fuzz.cpp and test_batch_reader_polling_loop_fuzz found)
     assert "rt.r_cout.iter().take(rt.g)" in drain
+    # range reads (FileReadBuilder::seek / take): the same part selection and trimming as the C++
+    # FileReadBuilder and the Python FileReader.read_range
+    rr = batch[batch.index("    pub fn read_range<"):batch.index("    pub fn read_parts<")]
+    for s in ("range_len(length, seek, take)", "skip >= part_len(first)", "covered < skip + want",
+              "self.read_parts(shapes, digests, first, end,"):
+        assert s in rr, s
+    assert "pub fn range_len(length: u64, seek: u64, take: u64) -> u64" in batch
     py = open(os.path.join(ROOT, "chunky-bits_amd", "chunky_ec", "batchreader.py")).read()
     for s in ("def _load", "def _submit", "def _check", "def _poll", "def _finish",
               "def _retry_start", "def _retry_round", "def _retry_collect", "have + added < d",
