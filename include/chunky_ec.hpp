@@ -807,7 +807,7 @@ struct FileReference {
     template <typename Sink>
     void read_span_to(const ChunkStore& src, size_t k_begin, size_t k_end, uint64_t skip,
                       uint64_t limit, Sink&& sink, size_t parts_per_batch = 0, size_t depth = 4,
-                      const std::vector<int>& devices = {}) const {
+                      const std::vector<int>& devices = {}, size_t buffer = kReadBuffer) const {
         k_end = std::min(k_end, parts.size());
         if (k_begin >= k_end) return;
         auto emit = [&](const uint8_t* p, size_t n) {
@@ -819,9 +819,9 @@ struct FileReference {
             if (m) sink(p, m);
             limit -= m;
         };
-        if (!parts_per_batch) {  // FileReadBuilder: part reads buffered(5) (reader.rs:63)
+        if (!parts_per_batch) {  // FileReadBuilder: part reads buffered(buffer) (reader.rs:63)
             detail::ordered_concurrent(
-                k_end - k_begin, kReadBuffer,
+                k_end - k_begin, buffer,
                 [&](size_t k) { return parts[k_begin + k].read_with_context(src); },
                 [&](size_t, const Bytes& b) { emit(b.data(), b.size()); });
             return;
@@ -1480,6 +1480,20 @@ class FileReadBuilder {
         take_ = n;
         return *this;
     }
+    // Part reads in flight on the per-part path (reader.rs:111-114, default 5), or as many parts
+    // as `bytes` hold, rounded, at least 1 (buffer_bytes, reader.rs:117-126).
+    FileReadBuilder& buffer(size_t parts) {
+        buffer_ = parts;
+        return *this;
+    }
+    FileReadBuilder& buffer_bytes(size_t bytes) {
+        if (!file_->parts.empty()) {
+            const size_t part_len = file_->parts.front().len_bytes();
+            buffer_ = std::max<size_t>((bytes + part_len / 2) / std::max<size_t>(part_len, 1), 1);
+        }
+        return *this;
+    }
+    size_t get_buffer() const { return buffer_; }
     FileReadBuilder& batch(size_t parts_per_batch, size_t depth = 4) {
         batch_ = parts_per_batch;
         depth_ = depth;
@@ -1510,7 +1524,7 @@ class FileReadBuilder {
         size_t end = k;
         for (uint64_t covered = 0; end < parts.size() && covered < skip + want; ++end)
             covered += parts[end].len_bytes();
-        file_->read_span_to(src, k, end, skip, want, sink, batch_, depth_, devices_);
+        file_->read_span_to(src, k, end, skip, want, sink, batch_, depth_, devices_, buffer_);
     }
     Bytes read(const ChunkStore& src) const {
         Bytes out;
@@ -1522,7 +1536,7 @@ class FileReadBuilder {
    private:
     const FileReference* file_;
     uint64_t seek_ = 0, take_ = 0;
-    size_t batch_ = 0, depth_ = 4;
+    size_t buffer_ = FileReference::kReadBuffer, batch_ = 0, depth_ = 4;
     std::vector<int> devices_;
 };
 

@@ -548,6 +548,11 @@ bool run_seed(uint64_t seed) {
         FileReadBuilder rb(file);
         rb.seek(seek).take(take);
         if (rng() % 2) rb.batch(ppb, depth).devices(devices);
+        else if (rng() % 2) rb.buffer_bytes(rng() % (4 * d * L));  // 1..4 part reads in flight
+        if (rb.get_buffer() < 1) {
+            std::fprintf(stderr, "seed %llu: buffer_bytes gave 0\n", (unsigned long long)seed);
+            return false;
+        }
         const uint64_t len = rb.len_bytes();
         const uint64_t exp_len = seek >= want.size() ? 0 : take == 0 ? want.size() - seek
                                                                    : std::min<uint64_t>(take, want.size() - seek);
