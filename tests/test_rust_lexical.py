@@ -3,8 +3,10 @@ cargo in this image compiles: every source file tokenizes (comments, strings, ra
 literals vs lifetimes) with balanced brackets, and every call of a method the crate defines --
 `self.f(..)` in an impl block and `self.multi.f(..)` / `self.rp.f(..)` on the crate's own
 wrappers -- names a method that exists with that many arguments, and so does every call of the
-crate's free and associated functions.  A renamed method or a call left with the old argument
-list (as an FFI wrapper grows a parameter) fails here."""
+crate's free and associated functions; every `self.field` names a field of its struct; and every
+variable a function body uses is declared in that function.  A renamed method, a call left with
+the old argument list (as an FFI wrapper grows a parameter) or a variable an edit left behind
+fails here.""" 
 import os
 import re
 
@@ -342,3 +344,139 @@ def test_self_fields_exist_in_their_struct():
                 assert name in fields[impl], f"{f}:{line}: {impl} has no field {name}"
                 checked += 1
     assert checked > 100
+
+
+# ---- per-function scope: every variable a function body uses is declared in it ----------------
+KW = set("""as break const continue crate else enum extern false fn for if impl in let loop match mod move mut
+pub ref return self Self static struct super trait true type unsafe use where while async await dyn box
+u8 u16 u32 u64 u128 usize i8 i16 i32 i64 i128 isize f32 f64 bool char str c_int c_uint c_char c_void
+c_long c_ulong""".split())
+
+def _module_names(toks):
+    names = set()
+    for i, (k, x, _) in enumerate(toks):
+        if k == 'ident' and x in ('fn', 'const', 'static', 'mod', 'struct', 'enum', 'type', 'trait') and i + 1 < len(toks):
+            names.add(toks[i + 1][1])
+        if k == 'ident' and x == 'use':
+            j = i + 1
+            while toks[j][1] != ';':
+                if toks[j][0] == 'ident':
+                    names.add(toks[j][1])
+                j += 1
+    return names
+
+def _pattern_idents(toks, a, b, closure=False):
+    out = set()
+    for j in range(a, b):
+        k, x, _ = toks[j]
+        if k == 'ident' and x not in KW and not x[0].isupper():
+            nxt = toks[j + 1][1] if j + 1 < len(toks) else ''
+            prv = toks[j - 1][1]
+            if nxt in ('(', '::', '{') or prv in ('::', '.'):
+                continue
+            if nxt == ':' and prv in ('{', ',') and not closure:  # field: pattern
+                continue
+            out.add(x)
+    return out
+
+def _undeclared_uses(fname):
+    src = _read(fname)
+    toks = tokens(src)
+    mods = _module_names(toks)
+    problems = []
+    i = 0
+    while i < len(toks):
+        if toks[i][1] == 'fn' and toks[i][0] == 'ident' and i + 1 < len(toks) and toks[i + 1][0] == 'ident':
+            name = toks[i + 1][1]
+            j = i + 2
+            while toks[j][1] != '(':
+                j += 1
+            pend = _group(toks, j)
+            declared = set()
+            # params: ident before ':' at depth 1 of the param list, or self
+            depth = 0
+            for q in range(j, pend):
+                x = toks[q][1]
+                if x in '([{':
+                    depth += 1
+                elif x in ')]}':
+                    depth -= 1
+                elif depth == 1 and toks[q][0] == 'ident' and toks[q + 1][1] == ':' :
+                    declared.add(x)
+            b = pend
+            while b < len(toks) and toks[b][1] not in ('{', ';'):
+                b += 1
+            if toks[b][1] == ';':
+                i = b
+                continue
+            bend = _group(toks, b)
+            body = range(b, bend)
+            # declarations in the body
+            for q in body:
+                k, x, _ = toks[q]
+                if x == 'let':
+                    r = q + 1
+                    depth = 0
+                    while not (depth == 0 and toks[r][1] in ('=', ';', ':')):
+                        if toks[r][1] in '([{':
+                            depth += 1
+                        elif toks[r][1] in ')]}':
+                            depth -= 1
+                        r += 1
+                    declared |= _pattern_idents(toks, q + 1, r)
+                elif x == 'for' and toks[q - 1][1] != '<':
+                    r = q + 1
+                    while toks[r][1] != 'in':
+                        r += 1
+                    declared |= _pattern_idents(toks, q + 1, r)
+                elif x in ('|', '||') and k == 'punct' and x == '|':
+                    # closure params: | ... | when preceded by ( , = move or start of arg
+                    prv = toks[q - 1][1]
+                    if prv in ('(', ',', '=', 'move', '{', ';', 'return') :
+                        r = q + 1
+                        while toks[r][1] != '|':
+                            r += 1
+                        declared |= _pattern_idents(toks, q + 1, r, closure=True)
+                elif x == '=>':
+                    # match arm pattern: back to the previous ',' or '{' at this depth
+                    r = q - 1
+                    depth = 0
+                    while True:
+                        y = toks[r][1]
+                        if y in ')]}':
+                            depth += 1
+                        elif y in '([{':
+                            if depth == 0:
+                                break
+                            depth -= 1
+                        elif y == ',' and depth == 0:
+                            break
+                        r -= 1
+                    declared |= _pattern_idents(toks, r + 1, q)
+            # uses
+            for q in body:
+                k, x, line = toks[q]
+                if k != 'ident' or x in KW or x[0].isupper() or x in declared or x in mods:
+                    continue
+                prv, nxt = toks[q - 1][1], toks[q + 1][1]
+                if prv in ('.', '::', "'") or nxt in ('(', '!', '::'):
+                    continue
+                if nxt == ':' and prv in ('{', ','):  # struct literal field
+                    continue
+                if prv == '<' or nxt == '>' :  # generic args / lifetimes-ish
+                    continue
+                problems.append((fname, line, name, x))
+            i = bend
+            continue
+        i += 1
+    return problems
+
+
+
+def test_function_bodies_use_only_declared_names():
+    """Every lower-case name a function body uses as a value is declared in that function (a
+    parameter, a `let` / `for` / `if let` / match-arm / closure pattern) or at module level (a
+    fn, const, static or import): a variable left behind by an edit (used in a function that
+    never binds it) fails here.  Conservative: calls, paths, fields and types are not checked."""
+    problems = [p for f in FILES for p in _undeclared_uses(f)]
+    assert not problems, problems
