@@ -527,6 +527,6 @@ def range_len(length: int, seek: int, take: int) -> int:
     """FileReadBuilder::len_bytes (reader.rs:129-138): the bytes a read from ``seek`` taking
     ``take`` (0: to the end) gives of a ``length``-byte file; 0 for a seek past the end (where the
     reference's u64 subtraction would underflow)."""
-    if take == 0 or length <= seek + take:
-        return max(length - seek, 0)
-    return take
+    if seek >= length:
+        return 0
+    return length - seek if take == 0 else min(take, length - seek)

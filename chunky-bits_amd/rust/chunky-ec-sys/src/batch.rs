@@ -1038,10 +1038,12 @@ fn shape_runs(shapes: &[Shape], first: usize, end: usize) -> Vec<(usize, usize)>
 /// (0: to the end) gives of a `length`-byte file; 0 for a seek past the end (where the reference's
 /// u64 subtraction would underflow).
 pub fn range_len(length: u64, seek: u64, take: u64) -> u64 {
-    if take == 0 || length <= seek.saturating_add(take) {
-        length.saturating_sub(seek)
+    if seek >= length {
+        0
+    } else if take == 0 {
+        length - seek
     } else {
-        take
+        take.min(length - seek)
     }
 }
 

@@ -1509,9 +1509,8 @@ class FileReadBuilder {
     // underflow there).
     uint64_t len_bytes() const {
         const uint64_t length = file_->len_bytes();
-        if (take_ == 0) return length > seek_ ? length - seek_ : 0;
-        if (length > seek_ + take_) return take_;
-        return length > seek_ ? length - seek_ : 0;
+        if (seek_ >= length) return 0;
+        return take_ == 0 ? length - seek_ : std::min(take_, length - seek_);
     }
     template <typename Sink>
     void read_to(const ChunkStore& src, Sink&& sink) const {

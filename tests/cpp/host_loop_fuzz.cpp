@@ -544,7 +544,9 @@ bool run_seed(uint64_t seed) {
     for (int r = 0; r < 3; ++r) {
         // a third of the seeks on a part boundary (the part before must not be read)
         const uint64_t seek = rng() % 3 == 0 ? (rng() % (n + 1)) * d * L : rng() % (want.size() + 2);
-        const uint64_t take = rng() % 3 == 0 ? 0 : rng() % (want.size() + 2);
+        const uint64_t take = rng() % 3 == 0   ? 0
+                              : rng() % 6 == 0 ? std::numeric_limits<uint64_t>::max()
+                                               : rng() % (want.size() + 2);
         FileReadBuilder rb(file);
         rb.seek(seek).take(take);
         if (rng() % 2) rb.batch(ppb, depth).devices(devices);
