@@ -623,7 +623,15 @@ struct cec_multi {
             if (job->kind == Kind::Write) run_write(s, job, lo, hi);
             else run_read(s, job, lo, hi);
         }
-        drain(s);
+        drain(s);  // the pipelines are freed by ~cec_multi, one shard after another
+    }
+
+    // A shard's pipelines and staging, freed on the destroying thread once every worker has
+    // exited: no HIP stream, event or buffer is destroyed while another shard's are (two shards
+    // of one device tearing down their priority streams at once ended one run of the GPU suite
+    // in an abort inside cec_multi_free, cause not isolated; the creation side is the round-5
+    // deadlock, profiles/HISTORY.md).
+    static void free_shard(Shard& s) {
         if (s.wp) cec_pipeline_free(s.wp);
         if (s.rp) cec_read_pipeline_free(s.rp);
         for (auto& sg : s.wstage) sg.release();
@@ -687,6 +695,7 @@ struct cec_multi {
         work_cv.notify_all();
         for (auto& s : shards)
             if (s->th.joinable()) s->th.join();
+        for (auto& s : shards) free_shard(*s);
     }
 };
 
