@@ -1,7 +1,8 @@
 """Markdown summary of a rocprofv3 kernel trace of the default bench command (tools/r6_check.sh):
 the launches the bench line times, by workgroup count, against the line's own HIP-event figures,
 and the top kernels by total time.
-    python3 tools/trace_summary.py <trace dir> <bench log> > profiles/r6_c2_trace_summary.md"""
+    python3 tools/trace_summary.py <trace dir> <bench log> [<stats csv as committed>] \
+        > profiles/r6/final/c2_trace_summary.md"""
 import collections
 import csv
 import json
@@ -9,7 +10,8 @@ import os
 import sys
 
 
-def main(trace_dir, bench_log):
+def main(trace_dir, bench_log, stats=None):
+    stats = stats or os.path.join(trace_dir, "run_kernel_stats.csv")
     rows = list(csv.DictReader(open(os.path.join(trace_dir, "run_kernel_trace.csv"))))
     line = json.loads([x for x in open(bench_log) if x.startswith("{")][-1])
     groups = collections.defaultdict(list)
@@ -29,7 +31,7 @@ def main(trace_dir, bench_log):
     print("# Round 6: kernel trace of the default command on the final tree\n")
     print("`rocprofv3 --kernel-trace --stats --output-format csv -- python3 bench.py --steps 10 "
           "--warmup 3 --no-cpu-baseline` (`tools/r6_check.sh`; raw stats: "
-          "`profiles/r6/trace_kernel_stats.csv`; this file: `tools/trace_summary.py`).  Trace only: "
+          f"`{stats}`; this file: `tools/trace_summary.py`).  Trace only: "
           "no hot-path kernel changed in rounds 5-6, so the PMC passes (HBM traffic, SQ counters) "
           "of `profiles/r4e_c2_summary.md` still describe them; this run checks that the round-6 "
           "tree's launches take what the bench line's HIP events say.\n")
@@ -53,4 +55,4 @@ def main(trace_dir, bench_log):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(*sys.argv[1:4])
