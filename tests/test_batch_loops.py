@@ -716,3 +716,36 @@ def test_file_reader_range_reads(fakes, seed):
         hi = int(np.searchsorted(starts, seek + len(want), side="left"))
         assert set(calls) <= set(range(lo, max(hi, lo + 1))), (seek, take, sorted(set(calls)))
         assert not want or seen[0] == lo
+
+
+def test_file_reader_range_read_fails_only_inside_the_range(fakes):
+    """A part without d good chunks fails a range read that reaches into it (TooFewShardsPresent,
+    file_part.rs:92-107) and not one that ends before it or starts after it: the parts outside
+    the range are not read."""
+    shapes, parts, digs, fb = _file(8 * D * L, 61)
+    copies = {(k, i): [c] for k, cs in enumerate(parts) for i, c in enumerate(cs)}
+    for i in range(P + 1):  # part 4: P + 1 chunks lost
+        copies[(4, i)] = [None]
+
+    def fetch(k, i, start):
+        locs = copies[(k, i)]
+        for j in range(start, len(locs)):
+            if locs[j] is not None:
+                return j, locs[j]
+        return None
+    reader = br.FileReader(2, 2, [0])
+    part, n = D * L, len(fb)
+    for seek, take, fails in ((0, 4 * part, False), (5 * part, 0, False), (4 * part - 1, 1, False),
+                              (4 * part - 1, 2, True), (3 * part, 2 * part, True), (0, 0, True)):
+        out = bytearray()
+        try:
+            reader.read_range(shapes, n, seek, take, fetch, lambda k: digs[k],
+                              lambda k, pieces: [out.extend(bytes(x)) for x in pieces])
+            err = None
+        except Error as e:
+            err = e.code
+        if fails:
+            assert err == TOO_FEW_SHARDS_PRESENT, (seek, take)
+        else:
+            want = fb[seek:] if take == 0 else fb[seek:seek + take]
+            assert err is None and bytes(out) == want, (seek, take)
