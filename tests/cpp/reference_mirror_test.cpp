@@ -207,7 +207,7 @@ void test_cp_50mib() {
 
 // FileReadBuilder::seek / take (reader.rs:22-173), the gateway's Range / Prefix / Suffix reads
 // (http.rs:37-56) of the 50 MiB cp file, holes in every part: the range's bytes, per part and
-// batched; len_bytes as reader.rs:129-138.
+// batched (one and two scheduler shards); len_bytes as reader.rs:129-138.
 void test_range_reads() {
     const size_t length = size_t(50) << 20, part = size_t(3) << 20;
     const Bytes input = random_bytes(length, 51);
@@ -222,9 +222,10 @@ void test_range_reads() {
     for (const auto& r : ranges) {
         const uint64_t want = r[0] >= length ? 0 : r[1] == 0 ? length - r[0]
                                                              : std::min<uint64_t>(r[1], length - r[0]);
-        for (size_t batch : {size_t(0), size_t(4)}) {
+        for (size_t batch : {size_t(0), size_t(4), size_t(3)}) {
             FileReadBuilder rb(f);
             rb.seek(r[0]).take(r[1]).batch(batch);
+            if (batch == 3) rb.devices({0, 0});  // two scheduler shards on one GPU
             CHECK(rb.len_bytes() == want && rb.get_seek() == r[0]);
             const Bytes got = rb.read(store);
             CHECK(got.size() == want);
