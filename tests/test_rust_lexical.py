@@ -480,3 +480,70 @@ def test_function_bodies_use_only_declared_names():
     never binds it) fails here.  Conservative: calls, paths, fields and types are not checked."""
     problems = [p for f in FILES for p in _undeclared_uses(f)]
     assert not problems, problems
+
+
+# ---- names: imports from the crate root exist there, and every type-like name resolves ---------
+_PRELUDE = set("""Vec Option Some None Result Ok Err String Box Self FnMut Fn FnOnce Copy Clone Debug
+PartialEq Eq Default Drop Send Sync Sized Iterator IntoIterator From Into AsRef AsMut ToString
+Display Hash Ord PartialOrd VecDeque HashMap BTreeMap Cow Arc Rc Mutex Duration Instant""".split())
+
+
+def _defined(toks):
+    """Names a file defines at any level: items, and the variants of its enums."""
+    out = set()
+    for i, (k, x, _) in enumerate(toks):
+        if k == "ident" and x in ("struct", "enum", "type", "trait", "fn", "const", "static", "mod",
+                                  "union"):
+            out.add(toks[i + 1][1])
+        if k == "ident" and x == "enum":
+            j = i + 2
+            while toks[j][1] != "{":
+                j += 1
+            end, depth = _group(toks, j), 0
+            for q in range(j + 1, end - 1):
+                y = toks[q][1]
+                if y in "([{":
+                    depth += 1
+                elif y in ")]}":
+                    depth -= 1
+                elif depth == 0 and toks[q][0] == "ident" and toks[q - 1][1] in ("{", ","):
+                    out.add(y)
+    return out
+
+
+def _imported(toks):
+    out = set()
+    for i, (k, x, _) in enumerate(toks):
+        if k == "ident" and x == "use":
+            j = i + 1
+            while toks[j][1] != ";":
+                if toks[j][0] == "ident":
+                    out.add(toks[j][1])
+                j += 1
+    return out
+
+
+def test_names_resolve():
+    """`use crate::{..}` names and `crate::name` paths exist at the crate root (lib.rs defines or
+    re-exports them), and every CamelCase name a file uses unqualified is defined in it, imported,
+    or in the std prelude: a type renamed in one file and not the other fails here."""
+    lib = tokens(_read("lib.rs"))
+    root = _defined(lib) | _imported(lib)
+    problems = []
+    for f in FILES:
+        toks = tokens(_read(f))
+        known = _defined(toks) | _imported(toks) | _PRELUDE | (root if f == "lib.rs" else set())
+        for i, (k, x, line) in enumerate(toks):
+            if x == "use" and toks[i + 1][1] == "crate":
+                j = i + 2
+                while toks[j][1] != ";":
+                    if toks[j][0] == "ident" and toks[j][1] != "self" and toks[j][1] not in root:
+                        problems.append((f, line, "use crate::" + toks[j][1]))
+                    j += 1
+            if (x == "crate" and toks[i + 1][1] == "::" and toks[i + 2][0] == "ident"
+                    and toks[i + 2][1] not in root | {"sys", "batch"}):
+                problems.append((f, line, "crate::" + toks[i + 2][1]))
+            if (k == "ident" and x[0].isupper() and not x.isupper() and toks[i - 1][1] not in ("::", ".")
+                    and x not in known):
+                problems.append((f, line, x))
+    assert not problems, problems
