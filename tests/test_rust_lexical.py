@@ -547,3 +547,37 @@ def test_names_resolve():
                     and x not in known):
                 problems.append((f, line, x))
     assert not problems, problems
+
+
+# method names the standard library also has: calls of these on other receivers are not checked
+_STD_METHODS = set("""len iter iter_mut read write get get_mut push insert new clone as_ptr as_mut_ptr map
+take skip filter collect chunks copy_from_slice fill extend resize contains min max wait drain flush
+run encode from into sum count any all first last is_empty unwrap expect ok err map_err and_then find
+position to_vec as_slice swap remove pop push_back pop_front sort dedup retain split_at chain zip
+enumerate rev windows step_by next send recv lock join spawn fmt eq cmp hash default drop as_ref
+as_mut borrow entry with_capacity reserve truncate clear set query stats release carry_release verify
+resilver""".split())
+
+
+def test_crate_method_calls_on_other_receivers_match_arity():
+    """`x.f(..)` where f is a method only this crate defines (not a std method name): called with
+    as many arguments as a definition takes, whatever the receiver."""
+    defs = {}
+    for f in FILES:
+        for impl, ms in _methods(_read(f)).items():
+            if impl.endswith("::") or impl == "":
+                continue
+            for name, ns in ms.items():
+                defs.setdefault(name, set()).update(ns)
+    own = {n: ns for n, ns in defs.items() if n not in _STD_METHODS}
+    problems, checked = [], 0
+    for f in FILES:
+        toks = tokens(_read(f))
+        for i in range(1, len(toks) - 2):
+            if (toks[i][1] == "." and toks[i + 1][0] == "ident" and toks[i + 2][1] == "("
+                    and toks[i - 1][1] != "self" and toks[i + 1][1] in own):
+                n = _args(toks, i + 2)
+                checked += 1
+                if n not in own[toks[i + 1][1]]:
+                    problems.append((f, toks[i][2], toks[i + 1][1], n))
+    assert checked >= 10 and not problems, problems
