@@ -526,7 +526,7 @@ bool run_seed(uint64_t seed) {
             ok = false;
         }
     };
-    expect(got.size() <= want.size() && std::memcmp(got.data(), want.data(), got.size()) == 0,
+    expect(got.size() <= want.size() && std::equal(got.begin(), got.end(), want.begin()),
            "bytes out differ from the file");
     expect(got.size() % (d * L) == 0 || got.size() == want.size(), "a part cut short");
     if (first_short < n) {

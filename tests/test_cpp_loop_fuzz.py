@@ -40,3 +40,23 @@ def test_cpp_host_loop_fuzz(fuzz_bin, first):
     r = subprocess.run([fuzz_bin, str(first), "300"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr[-4000:]
     assert "0 failed, 0 contract violations" in r.stdout
+
+
+def test_cpp_host_loop_fuzz_under_sanitizers(tmp_path):
+    """The same fuzz built with AddressSanitizer + UndefinedBehaviorSanitizer (host code only:
+    the header's loops, the stand-in and the oracle): no out-of-bounds access, use after free,
+    leak or undefined behaviour over 100 seeds."""
+    if not (shutil.which("gcc") and shutil.which("g++")):
+        pytest.skip("no host compiler")
+    san = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-g", "-O0"]
+    obj, exe = str(tmp_path / "oracle_san.o"), str(tmp_path / "host_loop_fuzz_san")
+    subprocess.run(["gcc", *san, "-c", os.path.join(ROOT, "oracle", "cec_oracle.c"), "-o", obj],
+                   check=True)
+    subprocess.run(["g++", "-std=c++17", *san, "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "cpp", "host_loop_fuzz.cpp"), obj, "-lpthread",
+                    "-o", exe], check=True)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+    r = subprocess.run([exe, "5000", "100"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr[-4000:]
+    assert "0 failed, 0 contract violations" in r.stdout
