@@ -9,4 +9,8 @@ ASAN_OPTIONS=detect_leaks=0:abort_on_error=0:halt_on_error=1 timeout -k 10 600 \
     ./tools/asan/reference_mirror_test > gpurun_out/asan/mirror_asan.log 2>&1
 s=$?
 tail -25 gpurun_out/asan/mirror_asan.log
-exit $s
+# The HIP runtime's own finalizer trips an AddressSanitizer CHECK at process exit
+# (sanitizer_allocator_device.h, "dev_runtime_unloaded_"), after main has returned: judge the run
+# by the tests' verdict and the absence of an ASan error report instead of the exit status.
+grep -q "^all passed" gpurun_out/asan/mirror_asan.log || exit 1
+! grep -q "ERROR: AddressSanitizer" gpurun_out/asan/mirror_asan.log
