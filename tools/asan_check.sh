@@ -1,5 +1,5 @@
 # The C++ mirror test against the host-AddressSanitizer build of the library
-# (make -C chunky-bits_amd/csrc asan): heap / stack errors in the host code of the C-ABI, the
+# (make -C chunky-bits_amd/csrc asan; remove ./tools/asan from .gpurunignore to ship it): heap / stack errors in the host code of the C-ABI, the
 # pipelines and the scheduler (one- and two-shard schedulers made and freed) on a real GPU.
 # Device code is not instrumented.  Leak checking is off: the HIP runtime keeps its allocations to
 # process exit.
